@@ -1,0 +1,352 @@
+"""CPU ORACLE for the SailRecon aggregator + camera-pose head hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker / the timed CPU baseline.  The product path (``sailrecon_amd``) never
+imports it and fails loudly when its HIP library is missing.
+
+What it is: a plain PyTorch-CPU fp32 restatement of the reference algorithm,
+written from the reference's behaviour (not copied), functional style over an
+explicit ``state_dict``.  It keeps the reference's own op choices, including the
+dense boolean reloc mask (``aggregator.py:302-311``) and the scatter
+reassembly (``aggregator.py:393-399``), so that it times like the reference CPU
+path.
+
+Pinning: checked against golden vectors produced by importing the real
+reference in the build container (``tests/golden/make_golden.py``); see
+``tests/test_oracle_golden.py``.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+SD = Dict[str, Tensor]
+
+RESNET_MEAN = (0.485, 0.456, 0.406)  # aggregator.py:31
+RESNET_STD = (0.229, 0.224, 0.225)  # aggregator.py:32
+
+
+# --------------------------------------------------------------------------
+# layers (sailrecon/layers)
+# --------------------------------------------------------------------------
+
+def layer_norm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float) -> Tensor:
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+def rope_tables(half_dim: int, max_pos: int, base: float = 100.0) -> Tuple[Tensor, Tensor]:
+    """cos/sin tables, rope.py:93-124 (fp32; angles duplicated cat(a, a))."""
+    exps = torch.arange(0, half_dim, 2).float() / half_dim
+    inv_freq = 1.0 / (base ** exps)
+    pos = torch.arange(max_pos, dtype=inv_freq.dtype)
+    ang = torch.einsum("i,j->ij", pos, inv_freq)
+    ang = torch.cat((ang, ang), dim=-1)
+    return ang.cos(), ang.sin()
+
+
+def rope2d(t: Tensor, pos: Tensor, base: float = 100.0) -> Tensor:
+    """2-D RoPE, rope.py:165-207.  t [B,H,L,D], pos [B,L,2] int (y, x)."""
+    half = t.shape[-1] // 2
+    cos_t, sin_t = rope_tables(half, int(pos.max()) + 1, base)
+
+    def one(x: Tensor, p: Tensor) -> Tensor:  # rope.py:140-163
+        c = F.embedding(p, cos_t)[:, None]
+        s = F.embedding(p, sin_t)[:, None]
+        x1, x2 = x[..., : half // 2], x[..., half // 2:]
+        return x * c + torch.cat((-x2, x1), dim=-1) * s
+
+    ty, tx = t.chunk(2, dim=-1)
+    return torch.cat((one(ty, pos[..., 0]), one(tx, pos[..., 1])), dim=-1)
+
+
+def attention(sd: SD, pre: str, x: Tensor, heads: int, pos: Optional[Tensor] = None,
+              mask: Optional[Tensor] = None, qk_norm: bool = False,
+              rope_base: Optional[float] = None) -> Tensor:
+    """Attention.forward, attention.py:70-122 (fused SDPA branch)."""
+    B, N, C = x.shape
+    D = C // heads
+    qkv = F.linear(x, sd[pre + "qkv.weight"], sd.get(pre + "qkv.bias"))
+    q, k, v = qkv.reshape(B, N, 3, heads, D).permute(2, 0, 3, 1, 4).unbind(0)
+    if qk_norm:  # attention.py:49-50,78 (LayerNorm(D), eps 1e-5)
+        q = layer_norm(q, sd[pre + "q_norm.weight"], sd[pre + "q_norm.bias"], 1e-5)
+        k = layer_norm(k, sd[pre + "k_norm.weight"], sd[pre + "k_norm.bias"], 1e-5)
+    if rope_base is not None:
+        q = rope2d(q, pos, rope_base)
+        k = rope2d(k, pos, rope_base)
+    o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+    o = o.transpose(1, 2).reshape(B, N, C)
+    return F.linear(o, sd[pre + "proj.weight"], sd.get(pre + "proj.bias"))
+
+
+def mlp(sd: SD, pre: str, x: Tensor) -> Tensor:
+    """Mlp.forward, mlp.py:34-40 (exact erf GELU)."""
+    h = F.gelu(F.linear(x, sd[pre + "fc1.weight"], sd.get(pre + "fc1.bias")))
+    return F.linear(h, sd[pre + "fc2.weight"], sd.get(pre + "fc2.bias"))
+
+
+def block(sd: SD, pre: str, x: Tensor, heads: int, eps: float, pos: Optional[Tensor] = None,
+          mask: Optional[Tensor] = None, qk_norm: bool = False,
+          rope_base: Optional[float] = None) -> Tensor:
+    """Block.forward eval branch, block.py:86-112 (LayerScale layer_scale.py:22-23)."""
+    a = attention(sd, pre + "attn.", layer_norm(x, sd[pre + "norm1.weight"], sd[pre + "norm1.bias"], eps),
+                  heads, pos, mask, qk_norm, rope_base)
+    x = x + a * sd[pre + "ls1.gamma"]
+    m = mlp(sd, pre + "mlp.", layer_norm(x, sd[pre + "norm2.weight"], sd[pre + "norm2.bias"], eps))
+    return x + m * sd[pre + "ls2.gamma"]
+
+
+# --------------------------------------------------------------------------
+# DINOv2 patch embed (vision_transformer.py, aggregator.py:196-240)
+# --------------------------------------------------------------------------
+
+def dino_pos_embed(sd: SD, pre: str, h_img: int, w_img: int, patch: int, npatch: int) -> Tensor:
+    """interpolate_pos_encoding, vision_transformer.py:206-240 (antialias, offset 0)."""
+    pe = sd[pre + "pos_embed"]
+    n0 = pe.shape[1] - 1
+    if npatch == n0 and w_img == h_img:
+        return pe
+    pe = pe.float()
+    cls_pe, patch_pe = pe[:, 0], pe[:, 1:]
+    dim = pe.shape[-1]
+    m = int(math.sqrt(n0))
+    # note the reference names the first spatial dim "w" (B, nc, w, h = x.shape)
+    out = F.interpolate(patch_pe.reshape(1, m, m, dim).permute(0, 3, 1, 2), mode="bicubic",
+                        antialias=True, size=(h_img // patch, w_img // patch))
+    out = out.permute(0, 2, 3, 1).view(1, -1, dim)
+    return torch.cat((cls_pe.unsqueeze(0), out), dim=1)
+
+
+def dino_forward(sd: SD, pre: str, img: Tensor, patch: int, depth: int, heads: int) -> Tensor:
+    """forward_features -> x_norm_patchtokens, vision_transformer.py:242-307."""
+    x = F.conv2d(img, sd[pre + "patch_embed.proj.weight"], sd[pre + "patch_embed.proj.bias"], stride=patch)
+    x = x.flatten(2).transpose(1, 2)
+    B = x.shape[0]
+    x = torch.cat((sd[pre + "cls_token"].expand(B, -1, -1), x), dim=1)
+    x = x + dino_pos_embed(sd, pre, img.shape[2], img.shape[3], patch, x.shape[1] - 1)
+    reg = sd[pre + "register_tokens"]
+    x = torch.cat((x[:, :1], reg.expand(B, -1, -1), x[:, 1:]), dim=1)
+    for i in range(depth):
+        x = block(sd, f"{pre}blocks.{i}.", x, heads, 1e-6)
+    x = layer_norm(x, sd[pre + "norm.weight"], sd[pre + "norm.bias"], 1e-6)
+    return x[:, 1 + reg.shape[1]:]
+
+
+# --------------------------------------------------------------------------
+# Aggregator (sailrecon/models/aggregator.py)
+# --------------------------------------------------------------------------
+
+def build_allow_block(L: int, la: Sequence[int], lb: Sequence[int]) -> Tensor:
+    """aggregator.py:832-847 (True = attend)."""
+    allow = torch.zeros(L, L, dtype=torch.bool)
+    ia = torch.tensor(list(la))
+    allow[ia[:, None], ia[None, :]] = True
+    if len(lb) > 0:
+        ib = torch.tensor(list(lb))
+        allow[ib[:, None], ia[None, :]] = True
+        allow[ib, ib] = True
+    return allow
+
+
+def draw_subsample_indices(generator: torch.Generator, depth: int, batch: int, n_anchor: int,
+                           n_patch: int, rank: int) -> Tensor:
+    """Replay of random_select_features' draws, aggregator.py:339,351-357,617-621.
+
+    Order: layer -> batch -> anchor frame; each draw ``randperm(n_patch)[:rank]``.
+    Returns int64 [depth, batch, n_anchor, rank].
+    """
+    out = torch.empty(depth, batch, n_anchor, rank, dtype=torch.long)
+    for l in range(depth):
+        for b in range(batch):
+            for a in range(n_anchor):
+                out[l, b, a] = torch.randperm(n_patch, generator=generator)[:rank]
+    return out
+
+
+class AggCfg:
+    def __init__(self, patch=14, embed_dim=1024, depth=24, heads=16, dino_depth=24, dino_heads=16,
+                 n_register=4, rope_base=100.0, inter_idx=(4, 11, 17, 23)):
+        self.patch, self.C, self.depth, self.heads = patch, embed_dim, depth, heads
+        self.dino_depth, self.dino_heads = dino_depth, dino_heads
+        self.n_register, self.rope_base, self.inter_idx = n_register, rope_base, tuple(inter_idx)
+
+
+def aggregator_forward(sd: SD, cfg: AggCfg, images: Tensor, no_reloc: List[int], reloc: List[int],
+                       fix_rank: int, sub_idx: Tensor, pre: str = "aggregator.") -> Tuple[Dict[int, Tensor], int, Tensor]:
+    """Aggregator.forward, aggregator.py:242-433, with explicit subsample indices.
+
+    ``sub_idx``: int64 [depth, B, Na, rank] patch indices (see draw_subsample_indices).
+    """
+    B, S, _, H, W = images.shape
+    Na, Nq = len(no_reloc), len(reloc)
+    C = cfg.C
+    psi = 1 + cfg.n_register
+    mean = torch.tensor(RESNET_MEAN).view(1, 1, 3, 1, 1)
+    std = torch.tensor(RESNET_STD).view(1, 1, 3, 1, 1)
+    imgs = ((images - mean) / std).reshape(B * S, 3, H, W)  # :267-270
+    patches = dino_forward(sd, pre + "patch_embed.", imgs, cfg.patch, cfg.dino_depth, cfg.dino_heads)
+    n_patch = patches.shape[1]
+    rank = min(fix_rank, n_patch)  # :277-278
+
+    # special tokens, :287-299 + slice_expand_and_flatten :806-829
+    def expand_special(t: Tensor) -> Tensor:
+        first = t[:, 0:1].expand(B, 1, *t.shape[2:])
+        rest = t[:, 1:].expand(B, S - 1, *t.shape[2:])
+        return torch.cat([first, rest], dim=1).clone()
+
+    cam = expand_special(sd[pre + "camera_token"])
+    reg = expand_special(sd[pre + "register_token"])
+    cam[:, reloc] = sd[pre + "camera_token_reloc"][:, 0:1].expand(B, Nq, *cam.shape[2:])
+    reg[:, reloc] = sd[pre + "register_token_reloc"][:, 0:1].expand(B, Nq, *reg.shape[2:])
+    tokens = torch.cat([cam.view(B * S, 1, C), reg.view(B * S, cfg.n_register, C), patches], dim=1)
+    P = tokens.shape[1]
+    P_prime = min(rank + psi, P)
+
+    # dense boolean mask (True = attend), :302-311
+    allow = build_allow_block(S, list(range(Na)), [i + Na for i in range(Nq)])
+    full = allow.repeat_interleave(P, 0).repeat_interleave(P, 1)
+    cut = (P - psi - rank) * Na
+    mask = full[cut:, cut:][None, None]
+
+    # positions, :313-328 + PositionGetter rope.py:40-66
+    hp, wp = H // cfg.patch, W // cfg.patch
+    yy, xx = torch.meshgrid(torch.arange(hp), torch.arange(wp), indexing="ij")
+    grid = torch.stack([yy.reshape(-1), xx.reshape(-1)], dim=-1) + 1
+    pos = torch.cat([torch.zeros(psi, 2, dtype=torch.long), grid], dim=0)[None].expand(B * S, P, 2).contiguous()
+
+    out: Dict[int, Tensor] = {}
+    cam_last = None
+    for layer in range(cfg.depth):  # :339
+        tokens = block(sd, f"{pre}frame_blocks.{layer}.", tokens, cfg.heads, 1e-5, pos=pos,
+                       qk_norm=True, rope_base=cfg.rope_base)  # :643-670
+        frame_out = tokens.view(B, S, P, C)
+        # select_scene_repe_for_reloc / random_select_features, :580-626
+        anc = frame_out[:, no_reloc]
+        anc_pos = pos.view(B, S, P, 2)[:, no_reloc]
+        sel = sub_idx[layer][..., :rank] + psi  # token index of selected patches
+        g_tok = torch.gather(anc, 2, sel[..., None].expand(B, Na, rank, C))
+        g_pos = torch.gather(anc_pos, 2, sel[..., None].expand(B, Na, rank, 2))
+        sub = torch.cat([anc[:, :, :psi], g_tok], dim=2).reshape(B, Na * P_prime, C)
+        sub_pos = torch.cat([anc_pos[:, :, :psi], g_pos], dim=2).reshape(B, Na * P_prime, 2)
+        # global_reloc block over [anchor subsample ; query frames] with mask, :672-741
+        q_tok = frame_out[:, reloc].reshape(B, Nq * P, C)
+        q_pos = pos.view(B, S, P, 2)[:, reloc].reshape(B, Nq * P, 2)
+        seq = torch.cat([sub, q_tok], dim=1)
+        seq = block(sd, f"{pre}global_reloc_blocks.{layer}.", seq, cfg.heads, 1e-5,
+                    pos=torch.cat([sub_pos, q_pos], dim=1), mask=mask, qk_norm=True,
+                    rope_base=cfg.rope_base)
+        reloc_out = seq[:, Na * P_prime:]
+        # global block over all anchor tokens, :743-769
+        g = frame_out[:, no_reloc].reshape(B, Na * P, C)
+        g = block(sd, f"{pre}global_blocks.{layer}.", g, cfg.heads, 1e-5,
+                  pos=pos.view(B, S, P, 2)[:, no_reloc].reshape(B, Na * P, 2), qk_norm=True,
+                  rope_base=cfg.rope_base)
+        # reassembly, :393-399
+        new = torch.ones(B, S, P, C, dtype=tokens.dtype)
+        new[:, no_reloc] = g.view(B, Na, P, C)
+        new[:, reloc] = reloc_out.view(B, Nq, P, C)
+        # intermediates, :403-423
+        if layer in cfg.inter_idx and Nq > 0:
+            out[layer] = torch.cat([frame_out[:, reloc], reloc_out.view(B, Nq, P, C)], dim=-1)
+        if layer == cfg.depth - 1:
+            cam_last = torch.cat([frame_out[:, no_reloc][:, :, 0], g.view(B, Na, P, C)[:, :, 0]], dim=-1).clone()
+        tokens = new.view(B * S, P, C)
+    if Nq > 0:
+        out[-1] = out[cfg.depth - 1]
+    return out, psi, cam_last
+
+
+# --------------------------------------------------------------------------
+# Camera head (sailrecon/heads/camera_head.py, head_act.py)
+# --------------------------------------------------------------------------
+
+def build_lr_mask(S: int, no_reloc: Sequence[int]) -> Tensor:
+    """camera_head.py:197-228 (True = MASKED)."""
+    r_idx = torch.tensor([i for i in range(S) if i not in no_reloc], dtype=torch.long)
+    l_idx = torch.as_tensor(list(no_reloc), dtype=torch.long).unique(sorted=True)
+    m = torch.zeros(S, S, dtype=torch.bool)
+    if l_idx.numel() and r_idx.numel():
+        m[l_idx[:, None], r_idx[None, :]] = True
+    if r_idx.numel() > 1:
+        m[r_idx[:, None], r_idx[None, :]] = True
+        m[r_idx, r_idx] = False
+    return m[None, None]
+
+
+def activate_pose(p: Tensor) -> Tensor:
+    """activate_pose(trans linear, quat linear, fl relu), head_act.py:12-60."""
+    return torch.cat([p[..., :3], p[..., 3:7], F.relu(p[..., 7:])], dim=-1)
+
+
+def camera_head_forward(sd: SD, feats_last: Tensor, cam_last: Tensor, heads: int = 16, trunk_depth: int = 4,
+                        iters: int = 4, pre: str = "camera_head.") -> List[Tensor]:
+    """CameraHead.forward + trunk_fn, camera_head.py:85-186 (fp32)."""
+    na = cam_last.shape[1]
+    tok = torch.cat([cam_last, feats_last[:, :, 0]], dim=1)  # :103-109
+    tok = layer_norm(tok, sd[pre + "token_norm.weight"], sd[pre + "token_norm.bias"], 1e-5)
+    B, S, C = tok.shape
+    attend = ~build_lr_mask(S, list(range(na)))  # :112-116,165
+    pred = None
+    outs = []
+    for _ in range(iters):
+        inp = sd[pre + "empty_pose_tokens"].expand(B, S, -1) if pred is None else pred
+        emb = F.linear(inp, sd[pre + "embed_pose.weight"], sd[pre + "embed_pose.bias"])
+        mod = F.linear(F.silu(emb), sd[pre + "poseLN_modulation.1.weight"], sd[pre + "poseLN_modulation.1.bias"])
+        shift, scale, gate = mod.chunk(3, dim=-1)
+        x = gate * (layer_norm(tok, None, None, 1e-6) * (1 + scale) + shift) + tok  # :158-161
+        for i in range(trunk_depth):
+            x = block(sd, f"{pre}trunk.{i}.", x, heads, 1e-5, mask=attend)
+        delta = mlp(sd, pre + "pose_branch.",
+                    layer_norm(x, sd[pre + "trunk_norm.weight"], sd[pre + "trunk_norm.bias"], 1e-5))
+        pred = delta if pred is None else pred + delta
+        outs.append(activate_pose(pred))
+    return [o[:, na:] for o in outs]
+
+
+# --------------------------------------------------------------------------
+# Pose decode (sailrecon/utils/pose_enc.py, rotation.py)
+# --------------------------------------------------------------------------
+
+def quat_to_mat(q: Tensor) -> Tensor:
+    """rotation.py:14-44 (xyzw, scalar last)."""
+    i, j, k, r = torch.unbind(q, -1)
+    two_s = 2.0 / (q * q).sum(-1)
+    o = torch.stack((1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+                     two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+                     two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)), -1)
+    return o.reshape(q.shape[:-1] + (3, 3))
+
+
+def pose_encoding_to_extri_intri(enc: Tensor, hw: Tuple[int, int]) -> Tuple[Tensor, Tensor]:
+    """pose_enc.py:68-135."""
+    T, quat, fov_h, fov_w = enc[..., :3], enc[..., 3:7], enc[..., 7], enc[..., 8]
+    ext = torch.cat([quat_to_mat(quat), T[..., None]], dim=-1)
+    H, W = hw
+    fy = (H / 2.0) / torch.tan(fov_h / 2.0)
+    fx = (W / 2.0) / torch.tan(fov_w / 2.0)
+    intr = torch.zeros(enc.shape[:2] + (3, 3))
+    intr[..., 0, 0] = fx
+    intr[..., 1, 1] = fy
+    intr[..., 0, 2] = W / 2
+    intr[..., 1, 2] = H / 2
+    intr[..., 2, 2] = 1.0
+    return ext, intr
+
+
+# --------------------------------------------------------------------------
+# end-to-end hot path (SailRecon.forward minus DPT heads), sail_recon.py:70-124
+# --------------------------------------------------------------------------
+
+def hot_path_forward(sd: SD, cfg: AggCfg, images: Tensor, no_reloc: List[int], reloc: List[int],
+                     fix_rank: int, sub_idx: Tensor, cam_heads: int = 16, cam_depth: int = 4) -> Dict[str, object]:
+    with torch.no_grad():
+        feats, psi, cam_last = aggregator_forward(sd, cfg, images, no_reloc, reloc, fix_rank, sub_idx)
+        poses = camera_head_forward(sd, feats[-1], cam_last, heads=cam_heads, trunk_depth=cam_depth)
+        ext, intr = pose_encoding_to_extri_intri(poses[-1], (images.shape[-2], images.shape[-1]))
+    return {"feats": feats, "patch_start_idx": psi, "cam_token_last_layer": cam_last,
+            "pose_enc_list": poses, "extrinsic": ext, "intrinsic": intr}

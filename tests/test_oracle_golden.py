@@ -1,0 +1,102 @@
+"""Pin the CPU oracle against golden vectors produced by the real reference.
+
+These run on CPU only (no GPU, no HIP library) — they establish that
+``oracle/sfm_oracle.py`` is a faithful restatement before it is trusted as the
+checker for the HIP path.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from goldens import SMALL_AGG, SMALL_CAM, load_npz, rel_l2, rule_state_dict
+from oracle import sfm_oracle as O
+
+
+def _run_small(tag):
+    g = load_npz(f"g1_small_{tag}.npz")
+    sd = rule_state_dict("small_state_dict_keys.json")
+    n = int(g["n_views"])
+    images = torch.from_numpy(g["images"])
+    S = images.shape[1]
+    n_patch = (images.shape[-1] // 14) ** 2
+    rank = min(int(g["fix_rank"]), n_patch)
+    gen = torch.Generator().manual_seed(0)
+    sub = O.draw_subsample_indices(gen, 2, 1, n, n_patch, rank)
+    assert np.array_equal(sub[:, 0].numpy(), g["sub_idx"]), "randperm replay order differs"
+    out = O.hot_path_forward(sd, O.AggCfg(**SMALL_AGG), images, list(range(n)), list(range(n, S)),
+                             int(g["fix_rank"]), sub, **SMALL_CAM)
+    return g, out
+
+
+@pytest.mark.parametrize("tag", ["56", "70"])
+def test_small_end_to_end(tag):
+    g, out = _run_small(tag)
+    assert out["patch_start_idx"] == 5
+    for layer in (0, 1):
+        assert rel_l2(out["feats"][layer].numpy(), g[f"feat_{layer}"]) < 1e-5
+    assert out["feats"][-1] is out["feats"][1]
+    assert rel_l2(out["cam_token_last_layer"].numpy(), g["cam_token_last_layer"]) < 1e-5
+    pe = np.stack([p.numpy() for p in out["pose_enc_list"]])
+    assert rel_l2(pe, g["pose_enc"]) < 1e-5
+    assert rel_l2(out["extrinsic"].numpy(), g["extrinsic"]) < 1e-5
+    assert rel_l2(out["intrinsic"].numpy(), g["intrinsic"]) < 1e-5
+
+
+def test_block_kats():
+    g = load_npz("g2_blocks.npz")
+    sd = rule_state_dict("block_state_dict_keys.json", "agg")
+    y = O.block(sd, "", torch.from_numpy(g["agg_x"]), 16, 1e-5, pos=torch.from_numpy(g["agg_pos"]),
+                qk_norm=True, rope_base=100.0)
+    assert rel_l2(y.numpy(), g["agg_y"]) < 1e-6
+    sd = rule_state_dict("block_state_dict_keys.json", "dino")
+    y = O.block(sd, "", torch.from_numpy(g["dino_x"]), 16, 1e-6)
+    assert rel_l2(y.numpy(), g["dino_y"]) < 1e-6
+    sd = rule_state_dict("block_state_dict_keys.json", "cam")
+    y = O.block(sd, "", torch.from_numpy(g["cam_x"]), 16, 1e-5, mask=torch.from_numpy(g["cam_mask"]))
+    assert rel_l2(y.numpy(), g["cam_y"]) < 1e-6
+
+
+def test_op_kats():
+    g = load_npz("g3_ops.npz")
+    y = O.rope2d(torch.from_numpy(g["rope_in"]), torch.from_numpy(g["rope_pos"]), 100.0)
+    assert rel_l2(y.numpy(), g["rope_out"]) < 1e-7
+    allow = O.build_allow_block(4, [0, 1], [2, 3])
+    assert np.array_equal(allow.numpy(), g["allow_4_2"])
+    assert np.array_equal(allow.repeat_interleave(3, 0).repeat_interleave(3, 1).numpy(), g["allow_tok"])
+    assert np.array_equal(O.build_lr_mask(6, [0, 1, 2]).numpy(), g["lr_mask_6_3"])
+
+
+def _full(fname, tol):
+    g = load_npz(fname)
+    sd = rule_state_dict("state_dict_keys.json")
+    n, img = int(g["n_views"]), int(g["img"])
+    gen = torch.Generator().manual_seed(n)
+    x = torch.rand(n, 3, img, img, generator=gen)
+    images = torch.cat([x, x])[None]
+    n_patch = (img // 14) ** 2
+    sub = O.draw_subsample_indices(torch.Generator().manual_seed(0), 24, 1, n, n_patch, min(300, n_patch))
+    assert np.array_equal(sub[:, 0].numpy(), g["sub_idx"])
+    out = O.hot_path_forward(sd, O.AggCfg(), images, list(range(n)), list(range(n, 2 * n)), 300, sub)
+    rows = torch.from_numpy(g["sample_rows"])
+    for layer in (4, 11, 17, 23):
+        v = out["feats"][layer][0]
+        assert rel_l2(v.norm(dim=-1).numpy(), g[f"feat_{layer}_rownorm"]) < tol
+        assert rel_l2(v[:, 0].numpy(), g[f"feat_{layer}_cam"]) < tol
+        assert rel_l2(v.reshape(-1, v.shape[-1])[rows].numpy(), g[f"feat_{layer}_rows"]) < tol
+    assert rel_l2(out["cam_token_last_layer"].numpy(), g["cam_token_last_layer"]) < tol
+    pe = np.stack([p.numpy() for p in out["pose_enc_list"]])
+    assert rel_l2(pe, g["pose_enc"]) < tol
+    assert rel_l2(out["extrinsic"].numpy(), g["extrinsic"]) < tol
+    assert np.isfinite(out["intrinsic"].numpy()).all()
+    assert rel_l2(out["intrinsic"].numpy(), g["intrinsic"]) < tol
+
+
+@pytest.mark.slow
+def test_full_c1_224():
+    _full("g4_c1_224.npz", 1e-5)
+
+
+@pytest.mark.slow
+def test_full_518_n1():
+    _full("g5_518_n1.npz", 1e-5)
