@@ -1,0 +1,181 @@
+/*
+ * sfm_amd.h — C ABI of the MI355X-native SailRecon hot path (libsfm_amd.so).
+ *
+ * The reference (ShngJZ/self-supervise-sfm) has no FFI: its boundary is the
+ * Python nn.Module API.  These entry points are what that API's
+ * torch ops bottom out in on the hot path; each names the reference call site
+ * it replaces.  The framework's Python mirror (sailrecon_amd.*) is the only
+ * caller and owns every buffer.
+ *
+ * Conventions
+ *   - every pointer is a borrowed DEVICE pointer (except where noted);
+ *   - leading dimensions / strides are in ELEMENTS of the pointed-to type;
+ *   - launches are asynchronous on the caller's stream (hipStream_t, NULL = default);
+ *   - return 0 (SR_OK) or a negative sr_status; sr_last_error() explains it;
+ *   - no global mutable state, no allocation, no synchronisation inside a call
+ *     (safe to capture into a hipGraph).
+ */
+#ifndef SFM_AMD_H
+#define SFM_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* sr_stream_t; /* hipStream_t */
+
+enum sr_dtype { SR_F32 = 0, SR_BF16 = 1 };
+
+enum sr_status {
+  SR_OK = 0,
+  SR_EINVAL = -1,       /* bad shape / pointer / enum */
+  SR_ELAUNCH = -2,      /* hipLaunch / runtime error */
+  SR_EUNSUPPORTED = -3  /* valid but not implemented shape */
+};
+
+/* Message for the most recent failing call on this thread ("" if none). */
+const char* sr_last_error(void);
+/* ABI version: (major << 16) | minor. */
+int sr_version(void);
+
+/* ------------------------------------------------------------------------
+ * GEMM with fused epilogue:  out = epilogue(A[M,K] . W[N,K]^T)
+ * Replaces nn.Linear -> addmm for qkv / proj / fc1 / fc2
+ * (attention.py:48,73,120; mlp.py:34-40) and the 14x14/s14 patch conv
+ * (patch_embed.py:62-64,78) as an im2col GEMM.
+ * A, W, out (except RESID / PATCH outputs, which are fp32) use `dtype`.
+ * Requires N % 128 == 0 and K % (64 bf16 | 32 f32) == 0; M arbitrary.
+ * ---------------------------------------------------------------------- */
+enum sr_epilogue {
+  SR_EPI_BIAS = 0,       /* out = acc + bias                                   */
+  SR_EPI_BIAS_GELU = 1,  /* out = gelu_erf(acc + bias)           (mlp.py:36)   */
+  SR_EPI_BIAS_RESID = 2, /* out(f32) += gamma * (acc + bias)  (block.py:110-111,
+                            layer_scale.py:22-23)                              */
+  SR_EPI_QKV = 3,        /* out = rope(qk_norm(acc + bias)) on Q,K columns
+                            (attention.py:72-82, rope.py:165-207)               */
+  SR_EPI_PATCH = 4       /* out(f32)[remap(row)] = acc + bias + row_add[row % seg_rows]
+                            (vision_transformer.py:242-259)                     */
+};
+
+typedef struct sr_gemm_epi {
+  const float* bias;  /* [N] or NULL */
+  const float* gamma; /* [N] LayerScale gamma (RESID) */
+  /* QKV: per-head LayerNorm(head_dim) over Q and K columns + 2-D RoPE */
+  const float* qn_w;
+  const float* qn_b;
+  const float* kn_w;
+  const float* kn_b;       /* [head_dim] each, or all NULL (no qk-norm)    */
+  float qk_eps;            /* 1e-5 (attention.py:49-50)                    */
+  const float* rope_cos;   /* [rope_npos][head_dim/4] or NULL (no RoPE)    */
+  const float* rope_sin;
+  int rope_npos;
+  int col_offset;          /* column of out-col 0 inside [Q|K|V] (K/V-only GEMM: embed_dim) */
+  int head_dim;
+  int embed_dim;
+  const int32_t* pos_yx;     /* explicit int32 (y, x) per GEMM row, or NULL: derive from the token row */
+  const int32_t* pos_rowmap; /* token row of GEMM row r (NULL: pos_row_base + r) */
+  int64_t pos_row_base;
+  int tokens_per_frame;    /* P = patch_start + grid_h*grid_w */
+  int patch_start;         /* 5 (aggregator.py:176) */
+  int grid_w;              /* W / patch */
+  /* PATCH */
+  int seg_rows;
+  int seg_stride;
+  int seg_offset;
+  const float* row_add;    /* [seg_rows][N] */
+} sr_gemm_epi;
+
+int sr_gemm(sr_stream_t stream, int dtype, int epilogue, const void* A, int64_t lda, const void* W,
+            int64_t ldw, void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep);
+
+/* ------------------------------------------------------------------------
+ * Fused multi-head attention  O = softmax(scale * Q K^T + mask) V
+ * Replaces F.scaled_dot_product_attention (attention.py:103-109) for the
+ * frame, global, global_reloc (implicit block mask, aggregator.py:302-311,
+ * 832-851) and camera-trunk (camera_head.py:165, 197-228) calls.
+ *
+ * Batch item b, head h: query rows  q + (b*q_bstride + i)*ldq + h*head_dim, i < lq
+ * keys: segment 0 rows k0 + (b*k0_bstride + j)*ldk0 (+h*head_dim), j < l0
+ *       segment 1 rows k1 + (b*k1_bstride + j)*ldk1,                j < l1
+ * Every query row attends to all l0 + l1 keys of its item (the reloc mask:
+ * anchor subsample shared via k0_bstride = 0, own frame via segment 1).
+ * mask_mode SR_MASK_CAMERA (l1 == 0): row i sees key j iff j < n_anchor or j == i.
+ * dtype SR_BF16: MFMA kernel, head_dim 64.  SR_F32: exact-f32 kernel, head_dim 64|128.
+ * ---------------------------------------------------------------------- */
+enum sr_mask_mode { SR_MASK_NONE = 0, SR_MASK_CAMERA = 1 };
+
+typedef struct sr_attn_desc {
+  const void* q;
+  int64_t ldq;
+  const void* k0;
+  const void* v0;
+  int64_t ldk0, ldv0;
+  const void* k1;
+  const void* v1;
+  int64_t ldk1, ldv1;
+  void* o;
+  int64_t ldo;
+  int batch, heads, head_dim;
+  int lq;
+  int64_t q_bstride;
+  int l0;
+  int64_t k0_bstride;
+  int l1;
+  int64_t k1_bstride;
+  int mask_mode, n_anchor;
+  float scale;
+} sr_attn_desc;
+
+int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
+
+/* ------------------------------------------------------------------------
+ * LayerNorm over the last dim of fp32 rows (block.py:50,70; camera_head.py:64-77;
+ * vision_transformer.py:192,300).  out_row r = LN(x[rowmap ? rowmap[r] : r]).
+ * w/b may be NULL (no affine).  out dtype = out_dtype.  cols % 64 == 0, <= 4096.
+ * ---------------------------------------------------------------------- */
+int sr_layernorm(sr_stream_t stream, int out_dtype, const float* x, int64_t ldx, const int32_t* rowmap,
+                 const float* w, const float* b, float eps, void* out, int64_t ldo, int rows, int cols);
+
+/* image normalisation (aggregator.py:267) + 14x14 patch im2col, K zero-padded
+ * to kpad: out[(f*gh+py)*gw+px][c*ps*ps + ky*ps + kx]  (patch_embed.py:78) */
+int sr_im2col_normalize(sr_stream_t stream, int dtype, const float* img, int frames, int H, int W,
+                        int patch, const float* mean3, const float* std3, void* out, int kpad);
+
+/* x[f*tokens_per_frame + t] = table[type_of_frame[f]][t] for t < n_special
+ * (aggregator.py:287-299, vision_transformer.py:250-257) */
+int sr_set_special_tokens(sr_stream_t stream, float* x, int64_t ldx, int frames, int tokens_per_frame,
+                          int n_special, const float* table, const int32_t* type_of_frame, int cols);
+
+/* dst[r] = src[rowmap ? rowmap[r] : r], fp32 rows (aggregator.py:403-423 intermediates) */
+int sr_copy_rows_f32(sr_stream_t stream, float* dst, int64_t ldd, const float* src, int64_t lds,
+                     const int32_t* rowmap, int rows, int cols);
+
+/* out[M,N] = act_in(A)[M,K] . W[N,K]^T + bias, fp32, any shape (small camera-head
+ * linears: embed_pose 9->C, pose_branch.fc2 C/2->9).  act_in: 0 none, 1 SiLU. */
+int sr_linear_small_f32(sr_stream_t stream, const float* A, int64_t lda, const float* W, const float* bias,
+                        float* out, int64_t ldo, int M, int N, int K, int act_in);
+
+/* elementwise SiLU, fp32 (camera_head.py:72-74) */
+int sr_silu_f32(sr_stream_t stream, const float* x, float* y, int64_t n);
+
+/* out = gate*(xn*(1+scale)+shift) + x, mod = [shift|scale|gate] rows of 3*cols
+ * (camera_head.py:153-161, modulate :189-194) */
+int sr_adaln_modulate_f32(sr_stream_t stream, const float* xn, const float* x, const float* mod,
+                          float* out, int rows, int cols);
+
+/* pred = first ? delta : pred + delta; act = activate_pose(pred) with
+ * trans/quat linear, fov ReLU (camera_head.py:172-184, head_act.py:12-60) */
+int sr_pose_update_f32(sr_stream_t stream, float* pred, const float* delta, int64_t ld_delta, float* act,
+                       int rows, int first);
+
+/* 9-d pose encoding -> extrinsic [n,3,4], intrinsic [n,3,3] (pose_enc.py:68-135) */
+int sr_pose_decode_f32(sr_stream_t stream, const float* enc, int64_t ld_enc, int n, int H, int W,
+                       float* extrinsic, float* intrinsic);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SFM_AMD_H */

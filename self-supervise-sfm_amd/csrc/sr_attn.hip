@@ -1,0 +1,326 @@
+// Fused multi-head attention for gfx950.
+//
+// Replaces F.scaled_dot_product_attention (attention.py:103-109) for
+//   frame attention      (one item per frame, keys = the frame),
+//   global attention     (one item, keys = every anchor token),
+//   global_reloc         (one item per query frame; keys = [anchor subsample (shared
+//                         segment 0) ; own frame (segment 1)] — exactly the rows the
+//                         reference's dense bool mask allows, aggregator.py:302-311,
+//                         832-851, without materialising the O((S*P)^2) mask),
+//   camera trunk         (camera_head.py:165, build_lr_mask :197-228) — fp32 kernel.
+//
+// attn_bf16 (performance path, head_dim 64):
+//   * workgroup = 4 waves = 128 query rows; each wave owns 32 rows for the whole key sweep;
+//   * K/V tiles of 64 keys staged by LDS-DMA, double-buffered, XOR-swizzled rows;
+//   * S^T = K.Q^T with v_mfma_f32_32x32x16_bf16 (Q fragments live in registers), so each
+//     lane holds 32 scores of ONE query row: the row max / sum are in-lane plus one
+//     lane^32 exchange (cdna_hip_programming.md App. B "Fused attention prefill");
+//   * online softmax in fp32 with exp2; the O rescale is skipped when no row max moved;
+//   * P (accumulator) feeds the PV MFMA as the B operand directly (no LDS round trip);
+//     V^T fragments come from ds_read_b64_tr_b16 on the row-major V tile.
+// attn_f32 (parity mode + camera trunk, head_dim 64 | 128): exact fp32 VALU kernel,
+//   K/V tiles broadcast from LDS, per-key online softmax.
+#include <cfloat>
+
+#include "sr_common.h"
+
+namespace {
+
+struct AttnArgs {
+  sr_attn_desc d;
+  int ntile0, ntile1;  // key tiles per segment
+};
+
+// ------------------------------------------------------------------ bf16 / MFMA
+constexpr int QROWS = 128;  // query rows per workgroup
+constexpr int KT = 64;      // keys per tile
+constexpr int TILE_B = KT * 128;  // bytes of one K (or V) tile: 64 rows x 64 bf16
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];  // [buf][K|V]
+  const sr_attn_desc& d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
+  const int hcol = head * 64;
+  const int l32 = lane & 31, hi = lane >> 5;
+
+  // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row l32][16s + 8hi .. +8]
+  const int qrow = qt * QROWS + wave * 32 + l32;
+  const int qrow_c = min(qrow, d.lq - 1);
+  const bf16* qp = (const bf16*)d.q + (item * d.q_bstride + qrow_c) * d.ldq + hcol + 8 * hi;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+
+  // ---- staging: waves 0,1 -> K rows [32w, 32w+32); waves 2,3 -> V rows [32(w-2), ..)
+  const bool is_v = wave >= 2;
+  const int srow0 = (wave & 1) * 32;
+  const uint32_t lds0 = sr::lds_addr(smem);
+  const uint32_t dst_w = __builtin_amdgcn_readfirstlane(lds0 + (is_v ? TILE_B : 0) + srow0 * 128);
+  const int ntiles = args.ntile0 + args.ntile1;
+
+  auto stage = [&](int t, int buf) {
+    const bool s1 = t >= args.ntile0;
+    const int tt = s1 ? t - args.ntile0 : t;
+    const int len = s1 ? d.l1 : d.l0;
+    const int64_t rbase = item * (s1 ? d.k1_bstride : d.k0_bstride);
+    const bf16* base = (const bf16*)(is_v ? (s1 ? d.v1 : d.v0) : (s1 ? d.k1 : d.k0));
+    const int64_t ld = is_v ? (s1 ? d.ldv1 : d.ldv0) : (s1 ? d.ldk1 : d.ldk0);
+    const uint32_t dst = dst_w + buf * 2 * TILE_B;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow0 + i * 8 + (lane >> 3);  // tile row (key)
+      const int key = min(tt * KT + r, len - 1);
+      const int chunk = (lane & 7) ^ ((r >> 1) & 7);
+      sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst + i * 1024);
+    }
+  };
+
+  const float c = d.scale * 1.4426950408889634f;  // scale * log2(e)
+  float m_run = -1e30f, l_run = 0.f;              // l_run: this lane's partial row sum
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+  }
+
+  // per-lane LDS read offsets
+  // K (A operand): row kb*32 + l32, chunk 2s + hi, swizzled
+  const int kswz = (l32 >> 1) & 7;
+  // V tr-read: group G = lane>>4, i = lane&15: row r0 + (i>>2), col db*32 + 16(G&1) + 4(i&3)
+  const int G = lane >> 4, gi = lane & 15;
+  const int vrow_in = gi >> 2;                 // + r0
+  const int vcol_in = 16 * (G & 1) + 4 * (gi & 3);  // + db*32
+
+  stage(0, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) {
+      stage(t + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sr::barrier_raw();
+    const char* kt_lds = smem + buf * 2 * TILE_B;
+    const char* vt_lds = kt_lds + TILE_B;
+
+    // ---- S^T = K Q^T for 2 blocks of 32 keys
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+      const int row = kb * 32 + l32;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *(const bf16x8*)(kt_lds + row * 128 + (((2 * s + hi) ^ kswz) * 16));
+        sacc[kb] = mfma32(kf, qf[s], sacc[kb]);
+      }
+    }
+
+    // ---- mask ragged tail of the segment
+    const bool s1 = t >= args.ntile0;
+    const int tt = s1 ? t - args.ntile0 : t;
+    const int valid = (s1 ? d.l1 : d.l0) - tt * KT;
+    if (valid < KT) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (key >= valid) sacc[kb][r] = -INFINITY;
+        }
+    }
+
+    // ---- online softmax (row = this lane's query; partner lane^32 holds the other 32 keys)
+    float mx = sacc[0][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[0][r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[1][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx * c);
+    if (__any(m_new > m_run)) {
+      const float alpha = exp2f(m_run - m_new);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+      }
+      m_run = m_new;
+    }
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = exp2f(fmaf(sacc[kb][8 * s2 + j], c, -m_run));
+          l_run += p;
+          pf[kb][s2][j] = (bf16)p;
+        }
+
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int r0 = kb * 32 + 16 * s2 + 4 * hi;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int col = db * 32 + vcol_in;
+          const int ra = r0 + vrow_in, rb = r0 + 8 + vrow_in;
+          const char* pa = vt_lds + ra * 128 + (((col >> 3) ^ ((ra >> 1) & 7)) * 16) + (col & 7) * 2;
+          const char* pb = vt_lds + rb * 128 + (((col >> 3) ^ ((rb >> 1) & 7)) * 16) + (col & 7) * 2;
+          const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(
+              (__attribute__((address_space(3))) char*)0 + sr::lds_addr(pa)));
+          const s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(
+              (__attribute__((address_space(3))) char*)0 + sr::lds_addr(pb)));
+          bf16x8 vf;
+          const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
+          vf[0] = a4[0]; vf[1] = a4[1]; vf[2] = a4[2]; vf[3] = a4[3];
+          vf[4] = b4[0]; vf[5] = b4[1]; vf[6] = b4[2]; vf[7] = b4[3];
+          o[db] = mfma32(vf, pf[kb][s2], o[db]);
+        }
+      }
+    sr::wait_lgkm0();
+    sr::barrier_raw();
+  }
+
+  // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_tot;
+  if (qrow < d.lq) {
+    bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[db][4 * g + j] * inv);
+        const int dd = db * 32 + 8 * g + 4 * hi;
+        *(bf16x4*)(op + dd) = v;
+      }
+  }
+}
+
+// ------------------------------------------------------------------ f32 / VALU
+constexpr int F32_KT = 32;       // keys per LDS tile
+constexpr int F32_THREADS = 128;  // query rows per workgroup
+
+template <int D>
+__global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
+  __shared__ float ks[F32_KT][D];
+  __shared__ float vs[F32_KT][D];
+  const sr_attn_desc& d = args.d;
+  const int tid = threadIdx.x;
+  const int head = blockIdx.y, item = blockIdx.z;
+  const int hcol = head * D;
+  const int qrow = blockIdx.x * F32_THREADS + tid;
+  const int qrow_c = min(qrow, d.lq - 1);
+  const float* qp = (const float*)d.q + (item * d.q_bstride + qrow_c) * d.ldq + hcol;
+  float q[D], o[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    q[i] = qp[i];
+    o[i] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  const int nkeys_total = d.l0 + d.l1;
+  for (int seg = 0; seg < 2; ++seg) {
+    const int len = seg ? d.l1 : d.l0;
+    if (len <= 0) continue;
+    const float* kb = (const float*)(seg ? d.k1 : d.k0);
+    const float* vb = (const float*)(seg ? d.v1 : d.v0);
+    const int64_t ldk = seg ? d.ldk1 : d.ldk0, ldv = seg ? d.ldv1 : d.ldv0;
+    const int64_t rb = item * (seg ? d.k1_bstride : d.k0_bstride);
+    const int key_base = seg ? d.l0 : 0;  // logical key index (for the camera mask)
+    for (int t0 = 0; t0 < len; t0 += F32_KT) {
+      const int n = min(F32_KT, len - t0);
+      __syncthreads();
+      for (int e = tid; e < F32_KT * D; e += F32_THREADS) {
+        const int r = e / D, cc = e - r * D;
+        const int key = min(t0 + r, len - 1);
+        ks[r][cc] = kb[(rb + key) * ldk + hcol + cc];
+        vs[r][cc] = vb[(rb + key) * ldv + hcol + cc];
+      }
+      __syncthreads();
+      for (int j = 0; j < n; ++j) {
+        const int kidx = key_base + t0 + j;
+        if (d.mask_mode == SR_MASK_CAMERA && !(kidx < d.n_anchor || kidx == qrow)) continue;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < D; ++i) s = fmaf(q[i], ks[j][i], s);
+        s *= d.scale;
+        if (s > m) {
+          const float corr = expf(m - s);
+          l = l * corr + 1.f;
+#pragma unroll
+          for (int i = 0; i < D; ++i) o[i] = fmaf(o[i], corr, vs[j][i]);
+          m = s;
+        } else {
+          const float p = expf(s - m);
+          l += p;
+#pragma unroll
+          for (int i = 0; i < D; ++i) o[i] = fmaf(p, vs[j][i], o[i]);
+        }
+      }
+    }
+  }
+  (void)nkeys_total;
+  if (qrow < d.lq) {
+    float* op = (float*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int i = 0; i < D; ++i) op[i] = o[i] * inv;
+  }
+}
+
+}  // namespace
+
+extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* desc) {
+  SR_CHECK(desc, SR_EINVAL, "sr_attention: null desc");
+  const sr_attn_desc& d = *desc;
+  SR_CHECK(d.q && d.o && d.k0 && d.v0, SR_EINVAL, "sr_attention: null q/k0/v0/o");
+  SR_CHECK(d.batch > 0 && d.heads > 0 && d.lq > 0 && d.l0 > 0 && d.l1 >= 0, SR_EINVAL,
+           "sr_attention: bad sizes batch=%d heads=%d lq=%d l0=%d l1=%d", d.batch, d.heads, d.lq, d.l0, d.l1);
+  SR_CHECK(d.l1 == 0 || (d.k1 && d.v1), SR_EINVAL, "sr_attention: segment 1 needs k1/v1");
+  SR_CHECK(d.mask_mode == SR_MASK_NONE || (d.mask_mode == SR_MASK_CAMERA && d.l1 == 0), SR_EINVAL,
+           "sr_attention: bad mask_mode %d", d.mask_mode);
+  AttnArgs a;
+  a.d = d;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16) {
+    SR_CHECK(d.head_dim == 64, SR_EUNSUPPORTED, "sr_attention(bf16): head_dim must be 64 (got %d)", d.head_dim);
+    SR_CHECK(d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED, "sr_attention(bf16): camera mask needs the f32 kernel");
+    SR_CHECK(d.ldq % 8 == 0 && d.ldk0 % 8 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0 &&
+                 (d.l1 == 0 || (d.ldk1 % 8 == 0 && d.ldv1 % 8 == 0)),
+             SR_EINVAL, "sr_attention(bf16): leading dims must be multiples of 8");
+    a.ntile0 = (d.l0 + KT - 1) / KT;
+    a.ntile1 = (d.l1 + KT - 1) / KT;
+    dim3 grid((d.lq + QROWS - 1) / QROWS, d.heads, d.batch);
+    hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, a);
+    return sr::check_launch("sr_attention(bf16)");
+  }
+  SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attention: bad dtype %d", dtype);
+  a.ntile0 = a.ntile1 = 0;
+  dim3 grid((d.lq + F32_THREADS - 1) / F32_THREADS, d.heads, d.batch);
+  if (d.head_dim == 64) {
+    hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(F32_THREADS), 0, s, a);
+  } else if (d.head_dim == 128) {
+    hipLaunchKernelGGL(attn_f32_kernel<128>, grid, dim3(F32_THREADS), 0, s, a);
+  } else {
+    sr::set_error("sr_attention(f32): head_dim must be 64 or 128 (got %d)", d.head_dim);
+    return SR_EUNSUPPORTED;
+  }
+  return sr::check_launch("sr_attention(f32)");
+}

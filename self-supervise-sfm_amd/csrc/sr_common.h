@@ -1,0 +1,87 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of libsfm_amd.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sfm_amd.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+namespace sr {
+
+// thread-local error message; set by host wrappers on failure
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+template <typename T> struct is_bf16 { static constexpr bool value = false; };
+template <> struct is_bf16<bf16> { static constexpr bool value = true; };
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
+
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// raw workgroup barrier that does NOT drain in-flight LDS-DMA (vmcnt); memory clobbers keep
+// the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void barrier_raw() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS address (32-bit) of a __shared__ pointer.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// One LDS-DMA wave-instruction: lane l copies 16 B from gptr (per lane) to
+// LDS[lds_base + 16*l] (lds_base wave-uniform).  Issued from inline asm so that the
+// compiler's waitcnt pass does not see an aliasing LDS write and drain it with
+// vmcnt(0) before every ds_read; the caller owns the counted s_waitcnt vmcnt(N).
+__device__ __forceinline__ void dma16(const void* gptr, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_base)
+               : "memory", "m0");
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks that share an XCD (same b % 8) get a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, local = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + local;
+}
+
+}  // namespace sr
+
+#define SR_CHECK(cond, code, ...)     \
+  do {                                \
+    if (!(cond)) {                    \
+      sr::set_error(__VA_ARGS__);     \
+      return (code);                  \
+    }                                 \
+  } while (0)

@@ -1,0 +1,321 @@
+// GEMM  out = epilogue(A[M,K] . W[N,K]^T)  for gfx950.
+//
+// Replaces nn.Linear (addmm) on the hot path: qkv / proj (attention.py:48,52,73,120),
+// fc1 / fc2 (mlp.py:34-40) and the patch-embed conv as an im2col GEMM
+// (patch_embed.py:62-64,78).  Both operands are K-contiguous ("NT"), which is the
+// natural MFMA operand layout: every lane reads 16 contiguous bytes of one row.
+//
+// Structure (v1):
+//   * 128x128 output tile per 256-thread workgroup, 4 waves as 2x2, 64x64 per wave;
+//   * K staged 128 bytes per row per k-tile (64 bf16 / 32 f32) by LDS-DMA
+//     (global_load_lds_dwordx4), double-buffered; the next tile's DMA stays in flight
+//     across the raw s_barrier (counted vmcnt, cdna_hip_programming.md §5);
+//   * LDS rows XOR-swizzled (16-B chunk ^= (row>>1)&7) on the DMA SOURCE address and on
+//     the ds_read_b128 address, conflict-free for the MFMA fragment pattern;
+//   * bf16: v_mfma_f32_16x16x32_bf16, one per 16-B chunk pair;
+//     f32 (parity mode): four v_mfma_f32_16x16x4_f32 per chunk pair — exact fp32;
+//   * bijective XCD-aware tile remap so tiles that share A rows share an L2;
+//   * epilogues fused in registers: bias, erf-GELU, LayerScale+residual, patch remap +
+//     positional add, and qk-LayerNorm + 2-D RoPE (each wave owns one 64-wide head).
+#include <cstdio>
+
+#include "sr_common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128;
+constexpr int ROWB = 128;                     // bytes per tile row per k-tile
+constexpr int STAGE_BYTES = (BM + BN) * ROWB; // 32 KiB
+constexpr int NTHREADS = 256;
+
+struct GemmArgs {
+  const char* A;
+  int64_t lda_b;
+  const char* W;
+  int64_t ldw_b;
+  void* out;
+  int64_t ldo;
+  int M, N, K, ktiles;
+  sr_gemm_epi ep;
+};
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  static constexpr int KT = 64;
+  __device__ __forceinline__ static void run(const uint4& a, const uint4& b, f32x4& c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static constexpr int KT = 32;
+  // lane group g holds k = 4*(chunk) + j; MFMA j consumes element j of every lane's chunk:
+  // A and B use the same k permutation, so the sum over (g, j) covers the chunk exactly.
+  __device__ __forceinline__ static void run(const uint4& a, const uint4& b, f32x4& c) {
+    const f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], c, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ float group16_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
+  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // LDS-DMA sources: instruction i of wave w fills tile rows (w*8+i)*8 .. +8 (rows < BM: A, else W).
+  const char* src[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tr = (wave * 8 + i) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
+    if (tr < BM) {
+      const int r = min(m0 + tr, g.M - 1);
+      src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
+    } else {
+      const int r = n0 + tr - BM;
+      src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
+    }
+  }
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
+  auto stage = [&](int kt, int buf) {
+    const uint32_t base = dst0 + buf * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+  };
+
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int swz = lr >> 1;  // (row>>1)&7 for every fragment row of this lane
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  for (int kt = 0; kt < g.ktiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < g.ktiles) {
+      stage(kt + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sr::barrier_raw();
+    const char* sb = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int coff = (((ks * 4 + lg) ^ swz) * 16);
+      uint4 a[4], b[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + (wr * 64 + mi * 16 + lr) * ROWB + coff);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) b[ni] = *(const uint4*)(sb + (BM + wc * 64 + ni * 16 + lr) * ROWB + coff);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) Mma<T>::run(a[mi], b[ni], acc[mi][ni]);
+    }
+    sr::wait_lgkm0();
+    sr::barrier_raw();
+  }
+
+  // ---------------- epilogue ----------------
+  const sr_gemm_epi& ep = g.ep;
+  const int colw = n0 + wc * 64;  // first output column of this wave
+  float bias[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) bias[ni] = ep.bias ? ep.bias[colw + ni * 16 + lr] : 0.f;
+
+  if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
+    T* out = (T*)g.out;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
+        if (row < g.M) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            float v = acc[mi][ni][r] + bias[ni];
+            if constexpr (EPI == SR_EPI_BIAS_GELU) v = sr::gelu_erf(v);
+            out[(int64_t)row * g.ldo + colw + ni * 16 + lr] = sr::from_f32<T>(v);
+          }
+        }
+      }
+  } else if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    float* x = (float*)g.out;
+    float gam[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) gam[ni] = ep.gamma[colw + ni * 16 + lr];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
+        if (row < g.M) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            float* p = x + (int64_t)row * g.ldo + colw + ni * 16 + lr;
+            *p = *p + (acc[mi][ni][r] + bias[ni]) * gam[ni];
+          }
+        }
+      }
+  } else if constexpr (EPI == SR_EPI_PATCH) {
+    float* x = (float*)g.out;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
+        if (row < g.M) {
+          const int f = row / ep.seg_rows, p = row - f * ep.seg_rows;
+          const int64_t orow = (int64_t)f * ep.seg_stride + ep.seg_offset + p;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            const int col = colw + ni * 16 + lr;
+            x[orow * g.ldo + col] = acc[mi][ni][r] + bias[ni] + ep.row_add[(int64_t)p * g.N + col];
+          }
+        }
+      }
+  } else if constexpr (EPI == SR_EPI_QKV) {
+    T* out = (T*)g.out;
+    const int region = (colw + ep.col_offset) / ep.embed_dim;  // 0 = Q, 1 = K, 2 = V
+    const bool qk = region < 2;
+    const float* nw = region == 0 ? ep.qn_w : ep.kn_w;
+    const float* nb = region == 0 ? ep.qn_b : ep.kn_b;
+    const bool do_norm = qk && nw != nullptr;
+    const bool do_rope = qk && ep.rope_cos != nullptr;
+    float w4[4], b4[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      w4[ni] = do_norm ? nw[ni * 16 + lr] : 1.f;
+      b4[ni] = do_norm ? nb[ni * 16 + lr] : 0.f;
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
+        float v[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) v[ni] = acc[mi][ni][r] + bias[ni];
+        if (do_norm) {  // LayerNorm over the 64 head columns: 4 per lane x 16 lanes
+          const float mean = group16_sum(v[0] + v[1] + v[2] + v[3]) * (1.f / 64.f);
+          float d2 = 0.f;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            v[ni] -= mean;
+            d2 += v[ni] * v[ni];
+          }
+          const float rstd = rsqrtf(group16_sum(d2) * (1.f / 64.f) + ep.qk_eps);
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) v[ni] = v[ni] * rstd * w4[ni] + b4[ni];
+        }
+        if (do_rope) {
+          const int rr = min(row, g.M - 1);
+          int py = 0, px = 0;
+          if (ep.pos_yx) {
+            py = ep.pos_yx[2 * rr];
+            px = ep.pos_yx[2 * rr + 1];
+          } else {
+            const int64_t tr = ep.pos_rowmap ? (int64_t)ep.pos_rowmap[rr] : ep.pos_row_base + rr;
+            const int t = (int)(tr % ep.tokens_per_frame);
+            if (t >= ep.patch_start) {
+              const int p = t - ep.patch_start;
+              py = p / ep.grid_w + 1;
+              px = p - (py - 1) * ep.grid_w + 1;
+            }
+          }
+          const float cy = ep.rope_cos[py * 16 + lr], sy = ep.rope_sin[py * 16 + lr];
+          const float cx = ep.rope_cos[px * 16 + lr], sx = ep.rope_sin[px * 16 + lr];
+          const float y0 = v[0] * cy - v[1] * sy, y1 = v[1] * cy + v[0] * sy;
+          const float x0 = v[2] * cx - v[3] * sx, x1 = v[3] * cx + v[2] * sx;
+          v[0] = y0;
+          v[1] = y1;
+          v[2] = x0;
+          v[3] = x1;
+        }
+        if (row < g.M) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) out[(int64_t)row * g.ldo + colw + ni * 16 + lr] = sr::from_f32<T>(v[ni]);
+        }
+      }
+  }
+}
+
+template <typename T, int EPI>
+int launch(const GemmArgs& a, hipStream_t s) {
+  const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg), dim3(NTHREADS), 0, s, a);
+  return sr::check_launch("sr_gemm");
+}
+
+template <typename T>
+int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
+  switch (epi) {
+    case SR_EPI_BIAS: return launch<T, SR_EPI_BIAS>(a, s);
+    case SR_EPI_BIAS_GELU: return launch<T, SR_EPI_BIAS_GELU>(a, s);
+    case SR_EPI_BIAS_RESID: return launch<T, SR_EPI_BIAS_RESID>(a, s);
+    case SR_EPI_QKV: return launch<T, SR_EPI_QKV>(a, s);
+    case SR_EPI_PATCH: return launch<T, SR_EPI_PATCH>(a, s);
+  }
+  sr::set_error("sr_gemm: unknown epilogue %d", epi);
+  return SR_EINVAL;
+}
+
+}  // namespace
+
+extern "C" int sr_gemm(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
+                       int64_t ldw, void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep) {
+  SR_CHECK(A && W && out && ep, SR_EINVAL, "sr_gemm: null pointer");
+  SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_gemm: bad dtype %d", dtype);
+  SR_CHECK(M > 0 && N > 0 && K > 0, SR_EINVAL, "sr_gemm: bad shape M=%d N=%d K=%d", M, N, K);
+  const int kt = dtype == SR_BF16 ? Mma<bf16>::KT : Mma<float>::KT;
+  const int esz = dtype == SR_BF16 ? 2 : 4;
+  SR_CHECK(N % BN == 0, SR_EUNSUPPORTED, "sr_gemm: N=%d must be a multiple of %d", N, BN);
+  SR_CHECK(K % kt == 0, SR_EUNSUPPORTED, "sr_gemm: K=%d must be a multiple of %d", K, kt);
+  SR_CHECK(lda >= K && ldw >= K && (lda * esz) % 16 == 0 && (ldw * esz) % 16 == 0, SR_EINVAL,
+           "sr_gemm: bad leading dims lda=%lld ldw=%lld", (long long)lda, (long long)ldw);
+  SR_CHECK(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0, SR_EINVAL, "sr_gemm: A/W must be 16-B aligned");
+  if (epi == SR_EPI_BIAS_RESID) SR_CHECK(ep->gamma, SR_EINVAL, "sr_gemm: RESID needs gamma");
+  if (epi == SR_EPI_PATCH)
+    SR_CHECK(ep->row_add && ep->seg_rows > 0 && ep->seg_stride >= ep->seg_rows, SR_EINVAL, "sr_gemm: PATCH params");
+  if (epi == SR_EPI_QKV) {
+    SR_CHECK(ep->head_dim == 64 && ep->embed_dim % 64 == 0 && ep->embed_dim > 0, SR_EUNSUPPORTED,
+             "sr_gemm: QKV epilogue needs head_dim 64 (got %d)", ep->head_dim);
+    if (ep->rope_cos)
+      SR_CHECK(ep->rope_sin && ep->rope_npos > 0 &&
+                   (ep->pos_yx || (ep->tokens_per_frame > ep->patch_start && ep->grid_w > 0)),
+               SR_EINVAL, "sr_gemm: QKV rope params");
+  }
+  GemmArgs a;
+  a.A = (const char*)A;
+  a.lda_b = lda * esz;
+  a.W = (const char*)W;
+  a.ldw_b = ldw * esz;
+  a.out = out;
+  a.ldo = ldo;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.ktiles = K / kt;
+  a.ep = *ep;
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == SR_BF16 ? dispatch<bf16>(epi, a, s) : dispatch<float>(epi, a, s);
+}

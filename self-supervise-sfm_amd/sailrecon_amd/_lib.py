@@ -1,0 +1,105 @@
+"""ctypes binding of libsfm_amd.so (the C ABI declared in include/sfm_amd.h).
+
+The library is built in-tree (``make -C self-supervise-sfm_amd/csrc``) and loaded
+from this package directory.  torch is imported first so that the HIP runtime
+(``libamdhip64.so.7``) the library depends on resolves to the one torch already
+loaded — one runtime, one set of streams.  There is no fallback: if the library is
+missing, every op raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load the HIP runtime before the library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsfm_amd.so")
+
+SR_F32, SR_BF16 = 0, 1
+SR_EPI_BIAS, SR_EPI_BIAS_GELU, SR_EPI_BIAS_RESID, SR_EPI_QKV, SR_EPI_PATCH = 0, 1, 2, 3, 4
+SR_MASK_NONE, SR_MASK_CAMERA = 0, 1
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+
+
+class GemmEpi(ctypes.Structure):
+    _fields_ = [
+        ("bias", _vp), ("gamma", _vp),
+        ("qn_w", _vp), ("qn_b", _vp), ("kn_w", _vp), ("kn_b", _vp), ("qk_eps", _f32),
+        ("rope_cos", _vp), ("rope_sin", _vp), ("rope_npos", _i32),
+        ("col_offset", _i32), ("head_dim", _i32), ("embed_dim", _i32),
+        ("pos_yx", _vp), ("pos_rowmap", _vp), ("pos_row_base", _i64),
+        ("tokens_per_frame", _i32), ("patch_start", _i32), ("grid_w", _i32),
+        ("seg_rows", _i32), ("seg_stride", _i32), ("seg_offset", _i32), ("row_add", _vp),
+    ]
+
+
+class AttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("q", _vp), ("ldq", _i64),
+        ("k0", _vp), ("v0", _vp), ("ldk0", _i64), ("ldv0", _i64),
+        ("k1", _vp), ("v1", _vp), ("ldk1", _i64), ("ldv1", _i64),
+        ("o", _vp), ("ldo", _i64),
+        ("batch", _i32), ("heads", _i32), ("head_dim", _i32),
+        ("lq", _i32), ("q_bstride", _i64),
+        ("l0", _i32), ("k0_bstride", _i64),
+        ("l1", _i32), ("k1_bstride", _i64),
+        ("mask_mode", _i32), ("n_anchor", _i32),
+        ("scale", _f32),
+    ]
+
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "sr_last_error": (ctypes.c_char_p, []),
+    "sr_version": (_i32, []),
+    "sr_gemm": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, ctypes.POINTER(GemmEpi)]),
+    "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
+    "sr_layernorm": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _f32, _vp, _i64, _i32, _i32]),
+    "sr_im2col_normalize": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, ctypes.POINTER(_f32),
+                                   ctypes.POINTER(_f32), _vp, _i32]),
+    "sr_set_special_tokens": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32]),
+    "sr_copy_rows_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i32, _i32]),
+    "sr_linear_small_f32": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32]),
+    "sr_silu_f32": (_i32, [_vp, _vp, _vp, _i64]),
+    "sr_adaln_modulate_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32]),
+    "sr_pose_update_f32": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _i32]),
+    "sr_pose_decode_f32": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
+}
+EXPORTED = tuple(_PROTOS)
+
+
+class SfmAmdError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and return the library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SfmAmdError(
+            f"libsfm_amd.so not found at {path}: build it with `make -C self-supervise-sfm_amd/csrc` "
+            "(there is no CPU fallback)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().sr_last_error().decode(errors="replace")
+        raise SfmAmdError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,108 @@
+"""Block parameter mirror + standalone device forward (reference: sailrecon/layers/block.py).
+
+``Block.forward(x, pos=None, attn_mask=None)`` keeps the reference signature
+(block.py:86).  It runs the whole block on the HIP path (runtime.run_block) for
+x on a ROCm device: bf16 under autocast, exact fp32 otherwise.  Supported masks:
+None, or the camera-trunk pattern (camera_head.py:197-228: the first n rows see
+only each other, later rows see the first n plus themselves) — the only masks the
+reference passes to a Block outside the aggregator's reloc stack, which the
+aggregator drives directly with its implicit block mask.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+from torch import Tensor, nn
+
+from .. import _lib, ops, runtime
+from .attention import Attention
+from .layer_scale import LayerScale
+from .mlp import Mlp
+
+
+def camera_mask_anchors(attn_mask: Tensor) -> Optional[int]:
+    """If ``attn_mask`` (True = attend, [1,1,S,S] or [S,S]) is the camera-trunk pattern,
+    return its anchor count; else None."""
+    m = attn_mask.reshape(attn_mask.shape[-2], attn_mask.shape[-1]).bool().cpu()
+    S = m.shape[0]
+    for n in range(1, S + 1):
+        ref = torch.zeros(S, S, dtype=torch.bool)
+        ref[:, :n] = True
+        idx = torch.arange(n, S)
+        ref[:n, n:] = False
+        ref[idx, idx] = True
+        if torch.equal(ref, m):
+            return n
+    return None
+
+
+class Block(nn.Module):
+    def __init__(self, dim: int, num_heads: int, mlp_ratio: float = 4.0, qkv_bias: bool = True,
+                 proj_bias: bool = True, ffn_bias: bool = True, drop: float = 0.0, attn_drop: float = 0.0,
+                 init_values=None, drop_path: float = 0.0, act_layer: Callable[..., nn.Module] = nn.GELU,
+                 norm_layer: Callable[..., nn.Module] = nn.LayerNorm, attn_class: Callable[..., nn.Module] = Attention,
+                 ffn_layer: Callable[..., nn.Module] = Mlp, qk_norm: bool = False, fused_attn: bool = True,
+                 rope=None, kv_cache: bool = False) -> None:
+        super().__init__()
+        self.norm1 = norm_layer(dim)
+        self.attn = attn_class(dim, num_heads=num_heads, qkv_bias=qkv_bias, proj_bias=proj_bias,
+                               attn_drop=attn_drop, proj_drop=drop, qk_norm=qk_norm, fused_attn=fused_attn,
+                               rope=rope, kv_cache=kv_cache)
+        self.ls1 = LayerScale(dim, init_values=init_values) if init_values else nn.Identity()
+        self.norm2 = norm_layer(dim)
+        self.mlp = ffn_layer(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop,
+                             bias=ffn_bias)
+        self.ls2 = LayerScale(dim, init_values=init_values) if init_values else nn.Identity()
+        self.sample_drop_ratio = drop_path
+        self._packed = {}
+
+    def packed(self, dtype: torch.dtype) -> runtime.PackedBlock:
+        if dtype not in self._packed:
+            self._packed[dtype] = runtime.pack_block(self, dtype)
+        return self._packed[dtype]
+
+    def invalidate_packed(self):
+        self._packed.clear()
+
+    def forward(self, x: Tensor, pos: Optional[Tensor] = None, attn_mask: Optional[Tensor] = None) -> Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("sailrecon_amd Block runs on the HIP path only (x must be on a ROCm device)")
+        dtype = runtime.compute_dtype()
+        B, N, C = x.shape
+        pb = self.packed(dtype)
+        n_anchor = None
+        if attn_mask is not None:
+            n_anchor = camera_mask_anchors(attn_mask)
+            if n_anchor is None:
+                raise NotImplementedError("Block.forward: only None or the camera-trunk mask is supported")
+            if B != 1:
+                raise NotImplementedError("Block.forward: masked attention needs B == 1")
+        if n_anchor is not None or pb.head_dim != 64:
+            dtype = torch.float32
+            pb = self.packed(dtype)
+        xf = x.detach().reshape(B * N, C).float().contiguous().clone()
+        ws = runtime.Workspace()
+        sc = runtime.scratch(ws, B * N, C, pb.w_fc1.shape[0], dtype, x.device)
+        rope = None
+        qkv_epi = None
+        if self.attn.rope is not None and pos is not None:
+            rope = self.attn.rope.tables(pb.head_dim, int(pos.max()) + 1, x.device)
+            pos_yx = pos.reshape(B * N, 2).to(device=x.device, dtype=torch.int32).contiguous()
+            qkv_epi = runtime.qkv_params(pb, rope, pos_yx=pos_yx)
+        else:
+            qkv_epi = runtime.qkv_params(pb, None)
+        if n_anchor is None:
+            attend = runtime.frame_attend(pb, B, N)
+        else:
+            def attend(qkv, o):
+                ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=pb.heads, head_dim=pb.head_dim,
+                              batch=1, lq=N, q_bstride=0, l0=N, k0_bstride=0, mask_mode=_lib.SR_MASK_CAMERA,
+                              n_anchor=n_anchor)
+        runtime.run_block(pb, xf, 0, B * N, sc, attend, qkv_epi)
+        return xf.view(B, N, C).to(x.dtype)
+
+
+class NestedTensorBlock(Block):
+    """DINOv2 block class name (block.py:271); tensors only (no xFormers nesting)."""

@@ -1,0 +1,78 @@
+"""SailRecon façade — drop-in for sailrecon/models/sail_recon.py:24-159.
+
+``SailRecon(...).forward(views, no_reloc_list=None, reloc_list=None, fix_rank=300)``
+returns one dict per query view, like the reference (sail_recon.py:153-159).  The
+aggregator and camera head run on the HIP path; the DPT point/depth heads
+ are separate modules that are only evaluated when enabled.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..heads.camera_head import CameraHead
+from ..utils.pose_enc import pose_encoding_to_extri_intri
+from .aggregator import Aggregator
+
+
+class SailRecon(nn.Module):
+    def __init__(self, img_size=518, patch_size=14, embed_dim=1024, enable_camera=True, enable_point=True,
+                 enable_depth=True, enable_track=True, kv_cache=False):
+        super().__init__()
+        self.aggregator = Aggregator(img_size=img_size, patch_size=patch_size, embed_dim=embed_dim, kv_cache=kv_cache)
+        self.camera_head = CameraHead(dim_in=2 * embed_dim) if enable_camera else None
+        self.point_head = None
+        self.depth_head = None
+        if enable_point or enable_depth:
+            from ..heads.dpt_head import DPTHead  # §8(f) rank 1
+            if enable_point:
+                self.point_head = DPTHead(dim_in=2 * embed_dim, output_dim=4, activation="inv_log",
+                                          conf_activation="expp1")
+            if enable_depth:
+                self.depth_head = DPTHead(dim_in=2 * embed_dim, output_dim=2, activation="exp",
+                                          conf_activation="expp1")
+        self.cam_token_last_layer = None
+        self.need_re_forward = False
+
+    def forward(self, views, no_reloc_list=None, reloc_list=None, fix_rank=300):
+        rgbs = views if isinstance(views, torch.Tensor) else torch.cat([v["img"] for v in views], dim=0)
+        if rgbs.dim() == 4:
+            rgbs = rgbs.unsqueeze(0)
+        if no_reloc_list is None:
+            no_reloc_list = list(range(rgbs.shape[1]))
+        if reloc_list is None:
+            reloc_list = list(range(rgbs.shape[1]))
+        rgb_feats, idx_patch, cam_token_last_layer = self.aggregator(rgbs, no_reloc_list, reloc_list,
+                                                                     fix_rank=fix_rank)
+        reloc_rgbs = rgbs[:, reloc_list]
+        cam_tokens = rgb_feats[-1][:, :, 0]
+        predictions = {}
+        with torch.autocast("cuda", enabled=False):  # heads in fp32, sail_recon.py:118-119
+            if self.camera_head is not None:
+                cam_maps = self.camera_head(rgb_feats, cam_token_last_layer)
+                extrinsic, intrinsic = pose_encoding_to_extri_intri(cam_maps[-1], (rgbs.shape[-2], rgbs.shape[-1]))
+                predictions["extrinsic"] = extrinsic
+                predictions["intrinsic"] = intrinsic
+                predictions["pose_enc"] = cam_maps[-1]
+            if self.point_head is not None:
+                xyz_map, xyz_cnf = self.point_head(rgb_feats, images=reloc_rgbs, patch_start_idx=idx_patch)
+                predictions["point_map"] = xyz_map
+                predictions["xyz_cnf"] = xyz_cnf
+            if self.depth_head is not None:
+                dpt_map, dpt_cnf = self.depth_head(rgb_feats, images=reloc_rgbs, patch_start_idx=idx_patch)
+                predictions["depth_map"] = dpt_map
+                predictions["dpt_cnf"] = dpt_cnf
+                if self.camera_head is not None:
+                    from ..utils.geometry import unproject_depth_map_to_point_map
+                    pts = unproject_depth_map_to_point_map(dpt_map.squeeze(0), predictions["extrinsic"].squeeze(0),
+                                                           predictions["intrinsic"].squeeze(0))
+                    predictions["point_map_by_unprojection"] = pts[None]
+        predictions["rgbs"] = reloc_rgbs
+        predictions["cam_tokens"] = cam_tokens
+        predictions["images"] = reloc_rgbs
+        final_results = [{} for _ in range(len(reloc_list))]
+        for key, value in predictions.items():
+            for i in range(len(reloc_list)):
+                final_results[i][key] = value[:, i]
+        return final_results

@@ -1,0 +1,178 @@
+"""Tensor-level wrappers over the C ABI (include/sfm_amd.h).
+
+Every function takes device tensors (2-D row-strided views, unit column stride),
+launches on the current torch stream and returns nothing (outputs are written in
+place).  No function here computes anything on the host.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import AttnDesc, GemmEpi, check
+
+Tensor = torch.Tensor
+
+
+def _p(t: Optional[Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.bfloat16:
+        return _lib.SR_BF16
+    if dt == torch.float32:
+        return _lib.SR_F32
+    raise TypeError(f"unsupported dtype {dt} (bf16 or fp32)")
+
+
+def _rowmajor(t: Tensor, name: str) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be a 2-D view with unit column stride, got shape {tuple(t.shape)} "
+                         f"stride {t.stride()}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    return t.stride(0)
+
+
+def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] = None,
+         gamma: Optional[Tensor] = None, rows: Optional[int] = None, qkv: Optional[dict] = None,
+         patch: Optional[dict] = None) -> None:
+    """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows)."""
+    lda = _rowmajor(a, "a")
+    ldw = _rowmajor(w, "w")
+    ldo = _rowmajor(out, "out")
+    M = a.shape[0] if rows is None else rows
+    N, K = w.shape
+    if a.shape[1] != K:
+        raise ValueError(f"gemm: a has K={a.shape[1]}, w has K={K}")
+    if a.dtype != w.dtype:
+        raise TypeError("gemm: a and w dtypes differ")
+    ep = GemmEpi()
+    ep.bias = _p(bias)
+    ep.gamma = _p(gamma)
+    if qkv is not None:
+        ep.qn_w, ep.qn_b = _p(qkv.get("qn_w")), _p(qkv.get("qn_b"))
+        ep.kn_w, ep.kn_b = _p(qkv.get("kn_w")), _p(qkv.get("kn_b"))
+        ep.qk_eps = qkv.get("qk_eps", 1e-5)
+        cos, sin = qkv.get("rope_cos"), qkv.get("rope_sin")
+        ep.rope_cos, ep.rope_sin = _p(cos), _p(sin)
+        ep.rope_npos = 0 if cos is None else cos.shape[0]
+        ep.col_offset = qkv.get("col_offset", 0)
+        ep.head_dim = qkv.get("head_dim", 64)
+        ep.embed_dim = qkv["embed_dim"]
+        ep.pos_yx = _p(qkv.get("pos_yx"))
+        ep.pos_rowmap = _p(qkv.get("pos_rowmap"))
+        ep.pos_row_base = qkv.get("pos_row_base", 0)
+        ep.tokens_per_frame = qkv.get("tokens_per_frame", 1)
+        ep.patch_start = qkv.get("patch_start", 0)
+        ep.grid_w = qkv.get("grid_w", 1)
+    if patch is not None:
+        ep.seg_rows = patch["seg_rows"]
+        ep.seg_stride = patch["seg_stride"]
+        ep.seg_offset = patch["seg_offset"]
+        ep.row_add = _p(patch["row_add"])
+    rc = _lib.load().sr_gemm(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
+                             M, N, K, ctypes.byref(ep))
+    check(rc, "sr_gemm")
+
+
+def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
+              q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
+              l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
+              scale: Optional[float] = None) -> None:
+    """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc."""
+    d = AttnDesc()
+    d.q, d.ldq = _p(q), _rowmajor(q, "q")
+    d.k0, d.ldk0 = _p(k0), _rowmajor(k0, "k0")
+    d.v0, d.ldv0 = _p(v0), _rowmajor(v0, "v0")
+    if l1 > 0:
+        d.k1, d.ldk1 = _p(k1), _rowmajor(k1, "k1")
+        d.v1, d.ldv1 = _p(v1), _rowmajor(v1, "v1")
+    d.o, d.ldo = _p(o), _rowmajor(o, "o")
+    d.batch, d.heads, d.head_dim = batch, heads, head_dim
+    d.lq, d.q_bstride = lq, q_bstride
+    d.l0, d.k0_bstride = l0, k0_bstride
+    d.l1, d.k1_bstride = l1, k1_bstride
+    d.mask_mode, d.n_anchor = mask_mode, n_anchor
+    d.scale = head_dim ** -0.5 if scale is None else scale
+    rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
+    check(rc, "sr_attention")
+
+
+def layernorm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float, out: Tensor,
+              rowmap: Optional[Tensor] = None, rows: Optional[int] = None) -> None:
+    ldx = _rowmajor(x, "x")
+    ldo = _rowmajor(out, "out")
+    if x.dtype != torch.float32:
+        raise TypeError("layernorm input must be fp32")
+    n = out.shape[0] if rows is None else rows
+    rc = _lib.load().sr_layernorm(_stream(x), dtype_code(out.dtype), _p(x), ldx, _p(rowmap), _p(w), _p(b),
+                                  eps, _p(out), ldo, n, x.shape[1])
+    check(rc, "sr_layernorm")
+
+
+_MEAN = (0.485, 0.456, 0.406)  # aggregator.py:31-32
+_STD = (0.229, 0.224, 0.225)
+
+
+def im2col_normalize(img: Tensor, patch: int, out: Tensor, kpad: int) -> None:
+    if not img.is_contiguous() or img.dtype != torch.float32:
+        raise ValueError("im2col: images must be contiguous fp32 [F,3,H,W]")
+    F_, C_, H, W = img.shape
+    mean = (ctypes.c_float * 3)(*_MEAN)
+    std = (ctypes.c_float * 3)(*_STD)
+    rc = _lib.load().sr_im2col_normalize(_stream(img), dtype_code(out.dtype), _p(img), F_, H, W, patch, mean, std,
+                                         _p(out), kpad)
+    check(rc, "sr_im2col_normalize")
+
+
+def set_special_tokens(x: Tensor, frames: int, tokens_per_frame: int, table: Tensor, type_of_frame: Tensor) -> None:
+    n_types, n_special, cols = table.shape
+    rc = _lib.load().sr_set_special_tokens(_stream(x), _p(x), _rowmajor(x, "x"), frames, tokens_per_frame, n_special,
+                                           _p(table), _p(type_of_frame), cols)
+    check(rc, "sr_set_special_tokens")
+
+
+def copy_rows(dst: Tensor, src: Tensor, rows: int, rowmap: Optional[Tensor] = None) -> None:
+    rc = _lib.load().sr_copy_rows_f32(_stream(dst), _p(dst), _rowmajor(dst, "dst"), _p(src), _rowmajor(src, "src"),
+                                      _p(rowmap), rows, dst.shape[1])
+    check(rc, "sr_copy_rows_f32")
+
+
+def linear_small(a: Tensor, w: Tensor, bias: Optional[Tensor], out: Tensor, rows: int, act_in: int = 0,
+                 lda: Optional[int] = None) -> None:
+    N, K = w.shape
+    lda = a.stride(0) if lda is None else lda
+    rc = _lib.load().sr_linear_small_f32(_stream(out), _p(a), lda, _p(w), _p(bias), _p(out),
+                                         _rowmajor(out, "out"), rows, N, K, act_in)
+    check(rc, "sr_linear_small_f32")
+
+
+def silu(x: Tensor, y: Tensor) -> None:
+    check(_lib.load().sr_silu_f32(_stream(x), _p(x), _p(y), x.numel()), "sr_silu_f32")
+
+
+def adaln_modulate(xn: Tensor, x: Tensor, mod: Tensor, out: Tensor) -> None:
+    rows, cols = x.shape
+    check(_lib.load().sr_adaln_modulate_f32(_stream(x), _p(xn), _p(x), _p(mod), _p(out), rows, cols),
+          "sr_adaln_modulate_f32")
+
+
+def pose_update(pred: Tensor, delta: Tensor, act: Tensor, first: bool) -> None:
+    check(_lib.load().sr_pose_update_f32(_stream(pred), _p(pred), _p(delta), delta.stride(0), _p(act),
+                                         pred.shape[0], int(first)), "sr_pose_update_f32")
+
+
+def pose_decode(enc: Tensor, hw, ext: Tensor, intr: Tensor) -> None:
+    H, W = hw
+    check(_lib.load().sr_pose_decode_f32(_stream(enc), _p(enc), enc.stride(0), enc.shape[0], int(H), int(W),
+                                         _p(ext), _p(intr)), "sr_pose_decode_f32")

@@ -1,0 +1,162 @@
+"""Block executor: packed weights + workspace + the per-block kernel sequence.
+
+One transformer Block (reference block.py:86-112, attention.py:70-122,
+mlp.py:34-40) is seven launches on the HIP path:
+
+    LN1 -> GEMM qkv (+bias, qk-LayerNorm, RoPE fused) -> attention
+        -> GEMM proj (+bias, LayerScale, residual add fused, in place on x)
+    LN2 -> GEMM fc1 (+bias, erf-GELU fused) -> GEMM fc2 (+bias, LayerScale, residual)
+
+The residual stream x is fp32 [rows, C] (as under the reference's bf16 autocast,
+where LayerScale's fp32 gamma promotes every residual add to fp32).  Workspace
+buffers are indexed with the SAME absolute rows as x, so blocks over disjoint row
+ranges (global anchors vs reloc queries) never share scratch.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+
+from . import _lib, ops
+
+Tensor = torch.Tensor
+
+
+def compute_dtype(explicit: Optional[torch.dtype] = None) -> torch.dtype:
+    """bf16 when the caller runs under autocast (demo_imc_forward.py:93), else fp32 parity mode."""
+    if explicit is not None:
+        return torch.bfloat16 if explicit in (torch.bfloat16, torch.float16) else torch.float32
+    if torch.is_autocast_enabled("cuda"):
+        return torch.bfloat16
+    return torch.float32
+
+
+@dataclass
+class PackedBlock:
+    dim: int
+    heads: int
+    head_dim: int
+    eps: float
+    qk_eps: float
+    qk_norm: bool
+    ln1_w: Tensor
+    ln1_b: Tensor
+    ln2_w: Tensor
+    ln2_b: Tensor
+    w_qkv: Tensor
+    b_qkv: Optional[Tensor]
+    qn_w: Optional[Tensor]
+    qn_b: Optional[Tensor]
+    kn_w: Optional[Tensor]
+    kn_b: Optional[Tensor]
+    w_proj: Tensor
+    b_proj: Optional[Tensor]
+    g1: Tensor
+    w_fc1: Tensor
+    b_fc1: Optional[Tensor]
+    w_fc2: Tensor
+    b_fc2: Optional[Tensor]
+    g2: Tensor
+
+
+def _f32(t: Optional[Tensor]) -> Optional[Tensor]:
+    return None if t is None else t.detach().float().contiguous()
+
+
+def _gamma(ls, dim: int, ref: Tensor) -> Tensor:
+    g = getattr(ls, "gamma", None)
+    return _f32(g) if g is not None else torch.ones(dim, device=ref.device, dtype=torch.float32)
+
+
+def pack_block(blk, dtype: torch.dtype) -> PackedBlock:
+    a = blk.attn
+    w = lambda t: t.detach().to(dtype).contiguous()  # noqa: E731
+    qk = bool(getattr(a, "qk_norm", False))
+    return PackedBlock(
+        dim=a.qkv.in_features, heads=a.num_heads, head_dim=a.head_dim, eps=blk.norm1.eps,
+        qk_eps=a.q_norm.eps if qk else 1e-5, qk_norm=qk,
+        ln1_w=_f32(blk.norm1.weight), ln1_b=_f32(blk.norm1.bias),
+        ln2_w=_f32(blk.norm2.weight), ln2_b=_f32(blk.norm2.bias),
+        w_qkv=w(a.qkv.weight), b_qkv=_f32(a.qkv.bias),
+        qn_w=_f32(a.q_norm.weight) if qk else None, qn_b=_f32(a.q_norm.bias) if qk else None,
+        kn_w=_f32(a.k_norm.weight) if qk else None, kn_b=_f32(a.k_norm.bias) if qk else None,
+        w_proj=w(a.proj.weight), b_proj=_f32(a.proj.bias), g1=_gamma(blk.ls1, a.qkv.in_features, a.qkv.weight),
+        w_fc1=w(blk.mlp.fc1.weight), b_fc1=_f32(blk.mlp.fc1.bias),
+        w_fc2=w(blk.mlp.fc2.weight), b_fc2=_f32(blk.mlp.fc2.bias),
+        g2=_gamma(blk.ls2, a.qkv.in_features, a.qkv.weight),
+    )
+
+
+class Workspace:
+    """Grow-only device scratch, keyed by name (reused across forwards)."""
+
+    def __init__(self):
+        self._bufs: Dict[str, Tensor] = {}
+
+    def get(self, name: str, rows: int, cols: int, dtype: torch.dtype, device) -> Tensor:
+        t = self._bufs.get(name)
+        need = rows * cols
+        if t is None or t.dtype != dtype or t.device != torch.device(device) or t.numel() < need:
+            t = torch.empty(max(need, 1), dtype=dtype, device=device)
+            self._bufs[name] = t
+        return t[:need].view(rows, cols)
+
+    def clear(self):
+        self._bufs.clear()
+
+
+@dataclass
+class BlockScratch:
+    xn: Tensor   # [R, C] dtype
+    qkv: Tensor  # [R, 3C] dtype
+    o: Tensor    # [R, C] dtype
+    h: Tensor    # [R, 4C] dtype
+
+
+def scratch(ws: Workspace, rows: int, dim: int, hidden: int, dtype: torch.dtype, device, tag: str = "") -> BlockScratch:
+    return BlockScratch(xn=ws.get("xn" + tag, rows, dim, dtype, device),
+                        qkv=ws.get("qkv" + tag, rows, 3 * dim, dtype, device),
+                        o=ws.get("o" + tag, rows, dim, dtype, device),
+                        h=ws.get("h" + tag, rows, hidden, dtype, device))
+
+
+def qkv_params(pb: PackedBlock, rope: Optional[Tuple[Tensor, Tensor]], **pos) -> Optional[dict]:
+    """Epilogue parameters for the fused qkv GEMM; None if plain bias suffices."""
+    if not pb.qk_norm and rope is None:
+        return None
+    d = dict(embed_dim=pb.dim, head_dim=pb.head_dim, qk_eps=pb.qk_eps,
+             qn_w=pb.qn_w, qn_b=pb.qn_b, kn_w=pb.kn_w, kn_b=pb.kn_b)
+    if rope is not None:
+        d["rope_cos"], d["rope_sin"] = rope
+        d.update(pos)
+    return d
+
+
+def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
+              attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict]) -> None:
+    """x[r0:r1] <- Block(x[r0:r1]); ``attend(qkv_rows, o_rows)`` launches the attention."""
+    xs = x[r0:r1]
+    xn, qkv, o, h = sc.xn[r0:r1], sc.qkv[r0:r1], sc.o[r0:r1], sc.h[r0:r1]
+    ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, xn)
+    if qkv_epi is None:
+        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv)
+    else:
+        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi)
+    attend(qkv, o)
+    ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1)
+    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
+    ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1)
+    ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2)
+
+
+def frame_attend(pb: PackedBlock, frames: int, tokens: int) -> Callable[[Tensor, Tensor], None]:
+    """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C])."""
+    C, D = pb.dim, pb.head_dim
+
+    def attend(qkv: Tensor, o: Tensor) -> None:
+        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads, head_dim=D,
+                      batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens)
+    return attend

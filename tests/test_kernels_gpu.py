@@ -1,0 +1,287 @@
+"""Op-level parity of every HIP kernel against a plain torch fp32 reference.
+
+All calls go through the C ABI (libsfm_amd.so via sailrecon_amd.ops).
+"""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sailrecon_amd import ops as _ops
+    return _ops
+
+
+def _lib():
+    from sailrecon_amd import _lib as L
+    return L
+
+
+DT = [(torch.float32, 2e-6), (torch.bfloat16, 8e-3)]
+
+
+@pytest.mark.parametrize("dtype,tol", DT)
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 256, 1024), (1374, 384, 128), (77, 3072, 1024)])
+def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
+    L = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(DEV, dtype)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV, dtype)
+    b = torch.randn(N, generator=g).to(DEV)
+    ref = a.float() @ w.float().t() + b
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    ops.gemm(a, w, out, L.SR_EPI_BIAS, bias=b)
+    assert rel(out.float(), ref) < tol
+    ops.gemm(a, w, out, L.SR_EPI_BIAS_GELU, bias=b)
+    assert rel(out.float(), F.gelu(ref)) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-5)])
+def test_gemm_resid_strided(ops, dtype, tol):
+    """fp32 residual epilogue on a row slice of a bigger buffer (the reloc/global stacks)."""
+    L = _lib()
+    M, N, K = 517, 256, 512
+    a = torch.randn(M, K, device=DEV).to(dtype)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(dtype)
+    b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
+    x = torch.randn(M + 100, N, device=DEV)
+    x0 = x.clone()
+    ops.gemm(a, w, x[50:50 + M], L.SR_EPI_BIAS_RESID, bias=b, gamma=gam)
+    ref = x0.clone()
+    ref[50:50 + M] += (a.float() @ w.float().t() + b) * gam
+    assert torch.equal(x[:50], x0[:50]) and torch.equal(x[50 + M:], x0[50 + M:])
+    assert rel(x[50:50 + M] - x0[50:50 + M], ref[50:50 + M] - x0[50:50 + M]) < max(tol, 1e-5)
+
+
+@pytest.mark.parametrize("dtype,tol", DT)
+def test_gemm_patch_epilogue(ops, dtype, tol):
+    L = _lib()
+    frames, npatch, P, C, K = 3, 16, 21, 128, 640
+    a = torch.randn(frames * npatch, K, device=DEV).to(dtype)
+    w = (torch.randn(C, K, device=DEV) / 25).to(dtype)
+    b = torch.randn(C, device=DEV)
+    pos = torch.randn(npatch, C, device=DEV)
+    x = torch.full((frames * P, C), 7.0, device=DEV)
+    ops.gemm(a, w, x, L.SR_EPI_PATCH, bias=b, rows=frames * npatch,
+             patch=dict(seg_rows=npatch, seg_stride=P, seg_offset=5, row_add=pos))
+    ref = (a.float() @ w.float().t() + b).view(frames, npatch, C) + pos
+    xv = x.view(frames, P, C)
+    assert torch.all(xv[:, :5] == 7.0)
+    assert rel(xv[:, 5:], ref) < tol
+
+
+def _rope_ref(t, pos, base=100.0):
+    from oracle.sfm_oracle import rope2d
+    return rope2d(t, pos, base)
+
+
+@pytest.mark.parametrize("dtype,tol", DT)
+@pytest.mark.parametrize("col_offset", [0, 1])
+def test_gemm_qkv_epilogue(ops, dtype, tol, col_offset):
+    """bias + qk-LayerNorm + 2-D RoPE fused into the qkv GEMM (attention.py:72-82)."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    L = _lib()
+    C, H, D = 256, 4, 64
+    P, gw, frames = 21, 4, 3
+    M = frames * P
+    a = torch.randn(M, C, device=DEV).to(dtype)
+    w = (torch.randn(3 * C, C, device=DEV) / 16).to(dtype)
+    b = torch.randn(3 * C, device=DEV)
+    qn_w, qn_b, kn_w, kn_b = (torch.randn(D, device=DEV) for _ in range(4))
+    rope = RotaryPositionEmbedding2D(100).tables(D, 5, DEV)
+    wo, bo = (w[C:], b[C:]) if col_offset else (w, b)
+    out = torch.empty(M, wo.shape[0], device=DEV, dtype=dtype)
+    epi = dict(embed_dim=C, head_dim=D, qk_eps=1e-5, qn_w=qn_w, qn_b=qn_b, kn_w=kn_w, kn_b=kn_b,
+               rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=P, patch_start=5, grid_w=gw, pos_row_base=0,
+               col_offset=C if col_offset else 0)
+    ops.gemm(a, wo, out, L.SR_EPI_QKV, bias=bo, qkv=epi)
+    y = (a.float() @ w.float().t() + b).cpu().view(M, 3, H, D)
+    t = torch.arange(M) % P
+    p = (t - 5).clamp_min(0)
+    pos = torch.stack([p // gw + 1, p % gw + 1], -1) * (t >= 5)[:, None]
+    q = F.layer_norm(y[:, 0], (D,), qn_w.cpu(), qn_b.cpu(), 1e-5)
+    k = F.layer_norm(y[:, 1], (D,), kn_w.cpu(), kn_b.cpu(), 1e-5)
+    q = _rope_ref(q.permute(1, 0, 2)[None], pos[None])[0].permute(1, 0, 2)
+    k = _rope_ref(k.permute(1, 0, 2)[None], pos[None])[0].permute(1, 0, 2)
+    ref = torch.stack([q, k, y[:, 2]], 1).reshape(M, 3 * C)
+    if col_offset:
+        ref = ref[:, C:]
+    assert rel(out.float().cpu(), ref) < tol
+
+
+def _attn_ref(q, k, v, scale, mask=None):
+    s = (q.double() @ k.double().transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s.masked_fill(~mask, float("-inf"))
+    return (torch.softmax(s, -1) @ v.double()).float()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("frames,P", [(2, 261), (3, 64), (1, 1374)])
+def test_attention_frame(ops, dtype, tol, frames, P):
+    H, D = 4, 64
+    C = H * D
+    qkv = torch.randn(frames * P, 3 * C, device=DEV).to(dtype)
+    o = torch.empty(frames * P, C, device=DEV, dtype=dtype)
+    ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=frames, lq=P,
+                  q_bstride=P, l0=P, k0_bstride=P)
+    t = qkv.float().view(frames, P, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = _attn_ref(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(frames * P, C)
+    assert rel(o.float(), ref) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+def test_attention_reloc_segments(ops, dtype, tol):
+    """global_reloc: queries see [shared anchor subsample ; own frame] = the reference bool mask."""
+    H, D, Nq, P, nsub = 2, 64, 3, 70, 45
+    C = H * D
+    qkv = torch.randn(Nq * P, 3 * C, device=DEV).to(dtype)
+    kv_sub = torch.randn(nsub, 2 * C, device=DEV).to(dtype)
+    o = torch.empty(Nq * P, C, device=DEV, dtype=dtype)
+    ops.attention(qkv[:, :C], kv_sub[:, :C], kv_sub[:, C:], o, heads=H, head_dim=D, batch=Nq, lq=P, q_bstride=P,
+                  l0=nsub, k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P)
+    # dense reference over [subsample ; queries] with the reference's allowed set
+    # (aggregator.py:302-311, 832-851): anchors see anchors; query frame j sees anchors + frame j
+    L_ = nsub + Nq * P
+    seq_k = torch.cat([kv_sub[:, :C], qkv[:, C:2 * C]]).float()
+    seq_v = torch.cat([kv_sub[:, C:], qkv[:, 2 * C:]]).float()
+    seq_q = torch.cat([torch.zeros(nsub, C, device=DEV), qkv[:, :C].float()])
+    mask = torch.zeros(L_, L_, dtype=torch.bool)
+    mask[:nsub, :nsub] = True
+    for j in range(Nq):
+        r = slice(nsub + j * P, nsub + (j + 1) * P)
+        mask[r, :nsub] = True
+        mask[r, r] = True
+    mask = mask.to(DEV)
+    qh = seq_q.view(L_, H, D).transpose(0, 1)
+    kh = seq_k.view(L_, H, D).transpose(0, 1)
+    vh = seq_v.view(L_, H, D).transpose(0, 1)
+    ref = _attn_ref(qh, kh, vh, D ** -0.5, mask[None]).transpose(0, 1).reshape(L_, C)[nsub:]
+    assert rel(o.float(), ref) < tol
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_camera_mask_f32(ops, D):
+    from sailrecon_amd.heads.camera_head import build_lr_mask
+    H, S, na = 3, 11, 6
+    C = H * D
+    qkv = torch.randn(S, 3 * C, device=DEV)
+    o = torch.empty(S, C, device=DEV)
+    ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=1, lq=S, q_bstride=0,
+                  l0=S, k0_bstride=0, mask_mode=_lib().SR_MASK_CAMERA, n_anchor=na)
+    mask = ~build_lr_mask(S, list(range(na)), device=DEV)[0]
+    t = qkv.view(S, 3, H, D).permute(1, 2, 0, 3)
+    ref = _attn_ref(t[0], t[1], t[2], D ** -0.5, mask).transpose(0, 1).reshape(S, C)
+    assert rel(o, ref) < 2e-6
+
+
+def test_attention_global_long(ops):
+    """one long sequence (global stack shape class), bf16, tail tile ragged."""
+    H, D, L_ = 2, 64, 5000
+    C = H * D
+    qkv = torch.randn(L_, 3 * C, device=DEV).bfloat16()
+    o = torch.empty(L_, C, device=DEV, dtype=torch.bfloat16)
+    ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=1, lq=L_, q_bstride=0,
+                  l0=L_, k0_bstride=0)
+    t = qkv.float().view(L_, 3, H, D).permute(1, 2, 0, 3)
+    ref = _attn_ref(t[0], t[1], t[2], D ** -0.5).transpose(0, 1).reshape(L_, C)
+    assert rel(o.float(), ref) < 1e-2
+
+
+def test_attention_softmax_spike(ops):
+    """force the online-softmax rescale branch late in the key sweep (rule 26)."""
+    H, D, L_ = 1, 64, 700
+    C = H * D
+    qkv = torch.randn(L_, 3 * C, device=DEV) * 0.1
+    qkv[:, :C] = 1.0
+    qkv[650, C:2 * C] = 3.0  # one key row scores far above the rest
+    for dt, tol in ((torch.float32, 2e-6), (torch.bfloat16, 1e-2)):
+        x = qkv.to(dt)
+        o = torch.empty(L_, C, device=DEV, dtype=dt)
+        ops.attention(x[:, :C], x[:, C:2 * C], x[:, 2 * C:], o, heads=H, head_dim=D, batch=1, lq=L_, q_bstride=0,
+                      l0=L_, k0_bstride=0)
+        t = x.float().view(L_, 3, H, D).permute(1, 2, 0, 3)
+        ref = _attn_ref(t[0], t[1], t[2], D ** -0.5).transpose(0, 1).reshape(L_, C)
+        assert rel(o.float(), ref) < tol
+
+
+@pytest.mark.parametrize("cols", [384, 768, 1024, 2048])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_rowmap(ops, cols, dtype):
+    x = torch.randn(300, cols, device=DEV) * 3 + 1
+    w, b = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV)
+    rm = torch.randint(0, 300, (123,), device=DEV, dtype=torch.int32)
+    out = torch.empty(123, cols, device=DEV, dtype=dtype)
+    ops.layernorm(x, w, b, 1e-5, out, rowmap=rm)
+    ref = F.layer_norm(x[rm.long()], (cols,), w, b, 1e-5)
+    assert rel(out.float(), ref) < (1e-6 if dtype == torch.float32 else 5e-3)
+    out2 = torch.empty(300, cols, device=DEV)
+    ops.layernorm(x, None, None, 1e-6, out2)
+    assert rel(out2, F.layer_norm(x, (cols,), eps=1e-6)) < 1e-6
+
+
+def test_im2col_and_tokens(ops):
+    img = torch.rand(2, 3, 28, 42, device=DEV)
+    out = torch.empty(2 * 6, 640, device=DEV)
+    ops.im2col_normalize(img, 14, out, 640)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=DEV).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=DEV).view(1, 3, 1, 1)
+    ref = F.unfold((img - mean) / std, 14, stride=14).transpose(1, 2).reshape(12, 588)
+    assert rel(out[:, :588], ref) < 1e-6 and torch.all(out[:, 588:] == 0)
+    x = torch.zeros(4 * 10, 8, device=DEV)
+    table = torch.randn(3, 2, 8, device=DEV)
+    types = torch.tensor([0, 1, 2, 1], dtype=torch.int32, device=DEV)
+    ops.set_special_tokens(x, 4, 10, table, types)
+    xv = x.view(4, 10, 8)
+    for f, t in enumerate([0, 1, 2, 1]):
+        assert torch.equal(xv[f, :2], table[t]) and torch.all(xv[f, 2:] == 0)
+
+
+def test_small_fp32_ops(ops):
+    a = torch.randn(7, 9, device=DEV)
+    w, b = torch.randn(33, 9, device=DEV), torch.randn(33, device=DEV)
+    out = torch.empty(7, 33, device=DEV)
+    ops.linear_small(a, w, b, out, rows=7)
+    assert rel(out, a @ w.t() + b) < 1e-6
+    ops.linear_small(a, w, b, out, rows=7, act_in=1)
+    assert rel(out, F.silu(a) @ w.t() + b) < 1e-6
+    a2 = torch.randn(5, 1024, device=DEV)
+    w2, b2 = torch.randn(9, 1024, device=DEV), torch.randn(9, device=DEV)
+    o2 = torch.empty(5, 9, device=DEV)
+    ops.linear_small(a2, w2, b2, o2, rows=5)
+    assert rel(o2, a2 @ w2.t() + b2) < 1e-6
+    y = torch.empty_like(a2)
+    ops.silu(a2, y)
+    assert rel(y, F.silu(a2)) < 1e-6
+    xn, x0, mod = torch.randn(5, 64, device=DEV), torch.randn(5, 64, device=DEV), torch.randn(5, 192, device=DEV)
+    o3 = torch.empty(5, 64, device=DEV)
+    ops.adaln_modulate(xn, x0, mod, o3)
+    sh, scl, gt = mod.chunk(3, -1)
+    assert rel(o3, gt * (xn * (1 + scl) + sh) + x0) < 1e-6
+    pred, delta, act = torch.zeros(5, 9, device=DEV), torch.randn(5, 9, device=DEV), torch.empty(5, 9, device=DEV)
+    ops.pose_update(pred, delta, act, first=True)
+    ops.pose_update(pred, delta, act, first=False)
+    assert torch.allclose(pred, 2 * delta)
+    assert torch.allclose(act, torch.cat([2 * delta[:, :7], F.relu(2 * delta[:, 7:])], -1))
+    from oracle.sfm_oracle import pose_encoding_to_extri_intri
+    enc = torch.randn(1, 5, 9)
+    enc[..., 7:] = enc[..., 7:].abs() + 0.3
+    ext, intr = torch.empty(5, 3, 4, device=DEV), torch.empty(5, 3, 3, device=DEV)
+    ops.pose_decode(enc[0].to(DEV), (224, 300), ext, intr)
+    re, ri = pose_encoding_to_extri_intri(enc, (224, 300))
+    assert rel(ext.cpu(), re[0]) < 1e-6 and rel(intr.cpu(), ri[0]) < 1e-6

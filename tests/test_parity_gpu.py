@@ -1,0 +1,141 @@
+"""End-to-end parity of the HIP path against the reference's golden vectors.
+
+fp32 parity mode (no autocast): exact-fp32 MFMA GEMMs + fp32 attention; tolerance
+1e-4 relative L2 (north star: pose within 1e-4 rel).
+bf16 mode (under torch.autocast, the demo_imc_forward.py:93 convention): bf16 MFMA
+GEMMs / attention with fp32 residual and fp32 camera head; tolerance 3e-2 relative L2
+(the reference's own bf16-vs-fp32 gap is 0.7-0.9 %).
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from goldens import load_npz, rel_l2, rule_state_dict
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TOL = {"fp32": 1e-4, "bf16": 3e-2}
+
+
+class Hot(nn.Module):
+    def __init__(self, agg_kw, cam_kw):
+        super().__init__()
+        from sailrecon_amd.heads.camera_head import CameraHead
+        from sailrecon_amd.models.aggregator import Aggregator
+        self.aggregator = Aggregator(**agg_kw)
+        self.camera_head = CameraHead(**cam_kw)
+
+
+def run(model, images, n, fix_rank, mode):
+    from sailrecon_amd.utils.pose_enc import pose_encoding_to_extri_intri
+    S = images.shape[1]
+    model.aggregator.generator.manual_seed(0)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=(mode == "bf16")):
+        feats, psi, cam_last = model.aggregator(images, list(range(n)), list(range(n, S)), fix_rank=fix_rank)
+        with torch.autocast("cuda", enabled=False):
+            poses = model.camera_head(feats, cam_last)
+            ext, intr = pose_encoding_to_extri_intri(poses[-1], (images.shape[-2], images.shape[-1]))
+    torch.cuda.synchronize()
+    return feats, psi, cam_last, poses, ext, intr
+
+
+@pytest.fixture(scope="module")
+def small_model():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.manual_seed(0)
+    m = Hot(dict(img_size=56, patch_size=14, embed_dim=384, depth=2, num_heads=6,
+                 patch_embed="dinov2_vits14_reg", intermediate_layer_idx=[0, 1]),
+            dict(dim_in=768, trunk_depth=2, num_heads=6)).eval()
+    m.load_state_dict(rule_state_dict("small_state_dict_keys.json"))
+    return m.to(DEV)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("tag", ["56", "70"])
+def test_small_end_to_end(small_model, tag, mode):
+    g = load_npz(f"g1_small_{tag}.npz")
+    n = int(g["n_views"])
+    images = torch.from_numpy(g["images"]).to(DEV)
+    feats, psi, cam_last, poses, ext, intr = run(small_model, images, n, int(g["fix_rank"]), mode)
+    assert psi == 5
+    assert np.array_equal(small_model.aggregator.last_subsample_indices[:, 0].numpy(), g["sub_idx"])
+    tol = TOL[mode]
+    for layer in (0, 1):
+        assert rel_l2(feats[layer].cpu().numpy(), g[f"feat_{layer}"]) < tol, layer
+    assert feats[-1] is feats[1]
+    assert rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"]) < tol
+    pe = np.stack([p.cpu().numpy() for p in poses])
+    assert rel_l2(pe, g["pose_enc"]) < tol
+    assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
+    assert rel_l2(intr.cpu().numpy(), g["intrinsic"]) < tol
+
+
+def test_block_kats_fp32():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sailrecon_amd.layers.block import Block
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    from functools import partial
+    g = load_npz("g2_blocks.npz")
+    blk = Block(dim=1024, num_heads=16, init_values=0.01, qk_norm=True, rope=RotaryPositionEmbedding2D(100))
+    blk.load_state_dict(rule_state_dict("block_state_dict_keys.json", "agg"))
+    blk = blk.to(DEV)
+    y = blk(torch.from_numpy(g["agg_x"]).to(DEV), pos=torch.from_numpy(g["agg_pos"]).to(DEV))
+    assert rel_l2(y.cpu().numpy(), g["agg_y"]) < 1e-5
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(torch.from_numpy(g["agg_x"]).to(DEV), pos=torch.from_numpy(g["agg_pos"]).to(DEV))
+    assert rel_l2(y.float().cpu().numpy(), g["agg_y"]) < 2e-2
+    blk = Block(dim=1024, num_heads=16, init_values=1.0, norm_layer=partial(nn.LayerNorm, eps=1e-6))
+    blk.load_state_dict(rule_state_dict("block_state_dict_keys.json", "dino"))
+    y = blk.to(DEV)(torch.from_numpy(g["dino_x"]).to(DEV))
+    assert rel_l2(y.cpu().numpy(), g["dino_y"]) < 1e-5
+    blk = Block(dim=2048, num_heads=16, init_values=0.01)
+    blk.load_state_dict(rule_state_dict("block_state_dict_keys.json", "cam"))
+    y = blk.to(DEV)(torch.from_numpy(g["cam_x"]).to(DEV), None, torch.from_numpy(g["cam_mask"]).to(DEV))
+    assert rel_l2(y.cpu().numpy(), g["cam_y"]) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def full_model():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.manual_seed(0)
+    m = Hot(dict(img_size=518, patch_size=14, embed_dim=1024), dict(dim_in=2048)).eval()
+    m.load_state_dict(rule_state_dict("state_dict_keys.json"))
+    return m.to(DEV)
+
+
+def _check_full(model, fname, mode):
+    g = load_npz(fname)
+    n, img = int(g["n_views"]), int(g["img"])
+    gen = torch.Generator().manual_seed(n)
+    x = torch.rand(n, 3, img, img, generator=gen)
+    images = torch.cat([x, x])[None].to(DEV)
+    feats, psi, cam_last, poses, ext, intr = run(model, images, n, 300, mode)
+    assert np.array_equal(model.aggregator.last_subsample_indices[:, 0].numpy(), g["sub_idx"])
+    tol = TOL[mode]
+    rows = torch.from_numpy(g["sample_rows"])
+    for layer in (4, 11, 17, 23):
+        v = feats[layer][0].cpu()
+        assert rel_l2(v.norm(dim=-1).numpy(), g[f"feat_{layer}_rownorm"]) < tol
+        assert rel_l2(v[:, 0].numpy(), g[f"feat_{layer}_cam"]) < tol
+        assert rel_l2(v.reshape(-1, v.shape[-1])[rows].numpy(), g[f"feat_{layer}_rows"]) < tol
+    assert rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"]) < tol
+    pe = np.stack([p.cpu().numpy() for p in poses])
+    assert rel_l2(pe, g["pose_enc"]) < tol
+    assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
+    assert rel_l2(intr.cpu().numpy(), g["intrinsic"]) < tol
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_full_c1_224(full_model, mode):
+    _check_full(full_model, "g4_c1_224.npz", mode)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_full_518_n1(full_model, mode):
+    _check_full(full_model, "g5_518_n1.npz", mode)
