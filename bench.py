@@ -1,0 +1,199 @@
+#!/usr/bin/env python
+"""Benchmark: aggregator fwd views/sec, N=32 @ 518px (BASELINE.json metric).
+
+One step = SailRecon.forward on a synthetic 32-view scene in the
+demo_imc_forward.py convention (the N images duplicated to 2N frames: anchors =
+first half, queries = second half, fix_rank=300), i.e. Aggregator.forward under
+bf16 autocast + CameraHead.forward (fp32) + pose decode — the north-star hot path.
+Inputs are resident in HBM before the timed region.  Weights: the seeded synthetic
+rule (pretrained weights are not available offline).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Multi-GPU: one process per GPU.  Until the frame-sharded global attention lands,
+N ranks run independent replicas of the same workload (value = all ranks' views /
+max-over-ranks time, scaling "weak").
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with a
+``roofline`` object for the dominant kernel class (live HIP-event timing inside
+the timed region) and a ``cpu_baseline`` object (the CPU oracle on a bounded
+sample, rank 0 at N=1 only).  A per-kernel-class breakdown goes to stderr.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "self-supervise-sfm_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_F32_TFLOPS = 157.3    # f32 MFMA
+PEAK_HBM_GBS = 8000.0
+
+
+def algorithmic_tflop(n_views: int, img: int, C: int = 1024) -> float:
+    """Required work per forward, SURVEY §8(d) closed form (TFLOP)."""
+    S = 2 * n_views
+    npatch = (img // 14) ** 2
+    P, Pp = npatch + 5, min(300, npatch) + 5
+    Lg = n_views * P
+    f_stack = 24 * S * (P * 24 * C * C + 4 * P * P * C)
+    f_global = 24 * (Lg * 24 * C * C + 4 * Lg * Lg * C)
+    f_reloc = 24 * (n_views * Pp * 4 * C * C + n_views * P * 24 * C * C + 4 * n_views * P * (n_views * Pp + P) * C)
+    f_patch = 2 * S * npatch * 588 * C
+    C2 = 2 * C
+    f_cam = 4 * (4 * S * 24 * C2 * C2 + 4 * 4 * S * S * C2 + S * (2 * 9 * C2 + 2 * C2 * 3 * C2 + 2 * C2 * C + 2 * C * 9))
+    return (2 * f_stack + f_global + f_reloc + f_patch + f_cam) / 1e12
+
+
+def build_model(device, seed_rule=True):
+    from sailrecon_amd.models.sail_recon import SailRecon
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    torch.manual_seed(0)
+    model = SailRecon(enable_point=False, enable_depth=False).eval()
+    sd = synth_state_dict_like(model) if seed_rule else None
+    if sd is not None:
+        model.load_state_dict(sd)
+    return model.to(device), sd
+
+
+def cpu_baseline(sd, img: int, n_views: int):
+    """The CPU oracle (oracle/sfm_oracle.py, a port of the reference path) on a bounded
+    sample: one full forward of an n_views scene (2*n_views frames)."""
+    from oracle import sfm_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(n_views)
+    x = torch.rand(n_views, 3, img, img, generator=g)
+    images = torch.cat([x, x])[None]
+    npatch = (img // 14) ** 2
+    sub = O.draw_subsample_indices(torch.Generator().manual_seed(0), 24, 1, n_views, npatch, min(300, npatch))
+    t0 = time.perf_counter()
+    O.hot_path_forward(sd, O.AggCfg(), images, list(range(n_views)), list(range(n_views, 2 * n_views)), 300, sub)
+    dt = time.perf_counter() - t0
+    return {"value": n_views / dt, "unit": "views/s", "cores": threads, "kind": "port",
+            "sample": f"1 full fp32 forward of a {n_views}-view scene @{img}px ({2 * n_views} frames; "
+                      f"aggregator+camera head+pose decode) on the host CPU, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--views", type=int, default=32)
+    ap.add_argument("--img", type=int, default=518)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-views", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local if world > 1 else 0)
+
+    from sailrecon_amd import ops
+
+    model, sd = build_model(device)
+    n = args.views
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(n, 3, args.img, args.img, generator=g)
+    images = torch.cat([x, x])[None].to(device)  # demo_imc_forward.py:76-82
+    no_reloc, reloc = list(range(n)), list(range(n, 2 * n))
+    use_bf16 = args.dtype == "bf16"
+
+    def step():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=use_bf16):
+            return model(images, no_reloc_list=no_reloc, reloc_list=reloc, fix_rank=300)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    if not args.no_kernel_timing:
+        ops.TIMER = ops.KernelTimer()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    timer, ops.TIMER = ops.TIMER, None
+    dt_t = torch.tensor([dt], device=device)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    total_views = n * world * args.steps
+
+    roofline = None
+    breakdown = {}
+    if timer is not None:
+        breakdown = timer.summary()
+        peak = PEAK_BF16_TFLOPS if use_bf16 else PEAK_F32_TFLOPS
+        dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
+        b = breakdown[dom]
+        achieved = b["tflops"]
+        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "avg_launch_ms": round(b["avg_ms"], 4), "flop_per_launch": b["flops_per_launch"]}
+        gem = breakdown.get("gemm")
+        if gem:
+            roofline["gemm_mfma_util"] = round(gem["tflops"] / peak, 4)
+        print(json.dumps({"kernel_breakdown": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
+                                                   for kk, vv in v.items()} for k, v in breakdown.items()},
+                          "step_ms": dt / args.steps * 1e3}), file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline({k: v for k, v in sd.items()}, args.img, args.cpu_views)
+
+    if rank == 0:
+        tflop = algorithmic_tflop(n, args.img)
+        line = {
+            "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px",
+            "value": total_views / dt,
+            "unit": "views/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded U[0,1) images, seeded synthetic weights)",
+            "config": {"workload": f"N={n} views @{args.img}px duplicated to {2 * n} frames (anchors+queries), "
+                                   "fix_rank=300: Aggregator + CameraHead + pose decode",
+                       "views": n, "img": args.img, "frames": 2 * n, "fix_rank": 300,
+                       "parallelism": f"replicas x{world}",
+                       "algorithmic_tflop_per_step": round(tflop, 2),
+                       "achieved_tflops_whole_step": round(tflop * world * args.steps / dt, 1)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -312,7 +312,7 @@ class Aggregator(nn.Module):
         def attend(qkv, o):
             ops.attention(qkv[:, 0:C], kv_sub[:, 0:C], kv_sub[:, C:2 * C], o, heads=pb.heads, head_dim=pb.head_dim,
                           batch=Nq, lq=P, q_bstride=P, l0=n_sub, k0_bstride=0,
-                          k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P)
+                          k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
 
         runtime.run_block(pb, x, q0, q1, sc, attend, runtime.qkv_params(pb, rope, pos_row_base=q0, **posctx))
 
@@ -323,6 +323,6 @@ class Aggregator(nn.Module):
 
         def attend(qkv, o):
             ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads,
-                          head_dim=pb.head_dim, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0)
+                          head_dim=pb.head_dim, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, tag="attn_global")
 
         runtime.run_block(pb, x, a0, a1, sc, attend, runtime.qkv_params(pb, rope, pos_row_base=a0, **posctx))

@@ -18,6 +18,46 @@ from ._lib import AttnDesc, GemmEpi, check
 Tensor = torch.Tensor
 
 
+class KernelTimer:
+    """Records HIP events around tagged launches on the launching (current torch) stream.
+
+    Used by bench.py to measure the dominant kernel's average launch duration inside the
+    timed region; ``work`` is the algorithmic FLOP count of the launch.
+    """
+
+    def __init__(self, tags=None):
+        self.tags = None if tags is None else set(tags)
+        self.records = {}
+
+    def wants(self, tag: Optional[str]) -> bool:
+        return tag is not None and (self.tags is None or tag in self.tags)
+
+    def start(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def stop(self, tag: str, ev0, work: float):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.records.setdefault(tag, []).append((ev0, ev1, work))
+
+    def summary(self):
+        """tag -> dict(launches, total_ms, avg_ms, flops_per_launch, tflops)"""
+        torch.cuda.synchronize()
+        out = {}
+        for tag, recs in self.records.items():
+            ms = [a.elapsed_time(b) for a, b, _ in recs]
+            work = sum(w for _, _, w in recs)
+            tot = sum(ms)
+            out[tag] = dict(launches=len(recs), total_ms=tot, avg_ms=tot / len(recs),
+                            flops_per_launch=work / len(recs), tflops=(work / (tot * 1e-3) / 1e12) if tot else 0.0)
+        return out
+
+
+TIMER: Optional[KernelTimer] = None
+
+
 def _p(t: Optional[Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -45,7 +85,7 @@ def _rowmajor(t: Tensor, name: str) -> int:
 
 def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] = None,
          gamma: Optional[Tensor] = None, rows: Optional[int] = None, qkv: Optional[dict] = None,
-         patch: Optional[dict] = None) -> None:
+         patch: Optional[dict] = None, tag: Optional[str] = None) -> None:
     """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows)."""
     lda = _rowmajor(a, "a")
     ldw = _rowmajor(w, "w")
@@ -80,15 +120,19 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         ep.seg_stride = patch["seg_stride"]
         ep.seg_offset = patch["seg_offset"]
         ep.row_add = _p(patch["row_add"])
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
     rc = _lib.load().sr_gemm(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
                              M, N, K, ctypes.byref(ep))
     check(rc, "sr_gemm")
+    if timed:
+        TIMER.stop(tag, ev0, 2.0 * M * N * K)
 
 
 def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
-              scale: Optional[float] = None) -> None:
+              scale: Optional[float] = None, tag: Optional[str] = None) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc."""
     d = AttnDesc()
     d.q, d.ldq = _p(q), _rowmajor(q, "q")
@@ -104,8 +148,12 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     d.l1, d.k1_bstride = l1, k1_bstride
     d.mask_mode, d.n_anchor = mask_mode, n_anchor
     d.scale = head_dim ** -0.5 if scale is None else scale
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
     rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
     check(rc, "sr_attention")
+    if timed:
+        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim)
 
 
 def layernorm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float, out: Tensor,

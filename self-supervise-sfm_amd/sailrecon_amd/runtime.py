@@ -136,20 +136,22 @@ def qkv_params(pb: PackedBlock, rope: Optional[Tuple[Tensor, Tensor]], **pos) ->
 
 
 def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
-              attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict]) -> None:
-    """x[r0:r1] <- Block(x[r0:r1]); ``attend(qkv_rows, o_rows)`` launches the attention."""
+              attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict], tag: str = "blk") -> None:
+    """x[r0:r1] <- Block(x[r0:r1]); ``attend(qkv_rows, o_rows)`` launches the attention.
+    ``tag`` prefixes the kernel-timer tags of the four GEMMs (e.g. "global.qkv")."""
     xs = x[r0:r1]
     xn, qkv, o, h = sc.xn[r0:r1], sc.qkv[r0:r1], sc.o[r0:r1], sc.h[r0:r1]
     ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, xn)
     if qkv_epi is None:
-        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv)
+        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
     else:
-        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi)
+        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
     attend(qkv, o)
-    ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1)
+    ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
     ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
-    ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1)
-    ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2)
+    ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
+    ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2,
+             tag="gemm")
 
 
 def frame_attend(pb: PackedBlock, frames: int, tokens: int) -> Callable[[Tensor, Tensor], None]:
@@ -158,5 +160,5 @@ def frame_attend(pb: PackedBlock, frames: int, tokens: int) -> Callable[[Tensor,
 
     def attend(qkv: Tensor, o: Tensor) -> None:
         ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads, head_dim=D,
-                      batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens)
+                      batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_frame")
     return attend
