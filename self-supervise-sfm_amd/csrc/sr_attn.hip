@@ -32,21 +32,61 @@ struct AttnArgs {
 };
 
 // ------------------------------------------------------------------ bf16 / MFMA
-constexpr int QROWS = 128;  // query rows per workgroup
-constexpr int KT = 64;      // keys per tile
-constexpr int TILE_B = KT * 128;  // bytes of one K (or V) tile: 64 rows x 64 bf16
+constexpr int KT = 64;               // keys per tile
+constexpr int TILE_B = KT * 128;     // bytes of one K (or V) tile: 64 keys x 64 bf16
+constexpr int STAGE_B = 2 * TILE_B;  // K + V
+constexpr int NBUF = 3;              // ring depth: one barrier per tile
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];  // [buf][K|V]
+// v and its lane^32 partner combined, via v_permlane32_swap (no LDS traffic)
+__device__ __forceinline__ float max_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// NW waves x 32 query rows per workgroup; KIND only names the call site for profiles
+// (0 frame, 1 global_reloc, 2 global).
+template <int NW, int KIND>
+__global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
+  constexpr int QROWS = NW * 32;
+  constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
   const int hcol = head * 64;
   const int l32 = lane & 31, hi = lane >> 5;
+  const int ntiles = args.ntile0 + args.ntile1;
+  const uint32_t lds0 = sr::lds_addr(smem);
+
+  // ---- staging: global DMA instruction gi = wave*DPW + i; gi < 8: K rows 8gi.., else V rows
+  auto stage = [&](int t, int buf) {
+    const bool s1 = t >= args.ntile0;
+    const int tt = s1 ? t - args.ntile0 : t;
+    const int len = s1 ? d.l1 : d.l0;
+    const int64_t rbase = item * (s1 ? d.k1_bstride : d.k0_bstride);
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int gi = wave * DPW + i;
+      const bool v = gi >= 8;
+      const bf16* base = (const bf16*)(v ? (s1 ? d.v1 : d.v0) : (s1 ? d.k1 : d.k0));
+      const int64_t ld = v ? (s1 ? d.ldv1 : d.ldv0) : (s1 ? d.ldk1 : d.ldk0);
+      const int r = (gi & 7) * 8 + (lane >> 3);  // key row inside the tile
+      const int key = min(tt * KT + r, len - 1);
+      const int chunk = (lane & 7) ^ ((r >> 1) & 7);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_B + (v ? TILE_B : 0) + (gi & 7) * 1024);
+      sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst);
+    }
+  };
+  stage(0, 0);
+  if (ntiles > 1) stage(1, 1);
 
   // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row l32][16s + 8hi .. +8]
   const int qrow = qt * QROWS + wave * 32 + l32;
@@ -56,30 +96,6 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
 
-  // ---- staging: waves 0,1 -> K rows [32w, 32w+32); waves 2,3 -> V rows [32(w-2), ..)
-  const bool is_v = wave >= 2;
-  const int srow0 = (wave & 1) * 32;
-  const uint32_t lds0 = sr::lds_addr(smem);
-  const uint32_t dst_w = __builtin_amdgcn_readfirstlane(lds0 + (is_v ? TILE_B : 0) + srow0 * 128);
-  const int ntiles = args.ntile0 + args.ntile1;
-
-  auto stage = [&](int t, int buf) {
-    const bool s1 = t >= args.ntile0;
-    const int tt = s1 ? t - args.ntile0 : t;
-    const int len = s1 ? d.l1 : d.l0;
-    const int64_t rbase = item * (s1 ? d.k1_bstride : d.k0_bstride);
-    const bf16* base = (const bf16*)(is_v ? (s1 ? d.v1 : d.v0) : (s1 ? d.k1 : d.k0));
-    const int64_t ld = is_v ? (s1 ? d.ldv1 : d.ldv0) : (s1 ? d.ldk1 : d.ldk0);
-    const uint32_t dst = dst_w + buf * 2 * TILE_B;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = srow0 + i * 8 + (lane >> 3);  // tile row (key)
-      const int key = min(tt * KT + r, len - 1);
-      const int chunk = (lane & 7) ^ ((r >> 1) & 7);
-      sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst + i * 1024);
-    }
-  };
-
   const float c = d.scale * 1.4426950408889634f;  // scale * log2(e)
   float m_run = -1e30f, l_run = 0.f;              // l_run: this lane's partial row sum
   f32x16 o[2];
@@ -88,26 +104,23 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
     o[0][i] = 0.f;
     o[1][i] = 0.f;
   }
-
-  // per-lane LDS read offsets
-  // K (A operand): row kb*32 + l32, chunk 2s + hi, swizzled
   const int kswz = (l32 >> 1) & 7;
-  // V tr-read: group G = lane>>4, i = lane&15: row r0 + (i>>2), col db*32 + 16(G&1) + 4(i&3)
-  const int G = lane >> 4, gi = lane & 15;
-  const int vrow_in = gi >> 2;                 // + r0
-  const int vcol_in = 16 * (G & 1) + 4 * (gi & 3);  // + db*32
+  // V tr-read: group G = lane>>4, i = lane&15 supplies row r0 + (i>>2), col db*32 + 16(G&1) + 4(i&3)
+  const int G = lane >> 4, gi_ = lane & 15;
+  const int vrow_in = gi_ >> 2;
+  const int vcol_in = 16 * (G & 1) + 4 * (gi_ & 3);
 
-  stage(0, 0);
+  int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
     if (t + 1 < ntiles) {
-      stage(t + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if constexpr (DPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    sr::barrier_raw();
-    const char* kt_lds = smem + buf * 2 * TILE_B;
+    sr::barrier_raw();  // tile t landed for every wave; every wave is done with tile t-1
+    if (t + 2 < ntiles) stage(t + 2, buf == 0 ? 2 : buf - 1);
+    const char* kt_lds = smem + buf * STAGE_B;
     const char* vt_lds = kt_lds + TILE_B;
 
     // ---- S^T = K Q^T for 2 blocks of 32 keys
@@ -124,10 +137,9 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
       }
     }
 
-    // ---- mask ragged tail of the segment
+    // ---- mask the ragged tail of a segment
     const bool s1 = t >= args.ntile0;
-    const int tt = s1 ? t - args.ntile0 : t;
-    const int valid = (s1 ? d.l1 : d.l0) - tt * KT;
+    const int valid = (s1 ? d.l1 : d.l0) - (s1 ? t - args.ntile0 : t) * KT;
     if (valid < KT) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -138,16 +150,16 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
         }
     }
 
-    // ---- online softmax (row = this lane's query; partner lane^32 holds the other 32 keys)
-    float mx = sacc[0][0];
+    // ---- online softmax: this lane's 32 scores of one query row; partner lane^32 holds 32 more
+    float t8[8];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[0][r]);
+    for (int i = 0; i < 8; ++i) t8[i] = fmaxf(fmaxf(sacc[0][i], sacc[0][i + 8]), fmaxf(sacc[1][i], sacc[1][i + 8]));
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[1][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
+    const float mx = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
     const float m_new = fmaxf(m_run, mx * c);
     if (__any(m_new > m_run)) {
-      const float alpha = exp2f(m_run - m_new);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       l_run *= alpha;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -156,21 +168,19 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
       }
       m_run = m_new;
     }
-    bf16x8 pf[2][2];
+    // ---- per 32-key block: P = exp2(S*c - m) -> bf16 (B operand), then O^T += V^T P^T
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 pf[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float p = exp2f(fmaf(sacc[kb][8 * s2 + j], c, -m_run));
-          l_run += p;
-          pf[kb][s2][j] = (bf16)p;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][8 * s2 + j], c, -m_run));
+          ps[j & 3] += p;
+          pf[s2][j] = (bf16)p;
         }
-
-    // ---- O^T += V^T P^T
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int r0 = kb * 32 + 16 * s2 + 4 * hi;
@@ -180,24 +190,20 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
           const int ra = r0 + vrow_in, rb = r0 + 8 + vrow_in;
           const char* pa = vt_lds + ra * 128 + (((col >> 3) ^ ((ra >> 1) & 7)) * 16) + (col & 7) * 2;
           const char* pb = vt_lds + rb * 128 + (((col >> 3) ^ ((rb >> 1) & 7)) * 16) + (col & 7) * 2;
-          const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(
-              (__attribute__((address_space(3))) char*)0 + sr::lds_addr(pa)));
-          const s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(
-              (__attribute__((address_space(3))) char*)0 + sr::lds_addr(pb)));
-          bf16x8 vf;
+          const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
+          const s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pb);
           const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
-          vf[0] = a4[0]; vf[1] = a4[1]; vf[2] = a4[2]; vf[3] = a4[3];
-          vf[4] = b4[0]; vf[5] = b4[1]; vf[6] = b4[2]; vf[7] = b4[3];
-          o[db] = mfma32(vf, pf[kb][s2], o[db]);
+          const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
+          o[db] = mfma32(vf, pf[s2], o[db]);
         }
       }
-    sr::wait_lgkm0();
-    sr::barrier_raw();
+    }
+    l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    buf = buf == 2 ? 0 : buf + 1;
   }
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / l_tot;
+  const float inv = 1.f / sum_x32(l_run);
   if (qrow < d.lq) {
     bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
 #pragma unroll
@@ -207,8 +213,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs args) {
         bf16x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[db][4 * g + j] * inv);
-        const int dd = db * 32 + 8 * g + 4 * hi;
-        *(bf16x4*)(op + dd) = v;
+        *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
       }
   }
 }
@@ -307,8 +312,17 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
              SR_EINVAL, "sr_attention(bf16): leading dims must be multiples of 8");
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
-    dim3 grid((d.lq + QROWS - 1) / QROWS, d.heads, d.batch);
-    hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, a);
+    const int kind = d.l1 > 0 ? 1 : (d.batch == 1 && d.lq >= 4096 ? 2 : 0);
+    if (d.lq >= 4096) {  // long sequences: 256-row query tiles halve K/V traffic per FLOP
+      dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
+      if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), grid, dim3(512), 0, s, a);
+      else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<8, 1>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((attn_bf16_kernel<8, 0>), grid, dim3(512), 0, s, a);
+    } else {  // frame-sized sequences (1374): 128-row tiles keep the ragged last tile small
+      dim3 grid((d.lq + 127) / 128, d.heads, d.batch);
+      if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<4, 1>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((attn_bf16_kernel<4, 0>), grid, dim3(256), 0, s, a);
+    }
     return sr::check_launch("sr_attention(bf16)");
   }
   SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attention: bad dtype %d", dtype);
