@@ -1,0 +1,40 @@
+#!/usr/bin/env bash
+# Run named GPU steps in order, each under its own time limit, logging to gpurun_out/.
+# Stops at the first step that crashes / aborts / times out (124, 134, 137, 139 or a
+# negative-signal exit); an ordinary failure (e.g. pytest rc=1) is recorded and the
+# next step still runs.
+#   tools/gpu_job.sh kernels parity smoke bench [prof]
+set -u
+mkdir -p gpurun_out
+status=0
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/job.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/job.log
+  tail -n 4 "gpurun_out/$name.log"
+  case $rc in
+    0) ;;
+    1|2|5) status=1 ;;
+    *) echo "=== $name crashed or timed out (rc=$rc): stopping"; exit $rc ;;
+  esac
+}
+for step in "$@"; do
+  case $step in
+    kernels) run kernels 600 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu ;;
+    parity)  run parity 900 python -m pytest tests/test_parity_gpu.py -x -q -m gpu ;;
+    gputests) run gputests 1200 python -m pytest tests -x -q -m gpu ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   run bench 600 python bench.py ;;
+    benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+               python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    pmc_fetch) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
+               python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    pmc_write) run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
+               python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+exit $status
