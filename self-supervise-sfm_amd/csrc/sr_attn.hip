@@ -35,7 +35,7 @@ struct AttnArgs {
 constexpr int KT = 64;               // keys per tile
 constexpr int TILE_B = KT * 128;     // bytes of one K (or V) tile: 64 keys x 64 bf16
 constexpr int STAGE_B = 2 * TILE_B;  // K + V
-constexpr int NBUF = 3;              // ring depth: one barrier per tile
+constexpr int NBUF = 4;              // K/V ring depth (power of 2)
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -53,6 +53,12 @@ __device__ __forceinline__ float sum_x32(float v) {
 
 // NW waves x 32 query rows per workgroup; KIND only names the call site for profiles
 // (0 frame, 1 global_reloc, 2 global).
+//
+// Software-pipelined tile loop (one barrier per tile, K/V ring of NBUF=4 stages, two
+// stages in flight):  iteration t
+//   [A] row max of S(t) (already in registers), rescale O/l if it grew
+//   [B] S(t+1) = K(t+1) Q^T MFMAs  ||  P(t) = exp2(S(t)*c - m) VALU   (independent: overlap)
+//   [C] O^T += V(t)^T P(t)^T MFMAs
 template <int NW, int KIND>
 __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
   constexpr int QROWS = NW * 32;
@@ -67,7 +73,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
   const uint32_t lds0 = sr::lds_addr(smem);
 
   // ---- staging: global DMA instruction gi = wave*DPW + i; gi < 8: K rows 8gi.., else V rows
-  auto stage = [&](int t, int buf) {
+  auto stage = [&](int t) {
+    const int buf = t & (NBUF - 1);
     const bool s1 = t >= args.ntile0;
     const int tt = s1 ? t - args.ntile0 : t;
     const int len = s1 ? d.l1 : d.l0;
@@ -85,8 +92,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
       sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst);
     }
   };
-  stage(0, 0);
-  if (ntiles > 1) stage(1, 1);
+  stage(0);
+  if (ntiles > 1) stage(1);
+  if (ntiles > 2) stage(2);
 
   // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row l32][16s + 8hi .. +8]
   const int qrow = qt * QROWS + wave * 32 + l32;
@@ -110,21 +118,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
   const int vrow_in = gi_ >> 2;
   const int vcol_in = 16 * (G & 1) + 4 * (gi_ & 3);
 
-  int buf = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) {
-      if constexpr (DPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    sr::barrier_raw();  // tile t landed for every wave; every wave is done with tile t-1
-    if (t + 2 < ntiles) stage(t + 2, buf == 0 ? 2 : buf - 1);
-    const char* kt_lds = smem + buf * STAGE_B;
-    const char* vt_lds = kt_lds + TILE_B;
-
-    // ---- S^T = K Q^T for 2 blocks of 32 keys
-    f32x16 sacc[2];
+  auto scores = [&](int t, f32x16 (&sacc)[2]) {  // S^T = K(t) Q^T, 2 blocks of 32 keys
+    const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -136,8 +131,24 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
         sacc[kb] = mfma32(kf, qf[s], sacc[kb]);
       }
     }
+  };
 
-    // ---- mask the ragged tail of a segment
+  // prologue: S(0)
+  if (ntiles > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+  else if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sr::barrier_raw();
+  f32x16 scur[2];
+  scores(0, scur);
+
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t+1 must have landed (tile t+2 may stay in flight); everyone is done with t-1
+    if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sr::barrier_raw();
+    if (t + 3 < ntiles) stage(t + 3);
+
+    // ---- [A] mask the ragged tail, row max, rescale
     const bool s1 = t >= args.ntile0;
     const int valid = (s1 ? d.l1 : d.l0) - (s1 ? t - args.ntile0 : t) * KT;
     if (valid < KT) {
@@ -146,14 +157,12 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= valid) sacc[kb][r] = -INFINITY;
+          if (key >= valid) scur[kb][r] = -INFINITY;
         }
     }
-
-    // ---- online softmax: this lane's 32 scores of one query row; partner lane^32 holds 32 more
     float t8[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t8[i] = fmaxf(fmaxf(sacc[0][i], sacc[0][i + 8]), fmaxf(sacc[1][i], sacc[1][i + 8]));
+    for (int i = 0; i < 8; ++i) t8[i] = fmaxf(fmaxf(scur[0][i], scur[0][i + 8]), fmaxf(scur[1][i], scur[1][i + 8]));
 #pragma unroll
     for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
     const float mx = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
@@ -168,19 +177,28 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
       }
       m_run = m_new;
     }
-    // ---- per 32-key block: P = exp2(S*c - m) -> bf16 (B operand), then O^T += V^T P^T
+
+    // ---- [B] S(t+1) on the matrix pipe while P(t) is formed on the VALU
+    f32x16 snext[2];
+    if (t + 1 < ntiles) scores(t + 1, snext);
+    bf16x8 pf[2][2];
     float ps[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      bf16x8 pf[2];
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][8 * s2 + j], c, -m_run));
+          const float p = __builtin_amdgcn_exp2f(fmaf(scur[kb][8 * s2 + j], c, -m_run));
           ps[j & 3] += p;
-          pf[s2][j] = (bf16)p;
+          pf[kb][s2][j] = (bf16)p;
         }
+    l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+
+    // ---- [C] O^T += V(t)^T P(t)^T   (P accumulator = B operand; V^T via transposed LDS reads)
+    const char* vt_lds = smem + (t & (NBUF - 1)) * STAGE_B + TILE_B;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int r0 = kb * 32 + 16 * s2 + 4 * hi;
@@ -194,12 +212,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
           const s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pb);
           const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
           const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
-          o[db] = mfma32(vf, pf[s2], o[db]);
+          o[db] = mfma32(vf, pf[kb][s2], o[db]);
         }
       }
+    if (t + 1 < ntiles) {
+      scur[0] = snext[0];
+      scur[1] = snext[1];
     }
-    l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-    buf = buf == 2 ? 0 : buf + 1;
   }
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l

@@ -1,0 +1,99 @@
+#!/usr/bin/env python
+"""Kernel microbenchmarks at the N=32 @ 518 hot-path shapes (random data).
+
+    python tools/kbench.py [attn] [gemm] [ln]
+
+Each case: warm up, then time R launches with HIP events on the launching stream;
+prints TFLOP/s (MFMA-bound kernels) or GB/s (LayerNorm) and the fraction of peak.
+"""
+
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "self-supervise-sfm_amd"))
+
+import torch  # noqa: E402
+
+from sailrecon_amd import _lib, ops  # noqa: E402
+
+DEV = "cuda"
+PEAK = 2500.0
+
+
+def timeit(fn, reps=10, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def attn():
+    C, H, D = 1024, 16, 64
+    P, N = 1374, 32
+    cases = {
+        "global L=43968": dict(rows=N * P, batch=1, lq=N * P, l0=N * P, kb=0),
+        "frame 64x1374": dict(rows=2 * N * P, batch=2 * N, lq=P, l0=P, kb=P),
+    }
+    for name, c in cases.items():
+        qkv = torch.randn(c["rows"], 3 * C, device=DEV, dtype=torch.bfloat16)
+        o = torch.empty(c["rows"], C, device=DEV, dtype=torch.bfloat16)
+
+        def f():
+            ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=c["batch"],
+                          lq=c["lq"], q_bstride=c["lq"], l0=c["l0"], k0_bstride=c["kb"])
+        ms = timeit(f, reps=5 if c["batch"] == 1 else 10)
+        fl = 4.0 * c["batch"] * H * c["lq"] * c["l0"] * D
+        print(f"attn {name:18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+    # reloc: 32 query frames x (32*305 subsample + own 1374)
+    nsub = N * 305
+    qkv = torch.randn(N * P, 3 * C, device=DEV, dtype=torch.bfloat16)
+    kv = torch.randn(nsub, 2 * C, device=DEV, dtype=torch.bfloat16)
+    o = torch.empty(N * P, C, device=DEV, dtype=torch.bfloat16)
+
+    def f():
+        ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], o, heads=H, head_dim=D, batch=N, lq=P, q_bstride=P, l0=nsub,
+                      k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P)
+    ms = timeit(f)
+    fl = 4.0 * N * H * P * (nsub + P) * D
+    print(f"attn {'reloc 32x(9760+1374)':18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+
+
+def gemm():
+    M = 2 * 32 * 1374
+    for name, (N, K, epi) in {"qkv": (3072, 1024, _lib.SR_EPI_BIAS), "proj": (1024, 1024, _lib.SR_EPI_BIAS_RESID),
+                              "fc1": (4096, 1024, _lib.SR_EPI_BIAS_GELU), "fc2": (1024, 4096, _lib.SR_EPI_BIAS_RESID)}.items():
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / 32
+        b = torch.randn(N, device=DEV)
+        g = torch.randn(N, device=DEV)
+        if epi == _lib.SR_EPI_BIAS_RESID:
+            out = torch.zeros(M, N, device=DEV)
+        else:
+            out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=g))
+        fl = 2.0 * M * N * K
+        print(f"gemm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+
+
+def ln():
+    M, C = 2 * 32 * 1374, 1024
+    x = torch.randn(M, C, device=DEV)
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    out = torch.empty(M, C, device=DEV, dtype=torch.bfloat16)
+    ms = timeit(lambda: ops.layernorm(x, w, b, 1e-5, out))
+    gb = M * C * 6 / 1e9
+    print(f"layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s")
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["attn", "gemm", "ln"]
+    for w in which:
+        globals()[w]()
