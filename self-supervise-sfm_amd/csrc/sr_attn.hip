@@ -72,23 +72,31 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
   const int ntiles = args.ntile0 + args.ntile1;
   const uint32_t lds0 = sr::lds_addr(smem);
 
-  // ---- staging: global DMA instruction gi = wave*DPW + i; gi < 8: K rows 8gi.., else V rows
+  // ---- staging: global DMA instruction gi = wave*DPW + i; gi < 8: K rows 8gi.., else V rows.
+  // Segment pointers are copied to scalars once: selecting between kernel-argument fields
+  // inside the loop compiles to vector loads whose vmcnt(0) wait would drain the ring.
+  const bool stage_v = wave * DPW >= 8;  // wave-uniform: a wave stages only K or only V
+  const bf16* const sb0 = (const bf16*)(stage_v ? d.v0 : d.k0);
+  const bf16* const sb1 = (const bf16*)(stage_v ? d.v1 : d.k1);
+  const int64_t sld0 = stage_v ? d.ldv0 : d.ldk0, sld1 = stage_v ? d.ldv1 : d.ldk1;
+  const int64_t srb0 = (int64_t)item * d.k0_bstride, srb1 = (int64_t)item * d.k1_bstride;
+  const int nt0 = args.ntile0, len0 = d.l0, len1 = d.l1;
   auto stage = [&](int t) {
     const int buf = t & (NBUF - 1);
-    const bool s1 = t >= args.ntile0;
-    const int tt = s1 ? t - args.ntile0 : t;
-    const int len = s1 ? d.l1 : d.l0;
-    const int64_t rbase = item * (s1 ? d.k1_bstride : d.k0_bstride);
+    const bool s1 = t >= nt0;
+    const int tt = s1 ? t - nt0 : t;
+    const int len = s1 ? len1 : len0;
+    const bf16* base = s1 ? sb1 : sb0;
+    const int64_t ld = s1 ? sld1 : sld0;
+    const int64_t rbase = s1 ? srb1 : srb0;
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
       const int gi = wave * DPW + i;
-      const bool v = gi >= 8;
-      const bf16* base = (const bf16*)(v ? (s1 ? d.v1 : d.v0) : (s1 ? d.k1 : d.k0));
-      const int64_t ld = v ? (s1 ? d.ldv1 : d.ldv0) : (s1 ? d.ldk1 : d.ldk0);
       const int r = (gi & 7) * 8 + (lane >> 3);  // key row inside the tile
       const int key = min(tt * KT + r, len - 1);
       const int chunk = (lane & 7) ^ ((r >> 1) & 7);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_B + (v ? TILE_B : 0) + (gi & 7) * 1024);
+      const uint32_t dst =
+          __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_B + (stage_v ? TILE_B : 0) + (gi & 7) * 1024);
       sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst);
     }
   };
@@ -149,8 +157,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
     if (t + 3 < ntiles) stage(t + 3);
 
     // ---- [A] mask the ragged tail, row max, rescale
-    const bool s1 = t >= args.ntile0;
-    const int valid = (s1 ? d.l1 : d.l0) - (s1 ? t - args.ntile0 : t) * KT;
+    const bool s1 = t >= nt0;
+    const int valid = (s1 ? len1 : len0) - (s1 ? t - nt0 : t) * KT;
     if (valid < KT) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -215,10 +223,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
           o[db] = mfma32(vf, pf[kb][s2], o[db]);
         }
       }
-    if (t + 1 < ntiles) {
-      scur[0] = snext[0];
-      scur[1] = snext[1];
-    }
+    scur[0] = snext[0];  // unconditional: a conditional copy costs 32 v_cndmask per tile
+    scur[1] = snext[1];
   }
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
