@@ -21,6 +21,7 @@
 // attn_f32 (parity mode + camera trunk, head_dim 64 | 128): exact fp32 VALU kernel,
 //   K/V tiles broadcast from LDS, per-key online softmax.
 #include <cfloat>
+#include <cstdlib>
 
 #include "sr_common.h"
 
@@ -94,7 +95,10 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
       const int gi = wave * DPW + i;
       const int r = (gi & 7) * 8 + (lane >> 3);  // key row inside the tile
       const int key = min(tt * KT + r, len - 1);
-      const int chunk = (lane & 7) ^ ((r >> 1) & 7);
+      // K rows: chunk ^ ((r>>1)&7) (conflict-free ds_read_b128 fragments);
+      // V rows: chunk ^ (((r>>1)&1)<<2) (conflict-free ds_read_b64_tr_b16: rows r, r+2 of a
+      // 4-row transposed block land in opposite 64-B halves of the same 128-B bank half)
+      const int chunk = (lane & 7) ^ (stage_v ? (((r >> 1) & 1) << 2) : ((r >> 1) & 7));
       const uint32_t dst =
           __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_B + (stage_v ? TILE_B : 0) + (gi & 7) * 1024);
       sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst);
@@ -141,15 +145,21 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
     }
   };
 
+  // V tr-read lane offsets (row r0 + vrow_in; the swizzle term depends only on vrow_in)
+  const int vsw = ((vrow_in >> 1) & 1) << 2;
+  const int voff0 = (4 * hi + vrow_in) * 128 + (((vcol_in >> 3) ^ vsw) * 16) + (vcol_in & 7) * 2;
+  const int voff1 = (4 * hi + vrow_in) * 128 + (((4 + (vcol_in >> 3)) ^ vsw) * 16) + (vcol_in & 7) * 2;
+
   // prologue: S(0)
   if (ntiles > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
   else if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sr::barrier_raw();
-  f32x16 scur[2];
-  scores(0, scur);
+  f32x16 sa[2], sb[2];
+  scores(0, sa);
 
-  for (int t = 0; t < ntiles; ++t) {
+  // one pipelined iteration: softmax/PV of tile t from scur, S(t+1) into snext
+  auto iteration = [&](int t, f32x16 (&scur)[2], f32x16 (&snext)[2]) {
     // tile t+1 must have landed (tile t+2 may stay in flight); everyone is done with t-1
     if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -187,7 +197,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
     }
 
     // ---- [B] S(t+1) on the matrix pipe while P(t) is formed on the VALU
-    f32x16 snext[2];
     if (t + 1 < ntiles) scores(t + 1, snext);
     bf16x8 pf[2][2];
     float ps[4] = {0.f, 0.f, 0.f, 0.f};
@@ -209,23 +218,27 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const int r0 = kb * 32 + 16 * s2 + 4 * hi;
+        const int rowoff = (kb * 32 + 16 * s2) * 128;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
-          const int col = db * 32 + vcol_in;
-          const int ra = r0 + vrow_in, rb = r0 + 8 + vrow_in;
-          const char* pa = vt_lds + ra * 128 + (((col >> 3) ^ ((ra >> 1) & 7)) * 16) + (col & 7) * 2;
-          const char* pb = vt_lds + rb * 128 + (((col >> 3) ^ ((rb >> 1) & 7)) * 16) + (col & 7) * 2;
+          const char* pa = vt_lds + rowoff + (db ? voff1 : voff0);
           const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
-          const s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pb);
+          const s16x4 vb =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
           const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
           const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
           o[db] = mfma32(vf, pf[kb][s2], o[db]);
         }
       }
-    scur[0] = snext[0];  // unconditional: a conditional copy costs 32 v_cndmask per tile
-    scur[1] = snext[1];
+  };
+
+  // unrolled by two with named score buffers (no register copies between iterations)
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    iteration(t, sa, sb);
+    iteration(t + 1, sb, sa);
   }
+  if (t < ntiles) iteration(t, sa, sb);
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
   const float inv = 1.f / sum_x32(l_run);
@@ -338,14 +351,23 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
     const int kind = d.l1 > 0 ? 1 : (d.batch == 1 && d.lq >= 4096 ? 2 : 0);
-    if (d.lq >= 4096) {  // long sequences: 256-row query tiles halve K/V traffic per FLOP
+    // 256-row query tiles (8 waves) for long sequences halve K/V traffic per FLOP;
+    // frame-sized sequences (1374) keep 128-row tiles so the ragged last tile stays small.
+    // SR_ATTN_WAVES=4|8 overrides (tuning experiments).
+    static const int force_nw = [] {
+      const char* e = getenv("SR_ATTN_WAVES");
+      return e ? atoi(e) : 0;
+    }();
+    const bool wide = force_nw ? force_nw == 8 : d.lq >= 4096;
+    if (wide) {
       dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
       if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), grid, dim3(512), 0, s, a);
       else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<8, 1>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((attn_bf16_kernel<8, 0>), grid, dim3(512), 0, s, a);
-    } else {  // frame-sized sequences (1374): 128-row tiles keep the ragged last tile small
+    } else {
       dim3 grid((d.lq + 127) / 128, d.heads, d.batch);
-      if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<4, 1>), grid, dim3(256), 0, s, a);
+      if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), grid, dim3(256), 0, s, a);
+      else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<4, 1>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((attn_bf16_kernel<4, 0>), grid, dim3(256), 0, s, a);
     }
     return sr::check_launch("sr_attention(bf16)");

@@ -29,12 +29,18 @@ for step in "$@"; do
     bench)   run bench 600 python bench.py ;;
     benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
+    kattn)   run kattn 300 python tools/kbench.py attn ;;
+    kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
+    kattn8)  run kattn8 300 env SR_ATTN_WAVES=8 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     pmc_fetch) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
                python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     pmc_write) run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
                python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    counters) run counters 120 rocprofv3 -L ;;
+    pmc_attn1) run pmc_attn1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_attn1 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
+    pmc_attn2) run pmc_attn2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_attn2 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
