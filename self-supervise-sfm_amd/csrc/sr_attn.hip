@@ -36,7 +36,6 @@ struct AttnArgs {
 constexpr int KT = 64;               // keys per tile
 constexpr int TILE_B = KT * 128;     // bytes of one K (or V) tile: 64 keys x 64 bf16
 constexpr int STAGE_B = 2 * TILE_B;  // K + V
-constexpr int NBUF = 4;              // K/V ring depth (power of 2)
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -52,17 +51,18 @@ __device__ __forceinline__ float sum_x32(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// NW waves x 32 query rows per workgroup; KIND only names the call site for profiles
-// (0 frame, 1 global_reloc, 2 global).
+// NW waves x 64 query rows per workgroup (two 32-row q-blocks per wave); KIND only names
+// the call site in profiles (0 frame, 1 global_reloc, 2 global).
 //
-// Software-pipelined tile loop (one barrier per tile, K/V ring of NBUF=4 stages, two
-// stages in flight):  iteration t
-//   [A] row max of S(t) (already in registers), rescale O/l if it grew
-//   [B] S(t+1) = K(t+1) Q^T MFMAs  ||  P(t) = exp2(S(t)*c - m) VALU   (independent: overlap)
-//   [C] O^T += V(t)^T P(t)^T MFMAs
+// Tile loop (K/V ring of NBUF=4 stages, up to 3 in flight, one barrier per tile):
+//   S0 = K Q0^T, S1 = K Q1^T       (16 MFMA; each K fragment read once, used twice)
+//   row max / rescale per q-block  (lane^32 exchange by v_permlane32_swap)
+//   P = exp2(S*c - m) -> bf16; O^T += V^T P^T  (16 MFMA; each V^T fragment used twice)
+// Two workgroups per CU (<= 256 VGPRs) interleave their MFMA / VALU phases freely.
 template <int NW, int KIND>
 __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
-  constexpr int QROWS = NW * 32;
+  constexpr int QROWS = NW * 64;
+  constexpr int NBUF = NW >= 4 ? 4 : 2;  // ring depth (power of 2); NBUF-1 stages in flight
   constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
@@ -97,127 +97,136 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
       const int key = min(tt * KT + r, len - 1);
       // K rows: chunk ^ ((r>>1)&7) (conflict-free ds_read_b128 fragments);
       // V rows: chunk ^ (((r>>1)&1)<<2) (conflict-free ds_read_b64_tr_b16: rows r, r+2 of a
-      // 4-row transposed block land in opposite 64-B halves of the same 128-B bank half)
+      // 4-row transposed block land in opposite 64-B halves)
       const int chunk = (lane & 7) ^ (stage_v ? (((r >> 1) & 1) << 2) : ((r >> 1) & 7));
       const uint32_t dst =
           __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_B + (stage_v ? TILE_B : 0) + (gi & 7) * 1024);
       sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst);
     }
   };
-  stage(0);
-  if (ntiles > 1) stage(1);
-  if (ntiles > 2) stage(2);
-
-  // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row l32][16s + 8hi .. +8]
-  const int qrow = qt * QROWS + wave * 32 + l32;
-  const int qrow_c = min(qrow, d.lq - 1);
-  const bf16* qp = (const bf16*)d.q + (item * d.q_bstride + qrow_c) * d.ldq + hcol + 8 * hi;
-  bf16x8 qf[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) stage(i);
+
+  // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row][16s + 8hi .. +8]
+  const int qrow0 = qt * QROWS + wave * 64 + l32;  // q-block b: row qrow0 + 32b
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int qr = min(qrow0 + 32 * b, d.lq - 1);
+    const bf16* qp = (const bf16*)d.q + (item * d.q_bstride + qr) * d.ldq + hcol + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[b][s] = *(const bf16x8*)(qp + 16 * s);
+  }
 
   const float c = d.scale * 1.4426950408889634f;  // scale * log2(e)
-  float m_run = -1e30f, l_run = 0.f;              // l_run: this lane's partial row sum
-  f32x16 o[2];
+  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};  // l_run: this lane's partial row sums
+  f32x16 o[2][2];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o[0][i] = 0.f;
-    o[1][i] = 0.f;
-  }
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[b][0][i] = 0.f;
+      o[b][1][i] = 0.f;
+    }
+  // K fragment: row kb*32 + l32, chunk (2s + hi) ^ kswz
   const int kswz = (l32 >> 1) & 7;
-  // V tr-read: group G = lane>>4, i = lane&15 supplies row r0 + (i>>2), col db*32 + 16(G&1) + 4(i&3)
+  int koff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = l32 * 128 + (((2 * s + hi) ^ kswz) * 16);
+  // V tr-read: group G = lane>>4, i = lane&15 supplies row r0 + (i>>2), col db*32 + 16(G&1) + 4(i&3);
+  // the V swizzle term depends only on (i>>2)
   const int G = lane >> 4, gi_ = lane & 15;
   const int vrow_in = gi_ >> 2;
   const int vcol_in = 16 * (G & 1) + 4 * (gi_ & 3);
-
-  auto scores = [&](int t, f32x16 (&sacc)[2]) {  // S^T = K(t) Q^T, 2 blocks of 32 keys
-    const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
-      const int row = kb * 32 + l32;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *(const bf16x8*)(kt_lds + row * 128 + (((2 * s + hi) ^ kswz) * 16));
-        sacc[kb] = mfma32(kf, qf[s], sacc[kb]);
-      }
-    }
-  };
-
-  // V tr-read lane offsets (row r0 + vrow_in; the swizzle term depends only on vrow_in)
   const int vsw = ((vrow_in >> 1) & 1) << 2;
   const int voff0 = (4 * hi + vrow_in) * 128 + (((vcol_in >> 3) ^ vsw) * 16) + (vcol_in & 7) * 2;
   const int voff1 = (4 * hi + vrow_in) * 128 + (((4 + (vcol_in >> 3)) ^ vsw) * 16) + (vcol_in & 7) * 2;
 
-  // prologue: S(0)
-  if (ntiles > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
-  else if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sr::barrier_raw();
-  f32x16 sa[2], sb[2];
-  scores(0, sa);
-
-  // one pipelined iteration: softmax/PV of tile t from scur, S(t+1) into snext
-  auto iteration = [&](int t, f32x16 (&scur)[2], f32x16 (&snext)[2]) {
-    // tile t+1 must have landed (tile t+2 may stay in flight); everyone is done with t-1
-    if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t must have landed (up to NBUF-2 later stages stay in flight); everyone is done
+    // with tile t-1, whose buffer the next stage overwrites
+    if (NBUF >= 4 && t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+    else if (NBUF >= 3 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sr::barrier_raw();
-    if (t + 3 < ntiles) stage(t + 3);
+    if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
+    const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
+    const char* vt_lds = kt_lds + TILE_B;
 
-    // ---- [A] mask the ragged tail, row max, rescale
+    // ---- S^T = K Q^T for both q-blocks (2 blocks of 32 keys each)
+    f32x16 sc[2][2];  // [q-block][key block]
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[b][kb][i] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *(const bf16x8*)(kt_lds + kb * 4096 + koff[s]);
+        sc[0][kb] = mfma32(kf, qf[0][s], sc[0][kb]);
+        sc[1][kb] = mfma32(kf, qf[1][s], sc[1][kb]);
+      }
+
+    // ---- mask the ragged tail of a segment
     const bool s1 = t >= nt0;
     const int valid = (s1 ? len1 : len0) - (s1 ? t - nt0 : t) * KT;
     if (valid < KT) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= valid) scur[kb][r] = -INFINITY;
-        }
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (key >= valid) sc[b][kb][r] = -INFINITY;
+          }
     }
-    float t8[8];
+
+    // ---- row max per q-block; rescale O / l when it grew
+    float m_new[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t8[i] = fmaxf(fmaxf(scur[0][i], scur[0][i + 8]), fmaxf(scur[1][i], scur[1][i + 8]));
+    for (int b = 0; b < 2; ++b) {
+      float t8[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
-    const float mx = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
-    const float m_new = fmaxf(m_run, mx * c);
-    if (__any(m_new > m_run)) {
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      l_run *= alpha;
+      for (int i = 0; i < 8; ++i)
+        t8[i] = fmaxf(fmaxf(sc[b][0][i], sc[b][0][i + 8]), fmaxf(sc[b][1][i], sc[b][1][i + 8]));
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        o[0][i] *= alpha;
-        o[1][i] *= alpha;
+      for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
+      m_new[b] = fmaxf(m_run[b], max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3]))) * c);
+    }
+    if (__any((m_new[0] > m_run[0]) | (m_new[1] > m_run[1]))) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run[b] - m_new[b]);
+        l_run[b] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o[b][0][i] *= alpha;
+          o[b][1][i] *= alpha;
+        }
+        m_run[b] = m_new[b];
       }
-      m_run = m_new;
     }
 
-    // ---- [B] S(t+1) on the matrix pipe while P(t) is formed on the VALU
-    if (t + 1 < ntiles) scores(t + 1, snext);
-    bf16x8 pf[2][2];
-    float ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(scur[kb][8 * s2 + j], c, -m_run));
-          ps[j & 3] += p;
-          pf[kb][s2][j] = (bf16)p;
-        }
-    l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-
-    // ---- [C] O^T += V(t)^T P(t)^T   (P accumulator = B operand; V^T via transposed LDS reads)
-    const char* vt_lds = smem + (t & (NBUF - 1)) * STAGE_B + TILE_B;
+    // ---- P = exp2(S*c - m) (B operand), O^T += V^T P^T; each V^T fragment feeds both q-blocks
+    float ps[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[b][kb][8 * s2 + j], c, -m_run[b]));
+            ps[b][j & 1] += p;
+            pf[b][j] = (bf16)p;
+          }
         const int rowoff = (kb * 32 + 16 * s2) * 128;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -227,32 +236,31 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
               __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
           const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
           const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
-          o[db] = mfma32(vf, pf[kb][s2], o[db]);
+          o[0][db] = mfma32(vf, pf[0], o[0][db]);
+          o[1][db] = mfma32(vf, pf[1], o[1][db]);
         }
       }
-  };
-
-  // unrolled by two with named score buffers (no register copies between iterations)
-  int t = 0;
-  for (; t + 1 < ntiles; t += 2) {
-    iteration(t, sa, sb);
-    iteration(t + 1, sb, sa);
+    l_run[0] += ps[0][0] + ps[0][1];
+    l_run[1] += ps[1][0] + ps[1][1];
   }
-  if (t < ntiles) iteration(t, sa, sb);
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
-  const float inv = 1.f / sum_x32(l_run);
-  if (qrow < d.lq) {
-    bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+  for (int b = 0; b < 2; ++b) {
+    const float inv = 1.f / sum_x32(l_run[b]);
+    const int qrow = qrow0 + 32 * b;
+    if (qrow < d.lq) {
+      bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v;
+      for (int db = 0; db < 2; ++db)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[db][4 * g + j] * inv);
-        *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
-      }
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
+          *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
+        }
+    }
   }
 }
 
@@ -358,17 +366,19 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
       const char* e = getenv("SR_ATTN_WAVES");
       return e ? atoi(e) : 0;
     }();
-    const bool wide = force_nw ? force_nw == 8 : d.lq >= 4096;
+    // 4 waves x 64 rows = 256-row query tiles for long sequences; frame-sized sequences
+    // (1374 rows) use 2 waves x 64 = 128-row tiles so the ragged last tile stays small.
+    const bool wide = force_nw ? force_nw == 4 : d.lq >= 4096;
     if (wide) {
       dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
-      if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), grid, dim3(512), 0, s, a);
-      else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<8, 1>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((attn_bf16_kernel<8, 0>), grid, dim3(512), 0, s, a);
-    } else {
-      dim3 grid((d.lq + 127) / 128, d.heads, d.batch);
       if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), grid, dim3(256), 0, s, a);
       else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<4, 1>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((attn_bf16_kernel<4, 0>), grid, dim3(256), 0, s, a);
+    } else {
+      dim3 grid((d.lq + 127) / 128, d.heads, d.batch);
+      if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<2, 2>), grid, dim3(128), 0, s, a);
+      else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<2, 1>), grid, dim3(128), 0, s, a);
+      else hipLaunchKernelGGL((attn_bf16_kernel<2, 0>), grid, dim3(128), 0, s, a);
     }
     return sr::check_launch("sr_attention(bf16)");
   }

@@ -31,7 +31,7 @@ for step in "$@"; do
     kbench)  run kbench 300 python tools/kbench.py ;;
     kattn)   run kattn 300 python tools/kbench.py attn ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
-    kattn8)  run kattn8 300 env SR_ATTN_WAVES=8 python tools/kbench.py attn ;;
+    kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     pmc_fetch) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
