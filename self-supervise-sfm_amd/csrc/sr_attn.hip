@@ -368,7 +368,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     }();
     // 4 waves x 64 rows = 256-row query tiles for long sequences; frame-sized sequences
     // (1374 rows) use 2 waves x 64 = 128-row tiles so the ragged last tile stays small.
-    const bool wide = force_nw ? force_nw == 4 : d.lq >= 4096;
+    const bool wide = force_nw ? force_nw == 4 : true;
     if (wide) {
       dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
       if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), grid, dim3(256), 0, s, a);

@@ -129,71 +129,99 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) Mma<T>::run(a[mi], b[ni], acc[mi][ni]);
+        for (int ni = 0; ni < 4; ++ni) Mma<T>::run(b[ni], a[mi], acc[mi][ni]);  // C^T tile
     }
     sr::wait_lgkm0();
     sr::barrier_raw();
   }
 
   // ---------------- epilogue ----------------
+  // acc[mi][ni] holds the C^T 16x16 tile (W rows as the MFMA A operand): lane owns output
+  // row  m0 + wr*64 + mi*16 + lr  and the 4 CONSECUTIVE columns  colw + ni*16 + 4*lg + r,
+  // so every store / residual update is one 8-B (bf16) or 16-B (fp32) vector access.
   const sr_gemm_epi& ep = g.ep;
   const int colw = n0 + wc * 64;  // first output column of this wave
-  float bias[4];
+  float4 bias[4];
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) bias[ni] = ep.bias ? ep.bias[colw + ni * 16 + lr] : 0.f;
+  for (int ni = 0; ni < 4; ++ni)
+    bias[ni] = ep.bias ? *(const float4*)(ep.bias + colw + ni * 16 + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
+  auto biased = [&](int mi, int ni, float (&v)[4]) {
+    v[0] = acc[mi][ni][0] + bias[ni].x;
+    v[1] = acc[mi][ni][1] + bias[ni].y;
+    v[2] = acc[mi][ni][2] + bias[ni].z;
+    v[3] = acc[mi][ni][3] + bias[ni].w;
+  };
+  auto store4 = [&](T* p, const float (&v)[4]) {
+    if constexpr (sr::is_bf16<T>::value) {
+      bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *(bf16x4*)p = o;
+    } else {
+      *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
 
   if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
     T* out = (T*)g.out;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = m0 + wr * 64 + mi * 16 + lr;
+      if (row < g.M) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
-        if (row < g.M) {
+        for (int ni = 0; ni < 4; ++ni) {
+          float v[4];
+          biased(mi, ni, v);
+          if constexpr (EPI == SR_EPI_BIAS_GELU) {
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            float v = acc[mi][ni][r] + bias[ni];
-            if constexpr (EPI == SR_EPI_BIAS_GELU) v = sr::gelu_erf(v);
-            out[(int64_t)row * g.ldo + colw + ni * 16 + lr] = sr::from_f32<T>(v);
+            for (int r = 0; r < 4; ++r) v[r] = sr::gelu_erf(v[r]);
           }
+          store4(out + (int64_t)row * g.ldo + colw + ni * 16 + 4 * lg, v);
         }
       }
+    }
   } else if constexpr (EPI == SR_EPI_BIAS_RESID) {
     float* x = (float*)g.out;
-    float gam[4];
+    float4 gam[4];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) gam[ni] = ep.gamma[colw + ni * 16 + lr];
+    for (int ni = 0; ni < 4; ++ni) gam[ni] = *(const float4*)(ep.gamma + colw + ni * 16 + 4 * lg);
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = m0 + wr * 64 + mi * 16 + lr;
+      if (row < g.M) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
-        if (row < g.M) {
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            float* p = x + (int64_t)row * g.ldo + colw + ni * 16 + lr;
-            *p = *p + (acc[mi][ni][r] + bias[ni]) * gam[ni];
-          }
+        for (int ni = 0; ni < 4; ++ni) {
+          float v[4];
+          biased(mi, ni, v);
+          float4* p = (float4*)(x + (int64_t)row * g.ldo + colw + ni * 16 + 4 * lg);
+          float4 xv = *p;
+          xv.x += v[0] * gam[ni].x;
+          xv.y += v[1] * gam[ni].y;
+          xv.z += v[2] * gam[ni].z;
+          xv.w += v[3] * gam[ni].w;
+          *p = xv;
         }
       }
+    }
   } else if constexpr (EPI == SR_EPI_PATCH) {
     float* x = (float*)g.out;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = m0 + wr * 64 + mi * 16 + lr;
+      if (row < g.M) {
+        const int f = row / ep.seg_rows, p = row - f * ep.seg_rows;
+        const int64_t orow = (int64_t)f * ep.seg_stride + ep.seg_offset + p;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
-        if (row < g.M) {
-          const int f = row / ep.seg_rows, p = row - f * ep.seg_rows;
-          const int64_t orow = (int64_t)f * ep.seg_stride + ep.seg_offset + p;
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            const int col = colw + ni * 16 + lr;
-            x[orow * g.ldo + col] = acc[mi][ni][r] + bias[ni] + ep.row_add[(int64_t)p * g.N + col];
-          }
+        for (int ni = 0; ni < 4; ++ni) {
+          const int col = colw + ni * 16 + 4 * lg;
+          float v[4];
+          biased(mi, ni, v);
+          const float4 ra = *(const float4*)(ep.row_add + (int64_t)p * g.N + col);
+          *(float4*)(x + orow * g.ldo + col) = make_float4(v[0] + ra.x, v[1] + ra.y, v[2] + ra.z, v[3] + ra.w);
         }
       }
+    }
   } else if constexpr (EPI == SR_EPI_QKV) {
+    // the wave's 64 columns are exactly one head: for one output row the 64 values sit in
+    // the 4 lanes lr, lr+16, lr+32, lr+48 (16 each: ni x r).  head dim d = 16 ni + 4 lg + r.
     T* out = (T*)g.out;
     const int region = (colw + ep.col_offset) / ep.embed_dim;  // 0 = Q, 1 = K, 2 = V
     const bool qk = region < 2;
@@ -201,61 +229,80 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
     const float* nb = region == 0 ? ep.qn_b : ep.kn_b;
     const bool do_norm = qk && nw != nullptr;
     const bool do_rope = qk && ep.rope_cos != nullptr;
-    float w4[4], b4[4];
+    float4 w4[4], b4[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-      w4[ni] = do_norm ? nw[ni * 16 + lr] : 1.f;
-      b4[ni] = do_norm ? nb[ni * 16 + lr] : 0.f;
+      w4[ni] = do_norm ? *(const float4*)(nw + ni * 16 + 4 * lg) : make_float4(1.f, 1.f, 1.f, 1.f);
+      b4[ni] = do_norm ? *(const float4*)(nb + ni * 16 + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = m0 + wr * 64 + mi * 16 + lr;
+      float v[4][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + mi * 16 + lg * 4 + r;
-        float v[4];
+      for (int ni = 0; ni < 4; ++ni) biased(mi, ni, v[ni]);
+      if (do_norm) {  // LayerNorm over the head's 64 values: 16 in-lane x 4 lanes (xor 16, 32)
+        float sum = 0.f;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) v[ni] = acc[mi][ni][r] + bias[ni];
-        if (do_norm) {  // LayerNorm over the 64 head columns: 4 per lane x 16 lanes
-          const float mean = group16_sum(v[0] + v[1] + v[2] + v[3]) * (1.f / 64.f);
-          float d2 = 0.f;
+        for (int ni = 0; ni < 4; ++ni) sum += (v[ni][0] + v[ni][1]) + (v[ni][2] + v[ni][3]);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mean = sum * (1.f / 64.f);
+        float d2 = 0.f;
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            v[ni] -= mean;
-            d2 += v[ni] * v[ni];
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[ni][r] -= mean;
+            d2 += v[ni][r] * v[ni][r];
           }
-          const float rstd = rsqrtf(group16_sum(d2) * (1.f / 64.f) + ep.qk_eps);
+        d2 += __shfl_xor(d2, 16, 64);
+        d2 += __shfl_xor(d2, 32, 64);
+        const float rstd = rsqrtf(d2 * (1.f / 64.f) + ep.qk_eps);
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) v[ni] = v[ni] * rstd * w4[ni] + b4[ni];
-        }
-        if (do_rope) {
-          const int rr = min(row, g.M - 1);
-          int py = 0, px = 0;
-          if (ep.pos_yx) {
-            py = ep.pos_yx[2 * rr];
-            px = ep.pos_yx[2 * rr + 1];
-          } else {
-            const int64_t tr = ep.pos_rowmap ? (int64_t)ep.pos_rowmap[rr] : ep.pos_row_base + rr;
-            const int t = (int)(tr % ep.tokens_per_frame);
-            if (t >= ep.patch_start) {
-              const int p = t - ep.patch_start;
-              py = p / ep.grid_w + 1;
-              px = p - (py - 1) * ep.grid_w + 1;
-            }
-          }
-          const float cy = ep.rope_cos[py * 16 + lr], sy = ep.rope_sin[py * 16 + lr];
-          const float cx = ep.rope_cos[px * 16 + lr], sx = ep.rope_sin[px * 16 + lr];
-          const float y0 = v[0] * cy - v[1] * sy, y1 = v[1] * cy + v[0] * sy;
-          const float x0 = v[2] * cx - v[3] * sx, x1 = v[3] * cx + v[2] * sx;
-          v[0] = y0;
-          v[1] = y1;
-          v[2] = x0;
-          v[3] = x1;
-        }
-        if (row < g.M) {
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) out[(int64_t)row * g.ldo + colw + ni * 16 + lr] = sr::from_f32<T>(v[ni]);
+        for (int ni = 0; ni < 4; ++ni) {
+          v[ni][0] = v[ni][0] * rstd * w4[ni].x + b4[ni].x;
+          v[ni][1] = v[ni][1] * rstd * w4[ni].y + b4[ni].y;
+          v[ni][2] = v[ni][2] * rstd * w4[ni].z + b4[ni].z;
+          v[ni][3] = v[ni][3] * rstd * w4[ni].w + b4[ni].w;
         }
       }
+      if (do_rope) {  // pairs (d, d+16): y half ni 0|1, x half ni 2|3; same lane, same r
+        const int rr = min(row, g.M - 1);
+        int py = 0, px = 0;
+        if (ep.pos_yx) {
+          py = ep.pos_yx[2 * rr];
+          px = ep.pos_yx[2 * rr + 1];
+        } else {
+          const int64_t tr = ep.pos_rowmap ? (int64_t)ep.pos_rowmap[rr] : ep.pos_row_base + rr;
+          const int t = (int)(tr % ep.tokens_per_frame);
+          if (t >= ep.patch_start) {
+            const int p = t - ep.patch_start;
+            py = p / ep.grid_w + 1;
+            px = p - (py - 1) * ep.grid_w + 1;
+          }
+        }
+        const float4 cy = *(const float4*)(ep.rope_cos + py * 16 + 4 * lg);
+        const float4 sy = *(const float4*)(ep.rope_sin + py * 16 + 4 * lg);
+        const float4 cx = *(const float4*)(ep.rope_cos + px * 16 + 4 * lg);
+        const float4 sx = *(const float4*)(ep.rope_sin + px * 16 + 4 * lg);
+        const float cyv[4] = {cy.x, cy.y, cy.z, cy.w}, syv[4] = {sy.x, sy.y, sy.z, sy.w};
+        const float cxv[4] = {cx.x, cx.y, cx.z, cx.w}, sxv[4] = {sx.x, sx.y, sx.z, sx.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float y0 = v[0][r] * cyv[r] - v[1][r] * syv[r], y1 = v[1][r] * cyv[r] + v[0][r] * syv[r];
+          const float x0 = v[2][r] * cxv[r] - v[3][r] * sxv[r], x1 = v[3][r] * cxv[r] + v[2][r] * sxv[r];
+          v[0][r] = y0;
+          v[1][r] = y1;
+          v[2][r] = x0;
+          v[3][r] = x1;
+        }
+      }
+      if (row < g.M) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) store4(out + (int64_t)row * g.ldo + colw + ni * 16 + 4 * lg, v[ni]);
+      }
+    }
   }
 }
 
