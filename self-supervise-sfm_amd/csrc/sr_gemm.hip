@@ -18,6 +18,7 @@
 //   * epilogues fused in registers: bias, erf-GELU, LayerScale+residual, patch remap +
 //     positional add, and qk-LayerNorm + 2-D RoPE (each wave owns one 64-wide head).
 #include <cstdio>
+#include <cstdlib>
 
 #include "sr_common.h"
 
@@ -60,87 +61,15 @@ template <> struct Mma<float> {
   }
 };
 
-__device__ __forceinline__ float group16_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  return v;
-}
-
-template <typename T, int EPI>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
-  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
-  const int tm = tile / ntn, tn = tile - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // LDS-DMA sources: instruction i of wave w fills tile rows (w*8+i)*8 .. +8 (rows < BM: A, else W).
-  const char* src[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int tr = (wave * 8 + i) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
-    if (tr < BM) {
-      const int r = min(m0 + tr, g.M - 1);
-      src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
-    } else {
-      const int r = n0 + tr - BM;
-      src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
-    }
-  }
-  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
-  auto stage = [&](int kt, int buf) {
-    const uint32_t base = dst0 + buf * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
-  };
-
-  const int wr = wave >> 1, wc = wave & 1;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int swz = lr >> 1;  // (row>>1)&7 for every fragment row of this lane
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0, 0);
-  for (int kt = 0; kt < g.ktiles; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < g.ktiles) {
-      stage(kt + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    sr::barrier_raw();
-    const char* sb = smem + buf * STAGE_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int coff = (((ks * 4 + lg) ^ swz) * 16);
-      uint4 a[4], b[4];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + (wr * 64 + mi * 16 + lr) * ROWB + coff);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) b[ni] = *(const uint4*)(sb + (BM + wc * 64 + ni * 16 + lr) * ROWB + coff);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) Mma<T>::run(b[ni], a[mi], acc[mi][ni]);  // C^T tile
-    }
-    sr::wait_lgkm0();
-    sr::barrier_raw();
-  }
-
-  // ---------------- epilogue ----------------
+// Fused epilogue on C^T accumulator tiles: acc[mi][ni] covers output rows
+// rowbase + mi*16 + lr and the 4 consecutive columns colw + ni*16 + 4*lg + r.
+template <typename T, int EPI, int MT>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
+                                         int lg) {
   // acc[mi][ni] holds the C^T 16x16 tile (W rows as the MFMA A operand): lane owns output
   // row  m0 + wr*64 + mi*16 + lr  and the 4 CONSECUTIVE columns  colw + ni*16 + 4*lg + r,
   // so every store / residual update is one 8-B (bf16) or 16-B (fp32) vector access.
   const sr_gemm_epi& ep = g.ep;
-  const int colw = n0 + wc * 64;  // first output column of this wave
   float4 bias[4];
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni)
@@ -163,8 +92,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
     T* out = (T*)g.out;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = m0 + wr * 64 + mi * 16 + lr;
+    for (int mi = 0; mi < MT; ++mi) {
+      const int row = rowbase + mi * 16 + lr;
       if (row < g.M) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
@@ -184,8 +113,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) gam[ni] = *(const float4*)(ep.gamma + colw + ni * 16 + 4 * lg);
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = m0 + wr * 64 + mi * 16 + lr;
+    for (int mi = 0; mi < MT; ++mi) {
+      const int row = rowbase + mi * 16 + lr;
       if (row < g.M) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
@@ -204,8 +133,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   } else if constexpr (EPI == SR_EPI_PATCH) {
     float* x = (float*)g.out;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = m0 + wr * 64 + mi * 16 + lr;
+    for (int mi = 0; mi < MT; ++mi) {
+      const int row = rowbase + mi * 16 + lr;
       if (row < g.M) {
         const int f = row / ep.seg_rows, p = row - f * ep.seg_rows;
         const int64_t orow = (int64_t)f * ep.seg_stride + ep.seg_offset + p;
@@ -236,8 +165,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
       b4[ni] = do_norm ? *(const float4*)(nb + ni * 16 + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = m0 + wr * 64 + mi * 16 + lr;
+    for (int mi = 0; mi < MT; ++mi) {
+      const int row = rowbase + mi * 16 + lr;
       float v[4][4];
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) biased(mi, ni, v[ni]);
@@ -307,6 +236,186 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
 }
 
 template <typename T, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
+  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // LDS-DMA sources: instruction i of wave w fills tile rows (w*8+i)*8 .. +8 (rows < BM: A, else W).
+  const char* src[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tr = (wave * 8 + i) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
+    if (tr < BM) {
+      const int r = min(m0 + tr, g.M - 1);
+      src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
+    } else {
+      const int r = n0 + tr - BM;
+      src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
+    }
+  }
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
+  auto stage = [&](int kt, int buf) {
+    const uint32_t base = dst0 + buf * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+  };
+
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int swz = lr >> 1;  // (row>>1)&7 for every fragment row of this lane
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  for (int kt = 0; kt < g.ktiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < g.ktiles) {
+      stage(kt + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sr::barrier_raw();
+    const char* sb = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int coff = (((ks * 4 + lg) ^ swz) * 16);
+      uint4 a[4], b[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + (wr * 64 + mi * 16 + lr) * ROWB + coff);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) b[ni] = *(const uint4*)(sb + (BM + wc * 64 + ni * 16 + lr) * ROWB + coff);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) Mma<T>::run(b[ni], a[mi], acc[mi][ni]);  // C^T tile
+    }
+    sr::wait_lgkm0();
+    sr::barrier_raw();
+  }
+
+  epilogue<T, EPI, 4>(g, acc, m0 + wr * 64, n0 + wc * 64, lr, lg);
+}
+
+// ---------------------------------------------------------------------------------------
+// 256x256 bf16 GEMM for the large-M aggregator GEMMs (M = S*P tokens).
+//   * 512 threads = 8 waves as 2 (M) x 4 (N); per wave 128 x 64 outputs = 8 x 4 C^T tiles
+//     (128 accumulator VGPRs); one workgroup per CU (128 KiB LDS);
+//   * K-tile = 64 (128 B rows), 2 LDS stages of 64 KiB [A 256 rows | W 256 rows], XOR-swizzled;
+//   * ONE barrier per K-tile: after it, the whole next stage is issued by LDS-DMA (8 per wave)
+//     and lands while the 64 MFMAs of the current tile run;
+//   * the tile is computed as 4 quadrant phases (64 rows x 32 cols, 16 MFMAs each) ordered so
+//     consecutive quadrants share A or B fragments (28 ds_read_b128 per 64 MFMAs);
+//   * s_setprio 1 around each MFMA cluster keeps the cluster intact (cdna_hip_programming.md T5).
+constexpr int BIG = 256;
+constexpr int STAGE_BIG = 2 * BIG * ROWB;  // 64 KiB
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = g.N / BIG, ntm = (g.M + BIG - 1) / BIG;
+  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int m0 = tm * BIG, n0 = tn * BIG;
+
+  // LDS-DMA sources: wave w, instruction i fills stage rows (w*8 + i)*8 .. +8 of the 512-row
+  // stage (rows < 256: A, else W).
+  const char* src[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tr = (wave * 8 + i) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
+    if (tr < BIG) {
+      const int r = min(m0 + tr, g.M - 1);
+      src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
+    } else {
+      src[i] = g.W + (int64_t)(n0 + tr - BIG) * g.ldw_b + chunk * 16;
+    }
+  }
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
+  auto stage = [&](int kt) {
+    const uint32_t base = dst0 + (kt & 1) * STAGE_BIG;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+  };
+
+  const int wr = wave >> 2, wc = wave & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int swz = lr >> 1;
+  // fragment row offsets (bytes) inside a stage
+  const int arow = (wr * 128 + lr) * ROWB;        // + (qm*64 + mi*16) * ROWB
+  const int brow = (BIG + wc * 64 + lr) * ROWB;   // + (qn*32 + ni*16) * ROWB
+  const int coff0 = ((0 + lg) ^ swz) * 16, coff1 = ((4 + lg) ^ swz) * 16;  // k-substep 0 / 1
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  for (int kt = 0; kt < g.ktiles; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
+    sr::barrier_raw();                                  // ... every wave's; all done with kt-1
+    if (kt + 1 < g.ktiles) stage(kt + 1);              // overwrites the buffer of kt-1
+    const char* sb = smem + (kt & 1) * STAGE_BIG;
+    uint4 a[4][2], b[2][2];
+    auto load_a = [&](int qm) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
+        a[mi][0] = *(const uint4*)(p + coff0);
+        a[mi][1] = *(const uint4*)(p + coff1);
+      }
+    };
+    auto load_b = [&](int qn) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
+        b[ni][0] = *(const uint4*)(p + coff0);
+        b[ni][1] = *(const uint4*)(p + coff1);
+      }
+    };
+    auto mma = [&](int qm, int qn) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    load_a(0);
+    load_b(0);
+    mma(0, 0);
+    load_b(1);
+    mma(0, 1);
+    load_a(1);
+    mma(1, 1);
+    load_b(0);
+    mma(1, 0);
+  }
+  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+}
+
+template <int EPI>
+int launch256(const GemmArgs& a, hipStream_t s) {
+  const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
+  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
+  return sr::check_launch("sr_gemm(256)");
+}
+
+template <typename T, int EPI>
 int launch(const GemmArgs& a, hipStream_t s) {
   const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
   hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg), dim3(NTHREADS), 0, s, a);
@@ -315,6 +424,18 @@ int launch(const GemmArgs& a, hipStream_t s) {
 
 template <typename T>
 int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
+  if constexpr (sr::is_bf16<T>::value) {
+    static const bool no_big = getenv("SR_GEMM_NO256") != nullptr;  // tuning A/B switch
+    if (!no_big && a.N % BIG == 0 && a.M >= 2048) {
+      switch (epi) {
+        case SR_EPI_BIAS: return launch256<SR_EPI_BIAS>(a, s);
+        case SR_EPI_BIAS_GELU: return launch256<SR_EPI_BIAS_GELU>(a, s);
+        case SR_EPI_BIAS_RESID: return launch256<SR_EPI_BIAS_RESID>(a, s);
+        case SR_EPI_QKV: return launch256<SR_EPI_QKV>(a, s);
+        case SR_EPI_PATCH: return launch256<SR_EPI_PATCH>(a, s);
+      }
+    }
+  }
   switch (epi) {
     case SR_EPI_BIAS: return launch<T, SR_EPI_BIAS>(a, s);
     case SR_EPI_BIAS_GELU: return launch<T, SR_EPI_BIAS_GELU>(a, s);

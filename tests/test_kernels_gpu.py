@@ -36,7 +36,8 @@ DT = [(torch.float32, 2e-6), (torch.bfloat16, 8e-3)]
 
 
 @pytest.mark.parametrize("dtype,tol", DT)
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 256, 1024), (1374, 384, 128), (77, 3072, 1024)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 256, 1024), (1374, 384, 128), (77, 3072, 1024),
+                                   (2500, 512, 256), (4100, 1024, 1024), (2048, 256, 4096)])
 def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
     L = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
@@ -52,10 +53,11 @@ def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-5)])
-def test_gemm_resid_strided(ops, dtype, tol):
+@pytest.mark.parametrize("M", [517, 3000])
+def test_gemm_resid_strided(ops, dtype, tol, M):
     """fp32 residual epilogue on a row slice of a bigger buffer (the reloc/global stacks)."""
     L = _lib()
-    M, N, K = 517, 256, 512
+    N, K = 256, 512
     a = torch.randn(M, K, device=DEV).to(dtype)
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(dtype)
     b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
@@ -69,14 +71,16 @@ def test_gemm_resid_strided(ops, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", DT)
-def test_gemm_patch_epilogue(ops, dtype, tol):
+@pytest.mark.parametrize("frames,npatch,C", [(3, 16, 128), (10, 256, 256)])
+def test_gemm_patch_epilogue(ops, dtype, tol, frames, npatch, C):
     L = _lib()
-    frames, npatch, P, C, K = 3, 16, 21, 128, 640
+    P, K = npatch + 5, 640
     a = torch.randn(frames * npatch, K, device=DEV).to(dtype)
     w = (torch.randn(C, K, device=DEV) / 25).to(dtype)
     b = torch.randn(C, device=DEV)
     pos = torch.randn(npatch, C, device=DEV)
     x = torch.full((frames * P, C), 7.0, device=DEV)
+    w = w / (K ** 0.5 / 25)
     ops.gemm(a, w, x, L.SR_EPI_PATCH, bias=b, rows=frames * npatch,
              patch=dict(seg_rows=npatch, seg_stride=P, seg_offset=5, row_add=pos))
     ref = (a.float() @ w.float().t() + b).view(frames, npatch, C) + pos
@@ -92,12 +96,13 @@ def _rope_ref(t, pos, base=100.0):
 
 @pytest.mark.parametrize("dtype,tol", DT)
 @pytest.mark.parametrize("col_offset", [0, 1])
-def test_gemm_qkv_epilogue(ops, dtype, tol, col_offset):
+@pytest.mark.parametrize("frames", [3, 100])
+def test_gemm_qkv_epilogue(ops, dtype, tol, col_offset, frames):
     """bias + qk-LayerNorm + 2-D RoPE fused into the qkv GEMM (attention.py:72-82)."""
     from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
     L = _lib()
     C, H, D = 256, 4, 64
-    P, gw, frames = 21, 4, 3
+    P, gw = 21, 4
     M = frames * P
     a = torch.randn(M, C, device=DEV).to(dtype)
     w = (torch.randn(3 * C, C, device=DEV) / 16).to(dtype)
