@@ -368,8 +368,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     sr::barrier_raw();                                  // ... every wave's; all done with kt-1
     if (kt + 1 < g.ktiles) stage(kt + 1);              // overwrites the buffer of kt-1
     const char* sb = smem + (kt & 1) * STAGE_BIG;
-    uint4 a[4][2], b[2][2];
-    auto load_a = [&](int qm) {
+    // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
+    // the current quadrant's MFMA cluster so their LDS latency hides under it
+    uint4 aX[4][2], aY[4][2], bX[2][2], bY[2][2];
+    auto load_a = [&](uint4 (&a)[4][2], int qm) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
@@ -377,7 +379,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         a[mi][1] = *(const uint4*)(p + coff1);
       }
     };
-    auto load_b = [&](int qn) {
+    auto load_b = [&](uint4 (&b)[2][2], int qn) {
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         b[ni][1] = *(const uint4*)(p + coff1);
       }
     };
-    auto mma = [&](int qm, int qn) {
+    auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -395,15 +397,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
           for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
       __builtin_amdgcn_s_setprio(0);
     };
-    load_a(0);
-    load_b(0);
-    mma(0, 0);
-    load_b(1);
-    mma(0, 1);
-    load_a(1);
-    mma(1, 1);
-    load_b(0);
-    mma(1, 0);
+    load_a(aX, 0);
+    load_b(bX, 0);
+    load_b(bY, 1);
+    mma(aX, bX, 0, 0);
+    load_a(aY, 1);
+    mma(aX, bY, 0, 1);
+    load_b(bX, 0);
+    mma(aY, bY, 1, 1);
+    mma(aY, bX, 1, 0);
   }
   epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
 }
