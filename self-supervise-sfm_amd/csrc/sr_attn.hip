@@ -359,16 +359,16 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
     const int kind = d.l1 > 0 ? 1 : (d.batch == 1 && d.lq >= 4096 ? 2 : 0);
-    // 256-row query tiles (8 waves) for long sequences halve K/V traffic per FLOP;
-    // frame-sized sequences (1374) keep 128-row tiles so the ragged last tile stays small.
-    // SR_ATTN_WAVES=4|8 overrides (tuning experiments).
+    // 4 waves x 64 rows = 256-row query tiles (measured fastest for the frame, reloc and global
+    // stacks at N=32); 2-wave 128-row tiles when 256-row tiles would leave CUs idle (fewer than
+    // 2 workgroups per CU, e.g. the per-rank query slice of a frame-sharded global block).
+    // SR_ATTN_WAVES=2|4 overrides (tuning experiments).
     static const int force_nw = [] {
       const char* e = getenv("SR_ATTN_WAVES");
       return e ? atoi(e) : 0;
     }();
-    // 4 waves x 64 rows = 256-row query tiles for long sequences; frame-sized sequences
-    // (1374 rows) use 2 waves x 64 = 128-row tiles so the ragged last tile stays small.
-    const bool wide = force_nw ? force_nw == 4 : true;
+    const long wgs256 = (long)((d.lq + 255) / 256) * d.heads * d.batch;
+    const bool wide = force_nw ? force_nw == 4 : wgs256 >= 512;
     if (wide) {
       dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
       if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), grid, dim3(256), 0, s, a);

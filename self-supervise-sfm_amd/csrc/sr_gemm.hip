@@ -428,7 +428,10 @@ template <typename T>
 int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
   if constexpr (sr::is_bf16<T>::value) {
     static const bool no_big = getenv("SR_GEMM_NO256") != nullptr;  // tuning A/B switch
-    if (!no_big && a.N % BIG == 0 && a.M >= 2048) {
+    // 256x256 tiles (one WG per CU) only when they still give >= 2 WGs per CU; smaller
+    // problems (frame-sharded ranks, small scenes) keep 4x more 128x128 workgroups.
+    const long tiles256 = (long)(a.N / BIG) * ((a.M + BIG - 1) / BIG);
+    if (!no_big && a.N % BIG == 0 && tiles256 >= 512) {
       switch (epi) {
         case SR_EPI_BIAS: return launch256<SR_EPI_BIAS>(a, s);
         case SR_EPI_BIAS_GELU: return launch256<SR_EPI_BIAS_GELU>(a, s);

@@ -76,8 +76,7 @@ class CameraHead(nn.Module):
     def forward(self, aggregated_tokens_list, cam_token_last_layer: torch.Tensor, num_iterations: int = 4) -> List:
         tokens = aggregated_tokens_list[-1]
         dev = tokens.device
-        if not tokens.is_cuda:
-            raise RuntimeError("sailrecon_amd CameraHead runs on the HIP path only")
+        runtime.require_device(tokens, "CameraHead")
         B, Nq = tokens.shape[0], tokens.shape[1]
         Na = cam_token_last_layer.shape[1]
         Sc = Na + Nq

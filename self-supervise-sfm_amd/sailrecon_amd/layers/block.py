@@ -67,8 +67,7 @@ class Block(nn.Module):
         self._packed.clear()
 
     def forward(self, x: Tensor, pos: Optional[Tensor] = None, attn_mask: Optional[Tensor] = None) -> Tensor:
-        if not x.is_cuda:
-            raise RuntimeError("sailrecon_amd Block runs on the HIP path only (x must be on a ROCm device)")
+        runtime.require_device(x, "Block")
         dtype = runtime.compute_dtype()
         B, N, C = x.shape
         pb = self.packed(dtype)

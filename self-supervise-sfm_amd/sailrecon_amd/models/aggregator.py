@@ -159,6 +159,33 @@ class Aggregator(nn.Module):
                     out[l, b, a] = torch.randperm(n_patch, generator=self.generator)[:rank].numpy()
         return out
 
+    # ------------------------------------------------------------------ multi-GPU
+    def set_frame_sharding(self, group=None):
+        """Shard frames across the ranks of ``group`` (torch.distributed, RCCL on ROCm).
+
+        Rank r of G owns anchors no_reloc_list[r*Na/G:(r+1)*Na/G] and the matching slice of
+        reloc_list.  DINO, frame blocks, subsampling and every per-token GEMM stay local;
+        the global block all-gathers K/V of the anchors, the global_reloc block all-gathers
+        the anchor-subsample K/V, and the camera head runs replicated on gathered camera
+        tokens.  The subsample generator is re-seeded identically on every
+        rank (broadcast from rank 0) so the draws do not depend on the world size.
+        ``group=None`` disables sharding."""
+        self._shard_group = group
+        if group is not None:
+            seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+            dist = torch.distributed
+            if dist.get_backend(group) == "nccl":
+                seed = seed.cuda()
+            dist.broadcast(seed, src=dist.get_global_rank(group, 0) if hasattr(dist, "get_global_rank") else 0,
+                           group=group)
+            self.generator.manual_seed(int(seed.item()))
+
+    def _world(self):
+        g = getattr(self, "_shard_group", None)
+        if g is None:
+            return None, 1, 0
+        return g, torch.distributed.get_world_size(g), torch.distributed.get_rank(g)
+
     # ------------------------------------------------------------------ forward
     def forward(self, images: torch.Tensor, no_reloc_list: list, reloc_list: list,
                 fix_rank: Union[int, None] = None) -> Tuple[Dict[int, torch.Tensor], int, torch.Tensor]:
@@ -167,8 +194,7 @@ class Aggregator(nn.Module):
         self.num_recon = num_recon
         if C_in != 3:
             raise ValueError(f"Expected 3 input channels, got {C_in}")
-        if not images.is_cuda:
-            raise RuntimeError("sailrecon_amd Aggregator runs on the HIP path only (images must be on a ROCm device)")
+        runtime.require_device(images, "Aggregator")
         if sorted(list(no_reloc_list) + list(reloc_list)) != list(range(S)):
             raise ValueError("no_reloc_list and reloc_list must be disjoint and cover every frame "
                              f"(S={S}, got {list(no_reloc_list)} / {list(reloc_list)}); the reference's "
@@ -177,6 +203,16 @@ class Aggregator(nn.Module):
             raise ValueError("at least one anchor (no_reloc) frame is required")
         ps = self.patch_size
         assert H % ps == 0 and W % ps == 0, f"image size {H}x{W} is not a multiple of the patch size {ps}"
+        group, G, r = self._world()
+        Na, Nq = num_recon, num_reloc
+        if G > 1 and (B != 1 or Na % G or Nq % G):
+            raise ValueError(f"frame sharding over {G} ranks needs B == 1 and anchor / query counts "
+                             f"divisible by {G} (got B={B}, Na={Na}, Nq={Nq})")
+        Na_l, Nq_l = Na // G, Nq // G
+        my_anchors = list(no_reloc_list)[r * Na_l:(r + 1) * Na_l]
+        my_queries = list(reloc_list)[r * Nq_l:(r + 1) * Nq_l]
+        S_l = Na_l + Nq_l
+
         dev = images.device
         dtype = runtime.compute_dtype(self.compute_dtype)
         C, nh = self.embed_dim, self.num_heads
@@ -184,14 +220,13 @@ class Aggregator(nn.Module):
         n_patch = gh * gw
         psi = self.patch_start_idx
         P = n_patch + psi
-        Na, Nq = num_recon, num_reloc
-        F_ = B * S
+        F_ = B * S_l
         R = F_ * P
         ws = self._ws
         hidden = self.frame_blocks[0].mlp.fc1.out_features
 
-        # ---- internal frame order: anchors then queries (per batch item)
-        order = list(no_reloc_list) + list(reloc_list)
+        # ---- internal (local) frame order: anchors then queries, per batch item
+        order = my_anchors + my_queries
         imgs = images if order == list(range(S)) else images[:, order]
         imgs = imgs.reshape(F_, 3, H, W).float().contiguous()
 
@@ -212,7 +247,7 @@ class Aggregator(nn.Module):
         else:
             row_add = ws.get("zeros_pos", n_patch, C, torch.float32, dev).zero_()
         ops.gemm(cols, misc["w_patch"], x, _lib.SR_EPI_PATCH, bias=misc["b_patch"], rows=F_ * n_patch,
-                 patch=dict(seg_rows=n_patch, seg_stride=P, seg_offset=psi, row_add=row_add))
+                 patch=dict(seg_rows=n_patch, seg_stride=P, seg_offset=psi, row_add=row_add), tag="gemm")
         if is_dino:
             nreg_d = dino.num_register_tokens
             if 1 + nreg_d != psi:
@@ -226,11 +261,11 @@ class Aggregator(nn.Module):
                 runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P), None)
             ops.layernorm(x, dino.norm.weight, dino.norm.bias, dino.norm.eps, x)  # in place (row-local)
 
-        # ---- aggregator special tokens, aggregator.py:287-299
+        # ---- aggregator special tokens, aggregator.py:287-299 (type by ORIGINAL frame index)
         ftype = []
         for b in range(B):
-            ftype += [0 if no_reloc_list[a] == 0 else 1 for a in range(Na)] + [2] * Nq
-        ftype_t = torch.tensor(ftype, dtype=torch.int32).to(dev, non_blocking=True)
+            ftype += [0 if a == 0 else 1 for a in my_anchors] + [2] * Nq_l
+        ftype_t = runtime.to_device(torch.tensor(ftype, dtype=torch.int32), dev)
         ops.set_special_tokens(x, F_, P, misc["special"], ftype_t)
 
         # ---- subsample draws (host, overlaps the GPU work above), aggregator.py:277-285, 580-626
@@ -239,28 +274,30 @@ class Aggregator(nn.Module):
         else:
             lo, hi = min(self.min_rank, n_patch // 2), max(self.min_rank, n_patch // 2)
             self.rank = int(torch.randint(lo, hi, (1,), generator=self.generator).item())
-        rank = self.rank
-        Pp = min(rank + psi, P)
-        idx = self.draw_subsample(self.depth, B, Na, n_patch, rank) if Nq > 0 else None
-        if idx is not None:
+        rank_ = self.rank
+        Pp = min(rank_ + psi, P)
+        rowmap_t = None
+        if Nq > 0:
+            idx = self.draw_subsample(self.depth, B, Na, n_patch, rank_)  # every rank draws all anchors
             self.last_subsample_indices = torch.from_numpy(idx)
-            base = (np.arange(B) * S * P)[None, :, None, None] + (np.arange(Na) * P)[None, None, :, None]
-            sel = base + psi + idx                                       # [depth, B, Na, rank]
-            spec = np.broadcast_to(base + np.arange(psi)[None, None, None, :], (self.depth, B, Na, psi))
-            rowmap = np.concatenate([spec, sel], axis=-1).reshape(self.depth, B, Na * Pp).astype(np.int32)
-            rowmap_t = torch.from_numpy(rowmap).pin_memory().to(dev, non_blocking=True)
+            idx = idx[:, :, r * Na_l:(r + 1) * Na_l]                      # this rank's anchors
+            base = (np.arange(B) * S_l * P)[None, :, None, None] + (np.arange(Na_l) * P)[None, None, :, None]
+            sel = base + psi + idx                                        # [depth, B, Na_l, rank]
+            spec = np.broadcast_to(base + np.arange(psi)[None, None, None, :], (self.depth, B, Na_l, psi))
+            rowmap = np.concatenate([spec, sel], axis=-1).reshape(self.depth, B, Na_l * Pp).astype(np.int32)
+            rowmap_t = runtime.to_device(torch.from_numpy(rowmap), dev)
         rope = self.rope.tables(C // nh, max(gh, gw) + 1, dev) if self.rope is not None else None
         posctx = dict(tokens_per_frame=P, patch_start=psi, grid_w=gw)
 
-        # ---- outputs
+        # ---- outputs (this rank's query frames)
         out_maps: Dict[int, torch.Tensor] = {}
         if Nq > 0:
             for l in self.intermediate_layer_idx:
-                out_maps[l] = torch.empty(B, Nq, P, 2 * C, device=dev, dtype=torch.float32)
-        cam_last = torch.empty(B, Na, 2 * C, device=dev, dtype=torch.float32)
-        anchor_rows0 = torch.tensor([b * S * P + a * P for b in range(B) for a in range(Na)],
-                                    dtype=torch.int32).to(dev, non_blocking=True)
-        cam_flat = cam_last.view(B * Na, 2 * C)
+                out_maps[l] = torch.empty(B, Nq_l, P, 2 * C, device=dev, dtype=torch.float32)
+        cam_loc = torch.empty(B, Na_l, 2 * C, device=dev, dtype=torch.float32)
+        anchor_rows0 = runtime.to_device(
+            torch.tensor([b * S_l * P + a * P for b in range(B) for a in range(Na_l)], dtype=torch.int32), dev)
+        cam_flat = cam_loc.view(B * Na_l, 2 * C)
 
         # ---- alternating layers, aggregator.py:339-423
         for l in range(self.depth):
@@ -268,61 +305,116 @@ class Aggregator(nn.Module):
             runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P),
                               runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
             if l in out_maps:  # frame half of the intermediate, :403-413
-                om = out_maps[l]
                 for b in range(B):
-                    ops.copy_rows(om[b].view(Nq * P, 2 * C)[:, :C], x[b * S * P + Na * P:(b + 1) * S * P], Nq * P)
+                    ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, :C],
+                                  x[b * S_l * P + Na_l * P:(b + 1) * S_l * P], Nq_l * P)
             if l == self.depth - 1:  # :414-423 frame half
-                ops.copy_rows(cam_flat[:, :C], x, B * Na, rowmap=anchor_rows0)
+                ops.copy_rows(cam_flat[:, :C], x, B * Na_l, rowmap=anchor_rows0)
             pr = self.global_reloc_blocks[l].packed(dtype)
             pg = self.global_blocks[l].packed(dtype)
             for b in range(B):
-                a0, q0, q1 = b * S * P, b * S * P + Na * P, (b + 1) * S * P
-                if Nq > 0:
-                    self._reloc_block(pr, x, sc, rowmap_t[l, b], Na * Pp, q0, q1, Nq, P, rope, posctx, dtype, dev)
-                self._global_block(pg, x, sc, a0, q0, rope, posctx)
-            if l in out_maps:  # reloc half, :403-413
-                om = out_maps[l]
+                a0, q0, q1 = b * S_l * P, b * S_l * P + Na_l * P, (b + 1) * S_l * P
+                self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if Nq > 0 else None, Na_l * Pp, a0, q0, q1,
+                                   Nq_l, P, rope, posctx, dtype, dev, group, G, r)
+            if l in out_maps:  # reloc half
                 for b in range(B):
-                    ops.copy_rows(om[b].view(Nq * P, 2 * C)[:, C:], x[b * S * P + Na * P:(b + 1) * S * P], Nq * P)
+                    ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, C:],
+                                  x[b * S_l * P + Na_l * P:(b + 1) * S_l * P], Nq_l * P)
             if l == self.depth - 1:
-                ops.copy_rows(cam_flat[:, C:], x, B * Na, rowmap=anchor_rows0)
+                ops.copy_rows(cam_flat[:, C:], x, B * Na_l, rowmap=anchor_rows0)
 
         output_dict: Dict[int, torch.Tensor] = dict(out_maps)
         assert (self.depth - 1 in output_dict) or Nq == 0, \
             f"Please make sure the last layer ({self.depth - 1}) is in the output_dict: {output_dict.keys()}"
         if Nq > 0:
             output_dict[-1] = output_dict[self.depth - 1]
+        if G > 1:
+            # camera head inputs for every frame: anchor camera tokens and query camera tokens
+            cam_last = torch.empty(B * Na, 2 * C, device=dev, dtype=torch.float32)
+            torch.distributed.all_gather_into_tensor(cam_last, cam_loc.view(B * Na_l, 2 * C), group=group)
+            cam_last = cam_last.view(B, Na, 2 * C)
+            if Nq > 0:
+                qcam = torch.empty(B * Nq, 2 * C, device=dev, dtype=torch.float32)
+                torch.distributed.all_gather_into_tensor(
+                    qcam, output_dict[-1][:, :, 0].reshape(B * Nq_l, 2 * C).contiguous(), group=group)
+                self.last_query_cam_tokens = qcam.view(B, Nq, 2 * C)
+        else:
+            cam_last = cam_loc
+            self.last_query_cam_tokens = output_dict[-1][:, :, 0] if Nq > 0 else None
         return output_dict, self.patch_start_idx, cam_last
 
     # ------------------------------------------------------------------ stacks
-    def _reloc_block(self, pb, x, sc, rowmap, n_sub, q0, q1, Nq, P, rope, posctx, dtype, dev):
-        """global_reloc Block for one batch item, aggregator.py:672-741 (query rows only)."""
+    def _layer_global(self, pr, pg, x, sc, rowmap, n_sub, a0, q0, q1, Nq_l, P, rope, posctx, dtype, dev,
+                      group, G, r):
+        """global_reloc (queries, aggregator.py:672-741) + global (anchors, :743-769) blocks of
+        one layer for one batch item.  With G > 1 the anchor K/V and the anchor-subsample K/V
+        are all-gathered (async, overlapped with the query-side QKV GEMM)."""
+        C = pg.dim
+        ws = self._ws
+        La_l = q0 - a0           # local anchor tokens
+        La = La_l * G            # all anchor tokens
+        work_sub = work_kv = None
+        if Nq_l > 0:
+            # anchor-subsample K/V (reads x before the global block updates the anchors)
+            xn_sub = ws.get("xn_sub", n_sub, C, dtype, dev)
+            if G > 1:  # separate send buffer: no aliasing between collective input and output
+                kv_sub = ws.get("kv_sub_loc", n_sub, 2 * C, dtype, dev)
+                kv_sub_all = ws.get("kv_sub", n_sub * G, 2 * C, dtype, dev)
+            else:
+                kv_sub = kv_sub_all = ws.get("kv_sub", n_sub, 2 * C, dtype, dev)
+            ops.layernorm(x, pr.ln1_w, pr.ln1_b, pr.eps, xn_sub, rowmap=rowmap, rows=n_sub)
+            self._kv_gemm(pr, xn_sub, kv_sub, rope, dict(pos_rowmap=rowmap, **posctx))
+            if G > 1:
+                work_sub = torch.distributed.all_gather_into_tensor(kv_sub_all, kv_sub, group=group, async_op=True)
+        if G > 1:
+            # global block, first half: LN1 + Q GEMM locally, K/V straight into this rank's slot
+            xs = x[a0:q0]
+            xn, qkv = sc.xn[a0:q0], sc.qkv[a0:q0]
+            kv_all = ws.get("kv_all", La, 2 * C, dtype, dev)
+            kv_loc = ws.get("kv_loc", La_l, 2 * C, dtype, dev)
+            ops.layernorm(xs, pg.ln1_w, pg.ln1_b, pg.eps, xn)
+            epi = runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx)
+            if epi is None:
+                ops.gemm(xn, pg.w_qkv[:C], qkv[:, :C], _lib.SR_EPI_BIAS, bias=_sl(pg.b_qkv, 0, C), tag="gemm")
+            else:
+                ops.gemm(xn, pg.w_qkv[:C], qkv[:, :C], _lib.SR_EPI_QKV, bias=_sl(pg.b_qkv, 0, C), qkv=epi,
+                         tag="gemm")
+            self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
+            work_kv = torch.distributed.all_gather_into_tensor(kv_all, kv_loc, group=group, async_op=True)
+        if Nq_l > 0:
+            def attend_reloc(qkv, o):
+                if work_sub is not None:
+                    work_sub.wait()
+                ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
+                              head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub * G, k0_bstride=0,
+                              k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
+            runtime.run_block(pr, x, q0, q1, sc, attend_reloc, runtime.qkv_params(pr, rope, pos_row_base=q0,
+                                                                                    **posctx))
+        if G > 1:
+            work_kv.wait()
+            o = sc.o[a0:q0]
+            ops.attention(sc.qkv[a0:q0, 0:C], kv_all[:, 0:C], kv_all[:, C:2 * C], o, heads=pg.heads,
+                          head_dim=pg.head_dim, batch=1, lq=La_l, q_bstride=0, l0=La, k0_bstride=0,
+                          tag="attn_global")
+            runtime.run_block_tail(pg, x, a0, q0, sc)
+        else:
+            def attend_global(qkv, o):
+                ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pg.heads,
+                              head_dim=pg.head_dim, batch=1, lq=La, q_bstride=0, l0=La, k0_bstride=0,
+                              tag="attn_global")
+            runtime.run_block(pg, x, a0, q0, sc, attend_global, runtime.qkv_params(pg, rope, pos_row_base=a0,
+                                                                                    **posctx))
+
+    def _kv_gemm(self, pb, xn, out, rope, pos):
+        """K/V-only projection (qkv weight rows C..3C) with k-norm + RoPE on the K half."""
         C = pb.dim
-        xn_sub = self._ws.get("xn_sub", n_sub, C, dtype, dev)
-        kv_sub = self._ws.get("kv_sub", n_sub, 2 * C, dtype, dev)
-        ops.layernorm(x, pb.ln1_w, pb.ln1_b, pb.eps, xn_sub, rowmap=rowmap, rows=n_sub)
-        epi = runtime.qkv_params(pb, rope, pos_rowmap=rowmap, **posctx)
+        epi = runtime.qkv_params(pb, rope, **pos)
         if epi is None:
-            ops.gemm(xn_sub, pb.w_qkv[C:], kv_sub, _lib.SR_EPI_BIAS, bias=pb.b_qkv[C:] if pb.b_qkv is not None else None)
+            ops.gemm(xn, pb.w_qkv[C:], out, _lib.SR_EPI_BIAS, bias=_sl(pb.b_qkv, C, 3 * C), tag="gemm")
         else:
             epi["col_offset"] = C
-            ops.gemm(xn_sub, pb.w_qkv[C:], kv_sub, _lib.SR_EPI_QKV,
-                     bias=pb.b_qkv[C:] if pb.b_qkv is not None else None, qkv=epi)
+            ops.gemm(xn, pb.w_qkv[C:], out, _lib.SR_EPI_QKV, bias=_sl(pb.b_qkv, C, 3 * C), qkv=epi, tag="gemm")
 
-        def attend(qkv, o):
-            ops.attention(qkv[:, 0:C], kv_sub[:, 0:C], kv_sub[:, C:2 * C], o, heads=pb.heads, head_dim=pb.head_dim,
-                          batch=Nq, lq=P, q_bstride=P, l0=n_sub, k0_bstride=0,
-                          k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
 
-        runtime.run_block(pb, x, q0, q1, sc, attend, runtime.qkv_params(pb, rope, pos_row_base=q0, **posctx))
-
-    def _global_block(self, pb, x, sc, a0, a1, rope, posctx):
-        """global Block over every anchor token of one batch item, aggregator.py:743-769."""
-        C = pb.dim
-        L = a1 - a0
-
-        def attend(qkv, o):
-            ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads,
-                          head_dim=pb.head_dim, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, tag="attn_global")
-
-        runtime.run_block(pb, x, a0, a1, sc, attend, runtime.qkv_params(pb, rope, pos_row_base=a0, **posctx))
+def _sl(t, a, b):
+    return None if t is None else t[a:b]

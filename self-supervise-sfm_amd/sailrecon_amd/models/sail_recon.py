@@ -45,16 +45,23 @@ class SailRecon(nn.Module):
             reloc_list = list(range(rgbs.shape[1]))
         rgb_feats, idx_patch, cam_token_last_layer = self.aggregator(rgbs, no_reloc_list, reloc_list,
                                                                      fix_rank=fix_rank)
-        reloc_rgbs = rgbs[:, reloc_list]
+        # frame-sharded aggregator (Aggregator.set_frame_sharding): this rank's query views only;
+        # the camera head runs replicated on the gathered camera tokens of every view
+        _, G, r = self.aggregator._world()
+        nq_l = len(reloc_list) // G
+        local_reloc = list(reloc_list)[r * nq_l:(r + 1) * nq_l]
+        reloc_rgbs = rgbs[:, local_reloc]
         cam_tokens = rgb_feats[-1][:, :, 0]
         predictions = {}
         with torch.autocast("cuda", enabled=False):  # heads in fp32, sail_recon.py:118-119
             if self.camera_head is not None:
-                cam_maps = self.camera_head(rgb_feats, cam_token_last_layer)
-                extrinsic, intrinsic = pose_encoding_to_extri_intri(cam_maps[-1], (rgbs.shape[-2], rgbs.shape[-1]))
+                cam_in = rgb_feats if G == 1 else [self.aggregator.last_query_cam_tokens[:, :, None]]
+                cam_maps = self.camera_head(cam_in, cam_token_last_layer)
+                pose = cam_maps[-1][:, r * nq_l:(r + 1) * nq_l]
+                extrinsic, intrinsic = pose_encoding_to_extri_intri(pose.contiguous(), (rgbs.shape[-2], rgbs.shape[-1]))
                 predictions["extrinsic"] = extrinsic
                 predictions["intrinsic"] = intrinsic
-                predictions["pose_enc"] = cam_maps[-1]
+                predictions["pose_enc"] = pose
             if self.point_head is not None:
                 xyz_map, xyz_cnf = self.point_head(rgb_feats, images=reloc_rgbs, patch_start_idx=idx_patch)
                 predictions["point_map"] = xyz_map
@@ -71,8 +78,8 @@ class SailRecon(nn.Module):
         predictions["rgbs"] = reloc_rgbs
         predictions["cam_tokens"] = cam_tokens
         predictions["images"] = reloc_rgbs
-        final_results = [{} for _ in range(len(reloc_list))]
+        final_results = [{} for _ in range(len(local_reloc))]
         for key, value in predictions.items():
-            for i in range(len(reloc_list)):
+            for i in range(len(local_reloc)):
                 final_results[i][key] = value[:, i]
         return final_results

@@ -25,6 +25,19 @@ from . import _lib, ops
 Tensor = torch.Tensor
 
 
+def require_device(t: Tensor, who: str) -> None:
+    """The product path runs only through libsfm_amd.so on a ROCm device: fail loudly."""
+    if not t.is_cuda:
+        raise RuntimeError(f"sailrecon_amd {who} runs on the HIP path only (tensors must be on a ROCm device)")
+
+
+def to_device(t: Tensor, device) -> Tensor:
+    """Small host->device copy (pinned, async) for index tables."""
+    if torch.device(device).type == "cuda":
+        return t.pin_memory().to(device, non_blocking=True)
+    return t.to(device)
+
+
 def compute_dtype(explicit: Optional[torch.dtype] = None) -> torch.dtype:
     """bf16 when the caller runs under autocast (demo_imc_forward.py:93), else fp32 parity mode."""
     if explicit is not None:
@@ -147,6 +160,18 @@ def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
     else:
         ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
     attend(qkv, o)
+    ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
+    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
+    ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
+    ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2,
+             tag="gemm")
+
+
+def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch) -> None:
+    """Second half of run_block (proj + residual, LN2, MLP + residual) when the attention
+    output sc.o[r0:r1] was produced separately (frame-sharded global block)."""
+    xs = x[r0:r1]
+    xn, o, h = sc.xn[r0:r1], sc.o[r0:r1], sc.h[r0:r1]
     ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
     ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
     ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")

@@ -1,0 +1,177 @@
+"""TEST-ONLY torch (CPU) implementation of the sailrecon_amd.ops API (= the C-ABI
+semantics of include/sfm_amd.h), used to exercise the HOST orchestration of the
+framework — row maps, subsample indices, token positions, frame sharding and the
+RCCL/gloo collectives — on a machine without a GPU.
+
+It is installed only by tests (``installed()`` context manager); the product path
+never imports it and keeps failing loudly without libsfm_amd.so on a ROCm device.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import math
+
+import torch
+import torch.nn.functional as F
+
+from sailrecon_amd import _lib, ops as real_ops, runtime
+
+
+def gemm(a, w, out, epi, *, bias=None, gamma=None, rows=None, qkv=None, patch=None, tag=None):
+    M = a.shape[0] if rows is None else rows
+    y = a[:M].float() @ w.float().t()
+    if bias is not None:
+        y = y + bias
+    if epi == _lib.SR_EPI_BIAS:
+        out[:M] = y.to(out.dtype)
+    elif epi == _lib.SR_EPI_BIAS_GELU:
+        out[:M] = F.gelu(y).to(out.dtype)
+    elif epi == _lib.SR_EPI_BIAS_RESID:
+        out[:M] += y * gamma
+    elif epi == _lib.SR_EPI_PATCH:
+        sr, st, so = patch["seg_rows"], patch["seg_stride"], patch["seg_offset"]
+        f = torch.arange(M) // sr
+        p = torch.arange(M) % sr
+        out[f * st + so + p] = y + patch["row_add"][p]
+    elif epi == _lib.SR_EPI_QKV:
+        C, D = qkv["embed_dim"], qkv.get("head_dim", 64)
+        off = qkv.get("col_offset", 0)
+        N = y.shape[1]
+        cols = torch.arange(N) + off
+        for h0 in range(0, N, D):
+            region = int(cols[h0]) // C
+            if region >= 2:
+                continue
+            seg = y[:, h0:h0 + D]
+            nw = qkv.get("qn_w") if region == 0 else qkv.get("kn_w")
+            nb = qkv.get("qn_b") if region == 0 else qkv.get("kn_b")
+            if nw is not None:
+                seg = F.layer_norm(seg, (D,), nw, nb, qkv.get("qk_eps", 1e-5))
+            if qkv.get("rope_cos") is not None:
+                py, px = _positions(qkv, M)
+                cos, sin = qkv["rope_cos"], qkv["rope_sin"]
+                q = D // 4
+
+                def rot(v, pos):
+                    c, s = cos[pos], sin[pos]
+                    v1, v2 = v[:, :q], v[:, q:]
+                    return torch.cat([v1 * c - v2 * s, v2 * c + v1 * s], 1)
+                seg = torch.cat([rot(seg[:, :2 * q], py), rot(seg[:, 2 * q:], px)], 1)
+            y[:, h0:h0 + D] = seg
+        out[:M] = y.to(out.dtype)
+    else:
+        raise ValueError(epi)
+
+
+def _positions(qkv, M):
+    if qkv.get("pos_yx") is not None:
+        p = qkv["pos_yx"].long()
+        return p[:, 0], p[:, 1]
+    rm = qkv.get("pos_rowmap")
+    tr = rm.long()[:M] if rm is not None else qkv.get("pos_row_base", 0) + torch.arange(M)
+    t = tr % qkv["tokens_per_frame"]
+    ps, gw = qkv["patch_start"], qkv["grid_w"]
+    p = (t - ps).clamp_min(0)
+    special = t < ps
+    py = torch.where(special, 0, p // gw + 1)
+    px = torch.where(special, 0, p % gw + 1)
+    return py, px
+
+
+def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
+              k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None):
+    D = head_dim
+    scale = D ** -0.5 if scale is None else scale
+    for b in range(batch):
+        qs = q[b * q_bstride:b * q_bstride + lq].float()
+        ks = [k0[b * k0_bstride:b * k0_bstride + l0].float()]
+        vs = [v0[b * k0_bstride:b * k0_bstride + l0].float()]
+        if l1 > 0:
+            ks.append(k1[b * k1_bstride:b * k1_bstride + l1].float())
+            vs.append(v1[b * k1_bstride:b * k1_bstride + l1].float())
+        kk, vv = torch.cat(ks), torch.cat(vs)
+        for h in range(heads):
+            sl = slice(h * D, (h + 1) * D)
+            s = (qs[:, sl] @ kk[:, sl].t()) * scale
+            if mask_mode == _lib.SR_MASK_CAMERA:
+                i = torch.arange(lq)[:, None]
+                j = torch.arange(kk.shape[0])[None]
+                s = s.masked_fill(~((j < n_anchor) | (j == i)), float("-inf"))
+            o[b * q_bstride:b * q_bstride + lq, sl] = (torch.softmax(s, -1) @ vv[:, sl]).to(o.dtype)
+
+
+def layernorm(x, w, b, eps, out, rowmap=None, rows=None):
+    n = out.shape[0] if rows is None else rows
+    src = x[rowmap.long()[:n]] if rowmap is not None else x[:n]
+    out[:n] = F.layer_norm(src, (x.shape[1],), w, b, eps).to(out.dtype)
+
+
+def im2col_normalize(img, patch, out, kpad):
+    mean = torch.tensor(real_ops._MEAN).view(1, 3, 1, 1)
+    std = torch.tensor(real_ops._STD).view(1, 3, 1, 1)
+    u = F.unfold((img - mean) / std, patch, stride=patch).transpose(1, 2).reshape(-1, 3 * patch * patch)
+    out.zero_()
+    out[:, :u.shape[1]] = u.to(out.dtype)
+
+
+def set_special_tokens(x, frames, tokens_per_frame, table, type_of_frame):
+    n = table.shape[1]
+    xv = x.view(frames, tokens_per_frame, -1)
+    xv[:, :n] = table[type_of_frame.reshape(-1).long()]
+
+
+def copy_rows(dst, src, rows, rowmap=None):
+    dst[:rows] = src[rowmap.long()[:rows]] if rowmap is not None else src[:rows]
+
+
+def linear_small(a, w, bias, out, rows, act_in=0, lda=None):
+    A = a.reshape(-1, w.shape[1])
+    if lda == 0:
+        A = A[:1].expand(rows, -1)
+    A = A[:rows]
+    if act_in:
+        A = F.silu(A)
+    out[:rows] = A @ w.t() + (bias if bias is not None else 0)
+
+
+def silu(x, y):
+    y.copy_(F.silu(x))
+
+
+def adaln_modulate(xn, x, mod, out):
+    sh, sc, g = mod.chunk(3, -1)
+    out.copy_(g * (xn * (1 + sc) + sh) + x)
+
+
+def pose_update(pred, delta, act, first):
+    pred.copy_(delta if first else pred + delta)
+    act.copy_(torch.cat([pred[:, :7], F.relu(pred[:, 7:])], -1))
+
+
+def pose_decode(enc, hw, ext, intr):
+    from oracle.sfm_oracle import pose_encoding_to_extri_intri
+    e, i = pose_encoding_to_extri_intri(enc[None], hw)
+    ext.copy_(e[0])
+    intr.copy_(i[0])
+
+
+_NAMES = ["gemm", "attention", "layernorm", "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
+          "silu", "adaln_modulate", "pose_update", "pose_decode"]
+
+
+@contextlib.contextmanager
+def installed():
+    """Route sailrecon_amd.ops through this module and allow CPU tensors."""
+    saved = {n: getattr(real_ops, n) for n in _NAMES}
+    saved_req = runtime.require_device
+    g = globals()
+    try:
+        for n in _NAMES:
+            setattr(real_ops, n, g[n])
+        runtime.require_device = lambda t, who: None
+        yield
+    finally:
+        for n, f in saved.items():
+            setattr(real_ops, n, f)
+        runtime.require_device = saved_req
