@@ -42,6 +42,26 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip t
 PEAK_F32_TFLOPS = 157.3    # f32 MFMA
 PEAK_HBM_GBS = 8000.0
 
+# timer class -> the kernel instantiation it launches at the N=32@518 workload
+# (rocprofv3 row names; see DESIGN.md "Kernels").
+KERNEL_OF_TAG = {
+    "attn_global": "attn_bf16_kernel<4, 2>", "attn_reloc": "attn_bf16_kernel<4, 1>",
+    "attn_frame": "attn_bf16_kernel<4, 0>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
+    "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
+}
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), or None."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            k = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if k is None else k["traffic_bytes"]
+
 
 def algorithmic_tflop(n_views: int, img: int, C: int = 1024) -> float:
     """Required work per forward, SURVEY §8(d) closed form (TFLOP)."""
@@ -156,12 +176,21 @@ def main():
         dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
         b = breakdown[dom]
         achieved = b["tflops"]
-        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+        kern = KERNEL_OF_TAG.get(dom) if use_bf16 else None
+        traffic = pmc_traffic(kern) if kern else None
+        roofline = {"bound": "mfma", "kernel": kern or dom, "timer_class": dom, "achieved": round(achieved, 2),
+                    "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                    "traffic": None if traffic is None else round(traffic),
+                    "traffic_unit": "bytes/launch (HBM, PMC 2xFETCH_SIZE+WRITE_SIZE)",
+                    "traffic_source": os.path.relpath(TRAFFIC_FILE, REPO) if traffic is not None else None,
+                    "algorithmic_bytes": round(b["bytes_per_launch"]),
                     "avg_launch_ms": round(b["avg_ms"], 4), "flop_per_launch": b["flops_per_launch"]}
-        gem = breakdown.get("gemm")
-        if gem:
-            roofline["gemm_mfma_util"] = round(gem["tflops"] / peak, 4)
+        gems = [v for k, v in breakdown.items() if k.startswith("gemm_")]
+        if gems:
+            flop = sum(v["flops_per_launch"] * v["launches"] for v in gems)
+            ms = sum(v["total_ms"] for v in gems)
+            roofline["gemm_all_tflops"] = round(flop / (ms * 1e-3) / 1e12, 1)
+            roofline["gemm_mfma_util"] = round(flop / (ms * 1e-3) / 1e12 / peak, 4)
         print(json.dumps({"kernel_breakdown": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                                                    for kk, vv in v.items()} for k, v in breakdown.items()},
                           "step_ms": dt / args.steps * 1e3}), file=sys.stderr)

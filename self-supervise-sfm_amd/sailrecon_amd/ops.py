@@ -37,25 +37,34 @@ class KernelTimer:
         ev.record()
         return ev
 
-    def stop(self, tag: str, ev0, work: float):
+    def stop(self, tag: str, ev0, work: float, nbytes: float = 0.0):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.records.setdefault(tag, []).append((ev0, ev1, work))
+        self.records.setdefault(tag, []).append((ev0, ev1, work, nbytes))
 
     def summary(self):
-        """tag -> dict(launches, total_ms, avg_ms, flops_per_launch, tflops)"""
+        """tag -> dict(launches, total_ms, avg_ms, flops_per_launch, tflops, bytes_per_launch, gbs)
+
+        ``bytes_per_launch`` is the algorithmic (compulsory) HBM traffic of a launch:
+        every operand read once, every output written once."""
         torch.cuda.synchronize()
         out = {}
         for tag, recs in self.records.items():
-            ms = [a.elapsed_time(b) for a, b, _ in recs]
-            work = sum(w for _, _, w in recs)
+            ms = [r[0].elapsed_time(r[1]) for r in recs]
+            work = sum(r[2] for r in recs)
+            nbytes = sum(r[3] for r in recs)
             tot = sum(ms)
+            sec = tot * 1e-3
             out[tag] = dict(launches=len(recs), total_ms=tot, avg_ms=tot / len(recs),
-                            flops_per_launch=work / len(recs), tflops=(work / (tot * 1e-3) / 1e12) if tot else 0.0)
+                            flops_per_launch=work / len(recs), tflops=(work / sec / 1e12) if tot else 0.0,
+                            bytes_per_launch=nbytes / len(recs), gbs=(nbytes / sec / 1e9) if tot else 0.0)
         return out
 
 
 TIMER: Optional[KernelTimer] = None
+
+_EPI_NAME = {_lib.SR_EPI_BIAS: "bias", _lib.SR_EPI_BIAS_GELU: "gelu", _lib.SR_EPI_BIAS_RESID: "resid",
+             _lib.SR_EPI_QKV: "qkv", _lib.SR_EPI_PATCH: "patch"}
 
 
 def _p(t: Optional[Tensor]):
@@ -120,13 +129,17 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         ep.seg_stride = patch["seg_stride"]
         ep.seg_offset = patch["seg_offset"]
         ep.row_add = _p(patch["row_add"])
+    if tag == "gemm":  # one timer class per kernel instantiation (matches rocprof rows)
+        tag = f"gemm_{_EPI_NAME.get(epi, epi)}" + ("" if a.dtype == torch.bfloat16 else "_f32")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
     rc = _lib.load().sr_gemm(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
                              M, N, K, ctypes.byref(ep))
     check(rc, "sr_gemm")
     if timed:
-        TIMER.stop(tag, ev0, 2.0 * M * N * K)
+        es, eo = a.element_size(), out.element_size()
+        nb = (M * K + N * K) * es + M * N * eo * (2 if epi == _lib.SR_EPI_BIAS_RESID else 1)
+        TIMER.stop(tag, ev0, 2.0 * M * N * K, nb)
 
 
 def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
@@ -153,7 +166,10 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
     check(rc, "sr_attention")
     if timed:
-        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim)
+        es = q.element_size()
+        kv_rows = (l0 if k0_bstride == 0 else batch * l0) + batch * l1  # shared segment read once
+        nb = es * heads * head_dim * (2 * batch * lq + 2 * kv_rows)
+        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim, nb)
 
 
 def layernorm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float, out: Tensor,
