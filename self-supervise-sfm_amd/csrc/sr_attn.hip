@@ -51,17 +51,24 @@ __device__ __forceinline__ float sum_x32(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// NW waves x 64 query rows per workgroup (two 32-row q-blocks per wave); KIND only names
-// the call site in profiles (0 frame, 1 global_reloc, 2 global).
+// NW waves x QB 32-row q-blocks per wave; KIND only names the call site in profiles
+// (0 frame, 1 global_reloc, 2 global).
 //
 // Tile loop (K/V ring of NBUF=4 stages, up to 3 in flight, one barrier per tile):
-//   S0 = K Q0^T, S1 = K Q1^T       (16 MFMA; each K fragment read once, used twice)
-//   row max / rescale per q-block  (lane^32 exchange by v_permlane32_swap)
-//   P = exp2(S*c - m) -> bf16; O^T += V^T P^T  (16 MFMA; each V^T fragment used twice)
-// Two workgroups per CU (<= 256 VGPRs) interleave their MFMA / VALU phases freely.
-template <int NW, int KIND>
-__global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
-  constexpr int QROWS = NW * 64;
+//   S_b = K Q_b^T                  (8 MFMA per q-block; each K fragment read once, used QB times)
+//   row max per q-block            (lane^32 exchange by v_permlane32_swap); O / l are rescaled
+//                                  only when some row max grew by more than 2^RESCALE_LOG2
+//                                  (stale maxima keep P <= 2^8: exact in fp32 sums, and bf16 P
+//                                  keeps its relative precision)
+//   P = exp2(S*c - m) -> bf16; O^T += V^T P^T  (8 MFMA per q-block)
+// Two workgroups per CU interleave their MFMA / VALU phases freely.
+constexpr float RESCALE_LOG2 = 8.f;
+#ifndef SR_ATTN_DEFAULT_CFG
+#define SR_ATTN_DEFAULT_CFG 0
+#endif
+template <int NW, int QB, int KIND>
+__global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(AttnArgs args) {
+  constexpr int QROWS = NW * 32 * QB;
   constexpr int NBUF = NW >= 4 ? 4 : 2;  // ring depth (power of 2); NBUF-1 stages in flight
   constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
@@ -76,59 +83,101 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
   // ---- staging: global DMA instruction gi = wave*DPW + i; gi < 8: K rows 8gi.., else V rows.
   // Segment pointers are copied to scalars once: selecting between kernel-argument fields
   // inside the loop compiles to vector loads whose vmcnt(0) wait would drain the ring.
-  const bool stage_v = wave * DPW >= 8;  // wave-uniform: a wave stages only K or only V
-  const bf16* const sb0 = (const bf16*)(stage_v ? d.v0 : d.k0);
-  const bf16* const sb1 = (const bf16*)(stage_v ? d.v1 : d.k1);
+  // Full tiles use a scalar base per 8-row group + a per-lane 32-bit offset (all tile-walk
+  // arithmetic on the SALU); a segment's ragged last tile clamps rows per lane.
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const bool stage_v = wave_u * DPW >= 8;  // wave-uniform: a wave stages only K or only V
+  const char* const sb0 = (const char*)(stage_v ? d.v0 : d.k0) + 2 * hcol;
+  const char* const sb1 = (const char*)(stage_v ? d.v1 : d.k1) + 2 * hcol;
   const int64_t sld0 = stage_v ? d.ldv0 : d.ldk0, sld1 = stage_v ? d.ldv1 : d.ldk1;
   const int64_t srb0 = (int64_t)item * d.k0_bstride, srb1 = (int64_t)item * d.k1_bstride;
   const int nt0 = args.ntile0, len0 = d.l0, len1 = d.l1;
+  // K rows: chunk ^ ((r>>1)&7) (conflict-free ds_read_b128 fragments); with r = 8(gi&7) + lane/8
+  // that is chunk ^ (4(gi&1) + lane/16).  V rows: chunk ^ (((r>>1)&1)<<2) = chunk ^ (((lane/16)&1)<<2)
+  // (conflict-free ds_read_b64_tr_b16: rows r, r+2 of a 4-row transposed block land in
+  // opposite 64-B halves).
+  const int lrow = lane >> 3;
+  const int chA = stage_v ? ((lane & 7) ^ (((lane >> 4) & 1) << 2)) : ((lane & 7) ^ (lane >> 4));
+  const int chB = stage_v ? chA : ((lane & 7) ^ (4 + (lane >> 4)));
+  const uint32_t voA0 = (uint32_t)((lrow * sld0 + chA * 8) * 2), voB0 = (uint32_t)((lrow * sld0 + chB * 8) * 2);
+  const uint32_t voA1 = (uint32_t)((lrow * sld1 + chA * 8) * 2), voB1 = (uint32_t)((lrow * sld1 + chB * 8) * 2);
   auto stage = [&](int t) {
     const int buf = t & (NBUF - 1);
     const bool s1 = t >= nt0;
     const int tt = s1 ? t - nt0 : t;
     const int len = s1 ? len1 : len0;
-    const bf16* base = s1 ? sb1 : sb0;
+    const char* base = s1 ? sb1 : sb0;
     const int64_t ld = s1 ? sld1 : sld0;
     const int64_t rbase = s1 ? srb1 : srb0;
+    const uint32_t ldsb = lds0 + buf * STAGE_B + (stage_v ? TILE_B : 0);
+    if ((tt + 1) * KT <= len) {
+      const uint32_t va = s1 ? voA1 : voA0, vb = s1 ? voB1 : voB0;
 #pragma unroll
-    for (int i = 0; i < DPW; ++i) {
-      const int gi = wave * DPW + i;
-      const int r = (gi & 7) * 8 + (lane >> 3);  // key row inside the tile
-      const int key = min(tt * KT + r, len - 1);
-      // K rows: chunk ^ ((r>>1)&7) (conflict-free ds_read_b128 fragments);
-      // V rows: chunk ^ (((r>>1)&1)<<2) (conflict-free ds_read_b64_tr_b16: rows r, r+2 of a
-      // 4-row transposed block land in opposite 64-B halves)
-      const int chunk = (lane & 7) ^ (stage_v ? (((r >> 1) & 1) << 2) : ((r >> 1) & 7));
-      const uint32_t dst =
-          __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_B + (stage_v ? TILE_B : 0) + (gi & 7) * 1024);
-      sr::dma16(base + (rbase + key) * ld + hcol + chunk * 8, dst);
+      for (int i = 0; i < DPW; ++i) {
+        const int gi = wave_u * DPW + i;
+        sr::dma16_s(base + (rbase + tt * KT + (gi & 7) * 8) * ld * 2, (gi & 1) ? vb : va, ldsb + (gi & 7) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < DPW; ++i) {
+        const int gi = wave_u * DPW + i;
+        const int r = (gi & 7) * 8 + lrow;  // key row inside the tile
+        const int key = min(tt * KT + r, len - 1);
+        sr::dma16(base + ((rbase + key) * ld + ((gi & 1) ? chB : chA) * 8) * 2, ldsb + (gi & 7) * 1024);
+      }
     }
   };
 #pragma unroll
   for (int i = 0; i < NBUF - 1; ++i)
     if (i < ntiles) stage(i);
 
-  // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row][16s + 8hi .. +8]
-  const int qrow0 = qt * QROWS + wave * 64 + l32;  // q-block b: row qrow0 + 32b
-  bf16x8 qf[2][4];
+  // ---- Q fragments (B operand of S^T = K Q^T): lane holds c*Q[row][16s + 8hi .. +8], with
+  // c = scale*log2(e) folded in so that the MFMA chain yields scores in the exp2 domain
+  const float c = d.scale * 1.4426950408889634f;
+  const int qrow0 = qt * QROWS + wave * 32 * QB + l32;  // q-block b: row qrow0 + 32b
+  bf16x8 qf[QB][4];
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < QB; ++b) {
     const int qr = min(qrow0 + 32 * b, d.lq - 1);
     const bf16* qp = (const bf16*)d.q + (item * d.q_bstride + qr) * d.ldq + hcol + 8 * hi;
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[b][s] = *(const bf16x8*)(qp + 16 * s);
   }
-
-  const float c = d.scale * 1.4426950408889634f;  // scale * log2(e)
-  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};  // l_run: this lane's partial row sums
-  f32x16 o[2][2];
+  // Retire the Q loads (and the prologue stages) with a wait the compiler sees: otherwise its
+  // scoreboard carries the Q loads into the loop and places vmcnt waits before the first
+  // MFMAs of every tile, which (counting the asm-issued DMAs too) drain the K/V ring.
+  __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
+  for (int b = 0; b < QB; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[b][s][j] = (bf16)((float)qf[b][s][j] * c);
+
+  // Running row max m (exp2 domain) enters the MFMA chain as one extra k-step:
+  //   S'[key][q] = sum_k K[key][k] (cQ)[q][k] + 1 * (-m_hi[q]) + 1 * (-m_lo[q])
+  // (A = ones in k-slots 0,1 of the hi=0 lanes; B = -m split into two bf16 parts), so that
+  // P = exp2(S') needs no per-score subtraction.  m is kept as exactly hi + lo, and every
+  // rescale factor is computed from those same values, so the split rounds nothing that
+  // does not cancel in O / l.
+  bf16x8 one_a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) one_a[j] = (bf16)((hi == 0 && j < 2) ? 1.f : 0.f);
+  float m_run[QB], l_run[QB];  // m_run == float(m_hi) + float(m_lo); l_run: this lane's partial sums
+  bf16x8 m_b[QB];
+  f32x16 o[QB][2];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    m_run[b] = 0.f;
+    l_run[b] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m_b[b][j] = (bf16)0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       o[b][0][i] = 0.f;
       o[b][1][i] = 0.f;
     }
+  }
   // K fragment: row kb*32 + l32, chunk (2s + hi) ^ kswz
   const int kswz = (l32 >> 1) & 7;
   int koff[4];
@@ -154,21 +203,20 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
     const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
     const char* vt_lds = kt_lds + TILE_B;
 
-    // ---- S^T = K Q^T for both q-blocks (2 blocks of 32 keys each)
-    f32x16 sc[2][2];  // [q-block][key block]
+    // ---- S'^T = K (cQ)^T - m for every q-block (2 blocks of 32 keys each)
+    f32x16 sc[QB][2];  // [q-block][key block]
+    const f32x16 zero = {};
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[b][kb][i] = 0.f;
+      for (int kb = 0; kb < 2; ++kb) sc[b][kb] = mfma32(one_a, m_b[b], zero);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const bf16x8 kf = *(const bf16x8*)(kt_lds + kb * 4096 + koff[s]);
-        sc[0][kb] = mfma32(kf, qf[0][s], sc[0][kb]);
-        sc[1][kb] = mfma32(kf, qf[1][s], sc[1][kb]);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) sc[b][kb] = mfma32(kf, qf[b][s], sc[b][kb]);
       }
 
     // ---- mask the ragged tail of a segment
@@ -176,7 +224,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
     const int valid = (s1 ? len1 : len0) - (s1 ? t - nt0 : t) * KT;
     if (valid < KT) {
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < QB; ++b)
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -186,44 +234,61 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
           }
     }
 
-    // ---- row max per q-block; rescale O / l when it grew
-    float m_new[2];
+    // ---- tile max of S' per row; rescale when a row max grew past the threshold (always on
+    // the first tile, which sets m from 0)
+    float mx[QB];
+    bool grow = t == 0;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < QB; ++b) {
       float t8[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         t8[i] = fmaxf(fmaxf(sc[b][0][i], sc[b][0][i + 8]), fmaxf(sc[b][1][i], sc[b][1][i + 8]));
 #pragma unroll
       for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
-      m_new[b] = fmaxf(m_run[b], max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3]))) * c);
+      mx[b] = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
+      grow |= mx[b] > RESCALE_LOG2;
     }
-    if (__any((m_new[0] > m_run[0]) | (m_new[1] > m_run[1]))) {
+    if (__any(grow)) {
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const float alpha = __builtin_amdgcn_exp2f(m_run[b] - m_new[b]);
+      for (int b = 0; b < QB; ++b) {
+        // new max (rows that did not grow keep theirs), split into bf16 hi + lo
+        const float target = t == 0 ? mx[b] : m_run[b] + fmaxf(mx[b], 0.f);
+        const bf16 nhi = (bf16)target;
+        const bf16 nlo = (bf16)(target - (float)nhi);
+        const float m_new = (float)nhi + (float)nlo;
+        const float delta = m_new - m_run[b];  // S' relative to the new max: S' - delta
+        const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
         l_run[b] *= alpha;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           o[b][0][i] *= alpha;
           o[b][1][i] *= alpha;
+          sc[b][0][i] -= delta;
+          sc[b][1][i] -= delta;
         }
-        m_run[b] = m_new[b];
+        m_run[b] = m_new;
+        if (hi == 0) {
+          m_b[b][0] = -nhi;
+          m_b[b][1] = -nlo;
+        }
       }
     }
 
-    // ---- P = exp2(S*c - m) (B operand), O^T += V^T P^T; each V^T fragment feeds both q-blocks
-    float ps[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    // ---- P = exp2(S') (B operand), O^T += V^T P^T; each V^T fragment feeds every q-block
+    float ps[QB][2];
+#pragma unroll
+    for (int b = 0; b < QB; ++b) ps[b][0] = ps[b][1] = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf[2];
+        bf16x8 pf[QB];
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < QB; ++b)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(sc[b][kb][8 * s2 + j], c, -m_run[b]));
+            const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
             ps[b][j & 1] += p;
             pf[b][j] = (bf16)p;
           }
@@ -236,17 +301,17 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bf16_kernel(AttnArgs args) {
               __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
           const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
           const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
-          o[0][db] = mfma32(vf, pf[0], o[0][db]);
-          o[1][db] = mfma32(vf, pf[1], o[1][db]);
+#pragma unroll
+          for (int b = 0; b < QB; ++b) o[b][db] = mfma32(vf, pf[b], o[b][db]);
         }
       }
-    l_run[0] += ps[0][0] + ps[0][1];
-    l_run[1] += ps[1][0] + ps[1][1];
+#pragma unroll
+    for (int b = 0; b < QB; ++b) l_run[b] += ps[b][0] + ps[b][1];
   }
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < QB; ++b) {
     const float inv = 1.f / sum_x32(l_run[b]);
     const int qrow = qrow0 + 32 * b;
     if (qrow < d.lq) {
@@ -359,27 +424,29 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
     const int kind = d.l1 > 0 ? 1 : (d.batch == 1 && d.lq >= 4096 ? 2 : 0);
-    // 4 waves x 64 rows = 256-row query tiles (measured fastest for the frame, reloc and global
-    // stacks at N=32); 2-wave 128-row tiles when 256-row tiles would leave CUs idle (fewer than
-    // 2 workgroups per CU, e.g. the per-rank query slice of a frame-sharded global block).
-    // SR_ATTN_WAVES=2|4 overrides (tuning experiments).
-    static const int force_nw = [] {
-      const char* e = getenv("SR_ATTN_WAVES");
-      return e ? atoi(e) : 0;
+    // Workgroup shapes (waves x 32-row q-blocks per wave):
+    //   0: 4 x 2 = 256 rows    1: 8 x 1 = 256 rows    2: 2 x 2 = 128 rows
+    // 256-row tiles unless they would leave CUs idle (fewer than 2 workgroups per CU, e.g. the
+    // per-rank query slice of a frame-sharded global block).  SR_ATTN_CFG=0|1|2 overrides
+    // (tuning experiments).
+    static const int force_cfg = [] {
+      const char* e = getenv("SR_ATTN_CFG");
+      return e ? atoi(e) : -1;
     }();
     const long wgs256 = (long)((d.lq + 255) / 256) * d.heads * d.batch;
-    const bool wide = force_nw ? force_nw == 4 : wgs256 >= 512;
-    if (wide) {
-      dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
-      if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), grid, dim3(256), 0, s, a);
-      else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<4, 1>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((attn_bf16_kernel<4, 0>), grid, dim3(256), 0, s, a);
-    } else {
-      dim3 grid((d.lq + 127) / 128, d.heads, d.batch);
-      if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<2, 2>), grid, dim3(128), 0, s, a);
-      else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<2, 1>), grid, dim3(128), 0, s, a);
-      else hipLaunchKernelGGL((attn_bf16_kernel<2, 0>), grid, dim3(128), 0, s, a);
-    }
+    const int cfg = force_cfg >= 0 ? force_cfg : (wgs256 >= 512 ? SR_ATTN_DEFAULT_CFG : 2);
+    const int rows = cfg == 2 ? 128 : 256;
+    dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
+#define SR_ATTN_LAUNCH(NW_, QB_)                                                                          \
+  do {                                                                                                  \
+    if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 2>), grid, dim3(NW_ * 64), 0, s, a);  \
+    else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 1>), grid, dim3(NW_ * 64), 0, s, a); \
+    else hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 0>), grid, dim3(NW_ * 64), 0, s, a);            \
+  } while (0)
+    if (cfg == 1) SR_ATTN_LAUNCH(8, 1);
+    else if (cfg == 2) SR_ATTN_LAUNCH(2, 2);
+    else SR_ATTN_LAUNCH(4, 2);
+#undef SR_ATTN_LAUNCH
     return sr::check_launch("sr_attention(bf16)");
   }
   SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attention: bad dtype %d", dtype);

@@ -66,6 +66,12 @@ __device__ __forceinline__ void dma16(const void* gptr, uint32_t lds_base) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_base)
                : "memory", "m0");
 }
+// Same with a wave-uniform 64-bit base (SGPR pair) + per-lane 32-bit byte offset: the
+// address arithmetic of a tile walk stays on the scalar unit.
+__device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base)
+               : "memory", "m0");
+}
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks that share an XCD (same b % 8) get a contiguous range of logical tiles.

@@ -15,7 +15,7 @@ import os
 import torch  # noqa: F401  (must load the HIP runtime before the library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsfm_amd.so")
+LIB_PATH = os.environ.get("SFM_AMD_LIB") or os.path.join(_HERE, "libsfm_amd.so")  # override: tuning builds
 
 SR_F32, SR_BF16 = 0, 1
 SR_EPI_BIAS, SR_EPI_BIAS_GELU, SR_EPI_BIAS_RESID, SR_EPI_QKV, SR_EPI_PATCH = 0, 1, 2, 3, 4

@@ -208,6 +208,44 @@ def test_attention_global_long(ops):
     assert rel(o.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("case", ["frame", "global", "reloc"])
+def test_attention_wide_tiles(ops, case):
+    """shapes with >= 512 256-row workgroups select the production 256-row tiles (the small
+    tests above run the 128-row fallback); bf16, ragged tails."""
+    H, D = 16, 64
+    C = H * D
+    if case == "frame":
+        B, P = 64, 261
+        qkv = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
+        o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=B, lq=P,
+                      q_bstride=P, l0=P, k0_bstride=P)
+        t = qkv.float().view(B, P, 3, H, D).permute(2, 0, 3, 1, 4)
+        ref = _attn_ref(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(B * P, C)
+    elif case == "global":
+        L_ = 8100
+        qkv = torch.randn(L_, 3 * C, device=DEV).bfloat16()
+        o = torch.empty(L_, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=1, lq=L_,
+                      q_bstride=0, l0=L_, k0_bstride=0)
+        t = qkv.float().view(L_, 3, H, D).permute(1, 2, 0, 3)
+        ref = torch.cat([_attn_ref(t[0][h:h + 1], t[1][h:h + 1], t[2][h:h + 1], D ** -0.5) for h in range(H)])
+        ref = ref.transpose(0, 1).reshape(L_, C)
+    else:
+        Nq, P, nsub = 64, 130, 300
+        qkv = torch.randn(Nq * P, 3 * C, device=DEV).bfloat16()
+        kv = torch.randn(nsub, 2 * C, device=DEV).bfloat16()
+        o = torch.empty(Nq * P, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], o, heads=H, head_dim=D, batch=Nq, lq=P, q_bstride=P,
+                      l0=nsub, k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P)
+        t = qkv.float().view(Nq, P, 3, H, D).permute(2, 0, 3, 1, 4)        # [3, Nq, H, P, D]
+        ks = kv[:, :C].float().view(nsub, H, D).transpose(0, 1)[None].expand(Nq, H, nsub, D)
+        vs = kv[:, C:].float().view(nsub, H, D).transpose(0, 1)[None].expand(Nq, H, nsub, D)
+        ref = _attn_ref(t[0], torch.cat([ks, t[1]], 2), torch.cat([vs, t[2]], 2), D ** -0.5)
+        ref = ref.permute(0, 2, 1, 3).reshape(Nq * P, C)
+    assert rel(o.float(), ref) < 1e-2
+
+
 def test_attention_softmax_spike(ops):
     """force the online-softmax rescale branch late in the key sweep (rule 26)."""
     H, D, L_ = 1, 64, 700

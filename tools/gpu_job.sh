@@ -25,6 +25,9 @@ for step in "$@"; do
     kernels) run kernels 600 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu ;;
     parity)  run parity 900 python -m pytest tests/test_parity_gpu.py -x -q -m gpu ;;
     gputests) run gputests 1200 python -m pytest tests -x -q -m gpu ;;
+    attn_tests) run attn_tests 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k attention ;;
+    attn_tests1) run attn_tests1 300 env SR_ATTN_CFG=1 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k attention ;;
+    kattn_cfg1) run kattn_cfg1 300 env SR_ATTN_CFG=1 python tools/kbench.py attn ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py ;;
     benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
