@@ -52,6 +52,29 @@ def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
     assert rel(out.float(), F.gelu(ref)) < tol
 
 
+@pytest.mark.parametrize("M,N,K", [(8300, 4096, 128), (33000, 1024, 192), (32769, 1024, 64)])
+def test_gemm256_persistent(ops, M, N, K):
+    """>= 512 256x256 tiles select the persistent 256x256 bf16 kernel (the production path):
+    ragged last M tile (including slabs that start past row M-1), every bf16 epilogue that
+    runs on it at this width."""
+    L = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV, torch.bfloat16)
+    b, gam = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+    ref = a.float() @ w.float().t() + b
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(a, w, out, L.SR_EPI_BIAS, bias=b)
+    assert rel(out.float(), ref) < 8e-3
+    ops.gemm(a, w, out, L.SR_EPI_BIAS_GELU, bias=b)
+    assert rel(out.float(), F.gelu(ref)) < 8e-3
+    x = torch.randn(M + 64, N, device=DEV)
+    x0 = x.clone()
+    ops.gemm(a, w, x[32:32 + M], L.SR_EPI_BIAS_RESID, bias=b, gamma=gam)
+    assert torch.equal(x[:32], x0[:32]) and torch.equal(x[32 + M:], x0[32 + M:])
+    assert rel(x[32:32 + M] - x0[32:32 + M], ref * gam) < 1e-5
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-5)])
 @pytest.mark.parametrize("M", [517, 3000])
 def test_gemm_resid_strided(ops, dtype, tol, M):
