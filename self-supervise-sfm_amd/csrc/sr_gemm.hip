@@ -37,6 +37,7 @@ struct GemmArgs {
   void* out;
   int64_t ldo;
   int M, N, K, ktiles;
+  int lds_epi;  // 256x256 kernels: stage the epilogue through LDS (outputs 16-B aligned rows)
   sr_gemm_epi ep;
 };
 
@@ -63,12 +64,15 @@ template <> struct Mma<float> {
 
 // Fused epilogue on C^T accumulator tiles: acc[mi][ni] covers output rows
 // rowbase + mi*16 + lr and the 4 consecutive columns colw + ni*16 + 4*lg + r.
-template <typename T, int EPI, int MT>
-__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
-                                         int lg) {
-  // acc[mi][ni] holds the C^T 16x16 tile (W rows as the MFMA A operand): lane owns output
-  // row  m0 + wr*64 + mi*16 + lr  and the 4 CONSECUTIVE columns  colw + ni*16 + 4*lg + r,
-  // so every store / residual update is one 8-B (bf16) or 16-B (fp32) vector access.
+// Final per-lane values of every epilogue but PATCH, handed to emit(row, col, v[4]):
+//   BIAS acc + bias;  GELU gelu(acc + bias);  RESID gamma * (acc + bias) (the sink adds it to x);
+//   QKV  rope(qk_norm(acc + bias)) on the Q / K column blocks, acc + bias on V.
+// acc[mi][ni] holds the C^T 16x16 tile (W rows as the MFMA A operand): lane owns output
+// row  rowbase + mi*16 + lr  and the 4 CONSECUTIVE columns  colw + ni*16 + 4*lg + r.
+// Rows >= M are emitted too; the sink drops them.
+template <typename T, int EPI, int MT, typename Emit>
+__device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
+                                        int lg, Emit&& emit) {
   const sr_gemm_epi& ep = g.ep;
   float4 bias[4];
 #pragma unroll
@@ -80,21 +84,12 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
     v[2] = acc[mi][ni][2] + bias[ni].z;
     v[3] = acc[mi][ni][3] + bias[ni].w;
   };
-  auto store4 = [&](T* p, const float (&v)[4]) {
-    if constexpr (sr::is_bf16<T>::value) {
-      bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      *(bf16x4*)p = o;
-    } else {
-      *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  };
 
   if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
-    T* out = (T*)g.out;
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int row = rowbase + mi * 16 + lr;
-      if (row < g.M) {
+      {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           float v[4];
@@ -106,55 +101,31 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
               else v[r] = sr::gelu_erf(v[r]);  // fp32 parity mode: exact erff
             }
           }
-          store4(out + (int64_t)row * g.ldo + colw + ni * 16 + 4 * lg, v);
+          emit(row, colw + ni * 16 + 4 * lg, v);
         }
       }
     }
   } else if constexpr (EPI == SR_EPI_BIAS_RESID) {
-    float* x = (float*)g.out;
     float4 gam[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) gam[ni] = *(const float4*)(ep.gamma + colw + ni * 16 + 4 * lg);
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int row = rowbase + mi * 16 + lr;
-      if (row < g.M) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          float v[4];
-          biased(mi, ni, v);
-          float4* p = (float4*)(x + (int64_t)row * g.ldo + colw + ni * 16 + 4 * lg);
-          float4 xv = *p;
-          xv.x += v[0] * gam[ni].x;
-          xv.y += v[1] * gam[ni].y;
-          xv.z += v[2] * gam[ni].z;
-          xv.w += v[3] * gam[ni].w;
-          *p = xv;
-        }
-      }
-    }
-  } else if constexpr (EPI == SR_EPI_PATCH) {
-    float* x = (float*)g.out;
-#pragma unroll
-    for (int mi = 0; mi < MT; ++mi) {
-      const int row = rowbase + mi * 16 + lr;
-      if (row < g.M) {
-        const int f = row / ep.seg_rows, p = row - f * ep.seg_rows;
-        const int64_t orow = (int64_t)f * ep.seg_stride + ep.seg_offset + p;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int col = colw + ni * 16 + 4 * lg;
-          float v[4];
-          biased(mi, ni, v);
-          const float4 ra = *(const float4*)(ep.row_add + (int64_t)p * g.N + col);
-          *(float4*)(x + orow * g.ldo + col) = make_float4(v[0] + ra.x, v[1] + ra.y, v[2] + ra.z, v[3] + ra.w);
-        }
+      for (int ni = 0; ni < 4; ++ni) {
+        float v[4];
+        biased(mi, ni, v);
+        v[0] *= gam[ni].x;
+        v[1] *= gam[ni].y;
+        v[2] *= gam[ni].z;
+        v[3] *= gam[ni].w;
+        emit(row, colw + ni * 16 + 4 * lg, v);
       }
     }
   } else if constexpr (EPI == SR_EPI_QKV) {
     // the wave's 64 columns are exactly one head: for one output row the 64 values sit in
     // the 4 lanes lr, lr+16, lr+32, lr+48 (16 each: ni x r).  head dim d = 16 ni + 4 lg + r.
-    T* out = (T*)g.out;
     const int region = (colw + ep.col_offset) / ep.embed_dim;  // 0 = Q, 1 = K, 2 = V
     const bool qk = region < 2;
     const float* nw = region == 0 ? ep.qn_w : ep.kn_w;
@@ -230,10 +201,124 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
           v[3][r] = x1;
         }
       }
-      if (row < g.M) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) store4(out + (int64_t)row * g.ldo + colw + ni * 16 + 4 * lg, v[ni]);
+      for (int ni = 0; ni < 4; ++ni) emit(row, colw + ni * 16 + 4 * lg, v[ni]);
+    }
+  }
+}
+
+// Register epilogue: every lane stores its own 4-column vectors (8 B bf16 / 16 B fp32).
+template <typename T, int EPI, int MT>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
+                                         int lg) {
+  const sr_gemm_epi& ep = g.ep;
+  if constexpr (EPI == SR_EPI_PATCH) {
+    float4 bias[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      bias[ni] = ep.bias ? *(const float4*)(ep.bias + colw + ni * 16 + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto biased = [&](int mi, int ni, float (&v)[4]) {
+      v[0] = acc[mi][ni][0] + bias[ni].x;
+      v[1] = acc[mi][ni][1] + bias[ni].y;
+      v[2] = acc[mi][ni][2] + bias[ni].z;
+      v[3] = acc[mi][ni][3] + bias[ni].w;
+    };
+    float* x = (float*)g.out;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int row = rowbase + mi * 16 + lr;
+      if (row < g.M) {
+        const int f = row / ep.seg_rows, p = row - f * ep.seg_rows;
+        const int64_t orow = (int64_t)f * ep.seg_stride + ep.seg_offset + p;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int col = colw + ni * 16 + 4 * lg;
+          float v[4];
+          biased(mi, ni, v);
+          const float4 ra = *(const float4*)(ep.row_add + (int64_t)p * g.N + col);
+          *(float4*)(x + orow * g.ldo + col) = make_float4(v[0] + ra.x, v[1] + ra.y, v[2] + ra.z, v[3] + ra.w);
+        }
       }
+    }
+  } else {
+    produce<T, EPI, MT>(g, acc, rowbase, colw, lr, lg, [&](int row, int col, const float (&v)[4]) {
+      if (row >= g.M) return;
+      if constexpr (EPI == SR_EPI_BIAS_RESID) {
+        float4* p = (float4*)((float*)g.out + (int64_t)row * g.ldo + col);
+        float4 xv = *p;
+        xv.x += v[0];
+        xv.y += v[1];
+        xv.z += v[2];
+        xv.w += v[3];
+        *p = xv;
+      } else if constexpr (sr::is_bf16<T>::value) {
+        const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        *(bf16x4*)((T*)g.out + (int64_t)row * g.ldo + col) = o;
+      } else {
+        *(float4*)((T*)g.out + (int64_t)row * g.ldo + col) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    });
+  }
+}
+
+// 256x256 bf16 epilogue staged through the (free) stage buffers so that global traffic is
+// whole rows with 16 B per lane (the register epilogue's per-lane 8-B stores touch 16 rows
+// per wave instruction).  bf16 outputs: the whole 256x256 tile (128 KiB, 512-B rows);
+// RESID: two 128-row fp32 passes (1-KiB rows), each a batched coalesced read-add-write of x.
+// 16-B chunk c of LDS row r sits at chunk c ^ (r & 15): the producers' 16-row column writes
+// and the copy-out's row reads are both bank-conflict free.
+template <int EPI>
+__device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4], char* smem, int m0, int n0,
+                                            int wr, int wc, int lr, int lg, int lane, int wave) {
+  if constexpr (EPI == SR_EPI_PATCH) {
+    epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+  } else if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    float* x = (float*)g.out;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      sr::barrier_raw();  // LDS free: k-loop reads / the previous pass's copy-out are done
+      if (wr == p)
+        produce<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg, [&](int row, int col, const float (&v)[4]) {
+          const int rl = row - m0 - p * 128, cl = col - n0;
+          *(float4*)(smem + rl * 1024 + (((cl >> 2) ^ (rl & 15)) << 4)) = make_float4(v[0], v[1], v[2], v[3]);
+        });
+      sr::barrier_raw();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // 8 rows in flight per wave
+        float4 xv[8];
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int row = m0 + p * 128 + wave * 16 + h * 8 + it;
+          if (row < g.M) xv[it] = *(const float4*)(x + (int64_t)row * g.ldo + n0 + lane * 4);
+        }
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int rl = wave * 16 + h * 8 + it, row = m0 + p * 128 + rl;
+          if (row < g.M) {
+            const float4 a = *(const float4*)(smem + rl * 1024 + ((lane ^ (rl & 15)) << 4));
+            xv[it].x += a.x;
+            xv[it].y += a.y;
+            xv[it].z += a.z;
+            xv[it].w += a.w;
+            *(float4*)(x + (int64_t)row * g.ldo + n0 + lane * 4) = xv[it];
+          }
+        }
+      }
+    }
+  } else {
+    sr::barrier_raw();  // LDS free: every wave's k-loop reads are done
+    produce<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg, [&](int row, int col, const float (&v)[4]) {
+      const int rl = row - m0, cl = col - n0;
+      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *(bf16x4*)(smem + rl * 512 + (((cl >> 3) ^ (rl & 15)) << 4) + ((cl & 7) << 1)) = o;
+    });
+    sr::barrier_raw();
+    bf16* out = (bf16*)g.out;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int rl = wave * 32 + it * 2 + (lane >> 5), c = lane & 31, row = m0 + rl;
+      if (row < g.M)
+        *(uint4*)(out + (int64_t)row * g.ldo + n0 + c * 8) = *(const uint4*)(smem + rl * 512 + ((c ^ (rl & 15)) << 4));
     }
   }
 }
@@ -367,8 +452,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 
   stage(0);
   for (int kt = 0; kt < g.ktiles; ++kt) {
+#ifndef SR_ABL_NOWAIT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
+#endif
+#ifndef SR_ABL_NOBAR
     sr::barrier_raw();                                  // ... every wave's; all done with kt-1
+#endif
 #ifdef SR_ABL_NODMA
     if (kt + 1 < g.ktiles && kt < 1) stage(kt + 1);     // tuning ablation: reuse the first 2 stages
 #else
@@ -415,9 +504,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     mma(aY, bX, 1, 0);
   }
 #ifdef SR_ABL_NOEPI
-  if (acc[0][0][0] == 12345.f) ((float*)g.out)[tid] = acc[1][1][1];  // tuning ablation: keep acc live
+#pragma unroll
+  for (int i = 0; i < 8; ++i)  // tuning ablation: keep every accumulator live, store nothing
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
 #else
-  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+  if (g.lds_epi) epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
+  else epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
 #endif
 }
 
@@ -499,6 +592,11 @@ extern "C" int sr_gemm(sr_stream_t stream, int dtype, int epi, const void* A, in
   a.N = N;
   a.K = K;
   a.ktiles = K / kt;
+  // LDS-staged epilogue (256x256 tiles): measured +8 % on bf16 BIAS / QKV outputs, -7 % on the
+  // fp32 residual update and -2 % with GELU (DESIGN.md "GEMM"), so only the former use it.
+  static const bool no_lds_epi = getenv("SR_GEMM_REG_EPI") != nullptr;  // tuning A/B switch
+  a.lds_epi = !no_lds_epi && (epi == SR_EPI_BIAS || epi == SR_EPI_QKV) && ((uintptr_t)out % 16) == 0 &&
+              (ldo * esz) % 16 == 0;
   a.ep = *ep;
   hipStream_t s = (hipStream_t)stream;
   return dtype == SR_BF16 ? dispatch<bf16>(epi, a, s) : dispatch<float>(epi, a, s);

@@ -53,8 +53,8 @@ def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(8300, 4096, 128), (33000, 1024, 192), (32769, 1024, 64)])
-def test_gemm256_persistent(ops, M, N, K):
-    """>= 512 256x256 tiles select the persistent 256x256 bf16 kernel (the production path):
+def test_gemm256_tiles(ops, M, N, K):
+    """>= 512 256x256 tiles select the 256x256 bf16 kernel (the production path):
     ragged last M tile (including slabs that start past row M-1), every bf16 epilogue that
     runs on it at this width."""
     L = _lib()
@@ -119,7 +119,7 @@ def _rope_ref(t, pos, base=100.0):
 
 @pytest.mark.parametrize("dtype,tol", DT)
 @pytest.mark.parametrize("col_offset", [0, 1])
-@pytest.mark.parametrize("frames", [3, 100])
+@pytest.mark.parametrize("frames", [3, 100, 3200])  # 3200 x 21 rows: >= 512 256x256 tiles (bf16 production path)
 def test_gemm_qkv_epilogue(ops, dtype, tol, col_offset, frames):
     """bias + qk-LayerNorm + 2-D RoPE fused into the qkv GEMM (attention.py:72-82)."""
     from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D

@@ -29,8 +29,7 @@ for step in "$@"; do
     benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
     kgemm)   run kgemm 300 python tools/kbench.py gemm ln ;;
-    kgemm1)  run kgemm1 300 env SR_GEMM_ONE_TILE=1 python tools/kbench.py gemm ;;
-    kgemm_head) run kgemm_head 300 env SFM_AMD_LIB=self-supervise-sfm_amd/variants/lib_HEADGEMM.so python tools/kbench.py gemm ;;
+    kgemm_reg) run kgemm_reg 300 env SR_GEMM_REG_EPI=1 python tools/kbench.py gemm ;;
     kattn)   run kattn 300 python tools/kbench.py attn ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
@@ -40,6 +39,9 @@ for step in "$@"; do
                python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     pmc_write) run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
                python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    pmc_gemm1) run pmc_gemm1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_gemm1 -o run --output-format csv -- python3 tools/kbench.py gemm ;;
+    pmc_gemm2) run pmc_gemm2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_gemm2 -o run --output-format csv -- python3 tools/kbench.py gemm ;;
+    pmc_gemm3) run pmc_gemm3 300 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL TA_BUSY_avr GRBM_GUI_ACTIVE -d gpurun_out/pmc_gemm3 -o run --output-format csv -- python3 tools/kbench.py gemm ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmc_attn1) run pmc_attn1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_attn1 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
     pmc_attn2) run pmc_attn2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_attn2 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
