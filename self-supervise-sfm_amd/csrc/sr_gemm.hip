@@ -38,6 +38,8 @@ struct GemmArgs {
   int64_t ldo;
   int M, N, K, ktiles;
   int lds_epi;  // 256x256 kernels: stage the epilogue through LDS (outputs 16-B aligned rows)
+  int kt_per_split;  // split-K (gemm_kernel, gridDim.y slices): k-tiles per slice
+  float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
   sr_gemm_epi ep;
 };
 
@@ -362,10 +364,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, 0);
-  for (int kt = 0; kt < g.ktiles; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < g.ktiles) {
+  // split-K: slice blockIdx.y covers k-tiles [kt0, kt1)
+  const int kt0 = g.partial ? blockIdx.y * g.kt_per_split : 0;
+  const int kt1 = g.partial ? min(kt0 + g.kt_per_split, g.ktiles) : g.ktiles;
+  stage(kt0, 0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    if (kt + 1 < kt1) {
       stage(kt + 1, buf ^ 1);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
@@ -390,7 +395,46 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
     sr::barrier_raw();
   }
 
+  if (g.partial) {  // raw fp32 partial tile of this K slice
+    float* part = g.partial + (int64_t)blockIdx.y * g.M * g.N;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = m0 + wr * 64 + mi * 16 + lr;
+      if (row < g.M) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          *(f32x4*)(part + (int64_t)row * g.N + n0 + wc * 64 + ni * 16 + 4 * lg) = acc[mi][ni];
+      }
+    }
+    return;
+  }
   epilogue<T, EPI, 4>(g, acc, m0 + wr * 64, n0 + wc * 64, lr, lg);
+}
+
+// Split-K reduction + epilogue: thread = 4 consecutive columns of one row; slices summed in
+// order (deterministic).  out row stride ldo; RESID adds gamma*(sum+bias) to the fp32 out.
+template <typename T, int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slices) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index
+  const int nq = g.N >> 2;
+  if (q >= (int64_t)g.M * nq) return;
+  const int row = (int)(q / nq), col = (int)(q - (int64_t)row * nq) * 4;
+  f32x4 v = *(const f32x4*)(g.partial + (int64_t)row * g.N + col);
+  for (int z = 1; z < slices; ++z) v += *(const f32x4*)(g.partial + ((int64_t)z * g.M + row) * g.N + col);
+  if (g.ep.bias) v += *(const f32x4*)(g.ep.bias + col);
+  if constexpr (EPI == SR_EPI_BIAS_GELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = sr::is_bf16<T>::value ? sr::gelu_erf_fast(v[r]) : sr::gelu_erf(v[r]);
+  }
+  if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    f32x4* xp = (f32x4*)((float*)g.out + (int64_t)row * g.ldo + col);
+    *xp += v * *(const f32x4*)(g.ep.gamma + col);
+  } else if constexpr (sr::is_bf16<T>::value) {
+    const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *(bf16x4*)((T*)g.out + (int64_t)row * g.ldo + col) = o;
+  } else {
+    *(f32x4*)((T*)g.out + (int64_t)row * g.ldo + col) = v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -524,7 +568,13 @@ int launch256(const GemmArgs& a, hipStream_t s) {
 template <typename T, int EPI>
 int launch(const GemmArgs& a, hipStream_t s) {
   const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg), dim3(NTHREADS), 0, s, a);
+  const int slices = a.partial ? (a.ktiles + a.kt_per_split - 1) / a.kt_per_split : 1;
+  hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
+  if (a.partial) {
+    const int64_t nq = (int64_t)a.M * (a.N / 4);
+    hipLaunchKernelGGL((splitk_reduce_kernel<T, EPI>), dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, a,
+                       slices);
+  }
   return sr::check_launch("sr_gemm");
 }
 
@@ -558,8 +608,9 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int sr_gemm(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
-                       int64_t ldw, void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep) {
+static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
+                       int64_t ldw, void* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,
+                       const sr_gemm_epi* ep) {
   SR_CHECK(A && W && out && ep, SR_EINVAL, "sr_gemm: null pointer");
   SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_gemm: bad dtype %d", dtype);
   SR_CHECK(M > 0 && N > 0 && K > 0, SR_EINVAL, "sr_gemm: bad shape M=%d N=%d K=%d", M, N, K);
@@ -598,6 +649,37 @@ extern "C" int sr_gemm(sr_stream_t stream, int dtype, int epi, const void* A, in
   a.lds_epi = !no_lds_epi && (epi == SR_EPI_BIAS || epi == SR_EPI_QKV) && ((uintptr_t)out % 16) == 0 &&
               (ldo * esz) % 16 == 0;
   a.ep = *ep;
+  a.partial = nullptr;
+  a.kt_per_split = a.ktiles;
   hipStream_t s = (hipStream_t)stream;
+  if (splits > 1) {
+    SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID, SR_EUNSUPPORTED,
+             "sr_gemm_splitk: epilogue %d not supported", epi);
+    SR_CHECK(workspace && ((uintptr_t)workspace % 16) == 0 && ((uintptr_t)out % 16) == 0 && ldo % 4 == 0 && N % 4 == 0,
+             SR_EINVAL, "sr_gemm_splitk: workspace / out must be 16-B aligned");
+    SR_CHECK(a.ktiles % splits == 0, SR_EUNSUPPORTED, "sr_gemm_splitk: %d k-tiles not divisible into %d slices",
+             a.ktiles, splits);
+    a.partial = workspace;
+    a.kt_per_split = a.ktiles / splits;
+    switch (epi) {  // always the 128x128 kernel (few rows)
+      case SR_EPI_BIAS: return dtype == SR_BF16 ? launch<bf16, SR_EPI_BIAS>(a, s) : launch<float, SR_EPI_BIAS>(a, s);
+      case SR_EPI_BIAS_GELU:
+        return dtype == SR_BF16 ? launch<bf16, SR_EPI_BIAS_GELU>(a, s) : launch<float, SR_EPI_BIAS_GELU>(a, s);
+      default:
+        return dtype == SR_BF16 ? launch<bf16, SR_EPI_BIAS_RESID>(a, s) : launch<float, SR_EPI_BIAS_RESID>(a, s);
+    }
+  }
   return dtype == SR_BF16 ? dispatch<bf16>(epi, a, s) : dispatch<float>(epi, a, s);
+}
+
+extern "C" int sr_gemm(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
+                       int64_t ldw, void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep) {
+  return gemm_common(stream, dtype, epi, A, lda, W, ldw, out, ldo, M, N, K, 1, nullptr, ep);
+}
+
+extern "C" int sr_gemm_splitk(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
+                              int64_t ldw, void* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,
+                              const sr_gemm_epi* ep) {
+  SR_CHECK(splits >= 1, SR_EINVAL, "sr_gemm_splitk: splits=%d", splits);
+  return gemm_common(stream, dtype, epi, A, lda, W, ldw, out, ldo, M, N, K, splits, workspace, ep);
 }

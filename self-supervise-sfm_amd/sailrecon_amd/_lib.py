@@ -59,6 +59,8 @@ _PROTOS = {
     "sr_last_error": (ctypes.c_char_p, []),
     "sr_version": (_i32, []),
     "sr_gemm": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, ctypes.POINTER(GemmEpi)]),
+    "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
+                              ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_layernorm": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _f32, _vp, _i64, _i32, _i32]),
     "sr_im2col_normalize": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, ctypes.POINTER(_f32),

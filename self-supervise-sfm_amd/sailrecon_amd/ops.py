@@ -92,10 +92,37 @@ def _rowmajor(t: Tensor, name: str) -> int:
     return t.stride(0)
 
 
+_SPLITK_WS = {}  # device -> fp32 workspace of sr_gemm_splitk (single-stream use)
+
+
+def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
+    """K slices for few-row GEMMs (the camera trunk, M = 2N views): enough 128x128-tile
+    workgroups to spread the weight stream over the CUs; 1 = plain sr_gemm."""
+    if M > 256 or epi not in (_lib.SR_EPI_BIAS, _lib.SR_EPI_BIAS_GELU, _lib.SR_EPI_BIAS_RESID):
+        return 1
+    ktiles = K // (64 if dtype == torch.bfloat16 else 32)
+    wgs = -(-M // 128) * (N // 128)
+    cap = max(1, K // (4 * M))  # partial-tile traffic (2 * splits * M * N) <= half the weight stream (N * K)
+    splits = 1
+    while (wgs * splits * 2 <= 1024 and splits * 2 <= cap and ktiles % (splits * 2) == 0
+           and ktiles // (splits * 2) >= 4):
+        splits *= 2
+    return splits
+
+
+def _splitk_workspace(device, numel: int) -> Tensor:
+    ws = _SPLITK_WS.get(device)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(numel, device=device, dtype=torch.float32)
+        _SPLITK_WS[device] = ws
+    return ws
+
+
 def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] = None,
          gamma: Optional[Tensor] = None, rows: Optional[int] = None, qkv: Optional[dict] = None,
-         patch: Optional[dict] = None, tag: Optional[str] = None) -> None:
-    """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows)."""
+         patch: Optional[dict] = None, tag: Optional[str] = None, splits: Optional[int] = None) -> None:
+    """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows).
+    ``splits`` K slices (sr_gemm_splitk); default: automatic for few rows."""
     lda = _rowmajor(a, "a")
     ldw = _rowmajor(w, "w")
     ldo = _rowmajor(out, "out")
@@ -133,9 +160,17 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         tag = f"gemm_{_EPI_NAME.get(epi, epi)}" + ("" if a.dtype == torch.bfloat16 else "_f32")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    rc = _lib.load().sr_gemm(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
-                             M, N, K, ctypes.byref(ep))
-    check(rc, "sr_gemm")
+    if splits is None:
+        splits = _splitk_plan(M, N, K, epi, a.dtype)
+    if splits > 1:
+        ws = _splitk_workspace(a.device, splits * M * N)
+        rc = _lib.load().sr_gemm_splitk(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
+                                        M, N, K, splits, _p(ws), ctypes.byref(ep))
+        check(rc, "sr_gemm_splitk")
+    else:
+        rc = _lib.load().sr_gemm(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
+                                 M, N, K, ctypes.byref(ep))
+        check(rc, "sr_gemm")
     if timed:
         es, eo = a.element_size(), out.element_size()
         nb = (M * K + N * K) * es + M * N * eo * (2 if epi == _lib.SR_EPI_BIAS_RESID else 1)

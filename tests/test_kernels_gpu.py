@@ -75,6 +75,28 @@ def test_gemm256_tiles(ops, M, N, K):
     assert rel(x[32:32 + M] - x0[32:32 + M], ref * gam) < 1e-5
 
 
+@pytest.mark.parametrize("dtype,tol", DT)
+@pytest.mark.parametrize("M,N,K,splits", [(64, 2048, 2048, None), (64, 1024, 8192, None), (37, 256, 1024, 4)])
+def test_gemm_splitk(ops, dtype, tol, M, N, K, splits):
+    """split-K (camera trunk shapes: few rows, long K) for every epilogue it supports."""
+    L = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    a = torch.randn(M, K, generator=g).to(DEV, dtype)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV, dtype)
+    b, gam = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+    assert (splits or ops._splitk_plan(M, N, K, L.SR_EPI_BIAS, dtype)) > 1
+    ref = a.float() @ w.float().t() + b
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    ops.gemm(a, w, out, L.SR_EPI_BIAS, bias=b, splits=splits)
+    assert rel(out.float(), ref) < tol
+    ops.gemm(a, w, out, L.SR_EPI_BIAS_GELU, bias=b, splits=splits)
+    assert rel(out.float(), F.gelu(ref)) < tol
+    x = torch.randn(M, N + 8, device=DEV)[:, :N]
+    x0 = x.clone()
+    ops.gemm(a, w, x, L.SR_EPI_BIAS_RESID, bias=b, gamma=gam, splits=splits)
+    assert rel(x - x0, ref * gam) < max(tol, 1e-5)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-5)])
 @pytest.mark.parametrize("M", [517, 3000])
 def test_gemm_resid_strided(ops, dtype, tol, M):
