@@ -9,50 +9,81 @@ namespace {
 // ------------------------------------------------------------------ LayerNorm
 // One wave per row; each lane holds NPL = cols/64 values loaded as VEC-wide vectors
 // (coalesced: vector i of lane l covers columns (i*64 + l)*VEC .. +VEC).
+constexpr int ln_rows_per_wave(int npl) { return npl >= 32 ? 1 : 2; }  // register budget
 template <int NPL, int VEC, typename TO>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t ldx,
                                                         const int32_t* __restrict__ rowmap,
                                                         const float* __restrict__ w, const float* __restrict__ b,
                                                         float eps, TO* __restrict__ out, int64_t ldo, int rows) {
+  // one wave per row pair (RPW rows in flight per wave: every load issued before the first
+  // reduction); VEC-wide vector loads of x, w, b and VEC-wide stores
+  constexpr int RPW = ln_rows_per_wave(NPL);
   constexpr int NV = NPL / VEC;
   constexpr int COLS = NPL * 64;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int64_t src = rowmap ? (int64_t)rowmap[row] : row;
-  const float* xr = x + src * ldx;
-  float v[NPL];
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  float v[RPW][NPL];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int col = (i * 64 + lane) * VEC;
-    if constexpr (VEC == 4) {
-      const float4 t = *(const float4*)(xr + col);
-      v[i * 4 + 0] = t.x; v[i * 4 + 1] = t.y; v[i * 4 + 2] = t.z; v[i * 4 + 3] = t.w;
-    } else {
-      const float2 t = *(const float2*)(xr + col);
-      v[i * 2 + 0] = t.x; v[i * 2 + 1] = t.y;
+  for (int r = 0; r < RPW; ++r) {
+    const int row = min(row0 + r, rows - 1);
+    const int64_t src = rowmap ? (int64_t)rowmap[row] : row;
+    const float* xr = x + src * ldx;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * VEC;
+      if constexpr (VEC == 4) {
+        const float4 t = *(const float4*)(xr + col);
+        v[r][i * 4 + 0] = t.x; v[r][i * 4 + 1] = t.y; v[r][i * 4 + 2] = t.z; v[r][i * 4 + 3] = t.w;
+      } else {
+        const float2 t = *(const float2*)(xr + col);
+        v[r][i * 2 + 0] = t.x; v[r][i * 2 + 1] = t.y;
+      }
     }
   }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) s += v[i];
-  const float mean = sr::wave_sum(s) * (1.f / COLS);
-  float s2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    v[i] -= mean;
-    s2 += v[i] * v[i];
-  }
-  const float rstd = rsqrtf(sr::wave_sum(s2) * (1.f / COLS) + eps);
-  TO* orow = out + (int64_t)row * ldo;
+  float wv[NPL], bv[NPL];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int col = (i * 64 + lane) * VEC;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      float y = v[i * VEC + j] * rstd;
-      if (w) y = y * w[col + j] + b[col + j];
-      orow[col + j] = sr::from_f32<TO>(y);
+      wv[i * VEC + j] = w ? w[col + j] : 1.f;
+      bv[i * VEC + j] = w ? b[col + j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) s += v[r][i];
+    const float mean = sr::wave_sum(s) * (1.f / COLS);
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      v[r][i] -= mean;
+      s2 += v[r][i] * v[r][i];
+    }
+    const float rstd = rsqrtf(sr::wave_sum(s2) * (1.f / COLS) + eps);
+    if (row >= rows) break;
+    TO* orow = out + (int64_t)row * ldo;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * VEC;
+      float y[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) y[j] = fmaf(v[r][i * VEC + j] * rstd, wv[i * VEC + j], bv[i * VEC + j]);
+      if constexpr (VEC == 4) {
+        if constexpr (sr::is_bf16<TO>::value) {
+          const bf16x4 o = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+          *(bf16x4*)(orow + col) = o;
+        } else {
+          *(float4*)(orow + col) = make_float4(y[0], y[1], y[2], y[3]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) orow[col + j] = sr::from_f32<TO>(y[j]);
+      }
     }
   }
 }
@@ -60,11 +91,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 template <typename TO>
 int layernorm_dispatch(hipStream_t s, const float* x, int64_t ldx, const int32_t* rowmap, const float* w,
                        const float* b, float eps, TO* out, int64_t ldo, int rows, int cols) {
-  const dim3 grid((rows + 3) / 4), block(256);
-#define LN_CASE(C, V)                                                                                  \
-  case C:                                                                                              \
-    hipLaunchKernelGGL((layernorm_kernel<C / 64, V, TO>), grid, block, 0, s, x, ldx, rowmap, w, b, eps, out, \
-                       ldo, rows);                                                                      \
+  const dim3 block(256);  // 4 waves x ln_rows_per_wave rows
+#define LN_CASE(C, V)                                                                                    \
+  case C:                                                                                                \
+    hipLaunchKernelGGL((layernorm_kernel<C / 64, V, TO>),                                                \
+                       dim3((rows + 4 * ln_rows_per_wave(C / 64) - 1) / (4 * ln_rows_per_wave(C / 64))), block, \
+                       0, s, x, ldx, rowmap, w, b, eps, out, ldo, rows);                                  \
     return sr::check_launch("sr_layernorm");
   switch (cols) {
     LN_CASE(128, 2)
