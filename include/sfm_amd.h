@@ -184,6 +184,42 @@ int sr_pose_update_f32(sr_stream_t stream, float* pred, const float* delta, int6
 int sr_pose_decode_f32(sr_stream_t stream, const float* enc, int64_t ld_enc, int n, int H, int W,
                        float* extrinsic, float* intrinsic);
 
+/* ------------------------------------------------------------------------
+ * DPT point / depth heads (dpt_head.py:151-349) and depth unprojection (geometry.py:19-130),
+ * SURVEY §8(f) rank 1.  Feature maps are NHWC fp32 [n][h][w][c] (c % 4 == 0); convolutions
+ * run as sr_gemm (fp32): 1x1 conv = GEMM over pixels, 3x3 conv = sr_im2col3x3_f32 + GEMM with
+ * K ordered (ky, kx, ci), ConvTranspose(k, stride k) = GEMM to (ky, kx, co) + scatter.
+ * ---------------------------------------------------------------------- */
+/* out[n*ho*wo][9c] im2col of a 3x3 / pad 1 / stride 1|2 conv; ReLU on the input when relu_in
+ * (ResidualConvUnit, dpt_head.py:470-476).  ho = (h-1)/stride + 1. */
+int sr_im2col3x3_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int stride, int relu_in,
+                     float* out);
+/* ConvTranspose2d(kernel = stride = k, pad 0) scatter: g[n*h*w][(ky*k+kx)*co + c] (+ bias[c])
+ * -> out[n][h*k][w*k][co]  (dpt_head.py:89-104). */
+int sr_convt_scatter_f32(sr_stream_t stream, const float* g, int n, int h, int w, int k, int co, const float* bias,
+                         float* out);
+/* Bilinear resize, align_corners=True (custom_interpolate, dpt_head.py:568-598), plus an
+ * optional same-shape `add` (NULL = none).  out must not alias x. */
+int sr_resize_bilinear_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int ho, int wo,
+                           const float* add, float* out);
+/* dst += src over n floats (n % 4 == 0): skip_add of FeatureFusionBlock (dpt_head.py:540-545). */
+int sr_add_f32(sr_stream_t stream, float* dst, const float* src, int64_t n);
+/* x = max(x, 0) in place over n floats: the in-place nn.ReLU at the entry of each
+ * ResidualConvUnit, whose skip connection therefore adds relu(x) (dpt_head.py:470-487). */
+int sr_relu_f32(sr_stream_t stream, float* x, int64_t n);
+/* x += ratio * sincos(uv grid) positional embedding (DPTHead._apply_pos_embed, dpt_head.py:300-315;
+ * utils.py create_uv_grid / position_grid_to_embed); aspect = image W / H. */
+int sr_dpt_pos_embed_f32(sr_stream_t stream, float* x, int n, int h, int w, int c, float aspect, float ratio);
+/* output_conv2[1:] + activate_head (dpt_head.py:285-290, head_act.py:63-127): o = W relu(hidden) + b
+ * (W [cout][cin]); preds[p][0..cout-2] = act(o), conf[p] = conf_act(o[cout-1]).
+ * act: 0 inv_log, 1 exp, 2 linear, 3 relu;  conf_act: 0 expp1, 1 expp0, 2 sigmoid. */
+int sr_dpt_head_out_f32(sr_stream_t stream, const float* hidden, int64_t ldh, int64_t npix, int cin, const float* w,
+                        const float* b, int cout, int act, int conf_act, float* preds, float* conf);
+/* Depth [s][h][w] -> world points [s][h][w][3] with extrinsic [s][3][4] (cam from world) and
+ * intrinsic [s][3][3] (unproject_depth_map_to_point_map, geometry.py:19-130). */
+int sr_unproject_depth_f32(sr_stream_t stream, const float* depth, const float* extrinsic, const float* intrinsic,
+                           int s, int h, int w, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -350,3 +350,116 @@ def hot_path_forward(sd: SD, cfg: AggCfg, images: Tensor, no_reloc: List[int], r
         ext, intr = pose_encoding_to_extri_intri(poses[-1], (images.shape[-2], images.shape[-1]))
     return {"feats": feats, "patch_start_idx": psi, "cam_token_last_layer": cam_last,
             "pose_enc_list": poses, "extrinsic": ext, "intrinsic": intr}
+
+
+# --------------------------------------------------------------------------
+# DPT point / depth heads (sailrecon/heads/dpt_head.py, utils.py, head_act.py) and
+# the depth unprojection (sailrecon/utils/geometry.py) — SURVEY §8(f) rank 1
+# --------------------------------------------------------------------------
+
+def _uv_pos_embed(h: int, w: int, c: int, aspect: float) -> Tensor:
+    """[h, w, c] uv-grid sin/cos embedding (utils.py create_uv_grid + position_grid_to_embed):
+    x half then y half, each [sin | cos] of pos * 100^(-i / (c/4)), evaluated in double."""
+    diag = (aspect ** 2 + 1.0) ** 0.5
+    sx, sy = aspect / diag, 1.0 / diag
+    xs = torch.linspace(-sx * (w - 1) / w, sx * (w - 1) / w, steps=w, dtype=torch.float32)
+    ys = torch.linspace(-sy * (h - 1) / h, sy * (h - 1) / h, steps=h, dtype=torch.float32)
+    q = c // 4
+    omega = 1.0 / 100.0 ** (torch.arange(q, dtype=torch.float64) / q)
+
+    def one(pos):  # [n] -> [n, c/2]
+        arg = pos.double()[:, None] * omega[None]
+        return torch.cat([arg.sin(), arg.cos()], 1).float()
+
+    ex = one(xs)[None, :, :].expand(h, w, c // 2)
+    ey = one(ys)[:, None, :].expand(h, w, c // 2)
+    return torch.cat([ex, ey], -1)
+
+
+def _add_pos(x: Tensor, aspect: float, ratio: float = 0.1) -> Tensor:  # x NCHW
+    pe = _uv_pos_embed(x.shape[2], x.shape[3], x.shape[1], aspect) * ratio
+    return x + pe.permute(2, 0, 1)[None]
+
+
+def _conv(sd: SD, pre: str, x: Tensor, stride: int = 1, pad: Optional[int] = None) -> Tensor:
+    w = sd[pre + ".weight"]
+    if pad is None:
+        pad = w.shape[-1] // 2
+    return F.conv2d(x, w, sd.get(pre + ".bias"), stride=stride, padding=pad)
+
+
+def _rcu(sd: SD, pre: str, x: Tensor) -> Tensor:  # dpt_head.py:470-487
+    # the reference's activation is nn.ReLU(inplace=True) applied to the unit's own input, so
+    # the skip connection adds relu(x), not x (dpt_head.py:377-380, 470-487)
+    x = F.relu(x)
+    out = _conv(sd, pre + ".conv1", x)
+    out = _conv(sd, pre + ".conv2", F.relu(out))
+    return out + x
+
+
+def _fusion(sd: SD, pre: str, x0: Tensor, x1: Optional[Tensor], size) -> Tensor:  # dpt_head.py:540-565
+    out = x0
+    if x1 is not None and (pre + ".resConfUnit1.conv1.weight") in sd:
+        out = out + _rcu(sd, pre + ".resConfUnit1", x1)
+    out = _rcu(sd, pre + ".resConfUnit2", out)
+    if size is None:
+        size = (int(out.shape[2] * 2), int(out.shape[3] * 2))
+    out = F.interpolate(out, size=size, mode="bilinear", align_corners=True)
+    return _conv(sd, pre + ".out_conv", out)
+
+
+def dpt_forward(sd: SD, pre: str, tokens: Dict[int, Tensor], images: Tensor, patch_start: int,
+                layers: Sequence[int] = (4, 11, 17, 23), activation: str = "inv_log",
+                conf_activation: str = "expp1", patch: int = 14) -> Tuple[Tensor, Tensor]:
+    """DPTHead.forward (dpt_head.py:151-298) for all frames at once; returns (preds, conf)."""
+    B, S, _, H, W = images.shape
+    ph, pw = H // patch, W // patch
+    aspect = W / H
+    feats = []
+    for i, l in enumerate(layers):
+        x = tokens[l][:, :, patch_start:].reshape(B * S, ph * pw, -1)
+        x = layer_norm(x, sd[pre + "norm.weight"], sd[pre + "norm.bias"], 1e-5)
+        x = x.permute(0, 2, 1).reshape(B * S, -1, ph, pw)
+        x = _conv(sd, pre + f"projects.{i}", x)
+        x = _add_pos(x, aspect)
+        rp = pre + f"resize_layers.{i}"
+        if i in (0, 1):
+            x = F.conv_transpose2d(x, sd[rp + ".weight"], sd[rp + ".bias"], stride=4 if i == 0 else 2)
+        elif i == 3:
+            x = _conv(sd, rp, x, stride=2, pad=1)
+        feats.append(x)
+    rn = [_conv(sd, pre + f"scratch.layer{i + 1}_rn", f) for i, f in enumerate(feats)]
+    out = _fusion(sd, pre + "scratch.refinenet4", rn[3], None, rn[2].shape[2:])
+    out = _fusion(sd, pre + "scratch.refinenet3", out, rn[2], rn[1].shape[2:])
+    out = _fusion(sd, pre + "scratch.refinenet2", out, rn[1], rn[0].shape[2:])
+    out = _fusion(sd, pre + "scratch.refinenet1", out, rn[0], None)
+    out = _conv(sd, pre + "scratch.output_conv1", out)
+    out = F.interpolate(out, size=(ph * patch, pw * patch), mode="bilinear", align_corners=True)
+    out = _add_pos(out, aspect)
+    out = F.relu(_conv(sd, pre + "scratch.output_conv2.0", out))
+    out = _conv(sd, pre + "scratch.output_conv2.2", out)
+    fmap = out.permute(0, 2, 3, 1)
+    xyz, cf = fmap[..., :-1], fmap[..., -1]
+    if activation == "inv_log":  # head_act.py:117-127
+        pts = torch.sign(xyz) * torch.expm1(xyz.abs())
+    elif activation == "exp":
+        pts = xyz.exp()
+    else:
+        raise ValueError(activation)
+    conf = 1 + cf.exp() if conf_activation == "expp1" else cf.exp()
+    return pts.reshape(B, S, H, W, -1), conf.reshape(B, S, H, W)
+
+
+def unproject_depth(depth: Tensor, extr: Tensor, intr: Tensor) -> Tensor:
+    """geometry.py:19-130 in float64: depth [S,H,W(,1)] -> world points [S,H,W,3]."""
+    if depth.dim() == 4:
+        depth = depth[..., 0]
+    S, H, W = depth.shape
+    v, u = torch.meshgrid(torch.arange(H, dtype=torch.float64), torch.arange(W, dtype=torch.float64), indexing="ij")
+    out = []
+    for s in range(S):
+        K, E, d = intr[s].double(), extr[s].double(), depth[s].double()
+        cam = torch.stack([(u - K[0, 2]) * d / K[0, 0], (v - K[1, 2]) * d / K[1, 1], d], -1)
+        R, t = E[:, :3], E[:, 3]
+        out.append(cam @ R + (-(R.T @ t)))  # R_c2w = R^T: cam @ R_c2w^T = cam @ R
+    return torch.stack(out)

@@ -79,7 +79,8 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
   float4 bias[4];
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni)
-    bias[ni] = ep.bias ? *(const float4*)(ep.bias + colw + ni * 16 + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bias[ni] = ep.bias && colw + ni * 16 + 4 * lg < g.N ? *(const float4*)(ep.bias + colw + ni * 16 + 4 * lg)
+                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
   auto biased = [&](int mi, int ni, float (&v)[4]) {
     v[0] = acc[mi][ni][0] + bias[ni].x;
     v[1] = acc[mi][ni][1] + bias[ni].y;
@@ -110,7 +111,9 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
   } else if constexpr (EPI == SR_EPI_BIAS_RESID) {
     float4 gam[4];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) gam[ni] = *(const float4*)(ep.gamma + colw + ni * 16 + 4 * lg);
+    for (int ni = 0; ni < 4; ++ni)
+      gam[ni] = colw + ni * 16 + 4 * lg < g.N ? *(const float4*)(ep.gamma + colw + ni * 16 + 4 * lg)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int row = rowbase + mi * 16 + lr;
@@ -218,7 +221,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
     float4 bias[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
-      bias[ni] = ep.bias ? *(const float4*)(ep.bias + colw + ni * 16 + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
+      bias[ni] = ep.bias && colw + ni * 16 + 4 * lg < g.N ? *(const float4*)(ep.bias + colw + ni * 16 + 4 * lg)
+                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
     auto biased = [&](int mi, int ni, float (&v)[4]) {
       v[0] = acc[mi][ni][0] + bias[ni].x;
       v[1] = acc[mi][ni][1] + bias[ni].y;
@@ -235,6 +239,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const int col = colw + ni * 16 + 4 * lg;
+          if (col >= g.N) continue;
           float v[4];
           biased(mi, ni, v);
           const float4 ra = *(const float4*)(ep.row_add + (int64_t)p * g.N + col);
@@ -244,7 +249,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
     }
   } else {
     produce<T, EPI, MT>(g, acc, rowbase, colw, lr, lg, [&](int row, int col, const float (&v)[4]) {
-      if (row >= g.M) return;
+      if (row >= g.M || col >= g.N) return;
       if constexpr (EPI == SR_EPI_BIAS_RESID) {
         float4* p = (float4*)((float*)g.out + (int64_t)row * g.ldo + col);
         float4 xv = *p;
@@ -329,7 +334,7 @@ template <typename T, int EPI>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;  // N % 4 == 0; last column tile ragged
   const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
   const int tm = tile / ntn, tn = tile - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
       const int r = min(m0 + tr, g.M - 1);
       src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
     } else {
-      const int r = n0 + tr - BM;
+      const int r = min(n0 + tr - BM, g.N - 1);  // ragged last column tile: re-read the last W row
       src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
     }
   }
@@ -403,7 +408,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
       if (row < g.M) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          *(f32x4*)(part + (int64_t)row * g.N + n0 + wc * 64 + ni * 16 + 4 * lg) = acc[mi][ni];
+          if (n0 + wc * 64 + ni * 16 + 4 * lg < g.N)
+            *(f32x4*)(part + (int64_t)row * g.N + n0 + wc * 64 + ni * 16 + 4 * lg) = acc[mi][ni];
       }
     }
     return;
@@ -567,7 +573,7 @@ int launch256(const GemmArgs& a, hipStream_t s) {
 
 template <typename T, int EPI>
 int launch(const GemmArgs& a, hipStream_t s) {
-  const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+  const int nwg = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
   const int slices = a.partial ? (a.ktiles + a.kt_per_split - 1) / a.kt_per_split : 1;
   hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
   if (a.partial) {
@@ -616,7 +622,7 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
   SR_CHECK(M > 0 && N > 0 && K > 0, SR_EINVAL, "sr_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   const int kt = dtype == SR_BF16 ? Mma<bf16>::KT : Mma<float>::KT;
   const int esz = dtype == SR_BF16 ? 2 : 4;
-  SR_CHECK(N % BN == 0, SR_EUNSUPPORTED, "sr_gemm: N=%d must be a multiple of %d", N, BN);
+  SR_CHECK(N % 4 == 0, SR_EUNSUPPORTED, "sr_gemm: N=%d must be a multiple of 4", N);
   SR_CHECK(K % kt == 0, SR_EUNSUPPORTED, "sr_gemm: K=%d must be a multiple of %d", K, kt);
   SR_CHECK(lda >= K && ldw >= K && (lda * esz) % 16 == 0 && (ldw * esz) % 16 == 0, SR_EINVAL,
            "sr_gemm: bad leading dims lda=%lld ldw=%lld", (long long)lda, (long long)ldw);

@@ -62,6 +62,14 @@ _PROTOS = {
     "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
+    "sr_im2col3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "sr_convt_scatter_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "sr_resize_bilinear_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "sr_add_f32": (_i32, [_vp, _vp, _vp, _i64]),
+    "sr_relu_f32": (_i32, [_vp, _vp, _i64]),
+    "sr_dpt_pos_embed_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _f32, _f32]),
+    "sr_dpt_head_out_f32": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    "sr_unproject_depth_f32": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "sr_layernorm": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _f32, _vp, _i64, _i32, _i32]),
     "sr_im2col_normalize": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, ctypes.POINTER(_f32),
                                    ctypes.POINTER(_f32), _vp, _i32]),

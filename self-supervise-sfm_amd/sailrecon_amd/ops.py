@@ -275,3 +275,77 @@ def pose_decode(enc: Tensor, hw, ext: Tensor, intr: Tensor) -> None:
     H, W = hw
     check(_lib.load().sr_pose_decode_f32(_stream(enc), _p(enc), enc.stride(0), enc.shape[0], int(H), int(W),
                                          _p(ext), _p(intr)), "sr_pose_decode_f32")
+
+
+# ---------------------------------------------------------------- DPT heads (NHWC fp32)
+def _nhwc(x: Tensor, name: str):
+    if x.dim() != 4 or not x.is_contiguous() or x.dtype != torch.float32 or not x.is_cuda:
+        raise ValueError(f"{name} must be a contiguous fp32 NHWC device tensor, got {tuple(x.shape)} {x.dtype}")
+    return x.shape
+
+
+def im2col3x3(x: Tensor, stride: int, relu_in: bool, out: Tensor) -> None:
+    """out[n*ho*wo, 9c] = im2col of a 3x3 / pad 1 conv (K order ky, kx, ci); ReLU on the input."""
+    n, h, w, c = _nhwc(x, "im2col3x3 x")
+    ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+    if not out.is_contiguous() or out.numel() < n * ho * wo * 9 * c:
+        raise ValueError("im2col3x3: output buffer too small / not contiguous")
+    check(_lib.load().sr_im2col3x3_f32(_stream(x), _p(x), n, h, w, c, stride, int(relu_in), _p(out)),
+          "sr_im2col3x3_f32")
+
+
+def convt_scatter(g: Tensor, n: int, h: int, w: int, k: int, co: int, bias: Optional[Tensor], out: Tensor) -> None:
+    _nhwc(out, "convt_scatter out")
+    check(_lib.load().sr_convt_scatter_f32(_stream(g), _p(g), n, h, w, k, co, _p(bias), _p(out)),
+          "sr_convt_scatter_f32")
+
+
+def resize_bilinear(x: Tensor, out: Tensor, add: Optional[Tensor] = None) -> None:
+    """out = interpolate(x, out's size, bilinear, align_corners=True) (+ add)."""
+    n, h, w, c = _nhwc(x, "resize x")
+    _, ho, wo, _ = _nhwc(out, "resize out")
+    if add is not None:
+        _nhwc(add, "resize add")
+    check(_lib.load().sr_resize_bilinear_f32(_stream(x), _p(x), n, h, w, c, ho, wo, _p(add), _p(out)),
+          "sr_resize_bilinear_f32")
+
+
+def add_(dst: Tensor, src: Tensor) -> None:
+    if dst.shape != src.shape or not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("add_: shapes differ / not contiguous")
+    check(_lib.load().sr_add_f32(_stream(dst), _p(dst), _p(src), dst.numel()), "sr_add_f32")
+
+
+def relu_(x: Tensor) -> None:
+    if not x.is_contiguous() or x.dtype != torch.float32:
+        raise ValueError("relu_: contiguous fp32 tensor required")
+    check(_lib.load().sr_relu_f32(_stream(x), _p(x), x.numel()), "sr_relu_f32")
+
+
+def dpt_pos_embed_(x: Tensor, aspect: float, ratio: float = 0.1) -> None:
+    n, h, w, c = _nhwc(x, "pos_embed x")
+    check(_lib.load().sr_dpt_pos_embed_f32(_stream(x), _p(x), n, h, w, c, aspect, ratio), "sr_dpt_pos_embed_f32")
+
+
+DPT_ACT = {"inv_log": 0, "exp": 1, "linear": 2, "relu": 3}
+DPT_CONF_ACT = {"expp1": 0, "expp0": 1, "sigmoid": 2}
+
+
+def dpt_head_out(hidden: Tensor, w: Tensor, b: Optional[Tensor], activation: str, conf_activation: str,
+                 preds: Tensor, conf: Tensor) -> None:
+    if activation not in DPT_ACT or conf_activation not in DPT_CONF_ACT:
+        raise ValueError(f"unsupported DPT activation {activation!r} / {conf_activation!r}")
+    npix, cin = hidden.shape
+    cout = w.shape[0]
+    check(_lib.load().sr_dpt_head_out_f32(_stream(hidden), _p(hidden), _rowmajor(hidden, "hidden"), npix, cin, _p(w),
+                                          _p(b), cout, DPT_ACT[activation], DPT_CONF_ACT[conf_activation], _p(preds),
+                                          _p(conf)), "sr_dpt_head_out_f32")
+
+
+def unproject_depth(depth: Tensor, extrinsic: Tensor, intrinsic: Tensor, out: Tensor) -> None:
+    s, h, w = depth.shape[:3]
+    for t, name in ((depth, "depth"), (extrinsic, "extrinsic"), (intrinsic, "intrinsic"), (out, "out")):
+        if not t.is_contiguous() or t.dtype != torch.float32 or not t.is_cuda:
+            raise ValueError(f"unproject_depth: {name} must be a contiguous fp32 device tensor")
+    check(_lib.load().sr_unproject_depth_f32(_stream(depth), _p(depth), _p(extrinsic), _p(intrinsic), s, h, w,
+                                             _p(out)), "sr_unproject_depth_f32")

@@ -43,7 +43,7 @@ def test_abi_validation_errors_without_gpu():
     lib = _lib.load()
     ep = _lib.GemmEpi()
     rc = lib.sr_gemm(None, _lib.SR_BF16, _lib.SR_EPI_BIAS, ctypes.c_void_p(16), 64, ctypes.c_void_p(16), 64,
-                     ctypes.c_void_p(16), 100, 10, 100, 64, ctypes.byref(ep))
-    assert rc == -3 and b"multiple of 128" in lib.sr_last_error()
+                     ctypes.c_void_p(16), 104, 10, 102, 64, ctypes.byref(ep))
+    assert rc == -3 and b"multiple of 4" in lib.sr_last_error()
     d = _lib.AttnDesc()
     assert lib.sr_attention(None, _lib.SR_BF16, ctypes.byref(d)) == -1

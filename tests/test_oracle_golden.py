@@ -100,3 +100,46 @@ def test_full_c1_224():
 @pytest.mark.slow
 def test_full_518_n1():
     _full("g5_518_n1.npz", 1e-5)
+
+
+# ---------------------------------------------------------------- DPT heads (§8(f) rank 1)
+@pytest.mark.parametrize("kind", ["point", "depth"])
+def test_dpt_small_matches_reference(kind):
+    from goldens import DPT_HEADS, DPT_SMALL, dpt_small_model_sd
+    g = load_npz("g6_dpt_small.npz")
+    _, sd = dpt_small_model_sd(kind)
+    toks = {l: torch.from_numpy(g[f"tok_{l}"]) for l in DPT_SMALL["intermediate_layer_idx"]}
+    preds, conf = O.dpt_forward(sd, "", toks, torch.from_numpy(g["images"]), 5,
+                                layers=DPT_SMALL["intermediate_layer_idx"],
+                                activation=DPT_HEADS[kind]["activation"],
+                                conf_activation=DPT_HEADS[kind]["conf_activation"])
+    assert rel_l2(preds.numpy(), g[f"{kind}_preds"]) < 1e-5
+    assert rel_l2(conf.numpy(), g[f"{kind}_conf"]) < 1e-5
+
+
+def test_dpt_224_matches_reference():
+    from goldens import DPT_HEADS, dpt_224_inputs, rule_state_dict
+    g = load_npz("g6_dpt_224.npz")
+    toks, images = dpt_224_inputs()
+    for kind in ("point", "depth"):
+        sd = rule_state_dict("dpt_state_dict_keys.json", kind)
+        preds, conf = O.dpt_forward(sd, "", toks, images, 5, activation=DPT_HEADS[kind]["activation"],
+                                    conf_activation=DPT_HEADS[kind]["conf_activation"])
+        assert rel_l2(preds.numpy(), g[f"{kind}_preds"]) < 1e-5
+        assert rel_l2(conf.numpy(), g[f"{kind}_conf"]) < 1e-5
+
+
+def test_dpt_mirror_state_dict_keys_match_reference():
+    """our DPTHead mirror has exactly the reference DPTHead's state_dict keys / shapes."""
+    from goldens import DPT_HEADS, key_shapes
+    from sailrecon_amd.heads.dpt_head import DPTHead
+    for kind in ("point", "depth"):
+        ours = sorted((k, tuple(v.shape)) for k, v in DPTHead(dim_in=2048, **DPT_HEADS[kind]).state_dict().items())
+        assert ours == key_shapes("dpt_state_dict_keys.json", kind)
+
+
+def test_unproject_matches_reference():
+    g = load_npz("g6_unproject.npz")
+    pts = O.unproject_depth(torch.from_numpy(g["depth"]), torch.from_numpy(g["extrinsic"]),
+                            torch.from_numpy(g["intrinsic"]))
+    assert rel_l2(pts.numpy(), g["points"]) < 1e-6
