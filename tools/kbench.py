@@ -93,6 +93,22 @@ def ln():
     print(f"layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s")
 
 
+def dpt():
+    """DPT point + depth heads on 32 query frames @518, fp32."""
+    from sailrecon_amd.heads.dpt_head import DPTHead
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    S, H, W, C, P = 32, 518, 518, 2048, 1374
+    g = torch.Generator(device=DEV).manual_seed(0)
+    toks = {l: torch.randn(1, S, P, C, device=DEV, generator=g) for l in (4, 11, 17, 23)}
+    images = torch.rand(1, S, 3, H, W, device=DEV, generator=g)
+    for kind, kw in (("point", dict(output_dim=4, activation="inv_log")), ("depth", dict(output_dim=2, activation="exp"))):
+        m = DPTHead(dim_in=C, **kw)
+        m.load_state_dict(synth_state_dict_like(m))
+        m = m.to(DEV)
+        ms = timeit(lambda: m(toks, images=images, patch_start_idx=5), reps=2, warm=1)
+        print(f"dpt {kind:5s} head S={S} @{H}  {ms:9.2f} ms  ({ms / S:.2f} ms/frame)")
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["attn", "gemm", "ln"]
     for w in which:
