@@ -87,6 +87,10 @@ class Aggregator(nn.Module):
         self._ws = runtime.Workspace()
         self._packed: Dict[Tuple[str, torch.dtype], object] = {}
         self.last_subsample_indices: Optional[torch.Tensor] = None
+        # two-phase relocalisation (attention.py:40-100, aggregator.py:435-578): anchor-subsample
+        # K|V of every global_reloc layer, kept in HBM (the reference round-trips it via the CPU)
+        self.kv_cache = kv_cache
+        self._kv_cache_layers: Optional[List[torch.Tensor]] = None
 
     # ------------------------------------------------------------------ construction
     def __build_patch_embed__(self, patch_embed, img_size, patch_size, num_register_tokens,
@@ -187,49 +191,19 @@ class Aggregator(nn.Module):
         return g, torch.distributed.get_world_size(g), torch.distributed.get_rank(g)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, images: torch.Tensor, no_reloc_list: list, reloc_list: list,
-                fix_rank: Union[int, None] = None) -> Tuple[Dict[int, torch.Tensor], int, torch.Tensor]:
-        B, S, C_in, H, W = images.shape
-        num_recon, num_reloc = len(no_reloc_list), len(reloc_list)
-        self.num_recon = num_recon
-        if C_in != 3:
-            raise ValueError(f"Expected 3 input channels, got {C_in}")
-        runtime.require_device(images, "Aggregator")
-        if sorted(list(no_reloc_list) + list(reloc_list)) != list(range(S)):
-            raise ValueError("no_reloc_list and reloc_list must be disjoint and cover every frame "
-                             f"(S={S}, got {list(no_reloc_list)} / {list(reloc_list)}); the reference's "
-                             "block mask (aggregator.py:302-311) assumes the same")
-        if num_recon == 0:
-            raise ValueError("at least one anchor (no_reloc) frame is required")
+    def _embed(self, imgs: torch.Tensor, F_: int, H: int, W: int, ftype_t_fn, dtype) -> Tuple[torch.Tensor, object]:
+        """Image normalise + DINO patch embed (+ its blocks and final norm) + aggregator special
+        tokens (aggregator.py:267-299): fills the residual stream x [F_*P, C] of the workspace."""
+        dev = imgs.device
+        C = self.embed_dim
         ps = self.patch_size
-        assert H % ps == 0 and W % ps == 0, f"image size {H}x{W} is not a multiple of the patch size {ps}"
-        group, G, r = self._world()
-        Na, Nq = num_recon, num_reloc
-        if G > 1 and (B != 1 or Na % G or Nq % G):
-            raise ValueError(f"frame sharding over {G} ranks needs B == 1 and anchor / query counts "
-                             f"divisible by {G} (got B={B}, Na={Na}, Nq={Nq})")
-        Na_l, Nq_l = Na // G, Nq // G
-        my_anchors = list(no_reloc_list)[r * Na_l:(r + 1) * Na_l]
-        my_queries = list(reloc_list)[r * Nq_l:(r + 1) * Nq_l]
-        S_l = Na_l + Nq_l
-
-        dev = images.device
-        dtype = runtime.compute_dtype(self.compute_dtype)
-        C, nh = self.embed_dim, self.num_heads
         gh, gw = H // ps, W // ps
         n_patch = gh * gw
         psi = self.patch_start_idx
         P = n_patch + psi
-        F_ = B * S_l
         R = F_ * P
         ws = self._ws
         hidden = self.frame_blocks[0].mlp.fc1.out_features
-
-        # ---- internal (local) frame order: anchors then queries, per batch item
-        order = my_anchors + my_queries
-        imgs = images if order == list(range(S)) else images[:, order]
-        imgs = imgs.reshape(F_, 3, H, W).float().contiguous()
-
         x = ws.get("x", R, C, torch.float32, dev)
         sc = runtime.scratch(ws, R, C, hidden, dtype, dev)
 
@@ -262,11 +236,60 @@ class Aggregator(nn.Module):
             ops.layernorm(x, dino.norm.weight, dino.norm.bias, dino.norm.eps, x)  # in place (row-local)
 
         # ---- aggregator special tokens, aggregator.py:287-299 (type by ORIGINAL frame index)
-        ftype = []
-        for b in range(B):
-            ftype += [0 if a == 0 else 1 for a in my_anchors] + [2] * Nq_l
-        ftype_t = runtime.to_device(torch.tensor(ftype, dtype=torch.int32), dev)
-        ops.set_special_tokens(x, F_, P, misc["special"], ftype_t)
+        ops.set_special_tokens(x, F_, P, misc["special"], ftype_t_fn())
+        return x, sc
+
+
+    def forward(self, images: torch.Tensor, no_reloc_list: list, reloc_list: list,
+                fix_rank: Union[int, None] = None) -> Tuple[Dict[int, torch.Tensor], int, torch.Tensor]:
+        B, S, C_in, H, W = images.shape
+        num_recon, num_reloc = len(no_reloc_list), len(reloc_list)
+        self.num_recon = num_recon
+        if C_in != 3:
+            raise ValueError(f"Expected 3 input channels, got {C_in}")
+        runtime.require_device(images, "Aggregator")
+        if sorted(list(no_reloc_list) + list(reloc_list)) != list(range(S)):
+            raise ValueError("no_reloc_list and reloc_list must be disjoint and cover every frame "
+                             f"(S={S}, got {list(no_reloc_list)} / {list(reloc_list)}); the reference's "
+                             "block mask (aggregator.py:302-311) assumes the same")
+        if num_recon == 0:
+            raise ValueError("at least one anchor (no_reloc) frame is required")
+        ps = self.patch_size
+        assert H % ps == 0 and W % ps == 0, f"image size {H}x{W} is not a multiple of the patch size {ps}"
+        group, G, r = self._world()
+        Na, Nq = num_recon, num_reloc
+        if self.kv_cache and Nq > 0:
+            raise NotImplementedError("a kv_cache aggregator runs anchors only here (SailRecon.tmp_forward) and "
+                                      "queries through forward_with_cache (SailRecon.reloc), like the reference")
+        fill_cache = self.kv_cache  # anchors-only pass: keep every layer's anchor-subsample K|V
+        if G > 1 and (B != 1 or Na % G or Nq % G):
+            raise ValueError(f"frame sharding over {G} ranks needs B == 1 and anchor / query counts "
+                             f"divisible by {G} (got B={B}, Na={Na}, Nq={Nq})")
+        Na_l, Nq_l = Na // G, Nq // G
+        my_anchors = list(no_reloc_list)[r * Na_l:(r + 1) * Na_l]
+        my_queries = list(reloc_list)[r * Nq_l:(r + 1) * Nq_l]
+        S_l = Na_l + Nq_l
+
+        dev = images.device
+        dtype = runtime.compute_dtype(self.compute_dtype)
+        C, nh = self.embed_dim, self.num_heads
+        gh, gw = H // ps, W // ps
+        n_patch = gh * gw
+        psi = self.patch_start_idx
+        P = n_patch + psi
+        F_ = B * S_l
+        R = F_ * P
+        ws = self._ws
+        hidden = self.frame_blocks[0].mlp.fc1.out_features
+
+        # ---- internal (local) frame order: anchors then queries, per batch item
+        order = my_anchors + my_queries
+        imgs = images if order == list(range(S)) else images[:, order]
+        imgs = imgs.reshape(F_, 3, H, W).float().contiguous()
+
+        x, sc = self._embed(imgs, F_, H, W, ftype_t_fn=lambda: runtime.to_device(
+            torch.tensor(sum(([0 if a == 0 else 1 for a in my_anchors] + [2] * Nq_l for _ in range(B)), []),
+                         dtype=torch.int32), dev), dtype=dtype)
 
         # ---- subsample draws (host, overlaps the GPU work above), aggregator.py:277-285, 580-626
         if fix_rank is not None:
@@ -277,9 +300,16 @@ class Aggregator(nn.Module):
         rank_ = self.rank
         Pp = min(rank_ + psi, P)
         rowmap_t = None
-        if Nq > 0:
-            idx = self.draw_subsample(self.depth, B, Na, n_patch, rank_)  # every rank draws all anchors
-            self.last_subsample_indices = torch.from_numpy(idx)
+        # the reference draws at every layer even without queries (select_scene_repe_for_reloc,
+        # aggregator.py:351-357), so the generator advances identically
+        idx = self.draw_subsample(self.depth, B, Na, n_patch, rank_)  # every rank draws all anchors
+        self.last_subsample_indices = torch.from_numpy(idx)
+        need_sub = Nq > 0 or fill_cache
+        if fill_cache:
+            if B != 1:
+                raise NotImplementedError("kv_cache needs B == 1 (aggregator.py:452)")
+            self._kv_cache_layers = [None] * self.depth
+        if need_sub:
             idx = idx[:, :, r * Na_l:(r + 1) * Na_l]                      # this rank's anchors
             base = (np.arange(B) * S_l * P)[None, :, None, None] + (np.arange(Na_l) * P)[None, None, :, None]
             sel = base + psi + idx                                        # [depth, B, Na_l, rank]
@@ -314,8 +344,9 @@ class Aggregator(nn.Module):
             pg = self.global_blocks[l].packed(dtype)
             for b in range(B):
                 a0, q0, q1 = b * S_l * P, b * S_l * P + Na_l * P, (b + 1) * S_l * P
-                self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if Nq > 0 else None, Na_l * Pp, a0, q0, q1,
-                                   Nq_l, P, rope, posctx, dtype, dev, group, G, r)
+                self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if need_sub else None, Na_l * Pp, a0, q0, q1,
+                                   Nq_l, P, rope, posctx, dtype, dev, group, G, r,
+                                   cache_layer=l if fill_cache else None)
             if l in out_maps:  # reloc half
                 for b in range(B):
                     ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, C:],
@@ -343,9 +374,76 @@ class Aggregator(nn.Module):
             self.last_query_cam_tokens = output_dict[-1][:, :, 0] if Nq > 0 else None
         return output_dict, self.patch_start_idx, cam_last
 
+    # ------------------------------------------------------------------ two-phase relocalisation
+    def clear_kv_cache(self) -> None:
+        """attention.py:48-60 for every global_reloc block."""
+        self._kv_cache_layers = None
+
+    def forward_with_cache(self, images: torch.Tensor, cameras: torch.Tensor = None, camera_dropout: float = False,
+                           fix_rank: Union[int, None] = None) -> Tuple[Dict[int, torch.Tensor], int]:
+        """aggregator.py:435-578: relocalise query frames against the anchors cached by an
+        anchors-only ``forward`` of a ``kv_cache=True`` aggregator.  Every frame of ``images``
+        is a query: reloc special tokens, frame blocks, and per layer the global_reloc block
+        over [cached anchor-subsample K|V ; the frame's own tokens] (the reference's cache
+        concatenation + block mask, attention.py:80-100, aggregator.py:497-509).  Returns
+        (output_dict {inter layers, -1: [1, S, P, 2C]}, patch_start_idx)."""
+        B, S, C_in, H, W = images.shape
+        assert B == 1, "Batch size must be 1 for this model"
+        if C_in != 3:
+            raise ValueError(f"Expected 3 input channels, got {C_in}")
+        runtime.require_device(images, "Aggregator.forward_with_cache")
+        if self._kv_cache_layers is None or any(t is None for t in self._kv_cache_layers):
+            raise RuntimeError("forward_with_cache needs a filled cache: run the anchors-only forward first "
+                               "(SailRecon.tmp_forward)")
+        if self._world()[1] > 1:
+            raise NotImplementedError("forward_with_cache under frame sharding")
+        ps = self.patch_size
+        assert H % ps == 0 and W % ps == 0, f"image size {H}x{W} is not a multiple of the patch size {ps}"
+        if fix_rank is not None:
+            self.rank = fix_rank
+        dev = images.device
+        dtype = runtime.compute_dtype(self.compute_dtype)
+        if self._kv_cache_layers[0].dtype != dtype:
+            raise RuntimeError(f"the cache was built in {self._kv_cache_layers[0].dtype}, this pass computes in "
+                               f"{dtype}: run both phases under the same autocast setting")
+        C, nh = self.embed_dim, self.num_heads
+        gh, gw = H // ps, W // ps
+        psi = self.patch_start_idx
+        P = gh * gw + psi
+        F_ = S
+        R = F_ * P
+        n_sub = self._kv_cache_layers[0].shape[0]
+        imgs = images.reshape(F_, 3, H, W).float().contiguous()
+        x, sc = self._embed(imgs, F_, H, W, ftype_t_fn=lambda: torch.full((F_,), 2, device=dev, dtype=torch.int32),
+                            dtype=dtype)
+        rope = self.rope.tables(C // nh, max(gh, gw) + 1, dev) if self.rope is not None else None
+        posctx = dict(tokens_per_frame=P, patch_start=psi, grid_w=gw)
+        out_maps = {l: torch.empty(1, S, P, 2 * C, device=dev, dtype=torch.float32) for l in self.intermediate_layer_idx}
+        for l in range(self.depth):
+            pb = self.frame_blocks[l].packed(dtype)
+            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P),
+                              runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
+            if l in out_maps:
+                ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, :C], x, R)
+            pr = self.global_reloc_blocks[l].packed(dtype)
+            kv = self._kv_cache_layers[l]
+
+            def attend_cached(qkv, o, kv=kv, pr=pr):
+                ops.attention(qkv[:, 0:C], kv[:, 0:C], kv[:, C:2 * C], o, heads=pr.heads, head_dim=pr.head_dim,
+                              batch=F_, lq=P, q_bstride=P, l0=n_sub, k0_bstride=0, k1=qkv[:, C:2 * C],
+                              v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
+            runtime.run_block(pr, x, 0, R, sc, attend_cached, runtime.qkv_params(pr, rope, pos_row_base=0, **posctx))
+            if l in out_maps:
+                ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, C:], x, R)
+        assert self.depth - 1 in out_maps, \
+            f"Please make sure the last layer ({self.depth - 1}) is in the output_dict: {out_maps.keys()}"
+        output_dict: Dict[int, torch.Tensor] = dict(out_maps)
+        output_dict[-1] = output_dict[self.depth - 1]
+        return output_dict, self.patch_start_idx
+
     # ------------------------------------------------------------------ stacks
     def _layer_global(self, pr, pg, x, sc, rowmap, n_sub, a0, q0, q1, Nq_l, P, rope, posctx, dtype, dev,
-                      group, G, r):
+                      group, G, r, cache_layer=None):
         """global_reloc (queries, aggregator.py:672-741) + global (anchors, :743-769) blocks of
         one layer for one batch item.  With G > 1 the anchor K/V and the anchor-subsample K/V
         are all-gathered (async, overlapped with the query-side QKV GEMM)."""
@@ -354,7 +452,7 @@ class Aggregator(nn.Module):
         La_l = q0 - a0           # local anchor tokens
         La = La_l * G            # all anchor tokens
         work_sub = work_kv = None
-        if Nq_l > 0:
+        if Nq_l > 0 or cache_layer is not None:
             # anchor-subsample K/V (reads x before the global block updates the anchors)
             xn_sub = ws.get("xn_sub", n_sub, C, dtype, dev)
             if G > 1:  # separate send buffer: no aliasing between collective input and output
@@ -366,6 +464,11 @@ class Aggregator(nn.Module):
             self._kv_gemm(pr, xn_sub, kv_sub, rope, dict(pos_rowmap=rowmap, **posctx))
             if G > 1:
                 work_sub = torch.distributed.all_gather_into_tensor(kv_sub_all, kv_sub, group=group, async_op=True)
+            if cache_layer is not None:  # two-phase reloc: every anchor's subsample K|V of this layer
+                if work_sub is not None:
+                    work_sub.wait()
+                    work_sub = None
+                self._kv_cache_layers[cache_layer] = kv_sub_all.clone()
         if G > 1:
             # global block, first half: LN1 + Q GEMM locally, K/V straight into this rank's slot
             xs = x[a0:q0]

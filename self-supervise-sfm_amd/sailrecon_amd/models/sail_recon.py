@@ -83,3 +83,75 @@ class SailRecon(nn.Module):
             for i in range(len(local_reloc)):
                 final_results[i][key] = value[:, i]
         return final_results
+
+    # ------------------------------------------------------------------ two-phase relocalisation
+    def clear_cache(self):
+        """sail_recon.py:161-174."""
+        self.aggregator.clear_kv_cache()
+        self.cam_token_last_layer = None
+        self.need_re_forward = False
+
+    @staticmethod
+    def _views_to_rgbs(views):
+        rgbs = views if isinstance(views, torch.Tensor) else torch.cat([v["img"] for v in views], dim=0)
+        return rgbs.unsqueeze(0) if rgbs.dim() == 4 else rgbs
+
+    def tmp_forward(self, views, no_reloc_list=None, reloc_list=[], fix_rank=300):  # noqa: B006 (reference)
+        """Phase 1 (sail_recon.py:176-200): run the anchors once with kv_cache=True, keeping every
+        layer's anchor-subsample K|V (in HBM) and the anchors' last-layer camera tokens."""
+        if not self.aggregator.kv_cache:
+            raise RuntimeError("tmp_forward needs SailRecon(kv_cache=True)")
+        if reloc_list:
+            raise NotImplementedError("tmp_forward with queries: the reference's cached attention returns zeros "
+                                      "for them; relocalise queries with reloc()")
+        if self.need_re_forward:
+            self.aggregator.clear_kv_cache()
+        else:
+            self.need_re_forward = True
+        rgbs = self._views_to_rgbs(views)
+        if no_reloc_list is None:
+            no_reloc_list = list(range(len(views)))
+        _, _, cam_token_last_layer = self.aggregator(rgbs, no_reloc_list, [], fix_rank=fix_rank)
+        if self.cam_token_last_layer is None:
+            self.cam_token_last_layer = cam_token_last_layer.clone()
+
+    def reloc(self, views, no_reloc_list=None, fix_rank=300, memory_save=True, save_depth=True, fast_reloc=False,
+              ret_img=False):
+        """Phase 2 (sail_recon.py:202-282): relocalise query views against the cached scene.
+        Same flags and result keys as the reference; heads whose outputs the flags drop are not
+        evaluated (the reference computes and discards them)."""
+        rgbs = self._views_to_rgbs(views)
+        rgb_feats, idx_patch = self.aggregator.forward_with_cache(rgbs, fix_rank=fix_rank)
+        cam_tokens = rgb_feats[-1][:, :, 0]
+        nviews = len(views)
+        predictions = {}
+        with torch.autocast("cuda", enabled=False):
+            cam_maps = self.camera_head(rgb_feats, self.cam_token_last_layer)
+            extrinsic, intrinsic = pose_encoding_to_extri_intri(cam_maps[-1].contiguous(),
+                                                                (rgbs.shape[-2], rgbs.shape[-1]))
+            predictions["extrinsic"] = extrinsic
+            predictions["intrinsic"] = intrinsic
+            if not fast_reloc:
+                if not memory_save and self.point_head is not None:
+                    xyz_map, xyz_cnf = self.point_head(rgb_feats, images=rgbs, patch_start_idx=idx_patch)
+                if (save_depth or not memory_save) and self.depth_head is not None:
+                    dpt_map, dpt_cnf = self.depth_head(rgb_feats, images=rgbs, patch_start_idx=idx_patch)
+                if not memory_save:
+                    from ..utils.geometry import unproject_depth_map_to_point_map
+                    pts = unproject_depth_map_to_point_map(dpt_map.squeeze(0), extrinsic.squeeze(0),
+                                                           intrinsic.squeeze(0))
+                    predictions["point_map_by_unprojection"] = pts[None]
+                    predictions["point_map"] = xyz_map
+                    predictions["rgbs"] = rgbs
+                    predictions["xyz_cnf"] = xyz_cnf
+                if save_depth:
+                    predictions["depth_map"] = dpt_map
+                    predictions["dpt_cnf"] = dpt_cnf
+                predictions["cam_tokens"] = cam_tokens
+                if ret_img:
+                    predictions["images"] = rgbs
+        final_results = [{} for _ in range(nviews)]
+        for key, value in predictions.items():
+            for i in range(nviews):
+                final_results[i][key] = value[:, i]
+        return final_results

@@ -143,3 +143,31 @@ def test_unproject_matches_reference():
     pts = O.unproject_depth(torch.from_numpy(g["depth"]), torch.from_numpy(g["extrinsic"]),
                             torch.from_numpy(g["intrinsic"]))
     assert rel_l2(pts.numpy(), g["points"]) < 1e-6
+
+
+# ---------------------------------------------------------------- two-phase relocalisation (§8(f) rank 3)
+@pytest.mark.slow
+def test_kvcache_reloc_equals_one_pass_oracle():
+    """The reference's tmp_forward + reloc(i) (g7, make_golden_kvcache.py) equals the one-pass
+    forward with image i as the query frame (the generator also printed this); the oracle's
+    one-pass hot path + DPT depth head reproduce it."""
+    from goldens import DPT_HEADS
+    g = load_npz("g7_kvcache.npz")
+    sd = rule_state_dict("state_dict_keys.json")
+    images = torch.from_numpy(g["images"])
+    n = images.shape[0]
+    n_patch = (images.shape[-1] // 14) ** 2
+    i = 1
+    sub = O.draw_subsample_indices(torch.Generator().manual_seed(0), 24, 1, n, n_patch, min(300, n_patch))
+    frames = torch.cat([images, images[i:i + 1]])[None]
+    out = O.hot_path_forward(sd, O.AggCfg(), frames, list(range(n)), [n], 300, sub)
+    assert rel_l2(out["extrinsic"][0].numpy(), g[f"extrinsic_{i}"][0]) < 1e-5
+    assert rel_l2(out["intrinsic"][0].numpy(), g[f"intrinsic_{i}"][0]) < 1e-5
+    assert rel_l2(out["feats"][-1][0, :, 0].numpy(), g[f"cam_tokens_{i}"]) < 1e-5
+    from goldens import key_shapes
+    from sailrecon_amd.utils.synth_weights import synth_state_dict
+    hsd = synth_state_dict(("depth_head." + k, s_) for k, s_ in key_shapes("dpt_state_dict_keys.json", "depth"))
+    d, c = O.dpt_forward(hsd, "depth_head.", out["feats"], frames[:, n:], 5,
+                         activation=DPT_HEADS["depth"]["activation"])
+    assert rel_l2(d[0].numpy(), g[f"depth_map_{i}"]) < 1e-5
+    assert rel_l2(c[0].numpy(), g[f"dpt_cnf_{i}"]) < 1e-5
