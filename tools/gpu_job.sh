@@ -31,6 +31,7 @@ for step in "$@"; do
     kgemm)   run kgemm 300 python tools/kbench.py gemm ln ;;
     kgemm_reg) run kgemm_reg 300 env SR_GEMM_REG_EPI=1 python tools/kbench.py gemm ;;
     kdpt)    run kdpt 600 python tools/kbench.py dpt ;;
+    kreloc)  run kreloc 600 python tools/kbench.py reloc ;;
     kattn)   run kattn 300 python tools/kbench.py attn ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;

@@ -109,6 +109,25 @@ def dpt():
         print(f"dpt {kind:5s} head S={S} @{H}  {ms:9.2f} ms  ({ms / S:.2f} ms/frame)")
 
 
+def reloc():
+    """Two-phase relocalisation at N=32 anchors @518 (bf16 aggregator, fp32 heads): tmp_forward
+    once, then reloc() of single query views (train/demo_imc.py flow)."""
+    from sailrecon_amd.models.sail_recon import SailRecon
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    n = 32
+    m = SailRecon(kv_cache=True)
+    m.load_state_dict(synth_state_dict_like(m))
+    m = m.to(DEV).eval()
+    x = torch.rand(n, 3, 518, 518, device=DEV, generator=torch.Generator(device=DEV).manual_seed(n))
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        ms1 = timeit(lambda: m.tmp_forward(x, fix_rank=300), reps=2, warm=1)
+        for flags, name in ((dict(fast_reloc=True), "pose only"), (dict(), "pose+depth"),
+                            (dict(memory_save=False, ret_img=True), "all heads")):
+            ms = timeit(lambda: m.reloc(x[:1], fix_rank=300, **flags), reps=5, warm=2)
+            print(f"reloc 1 view vs {n} anchors @518 ({name:10s}) {ms:8.2f} ms")
+    print(f"tmp_forward {n} anchors @518            {ms1:8.2f} ms")
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["attn", "gemm", "ln"]
     for w in which:
