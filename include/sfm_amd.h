@@ -220,6 +220,27 @@ int sr_dpt_head_out_f32(sr_stream_t stream, const float* hidden, int64_t ldh, in
 int sr_unproject_depth_f32(sr_stream_t stream, const float* depth, const float* extrinsic, const float* intrinsic,
                            int s, int h, int w, float* out);
 
+/* ------------------------------------------------------------------------------------------
+ * Input formation (ImagePreprocessor.process_image_with_matrices, train/utils/io.py:75-153;
+ * called per view by datasets/imc2021.py:264-280): zero-pad to a centred square of side
+ * `side`, PIL Image.resize((t, t), BICUBIC), ToTensor (RGB / 255) or uint16 depth / 1000.
+ * Bit-exact with Pillow's separable resampler.  Tables per axis (host-built, Pillow's filter):
+ * bounds[o] = {first input index, tap count}, coeffs[o][ksize] = int32 22-bit fixed point
+ * (mode 0, 8-bit) or double (mode 1, 'I;16').
+ * ------------------------------------------------------------------------------------------ */
+/* Horizontal pass: img [n][h][w][c] (uint8, mode 0, c <= 4; uint16, mode 1, c == 1) pasted at
+ * (pad_left, pad_top) into a zero canvas [canvas_h][canvas_w] -> tmp [n][canvas_h][tw][c] of the same
+ * element type (tw = output width; bounds/coeffs: the canvas_w -> tw table). */
+int sr_pil_resample_h(sr_stream_t stream, int mode, const void* img, int n, int h, int w, int c, int canvas_h,
+                      int canvas_w, int pad_left, int pad_top, const int* bounds, const void* coeffs, int ksize,
+                      int tw, void* tmp);
+/* Vertical pass + ToTensor: tmp [n][rows][tw][c] -> out[f * frame_stride + ch * chan_stride + y * ldo + x]
+ * = stored value / divisor (255 for RGB, 1000 for depth), fp32, for th output rows (bounds/coeffs:
+ * the rows -> output table, offset by the first output row for a centre crop). */
+int sr_pil_resample_v_f32(sr_stream_t stream, int mode, const void* tmp, int n, int rows, int tw, int c,
+                          const int* bounds, const void* coeffs, int ksize, int th, float divisor, float* out,
+                          int64_t frame_stride, int64_t chan_stride, int64_t ldo);
+
 #ifdef __cplusplus
 }
 #endif

@@ -463,3 +463,116 @@ def unproject_depth(depth: Tensor, extr: Tensor, intr: Tensor) -> Tensor:
         R, t = E[:, :3], E[:, 3]
         out.append(cam @ R + (-(R.T @ t)))  # R_c2w = R^T: cam @ R_c2w^T = cam @ R
     return torch.stack(out)
+
+
+# --------------------------------------------------------------------------
+# Input formation (train/utils/io.py:75-195 ImagePreprocessor; datasets/imc2021.py:260-301):
+# pad to square (zeros, centred), PIL BICUBIC resize to target, ToTensor / uint16 depth / 1000,
+# K <-> K' matrices — SURVEY §8(f) rank 2.  PIL's resample (Pillow Resample.c) restated.
+# --------------------------------------------------------------------------
+
+PIL_PRECISION_BITS = 32 - 8 - 2
+
+
+def _pil_bicubic(x: float, a: float = -0.5) -> float:
+    x = abs(x)
+    if x < 1.0:
+        return ((a + 2.0) * x - (a + 3.0)) * x * x + 1
+    if x < 2.0:
+        return (((x - 5) * x + 8) * x - 4) * a
+    return 0.0
+
+
+def pil_coeffs(in_size: int, out_size: int):
+    """Per output pixel: (first input index, normalised double weights) of PIL's antialiased
+    bicubic filter (support 2 * max(scale, 1), centre (i + 0.5) * scale)."""
+    scale = in_size / out_size
+    fs = max(scale, 1.0)
+    support, ss = 2.0 * fs, 1.0 / fs
+    out = []
+    for xx in range(out_size):
+        c = (xx + 0.5) * scale
+        xmin = max(int(c - support + 0.5), 0)
+        xmax = min(int(c + support + 0.5), in_size) - xmin
+        k = [_pil_bicubic((x + xmin - c + 0.5) * ss) for x in range(xmax)]
+        ww = sum(k)
+        out.append((xmin, [w / ww if ww != 0.0 else w for w in k]))
+    return out
+
+
+def pil_fixed(k):
+    """8-bit modes: weights as PRECISION_BITS fixed point (rounded away from zero)."""
+    s = 1 << PIL_PRECISION_BITS
+    return [int(-0.5 + w * s) if w < 0 else int(0.5 + w * s) for w in k]
+
+
+def pil_resize_u8(img, target: int):
+    """uint8 [h, w, c] -> [target, target, c]: horizontal then vertical integer pass, each
+    rounded (+half), shifted and clipped to 0..255."""
+    import numpy as np
+    h, w, c = img.shape
+    P = PIL_PRECISION_BITS
+
+    def run(src, coeffs, axis):
+        n = len(coeffs)
+        shape = list(src.shape)
+        shape[axis] = n
+        out = np.zeros(shape, np.int64)
+        for i, (xmin, k) in enumerate(coeffs):
+            kk = np.array(pil_fixed(k), np.int64)
+            seg = np.take(src, range(xmin, xmin + len(kk)), axis=axis).astype(np.int64)
+            acc = np.tensordot(seg, kk, axes=([axis], [0])) + (1 << (P - 1))
+            idx = [slice(None)] * src.ndim
+            idx[axis] = i
+            out[tuple(idx)] = np.clip(acc >> P, 0, 255)
+        return out
+
+    tmp = run(img, pil_coeffs(w, target), 1)
+    return run(tmp, pil_coeffs(h, target), 0).astype(np.uint8)
+
+
+def pil_resize_u16(img, target: int):
+    """'I;16' [h, w] -> [target, target]: double accumulation in tap order, round half away from
+    zero, stored as CLIP8(v % 256) | CLIP8(v >> 8) << 8 after each pass (Pillow's 16-bit path)."""
+    import numpy as np
+    h, w = img.shape
+
+    def store(v):
+        vi = np.where(v >= 0, np.trunc(v + 0.5), np.trunc(v - 0.5)).astype(np.int64)
+        return np.clip(np.fmod(vi, 256), 0, 255) + (np.clip(vi >> 8, 0, 255) << 8)
+
+    tmp = np.zeros((h, target), np.int64)
+    for xx, (xmin, k) in enumerate(pil_coeffs(w, target)):
+        acc = np.zeros(h)
+        for j, kw in enumerate(k):
+            acc = acc + img[:, xmin + j].astype(np.float64) * kw
+        tmp[:, xx] = store(acc)
+    out = np.zeros((target, target), np.int64)
+    for yy, (ymin, k) in enumerate(pil_coeffs(h, target)):
+        acc = np.zeros(target)
+        for j, kw in enumerate(k):
+            acc = acc + tmp[ymin + j].astype(np.float64) * kw
+        out[yy] = store(acc)
+    return out.astype(np.uint16)
+
+
+def preprocess_image(img, target: int = 518, is_depth: bool = False):
+    """ImagePreprocessor.process_image_with_matrices (io.py:75-195) on a uint8 [h, w, 3] RGB or
+    uint16 [h, w] depth array: (tensor [1, C, T, T] fp32, K_to_K_prime, K_prime_to_K)."""
+    import numpy as np
+    h, w = img.shape[:2]
+    m = max(h, w)
+    pl, pt = (m - w) // 2, (m - h) // 2
+    sq = np.zeros((m, m) + img.shape[2:], img.dtype)
+    sq[pt:pt + h, pl:pl + w] = img
+    if is_depth:
+        r = pil_resize_u16(sq, target).astype(np.float32) / 1000
+        t = torch.from_numpy(r)[None]
+    else:
+        r = pil_resize_u8(sq, target)
+        t = torch.from_numpy(r).permute(2, 0, 1).float().div(255)
+    s = target / m
+    k2kp = torch.tensor([[s, 0.0, pl * s], [0.0, s, pt * s], [0.0, 0.0, 1.0]], dtype=torch.float32)
+    kp2k = torch.tensor([[1.0 / s, 0.0, -(pl * s) / s], [0.0, 1.0 / s, -(pt * s) / s], [0.0, 0.0, 1.0]],
+                        dtype=torch.float32)
+    return t[None], k2kp, kp2k

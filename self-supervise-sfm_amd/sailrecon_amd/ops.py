@@ -349,3 +349,32 @@ def unproject_depth(depth: Tensor, extrinsic: Tensor, intrinsic: Tensor, out: Te
             raise ValueError(f"unproject_depth: {name} must be a contiguous fp32 device tensor")
     check(_lib.load().sr_unproject_depth_f32(_stream(depth), _p(depth), _p(extrinsic), _p(intrinsic), s, h, w,
                                              _p(out)), "sr_unproject_depth_f32")
+
+
+# ---------------------------------------------------------------- input formation (io.py:75-153)
+def pil_resample_h(mode: int, img: Tensor, canvas_h: int, canvas_w: int, pad_left: int, pad_top: int,
+                   bounds: Tensor, coeffs: Tensor, tw: int, tmp: Tensor) -> None:
+    """img [n, h, w, c] uint8 (mode 0) / [n, h, w, 1] int16-viewed uint16 (mode 1) -> tmp [n, canvas_h, tw, c]."""
+    n, h, w, c = img.shape
+    if not img.is_contiguous() or not tmp.is_contiguous() or tmp.shape != (n, canvas_h, tw, c):
+        raise ValueError(f"pil_resample_h: img {tuple(img.shape)} / tmp {tuple(tmp.shape)} mismatch")
+    if bounds.shape[0] < tw or coeffs.shape[0] < tw:
+        raise ValueError("pil_resample_h: table shorter than the output width")
+    check(_lib.load().sr_pil_resample_h(_stream(img), mode, _p(img), n, h, w, c, canvas_h, canvas_w, pad_left,
+                                        pad_top, _p(bounds), _p(coeffs), coeffs.shape[1], tw, _p(tmp)),
+          "sr_pil_resample_h")
+
+
+def pil_resample_v(mode: int, tmp: Tensor, bounds: Tensor, coeffs: Tensor, divisor: float, out: Tensor) -> None:
+    """tmp [n, rows, tw, c] -> out [n, c, th, tw] fp32 (any strides with unit column stride); the
+    table rows [0, th) are the output rows (slice the table for a crop)."""
+    n, rows, tw, c = tmp.shape
+    if out.dim() != 4 or out.shape[0] != n or out.shape[1] != c or out.shape[3] != tw or out.stride(3) != 1 \
+            or out.dtype != torch.float32:
+        raise ValueError(f"pil_resample_v: out {tuple(out.shape)} does not match tmp {tuple(tmp.shape)}")
+    th = out.shape[2]
+    if bounds.shape[0] < th or coeffs.shape[0] < th:
+        raise ValueError("pil_resample_v: table shorter than the output height")
+    check(_lib.load().sr_pil_resample_v_f32(_stream(tmp), mode, _p(tmp), n, rows, tw, c, _p(bounds), _p(coeffs),
+                                            coeffs.shape[1], th, float(divisor), _p(out), out.stride(0),
+                                            out.stride(1), out.stride(2)), "sr_pil_resample_v_f32")

@@ -63,3 +63,71 @@ def dpt_small_model_sd(kind):
     from sailrecon_amd.utils.synth_weights import synth_state_dict_like
     m = DPTHead(**DPT_SMALL, **DPT_HEADS[kind])
     return m, synth_state_dict_like(m)
+
+
+# ---------------------------------------------------------------- input formation (§8(f) rank 2)
+def pil_process_reference(arr, target, is_depth):
+    """train/utils/io.py:118-153 step by step with Pillow, which is what the reference calls
+    (torchvision's ToTensor is uint8 -> float / 255).  Returns [1, C, T, T] fp32 (host)."""
+    from PIL import Image
+    img = Image.fromarray(arr) if is_depth else Image.fromarray(arr).convert("RGB")
+    w, h = img.size
+    m = max(w, h)
+    if m != w or m != h:
+        sq = Image.new(img.mode, (m, m), color=0)
+        sq.paste(img, ((m - w) // 2, (m - h) // 2))
+        img = sq
+    img = img.resize((target, target), Image.Resampling.BICUBIC)
+    a = np.array(img)
+    if is_depth:
+        return torch.from_numpy(a.astype(np.float32) / 1000)[None][None]
+    return torch.from_numpy(a).permute(2, 0, 1).float().div(255)[None]
+
+
+def pil_load_reference(images, mode=None, square_target=None):
+    """sailrecon/utils/load_fn.py:13-96 (square_target set) or :99-240 (mode "crop"/"pad") with
+    Pillow + torch on the host, on PIL images instead of paths."""
+    from PIL import Image
+    T = 518
+    outs, coords = [], []
+    for img in images:
+        if img.mode == "RGBA":
+            bg = Image.new("RGBA", img.size, (255, 255, 255, 255))
+            img = Image.alpha_composite(bg, img)
+        img = img.convert("RGB")
+        w, h = img.size
+        if square_target is not None:
+            m = max(w, h)
+            left, top = (m - w) // 2, (m - h) // 2
+            s = square_target / m
+            coords.append(np.array([left * s, top * s, (left + w) * s, (top + h) * s, w, h]))
+            sq = Image.new("RGB", (m, m), (0, 0, 0))
+            sq.paste(img, (left, top))
+            sq = sq.resize((square_target, square_target), Image.Resampling.BICUBIC)
+            outs.append(torch.from_numpy(np.array(sq)).permute(2, 0, 1).float().div(255))
+            continue
+        if mode == "pad" and w < h:
+            nh, nw = T, round(w * (T / h) / 14) * 14
+        else:
+            nw, nh = T, round(h * (T / w) / 14) * 14
+        t = torch.from_numpy(np.array(img.resize((nw, nh), Image.Resampling.BICUBIC))).permute(2, 0, 1)
+        t = t.float().div(255)
+        if mode == "crop" and nh > T:
+            y0 = (nh - T) // 2
+            t = t[:, y0:y0 + T, :]
+        if mode == "pad":
+            hp, wp = T - t.shape[1], T - t.shape[2]
+            if hp > 0 or wp > 0:
+                t = torch.nn.functional.pad(t, (wp // 2, wp - wp // 2, hp // 2, hp - hp // 2), value=1.0)
+        outs.append(t)
+    if square_target is not None:
+        return torch.stack(outs), torch.from_numpy(np.array(coords)).float()
+    H = max(t.shape[1] for t in outs)
+    W = max(t.shape[2] for t in outs)
+    padded = []
+    for t in outs:
+        hp, wp = H - t.shape[1], W - t.shape[2]
+        if hp > 0 or wp > 0:
+            t = torch.nn.functional.pad(t, (wp // 2, wp - wp // 2, hp // 2, hp - hp // 2), value=1.0)
+        padded.append(t)
+    return torch.stack(padded)

@@ -171,3 +171,48 @@ def test_kvcache_reloc_equals_one_pass_oracle():
                          activation=DPT_HEADS["depth"]["activation"])
     assert rel_l2(d[0].numpy(), g[f"depth_map_{i}"]) < 1e-5
     assert rel_l2(c[0].numpy(), g[f"dpt_cnf_{i}"]) < 1e-5
+
+
+# ---------------------------------------------------------------- input formation (§8(f) rank 2)
+from goldens import pil_process_reference  # noqa: E402
+
+
+@pytest.mark.parametrize("hw", [(300, 400), (97, 61), (518, 518), (640, 480), (1000, 777)])
+def test_input_formation_oracle_bit_exact_vs_pil(hw):
+    rng = np.random.default_rng(hw[0] * hw[1])
+    rgb = rng.integers(0, 256, hw + (3,), dtype=np.uint8)
+    dep = rng.integers(0, 65536, hw, dtype=np.uint16)
+    t, k2kp, kp2k = O.preprocess_image(rgb, 518)
+    assert torch.equal(t, pil_process_reference(rgb, 518, False))
+    d, _, _ = O.preprocess_image(dep, 518, is_depth=True)
+    assert torch.equal(d, pil_process_reference(dep, 518, True))
+    K = torch.tensor([[500.0, 0, hw[1] / 2], [0, 510.0, hw[0] / 2], [0, 0, 1]])
+    assert torch.allclose(kp2k @ (k2kp @ K), K, rtol=1e-6)
+
+
+def test_input_formation_tables_match_oracle():
+    """The host-built tables the HIP path uploads (utils/io.py pil_table) equal the oracle's
+    restatement of Pillow's coefficients (8-bit fixed point and double)."""
+    from sailrecon_amd.utils import io
+    for i, o in ((1000, 518), (777, 518), (518, 518), (97, 518), (518, 1024), (1, 7)):
+        b8, k8 = io.pil_table(i, o, io.MODE_8BIT, "cpu")
+        b16, k16 = io.pil_table(i, o, io.MODE_I16, "cpu")
+        assert torch.equal(b8, b16)
+        for xx, (xmin, kk) in enumerate(O.pil_coeffs(i, o)):
+            assert b8[xx].tolist() == [xmin, len(kk)]
+            assert k8[xx, :len(kk)].tolist() == O.pil_fixed(kk)
+            assert k16[xx, :len(kk)].tolist() == kk
+            assert not k8[xx, len(kk):].any() and not k16[xx, len(kk):].any()
+
+
+def test_transformation_matrices_match_reference_formula():
+    from sailrecon_amd.utils.io import ImagePreprocessor
+    pre = ImagePreprocessor(518, device="cpu")
+    for h, w in ((300, 400), (640, 480), (518, 518)):
+        m = max(h, w)
+        pl, pt = (m - w) // 2, (m - h) // 2
+        s = 518 / m
+        k2kp, kp2k = pre._create_transformation_matrices({"scale_x": s, "scale_y": s, "offset_x": pl * s,
+                                                         "offset_y": pt * s})
+        _, r1, r2 = O.preprocess_image(np.zeros((h, w, 3), np.uint8), 518)
+        assert torch.equal(k2kp, r1) and torch.equal(kp2k, r2)

@@ -32,6 +32,8 @@ for step in "$@"; do
     kgemm_reg) run kgemm_reg 300 env SR_GEMM_REG_EPI=1 python tools/kbench.py gemm ;;
     kdpt)    run kdpt 600 python tools/kbench.py dpt ;;
     kreloc)  run kreloc 600 python tools/kbench.py reloc ;;
+    kio)     run kio 300 python tools/kbench.py io ;;
+    io_tests) run io_tests 600 python -m pytest tests/test_io_gpu.py -q -x ;;
     kattn)   run kattn 300 python tools/kbench.py attn ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;

@@ -128,6 +128,53 @@ def reloc():
     print(f"tmp_forward {n} anchors @518            {ms1:8.2f} ms")
 
 
+def io():
+    """Input formation: 32 views 768x1024 -> 518 (pad to square, Pillow
+    BICUBIC, ToTensor), RGB and uint16 depth; kernel passes with pixels resident in HBM, then the
+    whole ImagePreprocessor.process_views from PIL images (host decode arrays + H2D included),
+    beside Pillow on one host core."""
+    import numpy as np
+    from PIL import Image
+    from sailrecon_amd.utils import io as sio
+    n, h, w, T = 32, 768, 1024, 518
+    m, pl, pt = max(h, w), 0, (max(h, w) - h) // 2
+    rng = np.random.default_rng(0)
+    rgb = rng.integers(0, 256, (n, h, w, 3), dtype=np.uint8)
+    dep = rng.integers(0, 65536, (n, h, w), dtype=np.uint16)
+    for mode, arr, c, esz in ((sio.MODE_8BIT, rgb, 3, 1), (sio.MODE_I16, dep, 1, 2)):
+        pix = sio._upload(list(arr), DEV)
+        bh, kh = sio.pil_table(m, T, mode, DEV)
+        bv, kv = sio.pil_table(m, T, mode, DEV)
+        tmp = torch.empty(n, m, T, c, dtype=pix.dtype, device=DEV)
+        out = torch.empty(n, c, T, T, device=DEV)
+        div = 255.0 if mode == sio.MODE_8BIT else 1000.0
+        th_ = timeit(lambda: ops.pil_resample_h(mode, pix, m, m, pl, pt, bh, kh, T, tmp), reps=20)
+        tv_ = timeit(lambda: ops.pil_resample_v(mode, tmp, bv, kv, div, out), reps=20)
+        bh_ = n * (h * w * c * esz + m * T * c * esz)
+        bv_ = n * (m * T * c * esz + c * T * T * 4)
+        name = "rgb  " if mode == sio.MODE_8BIT else "depth"
+        print(f"io {name} h pass {th_ * 1e3:8.1f} us  {bh_ / th_ / 1e6:7.1f} GB/s   "
+              f"v pass {tv_ * 1e3:8.1f} us  {bv_ / tv_ / 1e6:7.1f} GB/s   ({(th_ + tv_) / n * 1e3:.1f} us/view)")
+    pre = sio.ImagePreprocessor(T, device=DEV)
+    ims = [Image.fromarray(a) for a in rgb]
+    dims = [Image.fromarray(a) for a in dep]
+    ms = timeit(lambda: pre.process_views(ims), reps=3, warm=1)
+    msd = timeit(lambda: pre.process_views(dims, is_depth=True), reps=3, warm=1)
+    print(f"io process_views from PIL (incl. host arrays + H2D): rgb {ms / n:.3f} ms/view  depth {msd / n:.3f} ms/view")
+    t0 = time.perf_counter()
+    for im in ims[:8]:
+        sq = Image.new("RGB", (m, m))
+        sq.paste(im, (pl, pt))
+        np.asarray(sq.resize((T, T), Image.Resampling.BICUBIC), dtype=np.float32) / 255
+    t1 = time.perf_counter()
+    for im in dims[:4]:
+        sq = Image.new(im.mode, (m, m))
+        sq.paste(im, (pl, pt))
+        np.asarray(sq.resize((T, T), Image.Resampling.BICUBIC)).astype(np.float32) / 1000
+    t2 = time.perf_counter()
+    print(f"io Pillow on 1 host core: rgb {(t1 - t0) / 8 * 1e3:.2f} ms/view  depth {(t2 - t1) / 4 * 1e3:.2f} ms/view")
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["attn", "gemm", "ln"]
     for w in which:
