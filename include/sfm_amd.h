@@ -226,17 +226,20 @@ int sr_unproject_depth_f32(sr_stream_t stream, const float* depth, const float* 
  * `side`, PIL Image.resize((t, t), BICUBIC), ToTensor (RGB / 255) or uint16 depth / 1000.
  * Bit-exact with Pillow's separable resampler.  Tables per axis (host-built, Pillow's filter):
  * bounds[o] = {first input index, tap count}, coeffs[o][ksize] = int32 22-bit fixed point
- * (mode 0, 8-bit) or double (mode 1, 'I;16').
+ * (mode 0, 8-bit) or double (mode 1, 'I;16'); the horizontal pass takes them quad-major.
  * ------------------------------------------------------------------------------------------ */
-/* Horizontal pass: img [n][h][w][c] (uint8, mode 0, c <= 4; uint16, mode 1, c == 1) pasted at
- * (pad_left, pad_top) into a zero canvas [canvas_h][canvas_w] -> tmp [n][canvas_h][tw][c] of the same
- * element type (tw = output width; bounds/coeffs: the canvas_w -> tw table). */
-int sr_pil_resample_h(sr_stream_t stream, int mode, const void* img, int n, int h, int w, int c, int canvas_h,
-                      int canvas_w, int pad_left, int pad_top, const int* bounds, const void* coeffs, int ksize,
-                      int tw, void* tmp);
-/* Vertical pass + ToTensor: tmp [n][rows][tw][c] -> out[f * frame_stride + ch * chan_stride + y * ldo + x]
+/* Horizontal pass: img [n][h][w][c] (uint8, mode 0, c <= 4; uint16, mode 1, c == 1) -> planar tmp
+ * [n][c][h][ldt] of the same element type, ldt = tw rounded up to a multiple of 4 (columns >= tw
+ * are 0).  bounds/coeffs: the w -> tw table in image coordinates (the canvas padding folded in:
+ * taps on padding dropped) in quad-major layout, one entry per 4 output columns: bounds int32
+ * [ldt/4][2][4] (first indices, tap counts), coeffs [ldt/4][ksize][4] (0 past a column's taps).
+ * SR_EUNSUPPORTED for image rows over 64 KiB. */
+int sr_pil_resample_h(sr_stream_t stream, int mode, const void* img, int n, int h, int w, int c, const int* bounds,
+                      const void* coeffs, int ksize, int tw, void* tmp);
+/* Vertical pass + ToTensor: tmp [n][c][rows][ldt] -> out[f * frame_stride + ch * chan_stride + y * ldo + x]
  * = stored value / divisor (255 for RGB, 1000 for depth), fp32, for th output rows (bounds/coeffs:
- * the rows -> output table, offset by the first output row for a centre crop). */
+ * the image-row table [th][2] / [th][ksize], padding folded in like the horizontal one, offset
+ * by the first output row for a centre crop). */
 int sr_pil_resample_v_f32(sr_stream_t stream, int mode, const void* tmp, int n, int rows, int tw, int c,
                           const int* bounds, const void* coeffs, int ksize, int th, float divisor, float* out,
                           int64_t frame_stride, int64_t chan_stride, int64_t ldo);

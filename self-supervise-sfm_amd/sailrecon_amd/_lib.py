@@ -70,8 +70,7 @@ _PROTOS = {
     "sr_dpt_pos_embed_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _f32, _f32]),
     "sr_dpt_head_out_f32": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
     "sr_unproject_depth_f32": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp]),
-    "sr_pil_resample_h": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32,
-                                 _i32, _vp]),
+    "sr_pil_resample_h": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _vp]),
     "sr_pil_resample_v_f32": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _f32, _vp,
                                      _i64, _i64, _i64]),
     "sr_layernorm": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _f32, _vp, _i64, _i32, _i32]),

@@ -352,25 +352,26 @@ def unproject_depth(depth: Tensor, extrinsic: Tensor, intrinsic: Tensor, out: Te
 
 
 # ---------------------------------------------------------------- input formation (io.py:75-153)
-def pil_resample_h(mode: int, img: Tensor, canvas_h: int, canvas_w: int, pad_left: int, pad_top: int,
-                   bounds: Tensor, coeffs: Tensor, tw: int, tmp: Tensor) -> None:
-    """img [n, h, w, c] uint8 (mode 0) / [n, h, w, 1] int16-viewed uint16 (mode 1) -> tmp [n, canvas_h, tw, c]."""
+def pil_resample_h(mode: int, img: Tensor, bounds: Tensor, coeffs: Tensor, tw: int, tmp: Tensor) -> None:
+    """img [n, h, w, c] uint8 (mode 0) / [n, h, w, 1] int16-viewed uint16 (mode 1) -> planar tmp
+    [n, c, h, ldt], ldt = tw rounded up to 4 (see pil_tmp); quad-major image-space table."""
     n, h, w, c = img.shape
-    if not img.is_contiguous() or not tmp.is_contiguous() or tmp.shape != (n, canvas_h, tw, c):
+    if not img.is_contiguous() or not tmp.is_contiguous() or tmp.shape != (n, c, h, (tw + 3) // 4 * 4) \
+            or tmp.dtype != img.dtype:
         raise ValueError(f"pil_resample_h: img {tuple(img.shape)} / tmp {tuple(tmp.shape)} mismatch")
-    if bounds.shape[0] < tw or coeffs.shape[0] < tw:
-        raise ValueError("pil_resample_h: table shorter than the output width")
-    check(_lib.load().sr_pil_resample_h(_stream(img), mode, _p(img), n, h, w, c, canvas_h, canvas_w, pad_left,
-                                        pad_top, _p(bounds), _p(coeffs), coeffs.shape[1], tw, _p(tmp)),
-          "sr_pil_resample_h")
+    if bounds.dim() != 3 or coeffs.dim() != 3 or bounds.shape[0] != (tw + 3) // 4 or coeffs.shape[0] != bounds.shape[0]:
+        raise ValueError("pil_resample_h: needs the quad-major table for the output width (pil_table(quads=True))")
+    check(_lib.load().sr_pil_resample_h(_stream(img), mode, _p(img), n, h, w, c, _p(bounds), _p(coeffs),
+                                        coeffs.shape[1], tw, _p(tmp)), "sr_pil_resample_h")
 
 
 def pil_resample_v(mode: int, tmp: Tensor, bounds: Tensor, coeffs: Tensor, divisor: float, out: Tensor) -> None:
-    """tmp [n, rows, tw, c] -> out [n, c, th, tw] fp32 (any strides with unit column stride); the
-    table rows [0, th) are the output rows (slice the table for a crop)."""
-    n, rows, tw, c = tmp.shape
-    if out.dim() != 4 or out.shape[0] != n or out.shape[1] != c or out.shape[3] != tw or out.stride(3) != 1 \
-            or out.dtype != torch.float32:
+    """planar tmp [n, c, rows, ldt] -> out [n, c, th, tw] fp32 (any strides with unit column stride);
+    the table rows [0, th) are the output rows (slice the table for a crop)."""
+    n, c, rows, ldt = tmp.shape
+    tw = out.shape[3]
+    if out.dim() != 4 or out.shape[0] != n or out.shape[1] != c or ldt != (tw + 3) // 4 * 4 or out.stride(3) != 1 \
+            or out.dtype != torch.float32 or not tmp.is_contiguous():
         raise ValueError(f"pil_resample_v: out {tuple(out.shape)} does not match tmp {tuple(tmp.shape)}")
     th = out.shape[2]
     if bounds.shape[0] < th or coeffs.shape[0] < th:
@@ -378,3 +379,9 @@ def pil_resample_v(mode: int, tmp: Tensor, bounds: Tensor, coeffs: Tensor, divis
     check(_lib.load().sr_pil_resample_v_f32(_stream(tmp), mode, _p(tmp), n, rows, tw, c, _p(bounds), _p(coeffs),
                                             coeffs.shape[1], th, float(divisor), _p(out), out.stride(0),
                                             out.stride(1), out.stride(2)), "sr_pil_resample_v_f32")
+
+
+
+def pil_tmp(n: int, c: int, rows: int, tw: int, dtype: torch.dtype, device) -> Tensor:
+    """Planar intermediate of the two resample passes: [n, c, rows, tw rounded up to 4]."""
+    return torch.empty(n, c, rows, (tw + 3) // 4 * 4, dtype=dtype, device=device)

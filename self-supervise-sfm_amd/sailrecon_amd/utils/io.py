@@ -37,13 +37,10 @@ def _bicubic(x: float) -> float:
     return 0.0
 
 
-def pil_table(in_size: int, out_size: int, mode: int, device) -> Tuple[Tensor, Tensor]:
+def pil_coeffs(in_size: int, out_size: int, mode: int) -> Tuple[np.ndarray, np.ndarray]:
     """Pillow's resample coefficients for one axis (Resample.c precompute_coeffs, bicubic,
-    box = whole axis): bounds int32 [out, 2] = (first input index, taps) and coeffs [out, ksize]
-    (int32 22-bit fixed point for 8-bit modes, float64 for 'I;16'), cached on ``device``."""
-    key = (in_size, out_size, mode, str(device))
-    if key in _TABLES:
-        return _TABLES[key]
+    box = whole axis): bounds int32 [out, 2] = (first input index, taps) and weights [out, ksize]
+    (int32 22-bit fixed point for 8-bit modes, float64 for 'I;16'; 0 past a column's taps)."""
     scale = in_size / out_size
     fs = max(scale, 1.0)
     support, ss = 2.0 * fs, 1.0 / fs
@@ -60,22 +57,66 @@ def pil_table(in_size: int, out_size: int, mode: int, device) -> Tuple[Tensor, T
             kk[xx, x] = w[x] / tot if tot != 0.0 else w[x]
         bounds[xx] = (xmin, xmax)
     if mode == MODE_8BIT:
-        q = np.where(kk < 0, np.trunc(-0.5 + kk * (1 << _PREC)), np.trunc(0.5 + kk * (1 << _PREC)))
-        coeffs = torch.from_numpy(q.astype(np.int32))
-    else:
-        coeffs = torch.from_numpy(kk)
-    tab = (runtime.to_device(torch.from_numpy(bounds), device), runtime.to_device(coeffs, device))
+        kk = np.where(kk < 0, np.trunc(-0.5 + kk * (1 << _PREC)), np.trunc(0.5 + kk * (1 << _PREC))).astype(np.int32)
+    return bounds, kk
+
+
+def _fold_padding(bounds: np.ndarray, kk: np.ndarray, pad: int, extent: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Canvas table -> image table: the image occupies canvas [pad, pad + extent) and the rest of
+    the canvas is 0, so taps outside it are dropped (Pillow adds 0 * weight for them: +-0, which
+    leaves an integer or double sum unchanged) and the first index becomes image-relative."""
+    b = np.zeros_like(bounds)
+    k = np.zeros_like(kk)
+    for o, (xmin, cnt) in enumerate(bounds):
+        lo, hi = max(xmin, pad), min(xmin + cnt, pad + extent)
+        if hi > lo:
+            b[o] = (lo - pad, hi - lo)
+            k[o, :hi - lo] = kk[o, lo - xmin:hi - xmin]
+    return b, k
+
+
+def _quad_major(bounds: np.ndarray, kk: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """[out, 2] / [out, ksize] -> [ceil(out/4), 2, 4] / [ceil(out/4), ksize, 4] (outputs past the
+    end get no taps)."""
+    out, ksize = kk.shape
+    nq = (out + 3) // 4
+    b = np.zeros((nq * 4, 2), np.int32)
+    b[:out] = bounds
+    c = np.zeros((nq * 4, ksize), kk.dtype)
+    c[:out] = kk
+    return (np.ascontiguousarray(b.reshape(nq, 4, 2).transpose(0, 2, 1)),
+            np.ascontiguousarray(c.reshape(nq, 4, ksize).transpose(0, 2, 1)))
+
+
+def pil_table(in_size: int, out_size: int, mode: int, device, quads: bool = False, pad: int = 0,
+              extent: int = None) -> Tuple[Tensor, Tensor]:
+    """Device tables for one axis of a canvas of ``in_size`` pixels holding the image at
+    [pad, pad + extent) (zeros elsewhere), cached per shape.  ``quads``: the horizontal pass's
+    quad-major layout.  Default pad/extent: the plain Pillow table of the whole axis."""
+    extent = in_size if extent is None else extent
+    key = (in_size, out_size, mode, str(device), quads, pad, extent)
+    if key in _TABLES:
+        return _TABLES[key]
+    bounds, kk = pil_coeffs(in_size, out_size, mode)
+    if pad != 0 or extent != in_size:
+        bounds, kk = _fold_padding(bounds, kk, pad, extent)
+    if quads:
+        bounds, kk = _quad_major(bounds, kk)
+    tab = (runtime.to_device(torch.from_numpy(bounds), device), runtime.to_device(torch.from_numpy(kk), device))
     _TABLES[key] = tab
     return tab
 
 
-def _identity_table(n: int, mode: int, device) -> Tuple[Tensor, Tensor]:
-    key = (-n, n, mode, str(device))
+def _identity_table(n: int, mode: int, device, quads: bool = False) -> Tuple[Tensor, Tensor]:
+    """One tap of weight 1 per output (ToTensor without resizing: both passes copy exactly)."""
+    key = (-n, n, mode, str(device), quads)
     if key not in _TABLES:
-        bounds = torch.stack([torch.arange(n, dtype=torch.int32), torch.ones(n, dtype=torch.int32)], 1)
-        coeffs = torch.full((n, 1), 1 << _PREC, dtype=torch.int32) if mode == MODE_8BIT \
-            else torch.ones(n, 1, dtype=torch.float64)
-        _TABLES[key] = (runtime.to_device(bounds, device), runtime.to_device(coeffs, device))
+        bounds = np.stack([np.arange(n, dtype=np.int32), np.ones(n, dtype=np.int32)], 1)
+        coeffs = np.full((n, 1), 1 << _PREC, np.int32) if mode == MODE_8BIT else np.ones((n, 1), np.float64)
+        if quads:
+            bounds, coeffs = _quad_major(bounds, coeffs)
+        _TABLES[key] = (runtime.to_device(torch.from_numpy(bounds), device),
+                        runtime.to_device(torch.from_numpy(coeffs), device))
     return _TABLES[key]
 
 
@@ -86,7 +127,7 @@ def _pixels(image, is_depth: bool) -> np.ndarray:
         if a.dtype != np.uint16 or a.ndim != 2:
             raise ValueError(f"depth images must be uint16 'I;16' [h, w] (got {a.dtype} {a.shape})")
         return a
-    if hasattr(image, "convert"):
+    if hasattr(image, "convert") and image.mode != "RGB":
         image = image.convert("RGB")
     a = np.asarray(image)
     if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
@@ -113,15 +154,17 @@ def resample_into(pix: Tensor, mode: int, canvas: Tuple[int, int], pad: Tuple[in
                   out: Tensor, row0: int = 0) -> None:
     """pix [n, h, w, c] on device, pasted at pad=(left, top) into a zero canvas=(h, w), resized
     (Pillow BICUBIC) to size=(th_full, tw); output rows [row0, row0 + out.shape[2]) go to out
-    [n, c, rows, tw] (fp32, strided) scaled by 1/255 (RGB) or 1/1000 (depth)."""
+    [n, c, rows, tw] (fp32, strided) scaled by 1/255 (RGB) or 1/1000 (depth).  The canvas
+    padding lives only in the tables (taps on it are dropped), so both passes touch image pixels only."""
     n, h, w, c = pix.shape
     ch_, cw_ = canvas
     th_full, tw = size
-    bh, kh = pil_table(cw_, tw, mode, pix.device)
-    bv, kv = pil_table(ch_, th_full, mode, pix.device)
-    tmp = torch.empty(n, ch_, tw, c, dtype=pix.dtype, device=pix.device)
-    ops.pil_resample_h(mode, pix, ch_, cw_, pad[0], pad[1], bh, kh, tw, tmp)
-    ops.pil_resample_v(mode, tmp, bv[row0:], kv[row0:], 255.0 if mode == MODE_8BIT else 1000.0, out)
+    bh, kh = pil_table(cw_, tw, mode, pix.device, quads=True, pad=pad[0], extent=w)
+    bv, kv = pil_table(ch_, th_full, mode, pix.device, pad=pad[1], extent=h)
+    div = 255.0 if mode == MODE_8BIT else 1000.0
+    tmp = ops.pil_tmp(n, c, h, tw, pix.dtype, pix.device)
+    ops.pil_resample_h(mode, pix, bh, kh, tw, tmp)
+    ops.pil_resample_v(mode, tmp, bv[row0:], kv[row0:], div, out)
 
 
 class ImagePreprocessor:
@@ -141,8 +184,11 @@ class ImagePreprocessor:
         pix = _upload([a], self.device)
         _, h, w, c = pix.shape
         out = torch.empty(1, c, h, w, device=self.device)
-        bounds, coeffs = _identity_table(h, mode, self.device)
-        ops.pil_resample_v(mode, pix, bounds, coeffs, 255.0 if mode == MODE_8BIT else 1000.0, out)
+        bh, kh = _identity_table(w, mode, self.device, quads=True)
+        bv, kv = _identity_table(h, mode, self.device)
+        tmp = ops.pil_tmp(1, c, h, w, pix.dtype, self.device)
+        ops.pil_resample_h(mode, pix, bh, kh, w, tmp)
+        ops.pil_resample_v(mode, tmp, bv, kv, 255.0 if mode == MODE_8BIT else 1000.0, out)
         return out[0]
 
     @staticmethod

@@ -108,3 +108,18 @@ def test_load_and_preprocess_images_square():
     ref, rcoords = pil_load_reference(ims, square_target=1024)
     assert torch.equal(got.cpu(), ref)
     assert torch.equal(coords, rcoords)
+
+
+def test_wide_rows_and_steep_downscale_bit_exact():
+    """Rows staged in LDS in bands of 1..8; a 7000-wide canvas (one row per band, 21 KB rows) and a
+    tall one (7000 rows -> 518, 14:1 vertical)."""
+    from PIL import Image
+    from sailrecon_amd.utils.io import ImagePreprocessor
+    pre = ImagePreprocessor(518, device=DEV)
+    for hw in ((40, 7000), (7000, 33)):
+        rgb = _rgb(hw, 41)
+        t, _, _ = pre(Image.fromarray(rgb))
+        assert torch.equal(t.cpu(), pil_process_reference(rgb, 518, False)), hw
+        dep = _depth(hw, 42)
+        d, _, _ = pre(Image.fromarray(dep), is_depth=True)
+        assert torch.equal(d.cpu(), pil_process_reference(dep, 518, True)), hw

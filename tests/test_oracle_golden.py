@@ -203,6 +203,13 @@ def test_input_formation_tables_match_oracle():
             assert k8[xx, :len(kk)].tolist() == O.pil_fixed(kk)
             assert k16[xx, :len(kk)].tolist() == kk
             assert not k8[xx, len(kk):].any() and not k16[xx, len(kk):].any()
+        for mode, k in ((io.MODE_8BIT, k8), (io.MODE_I16, k16)):  # quad-major layout of the h pass
+            bq, kq = io.pil_table(i, o, mode, "cpu", quads=True)
+            nq = (o + 3) // 4
+            assert bq.shape == (nq, 2, 4) and kq.shape == (nq, k.shape[1], 4)
+            assert torch.equal(bq.permute(0, 2, 1).reshape(-1, 2)[:o], b8)
+            assert torch.equal(kq.permute(0, 2, 1).reshape(-1, k.shape[1])[:o], k)
+            assert not bq.permute(0, 2, 1).reshape(-1, 2)[o:].any()
 
 
 def test_transformation_matrices_match_reference_formula():
@@ -216,3 +223,34 @@ def test_transformation_matrices_match_reference_formula():
                                                          "offset_y": pt * s})
         _, r1, r2 = O.preprocess_image(np.zeros((h, w, 3), np.uint8), 518)
         assert torch.equal(k2kp, r1) and torch.equal(kp2k, r2)
+
+
+def test_padding_folded_tables_equal_canvas_tables():
+    """Dropping the taps that land on the zero padding (utils/io.py _fold_padding) gives the same
+    integer and double sums as Pillow's pass over the padded canvas."""
+    from sailrecon_amd.utils import io
+    rng = np.random.default_rng(5)
+    for canvas, extent, out in ((1024, 768, 518), (640, 480, 518), (97, 61, 518), (7000, 40, 518)):
+        pad = (canvas - extent) // 2
+        img = rng.integers(0, 65536, (3, extent)).astype(np.int64)
+        full = np.zeros((3, canvas), np.int64)
+        full[:, pad:pad + extent] = img
+        for mode in (io.MODE_8BIT, io.MODE_I16):
+            bc, kc = io.pil_coeffs(canvas, out, mode)
+            bf, kf = io._fold_padding(bc, kc, pad, extent)
+            for o in range(out):
+                x0, n0 = bc[o]
+                x1, n1 = bf[o]
+                assert 0 <= x1 and x1 + n1 <= extent
+                if mode == io.MODE_8BIT:
+                    a = (full[:, x0:x0 + n0] * kc[o, :n0]).sum(1)
+                    b = (img[:, x1:x1 + n1] * kf[o, :n1]).sum(1)
+                    assert np.array_equal(a, b)
+                else:
+                    for r in range(3):
+                        a = b = 0.0
+                        for t in range(n0):
+                            a += float(full[r, x0 + t]) * kc[o, t]
+                        for t in range(kf.shape[1]):  # the kernel runs all taps (zeros past n1)
+                            b += float(img[r, min(x1 + t, extent - 1)]) * kf[o, t]
+                        assert a == b and np.signbit(a) == np.signbit(b)

@@ -143,18 +143,21 @@ def io():
     dep = rng.integers(0, 65536, (n, h, w), dtype=np.uint16)
     for mode, arr, c, esz in ((sio.MODE_8BIT, rgb, 3, 1), (sio.MODE_I16, dep, 1, 2)):
         pix = sio._upload(list(arr), DEV)
-        bh, kh = sio.pil_table(m, T, mode, DEV)
-        bv, kv = sio.pil_table(m, T, mode, DEV)
-        tmp = torch.empty(n, m, T, c, dtype=pix.dtype, device=DEV)
+        bh, kh = sio.pil_table(m, T, mode, DEV, quads=True, pad=pl, extent=w)
+        bv, kv = sio.pil_table(m, T, mode, DEV, pad=pt, extent=h)
+        tmp = ops.pil_tmp(n, c, h, T, pix.dtype, DEV)
         out = torch.empty(n, c, T, T, device=DEV)
         div = 255.0 if mode == sio.MODE_8BIT else 1000.0
-        th_ = timeit(lambda: ops.pil_resample_h(mode, pix, m, m, pl, pt, bh, kh, T, tmp), reps=20)
+        th_ = timeit(lambda: ops.pil_resample_h(mode, pix, bh, kh, T, tmp), reps=20)
         tv_ = timeit(lambda: ops.pil_resample_v(mode, tmp, bv, kv, div, out), reps=20)
-        bh_ = n * (h * w * c * esz + m * T * c * esz)
-        bv_ = n * (m * T * c * esz + c * T * T * 4)
         name = "rgb  " if mode == sio.MODE_8BIT else "depth"
+        ldt = (T + 3) // 4 * 4
+        bh_ = n * (h * w * c * esz + h * ldt * c * esz)
+        bv_ = n * (h * ldt * c * esz + c * T * T * 4)
+        ba_ = n * (h * w * c * esz + c * T * T * 4)
         print(f"io {name} h pass {th_ * 1e3:8.1f} us  {bh_ / th_ / 1e6:7.1f} GB/s   "
-              f"v pass {tv_ * 1e3:8.1f} us  {bv_ / tv_ / 1e6:7.1f} GB/s   ({(th_ + tv_) / n * 1e3:.1f} us/view)")
+              f"v pass {tv_ * 1e3:8.1f} us  {bv_ / tv_ / 1e6:7.1f} GB/s   ({(th_ + tv_) / n * 1e3:.1f} us/view; "
+              f"in+out {ba_ / n / 1e6:.2f} MB/view -> {ba_ / (th_ + tv_) / 1e6:.0f} GB/s)")
     pre = sio.ImagePreprocessor(T, device=DEV)
     ims = [Image.fromarray(a) for a in rgb]
     dims = [Image.fromarray(a) for a in dep]
