@@ -136,9 +136,37 @@ typedef struct sr_attn_desc {
   int64_t k1_bstride;
   int mask_mode, n_anchor;
   float scale;
+  float* lse;  /* optional (bf16 path): [batch][heads][lq] row log-sum-exp of scale*log2(e)*q.k
+                  (log2 domain), saved for sr_attention_bwd */
 } sr_attn_desc;
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
+
+/* ------------------------------------------------------------------------
+ * Attention backward (training step; the gradient of
+ * F.scaled_dot_product_attention in Attention.forward, attention.py:103-109), bf16 inputs,
+ * head_dim 64, the same key segments as the forward (frame / global / global_reloc):
+ *   delta = rowsum(dO * O);  P = exp2(scale*log2e*q.k - lse);  dS = P * (dO.v - delta)
+ *   dQ = scale * dS K,  dK = scale * dS^T Q,  dV = P^T dO      (fp32 outputs)
+ * A segment with batch stride 0 (the shared anchor subsample) gets the sum over every
+ * item's queries.  delta is caller workspace [batch][heads][lq].
+ * ---------------------------------------------------------------------- */
+typedef struct sr_attn_bwd_desc {
+  sr_attn_desc f;          /* the forward's description (q, k/v segments, o, sizes, scale, lse) */
+  const void* dout;        /* dO, bf16, o's layout */
+  int64_t lddo;
+  float* delta;            /* [batch][heads][lq] workspace */
+  float* dq;               /* fp32, q's layout */
+  int64_t lddq;
+  float* dk0;
+  float* dv0;
+  int64_t lddk0, lddv0;
+  float* dk1;
+  float* dv1;
+  int64_t lddk1, lddv1;
+} sr_attn_bwd_desc;
+
+int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* d);
 
 /* ------------------------------------------------------------------------
  * LayerNorm over the last dim of fp32 rows (block.py:50,70; camera_head.py:64-77;

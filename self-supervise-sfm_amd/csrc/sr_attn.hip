@@ -309,11 +309,14 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     for (int b = 0; b < QB; ++b) l_run[b] += ps[b][0] + ps[b][1];
   }
 
-  // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l
+  // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training)
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
-    const float inv = 1.f / sum_x32(l_run[b]);
+    const float lsum = sum_x32(l_run[b]);
+    const float inv = 1.f / lsum;
     const int qrow = qrow0 + 32 * b;
+    if (d.lse && hi == 0 && qrow < d.lq)
+      d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
     if (qrow < d.lq) {
       bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
 #pragma unroll

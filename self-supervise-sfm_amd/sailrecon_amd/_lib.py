@@ -51,6 +51,18 @@ class AttnDesc(ctypes.Structure):
         ("l1", _i32), ("k1_bstride", _i64),
         ("mask_mode", _i32), ("n_anchor", _i32),
         ("scale", _f32),
+        ("lse", _vp),
+    ]
+
+
+class AttnBwdDesc(ctypes.Structure):
+    _fields_ = [
+        ("f", AttnDesc),
+        ("dout", _vp), ("lddo", _i64),
+        ("delta", _vp),
+        ("dq", _vp), ("lddq", _i64),
+        ("dk0", _vp), ("dv0", _vp), ("lddk0", _i64), ("lddv0", _i64),
+        ("dk1", _vp), ("dv1", _vp), ("lddk1", _i64), ("lddv1", _i64),
     ]
 
 
@@ -62,6 +74,7 @@ _PROTOS = {
     "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
+    "sr_attention_bwd": (_i32, [_vp, ctypes.POINTER(AttnBwdDesc)]),
     "sr_im2col3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "sr_convt_scatter_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "sr_resize_bilinear_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),

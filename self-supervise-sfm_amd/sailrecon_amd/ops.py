@@ -180,8 +180,25 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
 def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
-              scale: Optional[float] = None, tag: Optional[str] = None) -> None:
-    """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc."""
+              scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None) -> None:
+    """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``lse``
+    (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd."""
+    d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
+                   k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
+                   n_anchor=n_anchor, scale=scale, lse=lse)
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
+    check(rc, "sr_attention")
+    if timed:
+        es = q.element_size()
+        kv_rows = (l0 if k0_bstride == 0 else batch * l0) + batch * l1  # shared segment read once
+        nb = es * heads * head_dim * (2 * batch * lq + 2 * kv_rows)
+        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim, nb)
+
+
+def _attn_desc(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
+               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, lse=None) -> AttnDesc:
     d = AttnDesc()
     d.q, d.ldq = _p(q), _rowmajor(q, "q")
     d.k0, d.ldk0 = _p(k0), _rowmajor(k0, "k0")
@@ -196,15 +213,43 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     d.l1, d.k1_bstride = l1, k1_bstride
     d.mask_mode, d.n_anchor = mask_mode, n_anchor
     d.scale = head_dim ** -0.5 if scale is None else scale
+    if lse is not None:
+        if lse.dtype != torch.float32 or not lse.is_contiguous() or lse.numel() != batch * heads * lq:
+            raise ValueError("attention: lse must be contiguous fp32 [batch, heads, lq]")
+        d.lse = _p(lse)
+    return d
+
+
+def attention_bwd(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, lse: Tensor, dout: Tensor, dq: Tensor, dk0: Tensor,
+                  dv0: Tensor, delta: Tensor, *, heads: int, batch: int, lq: int, q_bstride: int, l0: int,
+                  k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
+                  dk1: Optional[Tensor] = None, dv1: Optional[Tensor] = None, l1: int = 0, k1_bstride: int = 0,
+                  scale: Optional[float] = None, tag: Optional[str] = None) -> None:
+    """Gradient of attention() (bf16, head_dim 64): dq / dk* / dv* fp32 in q's / k's / v's layouts;
+    ``delta`` fp32 [batch, heads, lq] workspace.  See sr_attention_bwd."""
+    b = _lib.AttnBwdDesc()
+    b.f = _attn_desc(q, k0, v0, o, heads=heads, head_dim=64, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
+                     k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, scale=scale, lse=lse)
+    for t, name in ((dq, "dq"), (dk0, "dk0"), (dv0, "dv0"), (delta, "delta")) + \
+            (((dk1, "dk1"), (dv1, "dv1")) if l1 > 0 else ()):
+        if t is None or t.dtype != torch.float32 or not t.is_cuda:
+            raise ValueError(f"attention_bwd: {name} must be an fp32 device tensor")
+    if delta.numel() < batch * heads * lq:
+        raise ValueError("attention_bwd: delta too small")
+    b.dout, b.lddo = _p(dout), _rowmajor(dout, "dout")
+    b.delta = _p(delta)
+    b.dq, b.lddq = _p(dq), _rowmajor(dq, "dq")
+    b.dk0, b.lddk0 = _p(dk0), _rowmajor(dk0, "dk0")
+    b.dv0, b.lddv0 = _p(dv0), _rowmajor(dv0, "dv0")
+    if l1 > 0:
+        b.dk1, b.lddk1 = _p(dk1), _rowmajor(dk1, "dk1")
+        b.dv1, b.lddv1 = _p(dv1), _rowmajor(dv1, "dv1")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
-    check(rc, "sr_attention")
+    check(_lib.load().sr_attention_bwd(_stream(q), ctypes.byref(b)), "sr_attention_bwd")
     if timed:
-        es = q.element_size()
-        kv_rows = (l0 if k0_bstride == 0 else batch * l0) + batch * l1  # shared segment read once
-        nb = es * heads * head_dim * (2 * batch * lq + 2 * kv_rows)
-        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim, nb)
+        kv = (l0 if k0_bstride == 0 else batch * l0) + batch * l1
+        TIMER.stop(tag, ev0, 10.0 * batch * heads * lq * (l0 + l1) * 64, 2 * heads * 64 * (4 * batch * lq + 4 * kv))
 
 
 def layernorm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float, out: Tensor,

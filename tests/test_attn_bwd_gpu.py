@@ -1,0 +1,104 @@
+"""Attention backward (training step): sr_attention_bwd against torch
+autograd of fp32 softmax attention on the same bf16-rounded q / k / v / dO, for the forward's
+three key-segment shapes (frame: per-item keys; global: one item; global_reloc: a shared anchor
+segment with batch stride 0 plus each item's own frame).  P and dS enter the MFMAs in bf16, as
+in flash-attention backward: tolerance 2e-2 rel-L2."""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 2e-2
+
+
+def _rel(a, b):
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+def _ref(q, k, v, g, scale):
+    q, k, v = (t.float().detach().requires_grad_(True) for t in (q, k, v))
+    o = torch.softmax(q @ k.transpose(-1, -2) * scale, -1) @ v
+    o.backward(g.float())
+    return o.detach(), q.grad, k.grad, v.grad
+
+
+@pytest.mark.parametrize("case", ["frame", "global", "reloc"])
+def test_attention_bwd_matches_autograd(case):
+    from sailrecon_amd import ops
+    torch.manual_seed(0)
+    H, D = 4, 64
+    C = H * D
+    scale = D ** -0.5
+    if case == "frame":
+        B, P = 3, 150
+        x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
+        q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+        kw = dict(batch=B, lq=P, q_bstride=P, l0=P, k0_bstride=P)
+    elif case == "global":
+        B, P = 1, 700
+        x = torch.randn(P, 3 * C, device=DEV).bfloat16()
+        q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+        kw = dict(batch=1, lq=P, q_bstride=P, l0=P, k0_bstride=P)
+    else:
+        B, P, A = 3, 150, 97
+        x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
+        q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+        ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
+        k0, v0 = ka[:, :C], ka[:, C:]
+        kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, k1=k, v1=v, l1=P, k1_bstride=P)
+    if case != "reloc":
+        k0, v0 = k, v
+    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, P, device=DEV)
+    ops.attention(q, k0, v0, o, heads=H, head_dim=D, lse=lse, **kw)
+    g = torch.randn(B * P, C, device=DEV).bfloat16()
+    dq = torch.empty(B * P, C, device=DEV)
+    dk0 = torch.empty(k0.shape[0], C, device=DEV)
+    dv0 = torch.empty(k0.shape[0], C, device=DEV)
+    dk1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
+    dv1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
+    delta = torch.empty(B, H, P, device=DEV)
+    ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
+    torch.cuda.synchronize()
+    # reference, per item and head
+    def heads_of(t, rows):
+        return t.reshape(rows, H, D).transpose(0, 1)
+    dq_r = torch.zeros(B * P, C, device=DEV)
+    dk0_r = torch.zeros_like(dk0)
+    dv0_r = torch.zeros_like(dv0)
+    dk1_r = torch.zeros(B * P, C, device=DEV)
+    dv1_r = torch.zeros(B * P, C, device=DEV)
+    for b in range(B):
+        rs = slice(b * P, (b + 1) * P)
+        qb, gb = heads_of(q[rs], P), heads_of(g[rs], P)
+        if case == "frame":
+            kk, vv = heads_of(k[rs], P), heads_of(v[rs], P)
+        elif case == "global":
+            kk, vv = heads_of(k, P), heads_of(v, P)
+        else:
+            kk = torch.cat([heads_of(k0, A), heads_of(k[rs], P)], 1)
+            vv = torch.cat([heads_of(v0, A), heads_of(v[rs], P)], 1)
+        o_r, dqh, dkh, dvh = _ref(qb, kk, vv, gb, scale)
+        assert _rel(heads_of(o[rs], P).float(), o_r) < TOL
+        dq_r[rs] = dqh.transpose(0, 1).reshape(P, C)
+        if case == "reloc":
+            dk0_r += dkh[:, :A].transpose(0, 1).reshape(A, C)
+            dv0_r += dvh[:, :A].transpose(0, 1).reshape(A, C)
+            dk1_r[rs] = dkh[:, A:].transpose(0, 1).reshape(P, C)
+            dv1_r[rs] = dvh[:, A:].transpose(0, 1).reshape(P, C)
+        elif case == "frame":
+            dk0_r[rs] = dkh.transpose(0, 1).reshape(P, C)
+            dv0_r[rs] = dvh.transpose(0, 1).reshape(P, C)
+        else:
+            dk0_r[:] = dkh.transpose(0, 1).reshape(P, C)
+            dv0_r[:] = dvh.transpose(0, 1).reshape(P, C)
+        # lse (log2 domain) of this item's rows
+        s = (qb.float() @ kk.float().transpose(-1, -2)) * scale
+        assert torch.allclose(lse[b], torch.logsumexp(s, -1) / math.log(2), rtol=0, atol=2e-2)
+    assert _rel(dq, dq_r) < TOL
+    assert _rel(dk0, dk0_r) < TOL and _rel(dv0, dv0_r) < TOL
+    if case == "reloc":
+        assert _rel(dk1, dk1_r) < TOL and _rel(dv1, dv1_r) < TOL
