@@ -55,8 +55,13 @@ enum sr_epilogue {
                             layer_scale.py:22-23)                              */
   SR_EPI_QKV = 3,        /* out = rope(qk_norm(acc + bias)) on Q,K columns
                             (attention.py:72-82, rope.py:165-207)               */
-  SR_EPI_PATCH = 4       /* out(f32)[remap(row)] = acc + bias + row_add[row % seg_rows]
+  SR_EPI_PATCH = 4,      /* out(f32)[remap(row)] = acc + bias + row_add[row % seg_rows]
                             (vision_transformer.py:242-259)                     */
+  /* training step: backward epilogues of the same GEMM,
+     with W^T packed as the "W" operand (dX = dY . W) */
+  SR_EPI_F32 = 5,        /* out(f32) = acc + bias   (dgrad into LayerNorm backward) */
+  SR_EPI_GELU_BWD = 6    /* out = acc * gelu_erf'(aux[row, col])  (fc2 dgrad fused with
+                            the GELU backward, mlp.py:36; aux = saved fc1 pre-activation) */
 };
 
 typedef struct sr_gemm_epi {
@@ -85,6 +90,10 @@ typedef struct sr_gemm_epi {
   int seg_stride;
   int seg_offset;
   const float* row_add;    /* [seg_rows][N] */
+  /* training: BIAS_GELU / QKV also store the pre-activation (acc + bias, before GELU /
+     qk-norm / RoPE) to aux (dtype, row stride ld_aux) for the backward; GELU_BWD reads it */
+  void* aux;
+  int64_t ld_aux;
 } sr_gemm_epi;
 
 int sr_gemm(sr_stream_t stream, int dtype, int epilogue, const void* A, int64_t lda, const void* W,
@@ -167,6 +176,73 @@ typedef struct sr_attn_bwd_desc {
 } sr_attn_bwd_desc;
 
 int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* d);
+
+/* ------------------------------------------------------------------------
+ * Training step (train_imc.py:320-429, the backward of every
+ * nn.Linear / LayerNorm / LayerScale / qk-norm + RoPE of the Blocks, and the Adam step).
+ * ---------------------------------------------------------------------- */
+
+/* Weight gradient of nn.Linear (the addmm backward's mat2 grad, attention.py:48,52 /
+ * mlp.py:34-40):  G[N,K] = A[M,N]^T . B[M,K]  (A = dY, B = the layer input; bf16, fp32
+ * accumulation), reduction over M split into `splits` slices of fp32 partials in
+ * `workspace` (>= splits*N*K floats), then per output row n:
+ *   dW[n,:] = (accumulate ? dW[n,:] : 0) + (rowscale ? rowscale[n] : 1) * G[n,:]
+ *   rowdot[n] += sum_k wdot[n,k] * G[n,k]          (if rowdot: LayerScale gamma grads,
+ *                                                  layer_scale.py:22-23, with G unscaled)
+ * N % 128 == 0, K % 128 == 0, M > 0 arbitrary, 16-B aligned rows.  Deterministic. */
+int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B, int64_t ldb, float* dW,
+                  int64_t lddw, int M, int N, int K, int accumulate, const float* rowscale, const float* wdot,
+                  int64_t ldwd, float* rowdot, int splits, float* workspace);
+
+/* Column sums (bias / token / positional-embedding grads):
+ *   out[c] = (accumulate ? out[c] : 0) + scale * sum_{r<M} X[r*ldx + c],  c < N (N % 4 == 0).
+ * X is `dtype`; two deterministic passes through `workspace` (>= 2048 * N floats, or
+ * ceil(M / 16) * N if smaller). */
+int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
+              float scale, float* workspace);
+
+/* LayerNorm backward (block.py:50,70 norm1 / norm2; vision_transformer.py:300 norm):
+ * for row r (x row / dx row = rowmap ? rowmap[r] : r):
+ *   xhat = (x - mean) * rstd  (statistics recomputed as sr_layernorm does)
+ *   dx  += rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w (w NULL: 1)
+ *   dxb[r] = bf16(updated dx row)  (if dxb: the next GEMM operand)
+ *   dw  += sum_r dy * xhat,  db += sum_r dy   (if dw / db; accumulate)
+ * dy is `dtype` [rows][lddy].  `workspace` >= 3 * 1024 * cols floats.
+ * cols in {128,256,384,512,768,1024,1536,2048,4096}.  Rows of one call must map to distinct
+ * dx rows. */
+int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx, const int32_t* rowmap,
+                     const void* dy, int64_t lddy, const float* w, float eps, float* dx, int64_t lddx, void* dxb,
+                     int64_t lddxb, float* dw, float* db, int rows, int cols, float* workspace);
+
+/* qk-norm + 2-D RoPE backward (attention.py:72-82, rope.py:165-207), the inverse of the
+ * SR_EPI_QKV epilogue: raw = the saved pre-norm q|k|v (bf16, aux of the forward),
+ * dsrc = dq|dk|dv (fp32, from sr_attention_bwd); columns [0, ncols) of each row, column c
+ * in region (c + ep->col_offset) / embed_dim (0 = Q, 1 = K, 2 = V):
+ *   Q/K: dy = RoPE^T(dsrc); draw = rstd (dy w - mean(dy w) - nhat mean(dy w nhat))
+ *        dqn_w += dy nhat, dqn_b += dy (or dkn_*)     (norm params of ep; NULL = no norm)
+ *   V:   draw = dsrc
+ * out = bf16(draw) [rows][ldo].  ep supplies qn/kn weights, eps, rope tables and the row
+ * positions exactly as for the forward GEMM.  grads = fp32 [4][head_dim] accumulators
+ * (dqn_w, dqn_b, dkn_w, dkn_b; NULL if no norm).  workspace >= 4352 * 4 * head_dim floats.
+ * head_dim 64, ncols % 64 == 0. */
+int sr_qk_bwd(sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds, void* out,
+              int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace);
+
+/* out[r, c] = bf16(scale * src[r, c])  (fp32 -> bf16 GEMM operands), cols % 4 == 0 */
+int sr_cast_bf16(sr_stream_t stream, const float* src, int64_t lds, void* dst, int64_t ldd, int rows, int cols,
+                 float scale);
+
+/* found_inf |= any(!isfinite(g[i] * inv_scale)) over n values; inv_scale = 1 / *scale
+ * (scale NULL: 1).  GradScaler.unscale_'s check (torch.cuda.amp, train_imc.py:406-408). */
+int sr_nonfinite_check(sr_stream_t stream, const float* g, int64_t n, const float* scale, int* found_inf);
+
+/* torch.optim.Adam step (train_imc.py:480, betas / eps as given, amsgrad off) over one flat
+ * fp32 parameter buffer, skipped entirely if *found_inf (GradScaler.step):
+ *   g = grad * inv_scale (+ weight_decay * p);  m = lerp(m, g, 1 - beta1);
+ *   v = beta2 v + (1 - beta2) g^2;  p -= (lr / (1 - beta1^t)) m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
+ * `step` = t (already incremented). */
+int sr_adam_f32(sr_stream_t stream, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                float beta2, float eps, float weight_decay, int step, const float* scale, const int* found_inf);
 
 /* ------------------------------------------------------------------------
  * LayerNorm over the last dim of fp32 rows (block.py:50,70; camera_head.py:64-77;

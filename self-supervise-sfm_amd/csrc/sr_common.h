@@ -36,7 +36,8 @@ __device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + e
 // the 2^-9 rounding of the bf16 result), 2 transcendentals + ~11 VALU instead of erff's ~35.
 //   erf(|z|) = 1 - t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) exp(-z^2),  t = 1 / (1 + p |z|)
 //   gelu(x)  = x (1 + erf(x / sqrt2)) / 2 = x - x h  (x >= 0),  x h  (x < 0),  h = poly exp(-z^2) / 2
-__device__ __forceinline__ float gelu_erf_fast(float x) {
+// h(x) = (1 - erf(|x| / sqrt2)) / 2 = Phi(-|x|) by A&S 7.1.26
+__device__ __forceinline__ float phi_tail_fast(float x) {
   const float az = fabsf(x) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
   float poly = fmaf(1.061405429f, t, -1.453152027f);
@@ -45,8 +46,45 @@ __device__ __forceinline__ float gelu_erf_fast(float x) {
   poly = fmaf(poly, t, 0.254829592f);
   poly *= t;
   const float e = __builtin_amdgcn_exp2f(az * az * -1.4426950408889634f);
-  const float h = 0.5f * poly * e;
+  return 0.5f * poly * e;
+}
+__device__ __forceinline__ float gelu_erf_fast(float x) {
+  const float h = phi_tail_fast(x);
   return x >= 0.f ? fmaf(-x, h, x) : x * h;
+}
+
+// d/dx gelu_erf(x) = Phi(x) + x phi(x)  (backward of mlp.py:36's nn.GELU); `fast` uses the
+// A&S erf of gelu_erf_fast (bf16 gradients), otherwise erff (exact fp32).
+template <bool fast>
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  float cdf;
+  if constexpr (fast) {
+    const float h = phi_tail_fast(x);
+    cdf = x >= 0.f ? 1.f - h : h;
+  } else {
+    cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  }
+  return cdf + x * 0.3989422804014327f * __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
+}
+
+// 2-D RoPE position (y, x) of GEMM / token row `row` (rope.py:40-66 via PositionGetter):
+// explicit pos_yx, else the token row (pos_rowmap[row] or pos_row_base + row) inside a frame
+// of tokens_per_frame rows, patches after patch_start, (0, 0) for the special tokens.
+__device__ __forceinline__ void rope_pos(const sr_gemm_epi& ep, int row, int& py, int& px) {
+  py = 0;
+  px = 0;
+  if (ep.pos_yx) {
+    py = ep.pos_yx[2 * row];
+    px = ep.pos_yx[2 * row + 1];
+  } else {
+    const int64_t tr = ep.pos_rowmap ? (int64_t)ep.pos_rowmap[row] : ep.pos_row_base + row;
+    const int t = (int)(tr % ep.tokens_per_frame);
+    if (t >= ep.patch_start) {
+      const int p = t - ep.patch_start;
+      py = p / ep.grid_w + 1;
+      px = p - (py - 1) * ep.grid_w + 1;
+    }
+  }
 }
 
 // wave64 reductions

@@ -87,8 +87,41 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
     v[2] = acc[mi][ni][2] + bias[ni].z;
     v[3] = acc[mi][ni][3] + bias[ni].w;
   };
+  // training forward: the pre-activation (acc + bias) for the backward (sr_gemm_epi.aux)
+  auto save_aux = [&](int row, int col, const float (&v)[4]) {
+    if (row >= g.M || col >= g.N) return;
+    if constexpr (sr::is_bf16<T>::value) {
+      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *(bf16x4*)((T*)ep.aux + (int64_t)row * ep.ld_aux + col) = o;
+    } else {
+      *(float4*)((T*)ep.aux + (int64_t)row * ep.ld_aux + col) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
 
-  if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
+  if constexpr (EPI == SR_EPI_GELU_BWD) {
+    // dH = acc * gelu'(u), u = the saved fc1 pre-activation (aux, T) of the same element
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int row = rowbase + mi * 16 + lr;
+      const T* urow = (const T*)ep.aux + (int64_t)min(row, g.M - 1) * ep.ld_aux;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = min(colw + ni * 16 + 4 * lg, g.N - 4);
+        float u[4];
+        if constexpr (sr::is_bf16<T>::value) {
+          const bf16x4 t = *(const bf16x4*)(urow + col);
+          u[0] = (float)t[0]; u[1] = (float)t[1]; u[2] = (float)t[2]; u[3] = (float)t[3];
+        } else {
+          const float4 t = *(const float4*)(urow + col);
+          u[0] = t.x; u[1] = t.y; u[2] = t.z; u[3] = t.w;
+        }
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[mi][ni][r] * sr::gelu_erf_grad<sr::is_bf16<T>::value>(u[r]);
+        emit(row, colw + ni * 16 + 4 * lg, v);
+      }
+    }
+  } else if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU || EPI == SR_EPI_F32) {
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int row = rowbase + mi * 16 + lr;
@@ -98,6 +131,7 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
           float v[4];
           biased(mi, ni, v);
           if constexpr (EPI == SR_EPI_BIAS_GELU) {
+            if (ep.aux) save_aux(row, colw + ni * 16 + 4 * lg, v);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               if constexpr (sr::is_bf16<T>::value) v[r] = sr::gelu_erf_fast(v[r]);
@@ -149,6 +183,10 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
       float v[4][4];
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) biased(mi, ni, v[ni]);
+      if (ep.aux) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) save_aux(row, colw + ni * 16 + 4 * lg, v[ni]);
+      }
       if (do_norm) {  // LayerNorm over the head's 64 values: 16 in-lane x 4 lanes (xor 16, 32)
         float sum = 0.f;
 #pragma unroll
@@ -176,20 +214,8 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
         }
       }
       if (do_rope) {  // pairs (d, d+16): y half ni 0|1, x half ni 2|3; same lane, same r
-        const int rr = min(row, g.M - 1);
-        int py = 0, px = 0;
-        if (ep.pos_yx) {
-          py = ep.pos_yx[2 * rr];
-          px = ep.pos_yx[2 * rr + 1];
-        } else {
-          const int64_t tr = ep.pos_rowmap ? (int64_t)ep.pos_rowmap[rr] : ep.pos_row_base + rr;
-          const int t = (int)(tr % ep.tokens_per_frame);
-          if (t >= ep.patch_start) {
-            const int p = t - ep.patch_start;
-            py = p / ep.grid_w + 1;
-            px = p - (py - 1) * ep.grid_w + 1;
-          }
-        }
+        int py, px;
+        sr::rope_pos(ep, min(row, g.M - 1), py, px);
         const float4 cy = *(const float4*)(ep.rope_cos + py * 16 + 4 * lg);
         const float4 sy = *(const float4*)(ep.rope_sin + py * 16 + 4 * lg);
         const float4 cx = *(const float4*)(ep.rope_cos + px * 16 + 4 * lg);
@@ -258,11 +284,11 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
         xv.z += v[2];
         xv.w += v[3];
         *p = xv;
-      } else if constexpr (sr::is_bf16<T>::value) {
+      } else if constexpr (EPI == SR_EPI_F32 || !sr::is_bf16<T>::value) {
+        *(float4*)((float*)g.out + (int64_t)row * g.ldo + col) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
         const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         *(bf16x4*)((T*)g.out + (int64_t)row * g.ldo + col) = o;
-      } else {
-        *(float4*)((T*)g.out + (int64_t)row * g.ldo + col) = make_float4(v[0], v[1], v[2], v[3]);
       }
     });
   }
@@ -598,6 +624,8 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
         case SR_EPI_BIAS_RESID: return launch256<SR_EPI_BIAS_RESID>(a, s);
         case SR_EPI_QKV: return launch256<SR_EPI_QKV>(a, s);
         case SR_EPI_PATCH: return launch256<SR_EPI_PATCH>(a, s);
+        case SR_EPI_F32: return launch256<SR_EPI_F32>(a, s);
+        case SR_EPI_GELU_BWD: return launch256<SR_EPI_GELU_BWD>(a, s);
       }
     }
   }
@@ -607,6 +635,8 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
     case SR_EPI_BIAS_RESID: return launch<T, SR_EPI_BIAS_RESID>(a, s);
     case SR_EPI_QKV: return launch<T, SR_EPI_QKV>(a, s);
     case SR_EPI_PATCH: return launch<T, SR_EPI_PATCH>(a, s);
+    case SR_EPI_F32: return launch<T, SR_EPI_F32>(a, s);
+    case SR_EPI_GELU_BWD: return launch<T, SR_EPI_GELU_BWD>(a, s);
   }
   sr::set_error("sr_gemm: unknown epilogue %d", epi);
   return SR_EINVAL;
@@ -628,6 +658,13 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
            "sr_gemm: bad leading dims lda=%lld ldw=%lld", (long long)lda, (long long)ldw);
   SR_CHECK(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0, SR_EINVAL, "sr_gemm: A/W must be 16-B aligned");
   if (epi == SR_EPI_BIAS_RESID) SR_CHECK(ep->gamma, SR_EINVAL, "sr_gemm: RESID needs gamma");
+  if (epi == SR_EPI_GELU_BWD) SR_CHECK(ep->aux && ep->ld_aux >= N && (ep->ld_aux * esz) % 8 == 0, SR_EINVAL,
+                                       "sr_gemm: GELU_BWD needs aux (the saved pre-activation)");
+  if (ep->aux && (epi == SR_EPI_BIAS_GELU || epi == SR_EPI_QKV))
+    SR_CHECK(ep->ld_aux >= N && (ep->ld_aux * esz) % 8 == 0 && ((uintptr_t)ep->aux % 8) == 0, SR_EINVAL,
+             "sr_gemm: bad aux buffer");
+  if (epi == SR_EPI_F32)
+    SR_CHECK(ldo % 4 == 0 && ((uintptr_t)out % 16) == 0, SR_EINVAL, "sr_gemm: F32 output must be 16-B aligned");
   if (epi == SR_EPI_PATCH)
     SR_CHECK(ep->row_add && ep->seg_rows > 0 && ep->seg_stride >= ep->seg_rows, SR_EINVAL, "sr_gemm: PATCH params");
   if (epi == SR_EPI_QKV) {
@@ -652,8 +689,8 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
   // LDS-staged epilogue (256x256 tiles): measured +8 % on bf16 BIAS / QKV outputs, -7 % on the
   // fp32 residual update and -2 % with GELU (DESIGN.md "GEMM"), so only the former use it.
   static const bool no_lds_epi = getenv("SR_GEMM_REG_EPI") != nullptr;  // tuning A/B switch
-  a.lds_epi = !no_lds_epi && (epi == SR_EPI_BIAS || epi == SR_EPI_QKV) && ((uintptr_t)out % 16) == 0 &&
-              (ldo * esz) % 16 == 0;
+  a.lds_epi = !no_lds_epi && (epi == SR_EPI_BIAS || (epi == SR_EPI_QKV && !ep->aux)) &&
+              ((uintptr_t)out % 16) == 0 && (ldo * esz) % 16 == 0;
   a.ep = *ep;
   a.partial = nullptr;
   a.kt_per_split = a.ktiles;

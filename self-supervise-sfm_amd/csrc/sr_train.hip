@@ -1,0 +1,631 @@
+// Training-step kernels for gfx950 (train_imc.py:320-429): the parts of
+// the Block backward that are not attention (sr_attn_bwd.hip) or a dgrad GEMM (sr_gemm.hip
+// with the GELU_BWD / F32 epilogues), plus the optimizer step.
+//
+//   sr_gemm_wgrad       dW = dY^T X  (nn.Linear weight grads), MFMA 32x32x16 bf16 with both
+//                       operands read transposed from row-major LDS tiles (ds_read_b64_tr_b16)
+//   sr_colsum           bias / token / positional-embedding grads (column sums)
+//   sr_layernorm_bwd    LayerNorm backward with the residual accumulate and the bf16 operand copy
+//   sr_qk_bwd           RoPE^T + qk-LayerNorm backward of the fused QKV epilogue
+//   sr_cast_bf16, sr_nonfinite_check, sr_adam_f32
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "sr_common.h"
+
+namespace {
+
+// ================================================================ weight gradient GEMM
+// G[N,K] = sum_m A[m,n] B[m,k].  Workgroup = 128 (n) x 128 (k) output tile, 4 waves as 2 x 2,
+// each 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16.  The reduction walks M in tiles of 64
+// rows; a stage holds A[m0:m0+64, n0:n0+128] and B[m0:m0+64, k0:k0+128] as four 64-row x 64-col
+// sub-tiles (128-B rows, 16-B chunk c of row r at c ^ (((r >> 1) & 1) << 2), the layout the
+// transposed reads of sr_attn_bwd.hip expect), filled by LDS-DMA with the swizzle applied on the
+// source address, double-buffered with one barrier per m-tile.  Operand fragments: A^T (rows = n)
+// and B^T (columns = k) by ds_read_b64_tr_b16, both with the same k (= m) permutation.
+constexpr int WT = 128;
+constexpr int SUB = 64 * 128;    // one sub-tile, bytes
+constexpr int WSTAGE = 4 * SUB;  // 32 KiB
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+struct TrOff {
+  int off[2];
+};
+__device__ __forceinline__ TrOff tr_offsets(int lane) {
+  const int hi = lane >> 5, G = lane >> 4, gi = lane & 15;
+  const int vrow_in = gi >> 2;
+  const int vcol_in = 16 * (G & 1) + 4 * (gi & 3);
+  const int vsw = ((vrow_in >> 1) & 1) << 2;
+  TrOff t;
+  t.off[0] = (4 * hi + vrow_in) * 128 + (((vcol_in >> 3) ^ vsw) * 16) + (vcol_in & 7) * 2;
+  t.off[1] = (4 * hi + vrow_in) * 128 + (((4 + (vcol_in >> 3)) ^ vsw) * 16) + (vcol_in & 7) * 2;
+  return t;
+}
+// operand with rows = the tile's 32-column block db, k = tile rows row0 + {(e&3) + 8(e>>2) + 4hi}
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int row0, int off) {
+  const char* pa = tile + row0 * 128 + off;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
+  const bf16x4 a4 = __builtin_bit_cast(bf16x4, a), b4 = __builtin_bit_cast(bf16x4, b);
+  return bf16x8{a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
+}
+__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+struct WgradArgs {
+  const char* A;
+  int64_t lda_b;
+  const char* B;
+  int64_t ldb_b;
+  float* part;  // [splits][N][K]
+  int M, N, K, mtiles, mt_per_split;
+};
+
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * WSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int ntk = g.K / WT, ntiles = (g.N / WT) * ntk;
+  const int tile = sr::xcd_remap(blockIdx.x, ntiles);
+  const int tn = tile / ntk, tk = tile - tn * ntk;
+  const int n0 = tn * WT, k0 = tk * WT;
+
+  // wave w fills sub-tile w (0,1: A columns n0 + 64w; 2,3: B columns k0 + 64(w-2)), 8 DMAs of
+  // 8 rows each; lane -> row 8i + (lane >> 3), LDS chunk slot lane & 7 <- source chunk slot ^ swz
+  const char* base = wave < 2 ? g.A + (int64_t)(n0 + 64 * wave) * 2 : g.B + (int64_t)(k0 + 64 * (wave - 2)) * 2;
+  const int64_t ld = wave < 2 ? g.lda_b : g.ldb_b;
+  const int rsub = lane >> 3, slot = lane & 7;
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * SUB);
+  auto stage = [&](int mt, int buf) {
+    const uint32_t db = dst0 + buf * WSTAGE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 8 * i + rsub;
+      const int chunk = slot ^ (((r >> 1) & 1) << 2);
+      const int row = min(mt * 64 + r, g.M - 1);
+      sr::dma16(base + (int64_t)row * ld + chunk * 16, db + i * 1024);
+    }
+  };
+
+  const int wr = wave >> 1, wc = wave & 1;
+  const TrOff tro = tr_offsets(lane);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int mt0 = blockIdx.y * g.mt_per_split;
+  const int mt1 = min(mt0 + g.mt_per_split, g.mtiles);
+  if (mt0 < mt1) stage(mt0, 0);
+  for (int mt = mt0; mt < mt1; ++mt) {
+    const int buf = (mt - mt0) & 1;
+    sr::wait_vmcnt0();   // this wave's part of stage mt landed
+    sr::barrier_raw();   // ... every wave's; every wave is done reading the other buffer
+    if (mt + 1 < mt1) stage(mt + 1, buf ^ 1);
+    char* sb = smem + buf * WSTAGE;
+    const int valid = g.M - mt * 64;
+    if (valid < 64) {  // ragged last m-tile: zero the clamped rows (uniform branch)
+      for (int e = tid; e < 4 * 64 * 8; e += 256) {
+        const int st = e >> 9, r = (e >> 3) & 63, c = e & 7;
+        if (r >= valid) *(uint4*)(sb + st * SUB + r * 128 + c * 16) = uint4{0u, 0u, 0u, 0u};
+      }
+      __syncthreads();
+    }
+    const char* ta = sb + wr * SUB;
+    const char* tb = sb + (2 + wc) * SUB;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = tr_frag(ta, 16 * s, tro.off[i]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = tr_frag(tb, 16 * s, tro.off[j]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // lane: column k = k0 + 64 wc + 32 j + l32, rows n = n0 + 64 wr + 32 i + acc_row(e, hi)
+  float* part = g.part + (int64_t)blockIdx.y * g.N * g.K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + 64 * wr + 32 * i + acc_row(e, hi), k = k0 + 64 * wc + 32 * j + l32;
+        part[(int64_t)n * g.K + k] = acc[i][j][e];
+      }
+}
+
+// per output row n (one workgroup): slices summed in order, then scale / accumulate / rowdot
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int N, int K,
+                                                           float* dW, int64_t lddw, int accumulate,
+                                                           const float* __restrict__ rowscale,
+                                                           const float* __restrict__ wdot, int64_t ldwd, float* rowdot) {
+  __shared__ float red[4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float sc = rowscale ? rowscale[n] : 1.f;
+  float dot = 0.f;
+  for (int k = tid * 4; k < K; k += 1024) {
+    f32x4 gsum = *(const f32x4*)(part + (int64_t)n * K + k);
+    for (int z = 1; z < splits; ++z) gsum += *(const f32x4*)(part + ((int64_t)z * N + n) * K + k);
+    if (wdot) {
+      const f32x4 w = *(const f32x4*)(wdot + (int64_t)n * ldwd + k);
+      dot += w[0] * gsum[0] + w[1] * gsum[1] + w[2] * gsum[2] + w[3] * gsum[3];
+    }
+    f32x4* o = (f32x4*)(dW + (int64_t)n * lddw + k);
+    *o = accumulate ? *o + gsum * sc : gsum * sc;
+  }
+  if (wdot) {
+    dot = sr::wave_sum(dot);
+    if ((tid & 63) == 0) red[tid >> 6] = dot;
+    __syncthreads();
+    if (tid == 0) rowdot[n] += (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+// ================================================================ column sums
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ X, int64_t ldx, int M, int N,
+                                                             int rows_per_chunk, float* __restrict__ part) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(M, r0 + rows_per_chunk);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {  // 4 rows in flight
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const T* p = X + (int64_t)(r + u) * ldx + c;
+      if constexpr (sr::is_bf16<T>::value) {
+        const bf16x4 t = *(const bf16x4*)p;
+        v[u] = f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+      } else {
+        v[u] = *(const f32x4*)p;
+      }
+    }
+    s += (v[0] + v[1]) + (v[2] + v[3]);
+  }
+  for (; r < r1; ++r) {
+    const T* p = X + (int64_t)r * ldx + c;
+    if constexpr (sr::is_bf16<T>::value) {
+      const bf16x4 t = *(const bf16x4*)p;
+      s += f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+    } else {
+      s += *(const f32x4*)p;
+    }
+  }
+  *(f32x4*)(part + (int64_t)blockIdx.y * N + c) = s;
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
+                                                           float* out, int accumulate, float scale) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  f32x4 s = *(const f32x4*)(part + c);
+  for (int z = 1; z < chunks; ++z) s += *(const f32x4*)(part + (int64_t)z * N + c);
+  f32x4* o = (f32x4*)(out + c);
+  *o = accumulate ? *o + s * scale : s * scale;
+}
+
+int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
+                  float scale, float* ws) {
+  const int64_t gx = (N / 4 + 255) / 256;
+  int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((2048 + gx - 1) / gx, (M + 15) / 16));
+  chunks = std::min(chunks, 2048);
+  const int rpc = (M + chunks - 1) / chunks;
+  chunks = (M + rpc - 1) / rpc;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, dim3((unsigned)gx, chunks), dim3(256), 0, s, (const bf16*)X, ldx,
+                       M, N, rpc, ws);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((unsigned)gx, chunks), dim3(256), 0, s, (const float*)X, ldx,
+                       M, N, rpc, ws);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)gx), dim3(256), 0, s, ws, chunks, N, out, accumulate, scale);
+  return sr::check_launch("sr_colsum");
+}
+
+// ================================================================ LayerNorm backward
+// One wave per row (grid-stride); lane owns columns (i*64 + lane)*VEC + j as sr_layernorm.
+// dw / db: per-wave partial sums in registers, written to workspace [nwaves][2][cols] and
+// reduced by colsum.
+constexpr int LNB_WGS = 256;  // workgroups (x 4 waves = partial rows)
+
+template <int NPL, int VEC, typename TD>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ x, int64_t ldx,
+                                                            const int32_t* __restrict__ rowmap,
+                                                            const TD* __restrict__ dy, int64_t lddy,
+                                                            const float* __restrict__ w, float eps, float* dx,
+                                                            int64_t lddx, bf16* dxb, int64_t lddxb, int want_params,
+                                                            float* part, int rows) {
+  constexpr int NV = NPL / VEC;
+  constexpr int COLS = NPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  float wv[NPL], dws[NPL], dbs[NPL];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      wv[i * VEC + j] = w ? w[(i * 64 + lane) * VEC + j] : 1.f;
+      dws[i * VEC + j] = 0.f;
+      dbs[i * VEC + j] = 0.f;
+    }
+  for (int row = gw; row < rows; row += nw) {
+    const int64_t xr = rowmap ? (int64_t)rowmap[row] : row;
+    float v[NPL], g[NPL];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * VEC;
+      const float* xp = x + xr * ldx + col;
+      const TD* gp = dy + (int64_t)row * lddy + col;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        v[i * VEC + j] = xp[j];
+        g[i * VEC + j] = sr::to_f32(gp[j]);
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) s += v[i];
+    const float mean = sr::wave_sum(s) * (1.f / COLS);
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      v[i] -= mean;
+      s2 += v[i] * v[i];
+    }
+    const float rstd = rsqrtf(sr::wave_sum(s2) * (1.f / COLS) + eps);
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      v[i] *= rstd;  // xhat
+      if (want_params) {
+        dws[i] += g[i] * v[i];
+        dbs[i] += g[i];
+      }
+      g[i] *= wv[i];
+      sg += g[i];
+      sgx += g[i] * v[i];
+    }
+    const float mg = sr::wave_sum(sg) * (1.f / COLS), mgx = sr::wave_sum(sgx) * (1.f / COLS);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * VEC;
+      float* dp = dx + xr * lddx + col;
+      float o[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = dp[j] + rstd * (g[i * VEC + j] - mg - v[i * VEC + j] * mgx);
+      if constexpr (VEC == 4) {
+        *(float4*)dp = make_float4(o[0], o[1], o[2], o[3]);
+        if (dxb) *(bf16x4*)(dxb + (int64_t)row * lddxb + col) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      } else {
+        *(float2*)dp = make_float2(o[0], o[1]);
+        if (dxb) {
+          bf16* q = dxb + (int64_t)row * lddxb + col;
+          q[0] = (bf16)o[0];
+          q[1] = (bf16)o[1];
+        }
+      }
+    }
+  }
+  if (want_params) {
+    float* pw = part + (int64_t)gw * 2 * COLS;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const int col = (i * 64 + lane) * VEC + j;
+        pw[col] = dws[i * VEC + j];
+        pw[COLS + col] = dbs[i * VEC + j];
+      }
+  }
+}
+
+// ================================================================ qk-norm + RoPE backward
+// One wave per row; 4 heads per pass (16 lanes x 4 values per head: dims 4 li .. 4 li + 3).
+// RoPE pairs (d, d + 16) of each half sit in lanes li and li ^ 4.
+__global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ raw, int64_t ldr,
+                                                     const float* __restrict__ dsrc, int64_t lds, bf16* out,
+                                                     int64_t ldo, int rows, int ncols, sr_gemm_epi ep, float* part) {
+  const int lane = threadIdx.x & 63, li = lane & 15;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int C = ep.embed_dim;
+  const bool norm = ep.qn_w != nullptr;
+  const bool rope = ep.rope_cos != nullptr;
+  const bool first = (li & 4) == 0;  // first element of its RoPE pair
+  const int fj = 4 * (li & 3);       // frequency index of element 0
+  const bool xhalf = li >= 8;
+  float wq[4], bq[4], wk[4], bk[4];
+  float acc[4][4];  // dqn_w, dqn_b, dkn_w, dkn_b (this lane's 4 dims, summed over rows and heads)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    wq[e] = norm ? ep.qn_w[4 * li + e] : 1.f;
+    bq[e] = norm ? ep.qn_b[4 * li + e] : 0.f;
+    wk[e] = norm ? ep.kn_w[4 * li + e] : 1.f;
+    bk[e] = norm ? ep.kn_b[4 * li + e] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t][e] = 0.f;
+  }
+  (void)bq;
+  (void)bk;
+  for (int row = gw; row < rows; row += nw) {
+    float cs[4] = {1.f, 1.f, 1.f, 1.f}, sn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (rope) {
+      int py, px;
+      sr::rope_pos(ep, row, py, px);
+      const int p = xhalf ? px : py;
+      const float4 c4 = *(const float4*)(ep.rope_cos + p * 16 + fj);
+      const float4 s4 = *(const float4*)(ep.rope_sin + p * 16 + fj);
+      cs[0] = c4.x; cs[1] = c4.y; cs[2] = c4.z; cs[3] = c4.w;
+      sn[0] = s4.x; sn[1] = s4.y; sn[2] = s4.z; sn[3] = s4.w;
+    }
+    for (int c0 = 0; c0 < ncols; c0 += 256) {
+      // 4 heads per pass; a short last pass computes on clamped columns and stores nothing
+      const bool live = c0 + 4 * lane < ncols;
+      const int col = min(c0 + 4 * lane, ncols - 4);
+      const int region = (col + ep.col_offset) / C;
+      const float4 d4 = *(const float4*)(dsrc + (int64_t)row * lds + col);
+      float d[4] = {d4.x, d4.y, d4.z, d4.w};
+      if (region < 2) {
+        if (rope) {  // inverse rotation: first a: da = c dA + s dB; second b: db = c dB - s dA
+          float pd[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pd[e] = __shfl_xor(d[e], 4, 64);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = first ? fmaf(cs[e], d[e], sn[e] * pd[e]) : fmaf(cs[e], d[e], -sn[e] * pd[e]);
+        }
+        if (norm) {
+          const bf16x4 r4 = *(const bf16x4*)(raw + (int64_t)row * ldr + col);
+          float v[4] = {(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
+          float s = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+          const float mean = s * (1.f / 64.f);
+          float s2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] -= mean;
+            s2 += v[e] * v[e];
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+          const float rstd = rsqrtf(s2 * (1.f / 64.f) + ep.qk_eps);
+          const float* wv = region == 0 ? wq : wk;
+          float g[4], sg = 0.f, sgx = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] *= rstd;
+            if (live) {
+              acc[2 * region][e] += d[e] * v[e];
+              acc[2 * region + 1][e] += d[e];
+            }
+            g[e] = d[e] * wv[e];
+            sg += g[e];
+            sgx += g[e] * v[e];
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            sg += __shfl_xor(sg, o, 64);
+            sgx += __shfl_xor(sgx, o, 64);
+          }
+          sg *= 1.f / 64.f;
+          sgx *= 1.f / 64.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = rstd * (g[e] - sg - v[e] * sgx);
+        }
+      }
+      if (live) *(bf16x4*)(out + (int64_t)row * ldo + col) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+    }
+  }
+  if (norm) {  // lanes li, li+16, li+32, li+48 hold the same dims
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[t][e] += __shfl_xor(acc[t][e], 16, 64);
+        acc[t][e] += __shfl_xor(acc[t][e], 32, 64);
+      }
+    if (lane < 16) {
+      float* pw = part + (int64_t)gw * 256;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pw[t * 64 + 4 * li + e] = acc[t][e];
+    }
+  }
+}
+
+// ================================================================ elementwise / optimizer
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ src, int64_t lds, bf16* dst,
+                                                        int64_t ldd, int rows, int cols, float scale) {
+  const int cq = cols / 4;
+  const int64_t n = (int64_t)rows * cq;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / cq), c = (int)(e - (int64_t)r * cq) * 4;
+    const float4 v = *(const float4*)(src + (int64_t)r * lds + c);
+    *(bf16x4*)(dst + (int64_t)r * ldd + c) =
+        bf16x4{(bf16)(v.x * scale), (bf16)(v.y * scale), (bf16)(v.z * scale), (bf16)(v.w * scale)};
+  }
+}
+
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, int64_t n,
+                                                        const float* __restrict__ scale, int* found) {
+  const float inv = scale ? 1.f / *scale : 1.f;
+  int bad = 0;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    bad |= !isfinite(g[e] * inv);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found, 1);
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* p, const float* __restrict__ g, float* m, float* v,
+                                                   int64_t n, float lr, float beta1, float beta2, float eps, float wd,
+                                                   float bc1, float bc2_sqrt, const float* __restrict__ scale,
+                                                   const int* __restrict__ found) {
+  if (found && *found) return;  // GradScaler.step skips the update on inf / nan
+  const float inv = scale ? 1.f / *scale : 1.f;
+  const float step_size = lr / bc1;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    float gr = g[e] * inv;
+    const float pv = p[e];
+    if (wd != 0.f) gr += wd * pv;
+    const float mo = m[e];
+    const float mn = mo + (1.f - beta1) * (gr - mo);  // lerp(m, g, 1 - beta1), weight < 0.5
+    const float vn = beta2 * v[e] + (1.f - beta2) * gr * gr;
+    m[e] = mn;
+    v[e] = vn;
+    const float denom = sqrtf(vn) / bc2_sqrt + eps;
+    p[e] = pv - step_size * (mn / denom);
+  }
+}
+
+unsigned grid_for(int64_t n, int64_t cap = 4096) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B, int64_t ldb, float* dW,
+                             int64_t lddw, int M, int N, int K, int accumulate, const float* rowscale,
+                             const float* wdot, int64_t ldwd, float* rowdot, int splits, float* workspace) {
+  SR_CHECK(A && B && dW && workspace, SR_EINVAL, "sr_gemm_wgrad: null pointer");
+  SR_CHECK(M > 0 && N > 0 && K > 0 && N % WT == 0 && K % WT == 0, SR_EUNSUPPORTED,
+           "sr_gemm_wgrad: N=%d, K=%d must be multiples of 128 (M=%d)", N, K, M);
+  SR_CHECK(lda >= N && ldb >= K && lda % 8 == 0 && ldb % 8 == 0 && lddw >= K && lddw % 4 == 0 &&
+               ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 && ((uintptr_t)dW % 16) == 0,
+           SR_EINVAL, "sr_gemm_wgrad: bad leading dims / alignment");
+  SR_CHECK(!wdot || (rowdot && ldwd >= K && ldwd % 4 == 0), SR_EINVAL, "sr_gemm_wgrad: wdot needs rowdot");
+  SR_CHECK(splits >= 1, SR_EINVAL, "sr_gemm_wgrad: splits=%d", splits);
+  WgradArgs g;
+  g.A = (const char*)A;
+  g.lda_b = lda * 2;
+  g.B = (const char*)B;
+  g.ldb_b = ldb * 2;
+  g.part = workspace;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.mtiles = (M + 63) / 64;
+  splits = std::min(splits, g.mtiles);
+  g.mt_per_split = (g.mtiles + splits - 1) / splits;
+  splits = (g.mtiles + g.mt_per_split - 1) / g.mt_per_split;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wgrad_kernel, dim3((N / WT) * (K / WT), splits), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, workspace, splits, N, K, dW, lddw, accumulate,
+                     rowscale, wdot, ldwd, rowdot);
+  return sr::check_launch("sr_gemm_wgrad");
+}
+
+extern "C" int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out,
+                         int accumulate, float scale, float* workspace) {
+  SR_CHECK(X && out && workspace, SR_EINVAL, "sr_colsum: null pointer");
+  SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_colsum: bad dtype");
+  SR_CHECK(M > 0 && N > 0 && N % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)out % 16) == 0, SR_EINVAL,
+           "sr_colsum: bad shape M=%d N=%d ldx=%lld", M, N, (long long)ldx);
+  return colsum_launch((hipStream_t)stream, dtype, X, ldx, M, N, out, accumulate, scale, workspace);
+}
+
+extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx, const int32_t* rowmap,
+                                const void* dy, int64_t lddy, const float* w, float eps, float* dx, int64_t lddx,
+                                void* dxb, int64_t lddxb, float* dw, float* db, int rows, int cols, float* workspace) {
+  SR_CHECK(x && dy && dx && rows > 0, SR_EINVAL, "sr_layernorm_bwd: null pointer / no rows");
+  SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_layernorm_bwd: bad dtype");
+  SR_CHECK(!(dw || db) || (dw && db && workspace), SR_EINVAL, "sr_layernorm_bwd: dw and db need workspace");
+  hipStream_t s = (hipStream_t)stream;
+  const int want = dw != nullptr;
+  const int wgs = std::min(LNB_WGS, (rows + 3) / 4);
+#define LNB_CASE(C, V)                                                                                          \
+  case C:                                                                                                       \
+    if (dtype == SR_BF16)                                                                                       \
+      hipLaunchKernelGGL((layernorm_bwd_kernel<C / 64, V, bf16>), dim3(wgs), dim3(256), 0, s, x, ldx, rowmap,  \
+                         (const bf16*)dy, lddy, w, eps, dx, lddx, (bf16*)dxb, lddxb, want, workspace, rows);     \
+    else                                                                                                        \
+      hipLaunchKernelGGL((layernorm_bwd_kernel<C / 64, V, float>), dim3(wgs), dim3(256), 0, s, x, ldx, rowmap, \
+                         (const float*)dy, lddy, w, eps, dx, lddx, (bf16*)dxb, lddxb, want, workspace, rows);    \
+    break;
+  switch (cols) {
+    LNB_CASE(128, 2)
+    LNB_CASE(256, 4)
+    LNB_CASE(384, 2)
+    LNB_CASE(512, 4)
+    LNB_CASE(768, 4)
+    LNB_CASE(1024, 4)
+    LNB_CASE(1536, 4)
+    LNB_CASE(2048, 4)
+    LNB_CASE(4096, 4)
+    default:
+      sr::set_error("sr_layernorm_bwd: unsupported cols=%d", cols);
+      return SR_EUNSUPPORTED;
+  }
+#undef LNB_CASE
+  if (want) {  // partial rows [wgs*4][2*cols] -> dw | db
+    float* tail = workspace + (int64_t)wgs * 4 * 2 * cols;
+    int rc = colsum_launch(s, SR_F32, workspace, 2 * cols, wgs * 4, cols, dw, 1, 1.f, tail);
+    if (rc) return rc;
+    rc = colsum_launch(s, SR_F32, workspace + cols, 2 * cols, wgs * 4, cols, db, 1, 1.f, tail);
+    if (rc) return rc;
+  }
+  return sr::check_launch("sr_layernorm_bwd");
+}
+
+extern "C" int sr_qk_bwd(sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds, void* out,
+                         int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace) {
+  SR_CHECK(dsrc && out && ep && rows > 0, SR_EINVAL, "sr_qk_bwd: null pointer / no rows");
+  SR_CHECK(ep->head_dim == 64 && ep->embed_dim % 64 == 0 && ncols % 64 == 0, SR_EUNSUPPORTED,
+           "sr_qk_bwd: head_dim 64 and ncols %% 64 == 0 only (ncols=%d)", ncols);
+  const bool norm = ep->qn_w != nullptr;
+  SR_CHECK(!norm || (raw && ep->qn_b && ep->kn_w && ep->kn_b && grads && workspace), SR_EINVAL,
+           "sr_qk_bwd: qk-norm needs raw, the four norm params, grads and workspace");
+  SR_CHECK(!ep->rope_cos || (ep->rope_sin && (ep->pos_yx || (ep->tokens_per_frame > ep->patch_start && ep->grid_w > 0))),
+           SR_EINVAL, "sr_qk_bwd: rope params");
+  hipStream_t s = (hipStream_t)stream;
+  const int wgs = std::min(1024, (rows + 3) / 4);
+  hipLaunchKernelGGL(qk_bwd_kernel, dim3(wgs), dim3(256), 0, s, (const bf16*)raw, ldr, dsrc, lds, (bf16*)out, ldo,
+                     rows, ncols, *ep, workspace);
+  if (norm) {  // [wgs*4][4][64] -> grads[4][64]
+    const int rc = colsum_launch(s, SR_F32, workspace, 256, wgs * 4, 256, grads, 1, 1.f,
+                                 workspace + (int64_t)wgs * 4 * 256);
+    if (rc) return rc;
+  }
+  return sr::check_launch("sr_qk_bwd");
+}
+
+extern "C" int sr_cast_bf16(sr_stream_t stream, const float* src, int64_t lds, void* dst, int64_t ldd, int rows,
+                            int cols, float scale) {
+  SR_CHECK(src && dst && rows > 0 && cols > 0 && cols % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, SR_EINVAL,
+           "sr_cast_bf16: bad arguments");
+  const int64_t n = (int64_t)rows * (cols / 4);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n, 8192)), dim3(256), 0, (hipStream_t)stream, src, lds,
+                     (bf16*)dst, ldd, rows, cols, scale);
+  return sr::check_launch("sr_cast_bf16");
+}
+
+extern "C" int sr_nonfinite_check(sr_stream_t stream, const float* g, int64_t n, const float* scale, int* found_inf) {
+  SR_CHECK(g && found_inf && n >= 0, SR_EINVAL, "sr_nonfinite_check: bad arguments");
+  if (n == 0) return SR_OK;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, g, n, scale, found_inf);
+  return sr::check_launch("sr_nonfinite_check");
+}
+
+extern "C" int sr_adam_f32(sr_stream_t stream, float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                           float beta1, float beta2, float eps, float weight_decay, int step, const float* scale,
+                           const int* found_inf) {
+  SR_CHECK(p && g && m && v && n >= 0 && step >= 1, SR_EINVAL, "sr_adam_f32: bad arguments");
+  if (n == 0) return SR_OK;
+  const float bc1 = 1.f - (float)std::pow((double)beta1, step);
+  const float bc2 = 1.f - (float)std::pow((double)beta2, step);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
+                     beta2, eps, weight_decay, bc1, std::sqrt(bc2), scale, found_inf);
+  return sr::check_launch("sr_adam_f32");
+}

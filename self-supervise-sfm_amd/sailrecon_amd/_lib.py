@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("SFM_AMD_LIB") or os.path.join(_HERE, "libsfm_amd.so")
 
 SR_F32, SR_BF16 = 0, 1
 SR_EPI_BIAS, SR_EPI_BIAS_GELU, SR_EPI_BIAS_RESID, SR_EPI_QKV, SR_EPI_PATCH = 0, 1, 2, 3, 4
+SR_EPI_F32, SR_EPI_GELU_BWD = 5, 6
 SR_MASK_NONE, SR_MASK_CAMERA = 0, 1
 
 _vp = ctypes.c_void_p
@@ -36,6 +37,7 @@ class GemmEpi(ctypes.Structure):
         ("pos_yx", _vp), ("pos_rowmap", _vp), ("pos_row_base", _i64),
         ("tokens_per_frame", _i32), ("patch_start", _i32), ("grid_w", _i32),
         ("seg_rows", _i32), ("seg_stride", _i32), ("seg_offset", _i32), ("row_add", _vp),
+        ("aux", _vp), ("ld_aux", _i64),
     ]
 
 
@@ -96,6 +98,16 @@ _PROTOS = {
     "sr_adaln_modulate_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32]),
     "sr_pose_update_f32": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _i32]),
     "sr_pose_decode_f32": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
+    # training step
+    "sr_gemm_wgrad": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp,
+                             _i32, _vp]),
+    "sr_colsum": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i32, _f32, _vp]),
+    "sr_layernorm_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _f32, _vp, _i64, _vp, _i64, _vp, _vp,
+                                _i32, _i32, _vp]),
+    "sr_qk_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
+    "sr_cast_bf16": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _f32]),
+    "sr_nonfinite_check": (_i32, [_vp, _vp, _i64, _vp, _vp]),
+    "sr_adam_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
 }
 EXPORTED = tuple(_PROTOS)
 

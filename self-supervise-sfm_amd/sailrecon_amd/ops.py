@@ -64,7 +64,8 @@ class KernelTimer:
 TIMER: Optional[KernelTimer] = None
 
 _EPI_NAME = {_lib.SR_EPI_BIAS: "bias", _lib.SR_EPI_BIAS_GELU: "gelu", _lib.SR_EPI_BIAS_RESID: "resid",
-             _lib.SR_EPI_QKV: "qkv", _lib.SR_EPI_PATCH: "patch"}
+             _lib.SR_EPI_QKV: "qkv", _lib.SR_EPI_PATCH: "patch", _lib.SR_EPI_F32: "f32",
+             _lib.SR_EPI_GELU_BWD: "gelu_bwd"}
 
 
 def _p(t: Optional[Tensor]):
@@ -118,11 +119,32 @@ def _splitk_workspace(device, numel: int) -> Tensor:
     return ws
 
 
+def _fill_qkv_epi(ep: GemmEpi, qkv: dict) -> None:
+    """qk-norm / RoPE / position fields of sr_gemm_epi (runtime.qkv_params dict)."""
+    ep.qn_w, ep.qn_b = _p(qkv.get("qn_w")), _p(qkv.get("qn_b"))
+    ep.kn_w, ep.kn_b = _p(qkv.get("kn_w")), _p(qkv.get("kn_b"))
+    ep.qk_eps = qkv.get("qk_eps", 1e-5)
+    cos, sin = qkv.get("rope_cos"), qkv.get("rope_sin")
+    ep.rope_cos, ep.rope_sin = _p(cos), _p(sin)
+    ep.rope_npos = 0 if cos is None else cos.shape[0]
+    ep.col_offset = qkv.get("col_offset", 0)
+    ep.head_dim = qkv.get("head_dim", 64)
+    ep.embed_dim = qkv["embed_dim"]
+    ep.pos_yx = _p(qkv.get("pos_yx"))
+    ep.pos_rowmap = _p(qkv.get("pos_rowmap"))
+    ep.pos_row_base = qkv.get("pos_row_base", 0)
+    ep.tokens_per_frame = qkv.get("tokens_per_frame", 1)
+    ep.patch_start = qkv.get("patch_start", 0)
+    ep.grid_w = qkv.get("grid_w", 1)
+
+
 def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] = None,
          gamma: Optional[Tensor] = None, rows: Optional[int] = None, qkv: Optional[dict] = None,
-         patch: Optional[dict] = None, tag: Optional[str] = None, splits: Optional[int] = None) -> None:
+         patch: Optional[dict] = None, tag: Optional[str] = None, splits: Optional[int] = None,
+         aux: Optional[Tensor] = None) -> None:
     """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows).
-    ``splits`` K slices (sr_gemm_splitk); default: automatic for few rows."""
+    ``splits`` K slices (sr_gemm_splitk); default: automatic for few rows.  ``aux`` (a's dtype,
+    [M, N] view): BIAS_GELU / QKV store the pre-activation there; GELU_BWD reads it."""
     lda = _rowmajor(a, "a")
     ldw = _rowmajor(w, "w")
     ldo = _rowmajor(out, "out")
@@ -136,21 +158,11 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
     ep.bias = _p(bias)
     ep.gamma = _p(gamma)
     if qkv is not None:
-        ep.qn_w, ep.qn_b = _p(qkv.get("qn_w")), _p(qkv.get("qn_b"))
-        ep.kn_w, ep.kn_b = _p(qkv.get("kn_w")), _p(qkv.get("kn_b"))
-        ep.qk_eps = qkv.get("qk_eps", 1e-5)
-        cos, sin = qkv.get("rope_cos"), qkv.get("rope_sin")
-        ep.rope_cos, ep.rope_sin = _p(cos), _p(sin)
-        ep.rope_npos = 0 if cos is None else cos.shape[0]
-        ep.col_offset = qkv.get("col_offset", 0)
-        ep.head_dim = qkv.get("head_dim", 64)
-        ep.embed_dim = qkv["embed_dim"]
-        ep.pos_yx = _p(qkv.get("pos_yx"))
-        ep.pos_rowmap = _p(qkv.get("pos_rowmap"))
-        ep.pos_row_base = qkv.get("pos_row_base", 0)
-        ep.tokens_per_frame = qkv.get("tokens_per_frame", 1)
-        ep.patch_start = qkv.get("patch_start", 0)
-        ep.grid_w = qkv.get("grid_w", 1)
+        _fill_qkv_epi(ep, qkv)
+    if aux is not None:
+        if aux.dtype != a.dtype:
+            raise TypeError("gemm: aux must have the operand dtype")
+        ep.aux, ep.ld_aux = _p(aux), _rowmajor(aux, "aux")
     if patch is not None:
         ep.seg_rows = patch["seg_rows"]
         ep.seg_stride = patch["seg_stride"]
@@ -430,3 +442,110 @@ def pil_resample_v(mode: int, tmp: Tensor, bounds: Tensor, coeffs: Tensor, divis
 def pil_tmp(n: int, c: int, rows: int, tw: int, dtype: torch.dtype, device) -> Tensor:
     """Planar intermediate of the two resample passes: [n, c, rows, tw rounded up to 4]."""
     return torch.empty(n, c, rows, (tw + 3) // 4 * 4, dtype=dtype, device=device)
+
+
+# ---------------------------------------------------------------- training step (SURVEY §8(f) rank 4)
+_TRAIN_WS = {}  # (device, name) -> fp32 workspace (single-stream use)
+
+
+def _train_ws(device, name: str, numel: int) -> Tensor:
+    key = (device, name)
+    ws = _TRAIN_WS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(max(numel, 1), device=device, dtype=torch.float32)
+        _TRAIN_WS[key] = ws
+    return ws
+
+
+def _wgrad_splits(M: int, N: int, K: int) -> int:
+    """Reduction slices so that the 128x128-tile grid has >= 512 workgroups (2 per CU) while
+    every slice keeps >= 8 m-tiles of 64 rows; the fp32 partials stay <= 16x the output."""
+    tiles = (N // 128) * (K // 128)
+    mt = -(-M // 64)
+    s = 1
+    while tiles * s < 512 and mt // (2 * s) >= 8 and 2 * s <= 16:
+        s *= 2
+    return s
+
+
+def gemm_wgrad(dy: Tensor, x: Tensor, dw: Tensor, *, accumulate: bool = False, rowscale: Optional[Tensor] = None,
+               wdot: Optional[Tensor] = None, rowdot: Optional[Tensor] = None, splits: Optional[int] = None,
+               tag: Optional[str] = None) -> None:
+    """dw[N,K] (fp32) (+)= rowscale[n] * dy[M,N]^T x[M,K] (bf16); rowdot[n] += <wdot[n], G[n]>."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if x.shape[0] != M or dw.shape != (N, K) or dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 \
+            or dw.dtype != torch.float32:
+        raise ValueError(f"gemm_wgrad: dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)} mismatch")
+    if splits is None:
+        splits = _wgrad_splits(M, N, K)
+    ws = _train_ws(dy.device, "wgrad", splits * N * K)
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    rc = _lib.load().sr_gemm_wgrad(_stream(dy), _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(dw),
+                                   _rowmajor(dw, "dw"), M, N, K, int(accumulate), _p(rowscale), _p(wdot),
+                                   0 if wdot is None else _rowmajor(wdot, "wdot"), _p(rowdot), splits, _p(ws))
+    check(rc, "sr_gemm_wgrad")
+    if timed:
+        TIMER.stop(tag, ev0, 2.0 * M * N * K, 2 * M * (N + K) + 4 * N * K * (3 if accumulate else 2))
+
+
+def colsum(x: Tensor, out: Tensor, *, rows: Optional[int] = None, cols: Optional[int] = None,
+           accumulate: bool = False, scale: float = 1.0) -> None:
+    """out[c] (+)= scale * sum_r x[r, c] over a row-strided 2-D view (bf16 or fp32)."""
+    ldx = _rowmajor(x, "x")
+    M = x.shape[0] if rows is None else rows
+    N = x.shape[1] if cols is None else cols
+    if out.dtype != torch.float32 or out.numel() < N:
+        raise ValueError("colsum: out must be fp32 with >= cols elements")
+    ws = _train_ws(x.device, "colsum", min(2048, max(1, -(-M // 16))) * N)
+    rc = _lib.load().sr_colsum(_stream(x), dtype_code(x.dtype), _p(x), ldx, M, N, _p(out), int(accumulate),
+                               float(scale), _p(ws))
+    check(rc, "sr_colsum")
+
+
+def layernorm_bwd(x: Tensor, dy: Tensor, w: Optional[Tensor], eps: float, dx: Tensor, *,
+                  dxb: Optional[Tensor] = None, dw: Optional[Tensor] = None, db: Optional[Tensor] = None,
+                  rowmap: Optional[Tensor] = None, rows: Optional[int] = None) -> None:
+    """dx[rows] += LayerNorm backward (see sr_layernorm_bwd); dxb = bf16 copy of the updated rows."""
+    n = dy.shape[0] if rows is None else rows
+    cols = x.shape[1]
+    ws = _train_ws(x.device, "lnbwd", 3 * 1024 * cols) if dw is not None else None
+    rc = _lib.load().sr_layernorm_bwd(_stream(x), dtype_code(dy.dtype), _p(x), _rowmajor(x, "x"), _p(rowmap), _p(dy),
+                                      _rowmajor(dy, "dy"), _p(w), eps, _p(dx), _rowmajor(dx, "dx"), _p(dxb),
+                                      0 if dxb is None else _rowmajor(dxb, "dxb"), _p(dw), _p(db), n, cols, _p(ws))
+    check(rc, "sr_layernorm_bwd")
+
+
+def qk_bwd(raw: Optional[Tensor], dsrc: Tensor, out: Tensor, qkv: dict, *, grads: Optional[Tensor] = None,
+           ncols: Optional[int] = None) -> None:
+    """bf16 d(pre-norm q|k|v) from fp32 d(q|k|v) through RoPE^T and the qk-norm backward;
+    grads fp32 [4, 64] += (dqn_w, dqn_b, dkn_w, dkn_b)."""
+    ep = GemmEpi()
+    _fill_qkv_epi(ep, qkv)
+    rows = dsrc.shape[0]
+    nc = out.shape[1] if ncols is None else ncols
+    ws = _train_ws(dsrc.device, "qkbwd", 4352 * 256)
+    rc = _lib.load().sr_qk_bwd(_stream(dsrc), _p(raw), 0 if raw is None else _rowmajor(raw, "raw"), _p(dsrc),
+                               _rowmajor(dsrc, "dsrc"), _p(out), _rowmajor(out, "out"), rows, nc, ctypes.byref(ep),
+                               _p(grads), _p(ws))
+    check(rc, "sr_qk_bwd")
+
+
+def cast_bf16(src: Tensor, dst: Tensor, scale: float = 1.0) -> None:
+    rows, cols = src.shape
+    check(_lib.load().sr_cast_bf16(_stream(src), _p(src), _rowmajor(src, "src"), _p(dst), _rowmajor(dst, "dst"),
+                                   rows, cols, float(scale)), "sr_cast_bf16")
+
+
+def nonfinite_check(g: Tensor, found: Tensor, scale: Optional[Tensor] = None) -> None:
+    check(_lib.load().sr_nonfinite_check(_stream(g), _p(g), g.numel(), _p(scale), _p(found)), "sr_nonfinite_check")
+
+
+def adam(p: Tensor, g: Tensor, m: Tensor, v: Tensor, *, lr: float, beta1: float, beta2: float, eps: float,
+         weight_decay: float, step: int, scale: Optional[Tensor] = None, found_inf: Optional[Tensor] = None) -> None:
+    for t in (p, g, m, v):
+        if not t.is_contiguous() or t.dtype != torch.float32 or t.numel() != p.numel():
+            raise ValueError("adam: p / g / m / v must be contiguous fp32 of one size")
+    check(_lib.load().sr_adam_f32(_stream(p), _p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps,
+                                  weight_decay, step, _p(scale), _p(found_inf)), "sr_adam_f32")

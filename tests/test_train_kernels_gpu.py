@@ -1,0 +1,268 @@
+"""Training-step kernels against torch fp32 statements of the same op on
+the same (bf16-rounded) inputs, through the C ABI: weight-gradient GEMM, the backward GEMM
+epilogues (F32, GELU_BWD, saved pre-activations), column sums, LayerNorm backward, qk-norm +
+RoPE backward, cast, the non-finite check and the Adam step.
+
+Tolerances: fp32 accumulation of bf16 products -> 1e-5 rel-L2 where the inputs are bf16 and
+the output fp32 (wgrad, F32 epilogue, colsum); bf16 outputs 8e-3; LayerNorm / qk backward
+in fp32 1e-5 (fp32 dy) or 8e-3 (bf16 outputs); Adam 1e-6."""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sailrecon_amd import ops as _ops
+    return _ops
+
+
+def L():
+    from sailrecon_amd import _lib
+    return _lib
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(64, 128, 128, 1), (1000, 256, 384, 1), (4397, 384, 256, 3),
+                                          (43968 // 8, 1024, 1024, None), (130, 3072, 128, 2)])
+def test_gemm_wgrad(ops, M, N, K, splits):
+    torch.manual_seed(0)
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    dw = torch.empty(N, K, device=DEV)
+    ops.gemm_wgrad(dy, x, dw, splits=splits)
+    ref = dy.float().t() @ x.float()
+    assert rel(dw, ref) < 1e-5
+
+
+def test_gemm_wgrad_strided_accumulate_rowscale_rowdot(ops):
+    """Row-strided operands (column slices of wider buffers), accumulate, per-row scale
+    (LayerScale gamma folded into dW) and rowdot (the gamma gradient)."""
+    torch.manual_seed(1)
+    M, N, K = 777, 256, 128
+    big_dy = torch.randn(M, N + 128, device=DEV).bfloat16()
+    big_x = torch.randn(M, 3 * K, device=DEV).bfloat16()
+    dy, x = big_dy[:, 128:], big_x[:, K:2 * K]
+    dw0 = torch.randn(N, K, device=DEV)
+    dw = dw0.clone()
+    gamma = torch.randn(N, device=DEV)
+    wdot = torch.randn(N, K, device=DEV)
+    rowdot = torch.randn(N, device=DEV)
+    rd0 = rowdot.clone()
+    ops.gemm_wgrad(dy, x, dw, accumulate=True, rowscale=gamma, wdot=wdot, rowdot=rowdot, splits=4)
+    G = dy.float().t() @ x.float()
+    assert rel(dw, dw0 + gamma[:, None] * G) < 1e-5
+    assert rel(rowdot - rd0, (wdot * G).sum(1)) < 1e-5
+
+
+def test_gemm_f32_and_gelu_bwd_epilogues(ops):
+    torch.manual_seed(2)
+    lib = L()
+    for M, N, K in ((300, 256, 128), (33000, 1024, 64)):  # 128x128 and 256x256 (>= 512 tiles) kernels
+        a = torch.randn(M, K, device=DEV).bfloat16()
+        w = (torch.randn(N, K, device=DEV) / 8).bfloat16()
+        acc = a.float() @ w.float().t()
+        out = torch.empty(M, N, device=DEV)
+        bias = torch.randn(N, device=DEV)
+        ops.gemm(a, w, out, lib.SR_EPI_F32, bias=bias)
+        assert rel(out, acc + bias) < 1e-5
+        u = torch.randn(M, N, device=DEV).bfloat16()
+        dh = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.gemm(a, w, dh, lib.SR_EPI_GELU_BWD, aux=u)
+        uf = u.float()
+        gprime = 0.5 * (1 + torch.erf(uf / math.sqrt(2))) + uf * torch.exp(-0.5 * uf * uf) / math.sqrt(2 * math.pi)
+        assert rel(dh.float(), acc * gprime) < 8e-3
+
+
+def test_gemm_saves_preactivation(ops):
+    """Training forward: BIAS_GELU stores u = acc + bias; QKV stores the pre-norm q|k|v."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    torch.manual_seed(3)
+    lib = L()
+    M, C, D = 21 * 40, 256, 64
+    a = torch.randn(M, C, device=DEV).bfloat16()
+    w = (torch.randn(4 * C, C, device=DEV) / 16).bfloat16()
+    b = torch.randn(4 * C, device=DEV)
+    h = torch.empty(M, 4 * C, device=DEV, dtype=torch.bfloat16)
+    u = torch.empty_like(h)
+    ops.gemm(a, w, h, lib.SR_EPI_BIAS_GELU, bias=b, aux=u)
+    y = a.float() @ w.float().t() + b
+    assert rel(u.float(), y) < 8e-3
+    assert rel(h.float(), F.gelu(y)) < 8e-3
+    wq = w[:3 * C].contiguous()
+    raw = torch.empty(M, 3 * C, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty_like(raw)
+    rope = RotaryPositionEmbedding2D(100).tables(D, 5, DEV)
+    epi = dict(embed_dim=C, head_dim=D, qk_eps=1e-5, qn_w=torch.randn(D, device=DEV), qn_b=torch.randn(D, device=DEV),
+               kn_w=torch.randn(D, device=DEV), kn_b=torch.randn(D, device=DEV), rope_cos=rope[0], rope_sin=rope[1],
+               tokens_per_frame=21, patch_start=5, grid_w=4, pos_row_base=0)
+    ops.gemm(a, wq, out, lib.SR_EPI_QKV, bias=b[:3 * C], qkv=epi, aux=raw)
+    assert rel(raw.float(), y[:, :3 * C]) < 8e-3
+    assert rel(out[:, 2 * C:].float(), y[:, 2 * C:3 * C]) < 8e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(1, 5 * 1024), (31, 1369 * 64), (43968, 1024), (777, 4096)])
+def test_colsum(ops, dtype, M, N):
+    torch.manual_seed(4)
+    big = torch.randn(M, N + 8, device=DEV).to(dtype)
+    x = big[:, 4:N + 4]
+    out = torch.randn(N, device=DEV)
+    o0 = out.clone()
+    ops.colsum(x, out, accumulate=True, scale=0.5)
+    assert rel(out - o0, 0.5 * x.float().sum(0)) < 1e-5
+
+
+def _ln_ref(x, dy, w, b, eps):
+    x = x.detach().clone().requires_grad_(True)
+    w = w.detach().clone().requires_grad_(True)
+    b = b.detach().clone().requires_grad_(True)
+    y = F.layer_norm(x, (x.shape[1],), w, b, eps)
+    y.backward(dy)
+    return x.grad, w.grad, b.grad
+
+
+@pytest.mark.parametrize("cols", [384, 1024, 2048])
+@pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_bwd(ops, cols, dy_dtype):
+    torch.manual_seed(5)
+    R = 3001
+    x = torch.randn(R, cols, device=DEV) * 2 + 0.5
+    w = torch.randn(cols, device=DEV)
+    b = torch.randn(cols, device=DEV)
+    dy = torch.randn(R, cols, device=DEV).to(dy_dtype)
+    dx0 = torch.randn(R, cols, device=DEV)
+    dx = dx0.clone()
+    dxb = torch.empty(R, cols, device=DEV, dtype=torch.bfloat16)
+    dw = torch.zeros(cols, device=DEV)
+    db = torch.zeros(cols, device=DEV)
+    ops.layernorm_bwd(x, dy, w, 1e-5, dx, dxb=dxb, dw=dw, db=db)
+    gx, gw, gb = _ln_ref(x, dy.float(), w, b, 1e-5)
+    assert rel(dx - dx0, gx) < 1e-5
+    assert rel(dxb.float(), dx) < 8e-3
+    assert rel(dw, gw) < 1e-5 and rel(db, gb) < 1e-5
+
+
+def test_layernorm_bwd_rowmap(ops):
+    """Gathered rows (reloc anchor subsample): x rows and dx rows through the map."""
+    torch.manual_seed(6)
+    R, n, cols = 2000, 300, 1024
+    x = torch.randn(R, cols, device=DEV)
+    w = torch.randn(cols, device=DEV)
+    rowmap = torch.randperm(R, device=DEV)[:n].int()
+    dy = torch.randn(n, cols, device=DEV).bfloat16()
+    dx = torch.zeros(R, cols, device=DEV)
+    dw = torch.zeros(cols, device=DEV)
+    db = torch.zeros(cols, device=DEV)
+    ops.layernorm_bwd(x, dy, w, 1e-6, dx, rowmap=rowmap, dw=dw, db=db)
+    xs = x[rowmap.long()]
+    gx, gw, gb = _ln_ref(xs, dy.float(), w, torch.zeros_like(w), 1e-6)
+    ref = torch.zeros_like(dx)
+    ref[rowmap.long()] = gx
+    assert rel(dx, ref) < 1e-5
+    assert rel(dw, gw) < 1e-5 and rel(db, gb) < 1e-5
+
+
+def _qk_fwd_ref(raw, C, D, qkv, pos):
+    """fp32 statement of the SR_EPI_QKV transform on pre-norm rows (attention.py:72-82)."""
+    from oracle.sfm_oracle import rope2d
+    M = raw.shape[0]
+    H = C // D
+    y = raw.view(M, 3, H, D)
+    outs = []
+    for region, (nw, nb) in enumerate(((qkv["qn_w"], qkv["qn_b"]), (qkv["kn_w"], qkv["kn_b"]))):
+        t = F.layer_norm(y[:, region], (D,), nw, nb, qkv["qk_eps"])
+        t = rope2d(t.permute(1, 0, 2)[None], pos[None])[0].permute(1, 0, 2)
+        outs.append(t)
+    outs.append(y[:, 2])
+    return torch.stack(outs, 1).reshape(M, 3 * C)
+
+
+@pytest.mark.parametrize("C,frames,col_offset", [(256, 30, 0), (384, 7, 0), (1024, 4, 1)])
+def test_qk_bwd(ops, C, frames, col_offset):
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    torch.manual_seed(7)
+    D, P, gw = 64, 21, 4
+    M = frames * P
+    raw = (torch.randn(M, 3 * C) * 1.5 + 0.3).bfloat16().float()
+    dout = torch.randn(M, 3 * C)
+    nrm = [torch.randn(D) for _ in range(4)]
+    qkv_cpu = dict(qn_w=nrm[0], qn_b=nrm[1], kn_w=nrm[2], kn_b=nrm[3], qk_eps=1e-5)
+    t = torch.arange(M) % P
+    p = (t - 5).clamp_min(0)
+    pos = torch.stack([p // gw + 1, p % gw + 1], -1) * (t >= 5)[:, None]
+    params = [raw] + nrm
+    for z in params:
+        z.requires_grad_(True)
+    _qk_fwd_ref(raw, C, D, dict(qkv_cpu, qn_w=nrm[0], qn_b=nrm[1], kn_w=nrm[2], kn_b=nrm[3]), pos).backward(dout)
+    rope = RotaryPositionEmbedding2D(100).tables(D, 5, DEV)
+    epi = dict(embed_dim=C, head_dim=D, qk_eps=1e-5, qn_w=nrm[0].detach().to(DEV), qn_b=nrm[1].detach().to(DEV),
+               kn_w=nrm[2].detach().to(DEV), kn_b=nrm[3].detach().to(DEV), rope_cos=rope[0], rope_sin=rope[1],
+               tokens_per_frame=P, patch_start=5, grid_w=gw, pos_row_base=0)
+    lo = C if col_offset else 0
+    if col_offset:
+        epi["col_offset"] = C
+    raw_d = raw.detach()[:, lo:].to(DEV).bfloat16().contiguous()
+    d_d = dout[:, lo:].to(DEV).contiguous()
+    out = torch.empty(M, 3 * C - lo, device=DEV, dtype=torch.bfloat16)
+    grads = torch.zeros(4, D, device=DEV)
+    ops.qk_bwd(raw_d, d_d, out, epi, grads=grads)
+    assert rel(out.float().cpu(), raw.grad[:, lo:]) < 8e-3
+    gref = torch.stack([nrm[0].grad, nrm[1].grad, nrm[2].grad, nrm[3].grad])
+    if col_offset:
+        assert rel(grads[2:].cpu(), gref[2:]) < 1e-5
+    else:
+        assert rel(grads.cpu(), gref) < 1e-5
+
+
+def test_qk_bwd_plain_cast(ops):
+    """No qk-norm, no RoPE (DINO blocks): the backward is the bf16 cast of dq|dk|dv."""
+    M, C = 500, 384
+    d = torch.randn(M, 3 * C, device=DEV)
+    out = torch.empty(M, 3 * C, device=DEV, dtype=torch.bfloat16)
+    ops.qk_bwd(None, d, out, dict(embed_dim=C, head_dim=64))
+    assert torch.equal(out, d.bfloat16())
+
+
+def test_cast_nonfinite_adam(ops):
+    torch.manual_seed(8)
+    src = torch.randn(100, 64, device=DEV)
+    dst = torch.empty(100, 64, device=DEV, dtype=torch.bfloat16)
+    ops.cast_bf16(src, dst, 0.5)
+    assert torch.equal(dst, (src * 0.5).bfloat16())
+    n = 10007
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV) * 1024.0
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    scale = torch.tensor([1024.0], device=DEV)
+    found = torch.zeros(1, device=DEV, dtype=torch.int32)
+    ops.nonfinite_check(g, found, scale)
+    assert int(found.item()) == 0
+    ref_p = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref_p], lr=2e-4, betas=(0.9, 0.999), eps=1e-8)
+    for step in (1, 2, 3):
+        ref_p.grad = g / 1024.0
+        opt.step()
+        ops.adam(p, g, m, v, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=step, scale=scale,
+                 found_inf=found)
+    assert rel(p, ref_p.detach()) < 1e-6
+    g[17] = float("inf")
+    ops.nonfinite_check(g, found, scale)
+    assert int(found.item()) == 1
+    p0 = p.clone()
+    ops.adam(p, g, m, v, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=4, scale=scale,
+             found_inf=found)
+    assert torch.equal(p, p0)
