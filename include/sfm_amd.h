@@ -244,6 +244,37 @@ int sr_nonfinite_check(sr_stream_t stream, const float* g, int64_t n, const floa
 int sr_adam_f32(sr_stream_t stream, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                 float beta2, float eps, float weight_decay, int step, const float* scale, const int* found_inf);
 
+/* dst[c][r] = out_dtype(rowscale[r] * src[r][c])  (fp32 src [rows][lds]; W^T packs of the dgrad
+ * GEMMs with LayerScale gamma folded into W's rows; rowscale may be NULL) */
+int sr_transpose_f32(sr_stream_t stream, int out_dtype, const float* src, int64_t lds, int rows, int cols,
+                     const float* rowscale, void* dst, int64_t ldd);
+
+/* Camera-head backward (fp32, few rows; camera_head.py:123-186 under autocast off):
+ * G[n][k] = sum_m A[m][n] B[m][k];  db[n] (+)= sum_m A[m][n] (db may be NULL);
+ * dW = (accumulate ? dW : 0) + (rowscale ? rowscale[n] : 1) G;  rowdot[n] += <wdot[n], G[n]>
+ * (rowscale / wdot need workspace >= N*K floats and K % 4 == 0), any N, K otherwise. */
+int sr_wgrad_small_f32(sr_stream_t stream, const float* A, int64_t lda, const float* B, int64_t ldb, float* dW,
+                       int64_t lddw, int M, int N, int K, int accumulate, float* db, const float* rowscale,
+                       const float* wdot, int64_t ldwd, float* rowdot, float* workspace);
+
+/* fp32 attention backward of one item of L <= 1024 rows (q|k|v rows of stride ld, head h at
+ * column h*head_dim), mask SR_MASK_NONE or SR_MASK_CAMERA (~build_lr_mask): dq, dk, dv fp32
+ * [L][ldg] (written).  Softmax recomputed; workspace >= 2 * heads * L * L floats. */
+int sr_attention_bwd_small_f32(sr_stream_t stream, const float* q, const float* k, const float* v, int64_t ld,
+                               const float* dout, int64_t lddo, float* dq, float* dk, float* dv, int64_t ldg, int L,
+                               int heads, int head_dim, float scale, int mask_mode, int n_anchor, float* workspace);
+
+/* adaLN modulate backward (camera_head.py:156-161): dxn = dxm*gate*(1+scale); dmod [rows][3*cols]
+ * = [dxm*gate | dxm*gate*xn | dxm*(xn*(1+scale)+shift)] (the residual dx += dxm is the caller's). */
+int sr_adaln_bwd_f32(sr_stream_t stream, const float* xn, const float* mod, const float* dxm, float* dxn, float* dmod,
+                     int rows, int cols);
+
+/* dx = dy * act'(x): mode 0 SiLU, 1 erf-GELU (fp32, exact) */
+int sr_act_bwd_f32(sr_stream_t stream, int mode, const float* x, const float* dy, float* dx, int64_t n);
+
+/* out[i] += a[i] * b[i] */
+int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, const float* b, int n);
+
 /* ------------------------------------------------------------------------
  * LayerNorm over the last dim of fp32 rows (block.py:50,70; camera_head.py:64-77;
  * vision_transformer.py:192,300).  out_row r = LN(x[rowmap ? rowmap[r] : r]).

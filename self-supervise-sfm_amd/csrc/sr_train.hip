@@ -489,6 +489,191 @@ __global__ __launch_bounds__(256) void adam_kernel(float* p, const float* __rest
   }
 }
 
+
+// ================================================================ weight packs for the dgrad GEMMs
+// dst[c][r] = T(rowscale[r] * src[r][c])  (the W^T operand of dX = dY . W, with LayerScale gamma
+// folded into the rows of W); 64 x 64 LDS tiles, padded against bank conflicts.
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ src, int64_t lds, int R, int C,
+                                                        const float* __restrict__ rowscale, T* dst, int64_t ldd) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? src[(int64_t)r * lds + c] * (rowscale ? rowscale[r] : 1.f) : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) dst[(int64_t)c * ldd + r] = sr::from_f32<T>(tile[tx][i]);
+  }
+}
+
+// ================================================================ small fp32 backward (camera head)
+// dW[n][k] (+)= sum_m A[m][n] B[m][k] for few rows M (camera trunk / pose branch: M = 2N views);
+// thread = one (n, k); db[n] (+)= sum_m A[m][n] from the k == 0 threads.
+__global__ __launch_bounds__(256) void wgrad_small_kernel(const float* __restrict__ A, int64_t lda,
+                                                          const float* __restrict__ B, int64_t ldb, float* dW,
+                                                          int64_t lddw, int M, int N, int K, int accumulate, float* db) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)N * K) return;
+  const int n = (int)(e / K), k = (int)(e - (int64_t)n * K);
+  float s = 0.f, sb = 0.f;
+  for (int m = 0; m < M; ++m) {
+    const float a = A[(int64_t)m * lda + n];
+    s = fmaf(a, B[(int64_t)m * ldb + k], s);
+    sb += a;
+  }
+  float* o = dW + (int64_t)n * lddw + k;
+  *o = accumulate ? *o + s : s;
+  if (db && k == 0) db[n] = accumulate ? db[n] + sb : sb;
+}
+
+// Masked fp32 attention backward for one batch item of few rows (camera trunk: L = 2N tokens,
+// head_dim 128, SR_MASK_CAMERA = ~build_lr_mask, camera_head.py:165,197-228).
+// Pass 1, one workgroup per (query row i, head): scores over all allowed keys, softmax, P and
+// dS = P (dP - sum_j P dP) into workspace [heads][L][L].  Pass 2: dQ = c dS K, dK = c dS^T Q,
+// dV = P^T dO, one thread per output element.
+__device__ __forceinline__ bool cam_allowed(int mask_mode, int n_anchor, int i, int j) {
+  return mask_mode != SR_MASK_CAMERA || j < n_anchor || j == i;
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_small_p_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                               const float* __restrict__ v, int64_t ld,
+                                                               const float* __restrict__ dout, int64_t lddo, int L, int D,
+                                                               float scale, int mask_mode, int n_anchor, float* P,
+                                                               float* dS) {
+  __shared__ float red[2][4];
+  const int i = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const float* qi = q + (int64_t)i * ld + h * D;
+  const float* gi = dout + (int64_t)i * lddo + h * D;
+  float* Pi = P + ((int64_t)h * L + i) * L;
+  float* dSi = dS + ((int64_t)h * L + i) * L;
+  // scores / dP for keys j = tid, tid + 256, ...  (L <= 1024: 4 per thread)
+  float sc[4], dp[4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = tid + 256 * u;
+    sc[u] = -INFINITY;
+    dp[u] = 0.f;
+    if (j < L && cam_allowed(mask_mode, n_anchor, i, j)) {
+      const float* kj = k + (int64_t)j * ld + h * D;
+      const float* vj = v + (int64_t)j * ld + h * D;
+      float s = 0.f, d = 0.f;
+      for (int c = 0; c < D; ++c) {
+        s = fmaf(qi[c], kj[c], s);
+        d = fmaf(gi[c], vj[c], d);
+      }
+      sc[u] = s * scale;
+      dp[u] = d;
+      mx = fmaxf(mx, sc[u]);
+    }
+  }
+  mx = sr::wave_max(mx);
+  if ((tid & 63) == 0) red[0][tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  float sum = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    sc[u] = sc[u] == -INFINITY ? 0.f : expf(sc[u] - mx);
+    sum += sc[u];
+  }
+  sum = sr::wave_sum(sum);
+  __syncthreads();
+  if ((tid & 63) == 0) red[0][tid >> 6] = sum;
+  __syncthreads();
+  const float inv = 1.f / ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]));
+  float pd = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    sc[u] *= inv;
+    pd += sc[u] * dp[u];
+  }
+  pd = sr::wave_sum(pd);
+  if ((tid & 63) == 0) red[1][tid >> 6] = pd;
+  __syncthreads();
+  const float delta = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = tid + 256 * u;
+    if (j < L) {
+      Pi[j] = sc[u];
+      dSi[j] = sc[u] * (dp[u] - delta);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_small_grad_kernel(const float* __restrict__ q,
+                                                                  const float* __restrict__ k, int64_t ld,
+                                                                  const float* __restrict__ dout, int64_t lddo, int L,
+                                                                  int D, int H, float scale, const float* __restrict__ P,
+                                                                  const float* __restrict__ dS, float* dq, float* dk,
+                                                                  float* dv, int64_t ldg) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = (int64_t)L * H * D;
+  if (e >= 3 * per) return;
+  const int which = (int)(e / per);
+  const int64_t r = e - which * per;
+  const int row = (int)(r / (H * D)), hc = (int)(r - (int64_t)row * H * D), h = hc / D;
+  const float* Ph = P + (int64_t)h * L * L;
+  const float* dSh = dS + (int64_t)h * L * L;
+  float s = 0.f;
+  if (which == 0) {  // dQ[i] = c sum_j dS[i][j] K[j]
+    for (int j = 0; j < L; ++j) s = fmaf(dSh[(int64_t)row * L + j], k[(int64_t)j * ld + hc], s);
+    dq[(int64_t)row * ldg + hc] = s * scale;
+  } else if (which == 1) {  // dK[j] = c sum_i dS[i][j] Q[i]
+    for (int i = 0; i < L; ++i) s = fmaf(dSh[(int64_t)i * L + row], q[(int64_t)i * ld + hc], s);
+    dk[(int64_t)row * ldg + hc] = s * scale;
+  } else {  // dV[j] = sum_i P[i][j] dO[i]
+    for (int i = 0; i < L; ++i) s = fmaf(Ph[(int64_t)i * L + row], dout[(int64_t)i * lddo + hc], s);
+    dv[(int64_t)row * ldg + hc] = s;
+  }
+}
+
+// adaLN backward (camera_head.py:156-161): xm = gate * (xn (1 + scale) + shift) + x
+//   dxn = dxm gate (1 + scale);  dmod = [dshift | dscale | dgate] = [dxm gate | dxm gate xn | dxm (xn (1 + scale) + shift)]
+__global__ void adaln_bwd_kernel(const float* __restrict__ xn, const float* __restrict__ mod,
+                                 const float* __restrict__ dxm, float* dxn, float* dmod, int rows, int cols) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % cols);
+    const int64_t r = e / cols;
+    const float* mr = mod + r * 3 * cols;
+    const float shift = mr[c], scale = mr[cols + c], gate = mr[2 * cols + c];
+    const float g = dxm[e], x = xn[e];
+    dxn[e] = g * gate * (1.f + scale);
+    float* dm = dmod + r * 3 * cols;
+    dm[c] = g * gate;
+    dm[cols + c] = g * gate * x;
+    dm[2 * cols + c] = g * (x * (1.f + scale) + shift);
+  }
+}
+
+// elementwise activation backward: mode 0 SiLU (poseLN_modulation[0]), 1 erf-GELU (Mlp.act)
+__global__ void act_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* dx, int64_t n,
+                               int mode) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[e];
+    float d;
+    if (mode == 0) {
+      const float sg = 1.f / (1.f + expf(-v));
+      d = sg * (1.f + v * (1.f - sg));
+    } else {
+      d = sr::gelu_erf_grad<false>(v);
+    }
+    dx[e] = dy[e] * d;
+  }
+}
+
+// out[i] += a[i] * b[i]  (LayerScale gamma / bias grads from column sums)
+__global__ void vec_fma_kernel(float* out, const float* __restrict__ a, const float* __restrict__ b, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] += a[i] * b[i];
+}
+
 unsigned grid_for(int64_t n, int64_t cap = 4096) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap));
 }
@@ -628,4 +813,78 @@ extern "C" int sr_adam_f32(sr_stream_t stream, float* p, const float* g, float* 
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
                      beta2, eps, weight_decay, bc1, std::sqrt(bc2), scale, found_inf);
   return sr::check_launch("sr_adam_f32");
+}
+
+extern "C" int sr_transpose_f32(sr_stream_t stream, int out_dtype, const float* src, int64_t lds, int rows, int cols,
+                                const float* rowscale, void* dst, int64_t ldd) {
+  SR_CHECK(src && dst && rows > 0 && cols > 0 && lds >= cols && ldd >= rows, SR_EINVAL, "sr_transpose_f32: bad args");
+  const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  if (out_dtype == SR_BF16)
+    hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, src, lds, rows, cols, rowscale,
+                       (bf16*)dst, ldd);
+  else
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, src, lds, rows, cols, rowscale,
+                       (float*)dst, ldd);
+  return sr::check_launch("sr_transpose_f32");
+}
+
+extern "C" int sr_wgrad_small_f32(sr_stream_t stream, const float* A, int64_t lda, const float* B, int64_t ldb,
+                                  float* dW, int64_t lddw, int M, int N, int K, int accumulate, float* db,
+                                  const float* rowscale, const float* wdot, int64_t ldwd, float* rowdot,
+                                  float* workspace) {
+  SR_CHECK(A && B && dW && M > 0 && N > 0 && K > 0 && lda >= N && ldb >= K && lddw >= K, SR_EINVAL,
+           "sr_wgrad_small_f32: bad args");
+  const bool fin = rowscale || wdot;
+  SR_CHECK(!fin || (workspace && K % 4 == 0 && lddw % 4 == 0 && (!wdot || (rowdot && ldwd % 4 == 0))), SR_EINVAL,
+           "sr_wgrad_small_f32: rowscale / wdot need workspace, K %% 4 == 0 and rowdot");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = (int64_t)N * K;
+  if (!fin) {
+    hipLaunchKernelGGL(wgrad_small_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, A, lda, B, ldb, dW,
+                       lddw, M, N, K, accumulate, db);
+  } else {  // G -> workspace, then the per-row finish of sr_gemm_wgrad (scale, accumulate, rowdot)
+    hipLaunchKernelGGL(wgrad_small_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, A, lda, B, ldb,
+                       workspace, (int64_t)K, M, N, K, 0, db);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, workspace, 1, N, K, dW, lddw, accumulate,
+                       rowscale, wdot, ldwd, rowdot);
+  }
+  return sr::check_launch("sr_wgrad_small_f32");
+}
+
+extern "C" int sr_attention_bwd_small_f32(sr_stream_t stream, const float* q, const float* k, const float* v, int64_t ld,
+                                          const float* dout, int64_t lddo, float* dq, float* dk, float* dv, int64_t ldg,
+                                          int L, int heads, int head_dim, float scale, int mask_mode, int n_anchor,
+                                          float* workspace) {
+  SR_CHECK(q && k && v && dout && dq && dk && dv && workspace, SR_EINVAL, "sr_attention_bwd_small_f32: null pointer");
+  SR_CHECK(L > 0 && L <= 1024 && heads > 0 && head_dim > 0, SR_EUNSUPPORTED,
+           "sr_attention_bwd_small_f32: L=%d (<= 1024)", L);
+  hipStream_t s = (hipStream_t)stream;
+  float* P = workspace;
+  float* dS = workspace + (int64_t)heads * L * L;
+  hipLaunchKernelGGL(attn_bwd_small_p_kernel, dim3(L, heads), dim3(256), 0, s, q, k, v, ld, dout, lddo, L, head_dim,
+                     scale, mask_mode, n_anchor, P, dS);
+  const int64_t n = 3ll * L * heads * head_dim;
+  hipLaunchKernelGGL(attn_bwd_small_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, k, ld, dout,
+                     lddo, L, head_dim, heads, scale, P, dS, dq, dk, dv, ldg);
+  return sr::check_launch("sr_attention_bwd_small_f32");
+}
+
+extern "C" int sr_adaln_bwd_f32(sr_stream_t stream, const float* xn, const float* mod, const float* dxm, float* dxn,
+                                float* dmod, int rows, int cols) {
+  SR_CHECK(xn && mod && dxm && dxn && dmod && rows > 0 && cols > 0, SR_EINVAL, "sr_adaln_bwd_f32: bad args");
+  hipLaunchKernelGGL(adaln_bwd_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(256), 0, (hipStream_t)stream, xn, mod,
+                     dxm, dxn, dmod, rows, cols);
+  return sr::check_launch("sr_adaln_bwd_f32");
+}
+
+extern "C" int sr_act_bwd_f32(sr_stream_t stream, int mode, const float* x, const float* dy, float* dx, int64_t n) {
+  SR_CHECK(x && dy && dx && n > 0 && (mode == 0 || mode == 1), SR_EINVAL, "sr_act_bwd_f32: bad args");
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, dy, dx, n, mode);
+  return sr::check_launch("sr_act_bwd_f32");
+}
+
+extern "C" int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, const float* b, int n) {
+  SR_CHECK(out && a && b && n > 0, SR_EINVAL, "sr_vec_fma_f32: bad args");
+  hipLaunchKernelGGL(vec_fma_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, a, b, n);
+  return sr::check_launch("sr_vec_fma_f32");
 }

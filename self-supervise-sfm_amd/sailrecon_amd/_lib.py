@@ -108,6 +108,14 @@ _PROTOS = {
     "sr_cast_bf16": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _f32]),
     "sr_nonfinite_check": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "sr_adam_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
+    "sr_transpose_f32": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i64]),
+    "sr_wgrad_small_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _i64,
+                                  _vp, _vp]),
+    "sr_attention_bwd_small_f32": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32,
+                                          _f32, _i32, _i32, _vp]),
+    "sr_adaln_bwd_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32]),
+    "sr_act_bwd_f32": (_i32, [_vp, _i32, _vp, _vp, _vp, _i64]),
+    "sr_vec_fma_f32": (_i32, [_vp, _vp, _vp, _vp, _i32]),
 }
 EXPORTED = tuple(_PROTOS)
 

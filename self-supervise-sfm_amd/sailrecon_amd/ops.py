@@ -172,8 +172,10 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         tag = f"gemm_{_EPI_NAME.get(epi, epi)}" + ("" if a.dtype == torch.bfloat16 else "_f32")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    if splits is None:
-        splits = _splitk_plan(M, N, K, epi, a.dtype)
+    if splits is None:  # the split-K reduction has no aux output: saved pre-activations need one pass
+        splits = 1 if aux is not None else _splitk_plan(M, N, K, epi, a.dtype)
+    elif splits > 1 and aux is not None:
+        raise ValueError("gemm: aux outputs are not supported with split-K")
     if splits > 1:
         ws = _splitk_workspace(a.device, splits * M * N)
         rc = _lib.load().sr_gemm_splitk(_stream(a), dtype_code(a.dtype), epi, _p(a), lda, _p(w), ldw, _p(out), ldo,
@@ -549,3 +551,64 @@ def adam(p: Tensor, g: Tensor, m: Tensor, v: Tensor, *, lr: float, beta1: float,
             raise ValueError("adam: p / g / m / v must be contiguous fp32 of one size")
     check(_lib.load().sr_adam_f32(_stream(p), _p(p), _p(g), _p(m), _p(v), p.numel(), lr, beta1, beta2, eps,
                                   weight_decay, step, _p(scale), _p(found_inf)), "sr_adam_f32")
+
+
+def transpose(src: Tensor, dst: Tensor, rowscale: Optional[Tensor] = None) -> None:
+    """dst[c, r] = dst.dtype(rowscale[r] * src[r, c]) (fp32 src)."""
+    R, C = src.shape
+    if src.dtype != torch.float32 or dst.shape != (C, R):
+        raise ValueError(f"transpose: src {tuple(src.shape)} {src.dtype} -> dst {tuple(dst.shape)}")
+    check(_lib.load().sr_transpose_f32(_stream(src), dtype_code(dst.dtype), _p(src), _rowmajor(src, "src"), R, C,
+                                       _p(rowscale), _p(dst), _rowmajor(dst, "dst")), "sr_transpose_f32")
+
+
+def wgrad_small(dy: Tensor, x: Tensor, dw: Tensor, *, db: Optional[Tensor] = None, accumulate: bool = False,
+                rowscale: Optional[Tensor] = None, wdot: Optional[Tensor] = None,
+                rowdot: Optional[Tensor] = None) -> None:
+    """fp32 dw[N,K] (+)= rowscale[n] * dy[M,N]^T x[M,K]; db[N] (+)= colsum(dy); rowdot += <wdot, G>."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if dw.shape != (N, K) or x.shape[0] != M:
+        raise ValueError("wgrad_small: shape mismatch")
+    ws = _train_ws(dy.device, "wgrad", N * K) if (rowscale is not None or wdot is not None) else None
+    check(_lib.load().sr_wgrad_small_f32(_stream(dy), _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(dw),
+                                         _rowmajor(dw, "dw"), M, N, K, int(accumulate), _p(db), _p(rowscale),
+                                         _p(wdot), 0 if wdot is None else _rowmajor(wdot, "wdot"), _p(rowdot),
+                                         _p(ws)), "sr_wgrad_small_f32")
+
+
+def attention_bwd_small(q: Tensor, k: Tensor, v: Tensor, dout: Tensor, dq: Tensor, dk: Tensor, dv: Tensor, *,
+                        heads: int, head_dim: int, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
+                        scale: Optional[float] = None) -> None:
+    L = q.shape[0]
+    ld = _rowmajor(q, "q")
+    if _rowmajor(k, "k") != ld or _rowmajor(v, "v") != ld:
+        raise ValueError("attention_bwd_small: q / k / v must share a row stride")
+    ldg = _rowmajor(dq, "dq")
+    if _rowmajor(dk, "dk") != ldg or _rowmajor(dv, "dv") != ldg:
+        raise ValueError("attention_bwd_small: dq / dk / dv must share a row stride")
+    ws = _train_ws(q.device, "attn_small", 2 * heads * L * L)
+    check(_lib.load().sr_attention_bwd_small_f32(_stream(q), _p(q), _p(k), _p(v), ld, _p(dout),
+                                                 _rowmajor(dout, "dout"), _p(dq), _p(dk), _p(dv), ldg, L, heads,
+                                                 head_dim, head_dim ** -0.5 if scale is None else scale, mask_mode,
+                                                 n_anchor, _p(ws)), "sr_attention_bwd_small_f32")
+
+
+def adaln_bwd(xn: Tensor, mod: Tensor, dxm: Tensor, dxn: Tensor, dmod: Tensor) -> None:
+    rows, cols = xn.shape
+    check(_lib.load().sr_adaln_bwd_f32(_stream(xn), _p(xn), _p(mod), _p(dxm), _p(dxn), _p(dmod), rows, cols),
+          "sr_adaln_bwd_f32")
+
+
+ACT_SILU, ACT_GELU = 0, 1
+
+
+def act_bwd(mode: int, x: Tensor, dy: Tensor, dx: Tensor) -> None:
+    for t in (x, dy, dx):
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise ValueError("act_bwd: contiguous fp32 tensors required")
+    check(_lib.load().sr_act_bwd_f32(_stream(x), mode, _p(x), _p(dy), _p(dx), x.numel()), "sr_act_bwd_f32")
+
+
+def vec_fma(out: Tensor, a: Tensor, b: Tensor) -> None:
+    check(_lib.load().sr_vec_fma_f32(_stream(out), _p(out), _p(a), _p(b), out.numel()), "sr_vec_fma_f32")

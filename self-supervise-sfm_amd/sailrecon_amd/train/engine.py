@@ -1,0 +1,267 @@
+"""Block-level training engine: forward with saved activations ("tape") and backward, on the
+HIP kernels (the backward of block.py:86-112 / attention.py:70-122 /
+mlp.py:34-40 / layer_scale.py:22-23 that ``loss.backward()`` runs in train_imc.py:404).
+
+Forward (run_block_train) is run_block's kernel sequence with the backward's inputs kept:
+
+    x0 = x (copy)  LN1 -> xn1   GEMM qkv -> qkv  (+ aux: pre-norm q|k|v = raw)
+    attention(qkv) -> o (+ lse)   GEMM proj + gamma1 + residual (in place on x)
+    x1 = x (copy)  LN2 -> xn2   GEMM fc1 + GELU -> h (+ aux: pre-activation u)
+    GEMM fc2 + gamma2 + residual
+
+Backward (block_bwd) takes dx (fp32 residual grad of the block output, updated in place to the
+grad of its input) and dxb (its bf16 copy, the GEMM operand), and accumulates every parameter
+grad into the parameters' ``.grad`` tensors:
+
+    dU  = GELU'(u) * (dxb . (g2 W2))        dgrad GEMM, SR_EPI_GELU_BWD (W^T pack with g2 folded in)
+    dW2 = g2 * dxb^T h;  dg2 = <W2, dxb^T h> + b2 * colsum(dx);  db2 = g2 * colsum(dx)
+    dxn2 = dU . W1  (fp32);  dW1 = dU^T xn2;  db1 = colsum(dU)
+    dx  += LN2'(dxn2; x1)  (+ dxb refresh)   -> the same for proj (o), attention, qk-norm+RoPE, qkv, LN1
+
+Weights for the dgrad GEMMs are packed transposed once per optimizer step (BwdPack).  fp32
+blocks (the camera trunk, autocast off) use the same sequence with fp32 GEMMs, the small-row
+weight-gradient kernel and the masked fp32 attention backward.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+
+from .. import _lib, ops, runtime
+
+Tensor = torch.Tensor
+
+
+@dataclass
+class BlockTape:
+    x0: Tensor           # fp32 [R, C]  block input
+    x1: Tensor           # fp32 [R, C]  after the attention residual
+    xn1: Tensor          # dtype [R, C]
+    raw: Tensor          # dtype [R, 3C] pre-norm q|k|v (is qkv when there is no qk-norm / RoPE)
+    qkv: Tensor          # dtype [R, 3C]
+    o: Tensor            # dtype [R, C]
+    lse: Optional[Tensor]  # fp32 [batch*heads*lq] (bf16 attention)
+    xn2: Tensor          # dtype [R, C]
+    u: Tensor            # dtype [R, H] fc1 pre-activation
+    h: Tensor            # dtype [R, H]
+
+
+def alloc_tape(rows: int, dim: int, hidden: int, dtype: torch.dtype, device, lse_numel: int,
+               separate_raw: bool) -> BlockTape:
+    e = lambda r, c, dt=dtype: torch.empty(r, c, device=device, dtype=dt)  # noqa: E731
+    qkv = e(rows, 3 * dim)
+    return BlockTape(x0=e(rows, dim, torch.float32), x1=e(rows, dim, torch.float32), xn1=e(rows, dim),
+                     raw=e(rows, 3 * dim) if separate_raw else qkv, qkv=qkv, o=e(rows, dim),
+                     lse=torch.empty(lse_numel, device=device, dtype=torch.float32) if lse_numel else None,
+                     xn2=e(rows, dim), u=e(rows, hidden), h=e(rows, hidden))
+
+
+def run_block_train(pb: runtime.PackedBlock, x: Tensor, r0: int, r1: int, tape: BlockTape,
+                    attend: Callable[[Tensor, Tensor, Optional[Tensor]], None], qkv_epi: Optional[dict]) -> None:
+    """x[r0:r1] <- Block(x[r0:r1]) keeping the backward's inputs in ``tape``."""
+    xs = x[r0:r1]
+    R = r1 - r0
+    ops.copy_rows(tape.x0, xs, R)
+    ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, tape.xn1)
+    if qkv_epi is None:
+        ops.gemm(tape.xn1, pb.w_qkv, tape.qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
+    else:
+        ops.gemm(tape.xn1, pb.w_qkv, tape.qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, aux=tape.raw, tag="gemm")
+    attend(tape.qkv, tape.o, tape.lse)
+    ops.gemm(tape.o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
+    ops.copy_rows(tape.x1, xs, R)
+    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, tape.xn2)
+    ops.gemm(tape.xn2, pb.w_fc1, tape.h, _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, aux=tape.u, tag="gemm")
+    ops.gemm(tape.h, pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2, tag="gemm")
+
+
+# ----------------------------------------------------------------------------- parameters
+@dataclass
+class BlockGrads:
+    """The ``.grad`` tensors of one Block's parameters (fp32, accumulated into)."""
+    ln1_w: Tensor
+    ln1_b: Tensor
+    w_qkv: Tensor
+    b_qkv: Optional[Tensor]
+    qkn: Optional[Tensor]  # [4, head_dim] = q_norm.weight | q_norm.bias | k_norm.weight | k_norm.bias
+    w_proj: Tensor
+    b_proj: Optional[Tensor]
+    g1: Optional[Tensor]
+    ln2_w: Tensor
+    ln2_b: Tensor
+    w_fc1: Tensor
+    b_fc1: Optional[Tensor]
+    w_fc2: Tensor
+    b_fc2: Optional[Tensor]
+    g2: Optional[Tensor]
+
+
+def _grad(p) -> Optional[Tensor]:
+    if p is None:
+        return None
+    if p.grad is None:
+        raise RuntimeError("training engine: parameter grads must be allocated first (train.params.GradBuffer)")
+    return p.grad
+
+
+def block_grads(blk) -> BlockGrads:
+    a = blk.attn
+    qkn = None
+    if getattr(a, "qk_norm", False):
+        parts = [a.q_norm.weight.grad, a.q_norm.bias.grad, a.k_norm.weight.grad, a.k_norm.bias.grad]
+        if any(t is None for t in parts):
+            raise RuntimeError("training engine: qk-norm grads not allocated")
+        d = parts[0].numel()
+        base = parts[0].data_ptr()
+        if any(t.data_ptr() != base + 4 * d * i for i, t in enumerate(parts)):
+            raise RuntimeError("training engine: q_norm / k_norm grads must be one contiguous [4, head_dim] block")
+        qkn = parts[0].as_strided((4, d), (d, 1))
+    ls = lambda m: _grad(getattr(m, "gamma", None))  # noqa: E731
+    return BlockGrads(ln1_w=_grad(blk.norm1.weight), ln1_b=_grad(blk.norm1.bias), w_qkv=_grad(a.qkv.weight),
+                      b_qkv=_grad(a.qkv.bias), qkn=qkn, w_proj=_grad(a.proj.weight), b_proj=_grad(a.proj.bias),
+                      g1=ls(blk.ls1), ln2_w=_grad(blk.norm2.weight), ln2_b=_grad(blk.norm2.bias),
+                      w_fc1=_grad(blk.mlp.fc1.weight), b_fc1=_grad(blk.mlp.fc1.bias), w_fc2=_grad(blk.mlp.fc2.weight),
+                      b_fc2=_grad(blk.mlp.fc2.bias), g2=ls(blk.ls2))
+
+
+@dataclass
+class BwdPack:
+    """Per-optimizer-step transposed weights of one Block for the dgrad GEMMs (dtype), with the
+    LayerScale gammas folded into proj / fc2; fp32 masters for the gamma-grad row dots."""
+    wt_qkv: Tensor   # [C, 3C]  W_qkv^T
+    wt_proj: Tensor  # [C, C]   (g1 * W_proj)^T
+    wt_fc1: Tensor   # [C, H]   W_fc1^T
+    wt_fc2: Tensor   # [H, C]   (g2 * W_fc2)^T
+    w_proj: Tensor   # fp32 masters
+    w_fc2: Tensor
+    b_proj: Optional[Tensor]
+    b_fc2: Optional[Tensor]
+
+
+def pack_bwd(blk, pb: runtime.PackedBlock, dtype: torch.dtype, into: Optional[BwdPack] = None) -> BwdPack:
+    a = blk.attn
+    f = lambda t: t.detach()  # noqa: E731  (fp32 contiguous parameters: no copy)
+    wq, wp, w1, w2 = f(a.qkv.weight), f(a.proj.weight), f(blk.mlp.fc1.weight), f(blk.mlp.fc2.weight)
+    dev = wq.device
+    if into is None:
+        e = lambda r, c: torch.empty(r, c, device=dev, dtype=dtype)  # noqa: E731
+        into = BwdPack(wt_qkv=e(wq.shape[1], wq.shape[0]), wt_proj=e(wp.shape[1], wp.shape[0]),
+                       wt_fc1=e(w1.shape[1], w1.shape[0]), wt_fc2=e(w2.shape[1], w2.shape[0]), w_proj=wp, w_fc2=w2,
+                       b_proj=pb.b_proj, b_fc2=pb.b_fc2)
+    ops.transpose(wq, into.wt_qkv)
+    ops.transpose(wp, into.wt_proj, rowscale=pb.g1)
+    ops.transpose(w1, into.wt_fc1)
+    ops.transpose(w2, into.wt_fc2, rowscale=pb.g2)
+    return into
+
+
+class BwdScratch:
+    """Grow-only backward scratch shared by every block of one stream."""
+
+    def __init__(self):
+        self.ws = runtime.Workspace()
+
+    def get(self, name, rows, cols, dtype, device):
+        return self.ws.get(name, rows, cols, dtype, device)
+
+
+def _resid_param_grads(dx: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor], g_bias: Optional[Tensor],
+                       g_gamma: Optional[Tensor], tmp: Tensor) -> None:
+    """Bias and LayerScale-gamma grads of ``x += gamma * (a W^T + b)`` from colsum(dx):
+    db += gamma * s, dgamma += b * s (the <W, G> part comes from the wgrad row dots)."""
+    if g_bias is None and (g_gamma is None or bias is None):
+        return
+    ops.colsum(dx, tmp)
+    if g_bias is not None:
+        if gamma is None:
+            raise RuntimeError("bias grad without gamma")
+        ops.vec_fma(g_bias, gamma, tmp)
+    if g_gamma is not None and bias is not None:
+        ops.vec_fma(g_gamma, bias, tmp)
+
+
+def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTape, dx: Tensor,
+              dxb: Optional[Tensor], attend_bwd: Callable[[BlockTape, Tensor, Tensor], None],
+              qkv_epi: Optional[dict], sc: BwdScratch, tag: str = "bwd") -> None:
+    """dx (fp32 [R, C], the grad of the block's output) <- grad of its input, in place; dxb
+    (bf16 copy of dx, bf16 blocks) refreshed alongside; parameter grads accumulated.
+    ``attend_bwd(tape, dO, dqkv)`` writes fp32 dq|dk|dv into dqkv [R, 3C] (and any shared-segment
+    grads elsewhere)."""
+    R, C = dx.shape
+    Hd = tape.u.shape[1]
+    dev = dx.device
+    dt = tape.xn1.dtype
+    bf = dt == torch.bfloat16
+    a_op = dxb if bf else dx   # GEMM operand view of dx
+    tmp = sc.get("colsum_tmp", 1, max(C, Hd, 3 * C), torch.float32, dev)[0]
+
+    def wgrad(dy, x, dw, db=None, rowscale=None, wdot=None, rowdot=None):
+        if bf:
+            ops.gemm_wgrad(dy, x, dw, accumulate=True, rowscale=rowscale, wdot=wdot, rowdot=rowdot, tag=tag + ".wgrad")
+            if db is not None:
+                ops.colsum(dy, db, accumulate=True)
+        else:
+            ops.wgrad_small(dy, x, dw, db=db, accumulate=True, rowscale=rowscale, wdot=wdot, rowdot=rowdot)
+
+    # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
+    dU = sc.get("dU", R, Hd, dt, dev)
+    ops.gemm(a_op, bp.wt_fc2, dU, _lib.SR_EPI_GELU_BWD, aux=tape.u, tag=tag + ".dgrad")
+    wgrad(a_op, tape.h, g.w_fc2, rowscale=pb.g2, wdot=bp.w_fc2 if g.g2 is not None else None,
+          rowdot=g.g2 if g.g2 is not None else None)
+    _resid_param_grads(dx, bp.b_fc2, pb.g2, g.b_fc2, g.g2, tmp[:C])
+    dxn = sc.get("dxn", R, C, torch.float32, dev)
+    ops.gemm(dU, bp.wt_fc1, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
+    wgrad(dU, tape.xn2, g.w_fc1, db=g.b_fc1)
+    ops.layernorm_bwd(tape.x1, dxn, pb.ln2_w, pb.eps, dx, dxb=dxb, dw=g.ln2_w, db=g.ln2_b)
+
+    # ---- attention: x1 = x0 + g1 * proj(attn(qk(qkv(LN1(x0)))))
+    dO = sc.get("dO", R, C, dt, dev)
+    ops.gemm(a_op, bp.wt_proj, dO, _lib.SR_EPI_BIAS, tag=tag + ".dgrad")
+    wgrad(a_op, tape.o, g.w_proj, rowscale=pb.g1, wdot=bp.w_proj if g.g1 is not None else None,
+          rowdot=g.g1 if g.g1 is not None else None)
+    _resid_param_grads(dx, bp.b_proj, pb.g1, g.b_proj, g.g1, tmp[:C])
+    dqkv = sc.get("dqkv", R, 3 * C, torch.float32, dev)
+    attend_bwd(tape, dO, dqkv)
+    if bf:
+        draw = sc.get("draw", R, 3 * C, dt, dev)
+        ops.qk_bwd(tape.raw if qkv_epi is not None else None, dqkv, draw, qkv_epi or dict(embed_dim=C, head_dim=64),
+                   grads=g.qkn)
+    else:
+        if qkv_epi is not None:
+            raise NotImplementedError("fp32 block backward with qk-norm / RoPE")
+        draw = dqkv
+    ops.gemm(draw, bp.wt_qkv, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
+    wgrad(draw, tape.xn1, g.w_qkv, db=g.b_qkv)
+    ops.layernorm_bwd(tape.x0, dxn, pb.ln1_w, pb.eps, dx, dxb=dxb, dw=g.ln1_w, db=g.ln1_b)
+
+
+def frame_attend_train(pb: runtime.PackedBlock, frames: int, tokens: int):
+    """Forward / backward attention callbacks within each frame (frame and DINO blocks)."""
+    C = pb.dim
+
+    def fwd(qkv, o, lse):
+        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=pb.heads, head_dim=pb.head_dim,
+                      batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, lse=lse,
+                      tag="attn_frame")
+
+    def bwd(tape, dO, dqkv):
+        q = tape.qkv
+        delta = _delta(dqkv.device, frames * pb.heads * tokens)
+        ops.attention_bwd(q[:, 0:C], q[:, C:2 * C], q[:, 2 * C:], tape.o, tape.lse, dO, dqkv[:, 0:C],
+                          dqkv[:, C:2 * C], dqkv[:, 2 * C:], delta, heads=pb.heads, batch=frames, lq=tokens,
+                          q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_bwd_frame")
+    return fwd, bwd
+
+
+_DELTA = {}
+
+
+def _delta(device, n: int) -> Tensor:
+    t = _DELTA.get(device)
+    if t is None or t.numel() < n:
+        t = torch.empty(n, device=device, dtype=torch.float32)
+        _DELTA[device] = t
+    return t[:n]

@@ -1,0 +1,136 @@
+"""Block forward-with-tape + backward (training engine) against torch autograd of the oracle's
+fp32 Block (oracle.sfm_oracle.block = block.py:86-112) on the same parameters and input.
+
+bf16 blocks (aggregator / DINO style, frame attention; qk-norm + 2-D RoPE or neither): bf16
+GEMM / attention operands with fp32 accumulation against an fp32 reference -> 3e-2 rel-L2 on
+the input grad and every parameter grad.  fp32 camera-trunk block (head_dim 128, camera mask,
+f32 MFMA GEMMs, exact fp32 attention backward) -> 1e-4."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _randomize(blk, seed):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in blk.named_parameters():
+            if n.endswith("gamma"):
+                p.copy_(0.5 + torch.rand(p.shape, generator=g))
+            elif "norm" in n and n.endswith("weight"):
+                p.copy_(1 + 0.2 * torch.randn(p.shape, generator=g))
+            elif n.endswith("bias"):
+                p.copy_(0.1 * torch.randn(p.shape, generator=g))
+            else:
+                p.copy_(torch.randn(p.shape, generator=g) / p.shape[-1] ** 0.5)
+
+
+def _positions(frames, P, gw):
+    t = torch.arange(frames * P) % P
+    p = (t - 5).clamp_min(0)
+    return torch.stack([p // gw + 1, p % gw + 1], -1) * (t >= 5)[:, None]
+
+
+@pytest.mark.parametrize("style", ["aggregator", "dino"])
+def test_block_backward_bf16(style):
+    from oracle import sfm_oracle as O
+    from sailrecon_amd import runtime
+    from sailrecon_amd.layers.block import Block
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    from sailrecon_amd.train import engine
+    from sailrecon_amd.train.params import FlatParams
+    torch.manual_seed(0)
+    C, H, frames, gh, gw = 256, 4, 3, 4, 5
+    P = 5 + gh * gw
+    R = frames * P
+    agg = style == "aggregator"
+    rope = RotaryPositionEmbedding2D(100) if agg else None
+    blk = Block(dim=C, num_heads=H, init_values=0.01, qk_norm=agg, rope=rope)
+    _randomize(blk, 1)
+    sd = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    blk = blk.to(DEV)
+    fp = FlatParams(blk)
+    blk.invalidate_packed()
+    dt = torch.bfloat16
+    pb = blk.packed(dt)
+    qkv_epi = None
+    if agg:
+        tabs = rope.tables(C // H, max(gh, gw) + 1, DEV)
+        qkv_epi = runtime.qkv_params(pb, tabs, pos_row_base=0, tokens_per_frame=P, patch_start=5, grid_w=gw)
+    tape = engine.alloc_tape(R, C, 4 * C, dt, DEV, frames * H * P, separate_raw=qkv_epi is not None)
+    fwd, bwd = engine.frame_attend_train(pb, frames, P)
+    x = torch.randn(R, C)
+    xd = x.to(DEV)
+    engine.run_block_train(pb, xd, 0, R, tape, fwd, qkv_epi)
+    dy = torch.randn(R, C)
+    dx = dy.to(DEV)
+    dxb = dx.bfloat16()
+    fp.zero_grad()
+    bp = engine.pack_bwd(blk, pb, dt)
+    engine.block_bwd(pb, bp, engine.block_grads(blk), tape, dx, dxb, bwd, qkv_epi, engine.BwdScratch())
+    torch.cuda.synchronize()
+
+    # reference: autograd through the oracle block, fp32 CPU
+    ref = {k: v.clone().requires_grad_(True) for k, v in sd.items() if v.is_floating_point()}
+    xr = x.clone().requires_grad_(True)
+    pos = _positions(frames, P, gw).view(frames, P, 2) if agg else None
+    y = O.block(ref, "", xr.view(frames, P, C), H, 1e-5, pos=pos, qk_norm=agg,
+                rope_base=100.0 if agg else None)
+    y.backward(dy.view(frames, P, C))
+    assert rel(xd, y.detach().reshape(R, C)) < 1e-2  # forward output
+    assert rel(dx, xr.grad) < 3e-2, "input grad"
+    for n, p in blk.named_parameters():
+        assert rel(p.grad, ref[n].grad) < 3e-2, n
+
+
+def test_block_backward_fp32_camera():
+    from oracle import sfm_oracle as O
+    from sailrecon_amd import _lib, ops
+    from sailrecon_amd.layers.block import Block
+    from sailrecon_amd.train import engine
+    from sailrecon_amd.train.params import FlatParams
+    torch.manual_seed(0)
+    C, H, L, na = 256, 2, 24, 10   # head_dim 128 like the camera trunk
+    blk = Block(dim=C, num_heads=H, init_values=0.01)
+    _randomize(blk, 2)
+    sd = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    blk = blk.to(DEV)
+    fp = FlatParams(blk)
+    blk.invalidate_packed()
+    dt = torch.float32
+    pb = blk.packed(dt)
+    tape = engine.alloc_tape(L, C, 4 * C, dt, DEV, 0, separate_raw=False)
+
+    def fwd(qkv, o, lse):
+        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=C // H, batch=1, lq=L,
+                      q_bstride=0, l0=L, k0_bstride=0, mask_mode=_lib.SR_MASK_CAMERA, n_anchor=na)
+
+    def bwd(tp, dO, dqkv):
+        q = tp.qkv
+        ops.attention_bwd_small(q[:, 0:C], q[:, C:2 * C], q[:, 2 * C:], dO, dqkv[:, 0:C], dqkv[:, C:2 * C],
+                                dqkv[:, 2 * C:], heads=H, head_dim=C // H, mask_mode=_lib.SR_MASK_CAMERA, n_anchor=na)
+    x = torch.randn(L, C)
+    xd = x.to(DEV)
+    engine.run_block_train(pb, xd, 0, L, tape, fwd, None)
+    dy = torch.randn(L, C)
+    dx = dy.to(DEV)
+    fp.zero_grad()
+    bp = engine.pack_bwd(blk, pb, dt)
+    engine.block_bwd(pb, bp, engine.block_grads(blk), tape, dx, None, bwd, None, engine.BwdScratch())
+    torch.cuda.synchronize()
+    ref = {k: v.clone().requires_grad_(True) for k, v in sd.items() if v.is_floating_point()}
+    xr = x.clone().requires_grad_(True)
+    allow = ~O.build_lr_mask(L, list(range(na)))
+    y = O.block(ref, "", xr[None], H, 1e-5, mask=allow)
+    y.backward(dy[None])
+    assert rel(xd, y.detach()[0]) < 1e-5
+    assert rel(dx, xr.grad) < 1e-4, "input grad"
+    for n, p in blk.named_parameters():
+        assert rel(p.grad, ref[n].grad) < 1e-4, n

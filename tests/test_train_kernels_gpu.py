@@ -266,3 +266,63 @@ def test_cast_nonfinite_adam(ops):
     ops.adam(p, g, m, v, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=4, scale=scale,
              found_inf=found)
     assert torch.equal(p, p0)
+
+
+@pytest.mark.parametrize("mask", [False, True])
+def test_attention_bwd_small_f32(ops, mask):
+    """Camera-trunk attention backward: fp32, head_dim 128, ~build_lr_mask."""
+    torch.manual_seed(9)
+    L_, H, D, na = 24, 2, 128, 10
+    C = H * D
+    qkv = torch.randn(L_, 3 * C, device=DEV)
+    g = torch.randn(L_, C, device=DEV)
+    d = torch.empty(L_, 3 * C, device=DEV)
+    lib = L()
+    ops.attention_bwd_small(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], g, d[:, :C], d[:, C:2 * C], d[:, 2 * C:],
+                            heads=H, head_dim=D, mask_mode=lib.SR_MASK_CAMERA if mask else lib.SR_MASK_NONE,
+                            n_anchor=na)
+    q, k, v = (qkv[:, i * C:(i + 1) * C].view(L_, H, D).transpose(0, 1).detach().clone().requires_grad_(True)
+               for i in range(3))
+    allow = torch.ones(L_, L_, dtype=torch.bool, device=DEV)
+    if mask:
+        allow = torch.zeros(L_, L_, dtype=torch.bool, device=DEV)
+        allow[:, :na] = True
+        allow[torch.arange(L_), torch.arange(L_)] = True
+    s = (q @ k.transpose(-1, -2)) * D ** -0.5
+    o = torch.softmax(s.masked_fill(~allow, float("-inf")), -1) @ v
+    o.backward(g.view(L_, H, D).transpose(0, 1))
+    for i, t in enumerate((q, k, v)):
+        assert rel(d[:, i * C:(i + 1) * C], t.grad.transpose(0, 1).reshape(L_, C)) < 1e-5, "qkv"[i]
+
+
+def test_fp32_backward_gemms(ops):
+    """fp32 dgrad epilogues (F32, GELU_BWD with fp32 aux, split-K BIAS) and the small-row wgrad."""
+    torch.manual_seed(10)
+    lib = L()
+    M, N, K = 24, 256, 768
+    a = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) / 16
+    out = torch.empty(M, N, device=DEV)
+    ops.gemm(a, w, out, lib.SR_EPI_F32)
+    assert rel(out, a @ w.t()) < 1e-5
+    ops.gemm(a, w, out, lib.SR_EPI_BIAS)
+    assert rel(out, a @ w.t()) < 1e-5
+    u = torch.randn(M, N, device=DEV)
+    ops.gemm(a, w, out, lib.SR_EPI_GELU_BWD, aux=u)
+    gp = 0.5 * (1 + torch.erf(u / math.sqrt(2))) + u * torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi)
+    assert rel(out, (a @ w.t()) * gp) < 1e-5
+    dy = torch.randn(M, N, device=DEV)
+    dw = torch.randn(N, K, device=DEV)
+    dw0 = dw.clone()
+    db = torch.zeros(N, device=DEV)
+    gam = torch.randn(N, device=DEV)
+    wd = torch.randn(N, K, device=DEV)
+    rd = torch.zeros(N, device=DEV)
+    ops.wgrad_small(dy, a, dw, db=db, accumulate=True, rowscale=gam, wdot=wd, rowdot=rd)
+    G = dy.t() @ a
+    assert rel(dw, dw0 + gam[:, None] * G) < 1e-5
+    assert rel(db, dy.sum(0)) < 1e-5
+    assert rel(rd, (wd * G).sum(1)) < 1e-5
+    sw = torch.empty(K, N, device=DEV)
+    ops.transpose(w, sw, rowscale=gam)
+    assert torch.allclose(sw, (w * gam[:, None]).t())
