@@ -272,6 +272,21 @@ int sr_adaln_bwd_f32(sr_stream_t stream, const float* xn, const float* mod, cons
 /* dx = dy * act'(x): mode 0 SiLU, 1 erf-GELU (fp32, exact) */
 int sr_act_bwd_f32(sr_stream_t stream, int mode, const float* x, const float* dy, float* dx, int64_t n);
 
+/* dst[rowmap[r]] (+)= src[r] for r < rows (fp32 rows, cols % 4 == 0; lds 0 broadcasts one row):
+ * the gradient of the aggregator's camera-token reads / special-token writes
+ * (aggregator.py:287-299,414-423).  Rows of one call must be distinct. */
+int sr_scatter_rows_f32(sr_stream_t stream, float* dst, int64_t ldd, const int32_t* rowmap, const float* src,
+                        int64_t lds, int rows, int cols, int accumulate);
+
+/* dst[r][c] (+)= src[r][c], any cols (lds 0 broadcasts one row) */
+int sr_copy2d_f32(sr_stream_t stream, float* dst, int64_t ldd, const float* src, int64_t lds, int rows, int cols,
+                  int accumulate);
+
+/* activate_pose backward for the camera head's last iteration (head_act.py:12-60; T / quat
+ * linear, FoV ReLU): dd [rows][9] = 0 on anchor rows r < n_anchor, else
+ * d_act[r - n_anchor] * (c < 7 || act[r][c] > 0); act = the forward's activated encoding. */
+int sr_pose_act_bwd_f32(sr_stream_t stream, float* dd, const float* d_act, const float* act, int rows, int n_anchor);
+
 /* out[i] += a[i] * b[i] */
 int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, const float* b, int n);
 

@@ -294,6 +294,8 @@ def camera_head_forward(sd: SD, feats_last: Tensor, cam_last: Tensor, heads: int
     pred = None
     outs = []
     for _ in range(iters):
+        if pred is not None:  # :148-150 detach the previous prediction (no backprop through time)
+            pred = pred.detach()
         inp = sd[pre + "empty_pose_tokens"].expand(B, S, -1) if pred is None else pred
         emb = F.linear(inp, sd[pre + "embed_pose.weight"], sd[pre + "embed_pose.bias"])
         mod = F.linear(F.silu(emb), sd[pre + "poseLN_modulation.1.weight"], sd[pre + "poseLN_modulation.1.bias"])

@@ -668,6 +668,47 @@ __global__ void act_bwd_kernel(const float* __restrict__ x, const float* __restr
   }
 }
 
+// dst[rowmap[r]] (+)= src[r]  (lds 0: one broadcast row), cols % 4 == 0
+__global__ __launch_bounds__(256) void scatter_rows_kernel(float* dst, int64_t ldd, const int32_t* __restrict__ rowmap,
+                                                           const float* __restrict__ src, int64_t lds, int rows,
+                                                           int cols, int accumulate) {
+  const int cq = cols / 4;
+  const int64_t n = (int64_t)rows * cq;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / cq), c = (int)(e - (int64_t)r * cq) * 4;
+    const f32x4 v = *(const f32x4*)(src + (int64_t)r * lds + c);
+    f32x4* d = (f32x4*)(dst + (int64_t)rowmap[r] * ldd + c);
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+// dst[r][c] (+)= src[r][c] for any cols (strided fp32 2-D copy / accumulate)
+__global__ __launch_bounds__(256) void copy2d_kernel(float* dst, int64_t ldd, const float* __restrict__ src,
+                                                     int64_t lds, int rows, int cols, int accumulate) {
+  const int64_t n = (int64_t)rows * cols;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / cols), c = (int)(e - (int64_t)r * cols);
+    const float v = src[(int64_t)r * lds + c];
+    float* d = dst + (int64_t)r * ldd + c;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+// activate_pose backward (head_act.py:12-60, linear T / quat, ReLU FoV) for the camera head's
+// last iteration: dd[r] = 0 for anchor rows r < n_anchor, else d_act[r - n_anchor] * (c < 7 || act > 0)
+__global__ void pose_act_bwd_kernel(float* dd, const float* __restrict__ d_act, const float* __restrict__ act, int rows,
+                                    int n_anchor) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * 9) return;
+  const int r = e / 9, c = e - r * 9;
+  float v = 0.f;
+  if (r >= n_anchor) {
+    v = d_act[(r - n_anchor) * 9 + c];
+    if (c >= 7 && !(act[e] > 0.f)) v = 0.f;
+  }
+  dd[e] = v;
+}
+
 // out[i] += a[i] * b[i]  (LayerScale gamma / bias grads from column sums)
 __global__ void vec_fma_kernel(float* out, const float* __restrict__ a, const float* __restrict__ b, int n) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -887,4 +928,30 @@ extern "C" int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, co
   SR_CHECK(out && a && b && n > 0, SR_EINVAL, "sr_vec_fma_f32: bad args");
   hipLaunchKernelGGL(vec_fma_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, a, b, n);
   return sr::check_launch("sr_vec_fma_f32");
+}
+
+extern "C" int sr_scatter_rows_f32(sr_stream_t stream, float* dst, int64_t ldd, const int32_t* rowmap, const float* src,
+                                   int64_t lds, int rows, int cols, int accumulate) {
+  SR_CHECK(dst && rowmap && src && rows > 0 && cols > 0 && cols % 4 == 0 && ldd % 4 == 0 && lds % 4 == 0, SR_EINVAL,
+           "sr_scatter_rows_f32: bad args");
+  const int64_t n = (int64_t)rows * (cols / 4);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dst, ldd, rowmap, src,
+                     lds, rows, cols, accumulate);
+  return sr::check_launch("sr_scatter_rows_f32");
+}
+
+extern "C" int sr_copy2d_f32(sr_stream_t stream, float* dst, int64_t ldd, const float* src, int64_t lds, int rows,
+                             int cols, int accumulate) {
+  SR_CHECK(dst && src && rows > 0 && cols > 0 && ldd >= cols && lds >= 0, SR_EINVAL, "sr_copy2d_f32: bad args");
+  hipLaunchKernelGGL(copy2d_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(256), 0, (hipStream_t)stream, dst, ldd,
+                     src, lds, rows, cols, accumulate);
+  return sr::check_launch("sr_copy2d_f32");
+}
+
+extern "C" int sr_pose_act_bwd_f32(sr_stream_t stream, float* dd, const float* d_act, const float* act, int rows,
+                                   int n_anchor) {
+  SR_CHECK(dd && d_act && act && rows > 0 && n_anchor >= 0, SR_EINVAL, "sr_pose_act_bwd_f32: bad args");
+  hipLaunchKernelGGL(pose_act_bwd_kernel, dim3((rows * 9 + 255) / 256), dim3(256), 0, (hipStream_t)stream, dd, d_act,
+                     act, rows, n_anchor);
+  return sr::check_launch("sr_pose_act_bwd_f32");
 }

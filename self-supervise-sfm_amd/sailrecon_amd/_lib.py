@@ -116,6 +116,9 @@ _PROTOS = {
     "sr_adaln_bwd_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32]),
     "sr_act_bwd_f32": (_i32, [_vp, _i32, _vp, _vp, _vp, _i64]),
     "sr_vec_fma_f32": (_i32, [_vp, _vp, _vp, _vp, _i32]),
+    "sr_scatter_rows_f32": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32]),
+    "sr_copy2d_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32]),
+    "sr_pose_act_bwd_f32": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32]),
 }
 EXPORTED = tuple(_PROTOS)
 

@@ -612,3 +612,27 @@ def act_bwd(mode: int, x: Tensor, dy: Tensor, dx: Tensor) -> None:
 
 def vec_fma(out: Tensor, a: Tensor, b: Tensor) -> None:
     check(_lib.load().sr_vec_fma_f32(_stream(out), _p(out), _p(a), _p(b), out.numel()), "sr_vec_fma_f32")
+
+
+def scatter_rows(dst: Tensor, rowmap: Tensor, src: Tensor, *, accumulate: bool = True, rows: Optional[int] = None) -> None:
+    """dst[rowmap[r]] (+)= src[r] (src with row stride 0 = one broadcast row)."""
+    n = rowmap.numel() if rows is None else rows
+    lds = 0 if src.dim() == 1 else _rowmajor(src, "src")
+    check(_lib.load().sr_scatter_rows_f32(_stream(dst), _p(dst), _rowmajor(dst, "dst"), _p(rowmap), _p(src), lds, n,
+                                          dst.shape[1], int(accumulate)), "sr_scatter_rows_f32")
+
+
+def copy2d(dst: Tensor, src: Tensor, *, accumulate: bool = False) -> None:
+    """dst (+)= src for 2-D fp32 row-strided views of one shape (any column count)."""
+    if dst.shape != src.shape or dst.dtype != torch.float32 or src.dtype != torch.float32:
+        raise ValueError(f"copy2d: {tuple(dst.shape)} vs {tuple(src.shape)}")
+    check(_lib.load().sr_copy2d_f32(_stream(dst), _p(dst), _rowmajor(dst, "dst"), _p(src), _rowmajor(src, "src"),
+                                    dst.shape[0], dst.shape[1], int(accumulate)), "sr_copy2d_f32")
+
+
+def pose_act_bwd(dd: Tensor, d_act: Tensor, act: Tensor, n_anchor: int) -> None:
+    for t in (dd, d_act, act):
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise ValueError("pose_act_bwd: contiguous fp32 tensors required")
+    check(_lib.load().sr_pose_act_bwd_f32(_stream(dd), _p(dd), _p(d_act), _p(act), dd.shape[0], n_anchor),
+          "sr_pose_act_bwd_f32")
