@@ -290,6 +290,45 @@ int sr_pose_act_bwd_f32(sr_stream_t stream, float* dd, const float* d_act, const
 /* out[i] += a[i] * b[i] */
 int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, const float* b, int n);
 
+/* Self-supervised IMC loss (compute_loss, train/train_imc.py:141-246; CDFLossIndexPytorch,
+ * train/losses/cdf_loss.py:19-242; geometry, train/utils/geometry.py:89-303): value and the
+ * gradient with respect to the query views' pose encodings, in one call.
+ *   enc      [n_views][9] activated pose encoding (absT_quaR_FoV), image H x W
+ *   kp2k     [n_views][3][3] K' -> K recovery matrices; shared_focal averages the recovered K
+ *   pairs    src_idx / dst_idx [n_pairs] (views), coords [n_pairs][n_points][2], depths
+ *            [n_pairs][n_points]; node_src / node_dst [n_pairs] the CDF histogram of each side
+ *            (the reference's module indices; train_epoch builds it on [0] / [0])
+ *   CDF      [min_val, max_val) in num_bins bins; smooth_w [2*smooth_radius+1] Gaussian taps
+ *   out      loss[0] (device fp32) and d_enc [n_views][9] = grad_scale * dloss/denc
+ * workspace >= sr_imc_loss_workspace(...) floats.  n_views <= 64, num_bins <= 1024. */
+typedef struct sr_imc_loss_desc {
+  const float* enc;
+  int n_views, H, W;
+  const float* kp2k;
+  int shared_focal;
+  int n_pairs, n_points;
+  const int32_t* src_idx;
+  const int32_t* dst_idx;
+  const float* src_coords;
+  const float* dst_coords;
+  const float* src_depth;
+  const float* dst_depth;
+  const int32_t* node_src;
+  const int32_t* node_dst;
+  int n_nodes;
+  float min_val, max_val;
+  int num_bins;
+  const float* smooth_w;
+  int smooth_radius;
+  float grad_scale;
+  float* loss;
+  float* d_enc;
+  float* workspace;
+} sr_imc_loss_desc;
+
+int64_t sr_imc_loss_workspace(int n_views, int n_pairs, int n_points, int n_nodes, int num_bins);
+int sr_imc_loss(sr_stream_t stream, const sr_imc_loss_desc* desc);
+
 /* ------------------------------------------------------------------------
  * LayerNorm over the last dim of fp32 rows (block.py:50,70; camera_head.py:64-77;
  * vision_transformer.py:192,300).  out_row r = LN(x[rowmap ? rowmap[r] : r]).

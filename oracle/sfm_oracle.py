@@ -578,3 +578,101 @@ def preprocess_image(img, target: int = 518, is_depth: bool = False):
     kp2k = torch.tensor([[1.0 / s, 0.0, -(pl * s) / s], [0.0, 1.0 / s, -(pt * s) / s], [0.0, 0.0, 1.0]],
                         dtype=torch.float32)
     return t[None], k2kp, kp2k
+
+
+# --------------------------------------------------------------------------
+# Self-supervised training loss: compute_loss (train/train_imc.py:141-246)
+# with CDFLossIndexPytorch (train/losses/cdf_loss.py:19-242) and the projective geometry of
+# train/utils/geometry.py:89-303.  Pinned by tests/golden/g8_loss.npz (reference modules).
+# --------------------------------------------------------------------------
+
+def cdf_smooth_kernel(bin_width: float, gradient_smooth: float) -> Tensor:
+    """cdf_loss.py:62-84: Gaussian smoothing taps (identity [1.0] when smoothing is off)."""
+    if gradient_smooth <= 0:
+        return torch.ones(1)
+    r = max(1, int(gradient_smooth / bin_width))
+    idx = torch.arange(2 * r + 1, dtype=torch.float32) - r
+    sigma = gradient_smooth / bin_width
+    g = torch.exp(-0.5 * (idx / sigma) ** 2)
+    return g / torch.sum(g)
+
+
+def _reflect_conv(x: Tensor, taps: Tensor) -> Tensor:
+    """Conv1d(padding=len//2, padding_mode='reflect') over the last dim (cross-correlation)."""
+    r = taps.numel() // 2
+    if r == 0:
+        return x * taps[0]
+    xp = F.pad(x[:, None], (r, r), mode="reflect")[:, 0]
+    return sum(taps[k] * xp[:, k:k + x.shape[1]] for k in range(taps.numel()))
+
+
+def cdf_loss_values(res: Tensor, w: Tensor, node_src: Tensor, node_dst: Tensor, n_nodes: int,
+                    min_val: float = 0.0, max_val: float = 15.0, num_bins: int = 250,
+                    gradient_smooth: float = 0.05) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """CDFLossIndexPytorch.forward's values and gradients (cdf_loss.py:88-242):
+    (cdf_src, grad_src, cdf_dst, grad_dst), each [pairs, points]."""
+    P, K = res.shape
+    bw = (max_val - min_val) / num_bins
+    b = ((res - min_val) / bw).long()                                    # :136-139 histogram bin
+    ok = ((b >= 0) & (b < num_bins)).float()
+    b = b.clamp(0, num_bins - 1)
+    hist = torch.zeros(n_nodes * num_bins)
+    tot = torch.zeros(n_nodes)
+    ns = node_src.long()[:, None].expand(P, K).reshape(-1)
+    nd = node_dst.long()[:, None].expand(P, K).reshape(-1)
+    hist.index_add_(0, ns * num_bins + b.reshape(-1), (w * ok).reshape(-1))
+    hist.index_add_(0, nd * num_bins + b.reshape(-1), (w * ok).reshape(-1))
+    tot.index_add_(0, ns, w.reshape(-1))
+    tot.index_add_(0, nd, w.reshape(-1))
+    pmf = hist.view(n_nodes, num_bins) / (tot[:, None] + 1e-10)          # :177
+    cdf = torch.cumsum(pmf, 1)
+    sobel = torch.tensor([-1.0, 0.0, 1.0]) / (2.0 * bw)                  # :59-60
+    pdf = _reflect_conv(_reflect_conv(cdf, sobel), cdf_smooth_kernel(bw, gradient_smooth))
+    bl = ((res - min_val) / bw + 0.5).long()                              # :207-210 lookup bin
+    valid = (bl >= 0) & (bl < num_bins) & (w > 0)
+    bl = bl.clamp(0, num_bins - 1)
+    gs = node_src.long()[:, None] * num_bins + bl
+    gd = node_dst.long()[:, None] * num_bins + bl
+    fc, fp = cdf.reshape(-1), pdf.reshape(-1)
+    cs, cd = fc[gs], fc[gd]
+    two = torch.full_like(cs, 2.0)
+    return (torch.where(valid, cs, two), torch.where(valid, fp[gs] * w, torch.zeros_like(cs)),
+            torch.where(valid, cd, two), torch.where(valid, fp[gd] * w, torch.zeros_like(cs)))
+
+
+def _cdf_straight_through(res: Tensor, w: Tensor, *cdf_args) -> Tuple[Tensor, Tensor]:
+    """CDFLossTorchWrapper (cdf_loss.py:6-16): value = CDF lookup, d/dres = pdf * w."""
+    cs, gs, cd, gd = cdf_loss_values(res.detach(), w, *cdf_args)
+    return cs + (res - res.detach()) * gs, cd + (res - res.detach()) * gd
+
+
+def imc_loss(enc: Tensor, hw: Tuple[int, int], kp2k: Tensor, shared_focal: bool, src_idx: Tensor, dst_idx: Tensor,
+             src_coords: Tensor, dst_coords: Tensor, src_depth: Tensor, dst_depth: Tensor, node_src: Tensor,
+             node_dst: Tensor, n_nodes: int, min_val: float = 0.0, max_val: float = 15.0, num_bins: int = 250,
+             gradient_smooth: float = 0.05) -> Tensor:
+    """compute_loss (train_imc.py:141-246) for pose encodings enc [N, 9] (differentiable)."""
+    ext, intr = pose_encoding_to_extri_intri(enc[None], hw)
+    K = torch.bmm(kp2k, intr[0])                                           # :166 K' -> K
+    if shared_focal:                                                      # :169-174
+        K = K.mean(0, keepdim=True).repeat(K.shape[0], 1, 1)
+    pad = torch.tensor([0.0, 0.0, 0.0, 1.0])
+
+    def pad44(e):                                                         # geometry.py pad_poses
+        return torch.cat([e, pad.expand(e.shape[0], 1, 4)], 1)
+    Es, Ed = pad44(ext[0][src_idx.long()]), pad44(ext[0][dst_idx.long()])
+    rel = torch.bmm(Ed, torch.inverse(Es))                                # compute_relative_pose
+    Ks, Kd = K[src_idx.long()], K[dst_idx.long()]
+    h = torch.cat([src_coords, torch.ones_like(src_coords[..., :1])], -1)
+    X = torch.bmm(torch.inverse(Ks), h.transpose(1, 2)).transpose(1, 2) * src_depth[..., None]
+    Y = torch.bmm(rel, torch.cat([X, torch.ones_like(X[..., :1])], -1).transpose(1, 2)).transpose(1, 2)[..., :3]
+    p = torch.bmm(Kd, Y.transpose(1, 2)).transpose(1, 2)
+    pred = p[..., :2] / (p[..., 2:] + 1e-6)                               # from_homogeneous
+    pred2 = p[..., :2] / (dst_depth[..., None] + 1e-6)                    # approximation variant
+    w = torch.ones_like(src_depth)                                        # valid masks: all ones
+    args = (node_src, node_dst, n_nodes, min_val, max_val, num_bins, gradient_smooth)
+    total = 0.0
+    for pr in (pred, pred2):
+        res = torch.log1p(torch.norm(pr - dst_coords, dim=-1))            # :212-238
+        a, b = _cdf_straight_through(res, w, *args)
+        total = total + (a.mean() + b.mean()) / 2.0
+    return total / 2.0

@@ -68,6 +68,16 @@ class AttnBwdDesc(ctypes.Structure):
     ]
 
 
+class ImcLossDesc(ctypes.Structure):
+    _fields_ = [
+        ("enc", _vp), ("n_views", _i32), ("H", _i32), ("W", _i32), ("kp2k", _vp), ("shared_focal", _i32),
+        ("n_pairs", _i32), ("n_points", _i32), ("src_idx", _vp), ("dst_idx", _vp), ("src_coords", _vp),
+        ("dst_coords", _vp), ("src_depth", _vp), ("dst_depth", _vp), ("node_src", _vp), ("node_dst", _vp),
+        ("n_nodes", _i32), ("min_val", _f32), ("max_val", _f32), ("num_bins", _i32), ("smooth_w", _vp),
+        ("smooth_radius", _i32), ("grad_scale", _f32), ("loss", _vp), ("d_enc", _vp), ("workspace", _vp),
+    ]
+
+
 # name -> (restype, argtypes)
 _PROTOS = {
     "sr_last_error": (ctypes.c_char_p, []),
@@ -118,6 +128,8 @@ _PROTOS = {
     "sr_vec_fma_f32": (_i32, [_vp, _vp, _vp, _vp, _i32]),
     "sr_scatter_rows_f32": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32]),
     "sr_copy2d_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32]),
+    "sr_imc_loss_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32]),
+    "sr_imc_loss": (_i32, [_vp, ctypes.POINTER(ImcLossDesc)]),
     "sr_pose_act_bwd_f32": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32]),
 }
 EXPORTED = tuple(_PROTOS)

@@ -254,3 +254,24 @@ def test_padding_folded_tables_equal_canvas_tables():
                         for t in range(kf.shape[1]):  # the kernel runs all taps (zeros past n1)
                             b += float(img[r, min(x1 + t, extent - 1)]) * kf[o, t]
                         assert a == b and np.signbit(a) == np.signbit(b)
+
+
+@pytest.mark.parametrize("case", ["dummy", "shared", "multi"])
+def test_oracle_imc_loss_matches_reference(golden_dir, case):
+    """Oracle restatement of compute_loss + CDFLossIndexPytorch vs the reference modules
+    (tests/golden/make_golden_loss.py): loss and d loss / d pose encoding."""
+    import os
+
+    import numpy as np
+    from oracle import sfm_oracle as O
+    z = np.load(os.path.join(golden_dir, "g8_loss.npz"))
+    g = lambda k: torch.from_numpy(z[f"{case}/{k}"])  # noqa: E731
+    enc = g("enc").clone().requires_grad_(True)
+    n_nodes = int(max(g("nodes_src").max(), g("nodes_dst").max())) + 1
+    loss = O.imc_loss(enc, (518, 518), g("kp2k"), bool(z[f"{case}/shared"]), g("src_idx"), g("dst_idx"),
+                      g("src_coords"), g("dst_coords"), g("src_depth"), g("dst_depth"), g("nodes_src"),
+                      g("nodes_dst"), n_nodes)
+    loss.backward()
+    assert abs(float(loss) - float(z[f"{case}/out_loss"])) <= 1e-6 * abs(float(z[f"{case}/out_loss"]))
+    ref = g("out_grad")
+    assert float((enc.grad - ref).norm() / ref.norm()) < 1e-5
