@@ -52,6 +52,13 @@ class TrainGraph:
         self._tapes = {}
         self._sc = engine.BwdScratch()
         self.state: Optional[dict] = None
+        # grad_ready_hook(module): called once a module's parameter grads are final within the
+        # backward (data-parallel training starts that module's all-reduce right away)
+        self.grad_ready_hook = None
+
+    def _ready(self, module) -> None:
+        if self.grad_ready_hook is not None:
+            self.grad_ready_hook(module)
 
     # ------------------------------------------------------------------ parameter packs
     def invalidate(self) -> None:
@@ -338,6 +345,7 @@ class TrainGraph:
         if st is None:
             raise RuntimeError("backward() needs a training forward() first")
         d_raw = self._camera_backward(d_pose.reshape(-1, 9).float().contiguous())
+        self._ready(self.cam)
         self._aggregator_backward(d_raw)
         self.state = None
 
@@ -445,6 +453,8 @@ class TrainGraph:
                 ops.colsum(dkv_raw, gr.b_qkv[C:], accumulate=True)
             ops.layernorm_bwd(tg.x0, dxn_sub, pr.ln1_w, pr.eps, dx, rowmap=rowmap[l], rows=n_sub,
                               dw=gr.ln1_w, db=gr.ln1_b)
+            self._ready(br)
+            self._ready(bg)
             if l == agg.depth - 1:  # first half of the camera tokens = the frame block's output
                 ops.scatter_rows(dx, cam_rows, d_raw[:, :C], accumulate=True)
             ops.cast_bf16(dx, dxb)
@@ -453,6 +463,7 @@ class TrainGraph:
             _, fbwd = engine.frame_attend_train(pf, S, P)
             engine.block_bwd(pf, self._bwd_pack(bf_, BF16), engine.block_grads(bf_), self._tapes[("frame", l)], dx,
                              dxb, fbwd, runtime.qkv_params(pf, rope, pos_row_base=0, **posctx), self._sc, tag="frame")
+            self._ready(bf_)
         self._embed_backward(dx, dxb)
 
     def _embed_backward(self, dx: Tensor, dxb: Tensor) -> None:
@@ -487,6 +498,7 @@ class TrainGraph:
                 _, bwd = engine.frame_attend_train(pb, S, P)
                 engine.block_bwd(pb, self._bwd_pack(blk, BF16), engine.block_grads(blk), self._tapes[("dino", i)],
                                  dx, dxb, bwd, None, self._sc, tag="dino")
+                self._ready(blk)
             # cls + pos[0] (row 0), registers (rows 1..4), patches + pos[1:] (vision_transformer.py:242-259)
             ops.colsum(dx.as_strided((S, C), (P * C, 1)), dino.cls_token.grad.reshape(-1), accumulate=True)
             ops.colsum(dx.as_strided((S, C), (P * C, 1)), dino.pos_embed.grad[0, 0], accumulate=True)
@@ -513,6 +525,7 @@ class TrainGraph:
         ops.copy2d(conv.weight.grad.reshape(C, kk), wtmp[:, :kk], accumulate=True)
         if conv.bias is not None:
             ops.colsum(dpatch, conv.bias.grad, accumulate=True)
+        self._ready(None)  # every remaining parameter
 
 
 def _sl(t, a, b):
