@@ -31,14 +31,25 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
 
 __device__ __forceinline__ int swz(int r, int chunk) { return chunk ^ (((r >> 1) & 1) << 2); }
 
-// 64 rows x 64 bf16 of a row-major matrix (rows >= nrows clamped) into a swizzled LDS tile
-__device__ __forceinline__ void load_tile(char* lds, const bf16* base, int64_t ld, int row0, int nrows, int tid,
-                                          int nthreads) {
-  for (int e = tid; e < 512; e += nthreads) {
-    const int r = e >> 3, c = e & 7;
+// 64 rows x 64 bf16 tiles staged through registers (256 threads: 2 x 16 B each per tile): the
+// next tile's global loads are issued before the current tile's MFMAs and written to the other
+// LDS buffer after them, so one barrier per tile separates the two (rows >= nrows clamped).
+struct TileRegs {
+  uint4 v[2];
+};
+__device__ __forceinline__ void fetch_tile(TileRegs& t, const bf16* base, int64_t ld, int row0, int nrows, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i, r = e >> 3, c = e & 7;
     const int rr = min(row0 + r, nrows - 1);
-    const uint4 v = *(const uint4*)(base + (int64_t)rr * ld + c * 8);
-    *(uint4*)(lds + r * 128 + swz(r, c) * 16) = v;
+    t.v[i] = *(const uint4*)(base + (int64_t)rr * ld + c * 8);
+  }
+}
+__device__ __forceinline__ void store_tile(char* lds, const TileRegs& t, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i, r = e >> 3, c = e & 7;
+    *(uint4*)(lds + r * 128 + swz(r, c) * 16) = t.v[i];
   }
 }
 
@@ -97,11 +108,8 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 // grid (key tiles of 128, heads, SHARED ? 1 : batch); wave w owns keys tile*128 + 32 w + l32.
 template <int SEG>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
-  char* qt = smem;
-  char* ot = smem + TB;
-  float* lse_s = (float*)(smem + 2 * TB);
-  float* dl_s = lse_s + 64;
+  constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
   const sr_attn_desc& f = b.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
   const int head = blockIdx.y, hcol = head * 64;
@@ -126,21 +134,37 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
 #pragma unroll
   for (int i = 0; i < 16; ++i) dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f;
 
-  for (int item = it0; item < it1; ++item) {
-    const bf16* qb = (const bf16*)f.q + (int64_t)item * f.q_bstride * f.ldq + hcol;
-    const bf16* gb = (const bf16*)b.dout + (int64_t)item * f.q_bstride * b.lddo + hcol;
-    const float* lse = f.lse + ((int64_t)item * f.heads + head) * f.lq;
-    const float* dlt = b.delta + ((int64_t)item * f.heads + head) * f.lq;
-    for (int q0 = 0; q0 < f.lq; q0 += 64) {
-      __syncthreads();  // previous tile's reads done
-      load_tile(qt, qb, f.ldq, q0, f.lq, tid, 256);
-      load_tile(ot, gb, b.lddo, q0, f.lq, tid, 256);
+  // tiles t = (item - it0) * ntq + q-tile, staged through registers one tile ahead
+  const int ntq = (f.lq + 63) / 64, ntiles = (it1 - it0) * ntq;
+  TileRegs rq, ro;
+  float rl = 0.f, rd = 0.f;
+  auto fetch = [&](int t) {
+    const int item = it0 + t / ntq, q0 = (t % ntq) * 64;
+    fetch_tile(rq, (const bf16*)f.q + (int64_t)item * f.q_bstride * f.ldq + hcol, f.ldq, q0, f.lq, tid);
+    fetch_tile(ro, (const bf16*)b.dout + (int64_t)item * f.q_bstride * b.lddo + hcol, b.lddo, q0, f.lq, tid);
+    if (tid < 64) {
+      const bool ok = q0 + tid < f.lq;
+      const int64_t o = ((int64_t)item * f.heads + head) * f.lq + q0 + tid;
+      rl = ok ? f.lse[o] : INFINITY;  // padded rows: P = 0
+      rd = ok ? b.delta[o] : 0.f;
+    }
+  };
+  fetch(0);
+  for (int t = 0; t < ntiles; ++t) {
+    {
+      char* stg = smem + (t & 1) * STG;
+      char* qt = stg;
+      char* ot = stg + TB;
+      float* lse_s = (float*)(stg + 2 * TB);
+      float* dl_s = lse_s + 64;
+      store_tile(qt, rq, tid);
+      store_tile(ot, ro, tid);
       if (tid < 64) {
-        const bool ok = q0 + tid < f.lq;
-        lse_s[tid] = ok ? lse[q0 + tid] : INFINITY;  // padded rows: P = 0
-        dl_s[tid] = ok ? dlt[q0 + tid] : 0.f;
+        lse_s[tid] = rl;
+        dl_s[tid] = rd;
       }
-      __syncthreads();
+      __syncthreads();  // this stage written; every wave is past the previous use of this buffer
+      if (t + 1 < ntiles) fetch(t + 1);
       // S = Q K^T and dP = dO V^T for this wave's 32 keys (2 blocks of 32 query rows)
       f32x16 sc[2], dp[2];
       const f32x16 zero = {};
@@ -196,9 +220,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
 // ---------------------------------------------------------------- dQ
 // grid (query tiles of 128, heads, batch); wave w owns query rows tile*128 + 32 w + l32.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
-  char* kt = smem;
-  char* vt = smem + TB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TB];  // 2 stages of K tile | V tile
   const sr_attn_desc& f = b.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
   const int head = blockIdx.y, hcol = head * 64, item = blockIdx.z;
@@ -220,20 +242,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) dq[0][i] = dq[1][i] = 0.f;
-  for (int seg = 0; seg < 2; ++seg) {
-    const int len = seg ? f.l1 : f.l0;
-    if (len <= 0) continue;
-    const bf16* kp = (const bf16*)(seg ? f.k1 : f.k0) + (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride) *
-                                                          (seg ? f.ldk1 : f.ldk0) + hcol;
-    const bf16* vp = (const bf16*)(seg ? f.v1 : f.v0) + (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride) *
-                                                          (seg ? f.ldv1 : f.ldv0) + hcol;
-    const int64_t ldk = seg ? f.ldk1 : f.ldk0, ldv = seg ? f.ldv1 : f.ldv0;
-    for (int k0 = 0; k0 < len; k0 += 64) {
-      __syncthreads();
-      load_tile(kt, kp, ldk, k0, len, tid, 256);
-      load_tile(vt, vp, ldv, k0, len, tid, 256);
-      __syncthreads();
-      const int valid = len - k0;
+  // key tiles of both segments in order (segment 0 then 1), staged through registers one ahead
+  const int nt0 = (f.l0 + 63) / 64, nt1 = f.l1 > 0 ? (f.l1 + 63) / 64 : 0, ntiles = nt0 + nt1;
+  TileRegs rk, rv;
+  auto fetch = [&](int t) {
+    const int seg = t >= nt0, k0 = (seg ? t - nt0 : t) * 64, len = seg ? f.l1 : f.l0;
+    const int64_t row0 = (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride);
+    fetch_tile(rk, (const bf16*)(seg ? f.k1 : f.k0) + row0 * (seg ? f.ldk1 : f.ldk0) + hcol, seg ? f.ldk1 : f.ldk0,
+               k0, len, tid);
+    fetch_tile(rv, (const bf16*)(seg ? f.v1 : f.v0) + row0 * (seg ? f.ldv1 : f.ldv0) + hcol, seg ? f.ldv1 : f.ldv0,
+               k0, len, tid);
+  };
+  fetch(0);
+  for (int t = 0; t < ntiles; ++t) {
+    {
+      char* kt = smem + (t & 1) * 2 * TB;
+      char* vt = kt + TB;
+      store_tile(kt, rk, tid);
+      store_tile(vt, rv, tid);
+      __syncthreads();  // this stage written; every wave is past the previous use of this buffer
+      if (t + 1 < ntiles) fetch(t + 1);
+      const int seg = t >= nt0;
+      const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
       f32x16 sc[2], dp[2];
       const f32x16 zero = {};
 #pragma unroll

@@ -208,21 +208,33 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
   *(f32x4*)(part + (int64_t)blockIdx.y * N + c) = s;
 }
 
+// partial rows [chunks][N] -> out: workgroup = 16 column quads x 16 chunk groups; each thread sums
+// its chunks z = g, g + 16, ... in order, then a fixed LDS tree over the 16 groups (deterministic)
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
                                                            float* out, int accumulate, float scale) {
-  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (c >= N) return;
-  f32x4 s = *(const f32x4*)(part + c);
-  for (int z = 1; z < chunks; ++z) s += *(const f32x4*)(part + (int64_t)z * N + c);
-  f32x4* o = (f32x4*)(out + c);
-  *o = accumulate ? *o + s * scale : s * scale;
+  __shared__ f32x4 red[16][16];
+  const int qi = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t c = ((int64_t)blockIdx.x * 16 + qi) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < N)
+    for (int z = g; z < chunks; z += 16) s += *(const f32x4*)(part + (int64_t)z * N + c);
+  red[g][qi] = s;
+  __syncthreads();
+  for (int w = 8; w > 0; w >>= 1) {
+    if (g < w) red[g][qi] += red[g + w][qi];
+    __syncthreads();
+  }
+  if (g == 0 && c < N) {
+    f32x4* o = (f32x4*)(out + c);
+    *o = accumulate ? *o + red[0][qi] * scale : red[0][qi] * scale;
+  }
 }
 
 int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
                   float scale, float* ws) {
+  // ~1024 partial workgroups of >= 32 rows, then the parallel final reduction
   const int64_t gx = (N / 4 + 255) / 256;
-  int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((2048 + gx - 1) / gx, (M + 15) / 16));
-  chunks = std::min(chunks, 2048);
+  int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 31) / 32));
   const int rpc = (M + chunks - 1) / chunks;
   chunks = (M + rpc - 1) / rpc;
   if (dtype == SR_BF16)
@@ -231,7 +243,8 @@ int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, i
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((unsigned)gx, chunks), dim3(256), 0, s, (const float*)X, ldx,
                        M, N, rpc, ws);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)gx), dim3(256), 0, s, ws, chunks, N, out, accumulate, scale);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N / 4 + 15) / 16)), dim3(256), 0, s, ws, chunks, N, out,
+                     accumulate, scale);
   return sr::check_launch("sr_colsum");
 }
 

@@ -178,6 +178,51 @@ def io():
     print(f"io Pillow on 1 host core: rgb {(t1 - t0) / 8 * 1e3:.2f} ms/view  depth {(t2 - t1) / 4 * 1e3:.2f} ms/view")
 
 
+def train():
+    """BASELINE config 4 (train_imc.py step, 16-view batches): full-size SailRecon aggregator +
+    camera head (DPT heads off: no loss reaches them), seeded synthetic weights, a synthetic
+    16-view IMC-shaped batch (15 chained pairs x 1024 correspondences, per-frame CDF nodes), bf16
+    aggregator / fp32 heads, fwd + loss + bwd + Adam per step."""
+    from sailrecon_amd.models.sail_recon import SailRecon
+    from sailrecon_amd.train.data import synthetic_batch
+    from sailrecon_amd.train.loss import CDFLossIndexPytorch
+    from sailrecon_amd.train.step import Trainer, prepare_model_input
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    n = int(os.environ.get("SR_TRAIN_VIEWS", "16"))
+    steps = int(os.environ.get("SR_TRAIN_STEPS", "3"))
+    t0 = time.perf_counter()
+    m = SailRecon(enable_point=False, enable_depth=False)
+    m.load_state_dict(synth_state_dict_like(m), strict=False)
+    m = m.to(DEV)
+    print(f"train: model built in {time.perf_counter() - t0:.1f} s", flush=True)
+    b = synthetic_batch(n, n_points=1024, size=518, seed=0)
+    cdf = CDFLossIndexPytorch(0.0, 15.0, 250, b["src_idx"], b["dst_idx"], gradient_smooth=0.05, num_nodes=n)
+    tr = Trainer(m, max_lr=2e-4, warmup_steps=2000, max_steps=100_000, cdf=cdf)
+    imgs, na, nq = prepare_model_input(b["rgb_processed"].to(DEV))
+    ops.TIMER = ops.KernelTimer()
+    out = tr.step(imgs, na, nq, b)  # warmup (allocates tapes / packs)
+    torch.cuda.synchronize()
+    print(f"train: warmup step loss {out['loss']:.5f}  peak HBM {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB",
+          flush=True)
+    ops.TIMER = ops.KernelTimer()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(steps):
+        out = tr.step(imgs, na, nq, b)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / steps
+    summ = ops.TIMER.summary()
+    ops.TIMER = None
+    tot = 0.0
+    for tag, r in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
+        tot += r["total_ms"] / steps
+        print(f"  {tag:22s} {r['total_ms'] / steps:9.2f} ms/step  {r['launches'] // steps:5d} launches  "
+              f"{r['tflops']:7.1f} TF/s")
+    print(f"train: {n} views ({2 * n} frames @518) {ms:.1f} ms/step = {n / ms * 1e3:.2f} views/s "
+          f"({1e3 / ms:.3f} steps/s); timed kernels {tot:.1f} ms; loss {out['loss']:.5f}", flush=True)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["attn", "gemm", "ln"]
     for w in which:
