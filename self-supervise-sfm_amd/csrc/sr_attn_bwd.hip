@@ -16,8 +16,9 @@
 // from ds_read_b64_tr_b16 reads exactly as the forward reads V^T, and the P / dS operands straight
 // from the accumulators: a 32x32 accumulator holds in lane (l32, hi) the column l32 and rows
 // (r & 3) + 8 (r >> 2) + 4 hi, r = 0..15, which is the k order the tr-reads produce.
-// Tiles are 64 rows x 128 B, 16-B chunk c of row r stored at c ^ (((r >> 1) & 1) << 2).
+// Tiles are 64 rows x 128 B (swizzle: see swz below).
 #include <cfloat>
+#include <type_traits>
 
 #include "sr_common.h"
 
@@ -29,28 +30,34 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ int swz(int r, int chunk) { return chunk ^ (((r >> 1) & 1) << 2); }
+// Tiles are read both as rows (ds_read_b128 for S / dP: 16 lanes = 16 rows, one chunk) and
+// transposed (ds_read_b64_tr_b16 for dV / dK / dQ: 4 rows x 4 chunks per 32 lanes).  16-B chunk c
+// of row r sits at c ^ f((r >> 1) & 7) with f(g) = b0 b1 b2 reversed: bijective on g (the 8 rows of
+// one parity in a b128 lane group hit 8 distinct chunks) and rows r, r + 2 of a transposed read
+// land in opposite 4-chunk halves — bank-conflict free for both (the forward's
+// c ^ ((r >> 1) & 1) << 2 only serves the transposed reads: 4-way conflicts on the row reads).
+__device__ __forceinline__ int swz(int r, int chunk) {
+  const int g = (r >> 1) & 7;
+  return chunk ^ (((g & 1) << 2) | (g & 2) | (g >> 2));
+}
 
 // 64 rows x 64 bf16 tiles staged through registers (256 threads: 2 x 16 B each per tile): the
 // next tile's global loads are issued before the current tile's MFMAs and written to the other
 // LDS buffer after them, so one barrier per tile separates the two (rows >= nrows clamped).
-struct TileRegs {
-  uint4 v[2];
+struct TileRegs {  // named members (an array member here was demoted to scratch)
+  uint4 a, b;
 };
-__device__ __forceinline__ void fetch_tile(TileRegs& t, const bf16* base, int64_t ld, int row0, int nrows, int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int e = tid + 256 * i, r = e >> 3, c = e & 7;
-    const int rr = min(row0 + r, nrows - 1);
-    t.v[i] = *(const uint4*)(base + (int64_t)rr * ld + c * 8);
-  }
+__device__ __forceinline__ TileRegs fetch_tile(const bf16* base, int64_t ld, int row0, int nrows, int tid) {
+  const int r = tid >> 3, c = tid & 7;  // rows r and r + 32
+  TileRegs t;
+  t.a = *(const uint4*)(base + (int64_t)min(row0 + r, nrows - 1) * ld + c * 8);
+  t.b = *(const uint4*)(base + (int64_t)min(row0 + r + 32, nrows - 1) * ld + c * 8);
+  return t;
 }
 __device__ __forceinline__ void store_tile(char* lds, const TileRegs& t, int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int e = tid + 256 * i, r = e >> 3, c = e & 7;
-    *(uint4*)(lds + r * 128 + swz(r, c) * 16) = t.v[i];
-  }
+  const int r = tid >> 3, c = tid & 7;
+  *(uint4*)(lds + r * 128 + swz(r, c) * 16) = t.a;
+  *(uint4*)(lds + (r + 32) * 128 + swz(r + 32, c) * 16) = t.b;
 }
 
 // A/B fragment from a row read: row r, k-step s (d = 16 s + 8 hi)
@@ -59,23 +66,27 @@ __device__ __forceinline__ bf16x8 row_frag(const char* tile, int r, int s, int h
 }
 
 struct TrOff {
-  int off[2];  // column block db = 0 / 1
+  int off[2][2];  // [column block db = 0 / 1][rows +0 / +8]
 };
 __device__ __forceinline__ TrOff tr_offsets(int lane) {
   const int hi = lane >> 5, G = lane >> 4, gi = lane & 15;
   const int vrow_in = gi >> 2;
   const int vcol_in = 16 * (G & 1) + 4 * (gi & 3);
-  const int vsw = ((vrow_in >> 1) & 1) << 2;
   TrOff t;
-  t.off[0] = (4 * hi + vrow_in) * 128 + (((vcol_in >> 3) ^ vsw) * 16) + (vcol_in & 7) * 2;
-  t.off[1] = (4 * hi + vrow_in) * 128 + (((4 + (vcol_in >> 3)) ^ vsw) * 16) + (vcol_in & 7) * 2;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 8 * h + 4 * hi + vrow_in;  // row0 is a multiple of 16: the swizzle repeats
+      t.off[db][h] = r * 128 + swz(r, 4 * db + (vcol_in >> 3)) * 16 + (vcol_in & 7) * 2;
+    }
   return t;
 }
 // transposed operand: m = tile column (db block), k = tile rows row0 + {(r & 3) + 8 (r >> 2) + 4 hi}
-__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int row0, int off) {
-  const char* pa = tile + row0 * 128 + off;
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int row0, const int (&off)[2]) {
+  const char* pt = tile + row0 * 128;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pt + off[0]));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pt + off[1]));
   const bf16x4 a4 = __builtin_bit_cast(bf16x4, a), b4 = __builtin_bit_cast(bf16x4, b);
   return bf16x8{a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
 }
@@ -140,8 +151,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
   float rl = 0.f, rd = 0.f;
   auto fetch = [&](int t) {
     const int item = it0 + t / ntq, q0 = (t % ntq) * 64;
-    fetch_tile(rq, (const bf16*)f.q + (int64_t)item * f.q_bstride * f.ldq + hcol, f.ldq, q0, f.lq, tid);
-    fetch_tile(ro, (const bf16*)b.dout + (int64_t)item * f.q_bstride * b.lddo + hcol, b.lddo, q0, f.lq, tid);
+    rq = fetch_tile((const bf16*)f.q + (int64_t)item * f.q_bstride * f.ldq + hcol, f.ldq, q0, f.lq, tid);
+    ro = fetch_tile((const bf16*)b.dout + (int64_t)item * f.q_bstride * b.lddo + hcol, b.lddo, q0, f.lq, tid);
     if (tid < 64) {
       const bool ok = q0 + tid < f.lq;
       const int64_t o = ((int64_t)item * f.heads + head) * f.lq + q0 + tid;
@@ -168,16 +179,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
       // S = Q K^T and dP = dO V^T for this wave's 32 keys (2 blocks of 32 query rows)
       f32x16 sc[2], dp[2];
       const f32x16 zero = {};
+      sc[0] = sc[1] = dp[0] = dp[1] = zero;
 #pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2) {
-        sc[qb2] = zero;
-        dp[qb2] = zero;
+      for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int qb2 = 0; qb2 < 2; ++qb2) {
           sc[qb2] = mfma32(row_frag(qt, qb2 * 32 + l32, s, hi), kf[s], sc[qb2]);
           dp[qb2] = mfma32(row_frag(ot, qb2 * 32 + l32, s, hi), vf[s], dp[qb2]);
         }
-      }
       // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
 #pragma unroll
       for (int qb2 = 0; qb2 < 2; ++qb2)
@@ -248,10 +257,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
   auto fetch = [&](int t) {
     const int seg = t >= nt0, k0 = (seg ? t - nt0 : t) * 64, len = seg ? f.l1 : f.l0;
     const int64_t row0 = (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride);
-    fetch_tile(rk, (const bf16*)(seg ? f.k1 : f.k0) + row0 * (seg ? f.ldk1 : f.ldk0) + hcol, seg ? f.ldk1 : f.ldk0,
-               k0, len, tid);
-    fetch_tile(rv, (const bf16*)(seg ? f.v1 : f.v0) + row0 * (seg ? f.ldv1 : f.ldv0) + hcol, seg ? f.ldv1 : f.ldv0,
-               k0, len, tid);
+    rk = fetch_tile((const bf16*)(seg ? f.k1 : f.k0) + row0 * (seg ? f.ldk1 : f.ldk0) + hcol, seg ? f.ldk1 : f.ldk0,
+                    k0, len, tid);
+    rv = fetch_tile((const bf16*)(seg ? f.v1 : f.v0) + row0 * (seg ? f.ldv1 : f.ldv0) + hcol, seg ? f.ldv1 : f.ldv0,
+                    k0, len, tid);
   };
   fetch(0);
   for (int t = 0; t < ntiles; ++t) {
@@ -266,32 +275,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
       const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
       f32x16 sc[2], dp[2];
       const f32x16 zero = {};
+      sc[0] = sc[1] = dp[0] = dp[1] = zero;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        sc[kb] = zero;
-        dp[kb] = zero;
+      for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int kb = 0; kb < 2; ++kb) {
           sc[kb] = mfma32(row_frag(kt, kb * 32 + l32, s, hi), qf[s], sc[kb]);  // S^T = K (cQ)^T
           dp[kb] = mfma32(row_frag(vt, kb * 32 + l32, s, hi), of[s], dp[kb]);  // dP^T = V dO^T
         }
-      }
+      auto ds_tile = [&](auto masked) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 df;
+          for (int s2 = 0; s2 < 2; ++s2) {
+            bf16x8 df;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int r = 8 * s2 + j;
-            const int kk = kb * 32 + acc_row(r, hi);
-            const float p = kk < valid ? __builtin_amdgcn_exp2f(sc[kb][r] - lse) : 0.f;
-            df[j] = (bf16)(p * (dp[kb][r] - dlt));
+            for (int j = 0; j < 8; ++j) {
+              const int r = 8 * s2 + j;
+              float p = __builtin_amdgcn_exp2f(sc[kb][r] - lse);
+              if constexpr (decltype(masked)::value) p = kb * 32 + acc_row(r, hi) < valid ? p : 0.f;
+              df[j] = (bf16)(p * (dp[kb][r] - dlt));
+            }
+            const int row0 = kb * 32 + 16 * s2;
+#pragma unroll
+            for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
           }
-          const int row0 = kb * 32 + 16 * s2;
-#pragma unroll
-          for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
-        }
+      };
+      if (valid >= 64) ds_tile(std::false_type{});  // full key tile: no per-element mask (uniform branch)
+      else ds_tile(std::true_type{});
     }
   }
   if (qrow < f.lq) {

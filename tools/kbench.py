@@ -178,6 +178,28 @@ def io():
     print(f"io Pillow on 1 host core: rgb {(t1 - t0) / 8 * 1e3:.2f} ms/view  depth {(t2 - t1) / 4 * 1e3:.2f} ms/view")
 
 
+def attn_bwd():
+    """Attention backward at the training shapes (C4: 16 anchors -> global L = 21984; frames)."""
+    C, H, D, P = 1024, 16, 64, 1374
+    for name, rows, batch, lq in (("global L=21984", 16 * P, 1, 16 * P), ("frame 32x1374", 32 * P, 32, P)):
+        qkv = torch.randn(rows, 3 * C, device=DEV, dtype=torch.bfloat16)
+        o = torch.empty(rows, C, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(batch, H, lq, device=DEV)
+        kb = 0 if batch == 1 else lq
+        ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=batch, lq=lq,
+                      q_bstride=lq, l0=lq, k0_bstride=kb, lse=lse)
+        g = torch.randn(rows, C, device=DEV, dtype=torch.bfloat16)
+        d = torch.empty(rows, 3 * C, device=DEV)
+        delta = torch.empty(batch * H * lq, device=DEV)
+
+        def f():
+            ops.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, lse, g, d[:, :C], d[:, C:2 * C],
+                              d[:, 2 * C:], delta, heads=H, batch=batch, lq=lq, q_bstride=lq, l0=lq, k0_bstride=kb)
+        ms = timeit(f, reps=3 if batch == 1 else 5, warm=1)
+        fl = 10.0 * batch * H * lq * lq * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
+        print(f"attn_bwd {name:16s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+
+
 def train():
     """BASELINE config 4 (train_imc.py step, 16-view batches): full-size SailRecon aggregator +
     camera head (DPT heads off: no loss reaches them), seeded synthetic weights, a synthetic
