@@ -22,6 +22,7 @@ Layout (SURVEY §7 design stance):
 from __future__ import annotations
 
 import logging
+import os
 from typing import Dict, List, Optional, Tuple, Union
 
 import numpy as np
@@ -484,6 +485,11 @@ class Aggregator(nn.Module):
                          tag="gemm")
             self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
             work_kv = torch.distributed.all_gather_into_tensor(kv_all, kv_loc, group=group, async_op=True)
+        # G == 1: the reloc block (query rows) and the global block (anchor rows) are independent.
+        # SR_CONCURRENT_STACKS=1 runs the reloc block on a side stream so that each could fill the
+        # other's last partial wave; measured 3% SLOWER at N=32 (68.7 -> 66.7 views/s: the two
+        # streams' kernels interfere more than the tails cost), so it is off by default.
+        side = self._side_stream(dev) if (G == 1 and Nq_l > 0 and a0 < q0) else None
         if Nq_l > 0:
             def attend_reloc(qkv, o):
                 if work_sub is not None:
@@ -491,8 +497,14 @@ class Aggregator(nn.Module):
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub * G, k0_bstride=0,
                               k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
-            runtime.run_block(pr, x, q0, q1, sc, attend_reloc, runtime.qkv_params(pr, rope, pos_row_base=q0,
-                                                                                    **posctx))
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
+                with torch.cuda.stream(side):
+                    runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
+                                      runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
+            else:
+                runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
+                                  runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
         if G > 1:
             work_kv.wait()
             o = sc.o[a0:q0]
@@ -507,6 +519,18 @@ class Aggregator(nn.Module):
                               tag="attn_global")
             runtime.run_block(pg, x, a0, q0, sc, attend_global, runtime.qkv_params(pg, rope, pos_row_base=a0,
                                                                                     **posctx))
+        if side is not None:
+            torch.cuda.current_stream(dev).wait_stream(side)  # join before the next frame block
+
+    def _side_stream(self, dev):
+        """Second HIP stream for the concurrent reloc block (opt-in: SR_CONCURRENT_STACKS=1)."""
+        if os.environ.get("SR_CONCURRENT_STACKS", "0") != "1":
+            return None
+        s = getattr(self, "_side", None)
+        if s is None or s.device != torch.device(dev):
+            s = torch.cuda.Stream(device=dev)
+            self._side = s
+        return s
 
     def _kv_gemm(self, pb, xn, out, rope, pos):
         """K/V-only projection (qkv weight rows C..3C) with k-norm + RoPE on the K half."""
