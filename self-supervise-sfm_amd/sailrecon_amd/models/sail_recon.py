@@ -50,7 +50,14 @@ class SailRecon(nn.Module):
         _, G, r = self.aggregator._world()
         nq_l = len(reloc_list) // G
         local_reloc = list(reloc_list)[r * nq_l:(r + 1) * nq_l]
-        reloc_rgbs = rgbs[:, local_reloc]
+        # a list index is a blocking host->device copy of the index: it made the host wait for the
+        # whole aggregator before enqueueing the heads.  Contiguous query frames (the demo's
+        # reloc_list = range(N, 2N)) are a slice; others go through a pinned async index copy.
+        if local_reloc and local_reloc == list(range(local_reloc[0], local_reloc[0] + len(local_reloc))):
+            reloc_rgbs = rgbs[:, local_reloc[0]:local_reloc[0] + len(local_reloc)]
+        else:
+            idx = torch.tensor(local_reloc, dtype=torch.long).pin_memory().to(rgbs.device, non_blocking=True)
+            reloc_rgbs = rgbs.index_select(1, idx)
         cam_tokens = rgb_feats[-1][:, :, 0]
         predictions = {}
         with torch.autocast("cuda", enabled=False):  # heads in fp32, sail_recon.py:118-119
