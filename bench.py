@@ -52,12 +52,17 @@ KERNEL_OF_TAG = {
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, views: int, img: int):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), or None."""
+    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), or None.  The passes were run on
+    one workload (the file's ``workload``, default N=32 @518); other sizes get None."""
     try:
         with open(TRAFFIC_FILE) as f:
-            k = json.load(f)["kernels"].get(kernel)
+            d = json.load(f)
+        wl = d.get("workload", {"views": 32, "img": 518})
+        if (wl.get("views"), wl.get("img")) != (views, img):
+            return None
+        k = d["kernels"].get(kernel)
     except (OSError, ValueError, KeyError):
         return None
     return None if k is None else k["traffic_bytes"]
@@ -177,7 +182,7 @@ def main():
         b = breakdown[dom]
         achieved = b["tflops"]
         kern = KERNEL_OF_TAG.get(dom) if use_bf16 else None
-        traffic = pmc_traffic(kern) if kern else None
+        traffic = pmc_traffic(kern, n, args.img) if kern else None
         roofline = {"bound": "mfma", "kernel": kern or dom, "timer_class": dom, "achieved": round(achieved, 2),
                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                     "traffic": None if traffic is None else round(traffic),
