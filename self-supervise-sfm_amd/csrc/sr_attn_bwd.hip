@@ -41,23 +41,20 @@ __device__ __forceinline__ int swz(int r, int chunk) {
   return chunk ^ (((g & 1) << 2) | (g & 2) | (g >> 2));
 }
 
-// 64 rows x 64 bf16 tiles staged through registers (256 threads: 2 x 16 B each per tile): the
-// next tile's global loads are issued before the current tile's MFMAs and written to the other
-// LDS buffer after them, so one barrier per tile separates the two (rows >= nrows clamped).
-struct TileRegs {  // named members (an array member here was demoted to scratch)
-  uint4 a, b;
-};
-__device__ __forceinline__ TileRegs fetch_tile(const bf16* base, int64_t ld, int row0, int nrows, int tid) {
-  const int r = tid >> 3, c = tid & 7;  // rows r and r + 32
-  TileRegs t;
-  t.a = *(const uint4*)(base + (int64_t)min(row0 + r, nrows - 1) * ld + c * 8);
-  t.b = *(const uint4*)(base + (int64_t)min(row0 + r + 32, nrows - 1) * ld + c * 8);
-  return t;
+// Tiles reach LDS by LDS-DMA through a ring of NBUF stages (tiles t+1, t+2 in flight while tile
+// t is consumed; t+3 is issued right after the tile's barrier).  A workgroup stages a 64-row tile
+// with 8 dwordx4 wave-instructions: instruction g copies rows 8g .. 8g+7, lane l row 8g + l/8 into
+// LDS chunk l & 7, so the lane fetches source chunk swz(r, l & 7) (swz is an involution per row)
+// and LDS holds the swizzled image.
+constexpr int NBUF = 4;
+__device__ __forceinline__ void dma_rows(const bf16* base, int64_t ld, int row0, int nrows, int g, int lane,
+                                         uint32_t lds_tile) {
+  const int r = 8 * g + (lane >> 3);
+  sr::dma16(base + (int64_t)min(row0 + r, nrows - 1) * ld + swz(r, lane & 7) * 8, lds_tile + g * 1024);
 }
-__device__ __forceinline__ void store_tile(char* lds, const TileRegs& t, int tid) {
-  const int r = tid >> 3, c = tid & 7;
-  *(uint4*)(lds + r * 128 + swz(r, c) * 16) = t.a;
-  *(uint4*)(lds + (r + 32) * 128 + swz(r + 32, c) * 16) = t.b;
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // A/B fragment from a row read: row r, k-step s (d = 16 s + 8 hi)
@@ -117,12 +114,17 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 
 // ---------------------------------------------------------------- dK, dV
 // grid (key tiles of 128, heads, SHARED ? 1 : batch); wave w owns keys tile*128 + 32 w + l32.
+// Q / dO tiles and their lse / delta stream through the LDS-DMA ring.  The resident K and V
+// fragments are negated (K also scaled by c) and the S / dP chains are seeded with +lse / +delta
+// straight from LDS, so the chains return -(c q.k - lse) and -(dO.v - delta): P = exp2(-S'),
+// dS = -P dP', the signs folding into the VALU source modifiers.
 template <int SEG>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
-  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
   const sr_attn_desc& f = b.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int head = blockIdx.y, hcol = head * 64;
   const bool shared = (SEG == 0 ? f.k0_bstride : f.k1_bstride) == 0;
   const int it0 = shared ? 0 : blockIdx.z, it1 = shared ? f.batch : blockIdx.z + 1;
@@ -133,82 +135,120 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
   const int64_t ldk = SEG == 0 ? f.ldk0 : f.ldk1, ldv = SEG == 0 ? f.ldv0 : f.ldv1;
   const int key = blockIdx.x * 128 + wave * 32 + l32;
   const int keyc = min(key, len - 1);
+  const float c = f.scale * 1.4426950408889634f;
+
+  // staging: wave w issues row groups g = 4 (w & 1) .. + 3 of the Q (waves 0, 1) or dO (2, 3)
+  // tile; waves 0 / 1 also copy the tile's 64 lse / delta values (one dword DMA each)
+  const int ntq = (f.lq + 63) / 64, ntiles = (it1 - it0) * ntq;
+  const uint32_t lds0 = sr::lds_addr(smem);
+  const bool stage_o = wave_u >= 2;
+  const bf16* const sbase = (const bf16*)(stage_o ? b.dout : f.q) + hcol;
+  const int64_t sld = stage_o ? b.lddo : f.ldq;
+  const float* const lsrc = wave_u == 0 ? f.lse : b.delta;
+  // tile t = (item - it0) * ntq + query tile; cursors instead of divisions (the compiler
+  // expands an integer division into ~15 VALU)
+  auto stage = [&](int t, int item, int q0) {
+    const uint32_t sb = lds0 + (t & (NBUF - 1)) * STG;
+    const bf16* tb = sbase + (int64_t)item * f.q_bstride * sld;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma_rows(tb, sld, q0, f.lq, 4 * (wave_u & 1) + i, lane, sb + (stage_o ? TB : 0));
+    if (wave_u < 2)
+      sr::dma4(lsrc + ((int64_t)item * f.heads + head) * f.lq + min(q0 + lane, f.lq - 1), sb + 2 * TB + wave_u * 256);
+  };
+  int s_item = it0, s_q = 0;  // next tile to stage
+  for (int i = 0; i < NBUF - 1 && i < ntiles; ++i) {
+    stage(i, s_item, s_q * 64);
+    if (++s_q == ntq) s_q = 0, ++s_item;
+  }
+
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     kf[s] = *(const bf16x8*)(kp + (kb0 + keyc) * ldk + hcol + 16 * s + 8 * hi);
     vf[s] = *(const bf16x8*)(vp + (kb0 + keyc) * ldv + hcol + 16 * s + 8 * hi);
   }
-  const float c = f.scale * 1.4426950408889634f;
+  // retire these loads (and the prologue stages) with a wait the compiler sees: its scoreboard
+  // would otherwise carry them into the loop, and a vmcnt wait there drains the ring
+  __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      kf[s][j] = (bf16)(-(float)kf[s][j] * c);
+      vf[s][j] = (bf16)(-(float)vf[s][j]);
+    }
   const TrOff tro = tr_offsets(lane);
   f32x16 dk[2], dv[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f;
 
-  // tiles t = (item - it0) * ntq + q-tile, staged through registers one tile ahead
-  const int ntq = (f.lq + 63) / 64, ntiles = (it1 - it0) * ntq;
-  TileRegs rq, ro;
-  float rl = 0.f, rd = 0.f;
-  auto fetch = [&](int t) {
-    const int item = it0 + t / ntq, q0 = (t % ntq) * 64;
-    rq = fetch_tile((const bf16*)f.q + (int64_t)item * f.q_bstride * f.ldq + hcol, f.ldq, q0, f.lq, tid);
-    ro = fetch_tile((const bf16*)b.dout + (int64_t)item * f.q_bstride * b.lddo + hcol, b.lddo, q0, f.lq, tid);
-    if (tid < 64) {
-      const bool ok = q0 + tid < f.lq;
-      const int64_t o = ((int64_t)item * f.heads + head) * f.lq + q0 + tid;
-      rl = ok ? f.lse[o] : INFINITY;  // padded rows: P = 0
-      rd = ok ? b.delta[o] : 0.f;
+  for (int t = 0, cq = 0; t < ntiles; ++t, cq = cq + 1 == ntq ? 0 : cq + 1) {
+    // tile t has landed (later stages stay in flight: 5 DMA wave-instructions per stage on
+    // waves 0-1, 4 on waves 2-3); every wave is done with tile t-1, whose buffer stage t+3 reuses
+    if (t + 2 < ntiles) {
+      if (wave_u < 2) wait_vm<10>();
+      else wait_vm<8>();
+    } else if (t + 1 < ntiles) {
+      if (wave_u < 2) wait_vm<5>();
+      else wait_vm<4>();
+    } else {
+      wait_vm<0>();
     }
-  };
-  fetch(0);
-  for (int t = 0; t < ntiles; ++t) {
-    {
-      char* stg = smem + (t & 1) * STG;
-      char* qt = stg;
-      char* ot = stg + TB;
-      float* lse_s = (float*)(stg + 2 * TB);
-      float* dl_s = lse_s + 64;
-      store_tile(qt, rq, tid);
-      store_tile(ot, ro, tid);
-      if (tid < 64) {
-        lse_s[tid] = rl;
-        dl_s[tid] = rd;
+    sr::barrier_raw();
+    if (t + NBUF - 1 < ntiles) {
+      stage(t + NBUF - 1, s_item, s_q * 64);
+      if (++s_q == ntq) s_q = 0, ++s_item;
+    }
+    const char* qt = smem + (t & (NBUF - 1)) * STG;
+    const char* ot = qt + TB;
+    const float* lse_s = (const float*)(qt + 2 * TB);
+    const float* dl_s = lse_s + 64;
+    // seeds in accumulator order: rows qb2*32 + acc_row(r), four consecutive per float4
+    f32x16 sc[2], dp[2];
+#pragma unroll
+    for (int qb2 = 0; qb2 < 2; ++qb2)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 l4 = *(const float4*)(lse_s + qb2 * 32 + 8 * g + 4 * hi);
+        const float4 d4 = *(const float4*)(dl_s + qb2 * 32 + 8 * g + 4 * hi);
+        sc[qb2][4 * g] = l4.x; sc[qb2][4 * g + 1] = l4.y; sc[qb2][4 * g + 2] = l4.z; sc[qb2][4 * g + 3] = l4.w;
+        dp[qb2][4 * g] = d4.x; dp[qb2][4 * g + 1] = d4.y; dp[qb2][4 * g + 2] = d4.z; dp[qb2][4 * g + 3] = d4.w;
       }
-      __syncthreads();  // this stage written; every wave is past the previous use of this buffer
-      if (t + 1 < ntiles) fetch(t + 1);
-      // S = Q K^T and dP = dO V^T for this wave's 32 keys (2 blocks of 32 query rows)
-      f32x16 sc[2], dp[2];
-      const f32x16 zero = {};
-      sc[0] = sc[1] = dp[0] = dp[1] = zero;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
+    for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
 #pragma unroll
-        for (int qb2 = 0; qb2 < 2; ++qb2) {
-          sc[qb2] = mfma32(row_frag(qt, qb2 * 32 + l32, s, hi), kf[s], sc[qb2]);
-          dp[qb2] = mfma32(row_frag(ot, qb2 * 32 + l32, s, hi), vf[s], dp[qb2]);
-        }
-      // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
+      for (int qb2 = 0; qb2 < 2; ++qb2) {
+        sc[qb2] = mfma32(row_frag(qt, qb2 * 32 + l32, s, hi), kf[s], sc[qb2]);
+        dp[qb2] = mfma32(row_frag(ot, qb2 * 32 + l32, s, hi), vf[s], dp[qb2]);
+      }
+    const int qv = f.lq - cq * 64;  // valid query rows of this tile
+    if (qv < 64) {  // ragged last tile (uniform branch): clamped duplicate rows get P = 0
 #pragma unroll
       for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 pf, df;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int r = 8 * s2 + j;
-            const int q = qb2 * 32 + acc_row(r, hi);
-            const float p = __builtin_amdgcn_exp2f(sc[qb2][r] * c - lse_s[q]);
-            pf[j] = (bf16)p;
-            df[j] = (bf16)(p * (dp[qb2][r] - dl_s[q]));
-          }
-          const int row0 = qb2 * 32 + 16 * s2;
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
-            dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
-          }
-        }
+        for (int r = 0; r < 16; ++r)
+          if (qb2 * 32 + acc_row(r, hi) >= qv) sc[qb2][r] = INFINITY;
     }
+    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
+#pragma unroll
+    for (int qb2 = 0; qb2 < 2; ++qb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf, df;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * s2 + j;
+          const float p = __builtin_amdgcn_exp2f(-sc[qb2][r]);
+          pf[j] = (bf16)p;
+          df[j] = (bf16)(-(p * dp[qb2][r]));
+        }
+        const int row0 = qb2 * 32 + 16 * s2;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
+          dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
+        }
+      }
   }
   // dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key l32, d = 32 db + acc_row(r))
   if (key < len) {
@@ -229,80 +269,103 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
 // ---------------------------------------------------------------- dQ
 // grid (query tiles of 128, heads, batch); wave w owns query rows tile*128 + 32 w + l32.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TB];  // 2 stages of K tile | V tile
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TB];  // ring of K tile | V tile stages
   const sr_attn_desc& f = b.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int head = blockIdx.y, hcol = head * 64, item = blockIdx.z;
   const int qrow = blockIdx.x * 128 + wave * 32 + l32;
   const int qrc = min(qrow, f.lq - 1);
   const int64_t qr = (int64_t)item * f.q_bstride + qrc;
   const float c = f.scale * 1.4426950408889634f;
+
+  // key tiles of both segments in order (segment 0 then 1) through the LDS-DMA ring: wave w
+  // issues row groups g = 4 (w & 1) .. + 3 of the K (waves 0, 1) or V (2, 3) tile.  Segment
+  // bases are selected once, outside the loop.
+  const int nt0 = (f.l0 + 63) / 64, nt1 = f.l1 > 0 ? (f.l1 + 63) / 64 : 0, ntiles = nt0 + nt1;
+  const uint32_t lds0 = sr::lds_addr(smem);
+  const bool stage_v = wave_u >= 2;
+  const bf16* const sb0 = (const bf16*)(stage_v ? f.v0 : f.k0) + (int64_t)item * f.k0_bstride * (stage_v ? f.ldv0 : f.ldk0) + hcol;
+  const bf16* const sb1 = f.l1 > 0 ? (const bf16*)(stage_v ? f.v1 : f.k1) + (int64_t)item * f.k1_bstride * (stage_v ? f.ldv1 : f.ldk1) + hcol
+                                   : sb0;
+  const int64_t sld0 = stage_v ? f.ldv0 : f.ldk0, sld1 = stage_v ? f.ldv1 : f.ldk1;
+  auto stage = [&](int t) {
+    const bool s1 = t >= nt0;
+    const uint32_t sb = lds0 + (t & (NBUF - 1)) * 2 * TB + (stage_v ? TB : 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dma_rows(s1 ? sb1 : sb0, s1 ? sld1 : sld0, (s1 ? t - nt0 : t) * 64, s1 ? f.l1 : f.l0, 4 * (wave_u & 1) + i,
+               lane, sb);
+  };
+  for (int i = 0; i < NBUF - 1 && i < ntiles; ++i) stage(i);
+
   bf16x8 qf[4], of[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     qf[s] = *(const bf16x8*)((const bf16*)f.q + qr * f.ldq + hcol + 16 * s + 8 * hi);
     of[s] = *(const bf16x8*)((const bf16*)b.dout + qr * b.lddo + hcol + 16 * s + 8 * hi);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * c);
   }
   const int64_t lrow = ((int64_t)item * f.heads + head) * f.lq + qrc;
   const float lse = f.lse[lrow], dlt = b.delta[lrow];
+  __builtin_amdgcn_s_waitcnt(0);  // retire these loads with a wait the compiler sees (see dK, dV)
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * c);
+  // the S / dP chains of every tile start from -lse / -delta (this lane's query row in every
+  // accumulator entry), so they return S' = c q.k - lse and dP' = dO.v - delta
+  f32x16 nl, nd;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    nl[i] = -lse;
+    nd[i] = -dlt;
+  }
   const TrOff tro = tr_offsets(lane);
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) dq[0][i] = dq[1][i] = 0.f;
-  // key tiles of both segments in order (segment 0 then 1), staged through registers one ahead
-  const int nt0 = (f.l0 + 63) / 64, nt1 = f.l1 > 0 ? (f.l1 + 63) / 64 : 0, ntiles = nt0 + nt1;
-  TileRegs rk, rv;
-  auto fetch = [&](int t) {
-    const int seg = t >= nt0, k0 = (seg ? t - nt0 : t) * 64, len = seg ? f.l1 : f.l0;
-    const int64_t row0 = (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride);
-    rk = fetch_tile((const bf16*)(seg ? f.k1 : f.k0) + row0 * (seg ? f.ldk1 : f.ldk0) + hcol, seg ? f.ldk1 : f.ldk0,
-                    k0, len, tid);
-    rv = fetch_tile((const bf16*)(seg ? f.v1 : f.v0) + row0 * (seg ? f.ldv1 : f.ldv0) + hcol, seg ? f.ldv1 : f.ldv0,
-                    k0, len, tid);
-  };
-  fetch(0);
   for (int t = 0; t < ntiles; ++t) {
     {
-      char* kt = smem + (t & 1) * 2 * TB;
-      char* vt = kt + TB;
-      store_tile(kt, rk, tid);
-      store_tile(vt, rv, tid);
-      __syncthreads();  // this stage written; every wave is past the previous use of this buffer
-      if (t + 1 < ntiles) fetch(t + 1);
+      if (t + 2 < ntiles) wait_vm<8>();  // tile t landed; t+1, t+2 stay in flight (4 per stage)
+      else if (t + 1 < ntiles) wait_vm<4>();
+      else wait_vm<0>();
+      sr::barrier_raw();  // every wave is done with tile t-1, whose buffer stage t+3 reuses
+      if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
+      const char* kt = smem + (t & (NBUF - 1)) * 2 * TB;
+      const char* vt = kt + TB;
       const int seg = t >= nt0;
       const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
       f32x16 sc[2], dp[2];
-      const f32x16 zero = {};
-      sc[0] = sc[1] = dp[0] = dp[1] = zero;
 #pragma unroll
       for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-          sc[kb] = mfma32(row_frag(kt, kb * 32 + l32, s, hi), qf[s], sc[kb]);  // S^T = K (cQ)^T
-          dp[kb] = mfma32(row_frag(vt, kb * 32 + l32, s, hi), of[s], dp[kb]);  // dP^T = V dO^T
+          sc[kb] = mfma32(row_frag(kt, kb * 32 + l32, s, hi), qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
+          dp[kb] = mfma32(row_frag(vt, kb * 32 + l32, s, hi), of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
         }
-      auto ds_tile = [&](auto masked) {
+      if (valid < 64) {  // partial key tile (uniform branch): keys >= valid get S' = -inf, P = 0
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            bf16x8 df;
+          for (int r = 0; r < 16; ++r)
+            if (kb * 32 + acc_row(r, hi) >= valid) sc[kb][r] = -INFINITY;
+      }
+      // one code path for every tile: a masked copy of the dS / dQ block made the compiler join
+      // two register assignments of dq with 64 v_mov per tile
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int r = 8 * s2 + j;
-              float p = __builtin_amdgcn_exp2f(sc[kb][r] - lse);
-              if constexpr (decltype(masked)::value) p = kb * 32 + acc_row(r, hi) < valid ? p : 0.f;
-              df[j] = (bf16)(p * (dp[kb][r] - dlt));
-            }
-            const int row0 = kb * 32 + 16 * s2;
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 df;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int r = 8 * s2 + j;
+            df[j] = (bf16)(__builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r]);
           }
-      };
-      if (valid >= 64) ds_tile(std::false_type{});  // full key tile: no per-element mask (uniform branch)
-      else ds_tile(std::true_type{});
+          const int row0 = kb * 32 + 16 * s2;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
+        }
     }
   }
   if (qrow < f.lq) {

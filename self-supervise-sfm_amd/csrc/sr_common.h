@@ -121,6 +121,11 @@ __device__ __forceinline__ void dma16(const void* gptr, uint32_t lds_base) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_base)
                : "memory", "m0");
 }
+// 4-byte variant: lane l copies one dword to LDS[lds_base + 4*l] (256 B per wave-instruction).
+__device__ __forceinline__ void dma4(const void* gptr, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(gptr), "s"(lds_base)
+               : "memory", "m0");
+}
 // Same with a wave-uniform 64-bit base (SGPR pair) + per-lane 32-bit byte offset: the
 // address arithmetic of a tile walk stays on the scalar unit.
 __device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, uint32_t lds_base) {
