@@ -151,6 +151,24 @@ typedef struct sr_attn_desc {
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 
+/* fp8 (OCP e4m3) quantisation with ONE power-of-two scale per tensor (BASELINE C5, "fp8 QKV";
+ * e4m3 Q/K/V with per-tensor scales):
+ *   e = ceil(log2(amax(|mul * src|) / 448))   (0 for an all-zero tensor)
+ *   dst = e4m3(mul * src * 2^-e),  so  mul * src ~= dst * 2^e.
+ * src bf16 [rows][cols] (ld elements), dst bytes [rows][cols] (ldd bytes); *exp_out <- e (device
+ * int, read by sr_attention_qk8); workspace: 1 float.  cols, ld, ldd multiples of 8. */
+int sr_quant_fp8(sr_stream_t stream, const void* src, int64_t ld, int rows, int cols, float mul, void* dst,
+                 int64_t ldd, float* workspace, int* exp_out);
+
+/* Attention (replaces the global block's F.scaled_dot_product_attention, attention.py:103-109) with
+ * the score product q.k^T in block-scaled fp8 (v_mfma_scale_f32_32x32x64_f8f6f4, 2x the bf16 MFMA
+ * rate): q8 = sr_quant_fp8(q, mul = d->scale * log2(e)) with exponent qk_exp[0], k8 =
+ * sr_quant_fp8(k, mul = 1) with exponent qk_exp[1] (device ints).  V, O, lse and all sizes come
+ * from d (d->q / d->ldq unused); one key segment, no mask, head_dim 64.  Softmax and P.V as
+ * sr_attention's bf16 path. */
+int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* d, const void* q8, int64_t ldq8, const void* k8,
+                     int64_t ldk8, const int* qk_exp);
+
 /* ------------------------------------------------------------------------
  * Attention backward (training step; the gradient of
  * F.scaled_dot_product_attention in Attention.forward, attention.py:103-109), bf16 inputs,

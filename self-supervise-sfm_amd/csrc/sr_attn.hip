@@ -21,6 +21,7 @@
 // attn_f32 (parity mode + camera trunk, head_dim 64 | 128): exact fp32 VALU kernel,
 //   K/V tiles broadcast from LDS, per-key online softmax.
 #include <cfloat>
+#include <algorithm>
 #include <cstdlib>
 
 #include "sr_common.h"
@@ -332,6 +333,267 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   }
 }
 
+// ------------------------------------------------------------------ fp8 Q.K^T (BASELINE C5)
+// attn_bf16_kernel<4, 2> with the score product in block-scaled fp8: Q8 (e4m3 of c*q, c = scale *
+// log2 e) and K8 (e4m3 of k) carry one power-of-two scale each, handed to
+// v_mfma_scale_f32_32x32x64_f8f6f4 as e8m0 exponents, so the instruction returns c*S directly
+// (one 32x32x64 MFMA per q-block and key block instead of four 32x32x16 bf16 ones).  The -m fold
+// stays a bf16 MFMA on the same accumulator (the C/D layout does not depend on the input type),
+// and P.V is the bf16 path unchanged.  Stage = K8 tile (64 keys x 64 B, chunk c of row r at
+// c ^ ((r >> 2) & 3): conflict-free b128 reads) | V tile (as attn_bf16_kernel).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+constexpr int K8_TILE_B = KT * 64;
+constexpr int STAGE8_B = K8_TILE_B + TILE_B;
+
+template <int KIND>
+__global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const uint8_t* __restrict__ q8, int64_t ldq8,
+                                                          const uint8_t* __restrict__ k8, int64_t ldk8,
+                                                          const int* __restrict__ qk_exp) {
+  constexpr int NW = 4, QB = 2, QROWS = NW * 32 * QB, NBUF = 4, DPW = 3;  // 12 DMA instructions per stage
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE8_B];
+  const sr_attn_desc& d = args.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
+  const int hcol = head * 64;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int ntiles = args.ntile0;
+  const uint32_t lds0 = sr::lds_addr(smem);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int len = d.l0;
+  const int64_t rbase = (int64_t)item * d.k0_bstride;
+  const char* const kbase = (const char*)k8 + hcol;
+  const char* const vbase = (const char*)d.v0 + 2 * hcol;
+  // K8 instruction g (0..3): rows 16g + lane/4, LDS chunk lane & 3; V instruction g (0..7): rows
+  // 8g + lane/8, LDS chunk lane & 7 (V swizzle chunk ^ (((r >> 1) & 1) << 2))
+  const int kc = (lane & 3) ^ ((lane >> 4) & 3);  // ((16g + lane/4) >> 2) & 3 = (lane >> 4) & 3
+  const int vc = (lane & 7) ^ (((lane >> 4) & 1) << 2);
+  auto stage = [&](int t) {
+    const uint32_t sb = lds0 + (t & (NBUF - 1)) * STAGE8_B;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int gi = wave_u * DPW + i;
+      if (gi < 4) {
+        const int key = min(t * KT + 16 * gi + (lane >> 2), len - 1);
+        sr::dma16(kbase + (rbase + key) * ldk8 + kc * 16, sb + gi * 1024);
+      } else {
+        const int g = gi - 4;
+        const int key = min(t * KT + 8 * g + (lane >> 3), len - 1);
+        sr::dma16(vbase + ((rbase + key) * d.ldv0 + vc * 8) * 2, sb + K8_TILE_B + g * 1024);
+      }
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) stage(i);
+
+  // Q8 fragments (B operand): lane holds Q8[row][32 hi .. 32 hi + 31]
+  const int qrow0 = qt * QROWS + wave * 32 * QB + l32;
+  i32x8 qf[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const int qr = min(qrow0 + 32 * b, d.lq - 1);
+    const int4* qp = (const int4*)(q8 + (item * d.q_bstride + qr) * ldq8 + hcol + 32 * hi);
+    const int4 a = qp[0], c2 = qp[1];
+    qf[b] = i32x8{a.x, a.y, a.z, a.w, c2.x, c2.y, c2.z, c2.w};
+  }
+  const int sq = 127 + qk_exp[0], sk = 127 + qk_exp[1];  // e8m0 scales: Q8 * 2^eq = c q, K8 * 2^ek = k
+  __builtin_amdgcn_s_waitcnt(0);
+
+  bf16x8 one_a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) one_a[j] = (bf16)((hi == 0 && j < 2) ? 1.f : 0.f);
+  float m_run[QB], l_run[QB];
+  bf16x8 m_b[QB];
+  f32x16 o[QB][2];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    m_run[b] = 0.f;
+    l_run[b] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m_b[b][j] = (bf16)0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[b][0][i] = o[b][1][i] = 0.f;
+  }
+  // K8 fragment of key block kb: row kb*32 + l32, chunks 2hi, 2hi+1 (swizzled)
+  const int ksw = (l32 >> 2) & 3;
+  const int koff0 = l32 * 64 + (((2 * hi) ^ ksw) * 16), koff1 = l32 * 64 + (((2 * hi + 1) ^ ksw) * 16);
+  const int G = lane >> 4, gi_ = lane & 15;
+  const int vrow_in = gi_ >> 2;
+  const int vcol_in = 16 * (G & 1) + 4 * (gi_ & 3);
+  const int vsw = ((vrow_in >> 1) & 1) << 2;
+  const int voff0 = (4 * hi + vrow_in) * 128 + (((vcol_in >> 3) ^ vsw) * 16) + (vcol_in & 7) * 2;
+  const int voff1 = (4 * hi + vrow_in) * 128 + (((4 + (vcol_in >> 3)) ^ vsw) * 16) + (vcol_in & 7) * 2;
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+    else if (t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sr::barrier_raw();
+    if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
+    const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE8_B;
+    const char* vt_lds = kt_lds + K8_TILE_B;
+
+    f32x16 sc[QB][2];
+    const f32x16 zero = {};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int4 a = *(const int4*)(kt_lds + kb * 2048 + koff0);
+      const int4 c2 = *(const int4*)(kt_lds + kb * 2048 + koff1);
+      const i32x8 kf = {a.x, a.y, a.z, a.w, c2.x, c2.y, c2.z, c2.w};
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        sc[b][kb] = mfma32(one_a, m_b[b], zero);
+        sc[b][kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf[b], sc[b][kb], 0, 0, 0, sk, 0, sq);
+      }
+    }
+    const int valid = len - t * KT;
+    if (valid < KT) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (key >= valid) sc[b][kb][r] = -INFINITY;
+          }
+    }
+    float mx[QB];
+    bool grow = t == 0;
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      float t8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        t8[i] = fmaxf(fmaxf(sc[b][0][i], sc[b][0][i + 8]), fmaxf(sc[b][1][i], sc[b][1][i + 8]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
+      mx[b] = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
+      grow |= mx[b] > RESCALE_LOG2;
+    }
+    if (__any(grow)) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        const float target = t == 0 ? mx[b] : m_run[b] + fmaxf(mx[b], 0.f);
+        const bf16 nhi = (bf16)target;
+        const bf16 nlo = (bf16)(target - (float)nhi);
+        const float m_new = (float)nhi + (float)nlo;
+        const float delta = m_new - m_run[b];
+        const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
+        l_run[b] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o[b][0][i] *= alpha;
+          o[b][1][i] *= alpha;
+          sc[b][0][i] -= delta;
+          sc[b][1][i] -= delta;
+        }
+        m_run[b] = m_new;
+        if (hi == 0) {
+          m_b[b][0] = -nhi;
+          m_b[b][1] = -nlo;
+        }
+      }
+    }
+    float ps[QB][2];
+#pragma unroll
+    for (int b = 0; b < QB; ++b) ps[b][0] = ps[b][1] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf[QB];
+#pragma unroll
+        for (int b = 0; b < QB; ++b)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
+            ps[b][j & 1] += p;
+            pf[b][j] = (bf16)p;
+          }
+        const int rowoff = (kb * 32 + 16 * s2) * 128;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const char* pa = vt_lds + rowoff + (db ? voff1 : voff0);
+          const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
+          const s16x4 vb =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
+          const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
+          const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
+#pragma unroll
+          for (int b = 0; b < QB; ++b) o[b][db] = mfma32(vf, pf[b], o[b][db]);
+        }
+      }
+#pragma unroll
+    for (int b = 0; b < QB; ++b) l_run[b] += ps[b][0] + ps[b][1];
+  }
+
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const float lsum = sum_x32(l_run[b]);
+    const float inv = 1.f / lsum;
+    const int qrow = qrow0 + 32 * b;
+    if (d.lse && hi == 0 && qrow < d.lq)
+      d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
+    if (qrow < d.lq) {
+      bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
+          *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
+        }
+    }
+  }
+}
+
+// fp8 quantisation with one power-of-two scale per tensor: pass 1 = amax (atomic max on the bit
+// pattern of non-negative floats), pass 2 = e = ceil(log2(amax |mul| / 448)), e4m3(mul x 2^-e).
+__global__ __launch_bounds__(256) void amax_bf16_kernel(const bf16* __restrict__ src, int64_t ld, int rows, int cols,
+                                                        unsigned* __restrict__ amax) {
+  const int cpr = cols / 8;
+  const int64_t n = (int64_t)rows * cpr;
+  float m = 0.f;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / cpr), c = (int)(e % cpr) * 8;
+    const bf16x8 v = *(const bf16x8*)(src + r * ld + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)v[j]));
+  }
+  m = sr::wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+}
+
+__device__ __forceinline__ int fp8_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  int e = (int)ceilf(log2f(amax / 448.f));
+  if (amax * exp2f((float)-e) > 448.f) ++e;  // log2f rounding
+  return e;
+}
+
+__global__ __launch_bounds__(256) void quant_fp8_kernel(const bf16* __restrict__ src, int64_t ld, int rows, int cols,
+                                                        float mul, const unsigned* __restrict__ amax,
+                                                        uint8_t* __restrict__ dst, int64_t ldd, int* exp_out) {
+  const int e = fp8_exp(__uint_as_float(*amax) * fabsf(mul));
+  const float f = mul * exp2f((float)-e);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *exp_out = e;
+  const int cpr = cols / 8;
+  const int64_t n = (int64_t)rows * cpr;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / cpr), c = (int)(i % cpr) * 8;
+    const bf16x8 v = *(const bf16x8*)(src + r * ld + c);
+    int lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[0] * f, (float)v[1] * f, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[2] * f, (float)v[3] * f, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[4] * f, (float)v[5] * f, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] * f, (float)v[7] * f, hi, true);
+    *(int2*)(dst + r * ldd + c) = make_int2(lo, hi);
+  }
+}
+
 // ------------------------------------------------------------------ f32 / VALU
 constexpr int F32_KT = 32;       // keys per LDS tile
 constexpr int F32_THREADS = 128;  // query rows per workgroup
@@ -464,4 +726,45 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     return SR_EUNSUPPORTED;
   }
   return sr::check_launch("sr_attention(f32)");
+}
+
+extern "C" int sr_quant_fp8(sr_stream_t stream, const void* src, int64_t ld, int rows, int cols, float mul, void* dst,
+                            int64_t ldd, float* workspace, int* exp_out) {
+  SR_CHECK(src && dst && workspace && exp_out && rows > 0 && cols > 0, SR_EINVAL, "sr_quant_fp8: bad arguments");
+  SR_CHECK(cols % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0, SR_EINVAL, "sr_quant_fp8: cols / ld / ldd must be multiples of 8");
+  hipStream_t s = (hipStream_t)stream;
+  SR_CHECK(hipMemsetAsync(workspace, 0, sizeof(float), s) == hipSuccess, SR_ELAUNCH, "sr_quant_fp8: memset");
+  const int64_t n = (int64_t)rows * (cols / 8);
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(amax_bf16_kernel, dim3(grid), dim3(256), 0, s, (const bf16*)src, ld, rows, cols,
+                     (unsigned*)workspace);
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid), dim3(256), 0, s, (const bf16*)src, ld, rows, cols, mul,
+                     (const unsigned*)workspace, (uint8_t*)dst, ldd, exp_out);
+  return sr::check_launch("sr_quant_fp8");
+}
+
+extern "C" int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* desc, const void* q8, int64_t ldq8,
+                                const void* k8, int64_t ldk8, const int* qk_exp) {
+  SR_CHECK(desc && q8 && k8 && qk_exp, SR_EINVAL, "sr_attention_qk8: null pointer");
+  const sr_attn_desc& d = *desc;
+  SR_CHECK(d.v0 && d.o && d.batch > 0 && d.heads > 0 && d.lq > 0 && d.l0 > 0, SR_EINVAL,
+           "sr_attention_qk8: bad v0/o/sizes");
+  SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED,
+           "sr_attention_qk8: head_dim 64, one key segment, no mask");
+  SR_CHECK(ldq8 % 16 == 0 && ldk8 % 16 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0, SR_EINVAL,
+           "sr_attention_qk8: leading dims (fp8 rows 16-B aligned, bf16 multiples of 8)");
+  AttnArgs a;
+  a.d = d;
+  a.ntile0 = (d.l0 + KT - 1) / KT;
+  a.ntile1 = 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
+  const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : 0;
+  if (kind == 2)
+    hipLaunchKernelGGL(attn_qk8_kernel<2>, grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8, (const uint8_t*)k8,
+                       ldk8, qk_exp);
+  else
+    hipLaunchKernelGGL(attn_qk8_kernel<0>, grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8, (const uint8_t*)k8,
+                       ldk8, qk_exp);
+  return sr::check_launch("sr_attention_qk8");
 }

@@ -54,6 +54,10 @@ class Aggregator(nn.Module):
         self.rope = RotaryPositionEmbedding2D(frequency=rope_freq) if rope_freq > 0 else None
         self.position_getter = PositionGetter() if self.rope is not None else None
         self.intermediate_layer_idx = intermediate_layer_idx
+        # BASELINE C5 "fp8 QKV": the global blocks' q.k^T in block-scaled e4m3 (ops.attention_qk8);
+        # opt-in (set_fp8_global or SR_FP8_GLOBAL=1), no reference output pins its precision
+        self.fp8_global = os.environ.get("SR_FP8_GLOBAL", "0") == "1"
+        self._fp8_ws = None
 
         def blocks(cache=False):
             return nn.ModuleList([block_fn(dim=embed_dim, num_heads=num_heads, mlp_ratio=mlp_ratio, qkv_bias=qkv_bias,
@@ -508,19 +512,30 @@ class Aggregator(nn.Module):
         if G > 1:
             work_kv.wait()
             o = sc.o[a0:q0]
-            ops.attention(sc.qkv[a0:q0, 0:C], kv_all[:, 0:C], kv_all[:, C:2 * C], o, heads=pg.heads,
-                          head_dim=pg.head_dim, batch=1, lq=La_l, q_bstride=0, l0=La, k0_bstride=0,
-                          tag="attn_global")
+            self._global_attention(sc.qkv[a0:q0, 0:C], kv_all[:, 0:C], kv_all[:, C:2 * C], o, pg, La_l, La)
             runtime.run_block_tail(pg, x, a0, q0, sc)
         else:
             def attend_global(qkv, o):
-                ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pg.heads,
-                              head_dim=pg.head_dim, batch=1, lq=La, q_bstride=0, l0=La, k0_bstride=0,
-                              tag="attn_global")
+                self._global_attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, pg, La, La)
             runtime.run_block(pg, x, a0, q0, sc, attend_global, runtime.qkv_params(pg, rope, pos_row_base=a0,
                                                                                     **posctx))
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)  # join before the next frame block
+
+    def set_fp8_global(self, enabled: bool = True):
+        """Global blocks' q.k^T in block-scaled fp8 (BASELINE C5); P.V and everything else bf16."""
+        self.fp8_global = bool(enabled)
+        return self
+
+    def _global_attention(self, q, k, v, o, pg, lq, lk):
+        if self.fp8_global and pg.head_dim == 64 and q.dtype == torch.bfloat16:
+            if self._fp8_ws is None:
+                self._fp8_ws = ops.Fp8Workspace()
+            ops.attention_qk8(q, k, v, o, heads=pg.heads, batch=1, lq=lq, q_bstride=0, l0=lk, k0_bstride=0,
+                              tag="attn_global", ws=self._fp8_ws)
+        else:
+            ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
+                          k0_bstride=0, tag="attn_global")
 
     def _side_stream(self, dev):
         """Second HIP stream for the concurrent reloc block (opt-in: SR_CONCURRENT_STACKS=1)."""

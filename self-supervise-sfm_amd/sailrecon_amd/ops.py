@@ -211,6 +211,63 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
         TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim, nb)
 
 
+def quant_fp8(src: Tensor, mul: float, dst: Optional[Tensor] = None, exp_out: Optional[Tensor] = None):
+    """e4m3 copy of ``mul * src`` (bf16 [rows, cols]) with one power-of-two scale (sr_quant_fp8):
+    returns (dst uint8 [rows, cols], exp int32 device scalar) with mul * src ~= dst * 2^exp."""
+    if src.dtype != torch.bfloat16 or src.dim() != 2:
+        raise ValueError("quant_fp8: src must be 2-D bf16")
+    rows, cols = src.shape
+    if dst is None:
+        dst = torch.empty(rows, cols, device=src.device, dtype=torch.uint8)
+    if exp_out is None:
+        exp_out = torch.empty(1, device=src.device, dtype=torch.int32)
+    ws = _train_ws(src.device, "fp8_amax", 1)
+    rc = _lib.load().sr_quant_fp8(_stream(src), _p(src), _rowmajor(src, "src"), rows, cols, float(mul), _p(dst),
+                                  _rowmajor(dst, "dst"), _p(ws), _p(exp_out))
+    check(rc, "sr_quant_fp8")
+    return dst, exp_out
+
+
+class Fp8Workspace:
+    """Reusable fp8 buffers of one attention shape (q8, k8 and their exponents)."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, rows_q: int, rows_k: int, cols: int, device) -> tuple:
+        key = (rows_q, rows_k, cols, str(device))
+        if key not in self.bufs:
+            self.bufs.clear()
+            self.bufs[key] = (torch.empty(rows_q, cols, device=device, dtype=torch.uint8),
+                              torch.empty(rows_k, cols, device=device, dtype=torch.uint8),
+                              torch.empty(2, device=device, dtype=torch.int32))
+        return self.bufs[key]
+
+
+def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, batch: int, lq: int, q_bstride: int,
+                  l0: int, k0_bstride: int, scale: Optional[float] = None, tag: Optional[str] = None,
+                  lse: Optional[Tensor] = None, ws: Optional[Fp8Workspace] = None) -> None:
+    """attention() with q.k^T in block-scaled fp8 (BASELINE C5): q and k (bf16, head_dim 64) are
+    quantised to e4m3 with one power-of-two scale each (q with scale*log2(e) folded in), V / P.V
+    stay bf16.  One key segment, no mask."""
+    head_dim = 64
+    d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
+                   k0_bstride=k0_bstride, scale=scale, lse=lse)
+    C = heads * head_dim
+    ws = ws or Fp8Workspace()
+    q8, k8, ex = ws.get(q.shape[0], k0.shape[0], C, q.device)
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    quant_fp8(q[:, :C], d.scale * 1.4426950408889634, q8, ex[0:1])
+    quant_fp8(k0[:, :C], 1.0, k8, ex[1:2])
+    rc = _lib.load().sr_attention_qk8(_stream(q), ctypes.byref(d), _p(q8), C, _p(k8), C, _p(ex))
+    check(rc, "sr_attention_qk8")
+    if timed:
+        kv_rows = l0 if k0_bstride == 0 else batch * l0
+        nb = heads * head_dim * (2 * batch * lq + kv_rows) + 2 * heads * head_dim * (batch * lq + kv_rows)
+        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * l0 * head_dim, nb)
+
+
 def _attn_desc(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
                k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, lse=None) -> AttnDesc:
     d = AttnDesc()

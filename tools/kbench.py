@@ -178,6 +178,24 @@ def io():
     print(f"io Pillow on 1 host core: rgb {(t1 - t0) / 8 * 1e3:.2f} ms/view  depth {(t2 - t1) / 4 * 1e3:.2f} ms/view")
 
 
+def attn_fp8():
+    """Global attention with q.k^T in block-scaled fp8 (BASELINE C5) vs the bf16 kernel, at the
+    C3 (L = 43,968) and C5 (L = 175,872) global lengths; the fp8 time includes both quantisations."""
+    C, H, D, P = 1024, 16, 64, 1374
+    for n in (32, 128):
+        L = n * P
+        qkv = torch.randn(L, 3 * C, device=DEV, dtype=torch.bfloat16)
+        o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+        ws = ops.Fp8Workspace()
+        fl = 4.0 * H * L * L * D
+        for name, f in (("bf16", lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
+                                                        batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0)),
+                        ("fp8 qk", lambda: ops.attention_qk8(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H,
+                                                           batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws))):
+            ms = timeit(f, reps=3 if n == 128 else 5, warm=1)
+            print(f"attn global L={L:6d} {name:7s} {ms:9.3f} ms  {fl / ms / 1e9:8.1f} TF/s", flush=True)
+
+
 def attn_bwd():
     """Attention backward at the training shapes (C4: 16 anchors -> global L = 21984; frames)."""
     C, H, D, P = 1024, 16, 64, 1374
