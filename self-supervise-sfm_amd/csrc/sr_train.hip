@@ -383,12 +383,26 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
       cs[0] = c4.x; cs[1] = c4.y; cs[2] = c4.z; cs[3] = c4.w;
       sn[0] = s4.x; sn[1] = s4.y; sn[2] = s4.z; sn[3] = s4.w;
     }
-    for (int c0 = 0; c0 < ncols; c0 += 256) {
-      // 4 heads per pass; a short last pass computes on clamped columns and stores nothing
+    // passes of 4 heads (256 columns) in groups of 4: every load of a group is issued before its
+    // math (16 heads of loads in flight per wave; one pass at a time left HBM latency exposed)
+    for (int cb = 0; cb < ncols; cb += 1024) {
+      float4 d4s[4];
+      bf16x4 r4s[4] = {};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        // a short last pass computes on clamped columns and stores nothing
+        const int col = min(cb + 256 * p + 4 * lane, ncols - 4);
+        d4s[p] = *(const float4*)(dsrc + (int64_t)row * lds + col);
+        if (norm && (col + ep.col_offset) / C < 2) r4s[p] = *(const bf16x4*)(raw + (int64_t)row * ldr + col);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+      const int c0 = cb + 256 * p;
+      if (c0 < ncols) {
       const bool live = c0 + 4 * lane < ncols;
       const int col = min(c0 + 4 * lane, ncols - 4);
       const int region = (col + ep.col_offset) / C;
-      const float4 d4 = *(const float4*)(dsrc + (int64_t)row * lds + col);
+      const float4 d4 = d4s[p];
       float d[4] = {d4.x, d4.y, d4.z, d4.w};
       if (region < 2) {
         if (rope) {  // inverse rotation: first a: da = c dA + s dB; second b: db = c dB - s dA
@@ -399,7 +413,7 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
           for (int e = 0; e < 4; ++e) d[e] = first ? fmaf(cs[e], d[e], sn[e] * pd[e]) : fmaf(cs[e], d[e], -sn[e] * pd[e]);
         }
         if (norm) {
-          const bf16x4 r4 = *(const bf16x4*)(raw + (int64_t)row * ldr + col);
+          const bf16x4 r4 = r4s[p];
           float v[4] = {(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
           float s = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
@@ -414,14 +428,22 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
 #pragma unroll
           for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
           const float rstd = rsqrtf(s2 * (1.f / 64.f) + ep.qk_eps);
-          const float* wv = region == 0 ? wq : wk;
+          float wv[4];  // selected per element: a pointer / index select here demoted the arrays to scratch
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wv[e] = region == 0 ? wq[e] : wk[e];
           float g[4], sg = 0.f, sgx = 0.f;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v[e] *= rstd;
             if (live) {
-              acc[2 * region][e] += d[e] * v[e];
-              acc[2 * region + 1][e] += d[e];
+              const float gw_ = d[e] * v[e];
+              if (region == 0) {
+                acc[0][e] += gw_;
+                acc[1][e] += d[e];
+              } else {
+                acc[2][e] += gw_;
+                acc[3][e] += d[e];
+              }
             }
             g[e] = d[e] * wv[e];
             sg += g[e];
@@ -439,6 +461,8 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
         }
       }
       if (live) *(bf16x4*)(out + (int64_t)row * ldo + col) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+      }
+      }
     }
   }
   if (norm) {  // lanes li, li+16, li+32, li+48 hold the same dims
