@@ -136,6 +136,7 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   // c = scale*log2(e) folded in so that the MFMA chain yields scores in the exp2 domain
   const float c = d.scale * 1.4426950408889634f;
   const int qrow0 = qt * QROWS + wave * 32 * QB + l32;  // q-block b: row qrow0 + 32b
+  const bool wave_active = qt * QROWS + wave_u * 32 * QB < d.lq;
   bf16x8 qf[QB][4];
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
@@ -203,6 +204,9 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
     const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
     const char* vt_lds = kt_lds + TILE_B;
+    // a wave whose rows all lie past lq (the ragged last q-tile: 1374 = 5 x 256 + 94 leaves two
+    // of its four waves empty) keeps staging and barriers but leaves its SIMD to the other waves
+    if (!wave_active) continue;
 
     // ---- S'^T = K (cQ)^T - m for every q-block (2 blocks of 32 keys each)
     f32x16 sc[QB][2];  // [q-block][key block]

@@ -51,6 +51,8 @@ for step in "$@"; do
     pmc_attn2) run pmc_attn2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_attn2 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
     kattnb)  run kattnb 300 python tools/kbench.py attn_bwd ;;
     ktrain)  run ktrain 900 python tools/kbench.py train ;;
+    prof_train) run prof_train 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- \
+               python3 tools/kbench.py train ;;
     pmc_bwd1) run pmc_bwd1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_bwd1 -o run --output-format csv -- python3 tools/kbench.py attn_bwd ;;
     pmc_bwd2) run pmc_bwd2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_bwd2 -o run --output-format csv -- python3 tools/kbench.py attn_bwd ;;
     *) echo "unknown step $step"; exit 2 ;;
