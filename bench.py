@@ -124,8 +124,9 @@ def main():
     ap.add_argument("--cpu-views", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--fp8-global", action="store_true",
-                    help="BASELINE C5: the global blocks' q.k^T in block-scaled fp8 e4m3 (P.V and the rest bf16)")
+    ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
+                    help="BASELINE C5: the global blocks' q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 "
+                         "e4m3; everything else bf16")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,9 +148,9 @@ def main():
     images = torch.cat([x, x])[None].to(device)  # demo_imc_forward.py:76-82
     no_reloc, reloc = list(range(n)), list(range(n, 2 * n))
     use_bf16 = args.dtype == "bf16"
-    fp8 = args.fp8_global and use_bf16
+    fp8 = args.fp8_global != "off" and use_bf16
     if fp8:
-        model.aggregator.set_fp8_global(True)
+        model.aggregator.set_fp8_global(True, fp8_v=args.fp8_global == "qkv")
 
     def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=use_bf16):
@@ -189,7 +190,10 @@ def main():
         kern = KERNEL_OF_TAG.get(dom) if use_bf16 else None
         if fp8 and dom == "attn_global":
             # half the attention flops (q.k^T) at the fp8 rate (2x bf16), half (P.V) at the bf16 rate
-            kern, peak = "attn_qk8_kernel<2>", 1.0 / (0.5 / (2 * PEAK_BF16_TFLOPS) + 0.5 / PEAK_BF16_TFLOPS)
+            if args.fp8_global == "qkv":  # every attention flop at the fp8 rate
+                kern, peak = "attn_qk8_kernel<2, true>", 2 * PEAK_BF16_TFLOPS
+            else:
+                kern, peak = "attn_qk8_kernel<2, false>", 1.0 / (0.5 / (2 * PEAK_BF16_TFLOPS) + 0.5 / PEAK_BF16_TFLOPS)
         traffic = pmc_traffic(kern, n, args.img) if kern and not fp8 else None
         roofline = {"bound": "mfma", "kernel": kern or dom, "timer_class": dom, "achieved": round(achieved, 2),
                     "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
@@ -225,7 +229,8 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
-            "dtype": "bf16, global q.k^T fp8-e4m3" if fp8 else args.dtype,
+            "dtype": (f"bf16, global {'q.k^T' if args.fp8_global == 'qk' else 'q.k^T + P.V'} fp8-e4m3" if fp8
+                      else args.dtype),
             "data": "synthetic (seeded U[0,1) images, seeded synthetic weights)",
             "config": {"workload": f"N={n} views @{args.img}px duplicated to {2 * n} frames (anchors+queries), "
                                    "fix_rank=300: Aggregator + CameraHead + pose decode",

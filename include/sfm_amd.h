@@ -169,6 +169,19 @@ int sr_quant_fp8(sr_stream_t stream, const void* src, int64_t ld, int rows, int 
 int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* d, const void* q8, int64_t ldq8, const void* k8,
                      int64_t ldk8, const int* qk_exp);
 
+/* V for an fp8 P.V: e4m3 with one power-of-two scale (exponent -> *exp_out, as sr_quant_fp8),
+ * transposed into per-(head, 64-key tile) 64 x 64-B tiles [heads][ceil(L/64)][64 d][64 key slots]
+ * whose key slots follow the S accumulator's row order (slot 32h + 16kb + r holds key
+ * 32kb + (r & 3) + 8 (r >> 2) + 4h), so P needs no lane movement.  v bf16 [L][heads*64];
+ * dst heads * ceil(L/64) * 4096 bytes; workspace 1 float. */
+int sr_quant_fp8_vt(sr_stream_t stream, const void* v, int64_t ldv, int L, int heads, void* dst, float* workspace,
+                    int* exp_out);
+
+/* sr_attention_qk8 with P.V in fp8 too (P in e4m3 unscaled, V from sr_quant_fp8_vt with exponent
+ * qkv_exp[2]); one item (the global block: d->batch == 1). */
+int sr_attention_qkv8(sr_stream_t stream, const sr_attn_desc* d, const void* q8, int64_t ldq8, const void* k8,
+                      int64_t ldk8, const void* v8t, const int* qkv_exp);
+
 /* ------------------------------------------------------------------------
  * Attention backward (training step; the gradient of
  * F.scaled_dot_product_attention in Attention.forward, attention.py:103-109), bf16 inputs,

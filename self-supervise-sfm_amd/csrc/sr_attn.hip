@@ -349,12 +349,18 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 constexpr int K8_TILE_B = KT * 64;
 constexpr int STAGE8_B = K8_TILE_B + TILE_B;
 
-template <int KIND>
+// V8: P.V in fp8 as well: V pre-transposed by sr_quant_fp8_vt into [head][key tile][d][64 B]
+// tiles whose 64 key slots follow the accumulator's row order (slot 32h + 16kb + r = key
+// 32kb + acc_row(r, h)), so P leaves the S accumulator straight as the B operand (32 fp8 per lane)
+// and one 32x32x64 MFMA per (q-block, d block) replaces four 32x32x16 bf16 ones.
+template <int KIND, bool V8>
 __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const uint8_t* __restrict__ q8, int64_t ldq8,
                                                           const uint8_t* __restrict__ k8, int64_t ldk8,
-                                                          const int* __restrict__ qk_exp) {
-  constexpr int NW = 4, QB = 2, QROWS = NW * 32 * QB, NBUF = 4, DPW = 3;  // 12 DMA instructions per stage
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE8_B];
+                                                          const uint8_t* __restrict__ v8t, const int* __restrict__ qk_exp) {
+  constexpr int NW = 4, QB = 2, QROWS = NW * 32 * QB, NBUF = 4;
+  constexpr int DPW = V8 ? 2 : 3;  // DMA instructions per wave per stage: 4 K8 + 4 V8T | 8 V
+  constexpr int STG = V8 ? 2 * K8_TILE_B : STAGE8_B;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
   const sr_attn_desc& d = args.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
@@ -372,13 +378,17 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
   const int kc = (lane & 3) ^ ((lane >> 4) & 3);  // ((16g + lane/4) >> 2) & 3 = (lane >> 4) & 3
   const int vc = (lane & 7) ^ (((lane >> 4) & 1) << 2);
   auto stage = [&](int t) {
-    const uint32_t sb = lds0 + (t & (NBUF - 1)) * STAGE8_B;
+    const uint32_t sb = lds0 + (t & (NBUF - 1)) * STG;
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
       const int gi = wave_u * DPW + i;
       if (gi < 4) {
         const int key = min(t * KT + 16 * gi + (lane >> 2), len - 1);
         sr::dma16(kbase + (rbase + key) * ldk8 + kc * 16, sb + gi * 1024);
+      } else if constexpr (V8) {  // V8T tile rows d = 16g + lane/4: same 64-B row swizzle as K8
+        const int g = gi - 4;
+        sr::dma16(v8t + ((int64_t)head * ntiles + t) * K8_TILE_B + (16 * g + (lane >> 2)) * 64 + kc * 16,
+                  sb + K8_TILE_B + g * 1024);
       } else {
         const int g = gi - 4;
         const int key = min(t * KT + 8 * g + (lane >> 3), len - 1);
@@ -401,6 +411,7 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
     qf[b] = i32x8{a.x, a.y, a.z, a.w, c2.x, c2.y, c2.z, c2.w};
   }
   const int sq = 127 + qk_exp[0], sk = 127 + qk_exp[1];  // e8m0 scales: Q8 * 2^eq = c q, K8 * 2^ek = k
+  const int sv = V8 ? 127 + qk_exp[2] : 127;
   __builtin_amdgcn_s_waitcnt(0);
 
   bf16x8 one_a;
@@ -434,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sr::barrier_raw();
     if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
-    const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE8_B;
+    const char* kt_lds = smem + (t & (NBUF - 1)) * STG;
     const char* vt_lds = kt_lds + K8_TILE_B;
 
     f32x16 sc[QB][2];
@@ -502,32 +513,59 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
     float ps[QB][2];
 #pragma unroll
     for (int b = 0; b < QB; ++b) ps[b][0] = ps[b][1] = 0.f;
+    if constexpr (V8) {
+      // P (e4m3, unscaled: P <= 2^RESCALE_LOG2 < 448) packed in accumulator order: byte 16kb + r
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int b = 0; b < QB; ++b) {
+        i32x8 p8;
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf[QB];
+        for (int w = 0; w < 8; ++w) {
+          const int kb = w >> 2, r = 4 * (w & 3);
+          float p4[4];
 #pragma unroll
-        for (int b = 0; b < QB; ++b)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
-            ps[b][j & 1] += p;
-            pf[b][j] = (bf16)p;
+          for (int e = 0; e < 4; ++e) {
+            p4[e] = __builtin_amdgcn_exp2f(sc[b][kb][r + e]);
+            ps[b][e & 1] += p4[e];
           }
-        const int rowoff = (kb * 32 + 16 * s2) * 128;
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(p4[0], p4[1], 0, false);
+          p8[w] = __builtin_amdgcn_cvt_pk_fp8_f32(p4[2], p4[3], pk, true);
+        }
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
-          const char* pa = vt_lds + rowoff + (db ? voff1 : voff0);
-          const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
-          const s16x4 vb =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
-          const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
-          const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
-#pragma unroll
-          for (int b = 0; b < QB; ++b) o[b][db] = mfma32(vf, pf[b], o[b][db]);
+          const int4 a = *(const int4*)(vt_lds + db * 2048 + koff0);
+          const int4 c2 = *(const int4*)(vt_lds + db * 2048 + koff1);
+          const i32x8 vf = {a.x, a.y, a.z, a.w, c2.x, c2.y, c2.z, c2.w};
+          o[b][db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, p8, o[b][db], 0, 0, 0, sv, 0, 127);
         }
       }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pf[QB];
+#pragma unroll
+          for (int b = 0; b < QB; ++b)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
+              ps[b][j & 1] += p;
+              pf[b][j] = (bf16)p;
+            }
+          const int rowoff = (kb * 32 + 16 * s2) * 128;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const char* pa = vt_lds + rowoff + (db ? voff1 : voff0);
+            const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
+            const s16x4 vb =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(pa + 8 * 128));
+            const bf16x4 a4 = __builtin_bit_cast(bf16x4, va), b4 = __builtin_bit_cast(bf16x4, vb);
+            const bf16x8 vf = {a4[0], a4[1], a4[2], a4[3], b4[0], b4[1], b4[2], b4[3]};
+#pragma unroll
+            for (int b = 0; b < QB; ++b) o[b][db] = mfma32(vf, pf[b], o[b][db]);
+          }
+        }
+    }
 #pragma unroll
     for (int b = 0; b < QB; ++b) l_run[b] += ps[b][0] + ps[b][1];
   }
@@ -596,6 +634,41 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(const bf16* __restrict__
     hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] * f, (float)v[7] * f, hi, true);
     *(int2*)(dst + r * ldd + c) = make_int2(lo, hi);
   }
+}
+
+// V -> V8T tiles for the fp8 P.V: tile t of head h = 64 rows d x 64 B, byte 32 hh + 16 kb + r of row d
+// holds e4m3(V[64 t + 32 kb + acc_row(r, hh)][d] * 2^-ev) (keys past L are zero).
+__global__ __launch_bounds__(256) void quant_fp8_vt_kernel(const bf16* __restrict__ v, int64_t ldv, int L, int ntiles,
+                                                           const unsigned* __restrict__ amax, uint8_t* __restrict__ dst,
+                                                           int* exp_out) {
+  __shared__ bf16 tile[KT][64 + 2];  // +2: the column reads below hit different banks
+  const int t = blockIdx.x, head = blockIdx.y, tid = threadIdx.x;
+  const int e = fp8_exp(__uint_as_float(*amax));
+  const float f = exp2f((float)-e);
+  if (t == 0 && head == 0 && tid == 0) *exp_out = e;
+  for (int i = tid; i < KT * 8; i += 256) {  // 64 keys x 8 chunks of 8 bf16
+    const int key = i >> 3, c = (i & 7) * 8, gk = t * KT + key;
+    bf16x8 x = {};
+    if (gk < L) x = *(const bf16x8*)(v + (int64_t)gk * ldv + head * 64 + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[key][c + j] = x[j];
+  }
+  __syncthreads();
+  const int d = tid >> 2, p0 = (tid & 3) * 16;  // 16 output bytes per thread
+  int w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float x4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = p0 + 4 * q + k, hh = p >> 5, kb = (p >> 4) & 1, r = p & 15;
+      const int key = 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      x4[k] = (float)tile[key][d] * f;
+    }
+    const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(x4[0], x4[1], 0, false);
+    w[q] = __builtin_amdgcn_cvt_pk_fp8_f32(x4[2], x4[3], lo, true);
+  }
+  *(int4*)(dst + (((int64_t)head * ntiles + t) * 64 + d) * 64 + p0) = make_int4(w[0], w[1], w[2], w[3]);
 }
 
 // ------------------------------------------------------------------ f32 / VALU
@@ -764,11 +837,46 @@ extern "C" int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* desc, co
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
   const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : 0;
+  const uint8_t* nov = nullptr;
   if (kind == 2)
-    hipLaunchKernelGGL(attn_qk8_kernel<2>, grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8, (const uint8_t*)k8,
-                       ldk8, qk_exp);
+    hipLaunchKernelGGL((attn_qk8_kernel<2, false>), grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8,
+                       (const uint8_t*)k8, ldk8, nov, qk_exp);
   else
-    hipLaunchKernelGGL(attn_qk8_kernel<0>, grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8, (const uint8_t*)k8,
-                       ldk8, qk_exp);
+    hipLaunchKernelGGL((attn_qk8_kernel<0, false>), grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8,
+                       (const uint8_t*)k8, ldk8, nov, qk_exp);
   return sr::check_launch("sr_attention_qk8");
+}
+
+extern "C" int sr_quant_fp8_vt(sr_stream_t stream, const void* v, int64_t ldv, int L, int heads, void* dst,
+                               float* workspace, int* exp_out) {
+  SR_CHECK(v && dst && workspace && exp_out && L > 0 && heads > 0, SR_EINVAL, "sr_quant_fp8_vt: bad arguments");
+  SR_CHECK(ldv % 8 == 0, SR_EINVAL, "sr_quant_fp8_vt: ldv must be a multiple of 8");
+  hipStream_t s = (hipStream_t)stream;
+  SR_CHECK(hipMemsetAsync(workspace, 0, sizeof(float), s) == hipSuccess, SR_ELAUNCH, "sr_quant_fp8_vt: memset");
+  const int64_t n = (int64_t)L * heads * 8;
+  hipLaunchKernelGGL(amax_bf16_kernel, dim3((int)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s,
+                     (const bf16*)v, ldv, L, heads * 64, (unsigned*)workspace);
+  const int ntiles = (L + KT - 1) / KT;
+  hipLaunchKernelGGL(quant_fp8_vt_kernel, dim3(ntiles, heads), dim3(256), 0, s, (const bf16*)v, ldv, L, ntiles,
+                     (const unsigned*)workspace, (uint8_t*)dst, exp_out);
+  return sr::check_launch("sr_quant_fp8_vt");
+}
+
+extern "C" int sr_attention_qkv8(sr_stream_t stream, const sr_attn_desc* desc, const void* q8, int64_t ldq8,
+                                 const void* k8, int64_t ldk8, const void* v8t, const int* qkv_exp) {
+  SR_CHECK(desc && q8 && k8 && v8t && qkv_exp, SR_EINVAL, "sr_attention_qkv8: null pointer");
+  const sr_attn_desc& d = *desc;
+  SR_CHECK(d.o && d.batch == 1 && d.heads > 0 && d.lq > 0 && d.l0 > 0, SR_EINVAL,
+           "sr_attention_qkv8: o / sizes (one item: the global block)");
+  SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED,
+           "sr_attention_qkv8: head_dim 64, one key segment, no mask");
+  SR_CHECK(ldq8 % 16 == 0 && ldk8 % 16 == 0 && d.ldo % 4 == 0, SR_EINVAL, "sr_attention_qkv8: leading dims");
+  AttnArgs a;
+  a.d = d;
+  a.ntile0 = (d.l0 + KT - 1) / KT;
+  a.ntile1 = 0;
+  dim3 grid((d.lq + 255) / 256, d.heads, 1);
+  hipLaunchKernelGGL((attn_qk8_kernel<2, true>), grid, dim3(256), 0, (hipStream_t)stream, a, (const uint8_t*)q8, ldq8,
+                     (const uint8_t*)k8, ldk8, (const uint8_t*)v8t, qkv_exp);
+  return sr::check_launch("sr_attention_qkv8");
 }

@@ -88,6 +88,8 @@ _PROTOS = {
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_quant_fp8": (_i32, [_vp, _vp, _i64, _i32, _i32, _f32, _vp, _i64, _vp, _vp]),
     "sr_attention_qk8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp]),
+    "sr_quant_fp8_vt": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
+    "sr_attention_qkv8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp, _vp]),
     "sr_attention_bwd": (_i32, [_vp, ctypes.POINTER(AttnBwdDesc)]),
     "sr_im2col3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "sr_convt_scatter_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),

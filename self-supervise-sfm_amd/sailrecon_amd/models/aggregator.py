@@ -56,7 +56,8 @@ class Aggregator(nn.Module):
         self.intermediate_layer_idx = intermediate_layer_idx
         # BASELINE C5 "fp8 QKV": the global blocks' q.k^T in block-scaled e4m3 (ops.attention_qk8);
         # opt-in (set_fp8_global or SR_FP8_GLOBAL=1), no reference output pins its precision
-        self.fp8_global = os.environ.get("SR_FP8_GLOBAL", "0") == "1"
+        self.fp8_global = os.environ.get("SR_FP8_GLOBAL", "0") in ("1", "qkv")
+        self.fp8_v = os.environ.get("SR_FP8_GLOBAL", "0") == "qkv"
         self._fp8_ws = None
 
         def blocks(cache=False):
@@ -522,9 +523,11 @@ class Aggregator(nn.Module):
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)  # join before the next frame block
 
-    def set_fp8_global(self, enabled: bool = True):
-        """Global blocks' q.k^T in block-scaled fp8 (BASELINE C5); P.V and everything else bf16."""
+    def set_fp8_global(self, enabled: bool = True, fp8_v: bool = False):
+        """Global blocks' q.k^T in block-scaled fp8 (BASELINE C5); with ``fp8_v`` also V and P.V.
+        Everything else stays bf16."""
         self.fp8_global = bool(enabled)
+        self.fp8_v = bool(enabled and fp8_v)
         return self
 
     def _global_attention(self, q, k, v, o, pg, lq, lk):
@@ -532,7 +535,7 @@ class Aggregator(nn.Module):
             if self._fp8_ws is None:
                 self._fp8_ws = ops.Fp8Workspace()
             ops.attention_qk8(q, k, v, o, heads=pg.heads, batch=1, lq=lq, q_bstride=0, l0=lk, k0_bstride=0,
-                              tag="attn_global", ws=self._fp8_ws)
+                              tag="attn_global", ws=self._fp8_ws, fp8_v=self.fp8_v)
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
                           k0_bstride=0, tag="attn_global")

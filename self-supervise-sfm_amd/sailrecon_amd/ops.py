@@ -229,7 +229,7 @@ def quant_fp8(src: Tensor, mul: float, dst: Optional[Tensor] = None, exp_out: Op
 
 
 class Fp8Workspace:
-    """Reusable fp8 buffers of one attention shape (q8, k8 and their exponents)."""
+    """Reusable fp8 buffers of one attention shape (q8, k8, the V8T tiles and the exponents)."""
 
     def __init__(self):
         self.bufs = {}
@@ -238,18 +238,33 @@ class Fp8Workspace:
         key = (rows_q, rows_k, cols, str(device))
         if key not in self.bufs:
             self.bufs.clear()
+            ntiles = (rows_k + 63) // 64
             self.bufs[key] = (torch.empty(rows_q, cols, device=device, dtype=torch.uint8),
                               torch.empty(rows_k, cols, device=device, dtype=torch.uint8),
-                              torch.empty(2, device=device, dtype=torch.int32))
-        return self.bufs[key]
+                              torch.empty(3, device=device, dtype=torch.int32),
+                              torch.empty(cols // 64 * ntiles * 4096, device=device, dtype=torch.uint8))
+        return self.bufs[key][:3]
+
+    def v8t(self):
+        return next(iter(self.bufs.values()))[3]
+
+
+def quant_fp8_vt(v: Tensor, heads: int, dst: Tensor, exp_out: Tensor) -> None:
+    """V (bf16 [L, heads*64]) -> e4m3 tiles in the accumulator key order of the fp8 P.V
+    (sr_quant_fp8_vt), exponent into exp_out."""
+    ws = _train_ws(v.device, "fp8_amax", 1)
+    rc = _lib.load().sr_quant_fp8_vt(_stream(v), _p(v), _rowmajor(v, "v"), v.shape[0], heads, _p(dst), _p(ws),
+                                     _p(exp_out))
+    check(rc, "sr_quant_fp8_vt")
 
 
 def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, batch: int, lq: int, q_bstride: int,
                   l0: int, k0_bstride: int, scale: Optional[float] = None, tag: Optional[str] = None,
-                  lse: Optional[Tensor] = None, ws: Optional[Fp8Workspace] = None) -> None:
+                  lse: Optional[Tensor] = None, ws: Optional[Fp8Workspace] = None, fp8_v: bool = False) -> None:
     """attention() with q.k^T in block-scaled fp8 (BASELINE C5): q and k (bf16, head_dim 64) are
-    quantised to e4m3 with one power-of-two scale each (q with scale*log2(e) folded in), V / P.V
-    stay bf16.  One key segment, no mask."""
+    quantised to e4m3 with one power-of-two scale each (q with scale*log2(e) folded in); V / P.V
+    stay bf16 unless ``fp8_v`` (then V is quantised too and P enters the MFMA as e4m3).  One key
+    segment, no mask."""
     head_dim = 64
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, scale=scale, lse=lse)
@@ -260,8 +275,16 @@ def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, b
     ev0 = TIMER.start() if timed else None
     quant_fp8(q[:, :C], d.scale * 1.4426950408889634, q8, ex[0:1])
     quant_fp8(k0[:, :C], 1.0, k8, ex[1:2])
-    rc = _lib.load().sr_attention_qk8(_stream(q), ctypes.byref(d), _p(q8), C, _p(k8), C, _p(ex))
-    check(rc, "sr_attention_qk8")
+    if fp8_v:
+        if batch != 1:
+            raise ValueError("attention_qk8(fp8_v=True): one item (the global block) only")
+        v8t = ws.v8t()
+        quant_fp8_vt(v0[:, :C], heads, v8t, ex[2:3])
+        rc = _lib.load().sr_attention_qkv8(_stream(q), ctypes.byref(d), _p(q8), C, _p(k8), C, _p(v8t), _p(ex))
+        check(rc, "sr_attention_qkv8")
+    else:
+        rc = _lib.load().sr_attention_qk8(_stream(q), ctypes.byref(d), _p(q8), C, _p(k8), C, _p(ex))
+        check(rc, "sr_attention_qk8")
     if timed:
         kv_rows = l0 if k0_bstride == 0 else batch * l0
         nb = heads * head_dim * (2 * batch * lq + kv_rows) + 2 * heads * head_dim * (batch * lq + kv_rows)

@@ -76,7 +76,7 @@ def test_attention_qk8(case):
     ops.attention(q, k, v, o16, heads=H, head_dim=D, **kw)
     torch.cuda.synchronize()
     q8, k8, ex = ws.get(B * L, B * L, C, q.device)
-    eq, ek = (int(t) for t in ex.tolist())
+    eq, ek = (int(t) for t in ex.tolist()[:2])
     c = scale * math.log2(math.e)
     qd = _deq(q8, eq) / c  # = q as the kernel saw it
     kd = _deq(k8, ek)
@@ -91,6 +91,39 @@ def test_attention_qk8(case):
         assert torch.allclose(lse8[b], torch.logsumexp(s, -1) / math.log(2), rtol=0, atol=2e-2)
     assert _rel(o8, o_ref) < 1e-2
     assert _rel(o8, o16) < 5e-2
+
+
+def test_attention_qkv8():
+    """q.k^T and P.V in fp8 (global block, one item): against fp32 attention on the dequantised
+    q8 / k8 and the e4m3-rounded V (P unrounded: 3e-2 rel-L2 for P's e4m3 rounding), and against
+    the bf16 kernel (6e-2)."""
+    from sailrecon_amd import ops
+    torch.manual_seed(2)
+    H, D = 4, 64
+    C = H * D
+    scale = D ** -0.5
+    for L in (1024, 700):
+        x = torch.randn(L, 3 * C, device=DEV).bfloat16()
+        q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+        kw = dict(batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0)
+        o8 = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+        ws = ops.Fp8Workspace()
+        ops.attention_qk8(q, k, v, o8, heads=H, ws=ws, fp8_v=True, **kw)
+        o16 = torch.empty_like(o8)
+        ops.attention(q, k, v, o16, heads=H, head_dim=D, **kw)
+        torch.cuda.synchronize()
+        q8, k8, ex = ws.get(L, L, C, q.device)
+        eq, ek, ev = (int(t) for t in ex.tolist())
+        amax = float(v.float().abs().max())
+        assert ev == math.ceil(math.log2(amax / 448.0)) or amax * 2.0 ** -(ev - 1) > 448.0
+        vd = (v.float() * 2.0 ** -ev).to(torch.float8_e4m3fn).float() * 2.0 ** ev
+        c = scale * math.log2(math.e)
+        qh = (_deq(q8, eq) / c).reshape(L, H, D).transpose(0, 1)
+        kh = _deq(k8, ek).reshape(L, H, D).transpose(0, 1)
+        vh = vd.reshape(L, H, D).transpose(0, 1)
+        o_ref = (torch.softmax(qh @ kh.transpose(-1, -2) * scale, -1) @ vh).transpose(0, 1).reshape(L, C)
+        assert _rel(o8, o_ref) < 3e-2, (L, _rel(o8, o_ref))
+        assert _rel(o8, o16) < 6e-2, (L, _rel(o8, o16))
 
 
 def test_aggregator_fp8_global_close_to_bf16():
@@ -111,12 +144,13 @@ def test_aggregator_fp8_global_close_to_bf16():
     m = m.to(DEV)
     x = torch.rand(1, 4, 3, 56, 56, generator=torch.Generator().manual_seed(1)).to(DEV)
     outs = []
-    for fp8 in (False, True):
-        m.aggregator.set_fp8_global(fp8)
+    for fp8, fp8_v in ((False, False), (True, False), (True, True)):
+        m.aggregator.set_fp8_global(fp8, fp8_v=fp8_v)
         m.aggregator.generator.manual_seed(0)
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
             feats, _, cam = m.aggregator(x, [0, 1], [2, 3], fix_rank=10)
         outs.append((feats[-1].float(), cam.float()))
     m.aggregator.set_fp8_global(False)
-    assert _rel(outs[1][0], outs[0][0]) < 5e-2
-    assert _rel(outs[1][1], outs[0][1]) < 5e-2
+    for i in (1, 2):
+        assert _rel(outs[i][0], outs[0][0]) < 5e-2
+        assert _rel(outs[i][1], outs[0][1]) < 5e-2

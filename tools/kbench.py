@@ -191,7 +191,10 @@ def attn_fp8():
         for name, f in (("bf16", lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
                                                         batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0)),
                         ("fp8 qk", lambda: ops.attention_qk8(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H,
-                                                           batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws))):
+                                                           batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws)),
+                        ("fp8 qkv", lambda: ops.attention_qk8(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H,
+                                                            batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws,
+                                                            fp8_v=True))):
             ms = timeit(f, reps=3 if n == 128 else 5, warm=1)
             print(f"attn global L={L:6d} {name:7s} {ms:9.3f} ms  {fl / ms / 1e9:8.1f} TF/s", flush=True)
 
