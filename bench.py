@@ -207,7 +207,8 @@ def main():
             flop = sum(v["flops_per_launch"] * v["launches"] for v in gems)
             ms = sum(v["total_ms"] for v in gems)
             roofline["gemm_all_tflops"] = round(flop / (ms * 1e-3) / 1e12, 1)
-            roofline["gemm_mfma_util"] = round(flop / (ms * 1e-3) / 1e12 / peak, 4)
+            gpeak = PEAK_BF16_TFLOPS if use_bf16 else PEAK_F32_TFLOPS  # GEMMs stay bf16 in the fp8 modes
+            roofline["gemm_mfma_util"] = round(flop / (ms * 1e-3) / 1e12 / gpeak, 4)
         print(json.dumps({"kernel_breakdown": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                                                    for kk, vv in v.items()} for k, v in breakdown.items()},
                           "step_ms": dt / args.steps * 1e3}), file=sys.stderr)
