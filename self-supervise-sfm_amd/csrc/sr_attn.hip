@@ -319,20 +319,42 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   for (int b = 0; b < QB; ++b) {
     const float lsum = sum_x32(l_run[b]);
     const float inv = 1.f / lsum;
+    const bool wide_o = d.ldo % 8 == 0 && ((uintptr_t)d.o & 15) == 0;
     const int qrow = qrow0 + 32 * b;
     if (d.lse && hi == 0 && qrow < d.lq)
       d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
     if (qrow < d.lq) {
       bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+      if (wide_o) {
+        // lane halves hold columns 8g..8g+3 (hi = 0) and 8g+4..8g+7 (hi = 1) of the row: one
+        // permlane32 swap per dword joins groups (2k, 2k+1) into 16 contiguous bytes per lane,
+        // so the store tail issues 4 dwordx4 instead of 8 dwordx2 per q-block
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+        for (int db = 0; db < 2; ++db)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
+          for (int k = 0; k < 2; ++k) {
+            bf16x4 va, vb;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
-          *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
-        }
+            for (int j = 0; j < 4; ++j) {
+              va[j] = (bf16)(o[b][db][8 * k + j] * inv);
+              vb[j] = (bf16)(o[b][db][8 * k + 4 + j] * inv);
+            }
+            const uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
+            const auto x = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+            const auto y = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+            *(uint4*)(op + db * 32 + 16 * k + 8 * hi) = make_uint4(x[0], y[0], x[1], y[1]);
+          }
+      } else {
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
+            *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
+          }
+      }
     }
   }
 }
@@ -574,20 +596,42 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
   for (int b = 0; b < QB; ++b) {
     const float lsum = sum_x32(l_run[b]);
     const float inv = 1.f / lsum;
+    const bool wide_o = d.ldo % 8 == 0 && ((uintptr_t)d.o & 15) == 0;
     const int qrow = qrow0 + 32 * b;
     if (d.lse && hi == 0 && qrow < d.lq)
       d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
     if (qrow < d.lq) {
       bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+      if (wide_o) {
+        // lane halves hold columns 8g..8g+3 (hi = 0) and 8g+4..8g+7 (hi = 1) of the row: one
+        // permlane32 swap per dword joins groups (2k, 2k+1) into 16 contiguous bytes per lane,
+        // so the store tail issues 4 dwordx4 instead of 8 dwordx2 per q-block
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+        for (int db = 0; db < 2; ++db)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
+          for (int k = 0; k < 2; ++k) {
+            bf16x4 va, vb;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
-          *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
-        }
+            for (int j = 0; j < 4; ++j) {
+              va[j] = (bf16)(o[b][db][8 * k + j] * inv);
+              vb[j] = (bf16)(o[b][db][8 * k + 4 + j] * inv);
+            }
+            const uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
+            const auto x = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+            const auto y = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+            *(uint4*)(op + db * 32 + 16 * k + 8 * hi) = make_uint4(x[0], y[0], x[1], y[1]);
+          }
+      } else {
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
+            *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
+          }
+      }
     }
   }
 }

@@ -474,8 +474,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
 //   * 512 threads = 8 waves as 2 (M) x 4 (N); per wave 128 x 64 outputs = 8 x 4 C^T tiles
 //     (128 accumulator VGPRs); one workgroup per CU (128 KiB LDS);
 //   * K-tile = 64 (128 B rows), 2 LDS stages of 64 KiB [A 256 rows | W 256 rows], XOR-swizzled;
-//   * ONE barrier per K-tile: after it, the whole next stage is issued by LDS-DMA (8 per wave)
-//     and lands while the 64 MFMAs of the current tile run;
+//   * ONE barrier per K-tile: after it, the next stage is issued by LDS-DMA (8 per wave, 4 ahead
+//     of each of the first two MFMA phases) and lands while the 64 MFMAs of the current tile run;
 //   * the tile is computed as 4 quadrant phases (64 rows x 32 cols, 16 MFMAs each) ordered so
 //     consecutive quadrants share A or B fragments (28 ds_read_b128 per 64 MFMAs);
 //   * s_setprio 1 around each MFMA cluster keeps the cluster intact (cdna_hip_programming.md T5).
@@ -536,9 +536,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #endif
 #ifdef SR_ABL_NODMA
     if (kt + 1 < g.ktiles && kt < 1) stage(kt + 1);     // tuning ablation: reuse the first 2 stages
-#else
-    if (kt + 1 < g.ktiles) stage(kt + 1);              // overwrites the buffer of kt-1
 #endif
+    const bool more = kt + 1 < g.ktiles;
+    // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
+    // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
+    // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
+    // measured no better)
+    auto dma_phase = [&](int ph) {
+#ifndef SR_ABL_NODMA
+      if (!more || ph >= 2) return;
+      const uint32_t base = dst0 + ((kt + 1) & 1) * STAGE_BIG;
+#pragma unroll
+      for (int i = 4 * ph; i < 4 * ph + 4; ++i) sr::dma16(src[i] + (int64_t)(kt + 1) * ROWB, base + i * 1024);
+#else
+      (void)ph;
+#endif
+    };
     const char* sb = smem + (kt & 1) * STAGE_BIG;
     // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
     // the current quadrant's MFMA cluster so their LDS latency hides under it
@@ -572,11 +585,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     load_a(aX, 0);
     load_b(bX, 0);
     load_b(bY, 1);
+    dma_phase(0);
     mma(aX, bX, 0, 0);
     load_a(aY, 1);
+    dma_phase(1);
     mma(aX, bY, 0, 1);
     load_b(bX, 0);
+    dma_phase(2);
     mma(aY, bY, 1, 1);
+    dma_phase(3);
     mma(aY, bX, 1, 0);
   }
 #ifdef SR_ABL_NOEPI
