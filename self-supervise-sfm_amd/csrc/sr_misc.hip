@@ -9,7 +9,9 @@ namespace {
 // ------------------------------------------------------------------ LayerNorm
 // One wave per row; each lane holds NPL = cols/64 values loaded as VEC-wide vectors
 // (coalesced: vector i of lane l covers columns (i*64 + l)*VEC .. +VEC).
-constexpr int ln_rows_per_wave(int npl) { return npl >= 32 ? 1 : 2; }  // register budget
+// rows in flight per wave (register budget): C = 1024 takes 4 (4.45 -> 5.2 TB/s over 2; 8 rows
+// fell back to 4.6)
+constexpr int ln_rows_per_wave(int npl) { return npl >= 32 ? 1 : (npl == 16 ? 4 : 2); }
 template <int NPL, int VEC, typename TO>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t ldx,
                                                         const int32_t* __restrict__ rowmap,
