@@ -294,6 +294,50 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
   }
 }
 
+// x += gamma * (acc + bias) for a full 256x256 tile (every row < M; N % 256 == 0 here), without
+// per-vector guards: the guarded form compiles to an exec branch per vector with a vmcnt(0)
+// before every store.  Here the loads of the next quarter of the wave's rows are in flight
+// while the current quarter is updated and stored (kbench proj +3.5 %, fc2 +1 %).  An LDS-staged
+// variant with 16 rows per wave in flight was 11 % slower, and staggering the first-round
+// workgroups by 1/4 or 1/2 tile (so epilogues do not coincide across CUs) changed nothing.
+__device__ __forceinline__ void resid_full(const GemmArgs& g, f32x4 (&acc)[8][4], int rowbase, int colw, int lr,
+                                           int lg) {
+  const sr_gemm_epi& ep = g.ep;
+  f32x4 gm[4], bs[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col = colw + ni * 16 + 4 * lg;
+    gm[ni] = *(const f32x4*)(ep.gamma + col);
+    bs[ni] = ep.bias ? *(const f32x4*)(ep.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float* xb = (float*)g.out + (int64_t)(rowbase + lr) * g.ldo + colw + 4 * lg;
+  const int64_t rs = 16 * g.ldo;
+  // quarters of 2 row blocks (8 float4 per lane); quarter q+1's loads are in flight while
+  // quarter q is added and stored
+  f32x4 xq[2][2][4];
+  auto load = [&](int q) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) xq[q & 1][i][ni] = *(const f32x4*)(xb + (2 * q + i) * rs + ni * 16);
+  };
+  load(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < 3) load(q + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        f32x4& xv = xq[q & 1][i][ni];
+        xv += (acc[2 * q + i][ni] + bs[ni]) * gm[ni];
+        *(f32x4*)(xb + (2 * q + i) * rs + ni * 16) = xv;
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // 256x256 bf16 epilogue staged through the (free) stage buffers so that global traffic is
 // whole rows with 16 B per lane (the register epilogue's per-lane 8-B stores touch 16 rows
 // per wave instruction).  bf16 outputs: the whole 256x256 tile (128 KiB, 512-B rows);
@@ -602,6 +646,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
 #else
+  if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    if (m0 + BIG <= g.M && !g.lds_epi) {
+      resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+      return;
+    }
+  }
   if (g.lds_epi) epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
   else epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
 #endif
