@@ -33,25 +33,21 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 __device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
 
 // erf-GELU for bf16 outputs: erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
-// the 2^-9 rounding of the bf16 result), 2 transcendentals + ~11 VALU instead of erff's ~35.
+// the 2^-9 rounding of the bf16 result), 2 transcendentals + ~9 VALU instead of erff's ~35.
 //   erf(|z|) = 1 - t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) exp(-z^2),  t = 1 / (1 + p |z|)
-//   gelu(x)  = x (1 + erf(x / sqrt2)) / 2 = x - x h  (x >= 0),  x h  (x < 0),  h = poly exp(-z^2) / 2
-// h(x) = (1 - erf(|x| / sqrt2)) / 2 = Phi(-|x|) by A&S 7.1.26
+//   gelu(x)  = x (1 + erf(x / sqrt2)) / 2 = max(x, 0) - |x| h,  h = poly exp(-z^2) / 2
+// h(x) = (1 - erf(|x| / sqrt2)) / 2 = Phi(-|x|) by A&S 7.1.26; 1/sqrt2 is folded into p and into
+// the exponent, the 1/2 into the (exactly halved) coefficients.
 __device__ __forceinline__ float phi_tail_fast(float x) {
-  const float az = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
-  float poly = fmaf(1.061405429f, t, -1.453152027f);
-  poly = fmaf(poly, t, 1.421413741f);
-  poly = fmaf(poly, t, -0.284496736f);
-  poly = fmaf(poly, t, 0.254829592f);
-  poly *= t;
-  const float e = __builtin_amdgcn_exp2f(az * az * -1.4426950408889634f);
-  return 0.5f * poly * e;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(x), 1.0f));
+  float poly = fmaf(0.5f * 1.061405429f, t, 0.5f * -1.453152027f);
+  poly = fmaf(poly, t, 0.5f * 1.421413741f);
+  poly = fmaf(poly, t, 0.5f * -0.284496736f);
+  poly = fmaf(poly, t, 0.5f * 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
+  return poly * t * e;
 }
-__device__ __forceinline__ float gelu_erf_fast(float x) {
-  const float h = phi_tail_fast(x);
-  return x >= 0.f ? fmaf(-x, h, x) : x * h;
-}
+__device__ __forceinline__ float gelu_erf_fast(float x) { return fmaf(-fabsf(x), phi_tail_fast(x), fmaxf(x, 0.f)); }
 
 // d/dx gelu_erf(x) = Phi(x) + x phi(x)  (backward of mlp.py:36's nn.GELU); `fast` uses the
 // A&S erf of gelu_erf_fast (bf16 gradients), otherwise erff (exact fp32).
