@@ -147,7 +147,15 @@ typedef struct sr_attn_desc {
   float scale;
   float* lse;  /* optional (bf16 path): [batch][heads][lq] row log-sum-exp of scale*log2(e)*q.k
                   (log2 domain), saved for sr_attention_bwd */
+  float* key_bound; /* optional scratch (bf16 path, >= sr_attention_bound_floats(d) floats, 4-B
+                  aligned): per key-segment instance and head, max |k| over the keys.  With it a
+                  query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^100 of its first
+                  tile's max runs the sweep with a FIXED softmax offset (no per-tile row max,
+                  no rescale; every P <= 2^50, no overflow, same precision); NULL = per-tile max */
 } sr_attn_desc;
+
+/* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */
+int sr_attention_bound_floats(const sr_attn_desc* d);
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 
@@ -381,6 +389,12 @@ int sr_set_special_tokens(sr_stream_t stream, float* x, int64_t ldx, int frames,
 /* dst[r] = src[rowmap ? rowmap[r] : r], fp32 rows (aggregator.py:403-423 intermediates) */
 int sr_copy_rows_f32(sr_stream_t stream, float* dst, int64_t ldd, const float* src, int64_t lds,
                      const int32_t* rowmap, int rows, int cols);
+
+/* out[r][c] = x[r][c] * gamma[c] (dtype in = out; gamma fp32): LayerScale.forward as a standalone
+ * module call (layer_scale.py:22-23).  Inside a Block the scale is fused into the residual GEMM
+ * epilogue (SR_EPI_BIAS_RESID). */
+int sr_mul_cols(sr_stream_t stream, int dtype, const void* x, int64_t ldx, const float* gamma, void* out, int64_t ldo,
+                int rows, int cols);
 
 /* out[M,N] = act_in(A)[M,K] . W[N,K]^T + bias, fp32, any shape (small camera-head
  * linears: embed_pose 9->C, pose_branch.fc2 C/2->9).  act_in: 0 none, 1 SiLU. */

@@ -31,6 +31,7 @@ namespace {
 struct AttnArgs {
   sr_attn_desc d;
   int ntile0, ntile1;  // key tiles per segment
+  int kb_n0;           // segment-0 instances in d.key_bound (1 if shared, else batch)
 };
 
 // ------------------------------------------------------------------ bf16 / MFMA
@@ -84,10 +85,12 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   // ---- staging: global DMA instruction gi = wave*DPW + i; gi < 8: K rows 8gi.., else V rows.
   // Segment pointers are copied to scalars once: selecting between kernel-argument fields
   // inside the loop compiles to vector loads whose vmcnt(0) wait would drain the ring.
-  // Full tiles use a scalar base per 8-row group + a per-lane 32-bit offset (all tile-walk
-  // arithmetic on the SALU); a segment's ragged last tile clamps rows per lane.
+  // Tiles are staged in order, so full tiles walk a running scalar pointer (one 64-bit add per
+  // tile plus one per DMA piece) with a per-lane 32-bit offset; a segment's ragged last tile
+  // clamps rows per lane.
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const bool stage_v = wave_u * DPW >= 8;  // wave-uniform: a wave stages only K or only V
+  const int grow0 = ((wave_u * DPW) & 7) * 8;  // first tile row of this wave's pieces
   const char* const sb0 = (const char*)(stage_v ? d.v0 : d.k0) + 2 * hcol;
   const char* const sb1 = (const char*)(stage_v ? d.v1 : d.k1) + 2 * hcol;
   const int64_t sld0 = stage_v ? d.ldv0 : d.ldk0, sld1 = stage_v ? d.ldv1 : d.ldk1;
@@ -102,23 +105,32 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   const int chB = stage_v ? chA : ((lane & 7) ^ (4 + (lane >> 4)));
   const uint32_t voA0 = (uint32_t)((lrow * sld0 + chA * 8) * 2), voB0 = (uint32_t)((lrow * sld0 + chB * 8) * 2);
   const uint32_t voA1 = (uint32_t)((lrow * sld1 + chA * 8) * 2), voB1 = (uint32_t)((lrow * sld1 + chB * 8) * 2);
-  auto stage = [&](int t) {
+  const char* sp = sb0 + (srb0 + grow0) * sld0 * 2;  // row grow0 of the next tile to stage
+  int64_t sstep = (int64_t)KT * sld0 * 2, s8 = 8 * sld0 * 2;
+  uint32_t sva = voA0, svb = voB0;
+  auto stage = [&](int t) {  // t = 0, 1, 2, ... in order
     const int buf = t & (NBUF - 1);
     const bool s1 = t >= nt0;
+    if (t == nt0) {  // first tile of segment 1
+      sp = sb1 + (srb1 + grow0) * sld1 * 2;
+      sstep = (int64_t)KT * sld1 * 2;
+      s8 = 8 * sld1 * 2;
+      sva = voA1;
+      svb = voB1;
+    }
     const int tt = s1 ? t - nt0 : t;
     const int len = s1 ? len1 : len0;
-    const char* base = s1 ? sb1 : sb0;
-    const int64_t ld = s1 ? sld1 : sld0;
-    const int64_t rbase = s1 ? srb1 : srb0;
     const uint32_t ldsb = lds0 + buf * STAGE_B + (stage_v ? TILE_B : 0);
     if ((tt + 1) * KT <= len) {
-      const uint32_t va = s1 ? voA1 : voA0, vb = s1 ? voB1 : voB0;
 #pragma unroll
       for (int i = 0; i < DPW; ++i) {
         const int gi = wave_u * DPW + i;
-        sr::dma16_s(base + (rbase + tt * KT + (gi & 7) * 8) * ld * 2, (gi & 1) ? vb : va, ldsb + (gi & 7) * 1024);
+        sr::dma16_s(sp + i * s8, (gi & 1) ? svb : sva, ldsb + (gi & 7) * 1024);
       }
     } else {
+      const char* base = s1 ? sb1 : sb0;
+      const int64_t ld = s1 ? sld1 : sld0;
+      const int64_t rbase = s1 ? srb1 : srb0;
 #pragma unroll
       for (int i = 0; i < DPW; ++i) {
         const int gi = wave_u * DPW + i;
@@ -127,6 +139,7 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
         sr::dma16(base + ((rbase + key) * ld + ((gi & 1) ? chB : chA) * 8) * 2, ldsb + (gi & 7) * 1024);
       }
     }
+    sp += sstep;
   };
 #pragma unroll
   for (int i = 0; i < NBUF - 1; ++i)
@@ -155,6 +168,32 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[b][s][j] = (bf16)((float)qf[b][s][j] * c);
+
+  // Fixed-offset sweep (d.key_bound set): qb = |cq| max|k| bounds every score of the row
+  // (Cauchy-Schwarz).  After tile 0 a wave whose rows all satisfy qb - max_tile0 <= 100 fixes
+  // m = max(max_tile0, qb - 50) for the whole sweep: every later S' = c q.k - m <= 50 (P <= 2^50,
+  // no overflow in fp32 / bf16) and the row's true max stays >= m - 50 (l >= 2^-50), so the
+  // per-tile row max, its lane exchange and the rescale test are skipped.  P keeps bf16's
+  // relative precision at any magnitude, O and l are fp32: the result equals the per-tile-max
+  // sweep's up to rounding.
+  float qb[QB];
+  const bool use_bound = d.key_bound != nullptr;
+  if (use_bound) {
+    float kn2 = d.key_bound[(d.k0_bstride == 0 ? 0 : item) * d.heads + head];
+    if (args.ntile1 > 0)
+      kn2 = fmaxf(kn2, d.key_bound[(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head]);
+    const float kn = sqrtf(kn2);
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      float ss = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss = fmaf((float)qf[b][s][j], (float)qf[b][s][j], ss);
+      qb[b] = sqrtf(sum_x32(ss)) * kn * 1.0001f;  // margin for the fp32 sums
+    }
+  }
+  bool fixed_m = false;
 
   // Running row max m (exp2 domain) enters the MFMA chain as one extra k-step:
   //   S'[key][q] = sum_k K[key][k] (cQ)[q][k] + 1 * (-m_hi[q]) + 1 * (-m_lo[q])
@@ -240,42 +279,51 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     }
 
     // ---- tile max of S' per row; rescale when a row max grew past the threshold (always on
-    // the first tile, which sets m from 0)
-    float mx[QB];
-    bool grow = t == 0;
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      float t8[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        t8[i] = fmaxf(fmaxf(sc[b][0][i], sc[b][0][i + 8]), fmaxf(sc[b][1][i], sc[b][1][i + 8]));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
-      mx[b] = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
-      grow |= mx[b] > RESCALE_LOG2;
-    }
-    if (__any(grow)) {
+    // the first tile, which sets m from 0).  A fixed-offset sweep does this on tile 0 only.
+    if (!fixed_m) {
+      float mx[QB];
+      bool grow = t == 0;
 #pragma unroll
       for (int b = 0; b < QB; ++b) {
-        // new max (rows that did not grow keep theirs), split into bf16 hi + lo
-        const float target = t == 0 ? mx[b] : m_run[b] + fmaxf(mx[b], 0.f);
-        const bf16 nhi = (bf16)target;
-        const bf16 nlo = (bf16)(target - (float)nhi);
-        const float m_new = (float)nhi + (float)nlo;
-        const float delta = m_new - m_run[b];  // S' relative to the new max: S' - delta
-        const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
-        l_run[b] *= alpha;
+        float t8[8];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          o[b][0][i] *= alpha;
-          o[b][1][i] *= alpha;
-          sc[b][0][i] -= delta;
-          sc[b][1][i] -= delta;
-        }
-        m_run[b] = m_new;
-        if (hi == 0) {
-          m_b[b][0] = -nhi;
-          m_b[b][1] = -nlo;
+        for (int i = 0; i < 8; ++i)
+          t8[i] = fmaxf(fmaxf(sc[b][0][i], sc[b][0][i + 8]), fmaxf(sc[b][1][i], sc[b][1][i + 8]));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[i], t8[i + 4]);
+        mx[b] = max_x32(fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3])));
+        grow |= mx[b] > RESCALE_LOG2;
+      }
+      if (t == 0 && use_bound) {
+        bool ok = true;
+#pragma unroll
+        for (int b = 0; b < QB; ++b) ok &= qb[b] - mx[b] <= 100.f;
+        fixed_m = __all(ok);
+      }
+      if (__any(grow)) {
+#pragma unroll
+        for (int b = 0; b < QB; ++b) {
+          // new max (rows that did not grow keep theirs), split into bf16 hi + lo
+          const float target = t == 0 ? (fixed_m ? fmaxf(mx[b], qb[b] - 50.f) : mx[b])
+                                      : m_run[b] + fmaxf(mx[b], 0.f);
+          const bf16 nhi = (bf16)target;
+          const bf16 nlo = (bf16)(target - (float)nhi);
+          const float m_new = (float)nhi + (float)nlo;
+          const float delta = m_new - m_run[b];  // S' relative to the new max: S' - delta
+          const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
+          l_run[b] *= alpha;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            o[b][0][i] *= alpha;
+            o[b][1][i] *= alpha;
+            sc[b][0][i] -= delta;
+            sc[b][1][i] -= delta;
+          }
+          m_run[b] = m_new;
+          if (hi == 0) {
+            m_b[b][0] = -nhi;
+            m_b[b][1] = -nlo;
+          }
         }
       }
     }
@@ -715,6 +763,51 @@ __global__ __launch_bounds__(256) void quant_fp8_vt_kernel(const bf16* __restric
   *(int4*)(dst + (((int64_t)head * ntiles + t) * 64 + d) * 64 + p0) = make_int4(w[0], w[1], w[2], w[3]);
 }
 
+// key_bound of sr_attention: out[inst * heads + h] = max over the instance's rows of |k[row, h]|^2
+// (fp32 bits, non-negative, so an unsigned max orders them).  Each thread owns one 16-B chunk
+// of a row (8 lanes per head, head_dim 64); blockDim = (256 / (8 heads)) * 8 heads.
+__global__ __launch_bounds__(256) void key_norm_max_kernel(const bf16* __restrict__ k, int64_t ldk, int rows,
+                                                           int64_t inst_stride, int heads, unsigned* __restrict__ out) {
+  __shared__ unsigned red[32];
+  const int cpr = heads * 8;
+  const int rpi = blockDim.x / cpr;
+  const int t = threadIdx.x;
+  const int row_in = t / cpr, c = t - row_in * cpr, head = c >> 3;
+  const int64_t inst = blockIdx.y;
+  if (t < heads) red[t] = 0u;
+  __syncthreads();
+  float m = 0.f;
+  for (int r = blockIdx.x * rpi + row_in; r < rows; r += gridDim.x * rpi) {
+    const bf16x8 v = *(const bf16x8*)(k + (inst * inst_stride + r) * ldk + c * 8);
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss = fmaf((float)v[j], (float)v[j], ss);
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    ss += __shfl_xor(ss, 4, 64);
+    m = fmaxf(m, ss);
+  }
+  if ((c & 7) == 0) atomicMax(&red[head], __float_as_uint(m));
+  __syncthreads();
+  if (t < heads) atomicMax(&out[inst * heads + t], red[t]);
+}
+
+int bound_instances(const sr_attn_desc& d, int& n0) {
+  n0 = d.k0_bstride == 0 ? 1 : d.batch;
+  return n0 + (d.l1 > 0 ? (d.k1_bstride == 0 ? 1 : d.batch) : 0);
+}
+
+void launch_key_norm(hipStream_t s, const void* k, int64_t ldk, int rows, int64_t inst_stride, int n_inst, int heads,
+                     float* out) {
+  const int cpr = heads * 8;
+  const int threads = (256 / cpr) * cpr;
+  const int rpi = threads / cpr;
+  const int want = std::max(1, 2048 / n_inst);
+  const int gx = std::max(1, std::min((rows + rpi - 1) / rpi, want));
+  hipLaunchKernelGGL(key_norm_max_kernel, dim3(gx, n_inst), dim3(threads), 0, s, (const bf16*)k, ldk, rows,
+                     inst_stride, heads, (unsigned*)out);
+}
+
 // ------------------------------------------------------------------ f32 / VALU
 constexpr int F32_KT = 32;       // keys per LDS tile
 constexpr int F32_THREADS = 128;  // query rows per workgroup
@@ -789,6 +882,12 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
 
 }  // namespace
 
+extern "C" int sr_attention_bound_floats(const sr_attn_desc* desc) {
+  if (!desc || desc->head_dim != 64 || desc->mask_mode != SR_MASK_NONE || desc->heads > 32) return 0;
+  int n0;
+  return bound_instances(*desc, n0) * desc->heads;
+}
+
 extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* desc) {
   SR_CHECK(desc, SR_EINVAL, "sr_attention: null desc");
   const sr_attn_desc& d = *desc;
@@ -809,6 +908,16 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
              SR_EINVAL, "sr_attention(bf16): leading dims must be multiples of 8");
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
+    const int n_inst = bound_instances(d, a.kb_n0);
+    if (d.key_bound) {
+      SR_CHECK(d.heads <= 32 && ((uintptr_t)d.key_bound & 3) == 0, SR_EINVAL, "sr_attention: key_bound needs heads <= 32");
+      SR_CHECK(hipMemsetAsync(d.key_bound, 0, sizeof(float) * n_inst * d.heads, s) == hipSuccess, SR_ELAUNCH,
+               "sr_attention: key_bound memset");
+      launch_key_norm(s, (const char*)d.k0, d.ldk0, d.l0, d.k0_bstride, a.kb_n0, d.heads, d.key_bound);
+      if (d.l1 > 0)
+        launch_key_norm(s, (const char*)d.k1, d.ldk1, d.l1, d.k1_bstride, n_inst - a.kb_n0, d.heads,
+                        d.key_bound + a.kb_n0 * d.heads);
+    }
     const int kind = d.l1 > 0 ? 1 : (d.batch == 1 && d.lq >= 4096 ? 2 : 0);
     // Workgroup shapes (waves x 32-row q-blocks per wave):
     //   0: 4 x 2 = 256 rows    1: 8 x 1 = 256 rows    2: 2 x 2 = 128 rows

@@ -163,6 +163,18 @@ __global__ void copy_rows_kernel(float* __restrict__ dst, int64_t ldd, const flo
   }
 }
 
+// LayerScale (layer_scale.py:22-23) as a standalone op: out[r][c] = x[r][c] * gamma[c]
+template <typename T>
+__global__ void mul_cols_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ g, T* __restrict__ out,
+                                int64_t ldo, int rows, int cols) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % cols);
+    const int64_t r = e / cols;
+    out[r * ldo + c] = sr::from_f32<T>(sr::to_f32(x[r * ldx + c]) * g[c]);
+  }
+}
+
 // ------------------------------------------------------------------ small fp32 ops (camera head)
 __device__ __forceinline__ float silu(float v) { return v / (1.f + expf(-v)); }
 
@@ -306,6 +318,22 @@ extern "C" int sr_copy_rows_f32(sr_stream_t stream, float* dst, int64_t ldd, con
   hipLaunchKernelGGL(copy_rows_kernel, grid_for((int64_t)rows * cols / 4), dim3(256), 0, (hipStream_t)stream, dst, ldd,
                      src, lds, rowmap, rows, cols / 4);
   return sr::check_launch("sr_copy_rows_f32");
+}
+
+extern "C" int sr_mul_cols(sr_stream_t stream, int dtype, const void* x, int64_t ldx, const float* gamma, void* out,
+                           int64_t ldo, int rows, int cols) {
+  SR_CHECK(x && gamma && out && rows > 0 && cols > 0, SR_EINVAL, "sr_mul_cols: bad args");
+  const int64_t total = (int64_t)rows * cols;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(mul_cols_kernel<bf16>, grid_for(total), dim3(256), 0, s, (const bf16*)x, ldx, gamma, (bf16*)out,
+                       ldo, rows, cols);
+  else {
+    SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_mul_cols: bad dtype %d", dtype);
+    hipLaunchKernelGGL(mul_cols_kernel<float>, grid_for(total), dim3(256), 0, s, (const float*)x, ldx, gamma,
+                       (float*)out, ldo, rows, cols);
+  }
+  return sr::check_launch("sr_mul_cols");
 }
 
 extern "C" int sr_linear_small_f32(sr_stream_t stream, const float* A, int64_t lda, const float* W, const float* bias,

@@ -54,6 +54,7 @@ class AttnDesc(ctypes.Structure):
         ("mask_mode", _i32), ("n_anchor", _i32),
         ("scale", _f32),
         ("lse", _vp),
+        ("key_bound", _vp),
     ]
 
 
@@ -86,6 +87,7 @@ _PROTOS = {
     "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
+    "sr_attention_bound_floats": (_i32, [ctypes.POINTER(AttnDesc)]),
     "sr_quant_fp8": (_i32, [_vp, _vp, _i64, _i32, _i32, _f32, _vp, _i64, _vp, _vp]),
     "sr_attention_qk8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp]),
     "sr_quant_fp8_vt": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
@@ -107,6 +109,7 @@ _PROTOS = {
                                    ctypes.POINTER(_f32), _vp, _i32]),
     "sr_set_special_tokens": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32]),
     "sr_copy_rows_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i32, _i32]),
+    "sr_mul_cols": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _i64, _i32, _i32]),
     "sr_linear_small_f32": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32]),
     "sr_silu_f32": (_i32, [_vp, _vp, _vp, _i64]),
     "sr_adaln_modulate_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32]),

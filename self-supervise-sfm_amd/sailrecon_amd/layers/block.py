@@ -17,25 +17,9 @@ import torch
 from torch import Tensor, nn
 
 from .. import _lib, ops, runtime
-from .attention import Attention
+from .attention import Attention, camera_mask_anchors  # noqa: F401 (re-export)
 from .layer_scale import LayerScale
 from .mlp import Mlp
-
-
-def camera_mask_anchors(attn_mask: Tensor) -> Optional[int]:
-    """If ``attn_mask`` (True = attend, [1,1,S,S] or [S,S]) is the camera-trunk pattern,
-    return its anchor count; else None."""
-    m = attn_mask.reshape(attn_mask.shape[-2], attn_mask.shape[-1]).bool().cpu()
-    S = m.shape[0]
-    for n in range(1, S + 1):
-        ref = torch.zeros(S, S, dtype=torch.bool)
-        ref[:, :n] = True
-        idx = torch.arange(n, S)
-        ref[:n, n:] = False
-        ref[idx, idx] = True
-        if torch.equal(ref, m):
-            return n
-    return None
 
 
 class Block(nn.Module):

@@ -1,10 +1,16 @@
-"""PatchEmbed parameter mirror (reference: sailrecon/layers/patch_embed.py:25-84).
+"""PatchEmbed mirror (reference: sailrecon/layers/patch_embed.py:25-84).
 
-The 14x14/stride-14 conv runs as im2col (sr_im2col_normalize) + GEMM with the
-SR_EPI_PATCH epilogue (bias + positional add + token-row remap).
+Inside the aggregator the 14x14/stride-14 conv runs as im2col (sr_im2col_normalize, fused
+with the image normalisation) + GEMM with the SR_EPI_PATCH epilogue (bias + positional add +
+token-row remap).  A standalone ``PatchEmbed.forward(x)`` (patch_embed.py:67-84) is the same
+im2col without normalisation + a bias-epilogue GEMM: [B, 3, H, W] -> [B, HW, C] (or
+[B, H', W', C] without ``flatten_embedding``), bf16 under autocast, exact fp32 otherwise.
 """
 
-from torch import nn
+import torch
+from torch import Tensor, nn
+
+from .. import _lib, ops, runtime
 
 
 def make_2tuple(x):
@@ -30,3 +36,30 @@ class PatchEmbed(nn.Module):
         self.flatten_embedding = flatten_embedding
         self.proj = nn.Conv2d(in_chans, embed_dim, kernel_size=patch_hw, stride=patch_hw)
         self.norm = norm_layer(embed_dim) if norm_layer else nn.Identity()
+
+    def forward(self, x: Tensor) -> Tensor:
+        runtime.require_device(x, "PatchEmbed")
+        _, _, H, W = x.shape
+        ph, pw = self.patch_size
+        assert H % ph == 0, f"Input image height {H} is not a multiple of patch height {ph}"
+        assert W % pw == 0, f"Input image width {W} is not a multiple of patch width: {pw}"
+        if ph != pw or self.in_chans != 3:
+            raise NotImplementedError("PatchEmbed.forward: square patches over 3 channels")
+        if not isinstance(self.norm, nn.Identity):
+            raise NotImplementedError("PatchEmbed.forward: norm_layer (unused by every SailRecon config)")
+        dtype = runtime.compute_dtype()
+        B = x.shape[0]
+        C = self.embed_dim
+        kt = 64 if dtype == torch.bfloat16 else 32
+        kpad = -(-3 * ph * pw // kt) * kt
+        gh, gw = H // ph, W // pw
+        cols = torch.empty(B * gh * gw, kpad, device=x.device, dtype=dtype)
+        ops.im2col_normalize(x.detach().float().contiguous(), ph, cols, kpad, normalize=False)
+        w = torch.zeros(C, kpad, device=x.device, dtype=dtype)
+        w[:, : 3 * ph * pw] = self.proj.weight.detach().reshape(C, -1).to(dtype)
+        out = torch.empty(B * gh * gw, C, device=x.device, dtype=dtype)
+        bias = None if self.proj.bias is None else self.proj.bias.detach().float().contiguous()
+        ops.gemm(cols, w, out, _lib.SR_EPI_BIAS, bias=bias)
+        if not self.flatten_embedding:
+            return out.view(B, gh, gw, C)
+        return out.view(B, gh * gw, C)

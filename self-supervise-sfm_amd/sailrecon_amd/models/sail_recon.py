@@ -34,6 +34,10 @@ class SailRecon(nn.Module):
                                           conf_activation="expp1")
         self.cam_token_last_layer = None
         self.need_re_forward = False
+        # opt-in extra result key: each view's 9-d pose encoding (the last camera-head iteration),
+        # what train.loss.compute_loss differentiates; off by default so forward() returns exactly
+        # the reference's keys (sail_recon.py:144-151)
+        self.return_pose_enc = False
 
     def forward(self, views, no_reloc_list=None, reloc_list=None, fix_rank=300):
         rgbs = views if isinstance(views, torch.Tensor) else torch.cat([v["img"] for v in views], dim=0)
@@ -68,7 +72,8 @@ class SailRecon(nn.Module):
                 extrinsic, intrinsic = pose_encoding_to_extri_intri(pose.contiguous(), (rgbs.shape[-2], rgbs.shape[-1]))
                 predictions["extrinsic"] = extrinsic
                 predictions["intrinsic"] = intrinsic
-                predictions["pose_enc"] = pose
+                if self.return_pose_enc:
+                    predictions["pose_enc"] = pose
             if self.point_head is not None:
                 xyz_map, xyz_cnf = self.point_head(rgb_feats, images=reloc_rgbs, patch_start_idx=idx_patch)
                 predictions["point_map"] = xyz_map

@@ -8,6 +8,7 @@ place).  No function here computes anything on the host.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -93,7 +94,7 @@ def _rowmajor(t: Tensor, name: str) -> int:
     return t.stride(0)
 
 
-_SPLITK_WS = {}  # device -> fp32 workspace of sr_gemm_splitk (single-stream use)
+_SPLITK_WS = {}  # (device, stream) -> fp32 workspace of sr_gemm_splitk
 
 
 def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
@@ -111,11 +112,19 @@ def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
     return splits
 
 
+def _ws_stream_key(device):
+    """Scratch buffers are keyed by (device, current stream): launches on different streams (the
+    opt-in concurrent reloc stack, SR_CONCURRENT_STACKS) never share one."""
+    d = torch.device(device)
+    return (str(d), torch.cuda.current_stream(d).cuda_stream if d.type == "cuda" else 0)
+
+
 def _splitk_workspace(device, numel: int) -> Tensor:
-    ws = _SPLITK_WS.get(device)
+    key = _ws_stream_key(device)
+    ws = _SPLITK_WS.get(key)
     if ws is None or ws.numel() < numel:
         ws = torch.empty(numel, device=device, dtype=torch.float32)
-        _SPLITK_WS[device] = ws
+        _SPLITK_WS[key] = ws
     return ws
 
 
@@ -191,6 +200,10 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         TIMER.stop(tag, ev0, 2.0 * M * N * K, nb)
 
 
+# fixed-offset softmax sweep (sr_attn_desc.key_bound); SR_ATTN_BOUND=0 keeps the per-tile row max
+_ATTN_BOUND = os.environ.get("SR_ATTN_BOUND", "1") != "0"
+
+
 def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
@@ -200,6 +213,10 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
                    n_anchor=n_anchor, scale=scale, lse=lse)
+    if q.dtype == torch.bfloat16 and _ATTN_BOUND:
+        nb = _lib.load().sr_attention_bound_floats(ctypes.byref(d))
+        if nb > 0:
+            d.key_bound = _p(_train_ws(q.device, "attn_key_bound", nb))
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
     rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
@@ -362,12 +379,14 @@ _MEAN = (0.485, 0.456, 0.406)  # aggregator.py:31-32
 _STD = (0.229, 0.224, 0.225)
 
 
-def im2col_normalize(img: Tensor, patch: int, out: Tensor, kpad: int) -> None:
+def im2col_normalize(img: Tensor, patch: int, out: Tensor, kpad: int, normalize: bool = True) -> None:
+    """out[f*gh*gw + p][k] = patch p's pixel k of frame f ((x - mean) / std when ``normalize``,
+    aggregator.py:267; raw for a standalone PatchEmbed, patch_embed.py:78), K zero-padded."""
     if not img.is_contiguous() or img.dtype != torch.float32:
         raise ValueError("im2col: images must be contiguous fp32 [F,3,H,W]")
     F_, C_, H, W = img.shape
-    mean = (ctypes.c_float * 3)(*_MEAN)
-    std = (ctypes.c_float * 3)(*_STD)
+    mean = (ctypes.c_float * 3)(*(_MEAN if normalize else (0.0, 0.0, 0.0)))
+    std = (ctypes.c_float * 3)(*(_STD if normalize else (1.0, 1.0, 1.0)))
     rc = _lib.load().sr_im2col_normalize(_stream(img), dtype_code(out.dtype), _p(img), F_, H, W, patch, mean, std,
                                          _p(out), kpad)
     check(rc, "sr_im2col_normalize")
@@ -378,6 +397,14 @@ def set_special_tokens(x: Tensor, frames: int, tokens_per_frame: int, table: Ten
     rc = _lib.load().sr_set_special_tokens(_stream(x), _p(x), _rowmajor(x, "x"), frames, tokens_per_frame, n_special,
                                            _p(table), _p(type_of_frame), cols)
     check(rc, "sr_set_special_tokens")
+
+
+def mul_cols(x: Tensor, gamma: Tensor, out: Tensor) -> None:
+    """out = x * gamma (per column), x / out 2-D of one dtype, gamma fp32 [cols]."""
+    if x.shape != out.shape or x.dtype != out.dtype or gamma.dtype != torch.float32 or gamma.numel() != x.shape[1]:
+        raise ValueError("mul_cols: x / out [rows, cols] of one dtype, gamma fp32 [cols]")
+    check(_lib.load().sr_mul_cols(_stream(x), dtype_code(x.dtype), _p(x), _rowmajor(x, "x"), _p(gamma), _p(out),
+                                  _rowmajor(out, "out"), x.shape[0], x.shape[1]), "sr_mul_cols")
 
 
 def copy_rows(dst: Tensor, src: Tensor, rows: int, rowmap: Optional[Tensor] = None) -> None:
@@ -527,11 +554,11 @@ def pil_tmp(n: int, c: int, rows: int, tw: int, dtype: torch.dtype, device) -> T
 
 
 # ---------------------------------------------------------------- training step
-_TRAIN_WS = {}  # (device, name) -> fp32 workspace (single-stream use)
+_TRAIN_WS = {}  # ((device, stream), name) -> fp32 workspace
 
 
 def _train_ws(device, name: str, numel: int) -> Tensor:
-    key = (device, name)
+    key = (_ws_stream_key(device), name)
     ws = _TRAIN_WS.get(key)
     if ws is None or ws.numel() < numel:
         ws = torch.empty(max(numel, 1), device=device, dtype=torch.float32)

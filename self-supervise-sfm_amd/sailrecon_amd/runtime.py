@@ -103,6 +103,20 @@ def pack_block(blk, dtype: torch.dtype) -> PackedBlock:
     )
 
 
+def pack_attention(a, dtype: torch.dtype) -> PackedBlock:
+    """The attention half of pack_block for a standalone ``Attention.forward``."""
+    w = lambda t: t.detach().to(dtype).contiguous()  # noqa: E731
+    qk = bool(getattr(a, "qk_norm", False))
+    dim = a.qkv.in_features
+    return PackedBlock(
+        dim=dim, heads=a.num_heads, head_dim=a.head_dim, eps=0.0, qk_eps=a.q_norm.eps if qk else 1e-5, qk_norm=qk,
+        ln1_w=None, ln1_b=None, ln2_w=None, ln2_b=None, w_qkv=w(a.qkv.weight), b_qkv=_f32(a.qkv.bias),
+        qn_w=_f32(a.q_norm.weight) if qk else None, qn_b=_f32(a.q_norm.bias) if qk else None,
+        kn_w=_f32(a.k_norm.weight) if qk else None, kn_b=_f32(a.k_norm.bias) if qk else None,
+        w_proj=w(a.proj.weight), b_proj=_f32(a.proj.bias), g1=None, w_fc1=None, b_fc1=None, w_fc2=None, b_fc2=None,
+        g2=None)
+
+
 class Workspace:
     """Grow-only device scratch, keyed by name (reused across forwards)."""
 

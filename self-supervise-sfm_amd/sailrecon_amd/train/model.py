@@ -472,14 +472,20 @@ class TrainGraph:
         S, Na, P, R, C, n_patch = st["S"], st["Na"], st["P"], st["R"], st["C"], st["n_patch"]
         psi = agg.patch_start_idx
         g = lambda p: p.grad  # noqa: E731
-        # aggregator special tokens (aggregator.py:287-299): type 0 = first anchor, 1 = other
-        # anchors, 2 = queries; their rows were overwritten, so nothing flows below them
-        groups = [(0, 1, agg.camera_token.grad[0, 0, 0], agg.register_token.grad[0, 0]),
-                  (1, Na, agg.camera_token.grad[0, 1, 0], agg.register_token.grad[0, 1]),
-                  (Na, S, agg.camera_token_reloc.grad[0, 0, 0], agg.register_token_reloc.grad[0, 0])]
+        # aggregator special tokens (aggregator.py:287-299): type 0 = ORIGINAL frame 0 as an
+        # anchor, 1 = other anchors, 2 = queries (the forward's st["types"], per internal frame);
+        # their rows were overwritten, so nothing flows below them.  Runs of equal type are
+        # column-summed as strided frame views.
+        dst = {0: (agg.camera_token.grad[0, 0, 0], agg.register_token.grad[0, 0]),
+               1: (agg.camera_token.grad[0, 1, 0], agg.register_token.grad[0, 1]),
+               2: (agg.camera_token_reloc.grad[0, 0, 0], agg.register_token_reloc.grad[0, 0])}
+        types = st["types"]
+        groups, f0 = [], 0
+        for f in range(1, S + 1):
+            if f == S or types[f] != types[f0]:
+                groups.append((f0, f) + dst[types[f0]])
+                f0 = f
         for f0, f1, gcam, greg in groups:
-            if f1 <= f0:
-                continue
             view = dx[f0 * P:]
             ops.colsum(view.as_strided((f1 - f0, C), (P * C, 1)), gcam, accumulate=True)
             ops.colsum(view[1:].as_strided((f1 - f0, 4 * C), (P * C, 1)), greg.reshape(-1), accumulate=True)

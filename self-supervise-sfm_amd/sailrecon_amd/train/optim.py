@@ -67,10 +67,15 @@ class GradScaler:
         dev = optimizer.flat.grad.device
         scale_t, found = self._buffers(dev)
         scale_t.fill_(self._scale * world_size)
+        if not self.enabled:
+            # a disabled torch GradScaler steps unconditionally: no inf/NaN check, no skip
+            optimizer.step(scale=scale_t, found_inf=None)
+            self._found = False
+            return False
         found.zero_()
         ops.nonfinite_check(optimizer.flat.grad, found, scale_t)
         optimizer.step(scale=scale_t, found_inf=found)
-        self._found = bool(found.item()) if self.enabled else False
+        self._found = bool(found.item())
         if self._found:
             optimizer.step_count -= 1  # torch.optim.Adam's state step does not advance on a skipped step
         return self._found

@@ -14,6 +14,8 @@ Outputs (numpy .npz, no pickle):
   g3_ops.npz                        op KATs (RoPE, masks)
   g4_c1_224.npz                     full-size config 1 (N=2 @ 224) summaries
   g5_518_n1.npz                     full-size N=1 @ 518 summaries
+  g9_518_n8.npz, g10_518_n32.npz    full-size BASELINE C2 / C3 summaries (args c2, c3)
+  g11_small_interleaved.npz         small config, permuted + interleaved anchor/query lists
   state_dict_keys.json              reference state_dict keys + shapes
 """
 
@@ -68,9 +70,9 @@ class Hot(torch.nn.Module):
         self.camera_head = CameraHead(**cam_kw)
 
 
-def run_hot(model, images, na, fix_rank, seed=0):
+def run_hot(model, images, na, fix_rank, seed=0, lists=None):
     S = images.shape[1]
-    no_reloc, reloc = list(range(na)), list(range(na, S))
+    no_reloc, reloc = lists if lists is not None else (list(range(na)), list(range(na, S)))
     model.aggregator.generator.manual_seed(seed)
     with torch.no_grad():
         feats, psi, cam_last = model.aggregator(images, no_reloc, reloc, fix_rank=fix_rank)  # sail_recon.py:101
@@ -101,6 +103,27 @@ def small_case(tag, img, n_views, fix_rank):
     with open(os.path.join(HERE, "small_state_dict_keys.json"), "w") as f:
         json.dump({k: list(v.shape) for k, v in m.state_dict().items()}, f, indent=0, sort_keys=True)
     return m
+
+
+def interleaved_case():
+    """Frame-order semantics (aggregator.py:287-299,351-399): anchors and queries interleaved and
+    permuted, frame 0 a query (so no anchor gets camera_token[:, 0])."""
+    torch.manual_seed(0)
+    agg_kw = dict(img_size=56, patch_size=14, embed_dim=384, depth=2, num_heads=6,
+                  patch_embed="dinov2_vits14_reg", intermediate_layer_idx=[0, 1])
+    cam_kw = dict(dim_in=768, trunk_depth=2, num_heads=6)
+    m = Hot(agg_kw, cam_kw).eval()
+    m.load_state_dict(synth_state_dict_like(m))
+    g = torch.Generator().manual_seed(5)
+    images = torch.rand(1, 6, 3, 56, 56, generator=g)
+    no_reloc, reloc = [3, 1, 4], [0, 5, 2]
+    feats, psi, cam_last, poses, ext, intr = run_hot(m, images, 3, 10, lists=(no_reloc, reloc))
+    d = dict(images=np32(images), fix_rank=np.int64(10), no_reloc=np.array(no_reloc), reloc=np.array(reloc),
+             sub_idx=replay_indices(0, 2, 3, 16, 10),
+             feat_0=np32(feats[0]), feat_1=np32(feats[1]), cam_token_last_layer=np32(cam_last),
+             pose_enc=np.stack([np32(p) for p in poses]), extrinsic=np32(ext), intrinsic=np32(intr))
+    np.savez_compressed(os.path.join(HERE, "g11_small_interleaved.npz"), **d)
+    print("wrote g11_small_interleaved", {k: v.shape for k, v in d.items()})
 
 
 def block_kats():
@@ -207,3 +230,9 @@ if __name__ == "__main__":
             json.dump(keys, f, indent=0, sort_keys=True)
     if "518" in which:
         full_case("g5_518_n1.npz", 518, 1)
+    if "c2" in which:  # BASELINE config 2: N=8 @518 (~2 min on 8 cores)
+        full_case("g9_518_n8.npz", 518, 8)
+    if "c3" in which:  # BASELINE config 3: N=32 @518 (~17 min, ~30 GB RSS on 8 cores)
+        full_case("g10_518_n32.npz", 518, 32)
+    if "interleaved" in which:
+        interleaved_case()

@@ -71,7 +71,10 @@ def test_sailrecon_with_heads_end_to_end():
         model.aggregator.generator.manual_seed(0)  # same subsample draws as the forward above
         feats, psi, _ = model.aggregator(images, [0, 1], [2, 3], fix_rank=300)
     assert len(res) == 2
+    keys = {"extrinsic", "intrinsic", "point_map_by_unprojection", "point_map", "rgbs", "xyz_cnf", "depth_map",
+            "dpt_cnf", "cam_tokens", "images"}  # exactly the reference's (sail_recon.py:125-151)
     for r in res:
+        assert set(r) == keys, sorted(r)
         assert r["extrinsic"].shape == (1, 3, 4) and r["intrinsic"].shape == (1, 3, 3)
         assert r["point_map"].shape == (1, 224, 224, 3) and r["xyz_cnf"].shape == (1, 224, 224)
         assert r["depth_map"].shape == (1, 224, 224, 1) and r["dpt_cnf"].shape == (1, 224, 224)

@@ -1,0 +1,127 @@
+"""Standalone L1 module forwards (SURVEY §1 public interfaces): Attention.forward
+(attention.py:70-122), Mlp.forward (mlp.py:34-40), PatchEmbed.forward (patch_embed.py:67-84),
+LayerScale.forward (layer_scale.py:22-23) on the HIP path, against the CPU oracle's statement of
+each op (fp32: 1e-5 rel-L2; bf16 under autocast: 2e-2, operands rounded to bf16 as the
+reference's autocast Linear does).  Block KATs (reference goldens) are in test_parity_gpu.py."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return DEV
+
+
+def _seeded(m, seed):
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    torch.manual_seed(seed)
+    sd = synth_state_dict_like(m)
+    m.load_state_dict(sd)
+    return {k: v.float() for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", ["aggregator", "dino", "camera_mask"])
+def test_attention_forward(dev, mode, case):
+    from oracle import sfm_oracle as O
+    from sailrecon_amd.heads.camera_head import build_lr_mask
+    from sailrecon_amd.layers.attention import Attention, MemEffAttention
+    from sailrecon_amd.layers.rope import PositionGetter, RotaryPositionEmbedding2D
+    B, gh, gw = 2, 6, 7
+    if case == "aggregator":  # aggregator.py:99-114: qk-norm + RoPE(100)
+        C, H = 1024, 16
+        m = Attention(C, num_heads=H, qk_norm=True, rope=RotaryPositionEmbedding2D(100))
+        N = gh * gw + 5
+        pos = PositionGetter()(B, gh, gw, "cpu") + 1
+        pos = torch.cat([torch.zeros(B, 5, 2, dtype=pos.dtype), pos], 1)
+        kw = dict(qk_norm=True, rope_base=100.0)
+        mask = None
+    elif case == "dino":  # vision_transformer.py:161-177: MemEffAttention, no RoPE / qk-norm
+        C, H = 384, 6
+        m = MemEffAttention(C, num_heads=H)
+        N, pos, kw, mask = 37, None, {}, None
+    else:  # camera trunk (camera_head.py:51-61,165): D = 128, ~build_lr_mask
+        C, H = 2048, 16
+        m = Attention(C, num_heads=H)
+        B, N, pos, kw = 1, 10, None, {}
+        mask = ~build_lr_mask(N, list(range(6)))
+    sd = _seeded(m, 3)
+    m = m.to(dev)
+    x = torch.randn(B, N, C, generator=torch.Generator().manual_seed(4))
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=(mode == "bf16")):
+        if case == "dino":
+            y = m(x.to(dev))
+        else:
+            y = m(x.to(dev), pos=None if pos is None else pos.to(dev),
+                  attn_mask=None if mask is None else mask.to(dev))
+    ref = O.attention(sd, "", x, H, pos=pos, mask=mask, **kw)
+    tol = 1e-5 if mode == "fp32" or case == "camera_mask" else 2e-2
+    assert y.shape == (B, N, C)
+    # the masked / head_dim-128 camera case always runs the exact fp32 kernel
+    assert y.dtype == (torch.float32 if mode == "fp32" or case == "camera_mask" else torch.bfloat16)
+    assert rel(y.float(), ref) < tol
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("dims", [(1024, 4096, 1024), (384, 1536, 384), (2048, 1024, 9)])
+def test_mlp_forward(dev, mode, dims):
+    """block Mlp (4x) and the camera pose_branch shape (2048 -> 1024 -> 9, camera_head.py:70-75)."""
+    from oracle import sfm_oracle as O
+    from sailrecon_amd.layers.mlp import Mlp
+    cin, hid, cout = dims
+    m = Mlp(cin, hidden_features=hid, out_features=cout)
+    sd = _seeded(m, 5)
+    m = m.to(dev)
+    x = torch.randn(3, 77, cin, generator=torch.Generator().manual_seed(6))
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=(mode == "bf16")):
+        y = m(x.to(dev))
+    ref = O.mlp(sd, "", x)
+    assert y.shape == (3, 77, cout)
+    assert rel(y.float(), ref) < (1e-5 if mode == "fp32" else 2e-2)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("flatten", [True, False])
+def test_patch_embed_forward(dev, mode, flatten):
+    from sailrecon_amd.layers.patch_embed import PatchEmbed
+    m = PatchEmbed(img_size=518, patch_size=14, in_chans=3, embed_dim=1024, flatten_embedding=flatten)
+    sd = _seeded(m, 7)
+    m = m.to(dev)
+    x = torch.rand(2, 3, 70, 98, generator=torch.Generator().manual_seed(8))
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=(mode == "bf16")):
+        y = m(x.to(dev))
+    ref = F.conv2d(x, sd["proj.weight"], sd["proj.bias"], stride=14).flatten(2).transpose(1, 2)
+    if not flatten:
+        ref = ref.reshape(2, 5, 7, 1024)
+    assert y.shape == ref.shape
+    assert rel(y.float(), ref) < (1e-5 if mode == "fp32" else 2e-2)
+    with pytest.raises(AssertionError):
+        m(torch.rand(1, 3, 71, 98, device=dev))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_layer_scale_forward(dev, dtype, inplace):
+    from sailrecon_amd.layers.layer_scale import LayerScale
+    m = LayerScale(1024, init_values=0.01, inplace=inplace).to(dev)
+    with torch.no_grad():
+        m.gamma.copy_(torch.linspace(-2, 3, 1024))
+    x = torch.randn(5, 33, 1024, device=dev).to(dtype)
+    ref = x.float() * m.gamma.detach().float()
+    with torch.no_grad():
+        y = m(x)
+    if inplace:
+        assert y is x
+    assert rel(y.float(), ref) < (1e-7 if dtype == torch.float32 else 4e-3)

@@ -43,6 +43,23 @@ def test_small_end_to_end(tag):
     assert rel_l2(out["intrinsic"].numpy(), g["intrinsic"]) < 1e-5
 
 
+def test_small_interleaved_lists():
+    """Oracle on permuted + interleaved anchor/query lists (g11, reference-generated)."""
+    g = load_npz("g11_small_interleaved.npz")
+    sd = rule_state_dict("small_state_dict_keys.json")
+    no_reloc, reloc = g["no_reloc"].tolist(), g["reloc"].tolist()
+    images = torch.from_numpy(g["images"])
+    gen = torch.Generator().manual_seed(0)
+    sub = O.draw_subsample_indices(gen, 2, 1, len(no_reloc), 16, 10)
+    assert np.array_equal(sub[:, 0].numpy(), g["sub_idx"])
+    out = O.hot_path_forward(sd, O.AggCfg(**SMALL_AGG), images, no_reloc, reloc, 10, sub, **SMALL_CAM)
+    for layer in (0, 1):
+        assert rel_l2(out["feats"][layer].numpy(), g[f"feat_{layer}"]) < 1e-5
+    assert rel_l2(out["cam_token_last_layer"].numpy(), g["cam_token_last_layer"]) < 1e-5
+    pe = np.stack([p.numpy() for p in out["pose_enc_list"]])
+    assert rel_l2(pe, g["pose_enc"]) < 1e-5
+
+
 def test_block_kats():
     g = load_npz("g2_blocks.npz")
     sd = rule_state_dict("block_state_dict_keys.json", "agg")

@@ -29,12 +29,13 @@ class Hot(nn.Module):
         self.camera_head = CameraHead(**cam_kw)
 
 
-def run(model, images, n, fix_rank, mode):
+def run(model, images, n, fix_rank, mode, lists=None):
     from sailrecon_amd.utils.pose_enc import pose_encoding_to_extri_intri
     S = images.shape[1]
+    no_reloc, reloc = lists if lists is not None else (list(range(n)), list(range(n, S)))
     model.aggregator.generator.manual_seed(0)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=(mode == "bf16")):
-        feats, psi, cam_last = model.aggregator(images, list(range(n)), list(range(n, S)), fix_rank=fix_rank)
+        feats, psi, cam_last = model.aggregator(images, no_reloc, reloc, fix_rank=fix_rank)
         with torch.autocast("cuda", enabled=False):
             poses = model.camera_head(feats, cam_last)
             ext, intr = pose_encoding_to_extri_intri(poses[-1], (images.shape[-2], images.shape[-1]))
@@ -72,6 +73,26 @@ def test_small_end_to_end(small_model, tag, mode):
     assert rel_l2(pe, g["pose_enc"]) < tol
     assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
     assert rel_l2(intr.cpu().numpy(), g["intrinsic"]) < tol
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_small_interleaved_lists(small_model, mode):
+    """Frame-order semantics (aggregator.py:287-299,351-399): anchors [3, 1, 4] and queries
+    [0, 5, 2] interleaved and permuted, frame 0 a query (no anchor takes camera_token[:, 0]);
+    outputs in reloc_list / no_reloc_list order, subsample draws in no_reloc_list order."""
+    g = load_npz("g11_small_interleaved.npz")
+    no_reloc, reloc = g["no_reloc"].tolist(), g["reloc"].tolist()
+    images = torch.from_numpy(g["images"]).to(DEV)
+    feats, psi, cam_last, poses, ext, intr = run(small_model, images, len(no_reloc), int(g["fix_rank"]), mode,
+                                                 lists=(no_reloc, reloc))
+    assert np.array_equal(small_model.aggregator.last_subsample_indices[:, 0].numpy(), g["sub_idx"])
+    tol = TOL[mode]
+    for layer in (0, 1):
+        assert rel_l2(feats[layer].cpu().numpy(), g[f"feat_{layer}"]) < tol, layer
+    assert rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"]) < tol
+    pe = np.stack([p.cpu().numpy() for p in poses])
+    assert rel_l2(pe, g["pose_enc"]) < tol
+    assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
 
 
 def test_block_kats_fp32():
@@ -139,3 +160,15 @@ def test_full_c1_224(full_model, mode):
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_full_518_n1(full_model, mode):
     _check_full(full_model, "g5_518_n1.npz", mode)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_full_c2_518_n8(full_model, mode):
+    """BASELINE config 2: N=8 views @518 (S=16 frames, L_g = 10,992, L_r = 13,432)."""
+    _check_full(full_model, "g9_518_n8.npz", mode)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_full_c3_518_n32(full_model, mode):
+    """BASELINE config 3, the headline workload: N=32 views @518 (S=64 frames, L_g = 43,968)."""
+    _check_full(full_model, "g10_518_n32.npz", mode)

@@ -32,17 +32,21 @@ class Hot(torch.nn.Module):
         self.camera_head = CameraHead(dim_in=768, trunk_depth=2, num_heads=6)
 
 
-def _reference_grads(sd, images, sub, d, Na, Nq):
+def _reference_grads(sd, images, sub, d, no_reloc, reloc):
     from oracle import sfm_oracle as O
     ref = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
     cfg = O.AggCfg(patch=14, embed_dim=384, depth=2, heads=6, dino_depth=12, dino_heads=6, inter_idx=(0, 1))
-    feats, _, cam_last = O.aggregator_forward(ref, cfg, images, list(range(Na)), list(range(Na, Na + Nq)), 10, sub)
+    feats, _, cam_last = O.aggregator_forward(ref, cfg, images, no_reloc, reloc, 10, sub)
     poses = O.camera_head_forward(ref, feats[-1], cam_last, heads=6, trunk_depth=2)
     (poses[-1] * d).sum().backward()
     return poses[-1].detach(), {k: v.grad for k, v in ref.items() if v.is_floating_point()}
 
 
-def test_train_graph_matches_autograd():
+@pytest.mark.parametrize("lists", [([0, 1], [2, 3]), ([3, 1], [0, 2])], ids=["canonical", "frame0_query"])
+def test_train_graph_matches_autograd(lists):
+    """``frame0_query``: interleaved lists with original frame 0 a query, so no anchor takes
+    camera_token[:, 0] (the special-token grads follow the forward's types)."""
+    no_reloc, reloc = lists
     from sailrecon_amd.train.model import TrainGraph
     from sailrecon_amd.utils.synth_weights import synth_state_dict_like
     torch.manual_seed(0)
@@ -55,13 +59,13 @@ def test_train_graph_matches_autograd():
     x = torch.rand(n, 3, 56, 56, generator=torch.Generator().manual_seed(1))
     images = torch.cat([x, x])[None]
     m.aggregator.generator.manual_seed(0)
-    pose = tg.forward(images.to(DEV), [0, 1], [2, 3], fix_rank=10)
+    pose = tg.forward(images.to(DEV), no_reloc, reloc, fix_rank=10)
     d = torch.randn(1, n, 9, generator=torch.Generator().manual_seed(2))
     tg.flat.zero_grad()
     tg.backward(d.to(DEV))
     torch.cuda.synchronize()
     sub = m.aggregator.last_subsample_indices
-    ref_pose, ref_g = _reference_grads(sd, images, sub, d, n, n)
+    ref_pose, ref_g = _reference_grads(sd, images, sub, d, no_reloc, reloc)
     assert rel(pose, ref_pose) < 2e-2
     errs = {}
     for name, p in m.named_parameters():
