@@ -38,9 +38,60 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table); see gpu_peak()
 PEAK_F32_TFLOPS = 157.3    # f32 MFMA
 PEAK_HBM_GBS = 8000.0
+
+
+def gpu_peak(device_index: int = 0):
+    """Dense bf16 MFMA peak from rocminfo: CUs x max engine clock x 4096 bf16
+    FLOP/clk/CU (32x32x16 bf16 = 32768 FLOP per 32 cycles per SIMD, 4 SIMDs).  Returns
+    (TFLOP/s, description) or (None, reason) when rocminfo is unavailable."""
+    import subprocess
+    try:
+        out = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=60).stdout
+    except (OSError, subprocess.SubprocessError) as e:
+        return None, f"rocminfo unavailable ({e})"
+    agents, cur = [], {}
+    for line in out.splitlines():
+        line = line.strip()
+        if line.startswith("Agent ") and cur:
+            agents.append(cur)
+            cur = {}
+        if ":" in line:
+            k, v = line.split(":", 1)
+            cur.setdefault(k.strip(), v.strip())
+    if cur:
+        agents.append(cur)
+    gpus = [a for a in agents if a.get("Device Type") == "GPU" and a.get("Name", "").startswith("gfx")]
+    if not gpus:
+        return None, "no GPU agent in rocminfo"
+    a = gpus[min(device_index, len(gpus) - 1)]
+    cus, mhz = int(a["Compute Unit"]), int(a["Max Clock Freq. (MHz)"].split()[0])
+    tf = cus * mhz * 1e6 * 4096 / 1e12
+    return tf, f"rocminfo {a['Name']}: {cus} CU x {mhz} MHz x 4096 bf16 FLOP/clk/CU = {tf:.1f} TFLOP/s"
+
+
+def host_cpu():
+    """(model name, physical cores, logical CPUs os.cpu_count()) of this host."""
+    model, cores = "unknown", set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model == "unknown":
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+    except OSError:
+        pass
+    return model, len(cores) or (os.cpu_count() or 1), os.cpu_count()
 
 # timer class -> the kernel instantiation it launches at the N=32@518 workload
 # (rocprofv3 row names; see DESIGN.md "Kernels").
@@ -95,10 +146,15 @@ def build_model(device, seed_rule=True):
 
 
 def cpu_baseline(sd, img: int, n_views: int):
-    """The CPU oracle (oracle/sfm_oracle.py, a port of the reference path) on a bounded
-    sample: one full forward of an n_views scene (2*n_views frames)."""
+    """The CPU oracle (oracle/sfm_oracle.py, a port of the reference path: dense reloc mask,
+    scatter reassembly, fp32) on a bounded sample: one full forward of an n_views scene
+    (2*n_views frames, the headline's per-view structure at a size that runs in ~10-30 s).
+    Threads = the physical cores of this process's CPU share (OMP_NUM_THREADS caps it on the
+    GPU box, whose os.cpu_count() is the whole machine)."""
     from oracle import sfm_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    model, phys, logical = host_cpu()
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(phys, cap) if cap > 0 else phys
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(n_views)
     x = torch.rand(n_views, 3, img, img, generator=g)
@@ -109,8 +165,10 @@ def cpu_baseline(sd, img: int, n_views: int):
     O.hot_path_forward(sd, O.AggCfg(), images, list(range(n_views)), list(range(n_views, 2 * n_views)), 300, sub)
     dt = time.perf_counter() - t0
     return {"value": n_views / dt, "unit": "views/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "physical_cores": phys, "os_cpu_count": logical,
             "sample": f"1 full fp32 forward of a {n_views}-view scene @{img}px ({2 * n_views} frames; "
-                      f"aggregator+camera head+pose decode) on the host CPU, {dt:.1f} s"}
+                      f"aggregator+camera head+pose decode, the oracle port of the reference path) on the host "
+                      f"CPU, {threads} threads, {dt:.1f} s"}
 
 
 def main():
@@ -121,7 +179,7 @@ def main():
     ap.add_argument("--views", type=int, default=32)
     ap.add_argument("--img", type=int, default=518)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-views", type=int, default=1)
+    ap.add_argument("--cpu-views", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
@@ -181,9 +239,14 @@ def main():
 
     roofline = None
     breakdown = {}
+    peak_src = None
     if timer is not None:
         breakdown = timer.summary()
-        peak = PEAK_BF16_TFLOPS if use_bf16 else PEAK_F32_TFLOPS
+        bf16_peak = PEAK_BF16_TFLOPS
+        tf, peak_src = gpu_peak(device.index or 0)
+        if tf:
+            bf16_peak = tf
+        peak = bf16_peak if use_bf16 else PEAK_F32_TFLOPS
         dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
         b = breakdown[dom]
         achieved = b["tflops"]
@@ -191,12 +254,13 @@ def main():
         if fp8 and dom == "attn_global":
             # half the attention flops (q.k^T) at the fp8 rate (2x bf16), half (P.V) at the bf16 rate
             if args.fp8_global == "qkv":  # every attention flop at the fp8 rate
-                kern, peak = "attn_qk8_kernel<2, true>", 2 * PEAK_BF16_TFLOPS
+                kern, peak = "attn_qk8_kernel<2, true>", 2 * bf16_peak
             else:
-                kern, peak = "attn_qk8_kernel<2, false>", 1.0 / (0.5 / (2 * PEAK_BF16_TFLOPS) + 0.5 / PEAK_BF16_TFLOPS)
+                kern, peak = "attn_qk8_kernel<2, false>", 1.0 / (0.5 / (2 * bf16_peak) + 0.5 / bf16_peak)
         traffic = pmc_traffic(kern, n, args.img) if kern and not fp8 else None
         roofline = {"bound": "mfma", "kernel": kern or dom, "timer_class": dom, "achieved": round(achieved, 2),
-                    "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                    "peak": round(peak, 1), "peak_source": peak_src, "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4),
                     "traffic": None if traffic is None else round(traffic),
                     "traffic_unit": "bytes/launch (HBM, PMC 2xFETCH_SIZE+WRITE_SIZE)",
                     "traffic_source": os.path.relpath(TRAFFIC_FILE, REPO) if traffic is not None else None,
@@ -207,7 +271,7 @@ def main():
             flop = sum(v["flops_per_launch"] * v["launches"] for v in gems)
             ms = sum(v["total_ms"] for v in gems)
             roofline["gemm_all_tflops"] = round(flop / (ms * 1e-3) / 1e12, 1)
-            gpeak = PEAK_BF16_TFLOPS if use_bf16 else PEAK_F32_TFLOPS  # GEMMs stay bf16 in the fp8 modes
+            gpeak = bf16_peak if use_bf16 else PEAK_F32_TFLOPS  # GEMMs stay bf16 in the fp8 modes
             roofline["gemm_mfma_util"] = round(flop / (ms * 1e-3) / 1e12 / gpeak, 4)
         print(json.dumps({"kernel_breakdown": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                                                    for kk, vv in v.items()} for k, v in breakdown.items()},

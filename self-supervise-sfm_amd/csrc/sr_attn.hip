@@ -32,6 +32,7 @@ struct AttnArgs {
   sr_attn_desc d;
   int ntile0, ntile1;  // key tiles per segment
   int kb_n0;           // segment-0 instances in d.key_bound (1 if shared, else batch)
+  int allow_mzero;     // fixed offset m == 0 drops the -m fold MFMAs (SR_ATTN_MZERO=0: keep them)
 };
 
 // ------------------------------------------------------------------ bf16 / MFMA
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
       qb[b] = sqrtf(sum_x32(ss)) * kn * 1.0001f;  // margin for the fp32 sums
     }
   }
-  bool fixed_m = false;
+  bool fixed_m = false, m_zero = false;
 
   // Running row max m (exp2 domain) enters the MFMA chain as one extra k-step:
   //   S'[key][q] = sum_k K[key][k] (cQ)[q][k] + 1 * (-m_hi[q]) + 1 * (-m_lo[q])
@@ -247,21 +248,33 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     // of its four waves empty) keeps staging and barriers but leaves its SIMD to the other waves
     if (!wave_active) continue;
 
-    // ---- S'^T = K (cQ)^T - m for every q-block (2 blocks of 32 keys each)
+    // ---- S'^T = K (cQ)^T - m for every q-block (2 blocks of 32 keys each); once every row of
+    // the wave runs the fixed offset m = 0, the -m fold MFMAs are skipped (uniform branch)
     f32x16 sc[QB][2];  // [q-block][key block]
     const f32x16 zero = {};
+    if (m_zero) {
 #pragma unroll
-    for (int b = 0; b < QB; ++b)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) sc[b][kb] = mfma32(one_a, m_b[b], zero);
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = *(const bf16x8*)(kt_lds + kb * 4096 + koff[s]);
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+          for (int b = 0; b < QB; ++b) sc[b][kb] = mfma32(kf, qf[b][s], s == 0 ? zero : sc[b][kb]);
+        }
+    } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *(const bf16x8*)(kt_lds + kb * 4096 + koff[s]);
+      for (int b = 0; b < QB; ++b)
 #pragma unroll
-        for (int b = 0; b < QB; ++b) sc[b][kb] = mfma32(kf, qf[b][s], sc[b][kb]);
-      }
+        for (int kb = 0; kb < 2; ++kb) sc[b][kb] = mfma32(one_a, m_b[b], zero);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = *(const bf16x8*)(kt_lds + kb * 4096 + koff[s]);
+#pragma unroll
+          for (int b = 0; b < QB; ++b) sc[b][kb] = mfma32(kf, qf[b][s], sc[b][kb]);
+        }
+    }
 
     // ---- mask the ragged tail of a segment
     const bool s1 = t >= nt0;
@@ -272,10 +285,8 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (key >= valid) sc[b][kb][r] = -INFINITY;
-          }
+          for (int r = 0; r < 16; ++r)  // key kb*32 + (r&3) + 8(r>>2) + 4hi >= valid (immediate compares)
+            if (kb * 32 + (r & 3) + 8 * (r >> 2) >= valid - 4 * hi) sc[b][kb][r] = -INFINITY;
     }
 
     // ---- tile max of S' per row; rescale when a row max grew past the threshold (always on
@@ -304,7 +315,9 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
 #pragma unroll
         for (int b = 0; b < QB; ++b) {
           // new max (rows that did not grow keep theirs), split into bf16 hi + lo
-          const float target = t == 0 ? (fixed_m ? fmaxf(mx[b], qb[b] - 50.f) : mx[b])
+          // fixed offset: m = 0 when the row's bound allows it (every score <= qb <= 50 and the
+          // true max >= -qb >= -50), else max(tile-0 max, qb - 50)
+          const float target = t == 0 ? (fixed_m ? (qb[b] <= 50.f ? 0.f : fmaxf(mx[b], qb[b] - 50.f)) : mx[b])
                                       : m_run[b] + fmaxf(mx[b], 0.f);
           const bf16 nhi = (bf16)target;
           const bf16 nlo = (bf16)(target - (float)nhi);
@@ -324,6 +337,12 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
             m_b[b][0] = -nhi;
             m_b[b][1] = -nlo;
           }
+        }
+        if (fixed_m && args.allow_mzero) {
+          bool z = true;
+#pragma unroll
+          for (int b = 0; b < QB; ++b) z &= m_run[b] == 0.f;
+          m_zero = __all(z);
         }
       }
     }
@@ -538,10 +557,8 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (key >= valid) sc[b][kb][r] = -INFINITY;
-          }
+          for (int r = 0; r < 16; ++r)  // key kb*32 + (r&3) + 8(r>>2) + 4hi >= valid (immediate compares)
+            if (kb * 32 + (r & 3) + 8 * (r >> 2) >= valid - 4 * hi) sc[b][kb][r] = -INFINITY;
     }
     float mx[QB];
     bool grow = t == 0;
@@ -909,6 +926,11 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
     const int n_inst = bound_instances(d, a.kb_n0);
+    static const int allow_mz = [] {
+      const char* e = getenv("SR_ATTN_MZERO");
+      return e ? atoi(e) : 1;
+    }();
+    a.allow_mzero = allow_mz;
     if (d.key_bound) {
       SR_CHECK(d.heads <= 32 && ((uintptr_t)d.key_bound & 3) == 0, SR_EINVAL, "sr_attention: key_bound needs heads <= 32");
       SR_CHECK(hipMemsetAsync(d.key_bound, 0, sizeof(float) * n_inst * d.heads, s) == hipSuccess, SR_ELAUNCH,
