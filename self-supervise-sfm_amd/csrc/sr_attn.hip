@@ -77,7 +77,19 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
+  int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
+  if constexpr (KIND == 1) {
+    // global_reloc: every query frame of a head reads the same anchor-subsample K/V (segment 0,
+    // 2.5 MB per head at C3).  Blocks are dealt round-robin over the 8 XCDs; the bijective remap
+    // hands each XCD a contiguous range of (head, frame, q-tile) in head-major order, so one
+    // head's shared K/V stays in that XCD's L2 while all of its query frames sweep it.
+    const int nq = gridDim.x, nh = gridDim.y, nb = gridDim.z;
+    const int lin = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
+    const int tile = sr::xcd_remap(lin, nq * nh * nb);
+    qt = tile % nq;
+    item = (tile / nq) % nb;
+    head = tile / (nq * nb);
+  }
   const int hcol = head * 64;
   const int l32 = lane & 31, hi = lane >> 5;
   const int ntiles = args.ntile0 + args.ntile1;
