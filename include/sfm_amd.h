@@ -145,8 +145,8 @@ typedef struct sr_attn_desc {
   int64_t k1_bstride;
   int mask_mode, n_anchor;
   float scale;
-  float* lse;  /* optional (bf16 path): [batch][heads][lq] row log-sum-exp of scale*log2(e)*q.k
-                  (log2 domain), saved for sr_attention_bwd */
+  float* lse;  /* optional: [batch][heads][lq] row log-sum-exp of scale*log2(e)*q.k (log2
+                  domain), saved for sr_attention_bwd and for sr_attn_merge */
   float* key_bound; /* optional scratch (bf16 path, >= sr_attention_bound_floats(d) floats, 4-B
                   aligned): per key-segment instance and head, max |k| over the keys.  With it a
                   query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^100 of its first
@@ -158,6 +158,17 @@ typedef struct sr_attn_desc {
 int sr_attention_bound_floats(const sr_attn_desc* d);
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
+
+/* Merge two attention results of the same query rows over DISJOINT key sets, given each one's
+ * log2-domain LSE ([heads][rows] fp32, as sr_attention writes for batch 1):
+ *   out = (2^(la-m) o_a + 2^(lb-m) o_b) / (2^(la-m) + 2^(lb-m)),  m = max(la, lb)
+ * i.e. softmax over the union of the keys, exactly.  out may alias o_a or o_b; lse_out
+ * (optional, may alias lse_a) receives the union's LSE.  Replaces nothing in the reference:
+ * the frame-sharded global block starts on the local anchors' K/V while the
+ * remote anchors' K/V are still being all-gathered, then merges (DESIGN.md "Multi-GPU"). */
+int sr_attn_merge(sr_stream_t stream, int dtype, int rows, int heads, int head_dim, const void* o_a, int64_t lda,
+                  const float* lse_a, const void* o_b, int64_t ldb, const float* lse_b, void* out, int64_t ldo,
+                  float* lse_out);
 
 /* fp8 (OCP e4m3) quantisation with ONE power-of-two scale per tensor (BASELINE C5, "fp8 QKV";
  * e4m3 Q/K/V with per-tensor scales):

@@ -906,6 +906,50 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
     const float inv = 1.f / l;
 #pragma unroll
     for (int i = 0; i < D; ++i) op[i] = o[i] * inv;
+    // same log2-domain convention as the bf16 kernel: log2(sum_j 2^(scale*log2e*q.k_j))
+    if (d.lse) d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m * 1.4426950408889634f + log2f(l);
+  }
+}
+
+// ------------------------------------------------------------------ partial-softmax merge
+// out = (2^(la-mx) oa + 2^(lb-mx) ob) / (2^(la-mx) + 2^(lb-mx)), mx = max(la, lb): two attention
+// passes over disjoint key sets of the same queries (the frame-sharded global block: local
+// anchors while the all-gather is in flight, then the remote anchors).  One thread per 4
+// columns of one (row, head); consecutive threads walk a row's columns (coalesced).
+template <typename T>
+__global__ __launch_bounds__(256) void attn_merge_kernel(const T* __restrict__ oa, int64_t lda,
+                                                         const float* __restrict__ la, const T* __restrict__ ob,
+                                                         int64_t ldb, const float* __restrict__ lb, T* out,
+                                                         int64_t ldo, float* __restrict__ lout, int rows, int heads,
+                                                         int head_dim) {
+  const int chunks = head_dim >> 2;
+  const int64_t total = (int64_t)rows * heads * chunks;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % chunks);
+    const int64_t rh = e / chunks;
+    const int h = (int)(rh % heads);
+    const int64_t r = rh / heads;
+    const float a = la[(int64_t)h * rows + r], b = lb[(int64_t)h * rows + r];
+    const float mx = fmaxf(a, b);
+    float wa = 0.f, wb = 0.f, sum = 0.f;
+    if (mx != -INFINITY) {
+      wa = exp2f(a - mx);
+      wb = exp2f(b - mx);
+      sum = wa + wb;
+      const float inv = 1.f / sum;
+      wa *= inv;
+      wb *= inv;
+    }
+    const int col = h * head_dim + 4 * c;
+    const T* pa = oa + r * lda + col;
+    const T* pb = ob + r * ldb + col;
+    float y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = wa * sr::to_f32(pa[j]) + wb * sr::to_f32(pb[j]);
+    T* po = out + r * ldo + col;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) po[j] = sr::from_f32<T>(y[j]);
+    if (lout && c == 0) lout[(int64_t)h * rows + r] = mx == -INFINITY ? mx : mx + log2f(sum);
   }
 }
 
@@ -952,7 +996,9 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
         launch_key_norm(s, (const char*)d.k1, d.ldk1, d.l1, d.k1_bstride, n_inst - a.kb_n0, d.heads,
                         d.key_bound + a.kb_n0 * d.heads);
     }
-    const int kind = d.l1 > 0 ? 1 : (d.batch == 1 && d.lq >= 4096 ? 2 : 0);
+    // one long query item = the global block (also its two-segment remote-anchor pass under frame
+    // sharding); otherwise a second segment = global_reloc
+    const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : (d.l1 > 0 ? 1 : 0);
     // Workgroup shapes (waves x 32-row q-blocks per wave):
     //   0: 4 x 2 = 256 rows    1: 8 x 1 = 256 rows    2: 2 x 2 = 128 rows
     // 256-row tiles unless they would leave CUs idle (fewer than 2 workgroups per CU, e.g. the
@@ -990,6 +1036,25 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     return SR_EUNSUPPORTED;
   }
   return sr::check_launch("sr_attention(f32)");
+}
+
+extern "C" int sr_attn_merge(sr_stream_t stream, int dtype, int rows, int heads, int head_dim, const void* o_a,
+                             int64_t lda, const float* lse_a, const void* o_b, int64_t ldb, const float* lse_b,
+                             void* out, int64_t ldo, float* lse_out) {
+  SR_CHECK(o_a && o_b && lse_a && lse_b && out && rows > 0 && heads > 0 && head_dim > 0 && head_dim % 4 == 0,
+           SR_EINVAL, "sr_attn_merge: bad arguments");
+  const int64_t total = (int64_t)rows * heads * (head_dim / 4);
+  const dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 65536));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(attn_merge_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)o_a, lda, lse_a, (const bf16*)o_b,
+                       ldb, lse_b, (bf16*)out, ldo, lse_out, rows, heads, head_dim);
+  else {
+    SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attn_merge: bad dtype %d", dtype);
+    hipLaunchKernelGGL(attn_merge_kernel<float>, grid, dim3(256), 0, s, (const float*)o_a, lda, lse_a,
+                       (const float*)o_b, ldb, lse_b, (float*)out, ldo, lse_out, rows, heads, head_dim);
+  }
+  return sr::check_launch("sr_attn_merge");
 }
 
 extern "C" int sr_quant_fp8(sr_stream_t stream, const void* src, int64_t ld, int rows, int cols, float mul, void* dst,

@@ -88,6 +88,7 @@ _PROTOS = {
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_attention_bound_floats": (_i32, [ctypes.POINTER(AttnDesc)]),
+    "sr_attn_merge": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp]),
     "sr_quant_fp8": (_i32, [_vp, _vp, _i64, _i32, _i32, _f32, _vp, _i64, _vp, _vp]),
     "sr_attention_qk8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp]),
     "sr_quant_fp8_vt": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),

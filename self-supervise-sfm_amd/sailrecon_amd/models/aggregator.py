@@ -59,6 +59,10 @@ class Aggregator(nn.Module):
         self.fp8_global = os.environ.get("SR_FP8_GLOBAL", "0") in ("1", "qkv")
         self.fp8_v = os.environ.get("SR_FP8_GLOBAL", "0") == "qkv"
         self._fp8_ws = None
+        # frame sharding: global attention starts on the local anchors' K/V while the remote
+        # anchors' K/V are still being gathered, then merges the two passes by their LSEs
+        # (SR_SHARD_OVERLAP=0: wait for the gather, one pass over every anchor)
+        self.shard_overlap = os.environ.get("SR_SHARD_OVERLAP", "1") != "0"
 
         def blocks(cache=False):
             return nn.ModuleList([block_fn(dim=embed_dim, num_heads=num_heads, mlp_ratio=mlp_ratio, qkv_bias=qkv_bias,
@@ -173,11 +177,14 @@ class Aggregator(nn.Module):
     def set_frame_sharding(self, group=None):
         """Shard frames across the ranks of ``group`` (torch.distributed, RCCL on ROCm).
 
-        Rank r of G owns anchors no_reloc_list[r*Na/G:(r+1)*Na/G] and the matching slice of
-        reloc_list.  DINO, frame blocks, subsampling and every per-token GEMM stay local;
-        the global block all-gathers K/V of the anchors, the global_reloc block all-gathers
-        the anchor-subsample K/V, and the camera head runs replicated on gathered camera
-        tokens.  The subsample generator is re-seeded identically on every
+        Rank r of G owns a contiguous, balanced slice of no_reloc_list and of reloc_list
+        (``shard_range``: counts differ by at most one; uneven splits are exact, no padded
+        frames ever enter a softmax).  DINO, frame blocks, subsampling and every per-token GEMM
+        stay local; the global block all-gathers K/V of the anchors (attending to the local
+        anchors while the gather is in flight, then to the remote ones, merged by LSE), the
+        global_reloc block all-gathers the anchor-subsample K/V, and the camera head runs
+        replicated on gathered camera tokens (SURVEY §8(e)).  Every rank needs >= 1 anchor;
+        a rank may own no query frame.  The subsample generator is re-seeded identically on every
         rank (broadcast from rank 0) so the draws do not depend on the world size.
         ``group=None`` disables sharding."""
         self._shard_group = group
@@ -268,12 +275,15 @@ class Aggregator(nn.Module):
             raise NotImplementedError("a kv_cache aggregator runs anchors only here (SailRecon.tmp_forward) and "
                                       "queries through forward_with_cache (SailRecon.reloc), like the reference")
         fill_cache = self.kv_cache  # anchors-only pass: keep every layer's anchor-subsample K|V
-        if G > 1 and (B != 1 or Na % G or Nq % G):
-            raise ValueError(f"frame sharding over {G} ranks needs B == 1 and anchor / query counts "
-                             f"divisible by {G} (got B={B}, Na={Na}, Nq={Nq})")
-        Na_l, Nq_l = Na // G, Nq // G
-        my_anchors = list(no_reloc_list)[r * Na_l:(r + 1) * Na_l]
-        my_queries = list(reloc_list)[r * Nq_l:(r + 1) * Nq_l]
+        if G > 1 and (B != 1 or Na < G):
+            raise ValueError(f"frame sharding over {G} ranks needs B == 1 and at least one anchor frame per "
+                             f"rank (got B={B}, Na={Na})")
+        a_start, Na_l = shard_range(Na, G, r)
+        q_start, Nq_l = shard_range(Nq, G, r)
+        a_counts = [shard_range(Na, G, j)[1] for j in range(G)]
+        q_counts = [shard_range(Nq, G, j)[1] for j in range(G)]
+        my_anchors = list(no_reloc_list)[a_start:a_start + Na_l]
+        my_queries = list(reloc_list)[q_start:q_start + Nq_l]
         S_l = Na_l + Nq_l
 
         dev = images.device
@@ -316,7 +326,7 @@ class Aggregator(nn.Module):
                 raise NotImplementedError("kv_cache needs B == 1 (aggregator.py:452)")
             self._kv_cache_layers = [None] * self.depth
         if need_sub:
-            idx = idx[:, :, r * Na_l:(r + 1) * Na_l]                      # this rank's anchors
+            idx = idx[:, :, a_start:a_start + Na_l]                       # this rank's anchors
             base = (np.arange(B) * S_l * P)[None, :, None, None] + (np.arange(Na_l) * P)[None, None, :, None]
             sel = base + psi + idx                                        # [depth, B, Na_l, rank]
             spec = np.broadcast_to(base + np.arange(psi)[None, None, None, :], (self.depth, B, Na_l, psi))
@@ -340,7 +350,7 @@ class Aggregator(nn.Module):
             pb = self.frame_blocks[l].packed(dtype)
             runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P),
                               runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
-            if l in out_maps:  # frame half of the intermediate, :403-413
+            if l in out_maps and Nq_l > 0:  # frame half of the intermediate, :403-413
                 for b in range(B):
                     ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, :C],
                                   x[b * S_l * P + Na_l * P:(b + 1) * S_l * P], Nq_l * P)
@@ -350,10 +360,10 @@ class Aggregator(nn.Module):
             pg = self.global_blocks[l].packed(dtype)
             for b in range(B):
                 a0, q0, q1 = b * S_l * P, b * S_l * P + Na_l * P, (b + 1) * S_l * P
-                self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if need_sub else None, Na_l * Pp, a0, q0, q1,
-                                   Nq_l, P, rope, posctx, dtype, dev, group, G, r,
+                self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if need_sub else None, Pp, a0, q0, q1,
+                                   Nq_l, P, rope, posctx, dtype, dev, group, G, r, a_counts, need_sub,
                                    cache_layer=l if fill_cache else None)
-            if l in out_maps:  # reloc half
+            if l in out_maps and Nq_l > 0:  # reloc half
                 for b in range(B):
                     ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, C:],
                                   x[b * S_l * P + Na_l * P:(b + 1) * S_l * P], Nq_l * P)
@@ -368,13 +378,15 @@ class Aggregator(nn.Module):
         if G > 1:
             # camera head inputs for every frame: anchor camera tokens and query camera tokens
             cam_last = torch.empty(B * Na, 2 * C, device=dev, dtype=torch.float32)
-            torch.distributed.all_gather_into_tensor(cam_last, cam_loc.view(B * Na_l, 2 * C), group=group)
-            cam_last = cam_last.view(B, Na, 2 * C)
+            works = gather_rows(cam_last, cam_loc.view(B * Na_l, 2 * C), a_counts, group, r)
             if Nq > 0:
                 qcam = torch.empty(B * Nq, 2 * C, device=dev, dtype=torch.float32)
-                torch.distributed.all_gather_into_tensor(
-                    qcam, output_dict[-1][:, :, 0].reshape(B * Nq_l, 2 * C).contiguous(), group=group)
+                works += gather_rows(qcam, output_dict[-1][:, :, 0].reshape(B * Nq_l, 2 * C).contiguous(), q_counts,
+                                     group, r)
                 self.last_query_cam_tokens = qcam.view(B, Nq, 2 * C)
+            for w in works:
+                w.wait()
+            cam_last = cam_last.view(B, Na, 2 * C)
         else:
             cam_last = cam_loc
             self.last_query_cam_tokens = output_dict[-1][:, :, 0] if Nq > 0 else None
@@ -448,32 +460,34 @@ class Aggregator(nn.Module):
         return output_dict, self.patch_start_idx
 
     # ------------------------------------------------------------------ stacks
-    def _layer_global(self, pr, pg, x, sc, rowmap, n_sub, a0, q0, q1, Nq_l, P, rope, posctx, dtype, dev,
-                      group, G, r, cache_layer=None):
+    def _layer_global(self, pr, pg, x, sc, rowmap, Pp, a0, q0, q1, Nq_l, P, rope, posctx, dtype, dev,
+                      group, G, r, a_counts, need_sub, cache_layer=None):
         """global_reloc (queries, aggregator.py:672-741) + global (anchors, :743-769) blocks of
         one layer for one batch item.  With G > 1 the anchor K/V and the anchor-subsample K/V
-        are all-gathered (async, overlapped with the query-side QKV GEMM)."""
+        are gathered asynchronously (``gather_rows``; ``a_counts`` = anchor frames per rank):
+        the subsample K/V behind the query-side QKV GEMM, the anchor K/V behind the whole reloc
+        block and the local-anchor attention pass."""
         C = pg.dim
         ws = self._ws
-        La_l = q0 - a0           # local anchor tokens
-        La = La_l * G            # all anchor tokens
-        work_sub = work_kv = None
-        if Nq_l > 0 or cache_layer is not None:
+        La_l = q0 - a0                 # local anchor tokens
+        La = sum(a_counts) * P         # all anchor tokens
+        n_sub = (q0 - a0) // P * Pp    # local anchor-subsample rows
+        n_sub_all = sum(a_counts) * Pp
+        work_sub, work_kv = [], []
+        if need_sub:
             # anchor-subsample K/V (reads x before the global block updates the anchors)
             xn_sub = ws.get("xn_sub", n_sub, C, dtype, dev)
             if G > 1:  # separate send buffer: no aliasing between collective input and output
                 kv_sub = ws.get("kv_sub_loc", n_sub, 2 * C, dtype, dev)
-                kv_sub_all = ws.get("kv_sub", n_sub * G, 2 * C, dtype, dev)
+                kv_sub_all = ws.get("kv_sub", n_sub_all, 2 * C, dtype, dev)
             else:
                 kv_sub = kv_sub_all = ws.get("kv_sub", n_sub, 2 * C, dtype, dev)
             ops.layernorm(x, pr.ln1_w, pr.ln1_b, pr.eps, xn_sub, rowmap=rowmap, rows=n_sub)
             self._kv_gemm(pr, xn_sub, kv_sub, rope, dict(pos_rowmap=rowmap, **posctx))
             if G > 1:
-                work_sub = torch.distributed.all_gather_into_tensor(kv_sub_all, kv_sub, group=group, async_op=True)
+                work_sub = gather_rows(kv_sub_all, kv_sub, [c * Pp for c in a_counts], group, r)
             if cache_layer is not None:  # two-phase reloc: every anchor's subsample K|V of this layer
-                if work_sub is not None:
-                    work_sub.wait()
-                    work_sub = None
+                _wait(work_sub)
                 self._kv_cache_layers[cache_layer] = kv_sub_all.clone()
         if G > 1:
             # global block, first half: LN1 + Q GEMM locally, K/V straight into this rank's slot
@@ -489,7 +503,7 @@ class Aggregator(nn.Module):
                 ops.gemm(xn, pg.w_qkv[:C], qkv[:, :C], _lib.SR_EPI_QKV, bias=_sl(pg.b_qkv, 0, C), qkv=epi,
                          tag="gemm")
             self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
-            work_kv = torch.distributed.all_gather_into_tensor(kv_all, kv_loc, group=group, async_op=True)
+            work_kv = gather_rows(kv_all, kv_loc, [c * P for c in a_counts], group, r)
         # G == 1: the reloc block (query rows) and the global block (anchor rows) are independent.
         # SR_CONCURRENT_STACKS=1 runs the reloc block on a side stream so that each could fill the
         # other's last partial wave; measured 3% SLOWER at N=32 (68.7 -> 66.7 views/s: the two
@@ -497,10 +511,9 @@ class Aggregator(nn.Module):
         side = self._side_stream(dev) if (G == 1 and Nq_l > 0 and a0 < q0) else None
         if Nq_l > 0:
             def attend_reloc(qkv, o):
-                if work_sub is not None:
-                    work_sub.wait()
+                _wait(work_sub)
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
-                              head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub * G, k0_bstride=0,
+                              head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
                               k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
@@ -510,10 +523,15 @@ class Aggregator(nn.Module):
             else:
                 runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
                                   runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
+        _wait(work_sub)  # a rank without query frames still fed the others (send buffer reuse)
         if G > 1:
-            work_kv.wait()
-            o = sc.o[a0:q0]
-            self._global_attention(sc.qkv[a0:q0, 0:C], kv_all[:, 0:C], kv_all[:, C:2 * C], o, pg, La_l, La)
+            o, q = sc.o[a0:q0], sc.qkv[a0:q0, 0:C]
+            fp8 = self.fp8_global and pg.head_dim == 64 and q.dtype == torch.bfloat16
+            if self.shard_overlap and not fp8:
+                self._global_attention_sharded(q, kv_loc, kv_all, o, pg, La_l, La, sum(a_counts[:r]) * P, work_kv)
+            else:
+                _wait(work_kv)
+                self._global_attention(q, kv_all[:, 0:C], kv_all[:, C:2 * C], o, pg, La_l, La)
             runtime.run_block_tail(pg, x, a0, q0, sc)
         else:
             def attend_global(qkv, o):
@@ -529,6 +547,26 @@ class Aggregator(nn.Module):
         self.fp8_global = bool(enabled)
         self.fp8_v = bool(enabled and fp8_v)
         return self
+
+    def _global_attention_sharded(self, q, kv_loc, kv_all, o, pg, lq, lk, off, work_kv):
+        """softmax over every anchor's keys in two passes: the local anchors (kv_loc, ready now)
+        while the gather of the others is in flight, then the remote anchors (kv_all rows outside
+        [off, off + lq): up to two key segments), merged exactly by the passes' LSEs."""
+        C, H, D = pg.dim, pg.heads, pg.head_dim
+        ws = self._ws
+        lse_loc = ws.get("lse_loc", H, lq, torch.float32, q.device)
+        lse_rem = ws.get("lse_rem", H, lq, torch.float32, q.device)
+        o_rem = ws.get("o_rem", lq, C, o.dtype, q.device)
+        ops.attention(q, kv_loc[:, 0:C], kv_loc[:, C:2 * C], o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0,
+                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc)
+        _wait(work_kv)
+        segs = [(a, n) for a, n in ((0, off), (off + lq, lk - off - lq)) if n > 0]
+        (s0, n0), (s1, n1) = segs[0], (segs[1] if len(segs) > 1 else (0, 0))
+        ops.attention(q, kv_all[s0:s0 + n0, 0:C], kv_all[s0:s0 + n0, C:2 * C], o_rem, heads=H, head_dim=D, batch=1,
+                      lq=lq, q_bstride=0, l0=n0, k0_bstride=0, k1=kv_all[s1:s1 + n1, 0:C] if n1 else None,
+                      v1=kv_all[s1:s1 + n1, C:2 * C] if n1 else None, l1=n1, k1_bstride=0, tag="attn_global",
+                      lse=lse_rem)
+        ops.attn_merge(o, lse_loc, o_rem, lse_rem, o, heads=H, head_dim=D, tag="attn_merge")
 
     def _global_attention(self, q, k, v, o, pg, lq, lk):
         if self.fp8_global and pg.head_dim == 64 and q.dtype == torch.bfloat16:
@@ -563,3 +601,32 @@ class Aggregator(nn.Module):
 
 def _sl(t, a, b):
     return None if t is None else t[a:b]
+
+
+def _wait(works):
+    for w in works:
+        w.wait()
+    works.clear()
+
+
+def shard_range(n: int, G: int, r: int) -> Tuple[int, int]:
+    """(start, count) of rank r's contiguous share of n frames over G ranks: the first n % G
+    ranks own one frame more than the rest (counts differ by at most one)."""
+    base, extra = divmod(n, G)
+    return r * base + min(r, extra), base + (1 if r < extra else 0)
+
+
+def gather_rows(dst: torch.Tensor, src: torch.Tensor, counts: List[int], group, rank: int) -> list:
+    """Async gather of every rank's ``src`` rows into ``dst`` = [rank 0's rows ; rank 1's ; ...]
+    (``counts[j]`` rows from rank j; row-contiguous tensors).  Equal counts: one
+    all_gather_into_tensor (RCCL ring over xGMI).  Uneven counts: one broadcast per non-empty
+    rank straight into that rank's slot of ``dst`` — the rows land compact, so no padding row
+    can reach a softmax.  Returns the works to wait on."""
+    dist = torch.distributed
+    if len(set(counts)) == 1:
+        return [dist.all_gather_into_tensor(dst, src, group=group, async_op=True)]
+    offs = np.concatenate([[0], np.cumsum(counts)]).tolist()
+    if counts[rank]:
+        dst[offs[rank]:offs[rank + 1]].copy_(src)
+    return [dist.broadcast(dst[offs[j]:offs[j + 1]], src=dist.get_global_rank(group, j), group=group, async_op=True)
+            for j in range(len(counts)) if counts[j]]

@@ -13,7 +13,7 @@ import torch.nn as nn
 
 from ..heads.camera_head import CameraHead
 from ..utils.pose_enc import pose_encoding_to_extri_intri
-from .aggregator import Aggregator
+from .aggregator import Aggregator, shard_range
 
 
 class SailRecon(nn.Module):
@@ -52,8 +52,10 @@ class SailRecon(nn.Module):
         # frame-sharded aggregator (Aggregator.set_frame_sharding): this rank's query views only;
         # the camera head runs replicated on the gathered camera tokens of every view
         _, G, r = self.aggregator._world()
-        nq_l = len(reloc_list) // G
-        local_reloc = list(reloc_list)[r * nq_l:(r + 1) * nq_l]
+        q0, nq_l = shard_range(len(reloc_list), G, r)
+        local_reloc = list(reloc_list)[q0:q0 + nq_l]
+        if not local_reloc:  # more ranks than query views: this rank only served anchors
+            return []
         # a list index is a blocking host->device copy of the index: it made the host wait for the
         # whole aggregator before enqueueing the heads.  Contiguous query frames (the demo's
         # reloc_list = range(N, 2N)) are a slice; others go through a pinned async index copy.
@@ -68,7 +70,7 @@ class SailRecon(nn.Module):
             if self.camera_head is not None:
                 cam_in = rgb_feats if G == 1 else [self.aggregator.last_query_cam_tokens[:, :, None]]
                 cam_maps = self.camera_head(cam_in, cam_token_last_layer)
-                pose = cam_maps[-1][:, r * nq_l:(r + 1) * nq_l]
+                pose = cam_maps[-1][:, q0:q0 + nq_l]
                 extrinsic, intrinsic = pose_encoding_to_extri_intri(pose.contiguous(), (rgbs.shape[-2], rgbs.shape[-1]))
                 predictions["extrinsic"] = extrinsic
                 predictions["intrinsic"] = intrinsic

@@ -228,6 +228,27 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
         TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim, nb)
 
 
+def attn_merge(o_a: Tensor, lse_a: Tensor, o_b: Tensor, lse_b: Tensor, out: Tensor, *, heads: int, head_dim: int,
+               lse_out: Optional[Tensor] = None, tag: Optional[str] = None) -> None:
+    """Softmax over the union of two disjoint key sets from the two passes' outputs (o [rows, C])
+    and log2-domain LSEs (fp32 [heads, rows]); see sr_attn_merge.  out may alias o_a / o_b."""
+    rows = out.shape[0]
+    for t in (o_a, o_b):
+        if t.dtype != out.dtype or t.shape[0] != rows:
+            raise ValueError("attn_merge: o_a / o_b / out must share dtype and rows")
+    for t in (lse_a, lse_b) + (() if lse_out is None else (lse_out,)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != heads * rows:
+            raise ValueError("attn_merge: lse must be contiguous fp32 [heads, rows]")
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    rc = _lib.load().sr_attn_merge(_stream(out), dtype_code(out.dtype), rows, heads, head_dim, _p(o_a),
+                                   _rowmajor(o_a, "o_a"), _p(lse_a), _p(o_b), _rowmajor(o_b, "o_b"), _p(lse_b), _p(out),
+                                   _rowmajor(out, "out"), _p(lse_out))
+    check(rc, "sr_attn_merge")
+    if timed:
+        TIMER.stop(tag, ev0, 0.0, out.element_size() * rows * heads * head_dim * 3 + 12 * rows * heads)
+
+
 def quant_fp8(src: Tensor, mul: float, dst: Optional[Tensor] = None, exp_out: Optional[Tensor] = None):
     """e4m3 copy of ``mul * src`` (bf16 [rows, cols]) with one power-of-two scale (sr_quant_fp8):
     returns (dst uint8 [rows, cols], exp int32 device scalar) with mul * src ~= dst * 2^exp."""

@@ -80,7 +80,7 @@ def _positions(qkv, M):
 
 
 def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
-              k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None):
+              k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None, lse=None):
     D = head_dim
     scale = D ** -0.5 if scale is None else scale
     for b in range(batch):
@@ -99,6 +99,21 @@ def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bst
                 j = torch.arange(kk.shape[0])[None]
                 s = s.masked_fill(~((j < n_anchor) | (j == i)), float("-inf"))
             o[b * q_bstride:b * q_bstride + lq, sl] = (torch.softmax(s, -1) @ vv[:, sl]).to(o.dtype)
+            if lse is not None:
+                lse.view(batch, heads, lq)[b, h] = torch.logsumexp(s, -1) * (1.0 / math.log(2.0))
+
+
+def attn_merge(o_a, lse_a, o_b, lse_b, out, *, heads, head_dim, lse_out=None, tag=None):
+    la, lb = lse_a.view(heads, -1).t(), lse_b.view(heads, -1).t()  # [rows, heads]
+    m = torch.maximum(la, lb)
+    wa, wb = torch.exp2(la - m), torch.exp2(lb - m)
+    tot = wa + wb
+    rows = out.shape[0]
+    ya = o_a.float().view(rows, heads, head_dim) * (wa / tot)[..., None]
+    yb = o_b.float().view(rows, heads, head_dim) * (wb / tot)[..., None]
+    out.copy_((ya + yb).view(rows, heads * head_dim).to(out.dtype))
+    if lse_out is not None:
+        lse_out.view(heads, -1).copy_((m + torch.log2(tot)).t())
 
 
 def layernorm(x, w, b, eps, out, rowmap=None, rows=None):
@@ -156,7 +171,7 @@ def pose_decode(enc, hw, ext, intr):
     intr.copy_(i[0])
 
 
-_NAMES = ["gemm", "attention", "layernorm", "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
+_NAMES = ["gemm", "attention", "attn_merge", "layernorm", "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
           "silu", "adaln_modulate", "pose_update", "pose_decode"]
 
 

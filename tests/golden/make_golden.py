@@ -220,6 +220,8 @@ if __name__ == "__main__":
     if "small" in which:
         small_case("56", 56, 2, 10)
         small_case("70", 70, 3, 10)
+    if "small5" in which:  # 5 anchors + 5 queries: uneven frame sharding over 2 / 3 ranks
+        small_case("56_n5", 56, 5, 10)
     if "blocks" in which:
         block_kats()
     if "ops" in which:

@@ -92,6 +92,76 @@ def test_global_attention_production(ops, L):
     assert _rel(o[rows].float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("G,r", [(2, 0), (2, 1), (3, 1)], ids=["C3-2rk-r0", "C3-2rk-r1", "C3-3rk-mid"])
+def test_global_attention_sharded_passes(ops, G, r):
+    """The frame-sharded global block at C3 (32 anchors): rank r's query rows attend to its own
+    anchors (local pass), then to every other rank's (remote pass: one key segment at the ends,
+    two — before and after the local slice — on a middle rank; 32 over 3 ranks is the uneven
+    11 / 11 / 10 split), merged by sr_attn_merge.  Checked against fp64 attention over ALL keys
+    and against the kernel's single pass over all keys, LSE included."""
+    from sailrecon_amd.models.aggregator import shard_range
+    L = 32 * P
+    q, k, v = _make(L, 11, spikes=(L - 37, 3 * P + 5))
+    a0, na = shard_range(32, G, r)
+    off, lq = a0 * P, na * P
+    qs = q[off:off + lq]
+    lse_a = torch.empty(H, lq, device=DEV)
+    lse_b = torch.empty(H, lq, device=DEV)
+    o = torch.empty(lq, C, device=DEV, dtype=torch.bfloat16)
+    o_b = torch.empty_like(o)
+    ops.attention(qs, k[off:off + lq], v[off:off + lq], o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0,
+                  l0=lq, k0_bstride=0, lse=lse_a)
+    segs = [(s, n) for s, n in ((0, off), (off + lq, L - off - lq)) if n > 0]
+    (s0, n0), (s1, n1) = segs[0], (segs[1] if len(segs) > 1 else (0, 0))
+    ops.attention(qs, k[s0:s0 + n0], v[s0:s0 + n0], o_b, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=n0,
+                  k0_bstride=0, k1=k[s1:s1 + n1] if n1 else None, v1=v[s1:s1 + n1] if n1 else None, l1=n1,
+                  k1_bstride=0, lse=lse_b)
+    lse_m = torch.empty(H, lq, device=DEV)
+    ops.attn_merge(o, lse_a, o_b, lse_b, o, heads=H, head_dim=D, lse_out=lse_m)  # in place on o
+    one = torch.empty_like(o)
+    lse_1 = torch.empty(H, lq, device=DEV)
+    ops.attention(qs, k, v, one, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0, lse=lse_1)
+    torch.cuda.synchronize()
+    rows = _sample_rows(lq, 256, lq + G).to(DEV)
+    ref = _ref_rows(qs[rows], k, v, D ** -0.5)
+    assert _rel(o[rows].float(), ref) < 1e-2
+    assert _rel(o.float(), one.float()) < 1e-2
+    assert float((lse_m - lse_1).abs().max()) < 2e-3
+
+
+@pytest.mark.parametrize("alias", [False, True])
+def test_attn_merge_fp32_exact(ops, alias):
+    """fp32 kernel passes over a 3-way key split, merged pairwise (lse_out chaining): equal to the
+    one-pass fp32 kernel to float rounding; the fp32 kernel's LSE equals torch.logsumexp."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    lq, L, h, d = 300, 900, 6, 64
+    q, k, v = (torch.randn(n, h * d, device=DEV, generator=g) for n in (lq, L, L))
+    cuts = [(0, 250), (250, 610), (610, 900)]
+    outs, lses = [], []
+    for a, b in cuts:
+        o = torch.empty(lq, h * d, device=DEV)
+        lse = torch.empty(h, lq, device=DEV)
+        ops.attention(q, k[a:b], v[a:b], o, heads=h, head_dim=d, batch=1, lq=lq, q_bstride=0, l0=b - a,
+                      k0_bstride=0, lse=lse)
+        outs.append(o)
+        lses.append(lse)
+    o, lse = outs[0], lses[0]
+    for ob, lb in zip(outs[1:], lses[1:]):
+        dst = o if alias else torch.empty_like(o)
+        lse_dst = lse if alias else torch.empty_like(lse)
+        ops.attn_merge(o, lse, ob, lb, dst, heads=h, head_dim=d, lse_out=lse_dst)
+        o, lse = dst, lse_dst
+    one = torch.empty(lq, h * d, device=DEV)
+    lse1 = torch.empty(h, lq, device=DEV)
+    ops.attention(q, k, v, one, heads=h, head_dim=d, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0, lse=lse1)
+    s = torch.einsum("qhd,khd->hqk", q.view(lq, h, d).double(), k.view(L, h, d).double()) * d ** -0.5
+    ref_lse = torch.logsumexp(s, -1) / math.log(2.0)
+    torch.cuda.synchronize()
+    assert _rel(o, one) < 1e-5
+    assert float((lse1.double() - ref_lse).abs().max()) < 1e-4
+    assert float((lse.double() - ref_lse).abs().max()) < 1e-4
+
+
 def _deq(q8, e):
     return q8.view(torch.float8_e4m3fn).double() * (2.0 ** int(e))
 

@@ -134,3 +134,81 @@ def test_block_backward_fp32_camera():
     assert rel(dx, xr.grad) < 1e-4, "input grad"
     for n, p in blk.named_parameters():
         assert rel(p.grad, ref[n].grad) < 1e-4, n
+
+
+def test_block_backward_c4_global():
+    """BASELINE C4 (train_imc, 16 views): ONE full-width aggregator global block (C = 1024, 16
+    heads, qk-norm + RoPE) forward-with-tape + backward over L_g = 16 x 1374 = 21,984 anchor
+    tokens, the production attention shapes (frame_attend_train(pb, 1, L) is how train/model.py
+    drives the global stack).  The upstream gradient is nonzero on 192 sampled output rows only,
+    so the reference — autograd through the oracle's block (block.py:86-112, attention.py:70-122)
+    in fp32 on the CPU — needs those rows' queries / MLP only, while every key / value row and so
+    EVERY input row still receives a gradient through K and V.  Checked: the forward on the
+    sampled rows, the input grad on the sampled rows and separately on 1024 other rows (their
+    grad flows only through the attention backward's dK / dV), and every parameter grad; bf16
+    operands vs the fp32 reference -> 3e-2 rel-L2 like the small bf16 block test."""
+    from oracle import sfm_oracle as O
+    import torch.nn.functional as F
+    from sailrecon_amd import runtime
+    from sailrecon_amd.layers.block import Block
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    from sailrecon_amd.train import engine
+    from sailrecon_amd.train.params import FlatParams
+    torch.manual_seed(0)
+    C, H, frames, gh, gw = 1024, 16, 16, 37, 37
+    P = 5 + gh * gw
+    L = frames * P
+    D = C // H
+    rope = RotaryPositionEmbedding2D(100)
+    blk = Block(dim=C, num_heads=H, init_values=0.01, qk_norm=True, rope=rope)
+    _randomize(blk, 4)
+    sd = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    blk = blk.to(DEV)
+    fp = FlatParams(blk)
+    blk.invalidate_packed()
+    dt = torch.bfloat16
+    pb = blk.packed(dt)
+    tabs = rope.tables(D, max(gh, gw) + 1, DEV)
+    qkv_epi = runtime.qkv_params(pb, tabs, pos_row_base=0, tokens_per_frame=P, patch_start=5, grid_w=gw)
+    tape = engine.alloc_tape(L, C, 4 * C, dt, DEV, H * L, separate_raw=True)
+    fwd, bwd = engine.frame_attend_train(pb, 1, L)
+    x = torch.randn(L, C, generator=torch.Generator().manual_seed(5))
+    xd = x.to(DEV)
+    engine.run_block_train(pb, xd, 0, L, tape, fwd, qkv_epi)
+    g = torch.Generator().manual_seed(6)
+    rows = torch.sort(torch.randperm(L, generator=g)[:192]).values
+    w = torch.randn(len(rows), C, generator=g)
+    dy = torch.zeros(L, C)
+    dy[rows] = w
+    dx = dy.to(DEV)
+    dxb = dx.bfloat16()
+    fp.zero_grad()
+    bp = engine.pack_bwd(blk, pb, dt)
+    engine.block_bwd(pb, bp, engine.block_grads(blk), tape, dx, dxb, bwd, qkv_epi, engine.BwdScratch())
+    torch.cuda.synchronize()
+
+    # reference: the block's outputs at `rows` only, autograd through the oracle (fp32, CPU)
+    ref = {k: v.clone().requires_grad_(True) for k, v in sd.items() if v.is_floating_point()}
+    xr = x.clone().requires_grad_(True)
+    pos = _positions(frames, P, gw)[None]                       # [1, L, 2]
+    a = "attn."
+    xn = O.layer_norm(xr, ref["norm1.weight"], ref["norm1.bias"], 1e-5)
+    kv = F.linear(xn, ref[a + "qkv.weight"][C:], ref[a + "qkv.bias"][C:])       # K|V of every row
+    qr = F.linear(xn[rows], ref[a + "qkv.weight"][:C], ref[a + "qkv.bias"][:C])  # Q of the sampled rows
+    heads = lambda t: t.reshape(1, -1, H, D).transpose(1, 2)  # noqa: E731  [1, H, n, D]
+    q = O.layer_norm(heads(qr), ref[a + "q_norm.weight"], ref[a + "q_norm.bias"], 1e-5)
+    k = O.layer_norm(heads(kv[:, :C]), ref[a + "k_norm.weight"], ref[a + "k_norm.bias"], 1e-5)
+    q = O.rope2d(q, pos[:, rows], 100.0)
+    k = O.rope2d(k, pos, 100.0)
+    o = F.scaled_dot_product_attention(q, k, heads(kv[:, C:]))
+    o = o.transpose(1, 2).reshape(len(rows), C)
+    x1 = xr[rows] + F.linear(o, ref[a + "proj.weight"], ref[a + "proj.bias"]) * ref["ls1.gamma"]
+    y = x1 + O.mlp(ref, "mlp.", O.layer_norm(x1, ref["norm2.weight"], ref["norm2.bias"], 1e-5)) * ref["ls2.gamma"]
+    (y * w).sum().backward()
+    assert rel(xd[rows.to(DEV)], y.detach()) < 1e-2  # forward output
+    others = torch.tensor(sorted(set(torch.randperm(L, generator=g)[:1100].tolist()) - set(rows.tolist()))[:1024])
+    assert rel(dx[rows.to(DEV)], xr.grad[rows]) < 3e-2, "input grad (sampled rows)"
+    assert float(xr.grad[others].norm()) > 0
+    assert rel(dx[others.to(DEV)], xr.grad[others]) < 3e-2, "input grad through dK / dV"
+    for n, p in blk.named_parameters():
+        assert rel(p.grad, ref[n].grad) < 3e-2, n

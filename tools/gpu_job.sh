@@ -23,6 +23,8 @@ for step in "$@"; do
     newtests) run newtests 900 python -u -m pytest tests/test_baseline_shapes_gpu.py tests/test_layers_gpu.py \
                 tests/test_demo_entry_gpu.py tests/test_parity_gpu.py tests/test_train_graph_gpu.py -x -v -m gpu \
                 --timeout 600 --timeout-method thread ;;
+    disttests) run disttests 900 python -u -m pytest tests/test_dist_gpu.py tests/test_baseline_shapes_gpu.py -x -v -m gpu \
+                --timeout 600 --timeout-method thread ;;
     gemm_tests) run gemm_tests 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k gemm ;;
     attn_tests) run attn_tests 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k attention ;;
     attn_tests1) run attn_tests1 300 env SR_ATTN_CFG=1 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k attention ;;
