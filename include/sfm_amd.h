@@ -152,6 +152,10 @@ typedef struct sr_attn_desc {
                   query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^100 of its first
                   tile's max runs the sweep with a FIXED softmax offset (no per-tile row max,
                   no rescale; every P <= 2^50, no overflow, same precision); NULL = per-tile max */
+  float key_norm_max; /* optional (bf16 path): > 0 = a static upper bound of |k| (2-norm per head)
+                  for every key, used INSTEAD of key_bound (no key scan).  For keys that come out of
+                  the qk LayerNorm (attention.py:49-50,78) and RoPE (a rotation), |k| <=
+                  sqrt(head_dim) max|w| + |b| of the k_norm affine; 0 = unset */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */

@@ -190,12 +190,15 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   // relative precision at any magnitude, O and l are fp32: the result equals the per-tile-max
   // sweep's up to rounding.
   float qb[QB];
-  const bool use_bound = d.key_bound != nullptr;
+  const bool use_bound = d.key_bound != nullptr || d.key_norm_max > 0.f;
   if (use_bound) {
-    float kn2 = d.key_bound[(d.k0_bstride == 0 ? 0 : item) * d.heads + head];
-    if (args.ntile1 > 0)
-      kn2 = fmaxf(kn2, d.key_bound[(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head]);
-    const float kn = sqrtf(kn2);
+    float kn = d.key_norm_max;
+    if (!(kn > 0.f)) {
+      float kn2 = d.key_bound[(d.k0_bstride == 0 ? 0 : item) * d.heads + head];
+      if (args.ntile1 > 0)
+        kn2 = fmaxf(kn2, d.key_bound[(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head]);
+      kn = sqrtf(kn2);
+    }
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       float ss = 0.f;
@@ -987,7 +990,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
       return e ? atoi(e) : 1;
     }();
     a.allow_mzero = allow_mz;
-    if (d.key_bound) {
+    if (d.key_bound && !(d.key_norm_max > 0.f)) {
       SR_CHECK(d.heads <= 32 && ((uintptr_t)d.key_bound & 3) == 0, SR_EINVAL, "sr_attention: key_bound needs heads <= 32");
       SR_CHECK(hipMemsetAsync(d.key_bound, 0, sizeof(float) * n_inst * d.heads, s) == hipSuccess, SR_ELAUNCH,
                "sr_attention: key_bound memset");

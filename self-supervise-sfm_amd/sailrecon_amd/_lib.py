@@ -55,6 +55,7 @@ class AttnDesc(ctypes.Structure):
         ("scale", _f32),
         ("lse", _vp),
         ("key_bound", _vp),
+        ("key_norm_max", _f32),
     ]
 
 

@@ -449,7 +449,8 @@ class Aggregator(nn.Module):
             def attend_cached(qkv, o, kv=kv, pr=pr):
                 ops.attention(qkv[:, 0:C], kv[:, 0:C], kv[:, C:2 * C], o, heads=pr.heads, head_dim=pr.head_dim,
                               batch=F_, lq=P, q_bstride=P, l0=n_sub, k0_bstride=0, k1=qkv[:, C:2 * C],
-                              v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
+                              v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
+                              key_norm_max=runtime.key_norm_bound(pr))
             runtime.run_block(pr, x, 0, R, sc, attend_cached, runtime.qkv_params(pr, rope, pos_row_base=0, **posctx))
             if l in out_maps:
                 ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, C:], x, R)
@@ -514,7 +515,8 @@ class Aggregator(nn.Module):
                 _wait(work_sub)
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
-                              k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc")
+                              k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
+                              key_norm_max=runtime.key_norm_bound(pr))
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
                 with torch.cuda.stream(side):
@@ -557,15 +559,16 @@ class Aggregator(nn.Module):
         lse_loc = ws.get("lse_loc", H, lq, torch.float32, q.device)
         lse_rem = ws.get("lse_rem", H, lq, torch.float32, q.device)
         o_rem = ws.get("o_rem", lq, C, o.dtype, q.device)
+        kb = runtime.key_norm_bound(pg)
         ops.attention(q, kv_loc[:, 0:C], kv_loc[:, C:2 * C], o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0,
-                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc)
+                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc, key_norm_max=kb)
         _wait(work_kv)
         segs = [(a, n) for a, n in ((0, off), (off + lq, lk - off - lq)) if n > 0]
         (s0, n0), (s1, n1) = segs[0], (segs[1] if len(segs) > 1 else (0, 0))
         ops.attention(q, kv_all[s0:s0 + n0, 0:C], kv_all[s0:s0 + n0, C:2 * C], o_rem, heads=H, head_dim=D, batch=1,
                       lq=lq, q_bstride=0, l0=n0, k0_bstride=0, k1=kv_all[s1:s1 + n1, 0:C] if n1 else None,
                       v1=kv_all[s1:s1 + n1, C:2 * C] if n1 else None, l1=n1, k1_bstride=0, tag="attn_global",
-                      lse=lse_rem)
+                      lse=lse_rem, key_norm_max=kb)
         ops.attn_merge(o, lse_loc, o_rem, lse_rem, o, heads=H, head_dim=D, tag="attn_merge")
 
     def _global_attention(self, q, k, v, o, pg, lq, lk):
@@ -576,7 +579,7 @@ class Aggregator(nn.Module):
                               tag="attn_global", ws=self._fp8_ws, fp8_v=self.fp8_v)
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
-                          k0_bstride=0, tag="attn_global")
+                          k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg))
 
     def _side_stream(self, dev):
         """Second HIP stream for the concurrent reloc block (opt-in: SR_CONCURRENT_STACKS=1)."""

@@ -207,13 +207,18 @@ _ATTN_BOUND = os.environ.get("SR_ATTN_BOUND", "1") != "0"
 def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
-              scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None) -> None:
+              scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
+              key_norm_max: float = 0.0) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``lse``
-    (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd."""
+    (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd.
+    ``key_norm_max`` > 0: a static bound of every key's per-head 2-norm (runtime.key_norm_bound),
+    which replaces the key scan of the fixed-offset sweep."""
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
                    n_anchor=n_anchor, scale=scale, lse=lse)
-    if q.dtype == torch.bfloat16 and _ATTN_BOUND:
+    if q.dtype == torch.bfloat16 and _ATTN_BOUND and key_norm_max > 0.0:
+        d.key_norm_max = float(key_norm_max)
+    elif q.dtype == torch.bfloat16 and _ATTN_BOUND:
         nb = _lib.load().sr_attention_bound_floats(ctypes.byref(d))
         if nb > 0:
             d.key_bound = _p(_train_ws(q.device, "attn_key_bound", nb))

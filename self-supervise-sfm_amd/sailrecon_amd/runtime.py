@@ -73,6 +73,22 @@ class PackedBlock:
     w_fc2: Tensor
     b_fc2: Optional[Tensor]
     g2: Tensor
+    k_bound: float = -1.0  # key_norm_bound cache (-1: not computed yet)
+
+
+def key_norm_bound(pb: PackedBlock) -> float:
+    """Static bound of every key's per-head 2-norm for a qk-norm block (attention.py:49-50,78):
+    k = LN(x) * w + b with |LN(x)| <= sqrt(head_dim), then RoPE (a rotation), so
+    |k| <= sqrt(head_dim) max|w| + |b|; x (1 + 2^-6) covers the bf16 rounding of k.  0 without
+    qk-norm (the attention then scans the keys).  One host read per packing, cached."""
+    if pb.k_bound < 0.0:
+        if not pb.qk_norm or pb.kn_w is None:
+            pb.k_bound = 0.0
+        else:
+            w = float(pb.kn_w.abs().max())
+            b = float(pb.kn_b.norm()) if pb.kn_b is not None else 0.0
+            pb.k_bound = (pb.head_dim ** 0.5 * w + b) * (1.0 + 2.0 ** -6)
+    return pb.k_bound
 
 
 def _f32(t: Optional[Tensor]) -> Optional[Tensor]:
@@ -196,8 +212,10 @@ def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
 def frame_attend(pb: PackedBlock, frames: int, tokens: int) -> Callable[[Tensor, Tensor], None]:
     """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C])."""
     C, D = pb.dim, pb.head_dim
+    kb = key_norm_bound(pb)
 
     def attend(qkv: Tensor, o: Tensor) -> None:
         ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads, head_dim=D,
-                      batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_frame")
+                      batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_frame",
+                      key_norm_max=kb)
     return attend

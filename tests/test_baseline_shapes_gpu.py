@@ -92,6 +92,30 @@ def test_global_attention_production(ops, L):
     assert _rel(o[rows].float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("loose", [1.0, 3.0])
+@pytest.mark.parametrize("case", ["global-C3", "frame-C3"])
+def test_attention_static_key_bound(ops, case, loose):
+    """sr_attn_desc.key_norm_max (runtime.key_norm_bound for qk-norm blocks): a static bound of
+    |k| replaces the key scan of the fixed-offset sweep.  Tight (the true max) and 3x loose bounds
+    give the scan's result (same kernel, same arithmetic up to the offset) and match fp64."""
+    frames = 1 if case.startswith("global") else 64
+    L = 32 * P if frames == 1 else P
+    q, k, v = _make(frames * L, 13, spikes=(frames * L - 37, L // 2 + 5))
+    kmax = float(k.float().view(-1, H, D).norm(dim=-1).max()) * 1.01
+    outs = []
+    for kb in (0.0, kmax * loose):
+        o = torch.empty(frames * L, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(q, k, v, o, heads=H, head_dim=D, batch=frames, lq=L, q_bstride=L, l0=L, k0_bstride=L,
+                      key_norm_max=kb)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert _rel(outs[1].float(), outs[0].float()) < 5e-3
+    rows = _sample_rows(L, 128, 7).to(DEV)
+    f = frames - 1  # the last item (spike key 37 rows from its end)
+    ref = _ref_rows(q[f * L + rows], k[f * L:(f + 1) * L], v[f * L:(f + 1) * L], D ** -0.5)
+    assert _rel(outs[1][f * L + rows].float(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("G,r", [(2, 0), (2, 1), (3, 1)], ids=["C3-2rk-r0", "C3-2rk-r1", "C3-3rk-mid"])
 def test_global_attention_sharded_passes(ops, G, r):
     """The frame-sharded global block at C3 (32 anchors): rank r's query rows attend to its own

@@ -42,13 +42,17 @@ def attn():
         "global L=43968": dict(rows=N * P, batch=1, lq=N * P, l0=N * P, kb=0),
         "frame 64x1374": dict(rows=2 * N * P, batch=2 * N, lq=P, l0=P, kb=P),
     }
+    # SR_KB_STATIC=1: pass the keys' true max norm as the static bound (runtime.key_norm_bound's
+    # role for qk-norm blocks) instead of the key scan
+    static = os.environ.get("SR_KB_STATIC", "0") == "1"
     for name, c in cases.items():
         qkv = torch.randn(c["rows"], 3 * C, device=DEV, dtype=torch.bfloat16)
         o = torch.empty(c["rows"], C, device=DEV, dtype=torch.bfloat16)
+        kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max()) if static else 0.0
 
         def f():
             ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=c["batch"],
-                          lq=c["lq"], q_bstride=c["lq"], l0=c["l0"], k0_bstride=c["kb"])
+                          lq=c["lq"], q_bstride=c["lq"], l0=c["l0"], k0_bstride=c["kb"], key_norm_max=kb)
         ms = timeit(f, reps=5 if c["batch"] == 1 else 10)
         fl = 4.0 * c["batch"] * H * c["lq"] * c["l0"] * D
         print(f"attn {name:18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
@@ -57,10 +61,12 @@ def attn():
     qkv = torch.randn(N * P, 3 * C, device=DEV, dtype=torch.bfloat16)
     kv = torch.randn(nsub, 2 * C, device=DEV, dtype=torch.bfloat16)
     o = torch.empty(N * P, C, device=DEV, dtype=torch.bfloat16)
+    kb = max(float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max()),
+             float(kv[:, :C].float().view(-1, H, D).norm(dim=-1).max())) if static else 0.0
 
     def f():
         ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], o, heads=H, head_dim=D, batch=N, lq=P, q_bstride=P, l0=nsub,
-                      k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P)
+                      k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P, key_norm_max=kb)
     ms = timeit(f)
     fl = 4.0 * N * H * P * (nsub + P) * D
     print(f"attn {'reloc 32x(9760+1374)':18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
