@@ -220,6 +220,22 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   bf16x8 one_a;
 #pragma unroll
   for (int j = 0; j < 8; ++j) one_a[j] = (bf16)((hi == 0 && j < 2) ? 1.f : 0.f);
+#ifndef SR_ABL_VSUM
+  // Row sums of P on the matrix pipe: one v_mfma_f32_16x16x32_bf16 per 16-key P fragment with
+  // A = ones in row 0 at k-slots {0-7, 16-23} and row 1 at {8-15, 24-31}, so that with P's
+  // fragment as B (lane l: 8 keys of query l % 32) D[0][n] sums query n and D[1][n] query n + 16.
+  // 4 MFMAs (64 pipe cycles, 32 issue) replace 32 v_add_f32 (128 issue cycles) per q-block and
+  // tile in a VALU-issue-bound loop (global / reloc +3 %).  The sum runs over the bf16-rounded P
+  // that the P.V product uses, so numerator and denominator see the same P (SR_ABL_VSUM: the
+  // fp32 VALU sums)
+  bf16x8 sum_a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    sum_a[j] = (bf16)(((lane == 0 || lane == 32) || (lane == 17 || lane == 49)) ? 1.f : 0.f);
+  f32x4 lacc[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) lacc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#endif
   float m_run[QB], l_run[QB];  // m_run == float(m_hi) + float(m_lo); l_run: this lane's partial sums
   bf16x8 m_b[QB];
   f32x16 o[QB][2];
@@ -340,6 +356,13 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
           const float delta = m_new - m_run[b];  // S' relative to the new max: S' - delta
           const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
           l_run[b] *= alpha;
+#ifndef SR_ABL_VSUM
+          {  // lacc rows 0 / 1 of lane n hold queries n / n + 16: their alphas
+            const float a0 = __shfl(alpha, lane & 15), a1 = __shfl(alpha, (lane & 15) + 16);
+            lacc[b][0] *= a0;
+            lacc[b][1] *= a1;
+          }
+#endif
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             o[b][0][i] *= alpha;
@@ -376,9 +399,15 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
+#ifdef SR_ABL_VSUM
             ps[b][j & 1] += p;
+#endif
             pf[b][j] = (bf16)p;
           }
+#ifndef SR_ABL_VSUM
+#pragma unroll
+        for (int b = 0; b < QB; ++b) lacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sum_a, pf[b], lacc[b], 0, 0, 0);
+#endif
         const int rowoff = (kb * 32 + 16 * s2) * 128;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -399,7 +428,12 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training)
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
+#ifndef SR_ABL_VSUM
+    const float s0 = __shfl(lacc[b][0], l32 & 15), s1 = __shfl(lacc[b][1], l32 & 15);
+    const float lsum = l32 < 16 ? s0 : s1;
+#else
     const float lsum = sum_x32(l_run[b]);
+#endif
     const float inv = 1.f / lsum;
     const bool wide_o = d.ldo % 8 == 0 && ((uintptr_t)d.o & 15) == 0;
     const int qrow = qrow0 + 32 * b;

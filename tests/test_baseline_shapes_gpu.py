@@ -150,7 +150,8 @@ def test_global_attention_sharded_passes(ops, G, r):
     ref = _ref_rows(qs[rows], k, v, D ** -0.5)
     assert _rel(o[rows].float(), ref) < 1e-2
     assert _rel(o.float(), one.float()) < 1e-2
-    assert float((lse_m - lse_1).abs().max()) < 2e-3
+    # row sums accumulate the bf16-rounded P of the P.V product: ~2^-9 per dominant term
+    assert float((lse_m - lse_1).abs().max()) < 1e-2
 
 
 @pytest.mark.parametrize("alias", [False, True])
