@@ -78,17 +78,32 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   const sr_attn_desc& d = args.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
-  if constexpr (KIND == 1) {
-    // global_reloc: every query frame of a head reads the same anchor-subsample K/V (segment 0,
-    // 2.5 MB per head at C3).  Blocks are dealt round-robin over the 8 XCDs; the bijective remap
-    // hands each XCD a contiguous range of (head, frame, q-tile) in head-major order, so one
-    // head's shared K/V stays in that XCD's L2 while all of its query frames sweep it.
+  {
+    // Blocks are dealt round-robin over the 8 XCDs (each with its own L2); the bijective remap
+    // hands each XCD a contiguous range of tiles instead, so the q-tiles that read the same K/V
+    // run on one XCD:
+    //   global (one item): the 172 q-tiles of a head (C3) sweep its 11 MB K/V together;
+    //   frame: the 6 q-tiles of a (frame, head) share its 350 KB K/V (3.5x -> ~1x HBM traffic);
+    //   global_reloc: head-major, every query frame of a head reads the same anchor-subsample
+    //   K/V (segment 0, 2.5 MB per head at C3).
     const int nq = gridDim.x, nh = gridDim.y, nb = gridDim.z;
     const int lin = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
-    const int tile = sr::xcd_remap(lin, nq * nh * nb);
-    qt = tile % nq;
-    item = (tile / nq) % nb;
-    head = tile / (nq * nb);
+#ifdef SR_ABL_NOREMAP
+    const bool remap = KIND == 1;
+#else
+    const bool remap = true;
+#endif
+    if (remap) {
+      const int tile = sr::xcd_remap(lin, nq * nh * nb);
+      qt = tile % nq;
+      if constexpr (KIND == 1) {
+        item = (tile / nq) % nb;
+        head = tile / (nq * nb);
+      } else {
+        head = (tile / nq) % nh;
+        item = tile / (nq * nh);
+      }
+    }
   }
   const int hcol = head * 64;
   const int l32 = lane & 31, hi = lane >> 5;

@@ -89,6 +89,18 @@ def gemm():
         print(f"gemm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
 
 
+def torch_mm():
+    """Yardstick only (not a product path): the library GEMM (torch.matmul -> hipBLASLt) at the
+    block shapes, plain bf16 output, no epilogue."""
+    M = 2 * 32 * 1374
+    for name, (N, K) in {"qkv": (3072, 1024), "proj": (1024, 1024), "fc1": (4096, 1024), "fc2": (1024, 4096)}.items():
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        wt = (torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / 32).t()
+        ms = timeit(lambda: torch.matmul(a, wt))
+        fl = 2.0 * M * N * K
+        print(f"torch.mm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+
+
 def ln():
     M, C = 2 * 32 * 1374, 1024
     x = torch.randn(M, C, device=DEV)
