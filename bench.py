@@ -100,7 +100,7 @@ KERNEL_OF_TAG = {
     "attn_frame": "attn_bf16_kernel<4, 2, 0>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
     "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
 }
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
 
 
 def pmc_traffic(kernel: str, views: int, img: int):

@@ -32,6 +32,9 @@ for step in "$@"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py ;;
     benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench_c2) run bench_c2 400 python bench.py --views 8 --no-cpu-baseline ;;
+    bench_c5) run bench_c5 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench_c5q) run bench_c5q 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline --fp8-global qkv ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
     kgemm)   run kgemm 300 python tools/kbench.py gemm ln ;;
     kgemm_reg) run kgemm_reg 300 env SR_GEMM_REG_EPI=1 python tools/kbench.py gemm ;;
