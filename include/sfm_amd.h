@@ -443,6 +443,17 @@ int sr_pose_decode_f32(sr_stream_t stream, const float* enc, int64_t ld_enc, int
  * (ResidualConvUnit, dpt_head.py:470-476).  ho = (h-1)/stride + 1. */
 int sr_im2col3x3_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int stride, int relu_in,
                      float* out);
+/* Implicit-GEMM 3x3 / pad 1 / stride 1|2 conv, fp32 (every 3x3 conv of the DPT heads:
+ * layer{1-4}_rn, resize_layers[3], the ResidualConvUnits, output_conv1, output_conv2[0];
+ * dpt_head.py:79-108,470-565): out[n*ho*wo][cout] (row stride ldo) = epilogue(im2col(x) . wgt^T)
+ * without materialising im2col — the GEMM's LDS-DMA gathers each 32-channel slice of a tap
+ * straight from the NHWC input, out-of-image taps from `zero` (>= 128 zero bytes, 16-B aligned,
+ * caller-owned).  wgt [cout][9c] with K ordered (ky, kx, ci); relu_in applies ReLU to the input
+ * (ResidualConvUnit, dpt_head.py:470-476); epilogue SR_EPI_BIAS (out = acc + bias) or
+ * SR_EPI_BIAS_RESID (out += gamma * (acc + bias)).  c % 32 == 0, cout % 4 == 0. */
+int sr_conv3x3_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int stride, int relu_in,
+                   const float* wgt, int cout, int epilogue, const sr_gemm_epi* ep, float* out, int64_t ldo,
+                   const float* zero);
 /* ConvTranspose2d(kernel = stride = k, pad 0) scatter: g[n*h*w][(ky*k+kx)*co + c] (+ bias[c])
  * -> out[n][h*k][w*k][co]  (dpt_head.py:89-104). */
 int sr_convt_scatter_f32(sr_stream_t stream, const float* g, int n, int h, int w, int k, int co, const float* bias,

@@ -41,6 +41,14 @@ struct GemmArgs {
   int kt_per_split;  // split-K (gemm_kernel, gridDim.y slices): k-tiles per slice
   float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
   sr_gemm_epi ep;
+  // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
+  // (n, yo, xo) of the NHWC fp32 input x [n][H][W][C], A column k = (ky, kx, ci) — exactly
+  // the im2col row, gathered by the LDS-DMA itself (out-of-image taps read `zero`)
+  struct {
+    const char* x;
+    const char* zero;  // >= 128 bytes of zeros
+    int H, W, C, Ho, Wo, stride, relu;
+  } conv;
 };
 
 template <typename T> struct Mma;
@@ -400,7 +408,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4
   }
 }
 
-template <typename T, int EPI>
+template <typename T, int EPI, bool CONV = false>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -411,13 +419,25 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
 
   // LDS-DMA sources: instruction i of wave w fills tile rows (w*8+i)*8 .. +8 (rows < BM: A, else W).
   const char* src[8];
+  // CONV: A rows come from the 3x3 window of output pixel m (waves 0-1 stage A, 2-3 stage W)
+  const bool a_wave = __builtin_amdgcn_readfirstlane(wave) < 2;
+  int cy[8], cx[8];  // CONV: window top-left (yo*s - 1, xo*s - 1) of this lane's pixel per piece
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int tr = (wave * 8 + i) * 8 + (lane >> 3);
     const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
     if (tr < BM) {
       const int r = min(m0 + tr, g.M - 1);
-      src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
+      if constexpr (CONV) {
+        const int hw = g.conv.Ho * g.conv.Wo;
+        const int n = r / hw, rem = r - n * hw, yo = rem / g.conv.Wo, xo = rem - yo * g.conv.Wo;
+        cy[i] = yo * g.conv.stride - 1;
+        cx[i] = xo * g.conv.stride - 1;
+        // pixel (n, cy, cx) of x, + this lane's 16-B chunk (may point before x: used only in-image)
+        src[i] = g.conv.x + ((((int64_t)n * g.conv.H + cy[i]) * g.conv.W + cx[i]) * g.conv.C) * 4 + chunk * 16;
+      } else {
+        src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
+      }
     } else {
       const int r = min(n0 + tr - BM, g.N - 1);  // ragged last column tile: re-read the last W row
       src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
@@ -426,8 +446,21 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
   auto stage = [&](int kt, int buf) {
     const uint32_t base = dst0 + buf * STAGE_BYTES;
+    if (CONV && a_wave) {
+      // k-tile kt = 32 channels [ci0, ci0 + 32) of tap (ky, kx): C % 32 == 0, no tile straddles taps
+      const int k0 = kt * 32, tap = k0 / g.conv.C, ci0 = k0 - tap * g.conv.C;
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const int64_t off = ((int64_t)ky * g.conv.W + kx) * g.conv.C * 4 + (int64_t)ci0 * 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+      for (int i = 0; i < 8; ++i) {
+        const int yy = cy[i] + ky, xx = cx[i] + kx;
+        const bool in = (unsigned)yy < (unsigned)g.conv.H && (unsigned)xx < (unsigned)g.conv.W;
+        sr::dma16(in ? src[i] + off : g.conv.zero + (lane & 7) * 16, base + i * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+    }
   };
 
   const int wr = wave >> 1, wc = wave & 1;
@@ -461,6 +494,17 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
       for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + (wr * 64 + mi * 16 + lr) * ROWB + coff);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) b[ni] = *(const uint4*)(sb + (BM + wc * 64 + ni * 16 + lr) * ROWB + coff);
+      if constexpr (CONV) {
+        if (g.conv.relu) {  // the RCU's ReLU on the conv input (zero padding stays zero)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            f32x4 v = __builtin_bit_cast(f32x4, a[mi]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+            a[mi] = __builtin_bit_cast(uint4, v);
+          }
+        }
+      }
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -709,6 +753,13 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
   return SR_EINVAL;
 }
 
+template <int EPI>
+int launch_conv(const GemmArgs& a, hipStream_t s) {
+  const int nwg = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_kernel<float, EPI, true>), dim3(nwg), dim3(NTHREADS), 0, s, a);
+  return sr::check_launch("sr_conv3x3_f32");
+}
+
 }  // namespace
 
 static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
@@ -742,7 +793,7 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
                    (ep->pos_yx || (ep->tokens_per_frame > ep->patch_start && ep->grid_w > 0)),
                SR_EINVAL, "sr_gemm: QKV rope params");
   }
-  GemmArgs a;
+  GemmArgs a{};
   a.A = (const char*)A;
   a.lda_b = lda * esz;
   a.W = (const char*)W;
@@ -792,4 +843,45 @@ extern "C" int sr_gemm_splitk(sr_stream_t stream, int dtype, int epi, const void
                               const sr_gemm_epi* ep) {
   SR_CHECK(splits >= 1, SR_EINVAL, "sr_gemm_splitk: splits=%d", splits);
   return gemm_common(stream, dtype, epi, A, lda, W, ldw, out, ldo, M, N, K, splits, workspace, ep);
+}
+
+extern "C" int sr_conv3x3_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int stride, int relu_in,
+                              const float* wgt, int cout, int epi, const sr_gemm_epi* ep, float* out, int64_t ldo,
+                              const float* zero) {
+  SR_CHECK(x && wgt && out && ep && zero, SR_EINVAL, "sr_conv3x3_f32: null pointer");
+  SR_CHECK(n > 0 && h > 0 && w > 0 && c > 0 && c % 32 == 0 && (stride == 1 || stride == 2), SR_EUNSUPPORTED,
+           "sr_conv3x3_f32: needs C %% 32 == 0 and stride 1 | 2 (n=%d h=%d w=%d c=%d stride=%d)", n, h, w, c, stride);
+  SR_CHECK(cout > 0 && cout % 4 == 0 && ldo >= cout && ldo % 4 == 0, SR_EINVAL, "sr_conv3x3_f32: bad cout / ldo");
+  SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_RESID, SR_EUNSUPPORTED, "sr_conv3x3_f32: epilogue %d", epi);
+  if (epi == SR_EPI_BIAS_RESID) SR_CHECK(ep->gamma, SR_EINVAL, "sr_conv3x3_f32: RESID needs gamma");
+  SR_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)wgt % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+               ((uintptr_t)zero % 16) == 0, SR_EINVAL, "sr_conv3x3_f32: pointers must be 16-B aligned");
+  const int ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  SR_CHECK((int64_t)n * ho * wo < (1ll << 31), SR_EINVAL, "sr_conv3x3_f32: too many output pixels");
+  GemmArgs a{};
+  a.A = nullptr;
+  a.lda_b = 0;
+  a.W = (const char*)wgt;
+  a.ldw_b = (int64_t)9 * c * 4;
+  a.out = out;
+  a.ldo = ldo;
+  a.M = n * ho * wo;
+  a.N = cout;
+  a.K = 9 * c;
+  a.ktiles = a.K / Mma<float>::KT;
+  a.lds_epi = 0;
+  a.kt_per_split = a.ktiles;
+  a.partial = nullptr;
+  a.ep = *ep;
+  a.conv.x = (const char*)x;
+  a.conv.zero = (const char*)zero;
+  a.conv.H = h;
+  a.conv.W = w;
+  a.conv.C = c;
+  a.conv.Ho = ho;
+  a.conv.Wo = wo;
+  a.conv.stride = stride;
+  a.conv.relu = relu_in;
+  hipStream_t s = (hipStream_t)stream;
+  return epi == SR_EPI_BIAS ? launch_conv<SR_EPI_BIAS>(a, s) : launch_conv<SR_EPI_BIAS_RESID>(a, s);
 }

@@ -96,6 +96,8 @@ _PROTOS = {
     "sr_attention_qkv8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp, _vp]),
     "sr_attention_bwd": (_i32, [_vp, ctypes.POINTER(AttnBwdDesc)]),
     "sr_im2col3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "sr_conv3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _i32,
+                              ctypes.POINTER(GemmEpi), _vp, _i64, _vp]),
     "sr_convt_scatter_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "sr_resize_bilinear_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "sr_add_f32": (_i32, [_vp, _vp, _vp, _i64]),

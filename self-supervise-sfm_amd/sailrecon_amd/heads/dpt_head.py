@@ -29,7 +29,8 @@ from .. import _lib, ops, runtime
 
 Tensor = torch.Tensor
 
-IM2COL_BUDGET = 2 << 30  # bytes: largest im2col buffer per chunk
+IM2COL_BUDGET = 2 << 30  # bytes: largest im2col buffer per chunk (convs with C % 32 != 0 only)
+ACT_BUDGET = 16 << 30    # bytes: activations of one chunk of frames (implicit-GEMM convs)
 
 
 class ResidualConvUnit(nn.Module):
@@ -147,9 +148,19 @@ class DPTHead(nn.Module):
 
     def _conv3x3(self, x: Tensor, name: str, conv: nn.Conv2d, stride: int = 1, relu_in: bool = False,
                  out: Tensor = None, resid: bool = False) -> Tensor:
-        """3x3 / pad 1 conv of NHWC x; resid: out += conv(x) (+ bias) instead of out = ..."""
+        """3x3 / pad 1 conv of NHWC x; resid: out += conv(x) (+ bias) instead of out = ...
+        C % 32 == 0 (every conv of the default heads): implicit GEMM (sr_conv3x3_f32, nothing
+        materialised); otherwise im2col + GEMM."""
         n, h, w, c = x.shape
         ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+        cout = conv.weight.shape[0]
+        if c % 32 == 0 and cout % 4 == 0:
+            if out is None:
+                out = torch.empty(n, ho, wo, cout, device=x.device, dtype=torch.float32)
+            bias = None if conv.bias is None else self._pk(name + ".bias", lambda: conv.bias)
+            ops.conv3x3(x, self._conv_w(name, conv), out, stride=stride, relu_in=relu_in, bias=bias,
+                        resid_gamma=self._ones_for(cout, x.device) if resid else None, tag="dpt_conv3x3")
+            return out
         cols = torch.empty(n * ho * wo, 9 * c, device=x.device, dtype=torch.float32)
         ops.im2col3x3(x, stride, relu_in, cols)
         cout = conv.weight.shape[0]
@@ -206,9 +217,17 @@ class DPTHead(nn.Module):
         preds = torch.empty(B, S, H, W, self.output_dim - 1, device=dev, dtype=torch.float32)
         conf = torch.empty(B, S, H, W, device=dev, dtype=torch.float32)
         oh, ow = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
-        per_frame = max(oh * ow * 9 * (self.scratch.output_conv1.weight.shape[0]) * 4,
-                        (4 * ph) * (4 * pw) * 9 * self.scratch.layer1_rn.weight.shape[1] * 4)
-        chunk = max(1, min(frames, IM2COL_BUDGET // per_frame))
+        f = self.scratch.layer1_rn.weight.shape[0]  # features
+        convs3 = [m for m in self.modules() if isinstance(m, nn.Conv2d) and m.kernel_size == (3, 3)]
+        if all(m.in_channels % 32 == 0 and m.out_channels % 4 == 0 for m in convs3):
+            # implicit-GEMM convs: the chunk is bounded by its activations (largest: the upsampled
+            # output_conv1 map + output_conv2's hidden map at oh x ow, the refinenet1 maps at 8x)
+            per_frame = oh * ow * (f // 2 + 2 * (f // 8)) * 4 + (8 * ph) * (8 * pw) * f * 4 * 3
+            chunk = max(1, min(frames, ACT_BUDGET // per_frame))
+        else:
+            per_frame = max(oh * ow * 9 * (self.scratch.output_conv1.weight.shape[0]) * 4,
+                            (4 * ph) * (4 * pw) * 9 * self.scratch.layer1_rn.weight.shape[1] * 4)
+            chunk = max(1, min(frames, IM2COL_BUDGET // per_frame))
         toks = []
         for layer_idx in self.intermediate_layer_idx:
             t = aggregated_tokens_list[layer_idx]

@@ -486,6 +486,36 @@ def im2col3x3(x: Tensor, stride: int, relu_in: bool, out: Tensor) -> None:
           "sr_im2col3x3_f32")
 
 
+_ZERO128 = {}
+
+
+def conv3x3(x: Tensor, w: Tensor, out: Tensor, *, stride: int = 1, relu_in: bool = False,
+            bias: Optional[Tensor] = None, resid_gamma: Optional[Tensor] = None, tag: Optional[str] = None) -> None:
+    """Implicit-GEMM 3x3 / pad 1 conv of NHWC fp32 x [n,h,w,c] with w [cout, 9c] (K order ky, kx,
+    ci) into out [n,ho,wo,cout] (sr_conv3x3_f32): out = conv + bias, or out += gamma * (conv +
+    bias) when ``resid_gamma`` is given."""
+    n, h, wd, c = _nhwc(x, "conv3x3 x")
+    cout = w.shape[0]
+    ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+    if w.dtype != torch.float32 or not w.is_contiguous() or w.shape[1] != 9 * c:
+        raise ValueError("conv3x3: w must be contiguous fp32 [cout, 9*c]")
+    if out.dtype != torch.float32 or not out.is_contiguous() or tuple(out.shape) != (n, ho, wo, cout):
+        raise ValueError(f"conv3x3: out must be contiguous fp32 [{n}, {ho}, {wo}, {cout}]")
+    z = _ZERO128.get(x.device)
+    if z is None:
+        z = _ZERO128[x.device] = torch.zeros(32, device=x.device, dtype=torch.float32)
+    ep = GemmEpi()
+    ep.bias = _p(bias)
+    ep.gamma = _p(resid_gamma)
+    epi = _lib.SR_EPI_BIAS if resid_gamma is None else _lib.SR_EPI_BIAS_RESID
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    check(_lib.load().sr_conv3x3_f32(_stream(x), _p(x), n, h, wd, c, stride, int(relu_in), _p(w), cout, epi,
+                                     ctypes.byref(ep), _p(out), cout, _p(z)), "sr_conv3x3_f32")
+    if timed:
+        TIMER.stop(tag, ev0, 2.0 * n * ho * wo * cout * 9 * c, 4.0 * (x.numel() + w.numel() + out.numel()))
+
+
 def convt_scatter(g: Tensor, n: int, h: int, w: int, k: int, co: int, bias: Optional[Tensor], out: Tensor) -> None:
     _nhwc(out, "convt_scatter out")
     check(_lib.load().sr_convt_scatter_f32(_stream(g), _p(g), n, h, w, k, co, _p(bias), _p(out)),

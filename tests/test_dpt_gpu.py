@@ -92,3 +92,35 @@ def test_sailrecon_with_heads_end_to_end():
         gotc = torch.stack([r[ckey][0] for r in res]).cpu()
         assert rel_l2(got.numpy(), p_ref[0].numpy()) < TOL, kind
         assert rel_l2(gotc.numpy(), c_ref[0].numpy()) < TOL, kind
+
+
+@pytest.mark.parametrize("n,h,w,c,cout,stride,relu,resid", [
+    (2, 19, 23, 64, 32, 1, False, False),
+    (1, 37, 37, 128, 64, 2, False, False),     # resize_layers[3] shape class: 3x3 stride 2
+    (2, 15, 11, 32, 36, 1, True, True),        # ResidualConvUnit conv2: ReLU on the input, += residual
+    (1, 9, 130, 256, 4, 1, True, False),       # one image row spans several 128-pixel tiles
+])
+def test_conv3x3_implicit_gemm(n, h, w, c, cout, stride, relu, resid):
+    """sr_conv3x3_f32 (implicit GEMM, the LDS-DMA gathers each tap's channel slice from the NHWC
+    input, zero padding from a zero buffer) against fp64 F.conv2d; exact fp32 MFMA -> 1e-5."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.nn.functional as F
+    from sailrecon_amd import ops
+    g = torch.Generator().manual_seed(n * 1000 + c)
+    x = torch.randn(n, h, w, c, generator=g)
+    wt = torch.randn(cout, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    b = torch.randn(cout, generator=g)
+    xin = x.clamp_min(0) if relu else x
+    ref = F.conv2d(xin.permute(0, 3, 1, 2).double(), wt.double(), b.double(), stride=stride, padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    ho, wo = ref.shape[1:3]
+    base = torch.randn(n, ho, wo, cout, generator=g)
+    if resid:
+        ref = ref + base.double()
+    out = base.clone().cuda() if resid else torch.empty(n, ho, wo, cout, device="cuda")
+    wk = wt.permute(0, 2, 3, 1).reshape(cout, 9 * c).contiguous().cuda()
+    ops.conv3x3(x.cuda(), wk, out, stride=stride, relu_in=relu, bias=b.cuda(),
+                resid_gamma=torch.ones(cout, device="cuda") if resid else None)
+    torch.cuda.synchronize()
+    assert rel_l2(out.cpu().numpy(), ref.numpy()) < 1e-5

@@ -89,6 +89,19 @@ def gemm():
         print(f"gemm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
 
 
+def gemm_f32():
+    """The exact-fp32 GEMM at DPT conv shapes (im2col'd 3x3 convs, 8 frames per chunk)."""
+    for name, (M, N, K) in {"rn1 3x3 256->256 @148": (8 * 148 * 148, 256, 2304),
+                            "out1 3x3 256->128 @296": (8 * 296 * 296, 128, 2304),
+                            "out2 3x3 128->32 @518": (8 * 518 * 518, 32, 1152)}.items():
+        a = torch.randn(M, K, device=DEV)
+        w = torch.randn(N, K, device=DEV) / 32
+        out = torch.empty(M, N, device=DEV)
+        ms = timeit(lambda: ops.gemm(a, w, out, _lib.SR_EPI_BIAS, splits=1), reps=3)
+        fl = 2.0 * M * N * K
+        print(f"gemm_f32 {name:24s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:7.1f} TF/s  {fl / ms / 1e9 / 157.3:6.1%}")
+
+
 def torch_mm():
     """Yardstick only (not a product path): the library GEMM (torch.matmul -> hipBLASLt) at the
     block shapes, plain bf16 output, no epilogue."""
