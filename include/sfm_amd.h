@@ -459,7 +459,9 @@ int sr_conv3x3_f32(sr_stream_t stream, const float* x, int n, int h, int w, int 
 int sr_convt_scatter_f32(sr_stream_t stream, const float* g, int n, int h, int w, int k, int co, const float* bias,
                          float* out);
 /* Bilinear resize, align_corners=True (custom_interpolate, dpt_head.py:568-598), plus an
- * optional same-shape `add` (NULL = none).  out must not alias x. */
+ * optional `add` table [ho][wo][c] added to every frame (NULL = none): the DPT positional
+ * embedding of the upsampled map (dpt_head.py:263-266) fused into the resize.  out must not
+ * alias x. */
 int sr_resize_bilinear_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int ho, int wo,
                            const float* add, float* out);
 /* dst += src over n floats (n % 4 == 0): skip_add of FeatureFusionBlock (dpt_head.py:540-545). */

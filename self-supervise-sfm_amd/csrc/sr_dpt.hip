@@ -103,8 +103,8 @@ __global__ void resize_bilinear_kernel(const float* __restrict__ x, int n, int h
     v.y = ly0 * (lx0 * a.y + lx1 * b.y) + ly1 * (lx0 * cc.y + lx1 * d.y);
     v.z = ly0 * (lx0 * a.z + lx1 * b.z) + ly1 * (lx0 * cc.z + lx1 * d.z);
     v.w = ly0 * (lx0 * a.w + lx1 * b.w) + ly1 * (lx0 * cc.w + lx1 * d.w);
-    if (add) {
-      const float4 q = *(const float4*)(add + p * c + cq * 4);
+    if (add) {  // one [ho][wo][c] table for every frame
+      const float4 q = *(const float4*)(add + (p - (int64_t)f * ho * wo) * c + cq * 4);
       v.x += q.x;
       v.y += q.y;
       v.z += q.z;

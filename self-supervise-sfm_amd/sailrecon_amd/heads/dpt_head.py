@@ -133,6 +133,18 @@ class DPTHead(nn.Module):
         """[Cin, Cout, k, k] -> GEMM weight [(ky, kx, co), Cin]."""
         return self._pk(name, lambda: conv.weight.permute(2, 3, 1, 0).reshape(-1, conv.weight.shape[0]))
 
+    def _pos_table(self, h: int, w: int, c: int, aspect: float, device) -> Tensor:
+        """The positional embedding ratio * sincos(uv grid) (dpt_head.py:300-315) of one [h, w, c]
+        map: identical for every frame, so it is computed once per shape (the same kernel on a
+        zero map) and added by the producing op's epilogue."""
+        key = ("pos", h, w, c, float(aspect), str(device))
+        t = self._packed.get(key)
+        if t is None:
+            t = torch.zeros(1, h, w, c, device=device, dtype=torch.float32)
+            ops.dpt_pos_embed_(t, aspect, 0.1)
+            self._packed[key] = t
+        return t
+
     def _ones_for(self, c: int, device) -> Tensor:
         t = self._ones.get(c)
         if t is None or t.device != device:
@@ -259,9 +271,14 @@ class DPTHead(nn.Module):
             proj = self.projects[i]
             oc = proj.weight.shape[0]
             y = torch.empty(F_, ph, pw, oc, device=dev, dtype=torch.float32)
-            self._gemm(xn, self._conv_w(f"projects.{i}", proj), proj.bias, y.view(-1, oc))
-            if self.pos_embed:
-                ops.dpt_pos_embed_(y, aspect, 0.1)
+            if self.pos_embed:  # projection + bias + the per-frame positional table in one epilogue
+                ops.gemm(xn, self._conv_w(f"projects.{i}", proj), y.view(-1, oc), _lib.SR_EPI_PATCH,
+                         bias=self._pk(f"projects.{i}.bias", lambda: proj.bias),
+                         patch=dict(seg_rows=n_patch, seg_stride=n_patch, seg_offset=0,
+                                    row_add=self._pos_table(ph, pw, oc, aspect, dev).view(n_patch, oc)),
+                         splits=1)
+            else:
+                self._gemm(xn, self._conv_w(f"projects.{i}", proj), proj.bias, y.view(-1, oc))
             layer = self.resize_layers[i]
             if isinstance(layer, nn.ConvTranspose2d):
                 k = layer.kernel_size[0]
@@ -282,9 +299,7 @@ class DPTHead(nn.Module):
         out = self._fusion("scratch.refinenet1", sc.refinenet1, out, l1)
         out = self._conv3x3(out, "scratch.output_conv1", sc.output_conv1)
         up = torch.empty(F_, oh, ow, out.shape[3], device=dev, dtype=torch.float32)
-        ops.resize_bilinear(out, up)
-        if self.pos_embed:
-            ops.dpt_pos_embed_(up, aspect, 0.1)
+        ops.resize_bilinear(out, up, add=self._pos_table(oh, ow, out.shape[3], aspect, dev) if self.pos_embed else None)
         c0, c2 = sc.output_conv2[0], sc.output_conv2[2]
         hidden = self._conv3x3(up, "scratch.output_conv2.0", c0)
         ops.dpt_head_out(hidden.view(-1, hidden.shape[3]), self._conv_w("scratch.output_conv2.2", c2),

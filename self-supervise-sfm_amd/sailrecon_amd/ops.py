@@ -523,11 +523,12 @@ def convt_scatter(g: Tensor, n: int, h: int, w: int, k: int, co: int, bias: Opti
 
 
 def resize_bilinear(x: Tensor, out: Tensor, add: Optional[Tensor] = None) -> None:
-    """out = interpolate(x, out's size, bilinear, align_corners=True) (+ add)."""
+    """out = interpolate(x, out's size, bilinear, align_corners=True) (+ add: one [ho, wo, c]
+    table added to every frame)."""
     n, h, w, c = _nhwc(x, "resize x")
     _, ho, wo, _ = _nhwc(out, "resize out")
-    if add is not None:
-        _nhwc(add, "resize add")
+    if add is not None and (add.dtype != torch.float32 or not add.is_contiguous() or add.numel() != ho * wo * c):
+        raise ValueError("resize_bilinear: add must be a contiguous fp32 [ho, wo, c] table")
     check(_lib.load().sr_resize_bilinear_f32(_stream(x), _p(x), n, h, w, c, ho, wo, _p(add), _p(out)),
           "sr_resize_bilinear_f32")
 
