@@ -753,6 +753,104 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
   return SR_EINVAL;
 }
 
+// Narrow implicit-GEMM 3x3 conv for Cout <= 32 (DPT output_conv2[0]: 128 -> 32 at full
+// resolution, dpt_head.py:105-108): a 128-wide tile would leave 3/4 of its MFMAs on padding
+// columns, so this tile is 256 output pixels x 32 channels: 4 waves x 64 rows, stage = 256 A
+// rows + 32 W rows (36 KiB), 9 LDS-DMA pieces per wave, same swizzle and fragments as
+// gemm_kernel<float, EPI, true>.  Epilogue BIAS.
+constexpr int NBM = 256, NBN = 32;
+constexpr int NSTAGE = (NBM + NBN) * ROWB;  // 36 KiB
+
+__global__ __launch_bounds__(256, 2) void conv_narrow_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * NSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = sr::xcd_remap(blockIdx.x, gridDim.x) * NBM;
+  constexpr int PW = (NBM + NBN) / 8 / 4;  // 9 pieces per wave
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const char* src[PW];
+  int cy[PW], cx[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int gi = wave_u * PW + i;
+    const int tr = gi * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
+    if (gi < NBM / 8) {
+      const int r = min(m0 + tr, g.M - 1);
+      const int hw = g.conv.Ho * g.conv.Wo;
+      const int n = r / hw, rem = r - n * hw, yo = rem / g.conv.Wo, xo = rem - yo * g.conv.Wo;
+      cy[i] = yo * g.conv.stride - 1;
+      cx[i] = xo * g.conv.stride - 1;
+      src[i] = g.conv.x + ((((int64_t)n * g.conv.H + cy[i]) * g.conv.W + cx[i]) * g.conv.C) * 4 + chunk * 16;
+    } else {
+      const int r = min(tr - NBM, g.N - 1);
+      cy[i] = cx[i] = 0;
+      src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
+    }
+  }
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * PW * 1024);
+  auto stage = [&](int kt, int buf) {
+    const uint32_t base = dst0 + buf * NSTAGE;
+    const int k0 = kt * 32, tap = k0 / g.conv.C, ci0 = k0 - tap * g.conv.C;
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const int64_t off = ((int64_t)ky * g.conv.W + kx) * g.conv.C * 4 + (int64_t)ci0 * 4;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      if (wave_u * PW + i < NBM / 8) {
+        const int yy = cy[i] + ky, xx = cx[i] + kx;
+        const bool in = (unsigned)yy < (unsigned)g.conv.H && (unsigned)xx < (unsigned)g.conv.W;
+        sr::dma16(in ? src[i] + off : g.conv.zero + (lane & 7) * 16, base + i * 1024);
+      } else {
+        sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+      }
+    }
+  };
+  const int lr = lane & 15, lg = lane >> 4;
+  const int swz = lr >> 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  stage(0, 0);
+  for (int kt = 0; kt < g.ktiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < g.ktiles) {
+      stage(kt + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sr::barrier_raw();
+    const char* sb = smem + buf * NSTAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int coff = (((ks * 4 + lg) ^ swz) * 16);
+      uint4 a[4], b[2];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + (wave * 64 + mi * 16 + lr) * ROWB + coff);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b[ni] = *(const uint4*)(sb + (NBM + ni * 16 + lr) * ROWB + coff);
+      if (g.conv.relu) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          f32x4 v = __builtin_bit_cast(f32x4, a[mi]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          a[mi] = __builtin_bit_cast(uint4, v);
+        }
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) Mma<float>::run(b[ni], a[mi], acc[mi][ni]);
+    }
+    sr::wait_lgkm0();
+    sr::barrier_raw();
+  }
+  // columns 32..63 (acc[.][2..3], zeros) fall outside N and are dropped by the sink
+  epilogue<float, SR_EPI_BIAS, 4>(g, acc, m0 + wave * 64, 0, lr, lg);
+}
+
 template <int EPI>
 int launch_conv(const GemmArgs& a, hipStream_t s) {
   const int nwg = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
@@ -883,5 +981,10 @@ extern "C" int sr_conv3x3_f32(sr_stream_t stream, const float* x, int n, int h, 
   a.conv.stride = stride;
   a.conv.relu = relu_in;
   hipStream_t s = (hipStream_t)stream;
+  static const bool no_narrow = getenv("SR_CONV_NO_NARROW") != nullptr;  // tuning A/B switch
+  if (!no_narrow && epi == SR_EPI_BIAS && cout <= NBN) {
+    hipLaunchKernelGGL(conv_narrow_kernel, dim3((a.M + NBM - 1) / NBM), dim3(256), 0, s, a);
+    return sr::check_launch("sr_conv3x3_f32(narrow)");
+  }
   return epi == SR_EPI_BIAS ? launch_conv<SR_EPI_BIAS>(a, s) : launch_conv<SR_EPI_BIAS_RESID>(a, s);
 }
