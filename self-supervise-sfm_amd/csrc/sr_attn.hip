@@ -963,6 +963,85 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
   }
 }
 
+// ------------------------------------------------------------------ f32, short key sets
+// One wave per (query row, head, item) for short sequences (the camera trunk: 2N tokens,
+// head_dim 128, SR_MASK_CAMERA, camera_head.py:165): lane j scores key c0 + j of a 64-key chunk
+// with a full-length dot product, the chunk's softmax statistics are two wave reductions, and
+// P.V walks the chunk's keys with P broadcast by readlane while every lane accumulates D/64
+// output columns.  The 128-row-per-workgroup kernel above spends most of its time in a serial
+// per-key loop at these sizes (134 us per camera-trunk launch at N=32).
+template <int D>
+__global__ __launch_bounds__(256) void attn_f32_short_kernel(AttnArgs args) {
+  constexpr int DL = D / 64;  // output columns per lane
+  const sr_attn_desc& d = args.d;
+  const int lane = threadIdx.x & 63;
+  const int qrow = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int head = blockIdx.y, item = blockIdx.z;
+  if (qrow >= d.lq) return;  // wave-uniform; no barriers below
+  const int hcol = head * D;
+  const float* qp = (const float*)d.q + ((int64_t)item * d.q_bstride + qrow) * d.ldq + hcol;
+  float q[D];
+#pragma unroll
+  for (int i = 0; i < D; i += 4) {
+    const float4 t = *(const float4*)(qp + i);
+    q[i] = t.x * d.scale; q[i + 1] = t.y * d.scale; q[i + 2] = t.z * d.scale; q[i + 3] = t.w * d.scale;
+  }
+  float m = -INFINITY, l = 0.f, o[DL];
+#pragma unroll
+  for (int t = 0; t < DL; ++t) o[t] = 0.f;
+  for (int seg = 0; seg < 2; ++seg) {
+    const int len = seg ? d.l1 : d.l0;
+    if (len <= 0) continue;
+    const float* kb = (const float*)(seg ? d.k1 : d.k0);
+    const float* vb = (const float*)(seg ? d.v1 : d.v0);
+    const int64_t ldk = seg ? d.ldk1 : d.ldk0, ldv = seg ? d.ldv1 : d.ldv0;
+    const int64_t rb = (int64_t)item * (seg ? d.k1_bstride : d.k0_bstride);
+    const int key_base = seg ? d.l0 : 0;
+    for (int c0 = 0; c0 < len; c0 += 64) {
+      const int j = c0 + lane;
+      const int kidx = key_base + j;
+      bool ok = j < len;
+      if (d.mask_mode == SR_MASK_CAMERA) ok = ok && (kidx < d.n_anchor || kidx == qrow);
+      float sj = -INFINITY;
+      if (ok) {
+        const float* kp = kb + (rb + j) * ldk + hcol;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < D; i += 4) {
+          const float4 t = *(const float4*)(kp + i);
+          acc = fmaf(q[i], t.x, acc);
+          acc = fmaf(q[i + 1], t.y, acc);
+          acc = fmaf(q[i + 2], t.z, acc);
+          acc = fmaf(q[i + 3], t.w, acc);
+        }
+        sj = acc;
+      }
+      const float cmax = sr::wave_max(sj);
+      if (cmax == -INFINITY) continue;  // every key of the chunk masked (wave-uniform)
+      const float m_new = fmaxf(m, cmax);
+      const float alpha = expf(m - m_new);
+      const float pj = ok ? expf(sj - m_new) : 0.f;
+      l = l * alpha + sr::wave_sum(pj);
+#pragma unroll
+      for (int t = 0; t < DL; ++t) o[t] *= alpha;
+      m = m_new;
+      const int n = min(64, len - c0);
+      for (int jj = 0; jj < n; ++jj) {
+        const float p = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(pj), jj));
+        if (p == 0.f) continue;  // masked key (wave-uniform)
+        const float* vp = vb + (rb + c0 + jj) * ldv + hcol + lane * DL;
+#pragma unroll
+        for (int t = 0; t < DL; ++t) o[t] = fmaf(p, vp[t], o[t]);
+      }
+    }
+  }
+  float* op = (float*)d.o + ((int64_t)item * d.q_bstride + qrow) * d.ldo + hcol + lane * DL;
+  const float inv = 1.f / l;
+#pragma unroll
+  for (int t = 0; t < DL; ++t) op[t] = o[t] * inv;
+  if (d.lse && lane == 0) d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m * 1.4426950408889634f + log2f(l);
+}
+
 // ------------------------------------------------------------------ partial-softmax merge
 // out = (2^(la-mx) oa + 2^(lb-mx) ob) / (2^(la-mx) + 2^(lb-mx)), mx = max(la, lb): two attention
 // passes over disjoint key sets of the same queries (the frame-sharded global block: local
@@ -1078,6 +1157,15 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   }
   SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attention: bad dtype %d", dtype);
   a.ntile0 = a.ntile1 = 0;
+  static const bool no_short = getenv("SR_ATTN_NO_SHORT") != nullptr;  // tuning A/B switch
+  const bool al16 = (((uintptr_t)d.q | (uintptr_t)d.k0 | (uintptr_t)(d.l1 ? d.k1 : d.k0)) & 15) == 0;
+  if (!no_short && al16 && d.l0 + d.l1 <= 512 && (d.head_dim == 64 || d.head_dim == 128) && d.ldq % 4 == 0 &&
+      d.ldk0 % 4 == 0 && (d.l1 == 0 || d.ldk1 % 4 == 0)) {
+    dim3 g4((d.lq + 3) / 4, d.heads, d.batch);
+    if (d.head_dim == 64) hipLaunchKernelGGL(attn_f32_short_kernel<64>, g4, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(attn_f32_short_kernel<128>, g4, dim3(256), 0, s, a);
+    return sr::check_launch("sr_attention(f32 short)");
+  }
   dim3 grid((d.lq + F32_THREADS - 1) / F32_THREADS, d.heads, d.batch);
   if (d.head_dim == 64) {
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(F32_THREADS), 0, s, a);
