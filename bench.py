@@ -100,23 +100,27 @@ KERNEL_OF_TAG = {
     "attn_frame": "attn_bf16_kernel<4, 2, 0>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
     "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
 }
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
+TRAFFIC_FILES = [os.path.join(REPO, "profiles", f) for f in
+                 ("r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
 
 
-def pmc_traffic(kernel: str, views: int, img: int):
-    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), or None.  The passes were run on
-    one workload (the file's ``workload``, default N=32 @518); other sizes get None."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            d = json.load(f)
-        wl = d.get("workload", {"views": 32, "img": 518})
-        if (wl.get("views"), wl.get("img")) != (views, img):
-            return None
-        k = d["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
-        return None
-    return None if k is None else k["traffic_bytes"]
+def pmc_traffic(kernel: str, views: int, img: int, fp8: str = "off"):
+    """(HBM bytes per launch of ``kernel``, source file) from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), or (None, None).  Each file holds the
+    passes of one workload (its ``workload``: views, img, fp8 mode); other workloads get None."""
+    for path in TRAFFIC_FILES:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            wl = d.get("workload", {"views": 32, "img": 518})
+            if (wl.get("views"), wl.get("img"), wl.get("fp8_global", "off")) != (views, img, fp8):
+                continue
+            k = d["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k is not None:
+            return k["traffic_bytes"], path
+    return None, None
 
 
 def algorithmic_tflop(n_views: int, img: int, C: int = 1024) -> float:
@@ -257,13 +261,13 @@ def main():
                 kern, peak = "attn_qk8_kernel<2, true>", 2 * bf16_peak
             else:
                 kern, peak = "attn_qk8_kernel<2, false>", 1.0 / (0.5 / (2 * bf16_peak) + 0.5 / bf16_peak)
-        traffic = pmc_traffic(kern, n, args.img) if kern and not fp8 else None
+        traffic, tsrc = pmc_traffic(kern, n, args.img, args.fp8_global if fp8 else "off") if kern else (None, None)
         roofline = {"bound": "mfma", "kernel": kern or dom, "timer_class": dom, "achieved": round(achieved, 2),
                     "peak": round(peak, 1), "peak_source": peak_src, "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4),
                     "traffic": None if traffic is None else round(traffic),
                     "traffic_unit": "bytes/launch (HBM, PMC 2xFETCH_SIZE+WRITE_SIZE)",
-                    "traffic_source": os.path.relpath(TRAFFIC_FILE, REPO) if traffic is not None else None,
+                    "traffic_source": os.path.relpath(tsrc, REPO) if traffic is not None else None,
                     "algorithmic_bytes": round(b["bytes_per_launch"]),
                     "avg_launch_ms": round(b["avg_ms"], 4), "flop_per_launch": b["flops_per_launch"]}
         gems = [v for k, v in breakdown.items() if k.startswith("gemm_")]

@@ -576,7 +576,8 @@ class Aggregator(nn.Module):
             if self._fp8_ws is None:
                 self._fp8_ws = ops.Fp8Workspace()
             ops.attention_qk8(q, k, v, o, heads=pg.heads, batch=1, lq=lq, q_bstride=0, l0=lk, k0_bstride=0,
-                              tag="attn_global", ws=self._fp8_ws, fp8_v=self.fp8_v)
+                              tag="attn_global", ws=self._fp8_ws, fp8_v=self.fp8_v,
+                              key_norm_max=runtime.key_norm_bound(pg))
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
                           k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg))

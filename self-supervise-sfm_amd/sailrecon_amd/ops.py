@@ -303,7 +303,8 @@ def quant_fp8_vt(v: Tensor, heads: int, dst: Tensor, exp_out: Tensor) -> None:
 
 def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, batch: int, lq: int, q_bstride: int,
                   l0: int, k0_bstride: int, scale: Optional[float] = None, tag: Optional[str] = None,
-                  lse: Optional[Tensor] = None, ws: Optional[Fp8Workspace] = None, fp8_v: bool = False) -> None:
+                  lse: Optional[Tensor] = None, ws: Optional[Fp8Workspace] = None, fp8_v: bool = False,
+                  key_norm_max: float = 0.0) -> None:
     """attention() with q.k^T in block-scaled fp8 (BASELINE C5): q and k (bf16, head_dim 64) are
     quantised to e4m3 with one power-of-two scale each (q with scale*log2(e) folded in); V / P.V
     stay bf16 unless ``fp8_v`` (then V is quantised too and P enters the MFMA as e4m3).  One key
@@ -311,6 +312,8 @@ def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, b
     head_dim = 64
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, scale=scale, lse=lse)
+    if _ATTN_BOUND and key_norm_max > 0.0:  # fixed-offset sweep (q.k^T-only mode; see sr_attn_desc)
+        d.key_norm_max = float(key_norm_max)
     C = heads * head_dim
     ws = ws or Fp8Workspace()
     q8, k8, ex = ws.get(q.shape[0], k0.shape[0], C, q.device)

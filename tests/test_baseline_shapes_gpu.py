@@ -192,17 +192,22 @@ def _deq(q8, e):
 
 
 @pytest.mark.parametrize("fp8_v", [False, True], ids=["qk8", "qkv8"])
+@pytest.mark.parametrize("bound", [False, True], ids=["scan", "static"])
 @pytest.mark.parametrize("L", [43_968, 175_872], ids=["C3", "C5"])
-def test_global_attention_fp8_production(ops, L, fp8_v):
+def test_global_attention_fp8_production(ops, L, fp8_v, bound):
     """C5's fp8 path at full length with one power-of-two scale per tensor; a few outlier rows
     (x30) set amax, so the rest of q / k sit ~5 binades below it (the amax-driven
-    scale at full length)."""
+    scale at full length).  ``static``: the key_norm_max bound (the aggregator passes the qk-norm
+    bound), which turns on the fixed-offset sweep in the q.k^T-only mode (waves whose rows' bound
+    is > 100 above their tile-0 max, e.g. the x30 outlier, keep the per-tile max)."""
     q, k, v = _make(L, 11, spikes=(L - 101,))
     q[123] = (q[123].float() * 30).bfloat16()
     k[L // 3] = (k[L // 3].float() * 30).bfloat16()
     o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
     ws = ops.Fp8Workspace()
-    ops.attention_qk8(q, k, v, o, heads=H, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws, fp8_v=fp8_v)
+    kb = float(k.float().view(-1, H, D).norm(dim=-1).max()) if bound else 0.0
+    ops.attention_qk8(q, k, v, o, heads=H, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws, fp8_v=fp8_v,
+                      key_norm_max=kb)
     torch.cuda.synchronize()
     q8, k8, ex = ws.get(L, L, C, q.device)
     eq, ek, ev = (int(t) for t in ex.tolist())

@@ -49,6 +49,10 @@ for step in "$@"; do
                python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     pmc_fetch) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
                python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    pmc_fetch_c5q) run pmc_fetch_c5q 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_c5q -o run --output-format csv -- \
+               python3 bench.py --views 128 --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing --fp8-global qkv ;;
+    pmc_write_c5q) run pmc_write_c5q 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_c5q -o run --output-format csv -- \
+               python3 bench.py --views 128 --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing --fp8-global qkv ;;
     pmc_write) run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
                python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     pmc_gemm1) run pmc_gemm1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_gemm1 -o run --output-format csv -- python3 tools/kbench.py gemm ;;

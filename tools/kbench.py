@@ -219,10 +219,13 @@ def attn_fp8():
         o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
         ws = ops.Fp8Workspace()
         fl = 4.0 * H * L * L * D
+        kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())  # the static key bound's role
         for name, f in (("bf16", lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
-                                                        batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0)),
+                                                        batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                                                        key_norm_max=kb)),
                         ("fp8 qk", lambda: ops.attention_qk8(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H,
-                                                           batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws)),
+                                                           batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws,
+                                                           key_norm_max=kb)),
                         ("fp8 qkv", lambda: ops.attention_qk8(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H,
                                                             batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, ws=ws,
                                                             fp8_v=True))):
