@@ -170,6 +170,9 @@ def cpu_baseline(sd, img: int, n_views: int):
     dt = time.perf_counter() - t0
     return {"value": n_views / dt, "unit": "views/s", "cores": threads, "kind": "port",
             "cpu_model": model, "physical_cores": phys, "os_cpu_count": logical,
+            "threads_note": (f"min(physical cores {phys}, OMP_NUM_THREADS {cap}): the GPU box allots this "
+                             "process a share of the host's CPUs per GPU, and os.cpu_count() counts the whole "
+                             "machine") if cap > 0 else "physical cores",
             "sample": f"1 full fp32 forward of a {n_views}-view scene @{img}px ({2 * n_views} frames; "
                       f"aggregator+camera head+pose decode, the oracle port of the reference path) on the host "
                       f"CPU, {threads} threads, {dt:.1f} s"}
