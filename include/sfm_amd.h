@@ -156,6 +156,10 @@ typedef struct sr_attn_desc {
                   for every key, used INSTEAD of key_bound (no key scan).  For keys that come out of
                   the qk LayerNorm (attention.py:49-50,78) and RoPE (a rotation), |k| <=
                   sqrt(head_dim) max|w| + |b| of the k_norm affine; 0 = unset */
+  int64_t o_bstride; /* output rows per item (o and its rows); 0 = q_bstride.  With q_bstride = 0
+                  and k0_bstride = l0 the items split ONE query set's keys into chunks whose
+                  normalised partial outputs (o_bstride apart) and LSEs merge with sr_attn_merge_n
+                  (key-split attention: more workgroups when the queries alone cannot fill the chip) */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */
@@ -173,6 +177,16 @@ int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 int sr_attn_merge(sr_stream_t stream, int dtype, int rows, int heads, int head_dim, const void* o_a, int64_t lda,
                   const float* lse_a, const void* o_b, int64_t ldb, const float* lse_b, void* out, int64_t ldo,
                   float* lse_out);
+/* The same merge over `parts` (<= SR_ATTN_MERGE_MAX_PARTS) partial results: part p's output rows
+ * start at o_parts + p * part_rows * ld (row stride ld); its LSE block of heads * rows floats
+ * starts at lse_parts + p * heads * rows, laid out [rows / g][heads][g] with g = lse_seg_rows[p]
+ * (g = rows, i.e. [heads][rows], for every part when lse_seg_rows is null): g = rows for the parts
+ * of a key-split launch over one query set, g = lq for a batch launch of rows / lq items.  out
+ * must not alias o_parts; lse_out ([heads][rows]) optional. */
+#define SR_ATTN_MERGE_MAX_PARTS 16
+int sr_attn_merge_n(sr_stream_t stream, int dtype, int parts, int rows, int heads, int head_dim, const void* o_parts,
+                    int64_t ld, int64_t part_rows, const float* lse_parts, const int* lse_seg_rows, void* out,
+                    int64_t ldo, float* lse_out);
 
 /* fp8 (OCP e4m3) quantisation with ONE power-of-two scale per tensor (BASELINE C5, "fp8 QKV";
  * e4m3 Q/K/V with per-tensor scales):

@@ -455,7 +455,7 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     if (d.lse && hi == 0 && qrow < d.lq)
       d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
     if (qrow < d.lq) {
-      bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+      bf16* op = (bf16*)d.o + (item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol;
       if (wide_o) {
         // lane halves hold columns 8g..8g+3 (hi = 0) and 8g+4..8g+7 (hi = 1) of the row: one
         // permlane32 swap per dword joins groups (2k, 2k+1) into 16 contiguous bytes per lane,
@@ -787,7 +787,7 @@ __global__ __launch_bounds__(256, 2) void attn_qk8_kernel(AttnArgs args, const u
     if (d.lse && hi == 0 && qrow < d.lq)
       d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
     if (qrow < d.lq) {
-      bf16* op = (bf16*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+      bf16* op = (bf16*)d.o + (item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol;
       if (wide_o) {
         // lane halves hold columns 8g..8g+3 (hi = 0) and 8g+4..8g+7 (hi = 1) of the row: one
         // permlane32 swap per dword joins groups (2k, 2k+1) into 16 contiguous bytes per lane,
@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
   }
   (void)nkeys_total;
   if (qrow < d.lq) {
-    float* op = (float*)d.o + (item * d.q_bstride + qrow) * d.ldo + hcol;
+    float* op = (float*)d.o + (item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol;
     const float inv = 1.f / l;
 #pragma unroll
     for (int i = 0; i < D; ++i) op[i] = o[i] * inv;
@@ -1092,7 +1092,8 @@ __global__ __launch_bounds__(256) void attn_f32_short_kernel(AttnArgs args) {
       }
     }
   }
-  float* op = (float*)d.o + ((int64_t)item * d.q_bstride + qrow) * d.ldo + hcol + lane * DL;
+  float* op = (float*)d.o + ((int64_t)item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol +
+              lane * DL;
   const float inv = 1.f / l;
 #pragma unroll
   for (int t = 0; t < DL; ++t) op[t] = o[t] * inv;
@@ -1137,6 +1138,56 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const T* __restrict__ o
     T* po = out + r * ldo + col;
 #pragma unroll
     for (int j = 0; j < 4; ++j) po[j] = sr::from_f32<T>(y[j]);
+    if (lout && c == 0) lout[(int64_t)h * rows + r] = mx == -INFINITY ? mx : mx + log2f(sum);
+  }
+}
+
+// N-way form of attn_merge_kernel: part p's rows at op + p * pstride (elements); its LSE block
+// starts at lse + p * heads * rows, laid out [rows / seg][heads][seg] with seg = segrows.n[p]
+struct MergeSegRows {
+  int n[SR_ATTN_MERGE_MAX_PARTS];
+};
+template <typename T>
+__global__ __launch_bounds__(256) void attn_merge_n_kernel(const T* __restrict__ op, int64_t ld, int64_t pstride,
+                                                           const float* __restrict__ lse, MergeSegRows segrows,
+                                                           int parts, T* out, int64_t ldo, float* __restrict__ lout,
+                                                           int rows, int heads, int head_dim) {
+  const int chunks = head_dim >> 2;
+  const int64_t total = (int64_t)rows * heads * chunks;
+  const int64_t lstride = (int64_t)heads * rows;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % chunks);
+    const int64_t rh = e / chunks;
+    const int h = (int)(rh % heads);
+    const int r = (int)(rh / heads);
+    float lp[SR_ATTN_MERGE_MAX_PARTS];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < SR_ATTN_MERGE_MAX_PARTS; ++p) {
+      if (p < parts) {
+        const int sg = segrows.n[p];
+        lp[p] = lse[p * lstride + (int64_t)(r / sg) * heads * sg + (int64_t)h * sg + r % sg];
+        mx = fmaxf(mx, lp[p]);
+      }
+    }
+    const int col = h * head_dim + 4 * c;
+    float y[4] = {0.f, 0.f, 0.f, 0.f}, sum = 0.f;
+    if (mx != -INFINITY) {
+#pragma unroll
+      for (int p = 0; p < SR_ATTN_MERGE_MAX_PARTS; ++p) {
+        if (p < parts) {
+          const float w = exp2f(lp[p] - mx);
+          sum += w;
+          const T* pp = op + p * pstride + (int64_t)r * ld + col;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) y[j] = fmaf(w, sr::to_f32(pp[j]), y[j]);
+        }
+      }
+    }
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    T* po = out + (int64_t)r * ldo + col;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) po[j] = sr::from_f32<T>(y[j] * inv);
     if (lout && c == 0) lout[(int64_t)h * rows + r] = mx == -INFINITY ? mx : mx + log2f(sum);
   }
 }
@@ -1233,6 +1284,32 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     return SR_EUNSUPPORTED;
   }
   return sr::check_launch("sr_attention(f32)");
+}
+
+extern "C" int sr_attn_merge_n(sr_stream_t stream, int dtype, int parts, int rows, int heads, int head_dim,
+                               const void* o_parts, int64_t ld, int64_t part_rows, const float* lse_parts,
+                               const int* lse_seg_rows, void* out, int64_t ldo, float* lse_out) {
+  SR_CHECK(o_parts && lse_parts && out && parts > 0 && parts <= SR_ATTN_MERGE_MAX_PARTS && rows > 0 && heads > 0 &&
+               head_dim > 0 && head_dim % 4 == 0 && part_rows >= rows && out != o_parts,
+           SR_EINVAL, "sr_attn_merge_n: bad arguments (parts=%d rows=%d)", parts, rows);
+  MergeSegRows sg;
+  for (int p = 0; p < SR_ATTN_MERGE_MAX_PARTS; ++p) {
+    sg.n[p] = p < parts && lse_seg_rows ? lse_seg_rows[p] : rows;
+    SR_CHECK(sg.n[p] > 0 && rows % sg.n[p] == 0, SR_EINVAL, "sr_attn_merge_n: part %d LSE block of %d rows", p,
+             sg.n[p]);
+  }
+  const int64_t total = (int64_t)rows * heads * (head_dim / 4);
+  const dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 65536));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(attn_merge_n_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)o_parts, ld, part_rows * ld,
+                       lse_parts, sg, parts, (bf16*)out, ldo, lse_out, rows, heads, head_dim);
+  else {
+    SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attn_merge_n: bad dtype %d", dtype);
+    hipLaunchKernelGGL(attn_merge_n_kernel<float>, grid, dim3(256), 0, s, (const float*)o_parts, ld, part_rows * ld,
+                       lse_parts, sg, parts, (float*)out, ldo, lse_out, rows, heads, head_dim);
+  }
+  return sr::check_launch("sr_attn_merge_n");
 }
 
 extern "C" int sr_attn_merge(sr_stream_t stream, int dtype, int rows, int heads, int head_dim, const void* o_a,

@@ -21,6 +21,7 @@ SR_F32, SR_BF16 = 0, 1
 SR_EPI_BIAS, SR_EPI_BIAS_GELU, SR_EPI_BIAS_RESID, SR_EPI_QKV, SR_EPI_PATCH = 0, 1, 2, 3, 4
 SR_EPI_F32, SR_EPI_GELU_BWD = 5, 6
 SR_MASK_NONE, SR_MASK_CAMERA = 0, 1
+SR_ATTN_MERGE_MAX_PARTS = 16
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -56,6 +57,7 @@ class AttnDesc(ctypes.Structure):
         ("lse", _vp),
         ("key_bound", _vp),
         ("key_norm_max", _f32),
+        ("o_bstride", _i64),
     ]
 
 
@@ -89,6 +91,7 @@ _PROTOS = {
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_attention_bound_floats": (_i32, [ctypes.POINTER(AttnDesc)]),
+    "sr_attn_merge_n": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "sr_attn_merge": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp]),
     "sr_quant_fp8": (_i32, [_vp, _vp, _i64, _i32, _i32, _f32, _vp, _i64, _vp, _vp]),
     "sr_attention_qk8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp]),

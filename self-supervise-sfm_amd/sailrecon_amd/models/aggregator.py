@@ -555,15 +555,33 @@ class Aggregator(nn.Module):
         while the gather of the others is in flight, then the remote anchors (kv_all rows outside
         [off, off + lq): up to two key segments), merged exactly by the passes' LSEs."""
         C, H, D = pg.dim, pg.heads, pg.head_dim
+        kb = runtime.key_norm_bound(pg)
+        segs = [(a, n) for a, n in ((0, off), (off + lq, lk - off - lq)) if n > 0]
+        if q.dtype == torch.bfloat16:
+            # every pass key-split as one slice of a stacked partials buffer (the per-rank query
+            # slice alone leaves CUs idle at G >= 4), one N-way LSE merge at the end
+            split = lambda n: ops.key_split_parts(dtype=q.dtype, batch=1, lq=lq, heads=H, l0=n, l1=0,  # noqa: E731
+                                                  mask_mode=0)
+            plan = [(kv_loc, split(lq))] + [(kv_all[a:a + n], split(n)) for a, n in segs]
+            total = sum(p for _, p in plan)
+            o_parts, lse_parts = ops.key_split_workspace(q.device, total, lq, C, H, name="attn_shard")
+            p0 = 0
+            for i, (kv, p) in enumerate(plan):
+                if i == 1:
+                    _wait(work_kv)  # the remote anchors' K/V
+                ops.attention_partials(q, kv[:, 0:C], kv[:, C:2 * C], o_parts[p0 * lq:(p0 + p) * lq],
+                                       lse_parts[p0:p0 + p], heads=H, head_dim=D, lq=lq, l0=kv.shape[0], parts=p,
+                                       tag="attn_global", key_norm_max=kb)
+                p0 += p
+            ops.attn_merge_n(o_parts, lse_parts, o, parts=total, rows=lq, heads=H, head_dim=D)
+            return
         ws = self._ws
         lse_loc = ws.get("lse_loc", H, lq, torch.float32, q.device)
         lse_rem = ws.get("lse_rem", H, lq, torch.float32, q.device)
         o_rem = ws.get("o_rem", lq, C, o.dtype, q.device)
-        kb = runtime.key_norm_bound(pg)
         ops.attention(q, kv_loc[:, 0:C], kv_loc[:, C:2 * C], o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0,
                       l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc, key_norm_max=kb)
         _wait(work_kv)
-        segs = [(a, n) for a, n in ((0, off), (off + lq, lk - off - lq)) if n > 0]
         (s0, n0), (s1, n1) = segs[0], (segs[1] if len(segs) > 1 else (0, 0))
         ops.attention(q, kv_all[s0:s0 + n0, 0:C], kv_all[s0:s0 + n0, C:2 * C], o_rem, heads=H, head_dim=D, batch=1,
                       lq=lq, q_bstride=0, l0=n0, k0_bstride=0, k1=kv_all[s1:s1 + n1, 0:C] if n1 else None,

@@ -202,6 +202,55 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
 
 # fixed-offset softmax sweep (sr_attn_desc.key_bound); SR_ATTN_BOUND=0 keeps the per-tile row max
 _ATTN_BOUND = os.environ.get("SR_ATTN_BOUND", "1") != "0"
+# key-split attention: SR_ATTN_KSPLIT=0 disables it, =S forces S chunks where they divide the keys
+_KSPLIT_ENV = os.environ.get("SR_ATTN_KSPLIT")
+_KSPLIT_WGS = 2560  # 256-row workgroups a split launch should reach (10 per CU)
+_KSPLIT_MIN_KEYS = 2048  # shortest key chunk (32 tiles of 64 keys per workgroup)
+
+
+def reloc_split_parts(*, dtype: torch.dtype, batch: int, lq: int, q_bstride: int, heads: int, l0: int,
+                      k0_bstride: int, l1: int, mask_mode: int) -> int:
+    """Key chunks of the SHARED segment 0 for a global_reloc-shaped launch (batch query frames,
+    segment 0 common to all of them, segment 1 per frame) too small to fill the chip (the per-rank
+    query frames under frame sharding: 4 frames at G=8 leave 384 workgroups): the frames' query
+    rows then run as ONE query set against key chunks of segment 0 (attention_partials), the
+    per-frame segment as its own batch launch, and the partials merge.  1 = no split."""
+    if dtype != torch.bfloat16 or batch < 2 or l1 == 0 or k0_bstride != 0 or q_bstride != lq or \
+            mask_mode != _lib.SR_MASK_NONE:
+        return 1
+    if batch * ((lq + 255) // 256) * heads >= 2048:
+        return 1
+    return key_split_parts(dtype=dtype, batch=1, lq=batch * lq, heads=heads, l0=l0, l1=0, mask_mode=mask_mode)
+
+
+def key_split_parts(*, dtype: torch.dtype, batch: int, lq: int, heads: int, l0: int, l1: int, mask_mode: int) -> int:
+    """Key chunks one bf16 attention launch is split into (1 = no split).  A single query set too
+    short to fill the chip (the per-rank query slice of a frame-sharded global block: G=8 at C3
+    leaves 43 q-tiles x 16 heads = 688 workgroups for 256 CUs) runs as S items over key chunks
+    of equal length, each writing a normalised partial output and its LSE, merged by
+    sr_attn_merge_n.  The fp32 accumulation inside a chunk is unchanged; the partials round to
+    bf16 once before the merge."""
+    if dtype != torch.bfloat16 or batch != 1 or l1 != 0 or mask_mode != _lib.SR_MASK_NONE:
+        return 1
+    wgs = (lq + 255) // 256 * heads
+    if _KSPLIT_ENV is not None:
+        s = int(_KSPLIT_ENV)
+        return s if s > 1 and l0 % s == 0 else 1
+    if wgs >= 2048:  # the C3 global block (2752 workgroups) runs best unsplit
+        return 1
+    # powers of two first: measured at C3's per-rank slices (tools/kbench.py attn_rank), S = 3 / 6
+    # trail S = 2 / 4 / 8 by 3-8 %
+    for cands in ((2, 4, 8), (3, 6)):
+        best = 1
+        for s in cands:
+            if l0 % s or l0 // s < _KSPLIT_MIN_KEYS:
+                continue
+            best = s
+            if wgs * s >= _KSPLIT_WGS:
+                break
+        if best > 1:
+            return best
+    return 1
 
 
 def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_dim: int, batch: int, lq: int,
@@ -212,10 +261,42 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``lse``
     (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd.
     ``key_norm_max`` > 0: a static bound of every key's per-head 2-norm (runtime.key_norm_bound),
-    which replaces the key scan of the fixed-offset sweep."""
+    which replaces the key scan of the fixed-offset sweep.  A bf16 single query set too short to
+    fill the chip runs key-split (key_split_parts, attention_partials + attn_merge_n)."""
+    parts = key_split_parts(dtype=q.dtype, batch=batch, lq=lq, heads=heads, l0=l0, l1=l1, mask_mode=mask_mode)
+    if parts > 1:
+        if lse is not None and (lse.dtype != torch.float32 or not lse.is_contiguous() or lse.numel() != heads * lq):
+            raise ValueError("attention: lse must be contiguous fp32 [batch, heads, lq]")
+        o_parts, lse_parts = key_split_workspace(q.device, parts, lq, heads * head_dim, heads)
+        attention_partials(q, k0, v0, o_parts, lse_parts, heads=heads, head_dim=head_dim, lq=lq, l0=l0, parts=parts,
+                           scale=scale, tag=tag, key_norm_max=key_norm_max)
+        attn_merge_n(o_parts, lse_parts, o, parts=parts, rows=lq, heads=heads, head_dim=head_dim, lse_out=lse)
+        return
+    rparts = 1 if lse is not None else reloc_split_parts(dtype=q.dtype, batch=batch, lq=lq, q_bstride=q_bstride,
+                                                         heads=heads, l0=l0, k0_bstride=k0_bstride, l1=l1,
+                                                         mask_mode=mask_mode)
+    if rparts > 1:
+        rows = batch * lq
+        o_parts, lse_parts = key_split_workspace(q.device, rparts + 1, rows, heads * head_dim, heads)
+        attention_partials(q[:rows], k0, v0, o_parts, lse_parts[:rparts], heads=heads, head_dim=head_dim, lq=rows,
+                           l0=l0, parts=rparts, scale=scale, tag=tag, key_norm_max=key_norm_max)
+        d = _attn_desc(q, k1, v1, o_parts[rparts * rows:], heads=heads, head_dim=head_dim, batch=batch, lq=lq,
+                       q_bstride=lq, l0=l1, k0_bstride=k1_bstride, scale=scale, lse=lse_parts[rparts])
+        _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * l1 * head_dim,
+                          q.element_size() * heads * head_dim * 4 * batch * lq)
+        attn_merge_n(o_parts, lse_parts, o, parts=rparts + 1, rows=rows, heads=heads, head_dim=head_dim,
+                     seg_rows=[rows] * rparts + [lq])
+        return
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
                    n_anchor=n_anchor, scale=scale, lse=lse)
+    _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * (l0 + l1) * head_dim,
+                      q.element_size() * heads * head_dim *
+                      (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)))
+
+
+def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,
+                      nbytes: float) -> None:
     if q.dtype == torch.bfloat16 and _ATTN_BOUND and key_norm_max > 0.0:
         d.key_norm_max = float(key_norm_max)
     elif q.dtype == torch.bfloat16 and _ATTN_BOUND:
@@ -227,10 +308,36 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
     check(rc, "sr_attention")
     if timed:
-        es = q.element_size()
-        kv_rows = (l0 if k0_bstride == 0 else batch * l0) + batch * l1  # shared segment read once
-        nb = es * heads * head_dim * (2 * batch * lq + 2 * kv_rows)
-        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * (l0 + l1) * head_dim, nb)
+        TIMER.stop(tag, ev0, flops, nbytes)
+
+
+def key_split_workspace(device, parts: int, rows: int, cols: int, heads: int, name: str = "attn_ksplit"):
+    """(o_parts bf16 [parts*rows, cols], lse_parts fp32 [parts, heads, rows]) in one reusable
+    per-stream workspace."""
+    n_o = (parts * rows * cols + 1) // 2  # bf16 pairs
+    ws = _train_ws(device, name, n_o + parts * heads * rows)
+    o_parts = ws[:n_o].view(torch.bfloat16)[:parts * rows * cols].view(parts * rows, cols)
+    return o_parts, ws[n_o:n_o + parts * heads * rows].view(parts, heads, rows)
+
+
+def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_parts: Tensor, *, heads: int,
+                       head_dim: int, lq: int, l0: int, parts: int, scale: Optional[float] = None,
+                       tag: Optional[str] = None, key_norm_max: float = 0.0) -> None:
+    """One bf16 launch of ``parts`` items over equal key chunks of k0/v0 (item s: keys
+    [s*l0/parts, (s+1)*l0/parts)) against the same lq queries: item s writes its normalised
+    partial output at rows s*lq of o_parts and its LSE to lse_parts[s] ([heads, lq]).  The parts
+    of one or more such launches (stacked in one buffer) merge with attn_merge_n."""
+    if l0 % parts:
+        raise ValueError(f"attention_partials: {parts} parts do not divide {l0} keys")
+    if o_parts.shape[0] < parts * lq or lse_parts.dtype != torch.float32 or not lse_parts.is_contiguous() or \
+            lse_parts.numel() != parts * heads * lq:
+        raise ValueError("attention_partials: o_parts [parts*lq, C] / lse_parts fp32 [parts, heads, lq]")
+    chunk = l0 // parts
+    d = _attn_desc(q, k0, v0, o_parts, heads=heads, head_dim=head_dim, batch=parts, lq=lq, q_bstride=0, l0=chunk,
+                   k0_bstride=chunk, scale=scale, lse=lse_parts)
+    d.o_bstride = lq
+    _launch_attention(d, q, tag, key_norm_max, 4.0 * heads * lq * l0 * head_dim,
+                      q.element_size() * heads * head_dim * (lq + 2 * parts * lq + 2 * l0))
 
 
 def attn_merge(o_a: Tensor, lse_a: Tensor, o_b: Tensor, lse_b: Tensor, out: Tensor, *, heads: int, head_dim: int,
@@ -252,6 +359,31 @@ def attn_merge(o_a: Tensor, lse_a: Tensor, o_b: Tensor, lse_b: Tensor, out: Tens
     check(rc, "sr_attn_merge")
     if timed:
         TIMER.stop(tag, ev0, 0.0, out.element_size() * rows * heads * head_dim * 3 + 12 * rows * heads)
+
+
+def attn_merge_n(o_parts: Tensor, lse_parts: Tensor, out: Tensor, *, parts: int, rows: int, heads: int,
+                 head_dim: int, lse_out: Optional[Tensor] = None, seg_rows=None) -> None:
+    """attn_merge over ``parts`` partial results stacked in o_parts ([parts * rows, C], part p at
+    rows p*rows) with LSEs lse_parts (fp32, heads*rows per part); ``seg_rows[p]`` = the rows of
+    one LSE block of part p ([rows/g][heads][g]; default g = rows); see sr_attn_merge_n."""
+    if o_parts.dtype != out.dtype or o_parts.shape[0] < parts * rows or out.shape[0] < rows:
+        raise ValueError("attn_merge_n: o_parts must hold parts*rows rows of out's dtype")
+    if lse_parts.dtype != torch.float32 or not lse_parts.is_contiguous() or lse_parts.numel() < parts * heads * rows:
+        raise ValueError("attn_merge_n: lse_parts must be contiguous fp32 [parts, heads, rows]")
+    if lse_out is not None and (lse_out.dtype != torch.float32 or not lse_out.is_contiguous()
+                                or lse_out.numel() != heads * rows):
+        raise ValueError("attn_merge_n: lse_out must be contiguous fp32 [heads, rows]")
+    if parts > _lib.SR_ATTN_MERGE_MAX_PARTS:
+        raise ValueError(f"attn_merge_n: at most {_lib.SR_ATTN_MERGE_MAX_PARTS} parts")
+    sg = None
+    if seg_rows is not None:
+        if len(seg_rows) != parts:
+            raise ValueError("attn_merge_n: one seg_rows entry per part")
+        sg = (ctypes.c_int * parts)(*seg_rows)
+    rc = _lib.load().sr_attn_merge_n(_stream(out), dtype_code(out.dtype), parts, rows, heads, head_dim, _p(o_parts),
+                                     _rowmajor(o_parts, "o_parts"), rows, _p(lse_parts), sg, _p(out),
+                                     _rowmajor(out, "out"), _p(lse_out))
+    check(rc, "sr_attn_merge_n")
 
 
 def quant_fp8(src: Tensor, mul: float, dst: Optional[Tensor] = None, exp_out: Optional[Tensor] = None):

@@ -117,6 +117,32 @@ def attn_merge(o_a, lse_a, o_b, lse_b, out, *, heads, head_dim, lse_out=None, ta
         lse_out.view(heads, -1).copy_((m + torch.log2(tot)).t())
 
 
+def attention_partials(q, k0, v0, o_parts, lse_parts, *, heads, head_dim, lq, l0, parts, scale=None, tag=None,
+                       key_norm_max=0.0):
+    assert l0 % parts == 0
+    ch = l0 // parts
+    for s in range(parts):
+        attention(q, k0[s * ch:(s + 1) * ch], v0[s * ch:(s + 1) * ch], o_parts[s * lq:(s + 1) * lq], heads=heads,
+                  head_dim=head_dim, batch=1, lq=lq, q_bstride=0, l0=ch, k0_bstride=0, scale=scale,
+                  lse=lse_parts[s])
+
+
+def attn_merge_n(o_parts, lse_parts, out, *, parts, rows, heads, head_dim, lse_out=None, seg_rows=None):
+    blocks = []
+    for p in range(parts):
+        g = rows if seg_rows is None else seg_rows[p]
+        lp = lse_parts.reshape(-1)[p * heads * rows:(p + 1) * heads * rows].view(rows // g, heads, g)
+        blocks.append(lp.permute(0, 2, 1).reshape(rows, heads))
+    ls = torch.stack(blocks)  # [parts, rows, heads]
+    m = ls.max(0).values
+    w = torch.exp2(ls - m)
+    tot = w.sum(0)
+    y = (o_parts[:parts * rows].float().view(parts, rows, heads, head_dim) * (w / tot)[..., None]).sum(0)
+    out[:rows] = y.reshape(rows, heads * head_dim).to(out.dtype)
+    if lse_out is not None:
+        lse_out.view(heads, rows).copy_((m + torch.log2(tot)).t())
+
+
 def layernorm(x, w, b, eps, out, rowmap=None, rows=None):
     n = out.shape[0] if rows is None else rows
     src = x[rowmap.long()[:n]] if rowmap is not None else x[:n]
@@ -172,7 +198,7 @@ def pose_decode(enc, hw, ext, intr):
     intr.copy_(i[0])
 
 
-_NAMES = ["gemm", "attention", "attn_merge", "layernorm", "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
+_NAMES = ["gemm", "attention", "attn_merge", "attention_partials", "attn_merge_n", "layernorm", "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
           "silu", "adaln_modulate", "pose_update", "pose_decode"]
 
 

@@ -187,6 +187,89 @@ def test_attn_merge_fp32_exact(ops, alias):
     assert float((lse.double() - ref_lse).abs().max()) < 1e-4
 
 
+@pytest.mark.parametrize("G", [3, 8], ids=["C3-3rk", "C3-8rk"])
+def test_global_attention_key_split(ops, G):
+    """Key-split attention (ops.key_split_parts): one rank's query slice of the frame-sharded C3
+    global block against all 43,968 keys runs as S key chunks whose bf16 partials and LSEs merge
+    with sr_attn_merge_n.  Equal to the unsplit kernel (output and LSE) and to fp64 attention."""
+    L = 32 * P
+    lq = (32 // G) * P
+    q, k, v = _make(L, 17, spikes=(L - 37, 5 * P + 3))
+    qs = q[L - lq:]
+    parts = ops.key_split_parts(dtype=torch.bfloat16, batch=1, lq=lq, heads=H, l0=L, l1=0, mask_mode=0)
+    assert parts > 1
+    outs, lses = [], []
+    saved = ops._KSPLIT_ENV
+    try:
+        for split in ("0", None):
+            ops._KSPLIT_ENV = split
+            o = torch.empty(lq, C, device=DEV, dtype=torch.bfloat16)
+            lse = torch.empty(H, lq, device=DEV)
+            ops.attention(qs, k, v, o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0,
+                          lse=lse, key_norm_max=float(k.float().view(-1, H, D).norm(dim=-1).max()) * 1.01)
+            outs.append(o)
+            lses.append(lse)
+    finally:
+        ops._KSPLIT_ENV = saved
+    torch.cuda.synchronize()
+    assert _rel(outs[1].float(), outs[0].float()) < 1e-2
+    assert float((lses[1] - lses[0]).abs().max()) < 1e-2
+    rows = _sample_rows(lq, 256, G).to(DEV)
+    ref = _ref_rows(qs[rows], k, v, D ** -0.5)
+    print(f"key split S={parts}: rel {_rel(outs[1][rows].float(), ref):.2e} (unsplit "
+          f"{_rel(outs[0][rows].float(), ref):.2e})")
+    assert _rel(outs[1][rows].float(), ref) < 1e-2
+
+
+def test_attn_merge_n_seg_rows_fp32(ops):
+    """sr_attn_merge_n with mixed LSE layouts: two key chunks of a shared segment over 3 items' query
+    rows as one set ([heads][rows]) plus the items' own segments as a batch launch
+    ([items][heads][lq]) equal the two-segment fp32 kernel (global_reloc's shape)."""
+    g = torch.Generator(device=DEV).manual_seed(6)
+    nb, lq, ls, lo, h, d = 3, 150, 400, 120, 4, 64
+    q = torch.randn(nb * lq, h * d, device=DEV, generator=g)
+    ks, vs = (torch.randn(ls, h * d, device=DEV, generator=g) for _ in range(2))
+    ko, vo = (torch.randn(nb * lo, h * d, device=DEV, generator=g) for _ in range(2))
+    rows = nb * lq
+    o_parts = torch.empty(3 * rows, h * d, device=DEV)
+    lse_parts = torch.empty(3, h, rows, device=DEV)
+    for p in range(2):
+        ops.attention(q, ks[p * 200:(p + 1) * 200], vs[p * 200:(p + 1) * 200], o_parts[p * rows:(p + 1) * rows],
+                      heads=h, head_dim=d, batch=1, lq=rows, q_bstride=0, l0=200, k0_bstride=0, lse=lse_parts[p])
+    ops.attention(q, ko, vo, o_parts[2 * rows:], heads=h, head_dim=d, batch=nb, lq=lq, q_bstride=lq, l0=lo,
+                  k0_bstride=lo, lse=lse_parts[2])
+    o = torch.empty(rows, h * d, device=DEV)
+    ops.attn_merge_n(o_parts, lse_parts, o, parts=3, rows=rows, heads=h, head_dim=d, seg_rows=[rows, rows, lq])
+    one = torch.empty_like(o)
+    ops.attention(q, ks, vs, one, heads=h, head_dim=d, batch=nb, lq=lq, q_bstride=lq, l0=ls, k0_bstride=0, k1=ko,
+                  v1=vo, l1=lo, k1_bstride=lo)
+    torch.cuda.synchronize()
+    assert _rel(o, one) < 1e-5
+
+
+def test_attn_merge_n_fp32_exact(ops):
+    """sr_attn_merge_n over 4 equal fp32 key chunks (a key-split layout: partial p at rows p*lq,
+    LSE [parts, heads, lq]) equals the one-pass fp32 kernel to float rounding, LSE included."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    lq, L, h, d, S = 200, 800, 4, 64, 4
+    q, k, v = (torch.randn(n, h * d, device=DEV, generator=g) for n in (lq, L, L))
+    o_parts = torch.empty(S * lq, h * d, device=DEV)
+    lse_parts = torch.empty(S, h, lq, device=DEV)
+    ch = L // S
+    for p in range(S):
+        ops.attention(q, k[p * ch:(p + 1) * ch], v[p * ch:(p + 1) * ch], o_parts[p * lq:(p + 1) * lq], heads=h,
+                      head_dim=d, batch=1, lq=lq, q_bstride=0, l0=ch, k0_bstride=0, lse=lse_parts[p])
+    o = torch.empty(lq, h * d, device=DEV)
+    lse = torch.empty(h, lq, device=DEV)
+    ops.attn_merge_n(o_parts, lse_parts, o, parts=S, rows=lq, heads=h, head_dim=d, lse_out=lse)
+    one = torch.empty_like(o)
+    lse1 = torch.empty(h, lq, device=DEV)
+    ops.attention(q, k, v, one, heads=h, head_dim=d, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0, lse=lse1)
+    torch.cuda.synchronize()
+    assert _rel(o, one) < 1e-5
+    assert float((lse - lse1).abs().max()) < 1e-4
+
+
 def _deq(q8, e):
     return q8.view(torch.float8_e4m3fn).double() * (2.0 ** int(e))
 
@@ -231,10 +314,17 @@ def test_global_attention_fp8_production(ops, L, fp8_v, bound):
     assert e_exact < 0.15
 
 
-@pytest.mark.parametrize("nq,nsub", [(8, 8 * PP), (32, 32 * PP)], ids=["C2", "C3"])
+@pytest.mark.parametrize("nq,nsub", [(8, 8 * PP), (32, 32 * PP), (4, 32 * PP), (8, 32 * PP)],
+                         ids=["C2", "C3", "C3-8rk", "C3-4rk"])
 def test_reloc_attention_production(ops, nq, nsub):
     """global_reloc (aggregator.py:672-741): every query frame attends to the shared anchor
-    subsample (segment 0, batch stride 0) and to its own frame (segment 1)."""
+    subsample (segment 0, batch stride 0) and to its own frame (segment 1).  The per-rank shapes
+    of the frame-sharded C3 forward (4 / 8 query frames) run key-split (ops.reloc_split_parts:
+    the frames' rows as one query set against chunks of the subsample, the own frames as a batch
+    launch, one LSE merge)."""
+    if nq < 32 and nsub == 32 * PP:
+        assert ops.reloc_split_parts(dtype=torch.bfloat16, batch=nq, lq=P, q_bstride=P, heads=H, l0=nsub,
+                                     k0_bstride=0, l1=P, mask_mode=0) > 1
     q, k, v = _make(nq * P, 3, spikes=(nq * P - 11,))
     ks, _, vs = _make(nsub, 4, spikes=(nsub - 3,))
     o = torch.empty(nq * P, C, device=DEV, dtype=torch.bfloat16)

@@ -107,3 +107,49 @@ def test_shard_range_partitions():
             for s, c in parts:  # contiguous, in rank order
                 assert s == start
                 start += c
+
+
+@pytest.mark.parametrize("G,r", [(3, 0), (3, 1), (8, 7)])
+@pytest.mark.parametrize("force", [None, "2"])
+def test_sharded_global_partials_plan(G, r, force):
+    """Host plan of the bf16 frame-sharded global attention (Aggregator._global_attention_sharded):
+    the local pass plus one or two remote key segments, each key-split into its own slice of one
+    stacked partials buffer, merged once.  Through the CPU ops shim, against softmax attention over
+    all keys, with the split sizes the product picks (None) and a forced 2-way split."""
+    from types import SimpleNamespace
+
+    import cpu_ops
+    from sailrecon_amd import ops
+    from sailrecon_amd.models.aggregator import Aggregator, shard_range
+
+    H, D, P = 2, 64, 7 * 64
+    C = H * D
+    na_tot = 2 * G
+    a0, na = shard_range(na_tot, G, r)
+    La, lq, off = na_tot * P, na * P, a0 * P
+    g = torch.Generator().manual_seed(G * 10 + r)
+    q = torch.randn(lq, C, generator=g).bfloat16()
+    kv_all = torch.randn(La, 2 * C, generator=g).bfloat16()
+    kv_loc = kv_all[off:off + lq].clone()
+    o = torch.empty(lq, C, dtype=torch.bfloat16)
+    pg = SimpleNamespace(dim=C, heads=H, head_dim=D, k_bound=0.0)
+    calls = []
+    saved = ops._KSPLIT_ENV
+    with cpu_ops.installed():
+        real = ops.attention_partials
+        ops.attention_partials = lambda *a, **k: (calls.append((k["l0"], k["parts"])), real(*a, **k))
+        try:
+            ops._KSPLIT_ENV = force
+            Aggregator._global_attention_sharded(None, q, kv_loc, kv_all, o, pg, lq, La, off, [])
+        finally:
+            ops._KSPLIT_ENV = saved
+    segs = [n for n in (off, La - off - lq) if n > 0]
+    assert [l0 for l0, _ in calls] == [lq] + segs
+    if force:
+        assert all(p == 2 for _, p in calls)
+    ref = torch.empty(lq, C)
+    with cpu_ops.installed():
+        cpu_ops.attention(q.float(), kv_all[:, :C].float(), kv_all[:, C:].float(), ref, heads=H, head_dim=D, batch=1,
+                          lq=lq, q_bstride=0, l0=La, k0_bstride=0)
+    err = float((o.float() - ref).norm() / ref.norm())
+    assert err < 1e-2, err

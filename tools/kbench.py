@@ -72,6 +72,67 @@ def attn():
     print(f"attn {'reloc 32x(9760+1374)':18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
 
 
+def attn_rank():
+    """Per-rank global attention of the frame-sharded C3 forward: 32/G anchors' queries against
+    all 43,968 anchor keys (one pass), G = 2, 4, 8."""
+    C, H, D, P, N = 1024, 16, 64, 1374, 32
+    L = N * P
+    qkv = torch.randn(L, 3 * C, device=DEV, dtype=torch.bfloat16)
+    kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())
+    for G in (1, 2, 4, 8):
+        lq = L // G
+        o = torch.empty(lq, C, device=DEV, dtype=torch.bfloat16)
+
+        def f():
+            ops.attention(qkv[:lq, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=1, lq=lq,
+                          q_bstride=0, l0=L, k0_bstride=0, key_norm_max=kb)
+        saved = ops._KSPLIT_ENV
+        for split in ("0", "auto", "2", "3", "4", "6", "8"):
+            ops._KSPLIT_ENV = None if split == "auto" else split
+            parts = ops.key_split_parts(dtype=torch.bfloat16, batch=1, lq=lq, heads=H, l0=L, l1=0, mask_mode=0)
+            ms = timeit(f, reps=5)
+            fl = 4.0 * H * lq * L * D
+            print(f"attn rank G={G} lq={lq:6d} keys={L} split={split:4s}(S={parts}) {ms:8.3f} ms  "
+                  f"{fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+        ops._KSPLIT_ENV = saved
+
+
+def attn_rank_small():
+    """Per-rank reloc (32/G query frames x [9760 shared subsample + own 1374]) and frame
+    (64/G frames x 1374) attention of the frame-sharded C3 forward, G = 1, 2, 4, 8."""
+    C, H, D, P, N = 1024, 16, 64, 1374, 32
+    nsub = N * 305
+    for G in (1, 2, 4, 8):
+        nq = N // G
+        qkv = torch.randn(2 * nq * P, 3 * C, device=DEV, dtype=torch.bfloat16)
+        kv = torch.randn(nsub, 2 * C, device=DEV, dtype=torch.bfloat16)
+        o = torch.empty(2 * nq * P, C, device=DEV, dtype=torch.bfloat16)
+        kb = 1.01 * max(float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max()),
+                        float(kv[:, :C].float().view(-1, H, D).norm(dim=-1).max()))
+
+        def rl():
+            ops.attention(qkv[:nq * P, :C], kv[:, :C], kv[:, C:], o, heads=H, head_dim=D, batch=nq, lq=P,
+                          q_bstride=P, l0=nsub, k0_bstride=0, k1=qkv[:nq * P, C:2 * C], v1=qkv[:nq * P, 2 * C:],
+                          l1=P, k1_bstride=P, key_norm_max=kb)
+
+        def fr():
+            ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=2 * nq, lq=P,
+                          q_bstride=P, l0=P, k0_bstride=P, key_norm_max=kb)
+        saved = ops._KSPLIT_ENV
+        for split in ("0", "auto", "2", "4", "8"):
+            ops._KSPLIT_ENV = None if split == "auto" else split
+            parts = ops.reloc_split_parts(dtype=torch.bfloat16, batch=nq, lq=P, q_bstride=P, heads=H, l0=nsub,
+                                          k0_bstride=0, l1=P, mask_mode=0)
+            ms = timeit(rl)
+            fl = 4.0 * nq * H * P * (nsub + P) * D
+            print(f"attn rank G={G} reloc {nq:2d}x({nsub}+{P}) split={split:4s}(S={parts}) {ms:8.3f} ms  "
+                  f"{fl / ms / 1e9:8.1f} TF/s")
+        ops._KSPLIT_ENV = saved
+        ms = timeit(fr)
+        fl = 4.0 * 2 * nq * H * P * P * D
+        print(f"attn rank G={G} frame {2 * nq:2d}x{P}        {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s")
+
+
 def gemm():
     M = 2 * 32 * 1374
     for name, (N, K, epi) in {"qkv": (3072, 1024, _lib.SR_EPI_BIAS), "proj": (1024, 1024, _lib.SR_EPI_BIAS_RESID),
