@@ -40,6 +40,7 @@ struct GemmArgs {
   int lds_epi;  // 256x256 kernels: stage the epilogue through LDS (outputs 16-B aligned rows)
   int kt_per_split;  // split-K (gemm_kernel, gridDim.y slices): k-tiles per slice
   float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
+  int group_m;       // 256x256 kernels: tile order in groups of group_m row tiles (<= 1: row-major)
   sr_gemm_epi ep;
   // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
   // (n, yo, xo) of the NHWC fp32 input x [n][H][W][C], A column k = (ky, kx, ci) — exactly
@@ -576,7 +577,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = g.N / BIG, ntm = (g.M + BIG - 1) / BIG;
   const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
-  const int tm = tile / ntn, tn = tile - tm * ntn;
+  int tm, tn;
+  if (g.group_m > 1) {  // column-major inside groups of group_m row tiles
+    const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
+    const int gm = min(g.group_m, ntm - first), r = tile - grp * per;
+    tm = first + r % gm;
+    tn = r / gm;
+  } else {
+    tm = tile / ntn;
+    tn = tile - tm * ntn;
+  }
   const int m0 = tm * BIG, n0 = tn * BIG;
 
   // LDS-DMA sources: wave w, instruction i fills stage rows (w*8 + i)*8 .. +8 of the 512-row
@@ -702,8 +712,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 }
 
 template <int EPI>
-int launch256(const GemmArgs& a, hipStream_t s) {
+int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
+  static const int group_m = [] {
+    const char* e = getenv("SR_GEMM_GROUP_M");
+    return e ? atoi(e) : 0;
+  }();
+  a.group_m = group_m;
   hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
   return sr::check_launch("sr_gemm(256)");
 }

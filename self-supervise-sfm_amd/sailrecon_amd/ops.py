@@ -208,21 +208,6 @@ _KSPLIT_WGS = 2560  # 256-row workgroups a split launch should reach (10 per CU)
 _KSPLIT_MIN_KEYS = 2048  # shortest key chunk (32 tiles of 64 keys per workgroup)
 
 
-def reloc_split_parts(*, dtype: torch.dtype, batch: int, lq: int, q_bstride: int, heads: int, l0: int,
-                      k0_bstride: int, l1: int, mask_mode: int) -> int:
-    """Key chunks of the SHARED segment 0 for a global_reloc-shaped launch (batch query frames,
-    segment 0 common to all of them, segment 1 per frame) too small to fill the chip (the per-rank
-    query frames under frame sharding: 4 frames at G=8 leave 384 workgroups): the frames' query
-    rows then run as ONE query set against key chunks of segment 0 (attention_partials), the
-    per-frame segment as its own batch launch, and the partials merge.  1 = no split."""
-    if dtype != torch.bfloat16 or batch < 2 or l1 == 0 or k0_bstride != 0 or q_bstride != lq or \
-            mask_mode != _lib.SR_MASK_NONE:
-        return 1
-    if batch * ((lq + 255) // 256) * heads >= 2048:
-        return 1
-    return key_split_parts(dtype=dtype, batch=1, lq=batch * lq, heads=heads, l0=l0, l1=0, mask_mode=mask_mode)
-
-
 def key_split_parts(*, dtype: torch.dtype, batch: int, lq: int, heads: int, l0: int, l1: int, mask_mode: int) -> int:
     """Key chunks one bf16 attention launch is split into (1 = no split).  A single query set too
     short to fill the chip (the per-rank query slice of a frame-sharded global block: G=8 at C3
@@ -271,21 +256,6 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
         attention_partials(q, k0, v0, o_parts, lse_parts, heads=heads, head_dim=head_dim, lq=lq, l0=l0, parts=parts,
                            scale=scale, tag=tag, key_norm_max=key_norm_max)
         attn_merge_n(o_parts, lse_parts, o, parts=parts, rows=lq, heads=heads, head_dim=head_dim, lse_out=lse)
-        return
-    rparts = 1 if lse is not None else reloc_split_parts(dtype=q.dtype, batch=batch, lq=lq, q_bstride=q_bstride,
-                                                         heads=heads, l0=l0, k0_bstride=k0_bstride, l1=l1,
-                                                         mask_mode=mask_mode)
-    if rparts > 1:
-        rows = batch * lq
-        o_parts, lse_parts = key_split_workspace(q.device, rparts + 1, rows, heads * head_dim, heads)
-        attention_partials(q[:rows], k0, v0, o_parts, lse_parts[:rparts], heads=heads, head_dim=head_dim, lq=rows,
-                           l0=l0, parts=rparts, scale=scale, tag=tag, key_norm_max=key_norm_max)
-        d = _attn_desc(q, k1, v1, o_parts[rparts * rows:], heads=heads, head_dim=head_dim, batch=batch, lq=lq,
-                       q_bstride=lq, l0=l1, k0_bstride=k1_bstride, scale=scale, lse=lse_parts[rparts])
-        _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * l1 * head_dim,
-                          q.element_size() * heads * head_dim * 4 * batch * lq)
-        attn_merge_n(o_parts, lse_parts, o, parts=rparts + 1, rows=rows, heads=heads, head_dim=head_dim,
-                     seg_rows=[rows] * rparts + [lq])
         return
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,

@@ -118,23 +118,21 @@ def attn_rank_small():
         def fr():
             ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=2 * nq, lq=P,
                           q_bstride=P, l0=P, k0_bstride=P, key_norm_max=kb)
-        saved = ops._KSPLIT_ENV
-        for split in ("0", "auto", "2", "4", "8"):
-            ops._KSPLIT_ENV = None if split == "auto" else split
-            parts = ops.reloc_split_parts(dtype=torch.bfloat16, batch=nq, lq=P, q_bstride=P, heads=H, l0=nsub,
-                                          k0_bstride=0, l1=P, mask_mode=0)
-            ms = timeit(rl)
-            fl = 4.0 * nq * H * P * (nsub + P) * D
-            print(f"attn rank G={G} reloc {nq:2d}x({nsub}+{P}) split={split:4s}(S={parts}) {ms:8.3f} ms  "
-                  f"{fl / ms / 1e9:8.1f} TF/s")
-        ops._KSPLIT_ENV = saved
+        ms = timeit(rl)
+        fl = 4.0 * nq * H * P * (nsub + P) * D
+        print(f"attn rank G={G} reloc {nq:2d}x({nsub}+{P}) {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s")
         ms = timeit(fr)
         fl = 4.0 * 2 * nq * H * P * P * D
         print(f"attn rank G={G} frame {2 * nq:2d}x{P}        {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s")
 
 
-def gemm():
-    M = 2 * 32 * 1374
+def gemm_rank():
+    """The block GEMMs at the per-rank row counts of the frame-sharded C3 forward (64/G frames)."""
+    for G in (1, 2, 4, 8):
+        gemm(2 * 32 * 1374 // G)
+
+
+def gemm(M=2 * 32 * 1374):
     for name, (N, K, epi) in {"qkv": (3072, 1024, _lib.SR_EPI_BIAS), "proj": (1024, 1024, _lib.SR_EPI_BIAS_RESID),
                               "fc1": (4096, 1024, _lib.SR_EPI_BIAS_GELU), "fc2": (1024, 4096, _lib.SR_EPI_BIAS_RESID)}.items():
         a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
