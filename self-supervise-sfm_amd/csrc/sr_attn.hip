@@ -23,6 +23,7 @@
 #include <cfloat>
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "sr_common.h"
 
@@ -69,10 +70,11 @@ constexpr float RESCALE_LOG2 = 8.f;
 #ifndef SR_ATTN_DEFAULT_CFG
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
-template <int NW, int QB, int KIND>
-__global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(AttnArgs args) {
+template <int NW, int QB, int KIND, bool STAG = false>
+__global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf16_kernel(AttnArgs args) {
   constexpr int QROWS = NW * 32 * QB;
-  constexpr int NBUF = NW >= 4 ? 4 : 2;  // ring depth (power of 2); NBUF-1 stages in flight
+  constexpr int NBUF = STAG ? 8 : (NW >= 4 ? 4 : 2);  // ring depth (power of 2)
+  constexpr int LOOK = STAG ? 3 : NBUF - 1;           // stages in flight
   constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     sp += sstep;
   };
 #pragma unroll
-  for (int i = 0; i < NBUF - 1; ++i)
+  for (int i = 0; i < LOOK; ++i)
     if (i < ntiles) stage(i);
 
   // ---- Q fragments (B operand of S^T = K Q^T): lane holds c*Q[row][16s + 8hi .. +8], with
@@ -280,23 +282,12 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   const int voff0 = (4 * hi + vrow_in) * 128 + (((vcol_in >> 3) ^ vsw) * 16) + (vcol_in & 7) * 2;
   const int voff1 = (4 * hi + vrow_in) * 128 + (((4 + (vcol_in >> 3)) ^ vsw) * 16) + (vcol_in & 7) * 2;
 
-  for (int t = 0; t < ntiles; ++t) {
-    // tile t must have landed (up to NBUF-2 later stages stay in flight); everyone is done
-    // with tile t-1, whose buffer the next stage overwrites
-    if (NBUF >= 4 && t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
-    else if (NBUF >= 3 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    sr::barrier_raw();
-    if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
+  f32x16 sc[QB][2];  // [q-block][key block]: S' of the tile between qk_tile and pv_tile
+  // S'^T of tile t, its ragged-tail mask and (until the offset is fixed) the row-max update
+  auto qk_tile = [&](int t) __attribute__((always_inline)) {
     const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
-    const char* vt_lds = kt_lds + TILE_B;
-    // a wave whose rows all lie past lq (the ragged last q-tile: 1374 = 5 x 256 + 94 leaves two
-    // of its four waves empty) keeps staging and barriers but leaves its SIMD to the other waves
-    if (!wave_active) continue;
-
     // ---- S'^T = K (cQ)^T - m for every q-block (2 blocks of 32 keys each); once every row of
     // the wave runs the fixed offset m = 0, the -m fold MFMAs are skipped (uniform branch)
-    f32x16 sc[QB][2];  // [q-block][key block]
     const f32x16 zero = {};
     if (m_zero) {
 #pragma unroll
@@ -371,13 +362,13 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
           const float delta = m_new - m_run[b];  // S' relative to the new max: S' - delta
           const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
           l_run[b] *= alpha;
-#ifndef SR_ABL_VSUM
+  #ifndef SR_ABL_VSUM
           {  // lacc rows 0 / 1 of lane n hold queries n / n + 16: their alphas
             const float a0 = __shfl(alpha, lane & 15), a1 = __shfl(alpha, (lane & 15) + 16);
             lacc[b][0] *= a0;
             lacc[b][1] *= a1;
           }
-#endif
+  #endif
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             o[b][0][i] *= alpha;
@@ -400,6 +391,10 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
       }
     }
 
+  };
+  // P = exp2(S') of tile t, its row sums, O^T += V^T P^T
+  auto pv_tile = [&](int t) __attribute__((always_inline)) {
+    const char* vt_lds = smem + (t & (NBUF - 1)) * STAGE_B + TILE_B;
     // ---- P = exp2(S') (B operand), O^T += V^T P^T; each V^T fragment feeds every q-block
     float ps[QB][2];
 #pragma unroll
@@ -414,15 +409,15 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
-#ifdef SR_ABL_VSUM
+  #ifdef SR_ABL_VSUM
             ps[b][j & 1] += p;
-#endif
+  #endif
             pf[b][j] = (bf16)p;
           }
-#ifndef SR_ABL_VSUM
+  #ifndef SR_ABL_VSUM
 #pragma unroll
         for (int b = 0; b < QB; ++b) lacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sum_a, pf[b], lacc[b], 0, 0, 0);
-#endif
+  #endif
         const int rowoff = (kb * 32 + 16 * s2) * 128;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -438,7 +433,38 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
       }
 #pragma unroll
     for (int b = 0; b < QB; ++b) l_run[b] += ps[b][0] + ps[b][1];
-  }
+  };
+  // STAG (8 waves, one workgroup per CU): waves 4-7 run the sweep half a tile behind their SIMD
+  // partners (waves 0-3): in each barrier interval a partner's q.k^T MFMAs pair with this wave's
+  // exp2 / P.V stretch and vice versa (MI355X_MICROARCH.md "Two waves per SIMD" 9).  S' of the
+  // late waves' tile t crosses the barrier in registers; the ring keeps tile t-1 (8 stages,
+  // 3 in flight), and every wave runs ntiles + 1 barrier intervals.
+  auto sweep = [&](auto late_c) __attribute__((always_inline)) {
+    constexpr bool LATE = decltype(late_c)::value;
+    for (int t = 0; t < ntiles + (STAG ? 1 : 0); ++t) {
+      // tile t must have landed (up to LOOK-1 later stages stay in flight); everyone is done
+      // with the buffer the next stage overwrites
+      if (LOOK >= 3 && t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+      else if (LOOK >= 2 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sr::barrier_raw();
+      if (t + LOOK < ntiles) stage(t + LOOK);
+      // a wave whose rows all lie past lq (the ragged last q-tile: 1374 = 5 x 256 + 94 leaves two
+      // of its four waves empty) keeps staging and barriers but leaves its SIMD to the other waves
+      if (!wave_active) continue;
+      if constexpr (LATE) {
+        if (t > 0) pv_tile(t - 1);
+        if (t < ntiles) qk_tile(t);
+      } else {
+        if (t < ntiles) {
+          qk_tile(t);
+          pv_tile(t);
+        }
+      }
+    }
+  };
+  if (STAG && wave_u >= 4) sweep(std::true_type{});
+  else sweep(std::false_type{});
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training)
 #pragma unroll
@@ -1240,6 +1266,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : (d.l1 > 0 ? 1 : 0);
     // Workgroup shapes (waves x 32-row q-blocks per wave):
     //   0: 4 x 2 = 256 rows    1: 8 x 1 = 256 rows    2: 2 x 2 = 128 rows
+    //   3: 8 x 2 = 512 rows, waves 4-7 staggered by half a tile (one workgroup per CU)
     // 256-row tiles unless they would leave CUs idle (fewer than 2 workgroups per CU, e.g. the
     // per-rank query slice of a frame-sharded global block).  SR_ATTN_CFG=0|1|2 overrides
     // (tuning experiments).
@@ -1249,17 +1276,18 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     }();
     const long wgs256 = (long)((d.lq + 255) / 256) * d.heads * d.batch;
     const int cfg = force_cfg >= 0 ? force_cfg : (wgs256 >= 512 ? SR_ATTN_DEFAULT_CFG : 2);
-    const int rows = cfg == 2 ? 128 : 256;
+    const int rows = cfg == 2 ? 128 : (cfg == 3 ? 512 : 256);
     dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
-#define SR_ATTN_LAUNCH(NW_, QB_)                                                                          \
-  do {                                                                                                  \
-    if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 2>), grid, dim3(NW_ * 64), 0, s, a);  \
-    else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 1>), grid, dim3(NW_ * 64), 0, s, a); \
-    else hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 0>), grid, dim3(NW_ * 64), 0, s, a);            \
+#define SR_ATTN_LAUNCH(NW_, QB_, ST_)                                                                           \
+  do {                                                                                                        \
+    if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 2, ST_>), grid, dim3(NW_ * 64), 0, s, a);     \
+    else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 1, ST_>), grid, dim3(NW_ * 64), 0, s, a); \
+    else hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 0, ST_>), grid, dim3(NW_ * 64), 0, s, a);               \
   } while (0)
-    if (cfg == 1) SR_ATTN_LAUNCH(8, 1);
-    else if (cfg == 2) SR_ATTN_LAUNCH(2, 2);
-    else SR_ATTN_LAUNCH(4, 2);
+    if (cfg == 1) SR_ATTN_LAUNCH(8, 1, false);
+    else if (cfg == 2) SR_ATTN_LAUNCH(2, 2, false);
+    else if (cfg == 3) SR_ATTN_LAUNCH(8, 2, true);
+    else SR_ATTN_LAUNCH(4, 2, false);
 #undef SR_ATTN_LAUNCH
     return sr::check_launch("sr_attention(bf16)");
   }

@@ -124,7 +124,12 @@ __device__ __forceinline__ void dma4(const void* gptr, uint32_t lds_base) {
 }
 // Same with a wave-uniform 64-bit base (SGPR pair) + per-lane 32-bit byte offset: the
 // address arithmetic of a tile walk stays on the scalar unit.
+// The base is wave-uniform by contract; readfirstlane pins it to SGPRs where the compiler's
+// divergence analysis lost track (it folds away when the value already lives in SGPRs).
 __device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  const uint64_t a = (uint64_t)(uintptr_t)sbase;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  sbase = (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base)
                : "memory", "m0");
 }

@@ -20,6 +20,13 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <type_traits>
+
+#ifdef SR_ABL_STAGP  // tuning build: stagger + static priority for waves 4-7
+#define SR_ABL_STAG
+#define SR_ABL_PRIO4
+#endif
+
 #include "sr_common.h"
 
 namespace {
@@ -587,28 +594,41 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     tm = tile / ntn;
     tn = tile - tm * ntn;
   }
-  const int m0 = tm * BIG, n0 = tn * BIG;
+  int m0 = tm * BIG, n0 = tn * BIG;
 
   // LDS-DMA sources: wave w, instruction i fills stage rows (w*8 + i)*8 .. +8 of the 512-row
-  // stage (rows < 256: A, else W).
-  const char* src[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int tr = (wave * 8 + i) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
-    if (tr < BIG) {
-      const int r = min(m0 + tr, g.M - 1);
-      src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
-    } else {
-      src[i] = g.W + (int64_t)(n0 + tr - BIG) * g.ldw_b + chunk * 16;
-    }
-  }
+  // stage: waves 0-3 stage A rows m0 + 64w + 8i + lane/8, waves 4-7 W rows n0 + 64(w-4) + 8i +
+  // lane/8.  The 16-B chunk lane&7 goes to chunk ^ ((row>>1)&7) = ^ (4(i&1) + lane/16), so a
+  // piece is a wave-uniform (scalar) base + one of two per-lane 32-bit offsets (no 64-bit vector
+  // pointers: 14 VGPRs fewer).  Only the A waves of a ragged last row tile clamp rows per lane.
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const bool a_wave = wave_u < 4;
+  const int64_t ld_b = a_wave ? g.lda_b : g.ldw_b;
+  // first staged row of this wave (A rows clamped to M - 1 for a ragged last row tile)
+  const int brow0 = a_wave ? min(m0 + wave_u * 64, g.M - 1) : n0 + (wave_u - 4) * 64;
+  const char* const sbase = (a_wave ? g.A : g.W) + (int64_t)brow0 * ld_b;
+  const bool ragged = a_wave && m0 + BIG > g.M;
+  const int rlim = g.M - 1 - brow0;  // ragged: last valid row relative to brow0
+  const uint32_t voA = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (lane >> 4)) << 4));
+  const uint32_t voB = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
   const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
-  auto stage = [&](int kt) {
+  // pieces [i0, i1) of stage kt (one wave-uniform branch per call)
+  auto dma_pieces = [&](int kt, int i0, int i1) {
     const uint32_t base = dst0 + (kt & 1) * STAGE_BIG;
+    const char* sp = sbase + (int64_t)kt * ROWB;
+    if (!ragged) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+      for (int i = i0; i < i1; ++i) sr::dma16_s(sp + (int64_t)i * 8 * ld_b, (i & 1) ? voB : voA, base + i * 1024);
+    } else {
+#pragma unroll
+      for (int i = i0; i < i1; ++i) {
+        const int r = min(i * 8 + (lane >> 3), rlim);
+        const int chunk = (lane & 7) ^ (4 * (i & 1) + (lane >> 4));
+        sr::dma16_s(sp, (uint32_t)(r * ld_b + chunk * 16), base + i * 1024);
+      }
+    }
   };
+  auto stage = [&](int kt) { dma_pieces(kt, 0, 8); };
 
   const int wr = wave >> 2, wc = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
@@ -624,82 +644,127 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0);
-  for (int kt = 0; kt < g.ktiles; ++kt) {
+#ifdef SR_ABL_PRIO4
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" 4)
+  if (wave_u >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  // The k loop, instantiated per wave role (LATE: waves 4-7 under SR_ABL_STAG) so that a role
+  // test never splits an accumulator's register assignment.
+  auto kloop = [&](auto late_c) {
+    constexpr bool LATE = decltype(late_c)::value;
+    uint4 dA[4], dB[2];  // LATE: the k-substep-1 half of the previous tile's last quadrant
+    stage(0);
+    for (int kt = 0; kt < g.ktiles; ++kt) {
 #ifndef SR_ABL_NOWAIT
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
 #endif
 #ifndef SR_ABL_NOBAR
-    sr::barrier_raw();                                  // ... every wave's; all done with kt-1
+      sr::barrier_raw();                                  // ... every wave's; all done with kt-1
 #endif
 #ifdef SR_ABL_NODMA
-    if (kt + 1 < g.ktiles && kt < 1) stage(kt + 1);     // tuning ablation: reuse the first 2 stages
+      if (kt + 1 < g.ktiles && kt < 1) stage(kt + 1);     // tuning ablation: reuse the first 2 stages
 #endif
-    const bool more = kt + 1 < g.ktiles;
-    // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
-    // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
-    // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
-    // measured no better)
-    auto dma_phase = [&](int ph) {
+      const bool more = kt + 1 < g.ktiles;
+      // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
+      // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
+      // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
+      // measured no better)
+      auto dma_phase = [&](int ph) {
 #ifndef SR_ABL_NODMA
-      if (!more || ph >= 2) return;
-      const uint32_t base = dst0 + ((kt + 1) & 1) * STAGE_BIG;
-#pragma unroll
-      for (int i = 4 * ph; i < 4 * ph + 4; ++i) sr::dma16(src[i] + (int64_t)(kt + 1) * ROWB, base + i * 1024);
+        if (!more || ph >= 2) return;
+        dma_pieces(kt + 1, 4 * ph, 4 * ph + 4);
 #else
-      (void)ph;
+        (void)ph;
 #endif
-    };
-    const char* sb = smem + (kt & 1) * STAGE_BIG;
-    // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
-    // the current quadrant's MFMA cluster so their LDS latency hides under it
-    uint4 aX[4][2], aY[4][2], bX[2][2], bY[2][2];
-    auto load_a = [&](uint4 (&a)[4][2], int qm) {
+      };
+      const char* sb = smem + (kt & 1) * STAGE_BIG;
+      // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
+      // the current quadrant's MFMA cluster so their LDS latency hides under it
+      uint4 aX[4][2], aY[4][2], bX[2][2], bY[2][2];
+      auto load_a = [&](uint4 (&a)[4][2], int qm) {
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
-        a[mi][0] = *(const uint4*)(p + coff0);
-        a[mi][1] = *(const uint4*)(p + coff1);
+        for (int mi = 0; mi < 4; ++mi) {
+          const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
+          a[mi][0] = *(const uint4*)(p + coff0);
+          a[mi][1] = *(const uint4*)(p + coff1);
+        }
+      };
+      auto load_b = [&](uint4 (&b)[2][2], int qn) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
+          b[ni][0] = *(const uint4*)(p + coff0);
+          b[ni][1] = *(const uint4*)(p + coff1);
+        }
+      };
+      auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn, int ks1 = 2) {
+#ifndef SR_ABL_PRIO4
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          if (ks < ks1)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+              for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
+#ifndef SR_ABL_PRIO4
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      };
+      if constexpr (LATE) {
+        // waves 4-7 run half a quadrant behind their SIMD partners (waves 0-3): the deferred 8
+        // MFMAs feed the matrix pipe across the barrier while both waves' first fragments load
+        if (kt > 0)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(dB[ni], dA[mi], acc[4 + mi][ni]);
       }
-    };
-    auto load_b = [&](uint4 (&b)[2][2], int qn) {
+      load_a(aX, 0);
+      load_b(bX, 0);
+      load_b(bY, 1);
+      dma_phase(0);
+      mma(aX, bX, 0, 0);
+      load_a(aY, 1);
+      dma_phase(1);
+      mma(aX, bY, 0, 1);
+      load_b(bX, 0);
+      dma_phase(2);
+      mma(aY, bY, 1, 1);
+      dma_phase(3);
+      if constexpr (LATE) {
+        mma(aY, bX, 1, 0, 1);
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
-        b[ni][0] = *(const uint4*)(p + coff0);
-        b[ni][1] = *(const uint4*)(p + coff1);
+        for (int mi = 0; mi < 4; ++mi) dA[mi] = aY[mi][1];
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) dB[ni] = bX[ni][1];
+      } else {
+        mma(aY, bX, 1, 0);
       }
-    };
-    auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn) {
-      __builtin_amdgcn_s_setprio(1);
+    }
+    if constexpr (LATE)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    load_a(aX, 0);
-    load_b(bX, 0);
-    load_b(bY, 1);
-    dma_phase(0);
-    mma(aX, bX, 0, 0);
-    load_a(aY, 1);
-    dma_phase(1);
-    mma(aX, bY, 0, 1);
-    load_b(bX, 0);
-    dma_phase(2);
-    mma(aY, bY, 1, 1);
-    dma_phase(3);
-    mma(aY, bX, 1, 0);
-  }
+        for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(dB[ni], dA[mi], acc[4 + mi][ni]);
+  };
+#ifdef SR_ABL_STAG
+  if (wave_u >= 4) kloop(std::true_type{});
+  else kloop(std::false_type{});
+#else
+  kloop(std::false_type{});
+#endif
 #ifdef SR_ABL_NOEPI
 #pragma unroll
   for (int i = 0; i < 8; ++i)  // tuning ablation: keep every accumulator live, store nothing
 #pragma unroll
     for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
 #else
+#ifdef SR_ABL_SAMEOUT  // tuning ablation: every tile's epilogue targets tile (0, 0) (L2-resident stores)
+  m0 = 0;
+  n0 = 0;
+#endif
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
     if (m0 + BIG <= g.M && !g.lds_epi) {
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
