@@ -777,195 +777,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #endif
 }
 
-// ---------------------------------------------------------------------------------------
-// Persistent 256x256 bf16 GEMM for the bias / erf-GELU epilogues (fc1, DINO QKV; no aux).
-// gemm256_kernel's k loop, but each workgroup walks tiles lin = blockIdx.x + j * gridDim.x
-// (gridDim.x = CUs, a multiple of 8, so every lin of a workgroup maps to its own XCD and
-// sr::xcd_remap keeps each XCD's tiles contiguous) and runs a tile's epilogue inside the NEXT
-// tile's first k-tile, after that k-tile's barrier and after the second stage's LDS-DMA went
-// out.  gfx950 counts stores and loads in one in-order vmcnt, so:
-//   k-tile 0 of tile j+1: barrier; LDS-DMA of stage 1; 32 bf16 stores of tile j (register
-//                         epilogue, bias from LDS); accumulators cleared; MFMAs on stage 0
-//   k-tile 1:             vmcnt(32) = stage 1 landed while tile j's stores stay in flight
-//   k-tile 2:             vmcnt(0)  (stage 2 went out after the stores)
-// so a tile's stores drain under two k-tiles of MFMAs instead of in front of them.  The tile's
-// bias row (1 KB) rides along with its stage 0 as 4 LDS-DMA dword pieces into a 2-slot LDS area.
-// A ragged last row tile stores under row guards and the k-tile after it waits vmcnt(0).
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256p_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG + 2048];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int ntn = g.N / BIG, ntm = (g.M + BIG - 1) / BIG, ntiles = ntn * ntm;
-  const bool a_wave = wave_u < 4;
-  const int64_t ld_b = a_wave ? g.lda_b : g.ldw_b;
-  const uint32_t voA = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (lane >> 4)) << 4));
-  const uint32_t voB = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
-  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
-  const uint32_t bias_lds = sr::lds_addr(smem) + 2 * STAGE_BIG;
-
-  struct Tile {
-    int m0, n0, rlim;
-    const char* sbase;
-    bool ragged;
-  };
-  auto tile_of = [&](int lin) {
-    Tile t;
-    const int tile = sr::xcd_remap(lin, ntiles);
-    const int tm = tile / ntn;
-    t.m0 = tm * BIG;
-    t.n0 = (tile - tm * ntn) * BIG;
-    const int brow0 = a_wave ? min(t.m0 + wave_u * 64, g.M - 1) : t.n0 + (wave_u - 4) * 64;
-    t.sbase = (a_wave ? g.A : g.W) + (int64_t)brow0 * ld_b;
-    t.ragged = t.m0 + BIG > g.M;
-    t.rlim = g.M - 1 - brow0;
-    return t;
-  };
-  auto dma_pieces = [&](const Tile& t, int kt, int i0, int i1, int buf) {
-    const uint32_t base = dst0 + buf * STAGE_BIG;
-    const char* sp = t.sbase + (int64_t)kt * ROWB;
-    if (!(a_wave && t.ragged)) {
-#pragma unroll
-      for (int i = i0; i < i1; ++i) sr::dma16_s(sp + (int64_t)i * 8 * ld_b, (i & 1) ? voB : voA, base + i * 1024);
-    } else {
-#pragma unroll
-      for (int i = i0; i < i1; ++i) {
-        const int r = min(i * 8 + (lane >> 3), t.rlim);
-        const int chunk = (lane & 7) ^ (4 * (i & 1) + (lane >> 4));
-        sr::dma16_s(sp, (uint32_t)(r * ld_b + chunk * 16), base + i * 1024);
-      }
-    }
-  };
-  auto bias_dma = [&](const Tile& t, int slot) {  // waves 0-3: 64 bias floats each
-    if (wave_u < 4) sr::dma4(g.ep.bias + t.n0 + wave_u * 64 + lane, bias_lds + slot * 1024 + wave_u * 256);
-  };
-
-  const int wr = wave >> 2, wc = wave & 3;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int swz = lr >> 1;
-  const int arow = (wr * 128 + lr) * ROWB;
-  const int brow = (BIG + wc * 64 + lr) * ROWB;
-  const int coff0 = ((0 + lg) ^ swz) * 16, coff1 = ((4 + lg) ^ swz) * 16;
-
-  f32x4 acc[8][4];
-  auto clear = [&]() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-  // register epilogue of tile t from the bias in LDS slot `slot`: 32 x 8-B bf16 stores per lane
-  auto store_tile = [&](const Tile& t, int slot) {
-    const char* bl = smem + 2 * STAGE_BIG + slot * 1024 + (wc * 64 + 4 * lg) * 4;
-    f32x4 bs[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) bs[ni] = *(const f32x4*)(bl + ni * 64);
-    bf16* out = (bf16*)g.out + (int64_t)(t.m0 + wr * 128 + lr) * g.ldo + t.n0 + wc * 64 + 4 * lg;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      if (t.ragged && t.m0 + wr * 128 + mi * 16 + lr >= g.M) continue;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        f32x4 v = acc[mi][ni] + bs[ni];
-        if constexpr (EPI == SR_EPI_BIAS_GELU) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = sr::gelu_erf_fast(v[r]);
-        }
-        const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        *(bf16x4*)(out + (int64_t)mi * 16 * g.ldo + ni * 16) = o;
-      }
-    }
-  };
-
-  int lin = blockIdx.x;
-  if (lin >= ntiles) return;
-  Tile cur = tile_of(lin), prev = cur;
-  bool have_prev = false;
-  int G = 0, j = 0;  // k-tiles run so far (stage buffer parity), tiles started (bias slot parity)
-  clear();
-  dma_pieces(cur, 0, 0, 8, 0);
-  bias_dma(cur, 0);
-  for (;;) {
-    const int nlin = lin + gridDim.x;
-    const bool has_next = nlin < ntiles;
-    const Tile nxt = has_next ? tile_of(nlin) : cur;
-    for (int kt = 0; kt < g.ktiles; ++kt, ++G) {
-      if (kt == 1 && have_prev && !prev.ragged) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sr::barrier_raw();
-      const bool epi_now = kt == 0 && have_prev;
-      if (epi_now) {
-        if (g.ktiles > 1) {
-          dma_pieces(cur, 1, 0, 8, (G + 1) & 1);
-        } else if (has_next) {
-          dma_pieces(nxt, 0, 0, 8, (G + 1) & 1);
-          bias_dma(nxt, (j + 1) & 1);
-        }
-        store_tile(prev, (j - 1) & 1);
-        clear();
-      }
-      __builtin_amdgcn_sched_barrier(0);  // no fragment load hoisted into the epilogue's registers
-      // the next stage (this tile's kt+1, or the next tile's stage 0 + bias) goes out 4 pieces
-      // ahead of each of the first two MFMA phases, as in gemm256_kernel
-      auto dma_phase = [&](int ph) {
-        if (epi_now || ph >= 2) return;
-        if (kt + 1 < g.ktiles) {
-          dma_pieces(cur, kt + 1, 4 * ph, 4 * ph + 4, (G + 1) & 1);
-        } else if (has_next) {
-          dma_pieces(nxt, 0, 4 * ph, 4 * ph + 4, (G + 1) & 1);
-          if (ph == 1) bias_dma(nxt, (j + 1) & 1);
-        }
-      };
-      const char* sb = smem + (G & 1) * STAGE_BIG;
-      uint4 aX[4][2], aY[4][2], bX[2][2], bY[2][2];
-      auto load_a = [&](uint4 (&a)[4][2], int qm) {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
-          a[mi][0] = *(const uint4*)(p + coff0);
-          a[mi][1] = *(const uint4*)(p + coff1);
-        }
-      };
-      auto load_b = [&](uint4 (&b)[2][2], int qn) {
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
-          b[ni][0] = *(const uint4*)(p + coff0);
-          b[ni][1] = *(const uint4*)(p + coff1);
-        }
-      };
-      auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
-        __builtin_amdgcn_s_setprio(0);
-      };
-      load_a(aX, 0);
-      load_b(bX, 0);
-      load_b(bY, 1);
-      dma_phase(0);
-      mma(aX, bX, 0, 0);
-      load_a(aY, 1);
-      dma_phase(1);
-      mma(aX, bY, 0, 1);
-      load_b(bX, 0);
-      mma(aY, bY, 1, 1);
-      mma(aY, bX, 1, 0);
-    }
-    prev = cur;
-    have_prev = true;
-    if (!has_next) break;
-    cur = nxt;
-    lin = nlin;
-    ++j;
-  }
-  store_tile(prev, j & 1);
-}
-
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
@@ -999,22 +810,6 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
     // problems (frame-sharded ranks, small scenes) keep 4x more 128x128 workgroups.
     const long tiles256 = (long)(a.N / BIG) * ((a.M + BIG - 1) / BIG);
     if (!no_big && a.N % BIG == 0 && tiles256 >= 512) {
-      static const int persist = [] {
-        const char* e = getenv("SR_GEMM_PERSIST");
-        return e ? atoi(e) : 0;
-      }();
-      if (persist && (epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_GELU) && a.ep.bias && !a.ep.aux && a.ldo % 4 == 0) {
-        static const int cus = [] {
-          int d = 0, n = 0;
-          (void)hipGetDevice(&d);
-          (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
-          return n;
-        }();
-        const int nwg = (int)std::min<long>(tiles256, (long)(cus / 8) * 8);
-        if (epi == SR_EPI_BIAS) hipLaunchKernelGGL((gemm256p_kernel<SR_EPI_BIAS>), dim3(nwg), dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((gemm256p_kernel<SR_EPI_BIAS_GELU>), dim3(nwg), dim3(512), 0, s, a);
-        return sr::check_launch("sr_gemm(256, persistent)");
-      }
       switch (epi) {
         case SR_EPI_BIAS: return launch256<SR_EPI_BIAS>(a, s);
         case SR_EPI_BIAS_GELU: return launch256<SR_EPI_BIAS_GELU>(a, s);
