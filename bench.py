@@ -100,6 +100,23 @@ KERNEL_OF_TAG = {
     "attn_frame": "attn_bf16_kernel<4, 2, 0, false>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
     "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
 }
+# GEMM output width per timer class: the 256x256 kernel runs only when it yields >= 512 tiles
+# (sr_gemm.hip dispatch); smaller row counts (C2) run the 128x128 gemm_kernel
+_GEMM_N = {"gemm_bias": 3072, "gemm_gelu": 4096, "gemm_resid": 1024, "gemm_qkv": 3072, "gemm_patch": 1024}
+_GEMM_EPI = {"gemm_bias": 0, "gemm_gelu": 1, "gemm_resid": 2, "gemm_qkv": 3, "gemm_patch": 4}
+
+
+def kernel_of_tag(tag: str, views: int, img: int):
+    """rocprofv3 row name of the kernel a timer class launches at this workload."""
+    if tag in _GEMM_N:
+        rows = 2 * views * ((img // 14) ** 2 + 5)
+        if tag == "gemm_patch":
+            rows = 2 * views * (img // 14) ** 2
+        if (_GEMM_N[tag] // 256) * ((rows + 255) // 256) < 512:
+            return f"gemm_kernel<__bf16, {_GEMM_EPI[tag]}, false>"
+    return KERNEL_OF_TAG.get(tag)
+
+
 TRAFFIC_FILES = [os.path.join(REPO, "profiles", f) for f in
                  ("r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
 
@@ -257,7 +274,7 @@ def main():
         dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
         b = breakdown[dom]
         achieved = b["tflops"]
-        kern = KERNEL_OF_TAG.get(dom) if use_bf16 else None
+        kern = kernel_of_tag(dom, n, args.img) if use_bf16 else None
         if fp8 and dom == "attn_global":
             # half the attention flops (q.k^T) at the fp8 rate (2x bf16), half (P.V) at the bf16 rate
             if args.fp8_global == "qkv":  # every attention flop at the fp8 rate
