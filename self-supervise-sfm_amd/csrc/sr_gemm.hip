@@ -355,6 +355,32 @@ __device__ __forceinline__ void resid_full(const GemmArgs& g, f32x4 (&acc)[8][4]
   }
 }
 
+// bias (+ erf-GELU) -> bf16 for a full 256x256 tile (every row < M; N % 256 == 0 here; no aux):
+// the guarded produce/emit form compiles to an exec branch around every one of the 32 stores
+// per lane; here they are plain stores with the math of the next vectors in between.
+template <int EPI>
+__device__ __forceinline__ void bias_full(const GemmArgs& g, f32x4 (&acc)[8][4], int rowbase, int colw, int lr,
+                                          int lg) {
+  const sr_gemm_epi& ep = g.ep;
+  f32x4 bs[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+    bs[ni] = ep.bias ? *(const f32x4*)(ep.bias + colw + ni * 16 + 4 * lg) : f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16* ob = (bf16*)g.out + (int64_t)(rowbase + lr) * g.ldo + colw + 4 * lg;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      f32x4 v = acc[mi][ni] + bs[ni];
+      if constexpr (EPI == SR_EPI_BIAS_GELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = sr::gelu_erf_fast(v[r]);
+      }
+      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *(bf16x4*)(ob + (int64_t)mi * 16 * g.ldo + ni * 16) = o;
+    }
+}
+
 // 256x256 bf16 epilogue staged through the (free) stage buffers so that global traffic is
 // whole rows with 16 B per lane (the register epilogue's per-lane 8-B stores touch 16 rows
 // per wave instruction).  bf16 outputs: the whole 256x256 tile (128 KiB, 512-B rows);
@@ -408,6 +434,24 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4
     });
     sr::barrier_raw();
     bf16* out = (bf16*)g.out;
+#ifndef SR_ABL_GUARDED
+    if (m0 + 256 <= g.M) {
+      // full tile: all 16 row reads in flight, then 16 unguarded stores (the guarded form waits
+      // out each read's LDS latency behind an exec branch)
+      uint4 v[16];
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int rl = wave * 32 + it * 2 + (lane >> 5), c = lane & 31;
+        v[it] = *(const uint4*)(smem + rl * 512 + ((c ^ (rl & 15)) << 4));
+      }
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int rl = wave * 32 + it * 2 + (lane >> 5), c = lane & 31;
+        *(uint4*)(out + (int64_t)(m0 + rl) * g.ldo + n0 + c * 8) = v[it];
+      }
+      return;
+    }
+#endif
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int rl = wave * 32 + it * 2 + (lane >> 5), c = lane & 31, row = m0 + rl;
@@ -771,6 +815,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
       return;
     }
+  }
+  if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
+#ifndef SR_ABL_GUARDED
+    if (m0 + BIG <= g.M && !g.lds_epi && !g.ep.aux) {
+      bias_full<EPI>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+      return;
+    }
+#endif
   }
   if (g.lds_epi) epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
   else epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
