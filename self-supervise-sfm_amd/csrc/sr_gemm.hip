@@ -832,11 +832,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
+  // tile order: column-major inside groups of 4 row tiles for the wide outputs (fc1, QKV:
+  // N >= 3072; kbench A/B fc1 -3 %, qkv -1.5 %), row-major for N = 1024 (proj / fc2, where
+  // grouping measured neutral to +1-2 % slower).  SR_GEMM_GROUP_M=g overrides (<= 1: row-major).
   static const int group_m = [] {
     const char* e = getenv("SR_GEMM_GROUP_M");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
-  a.group_m = group_m;
+  a.group_m = group_m >= 0 ? group_m : (a.N >= 3072 ? 4 : 0);
   hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
   return sr::check_launch("sr_gemm(256)");
 }
