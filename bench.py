@@ -11,11 +11,21 @@ rule (pretrained weights are not available offline).
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Multi-GPU: one process per GPU; the ONE 32-view scene is sharded by frame across the
-ranks (Aggregator.set_frame_sharding: local DINO / frame / MLP work, RCCL all-gathers
-of anchor K/V for the global block and of the anchor-subsample K/V for the reloc
-block, replicated camera head).  value = the scene's views / max-over-ranks time,
-scaling "strong" (total work fixed as N grows).
+Multi-GPU: one process per GPU.  Launched by torch.distributed.run (WORLD_SIZE set) the
+ranks come from the environment; launched plainly with --gpus N > 1, bench.py starts N
+worker processes itself (fresh interpreters, before anything touches the GPU — the
+reference's mp.spawn(train_worker, nprocs=world_size), train/train_imc.py:555-576) with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 set, and exits with the worst
+worker exit code.  Each worker joins an RCCL ("nccl") process group; rank 0 reports
+n_gpus = the group's world size and ``ranks_seen`` = the all-gathered (rank, device,
+PCI bus) list, so the JSON line itself shows which devices took part.
+The ONE 32-view scene is sharded by frame across the ranks
+(Aggregator.set_frame_sharding: local DINO / frame / MLP work, RCCL all-gathers of
+anchor K/V for the global block and of the anchor-subsample K/V for the reloc block,
+replicated camera head).  value = the scene's views / max-over-ranks time, scaling
+"strong" (total work fixed as N grows).  --launch-only runs the launcher, the process
+group and the ranks_seen report without the model (gloo when no GPU is visible: the
+CPU test of the launcher).
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with a
 ``roofline`` object for the dominant kernel class (live HIP-event timing inside
@@ -166,17 +176,19 @@ def build_model(device, seed_rule=True):
     return model.to(device), sd
 
 
-def cpu_baseline(sd, img: int, n_views: int):
-    """The CPU oracle (oracle/sfm_oracle.py, a port of the reference path: dense reloc mask,
-    scatter reassembly, fp32) on a bounded sample: one full forward of an n_views scene
-    (2*n_views frames, the headline's per-view structure at a size that runs in ~10-30 s).
-    Threads = the physical cores of this process's CPU share (OMP_NUM_THREADS caps it on the
-    GPU box, whose os.cpu_count() is the whole machine)."""
-    from oracle import sfm_oracle as O
+def _cpu_threads():
     model, phys, logical = host_cpu()
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = min(phys, cap) if cap > 0 else phys
-    torch.set_num_threads(threads)
+    note = (f"min(physical cores {phys}, OMP_NUM_THREADS {cap}): the GPU box allots this process a share of the "
+            "host's CPUs per GPU, and os.cpu_count() counts the whole machine") if cap > 0 else "physical cores"
+    return model, phys, logical, threads, note
+
+
+def cpu_full_forward(sd, img: int, n_views: int) -> float:
+    """Seconds for one full oracle forward (aggregator + camera head + pose decode) of an
+    n_views scene: the cross-check of the per-layer estimate below at a size that runs whole."""
+    from oracle import sfm_oracle as O
     g = torch.Generator().manual_seed(n_views)
     x = torch.rand(n_views, 3, img, img, generator=g)
     images = torch.cat([x, x])[None]
@@ -184,15 +196,172 @@ def cpu_baseline(sd, img: int, n_views: int):
     sub = O.draw_subsample_indices(torch.Generator().manual_seed(0), 24, 1, n_views, npatch, min(300, npatch))
     t0 = time.perf_counter()
     O.hot_path_forward(sd, O.AggCfg(), images, list(range(n_views)), list(range(n_views, 2 * n_views)), 300, sub)
-    dt = time.perf_counter() - t0
-    return {"value": n_views / dt, "unit": "views/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "physical_cores": phys, "os_cpu_count": logical,
-            "threads_note": (f"min(physical cores {phys}, OMP_NUM_THREADS {cap}): the GPU box allots this "
-                             "process a share of the host's CPUs per GPU, and os.cpu_count() counts the whole "
-                             "machine") if cap > 0 else "physical cores",
-            "sample": f"1 full fp32 forward of a {n_views}-view scene @{img}px ({2 * n_views} frames; "
-                      f"aggregator+camera head+pose decode, the oracle port of the reference path) on the host "
-                      f"CPU, {threads} threads, {dt:.1f} s"}
+    return time.perf_counter() - t0
+
+
+def cpu_forward_by_layer(sd, img: int, n_views: int, depth: int = 24):
+    """Seconds for one oracle forward of the n_views headline scene, timed per stack: the
+    aggregator's 24 layers all have the same shapes, so one layer of each stack is run on
+    tensors of the headline shape and multiplied by 24 (aggregator.py:242-433 order):
+      patch embed (conv + cls + pos-embed + registers) of 2N frames, once;
+      DINO block [2N, P, C] (eps 1e-6, no RoPE), x24, and the final DINO LayerNorm;
+      frame block [2N, P, C] (qk-norm + RoPE), x24;
+      the dense reloc mask (aggregator.py:302-311), once per forward as the reference builds it;
+      subsample gather + global_reloc block over [N*P' ; N*P] tokens with that mask, x24;
+      global block over the N*P anchor tokens, x24;
+      reassembly into a fresh ones() tensor with two scatters (aggregator.py:393-399), x24;
+      camera head (4 iterations x 4 trunk blocks, fp32) + pose decode on the 2N camera tokens, once.
+    Returns (total seconds, {part: seconds per application})."""
+    from oracle import sfm_oracle as O
+    pre = "aggregator."
+    S, n = 2 * n_views, n_views
+    hp = img // 14
+    npatch, psi, C = hp * hp, 5, 1024
+    P, rank = npatch + psi, min(300, npatch)
+    Pp = rank + psi
+    g = torch.Generator().manual_seed(n_views)
+    parts = {}
+
+    def timed(name, fn):
+        t0 = time.perf_counter()
+        r = fn()
+        parts[name] = time.perf_counter() - t0
+        return r
+
+    with torch.no_grad():
+        imgs = torch.rand(S, 3, img, img, generator=g)
+        mean = torch.tensor(O.RESNET_MEAN).view(1, 3, 1, 1)
+        std = torch.tensor(O.RESNET_STD).view(1, 3, 1, 1)
+        x = timed("patch_embed", lambda: O.dino_embed(sd, pre + "patch_embed.", (imgs - mean) / std, 14))
+        x = timed("dino_block", lambda: O.block(sd, pre + "patch_embed.blocks.0.", x, 16, 1e-6))
+        timed("dino_norm", lambda: O.layer_norm(x, sd[pre + "patch_embed.norm.weight"],
+                                                sd[pre + "patch_embed.norm.bias"], 1e-6))
+        tokens = torch.randn(S, P, C, generator=g)
+        yy, xx = torch.meshgrid(torch.arange(hp), torch.arange(hp), indexing="ij")
+        grid = torch.stack([yy.reshape(-1), xx.reshape(-1)], dim=-1) + 1
+        pos = torch.cat([torch.zeros(psi, 2, dtype=torch.long), grid], dim=0)[None].expand(S, P, 2).contiguous()
+        tokens = timed("frame_block", lambda: O.block(sd, pre + "frame_blocks.0.", tokens, 16, 1e-5, pos=pos,
+                                                      qk_norm=True, rope_base=100.0))
+        mask = timed("reloc_mask", lambda: O.reloc_mask(S, n, n, P, psi, rank))
+        sub_idx = O.draw_subsample_indices(torch.Generator().manual_seed(0), 1, 1, n, npatch, rank)[0]
+
+        def reloc():
+            fo = tokens.view(1, S, P, C)
+            anc, anc_pos = fo[:, :n], pos.view(1, S, P, 2)[:, :n]
+            sel = sub_idx[..., :rank] + psi
+            gt = torch.gather(anc, 2, sel[..., None].expand(1, n, rank, C))
+            gp = torch.gather(anc_pos, 2, sel[..., None].expand(1, n, rank, 2))
+            sub = torch.cat([anc[:, :, :psi], gt], dim=2).reshape(1, n * Pp, C)
+            sub_pos = torch.cat([anc_pos[:, :, :psi], gp], dim=2).reshape(1, n * Pp, 2)
+            seq = torch.cat([sub, fo[:, n:].reshape(1, n * P, C)], dim=1)
+            sp = torch.cat([sub_pos, pos.view(1, S, P, 2)[:, n:].reshape(1, n * P, 2)], dim=1)
+            return O.block(sd, pre + "global_reloc_blocks.0.", seq, 16, 1e-5, pos=sp, mask=mask, qk_norm=True,
+                           rope_base=100.0)[:, n * Pp:]
+
+        reloc_out = timed("reloc_block", reloc)
+        del mask
+        glob = timed("global_block", lambda: O.block(
+            sd, pre + "global_blocks.0.", tokens.view(1, S, P, C)[:, :n].reshape(1, n * P, C), 16, 1e-5,
+            pos=pos.view(1, S, P, 2)[:, :n].reshape(1, n * P, 2), qk_norm=True, rope_base=100.0))
+
+        def reassemble():
+            new = torch.ones(1, S, P, C)
+            new[:, :n] = glob.view(1, n, P, C)
+            new[:, n:] = reloc_out.view(1, n, P, C)
+            return new
+
+        timed("reassembly", reassemble)
+        feats_last = torch.randn(1, n, P, 2 * C, generator=g)
+        cam_last = torch.randn(1, n, 2 * C, generator=g)
+
+        def head():
+            poses = O.camera_head_forward(sd, feats_last, cam_last)
+            return O.pose_encoding_to_extri_intri(poses[-1], (img, img))
+
+        timed("camera_head_pose", head)
+    per_layer = ("dino_block", "frame_block", "reloc_block", "global_block", "reassembly")
+    total = sum(parts[k] * (depth if k in per_layer else 1) for k in parts)
+    return total, parts
+
+
+def cpu_baseline(sd, img: int, n_views: int, cross_views: int = 4):
+    """The CPU oracle (oracle/sfm_oracle.py, a port of the reference path: dense reloc mask,
+    scatter reassembly, fp32 torch ops) on the headline scene, estimated per layer
+    (cpu_forward_by_layer: one layer of each stack at the N-view shapes x 24 + the once-per-
+    forward parts), with one full forward of a small scene as a cross-check.  Threads = the
+    physical cores of this process's CPU share (OMP_NUM_THREADS caps it on the GPU box, whose
+    os.cpu_count() is the whole machine)."""
+    model, phys, logical, threads, note = _cpu_threads()
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    est, parts = cpu_forward_by_layer(sd, img, n_views)
+    wall = time.perf_counter() - t0
+    out = {"value": n_views / est, "unit": "views/s", "cores": threads, "kind": "port",
+           "cpu_model": model, "physical_cores": phys, "os_cpu_count": logical, "threads_note": note,
+           "sample": f"N={n_views} @{img}px ({2 * n_views} frames, fp32 oracle port of the reference path), one "
+                     f"layer of each stack timed at the N={n_views} shapes x 24 layers + patch embed, dense reloc "
+                     f"mask, camera head and pose decode once: {est:.1f} s per forward estimated from {wall:.1f} s "
+                     f"of CPU work on {threads} threads",
+           "seconds_per_part": {k: round(v, 3) for k, v in parts.items()}}
+    if cross_views:
+        dt = cpu_full_forward(sd, img, cross_views)
+        est_small, _ = cpu_forward_by_layer(sd, img, cross_views)
+        out["cross_check"] = {"views": cross_views, "full_forward_s": round(dt, 2),
+                              "per_layer_estimate_s": round(est_small, 2),
+                              "views_per_s_full_forward": round(cross_views / dt, 4)}
+    return out
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(n: int, argv) -> int:
+    """Start n bench.py worker processes (one per GPU) and wait for them.  The parent never
+    initialises the GPU: the world size comes from --gpus, not from a device query.  A worker
+    that fails ends the others (their exact PIDs); the parent returns the worst exit code."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:  # a failed rank would leave its peers waiting in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc if rc >= 0 else 128 - rc
+
+
+def ranks_report(device):
+    """(rank, local device, PCI bus, host) of every rank, all-gathered over the process group."""
+    import socket
+    me = {"rank": dist.get_rank() if dist.is_initialized() else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "device": str(device), "host": socket.gethostname()}
+    if device.type == "cuda":
+        p = torch.cuda.get_device_properties(device)
+        me["pci_bus"] = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:" \
+                        f"{getattr(p, 'pci_device_id', 0):02x}"
+        me["gpu"] = p.name
+    if not dist.is_initialized():
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
 
 
 def main():
@@ -203,21 +372,45 @@ def main():
     ap.add_argument("--views", type=int, default=32)
     ap.add_argument("--img", type=int, default=518)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-views", type=int, default=4)
+    ap.add_argument("--cpu-views", type=int, default=4,
+                    help="views of the full-forward cross-check of the per-layer CPU estimate (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
                     help="BASELINE C5: the global blocks' q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 "
                          "e4m3; everything else bf16")
+    ap.add_argument("--launch-only", action="store_true",
+                    help="launcher / process-group / ranks_seen check without the model (gloo if no GPU)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local if world > 1 else 0)
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; reporting the process group's size",
+              file=sys.stderr)
+    on_gpu = torch.cuda.is_available()
+    if not on_gpu and not args.launch_only:
+        raise SystemExit("bench.py: no ROCm GPU visible (the HIP path has no CPU fallback); "
+                         "--launch-only checks the launcher alone")
+    device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+    if on_gpu:
+        torch.cuda.set_device(device)
+    use_pg = "WORLD_SIZE" in os.environ  # torchrun / the launcher, any world size
+    if use_pg:
+        dist.init_process_group("nccl" if on_gpu else "gloo")
+    seen = ranks_report(device)
+    if args.launch_only:
+        if rank == 0:
+            print(json.dumps({"launch_only": True, "n_gpus": dist.get_world_size() if use_pg else 1,
+                              "backend": dist.get_backend() if use_pg else None, "ranks_seen": seen}))
+        if use_pg:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from sailrecon_amd import ops
 
@@ -303,7 +496,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline({k: v for k, v in sd.items()}, args.img, args.cpu_views)
+        cpu = cpu_baseline({k: v for k, v in sd.items()}, args.img, n, args.cpu_views)
 
     if rank == 0:
         tflop = algorithmic_tflop(n, args.img)
@@ -311,7 +504,9 @@ def main():
             "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px",
             "value": total_views / dt,
             "unit": "views/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if use_pg else 1,
+            "backend": dist.get_backend() if use_pg else None,
+            "ranks_seen": seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -331,7 +526,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

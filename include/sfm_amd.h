@@ -123,7 +123,7 @@ int sr_gemm_splitk(sr_stream_t stream, int dtype, int epilogue, const void* A, i
  * mask_mode SR_MASK_CAMERA (l1 == 0): row i sees key j iff j < n_anchor or j == i.
  * dtype SR_BF16: MFMA kernel, head_dim 64.  SR_F32: exact-f32 kernel, head_dim 64|128.
  * ---------------------------------------------------------------------- */
-enum sr_mask_mode { SR_MASK_NONE = 0, SR_MASK_CAMERA = 1 };
+enum sr_mask_mode { SR_MASK_NONE = 0, SR_MASK_CAMERA = 1, SR_MASK_DENSE = 2, SR_MASK_ADD = 3 };
 
 typedef struct sr_attn_desc {
   const void* q;
@@ -160,6 +160,15 @@ typedef struct sr_attn_desc {
                   and k0_bstride = l0 the items split ONE query set's keys into chunks whose
                   normalised partial outputs (o_bstride apart) and LSEs merge with sr_attn_merge_n
                   (key-split attention: more workgroups when the queries alone cannot fill the chip) */
+  /* SR_MASK_DENSE / SR_MASK_ADD (f32 path): Attention.forward's general attn_mask
+     (attention.py:70,103-109 — F.scaled_dot_product_attention(q, k, v, attn_mask)).  Element
+     (item b, head h, query row i, key j; j the logical key index: segment 0 then segment 1) at
+     mask + b*mask_bstride + h*mask_hstride + i*mask_ld + j (element strides; 0 = broadcast).
+     DENSE: uint8, nonzero = attend (SDPA's bool mask); ADD: fp32 added to scale*q.k before the
+     softmax (SDPA's float mask; -inf = masked).  A row with no attended key yields NaN like
+     SDPA's math path. */
+  const void* mask;
+  int64_t mask_bstride, mask_hstride, mask_ld;
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */

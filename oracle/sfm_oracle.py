@@ -122,15 +122,21 @@ def dino_pos_embed(sd: SD, pre: str, h_img: int, w_img: int, patch: int, npatch:
     return torch.cat((cls_pe.unsqueeze(0), out), dim=1)
 
 
-def dino_forward(sd: SD, pre: str, img: Tensor, patch: int, depth: int, heads: int) -> Tensor:
-    """forward_features -> x_norm_patchtokens, vision_transformer.py:242-307."""
+def dino_embed(sd: SD, pre: str, img: Tensor, patch: int) -> Tensor:
+    """prepare_tokens_with_masks, vision_transformer.py:242-259: patch conv, cls, pos-embed, registers."""
     x = F.conv2d(img, sd[pre + "patch_embed.proj.weight"], sd[pre + "patch_embed.proj.bias"], stride=patch)
     x = x.flatten(2).transpose(1, 2)
     B = x.shape[0]
     x = torch.cat((sd[pre + "cls_token"].expand(B, -1, -1), x), dim=1)
     x = x + dino_pos_embed(sd, pre, img.shape[2], img.shape[3], patch, x.shape[1] - 1)
     reg = sd[pre + "register_tokens"]
-    x = torch.cat((x[:, :1], reg.expand(B, -1, -1), x[:, 1:]), dim=1)
+    return torch.cat((x[:, :1], reg.expand(B, -1, -1), x[:, 1:]), dim=1)
+
+
+def dino_forward(sd: SD, pre: str, img: Tensor, patch: int, depth: int, heads: int) -> Tensor:
+    """forward_features -> x_norm_patchtokens, vision_transformer.py:242-307."""
+    x = dino_embed(sd, pre, img, patch)
+    reg = sd[pre + "register_tokens"]
     for i in range(depth):
         x = block(sd, f"{pre}blocks.{i}.", x, heads, 1e-6)
     x = layer_norm(x, sd[pre + "norm.weight"], sd[pre + "norm.bias"], 1e-6)
@@ -151,6 +157,14 @@ def build_allow_block(L: int, la: Sequence[int], lb: Sequence[int]) -> Tensor:
         allow[ib[:, None], ia[None, :]] = True
         allow[ib, ib] = True
     return allow
+
+
+def reloc_mask(S: int, Na: int, Nq: int, P: int, psi: int, rank: int) -> Tensor:
+    """The global_reloc block's dense boolean mask (True = attend), aggregator.py:302-311."""
+    allow = build_allow_block(S, list(range(Na)), [i + Na for i in range(Nq)])
+    full = allow.repeat_interleave(P, 0).repeat_interleave(P, 1)
+    cut = (P - psi - rank) * Na
+    return full[cut:, cut:][None, None]
 
 
 def draw_subsample_indices(generator: torch.Generator, depth: int, batch: int, n_anchor: int,
@@ -207,11 +221,7 @@ def aggregator_forward(sd: SD, cfg: AggCfg, images: Tensor, no_reloc: List[int],
     P = tokens.shape[1]
     P_prime = min(rank + psi, P)
 
-    # dense boolean mask (True = attend), :302-311
-    allow = build_allow_block(S, list(range(Na)), [i + Na for i in range(Nq)])
-    full = allow.repeat_interleave(P, 0).repeat_interleave(P, 1)
-    cut = (P - psi - rank) * Na
-    mask = full[cut:, cut:][None, None]
+    mask = reloc_mask(S, Na, Nq, P, psi, rank)
 
     # positions, :313-328 + PositionGetter rope.py:40-66
     hp, wp = H // cfg.patch, W // cfg.patch
@@ -412,8 +422,9 @@ def _fusion(sd: SD, pre: str, x0: Tensor, x1: Optional[Tensor], size) -> Tensor:
 
 def dpt_forward(sd: SD, pre: str, tokens: Dict[int, Tensor], images: Tensor, patch_start: int,
                 layers: Sequence[int] = (4, 11, 17, 23), activation: str = "inv_log",
-                conf_activation: str = "expp1", patch: int = 14) -> Tuple[Tensor, Tensor]:
-    """DPTHead.forward (dpt_head.py:151-298) for all frames at once; returns (preds, conf)."""
+                conf_activation: str = "expp1", patch: int = 14, feature_only: bool = False):
+    """DPTHead.forward (dpt_head.py:151-298) for all frames at once; returns (preds, conf), or with
+    feature_only the fused feature map [B, S, features, H, W] (dpt_head.py:123-126,286-287)."""
     B, S, _, H, W = images.shape
     ph, pw = H // patch, W // patch
     aspect = W / H
@@ -438,6 +449,8 @@ def dpt_forward(sd: SD, pre: str, tokens: Dict[int, Tensor], images: Tensor, pat
     out = _conv(sd, pre + "scratch.output_conv1", out)
     out = F.interpolate(out, size=(ph * patch, pw * patch), mode="bilinear", align_corners=True)
     out = _add_pos(out, aspect)
+    if feature_only:
+        return out.view(B, S, *out.shape[1:])
     out = F.relu(_conv(sd, pre + "scratch.output_conv2.0", out))
     out = _conv(sd, pre + "scratch.output_conv2.2", out)
     fmap = out.permute(0, 2, 3, 1)

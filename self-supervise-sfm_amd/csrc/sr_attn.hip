@@ -90,12 +90,7 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
     //   K/V (segment 0, 2.5 MB per head at C3).
     const int nq = gridDim.x, nh = gridDim.y, nb = gridDim.z;
     const int lin = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
-#ifdef SR_ABL_NOREMAP
-    const bool remap = KIND == 1;
-#else
-    const bool remap = true;
-#endif
-    if (remap) {
+    {
       const int tile = sr::xcd_remap(lin, nq * nh * nb);
       qt = tile % nq;
       if constexpr (KIND == 1) {
@@ -237,14 +232,12 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   bf16x8 one_a;
 #pragma unroll
   for (int j = 0; j < 8; ++j) one_a[j] = (bf16)((hi == 0 && j < 2) ? 1.f : 0.f);
-#ifndef SR_ABL_VSUM
   // Row sums of P on the matrix pipe: one v_mfma_f32_16x16x32_bf16 per 16-key P fragment with
   // A = ones in row 0 at k-slots {0-7, 16-23} and row 1 at {8-15, 24-31}, so that with P's
   // fragment as B (lane l: 8 keys of query l % 32) D[0][n] sums query n and D[1][n] query n + 16.
   // 4 MFMAs (64 pipe cycles, 32 issue) replace 32 v_add_f32 (128 issue cycles) per q-block and
   // tile in a VALU-issue-bound loop (global / reloc +3 %).  The sum runs over the bf16-rounded P
-  // that the P.V product uses, so numerator and denominator see the same P (SR_ABL_VSUM: the
-  // fp32 VALU sums)
+  // that the P.V product uses, so numerator and denominator see the same P
   bf16x8 sum_a;
 #pragma unroll
   for (int j = 0; j < 8; ++j)
@@ -252,14 +245,12 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   f32x4 lacc[QB];
 #pragma unroll
   for (int b = 0; b < QB; ++b) lacc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#endif
-  float m_run[QB], l_run[QB];  // m_run == float(m_hi) + float(m_lo); l_run: this lane's partial sums
+  float m_run[QB];  // m_run == float(m_hi) + float(m_lo)
   bf16x8 m_b[QB];
   f32x16 o[QB][2];
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     m_run[b] = 0.f;
-    l_run[b] = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) m_b[b][j] = (bf16)0.f;
 #pragma unroll
@@ -361,14 +352,11 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
           const float m_new = (float)nhi + (float)nlo;
           const float delta = m_new - m_run[b];  // S' relative to the new max: S' - delta
           const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
-          l_run[b] *= alpha;
-  #ifndef SR_ABL_VSUM
           {  // lacc rows 0 / 1 of lane n hold queries n / n + 16: their alphas
             const float a0 = __shfl(alpha, lane & 15), a1 = __shfl(alpha, (lane & 15) + 16);
             lacc[b][0] *= a0;
             lacc[b][1] *= a1;
           }
-  #endif
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             o[b][0][i] *= alpha;
@@ -396,9 +384,6 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   auto pv_tile = [&](int t) __attribute__((always_inline)) {
     const char* vt_lds = smem + (t & (NBUF - 1)) * STAGE_B + TILE_B;
     // ---- P = exp2(S') (B operand), O^T += V^T P^T; each V^T fragment feeds every q-block
-    float ps[QB][2];
-#pragma unroll
-    for (int b = 0; b < QB; ++b) ps[b][0] = ps[b][1] = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -408,16 +393,10 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
         for (int b = 0; b < QB; ++b)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float p = __builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
-  #ifdef SR_ABL_VSUM
-            ps[b][j & 1] += p;
-  #endif
-            pf[b][j] = (bf16)p;
+            pf[b][j] = (bf16)__builtin_amdgcn_exp2f(sc[b][kb][8 * s2 + j]);
           }
-  #ifndef SR_ABL_VSUM
 #pragma unroll
         for (int b = 0; b < QB; ++b) lacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sum_a, pf[b], lacc[b], 0, 0, 0);
-  #endif
         const int rowoff = (kb * 32 + 16 * s2) * 128;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -431,8 +410,6 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
           for (int b = 0; b < QB; ++b) o[b][db] = mfma32(vf, pf[b], o[b][db]);
         }
       }
-#pragma unroll
-    for (int b = 0; b < QB; ++b) l_run[b] += ps[b][0] + ps[b][1];
   };
   // STAG (8 waves, one workgroup per CU): waves 4-7 run the sweep half a tile behind their SIMD
   // partners (waves 0-3): in each barrier interval a partner's q.k^T MFMAs pair with this wave's
@@ -469,12 +446,8 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training)
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
-#ifndef SR_ABL_VSUM
     const float s0 = __shfl(lacc[b][0], l32 & 15), s1 = __shfl(lacc[b][1], l32 & 15);
     const float lsum = l32 < 16 ? s0 : s1;
-#else
-    const float lsum = sum_x32(l_run[b]);
-#endif
     const float inv = 1.f / lsum;
     const bool wide_o = d.ldo % 8 == 0 && ((uintptr_t)d.o & 15) == 0;
     const int qrow = qrow0 + 32 * b;
@@ -994,7 +967,10 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
     o[i] = 0.f;
   }
   float m = -INFINITY, l = 0.f;
-  const int nkeys_total = d.l0 + d.l1;
+  const char* mrow = d.mask_mode >= SR_MASK_DENSE
+                         ? (const char*)d.mask + ((int64_t)item * d.mask_bstride + (int64_t)head * d.mask_hstride +
+                                                  (int64_t)qrow_c * d.mask_ld) * (d.mask_mode == SR_MASK_ADD ? 4 : 1)
+                         : nullptr;
   for (int seg = 0; seg < 2; ++seg) {
     const int len = seg ? d.l1 : d.l0;
     if (len <= 0) continue;
@@ -1016,10 +992,15 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
       for (int j = 0; j < n; ++j) {
         const int kidx = key_base + t0 + j;
         if (d.mask_mode == SR_MASK_CAMERA && !(kidx < d.n_anchor || kidx == qrow)) continue;
+        if (d.mask_mode == SR_MASK_DENSE && !((const uint8_t*)mrow)[kidx]) continue;
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < D; ++i) s = fmaf(q[i], ks[j][i], s);
         s *= d.scale;
+        if (d.mask_mode == SR_MASK_ADD) {
+          s += ((const float*)mrow)[kidx];
+          if (s == -INFINITY) continue;
+        }
         if (s > m) {
           const float corr = expf(m - s);
           l = l * corr + 1.f;
@@ -1035,7 +1016,6 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
       }
     }
   }
-  (void)nkeys_total;
   if (qrow < d.lq) {
     float* op = (float*)d.o + (item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol;
     const float inv = 1.f / l;
@@ -1072,6 +1052,10 @@ __global__ __launch_bounds__(256) void attn_f32_short_kernel(AttnArgs args) {
   float m = -INFINITY, l = 0.f, o[DL];
 #pragma unroll
   for (int t = 0; t < DL; ++t) o[t] = 0.f;
+  const char* mrow = d.mask_mode >= SR_MASK_DENSE
+                         ? (const char*)d.mask + ((int64_t)item * d.mask_bstride + (int64_t)head * d.mask_hstride +
+                                                  (int64_t)qrow * d.mask_ld) * (d.mask_mode == SR_MASK_ADD ? 4 : 1)
+                         : nullptr;
   for (int seg = 0; seg < 2; ++seg) {
     const int len = seg ? d.l1 : d.l0;
     if (len <= 0) continue;
@@ -1085,6 +1069,7 @@ __global__ __launch_bounds__(256) void attn_f32_short_kernel(AttnArgs args) {
       const int kidx = key_base + j;
       bool ok = j < len;
       if (d.mask_mode == SR_MASK_CAMERA) ok = ok && (kidx < d.n_anchor || kidx == qrow);
+      if (d.mask_mode == SR_MASK_DENSE) ok = ok && ((const uint8_t*)mrow)[kidx] != 0;
       float sj = -INFINITY;
       if (ok) {
         const float* kp = kb + (rb + j) * ldk + hcol;
@@ -1098,6 +1083,10 @@ __global__ __launch_bounds__(256) void attn_f32_short_kernel(AttnArgs args) {
           acc = fmaf(q[i + 3], t.w, acc);
         }
         sj = acc;
+        if (d.mask_mode == SR_MASK_ADD) {
+          sj += ((const float*)mrow)[kidx];
+          ok = sj != -INFINITY;
+        }
       }
       const float cmax = sr::wave_max(sj);
       if (cmax == -INFINITY) continue;  // every key of the chunk masked (wave-uniform)
@@ -1233,14 +1222,15 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   SR_CHECK(d.batch > 0 && d.heads > 0 && d.lq > 0 && d.l0 > 0 && d.l1 >= 0, SR_EINVAL,
            "sr_attention: bad sizes batch=%d heads=%d lq=%d l0=%d l1=%d", d.batch, d.heads, d.lq, d.l0, d.l1);
   SR_CHECK(d.l1 == 0 || (d.k1 && d.v1), SR_EINVAL, "sr_attention: segment 1 needs k1/v1");
-  SR_CHECK(d.mask_mode == SR_MASK_NONE || (d.mask_mode == SR_MASK_CAMERA && d.l1 == 0), SR_EINVAL,
-           "sr_attention: bad mask_mode %d", d.mask_mode);
+  SR_CHECK(d.mask_mode == SR_MASK_NONE || (d.mask_mode == SR_MASK_CAMERA && d.l1 == 0) ||
+               ((d.mask_mode == SR_MASK_DENSE || d.mask_mode == SR_MASK_ADD) && d.mask && d.mask_ld >= 0),
+           SR_EINVAL, "sr_attention: bad mask_mode %d (or mask / mask_ld)", d.mask_mode);
   AttnArgs a;
   a.d = d;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SR_BF16) {
     SR_CHECK(d.head_dim == 64, SR_EUNSUPPORTED, "sr_attention(bf16): head_dim must be 64 (got %d)", d.head_dim);
-    SR_CHECK(d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED, "sr_attention(bf16): camera mask needs the f32 kernel");
+    SR_CHECK(d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED, "sr_attention(bf16): masks need the f32 kernel");
     SR_CHECK(d.ldq % 8 == 0 && d.ldk0 % 8 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0 &&
                  (d.l1 == 0 || (d.ldk1 % 8 == 0 && d.ldv1 % 8 == 0)),
              SR_EINVAL, "sr_attention(bf16): leading dims must be multiples of 8");

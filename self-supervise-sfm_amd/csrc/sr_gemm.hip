@@ -23,11 +23,6 @@
 
 #include <type_traits>
 
-#ifdef SR_ABL_STAGP  // tuning build: stagger + static priority for waves 4-7
-#define SR_ABL_STAG
-#define SR_ABL_PRIO4
-#endif
-
 #include "sr_common.h"
 
 namespace {
@@ -434,7 +429,6 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4
     });
     sr::barrier_raw();
     bf16* out = (bf16*)g.out;
-#ifndef SR_ABL_GUARDED
     if (m0 + 256 <= g.M) {
       // full tile: all 16 row reads in flight, then 16 unguarded stores (the guarded form waits
       // out each read's LDS latency behind an exec branch)
@@ -451,7 +445,6 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4
       }
       return;
     }
-#endif
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int rl = wave * 32 + it * 2 + (lane >> 5), c = lane & 31, row = m0 + rl;
@@ -689,38 +682,19 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#ifdef SR_ABL_PRIO4
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" 4)
-  if (wave_u >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-  // The k loop, instantiated per wave role (LATE: waves 4-7 under SR_ABL_STAG) so that a role
-  // test never splits an accumulator's register assignment.
-  auto kloop = [&](auto late_c) {
-    constexpr bool LATE = decltype(late_c)::value;
-    uint4 dA[4], dB[2];  // LATE: the k-substep-1 half of the previous tile's last quadrant
+  {
     stage(0);
     for (int kt = 0; kt < g.ktiles; ++kt) {
-#ifndef SR_ABL_NOWAIT
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
-#endif
-#ifndef SR_ABL_NOBAR
       sr::barrier_raw();                                  // ... every wave's; all done with kt-1
-#endif
-#ifdef SR_ABL_NODMA
-      if (kt + 1 < g.ktiles && kt < 1) stage(kt + 1);     // tuning ablation: reuse the first 2 stages
-#endif
       const bool more = kt + 1 < g.ktiles;
       // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
       // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
       // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
       // measured no better)
       auto dma_phase = [&](int ph) {
-#ifndef SR_ABL_NODMA
         if (!more || ph >= 2) return;
         dma_pieces(kt + 1, 4 * ph, 4 * ph + 4);
-#else
-        (void)ph;
-#endif
       };
       const char* sb = smem + (kt & 1) * STAGE_BIG;
       // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
@@ -742,30 +716,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
           b[ni][1] = *(const uint4*)(p + coff1);
         }
       };
-      auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn, int ks1 = 2) {
-#ifndef SR_ABL_PRIO4
+      auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn) {
         __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          if (ks < ks1)
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-              for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
-#ifndef SR_ABL_PRIO4
-        __builtin_amdgcn_s_setprio(0);
-#endif
-      };
-      if constexpr (LATE) {
-        // waves 4-7 run half a quadrant behind their SIMD partners (waves 0-3): the deferred 8
-        // MFMAs feed the matrix pipe across the barrier while both waves' first fragments load
-        if (kt > 0)
 #pragma unroll
           for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(dB[ni], dA[mi], acc[4 + mi][ni]);
-      }
+            for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
+        __builtin_amdgcn_s_setprio(0);
+      };
       load_a(aX, 0);
       load_b(bX, 0);
       load_b(bY, 1);
@@ -778,38 +738,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
       dma_phase(2);
       mma(aY, bY, 1, 1);
       dma_phase(3);
-      if constexpr (LATE) {
-        mma(aY, bX, 1, 0, 1);
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) dA[mi] = aY[mi][1];
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) dB[ni] = bX[ni][1];
-      } else {
-        mma(aY, bX, 1, 0);
-      }
+      mma(aY, bX, 1, 0);
     }
-    if constexpr (LATE)
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(dB[ni], dA[mi], acc[4 + mi][ni]);
-  };
-#ifdef SR_ABL_STAG
-  if (wave_u >= 4) kloop(std::true_type{});
-  else kloop(std::false_type{});
-#else
-  kloop(std::false_type{});
-#endif
-#ifdef SR_ABL_NOEPI
-#pragma unroll
-  for (int i = 0; i < 8; ++i)  // tuning ablation: keep every accumulator live, store nothing
-#pragma unroll
-    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-#else
-#ifdef SR_ABL_SAMEOUT  // tuning ablation: every tile's epilogue targets tile (0, 0) (L2-resident stores)
-  m0 = 0;
-  n0 = 0;
-#endif
+  }
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
     if (m0 + BIG <= g.M && !g.lds_epi) {
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
@@ -817,16 +748,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     }
   }
   if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
-#ifndef SR_ABL_GUARDED
     if (m0 + BIG <= g.M && !g.lds_epi && !g.ep.aux) {
       bias_full<EPI>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
       return;
     }
-#endif
   }
   if (g.lds_epi) epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
   else epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-#endif
 }
 
 template <int EPI>

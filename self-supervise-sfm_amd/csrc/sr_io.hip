@@ -77,7 +77,6 @@ __global__ __launch_bounds__(TPB) void pil_h_kernel(const uint8_t* __restrict__ 
   const uint8_t* src = img + ((int64_t)f * h + r0) * rowbytes;
   const uint4* a0 = (const uint4*)(src - ((uintptr_t)src & 15));
   const int shift = (int)((uintptr_t)src & 15);
-#ifndef SR_ABL_NOSTAGE
   {
     // all of a thread's 16-byte loads in flight before its LDS stores
     const int nq = (shift + nr * rowbytes + 15) >> 4;
@@ -96,7 +95,6 @@ __global__ __launch_bounds__(TPB) void pil_h_kernel(const uint8_t* __restrict__ 
       }
     }
   }
-#endif
   __syncthreads();
   const int quads = ldt >> 2;
   const int plane = h * ldt;
@@ -113,11 +111,7 @@ __global__ __launch_bounds__(TPB) void pil_h_kernel(const uint8_t* __restrict__ 
       for (int ch = 0; ch < C; ++ch)
         for (int u = 0; u < 4; ++u) acc[ch][u] = 1 << (PREC - 1);
       const int4* k = (const int4*)hk_ + q * hks;
-#ifdef SR_ABL_NOTAPS
-      for (int t0 = 0; t0 < hks && r0 < 0; t0 += KB) {
-#else
       for (int t0 = 0; t0 < hks; t0 += KB) {
-#endif
         int4 kc[KB];
 #pragma unroll
         for (int i = 0; i < KB; ++i) kc[i] = t0 + i < hks ? k[t0 + i] : make_int4(0, 0, 0, 0);
@@ -169,9 +163,6 @@ __global__ __launch_bounds__(TPB) void pil_h_kernel(const uint8_t* __restrict__ 
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[0][u] = (uint32_t)store16(ss[u]);
     }
-#ifdef SR_ABL_NOSTORE
-    if (o[0][0] != 77 || o[0][1] != 78) continue;
-#endif
     T* dst = (T*)tmp + ((int64_t)f * C * h + r0 + j) * ldt + q * 4;
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) {

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("SFM_AMD_LIB") or os.path.join(_HERE, "libsfm_amd.so")
 SR_F32, SR_BF16 = 0, 1
 SR_EPI_BIAS, SR_EPI_BIAS_GELU, SR_EPI_BIAS_RESID, SR_EPI_QKV, SR_EPI_PATCH = 0, 1, 2, 3, 4
 SR_EPI_F32, SR_EPI_GELU_BWD = 5, 6
-SR_MASK_NONE, SR_MASK_CAMERA = 0, 1
+SR_MASK_NONE, SR_MASK_CAMERA, SR_MASK_DENSE, SR_MASK_ADD = 0, 1, 2, 3
 SR_ATTN_MERGE_MAX_PARTS = 16
 
 _vp = ctypes.c_void_p
@@ -58,6 +58,7 @@ class AttnDesc(ctypes.Structure):
         ("key_bound", _vp),
         ("key_norm_max", _f32),
         ("o_bstride", _i64),
+        ("mask", _vp), ("mask_bstride", _i64), ("mask_hstride", _i64), ("mask_ld", _i64),
     ]
 
 

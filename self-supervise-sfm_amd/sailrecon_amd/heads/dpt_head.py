@@ -71,8 +71,6 @@ class DPTHead(nn.Module):
                  intermediate_layer_idx: List[int] = [4, 11, 17, 23],  # noqa: B006
                  pos_embed: bool = True, feature_only: bool = False, down_ratio: int = 1) -> None:
         super().__init__()
-        if feature_only:
-            raise NotImplementedError("DPTHead(feature_only=True) is not on the SailRecon path")
         if activation not in ops.DPT_ACT or conf_activation not in ops.DPT_CONF_ACT:
             raise ValueError(f"unsupported activation {activation!r} / {conf_activation!r}")
         self.patch_size = patch_size
@@ -100,13 +98,17 @@ class DPTHead(nn.Module):
         self.scratch.refinenet3 = FeatureFusionBlock(features)
         self.scratch.refinenet4 = FeatureFusionBlock(features, has_residual=False)
         head_features_1, head_features_2 = features, 32
-        self.scratch.output_conv1 = nn.Conv2d(head_features_1, head_features_1 // 2, kernel_size=3, stride=1,
-                                              padding=1)
-        self.scratch.output_conv2 = nn.Sequential(
-            nn.Conv2d(head_features_1 // 2, head_features_2, kernel_size=3, stride=1, padding=1),
-            nn.ReLU(inplace=True),
-            nn.Conv2d(head_features_2, output_dim, kernel_size=1, stride=1, padding=0),
-        )
+        if feature_only:  # dpt_head.py:123-126: no output_conv2, features out
+            self.scratch.output_conv1 = nn.Conv2d(head_features_1, head_features_1, kernel_size=3, stride=1,
+                                                  padding=1)
+        else:
+            self.scratch.output_conv1 = nn.Conv2d(head_features_1, head_features_1 // 2, kernel_size=3, stride=1,
+                                                  padding=1)
+            self.scratch.output_conv2 = nn.Sequential(
+                nn.Conv2d(head_features_1 // 2, head_features_2, kernel_size=3, stride=1, padding=1),
+                nn.ReLU(inplace=True),
+                nn.Conv2d(head_features_2, output_dim, kernel_size=1, stride=1, padding=0),
+            )
         self._packed: Dict[str, Tensor] = {}
         self._ones: Dict[int, Tensor] = {}
 
@@ -217,19 +219,25 @@ class DPTHead(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, aggregated_tokens_list: Union[List[Tensor], Dict[int, Tensor]], images: Tensor,
-                patch_start_idx: int, frames_chunk_size: int = 8) -> Tuple[Tensor, Tensor]:
-        """dpt_head.py:151-229: returns (preds [B,S,H,W,output_dim-1], conf [B,S,H,W]) fp32.
-        ``frames_chunk_size`` is accepted for signature parity; chunking here is sized by memory."""
+                patch_start_idx: int, frames_chunk_size: int = 8) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        """dpt_head.py:151-229: returns (preds [B,S,H,W,output_dim-1], conf [B,S,H,W]) fp32, or with
+        feature_only the fused feature map [B, S, features, H', W'] (dpt_head.py:286-287; an NCHW
+        view of the NHWC map the kernels write, no copy).  ``frames_chunk_size`` is accepted for
+        signature parity; chunking here is sized by memory."""
         B, S, _, H, W = images.shape
         runtime.require_device(images, "DPTHead")
         dev = images.device
         ph, pw = H // self.patch_size, W // self.patch_size
         n_patch = ph * pw
         frames = B * S
-        preds = torch.empty(B, S, H, W, self.output_dim - 1, device=dev, dtype=torch.float32)
-        conf = torch.empty(B, S, H, W, device=dev, dtype=torch.float32)
         oh, ow = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
         f = self.scratch.layer1_rn.weight.shape[0]  # features
+        if self.feature_only:
+            preds = torch.empty(frames, oh, ow, f, device=dev, dtype=torch.float32)
+            conf = None
+        else:
+            preds = torch.empty(B, S, H, W, self.output_dim - 1, device=dev, dtype=torch.float32)
+            conf = torch.empty(B, S, H, W, device=dev, dtype=torch.float32)
         convs3 = [m for m in self.modules() if isinstance(m, nn.Conv2d) and m.kernel_size == (3, 3)]
         if all(m.in_channels % 32 == 0 and m.out_channels % 4 == 0 for m in convs3):
             # implicit-GEMM convs: the chunk is bounded by its activations (largest: the upsampled
@@ -251,8 +259,13 @@ class DPTHead(nn.Module):
         with torch.no_grad():
             for f0 in range(0, frames, chunk):
                 f1 = min(frames, f0 + chunk)
-                self._forward_chunk(toks, P, patch_start_idx, f0, f1, ph, pw, H, W, oh, ow,
-                                    preds.view(frames, H, W, -1)[f0:f1], conf.view(frames, H, W)[f0:f1])
+                if self.feature_only:
+                    self._forward_chunk(toks, P, patch_start_idx, f0, f1, ph, pw, H, W, oh, ow, preds[f0:f1], None)
+                else:
+                    self._forward_chunk(toks, P, patch_start_idx, f0, f1, ph, pw, H, W, oh, ow,
+                                        preds.view(frames, H, W, -1)[f0:f1], conf.view(frames, H, W)[f0:f1])
+        if self.feature_only:
+            return preds.view(B, S, oh, ow, f).permute(0, 1, 4, 2, 3)
         return preds, conf
 
     def _forward_chunk(self, toks, P, psi, f0, f1, ph, pw, H, W, oh, ow, preds, conf):
@@ -298,8 +311,10 @@ class DPTHead(nn.Module):
         out = self._fusion("scratch.refinenet2", sc.refinenet2, out, l2, size=tuple(l1.shape[1:3]))
         out = self._fusion("scratch.refinenet1", sc.refinenet1, out, l1)
         out = self._conv3x3(out, "scratch.output_conv1", sc.output_conv1)
-        up = torch.empty(F_, oh, ow, out.shape[3], device=dev, dtype=torch.float32)
+        up = preds if self.feature_only else torch.empty(F_, oh, ow, out.shape[3], device=dev, dtype=torch.float32)
         ops.resize_bilinear(out, up, add=self._pos_table(oh, ow, out.shape[3], aspect, dev) if self.pos_embed else None)
+        if self.feature_only:  # dpt_head.py:286-287: the fused, upsampled, position-embedded map
+            return
         c0, c2 = sc.output_conv2[0], sc.output_conv2[2]
         hidden = self._conv3x3(up, "scratch.output_conv2.0", c0)
         ops.dpt_head_out(hidden.view(-1, hidden.shape[3]), self._conv_w("scratch.output_conv2.2", c2),

@@ -5,12 +5,15 @@ the math runs as part of ``runtime.run_block`` (SR_EPI_QKV GEMM with bias + qk-L
 fused -> sr_attention -> proj GEMM with LayerScale and the residual add fused).  A standalone
 ``Attention.forward(x, pos, attn_mask)`` (attention.py:70-122) runs the same kernels with a plain
 bias epilogue on proj: bf16 under autocast (the reference's autocast Linear returns bf16), exact
-fp32 otherwise.  Masks: None, or the camera-trunk pattern (camera_head.py:197-228), as Block.
+fp32 otherwise.  ``attn_mask``: anything F.scaled_dot_product_attention accepts — a bool mask
+(True = attend) or a float mask added to the scores, broadcastable to [B, heads, N, N] — runs on
+the exact fp32 kernel with the mask read in place (SR_MASK_DENSE / SR_MASK_ADD; broadcast dims
+keep stride 0, nothing is expanded in memory and nothing is inspected on the host).
 """
 
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -18,20 +21,25 @@ from torch import Tensor, nn
 from .. import _lib, ops, runtime
 
 
-def camera_mask_anchors(attn_mask: Tensor) -> Optional[int]:
-    """If ``attn_mask`` (True = attend, [1,1,S,S] or [S,S]) is the camera-trunk pattern,
-    return its anchor count; else None."""
-    m = attn_mask.reshape(attn_mask.shape[-2], attn_mask.shape[-1]).bool().cpu()
-    S = m.shape[0]
-    for n in range(1, S + 1):
-        ref = torch.zeros(S, S, dtype=torch.bool)
-        ref[:, :n] = True
-        idx = torch.arange(n, S)
-        ref[:n, n:] = False
-        ref[idx, idx] = True
-        if torch.equal(ref, m):
-            return n
-    return None
+def sdpa_mask(attn_mask: Tensor, B: int, heads: int, N: int, L: int, device) -> Tuple[int, Tensor]:
+    """(mask_mode, [B, heads, N, L] view) for ops.attention from an SDPA ``attn_mask``
+    (attention.py:103-109): bool -> SR_MASK_DENSE (True = attend), floating -> SR_MASK_ADD (fp32,
+    added to the scaled scores).  Broadcast dims stay stride 0; only a mask whose key dim is not
+    unit-stride is copied."""
+    if attn_mask.dim() > 4:
+        raise ValueError(f"attn_mask of rank {attn_mask.dim()} cannot broadcast to [B, heads, N, N]")
+    m = attn_mask.to(device)
+    if m.dtype == torch.bool:
+        mode = _lib.SR_MASK_DENSE
+    elif m.is_floating_point():
+        mode = _lib.SR_MASK_ADD
+        m = m.float()
+    else:
+        raise TypeError(f"attn_mask must be bool or floating (got {m.dtype})")
+    m = m.expand(B, heads, N, L)
+    if m.stride(3) != 1:
+        m = m.contiguous()
+    return mode, m
 
 
 class Attention(nn.Module):
@@ -79,15 +87,7 @@ class Attention(nn.Module):
             raise NotImplementedError("attention dropout")
         B, N, C = x.shape
         dtype = runtime.compute_dtype()
-        n_anchor = None
-        if attn_mask is not None:
-            n_anchor = camera_mask_anchors(attn_mask)
-            if n_anchor is None:
-                raise NotImplementedError("Attention.forward: only None or the camera-trunk mask is supported "
-                                          "(the aggregator drives the reloc block mask implicitly)")
-            if B != 1:
-                raise NotImplementedError("Attention.forward: masked attention needs B == 1")
-        if n_anchor is not None or self.head_dim != 64:
+        if attn_mask is not None or self.head_dim != 64:
             dtype = torch.float32  # the MFMA attention kernel is head_dim 64, unmasked
         pa = self.packed(dtype)
         xa = x.detach().reshape(B * N, C).to(dtype).contiguous()
@@ -103,12 +103,13 @@ class Attention(nn.Module):
         else:
             ops.gemm(xa, pa.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pa.b_qkv, qkv=epi)
         o = torch.empty(B * N, C, device=x.device, dtype=dtype)
-        if n_anchor is None:
+        if attn_mask is None:
             runtime.frame_attend(pa, B, N)(qkv, o)
         else:
+            mode, m = sdpa_mask(attn_mask, B, self.num_heads, N, N, x.device)
             ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=self.num_heads,
-                          head_dim=self.head_dim, batch=1, lq=N, q_bstride=0, l0=N, k0_bstride=0,
-                          mask_mode=_lib.SR_MASK_CAMERA, n_anchor=n_anchor)
+                          head_dim=self.head_dim, batch=B, lq=N, q_bstride=N, l0=N, k0_bstride=N,
+                          mask_mode=mode, mask=m)
         out = torch.empty(B * N, C, device=x.device, dtype=dtype)
         ops.gemm(o, pa.w_proj, out, _lib.SR_EPI_BIAS, bias=pa.b_proj)
         return out.view(B, N, C)

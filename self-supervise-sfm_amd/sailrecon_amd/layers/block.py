@@ -2,11 +2,12 @@
 
 ``Block.forward(x, pos=None, attn_mask=None)`` keeps the reference signature
 (block.py:86).  It runs the whole block on the HIP path (runtime.run_block) for
-x on a ROCm device: bf16 under autocast, exact fp32 otherwise.  Supported masks:
-None, or the camera-trunk pattern (camera_head.py:197-228: the first n rows see
-only each other, later rows see the first n plus themselves) — the only masks the
-reference passes to a Block outside the aggregator's reloc stack, which the
-aggregator drives directly with its implicit block mask.
+x on a ROCm device: bf16 under autocast, exact fp32 otherwise.  ``attn_mask`` is
+anything F.scaled_dot_product_attention accepts (bool, True = attend, or an additive
+float mask, broadcastable to [B, heads, N, N]); a masked block runs the exact fp32
+kernel with the mask read in place (layers/attention.py sdpa_mask).  Inside the
+model the aggregator drives the reloc block mask and the camera head its trunk mask
+implicitly (no mask tensor).
 """
 
 from __future__ import annotations
@@ -16,8 +17,8 @@ from typing import Callable, Optional
 import torch
 from torch import Tensor, nn
 
-from .. import _lib, ops, runtime
-from .attention import Attention, camera_mask_anchors  # noqa: F401 (re-export)
+from .. import ops, runtime
+from .attention import Attention, sdpa_mask
 from .layer_scale import LayerScale
 from .mlp import Mlp
 
@@ -55,14 +56,7 @@ class Block(nn.Module):
         dtype = runtime.compute_dtype()
         B, N, C = x.shape
         pb = self.packed(dtype)
-        n_anchor = None
-        if attn_mask is not None:
-            n_anchor = camera_mask_anchors(attn_mask)
-            if n_anchor is None:
-                raise NotImplementedError("Block.forward: only None or the camera-trunk mask is supported")
-            if B != 1:
-                raise NotImplementedError("Block.forward: masked attention needs B == 1")
-        if n_anchor is not None or pb.head_dim != 64:
+        if attn_mask is not None or pb.head_dim != 64:
             dtype = torch.float32
             pb = self.packed(dtype)
         xf = x.detach().reshape(B * N, C).float().contiguous().clone()
@@ -76,13 +70,14 @@ class Block(nn.Module):
             qkv_epi = runtime.qkv_params(pb, rope, pos_yx=pos_yx)
         else:
             qkv_epi = runtime.qkv_params(pb, None)
-        if n_anchor is None:
+        if attn_mask is None:
             attend = runtime.frame_attend(pb, B, N)
         else:
+            mode, m = sdpa_mask(attn_mask, B, pb.heads, N, N, x.device)
+
             def attend(qkv, o):
                 ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=pb.heads, head_dim=pb.head_dim,
-                              batch=1, lq=N, q_bstride=0, l0=N, k0_bstride=0, mask_mode=_lib.SR_MASK_CAMERA,
-                              n_anchor=n_anchor)
+                              batch=B, lq=N, q_bstride=N, l0=N, k0_bstride=N, mask_mode=mode, mask=m)
         runtime.run_block(pb, xf, 0, B * N, sc, attend, qkv_epi)
         return xf.view(B, N, C).to(x.dtype)
 

@@ -242,8 +242,11 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
               scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
-              key_norm_max: float = 0.0) -> None:
-    """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``lse``
+              key_norm_max: float = 0.0, mask: Optional[Tensor] = None) -> None:
+    """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``mask``
+    (mask_mode SR_MASK_DENSE: bool / uint8, nonzero = attend; SR_MASK_ADD: fp32 added to the
+    scores) is a [batch, heads, lq, l0 + l1] view (broadcast dims may have stride 0, the last dim
+    stride 1), fp32 q / k / v only.  ``lse``
     (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd.
     ``key_norm_max`` > 0: a static bound of every key's per-head 2-norm (runtime.key_norm_bound),
     which replaces the key scan of the fixed-offset sweep.  A bf16 single query set too short to
@@ -260,6 +263,18 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
                    n_anchor=n_anchor, scale=scale, lse=lse)
+    if mask_mode in (_lib.SR_MASK_DENSE, _lib.SR_MASK_ADD):
+        want = torch.float32 if mask_mode == _lib.SR_MASK_ADD else (torch.bool, torch.uint8)
+        if mask is None or mask.dim() != 4 or tuple(mask.shape) != (batch, heads, lq, l0 + l1) or \
+                mask.device != q.device or (mask.dtype != want if mask_mode == _lib.SR_MASK_ADD else
+                                            mask.dtype not in want) or mask.stride(3) != 1:
+            raise ValueError(f"attention: mask must be a [{batch}, {heads}, {lq}, {l0 + l1}] "
+                             f"{'fp32' if mask_mode == _lib.SR_MASK_ADD else 'bool'} view with unit key stride "
+                             f"on {q.device}")
+        if q.dtype != torch.float32:
+            raise ValueError("attention: dense / additive masks run on the fp32 kernel")
+        d.mask = _p(mask)
+        d.mask_bstride, d.mask_hstride, d.mask_ld = mask.stride(0), mask.stride(1), mask.stride(2)
     _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * (l0 + l1) * head_dim,
                       q.element_size() * heads * head_dim *
                       (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)))

@@ -14,6 +14,9 @@ DPTHead's own state_dict keys.  Inputs: seeded randn tokens / rand images.
   g6_unproject.npz   unproject_depth_map_to_point_map on the 224 depth maps with random
                      cameras (geometry.py:19-130)
   dpt_state_dict_keys.json
+  g6_dpt_feat_small.npz  DPTHead(SMALL, feature_only=True) (dpt_head.py:123-126,286-287):
+                     the fused feature map [1, S, 64, H, W], frames_chunk_size=2
+                     (``--only feature`` writes this file alone)
 """
 
 from __future__ import annotations
@@ -53,6 +56,21 @@ def build(cfg, kind):
 def tokens_for(layers, S, P, C, seed):
     g = torch.Generator().manual_seed(seed)
     return {l: torch.randn(1, S, P, C, generator=g) for l in layers}
+
+
+def feature_only():
+    S, H, W = 3, 56, 70
+    P = 5 + (H // 14) * (W // 14)
+    toks = tokens_for(SMALL["intermediate_layer_idx"], S, P, SMALL["dim_in"], 5)
+    images = torch.rand(1, S, 3, H, W, generator=torch.Generator().manual_seed(6))
+    m = DPTHead(**SMALL, feature_only=True).eval()
+    m.load_state_dict(synth_state_dict_like(m))
+    with torch.no_grad():
+        feat = m(toks, images=images, patch_start_idx=5, frames_chunk_size=2)
+    out = dict(images=images.numpy(), feat=feat.numpy())
+    for l, t in toks.items():
+        out[f"tok_{l}"] = t.numpy()
+    np.savez(os.path.join(HERE, "g6_dpt_feat_small.npz"), **out)
 
 
 def main():
@@ -114,4 +132,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--only", "feature"]:
+        feature_only()
+    else:
+        main()
+        feature_only()

@@ -65,6 +65,14 @@ def dpt_small_model_sd(kind):
     return m, synth_state_dict_like(m)
 
 
+def dpt_feat_model_sd():
+    """The small DPT config with feature_only=True (dpt_head.py:123-126) and its rule state_dict."""
+    from sailrecon_amd.heads.dpt_head import DPTHead
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    m = DPTHead(**DPT_SMALL, feature_only=True)
+    return m, synth_state_dict_like(m)
+
+
 # ---------------------------------------------------------------- input formation (§8(f) rank 2)
 def pil_process_reference(arr, target, is_depth):
     """train/utils/io.py:118-153 step by step with Pillow, which is what the reference calls

@@ -82,7 +82,7 @@ def _ref_rows(qs, ks, vs, scale):
     return out
 
 
-@pytest.mark.parametrize("L", [10_992, 43_968, 175_872], ids=["C2", "C3", "C5"])
+@pytest.mark.parametrize("L", [10_992, 43_968, 87_936, 175_872], ids=["C2", "C3", "N64", "C5"])
 def test_global_attention_production(ops, L):
     q, k, v = _make(L, 7, spikes=(L - 37, L // 2 + 5))
     o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)

@@ -28,13 +28,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, golden, mode, overlap):
+def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo"):
     for p in (REPO, os.path.join(REPO, "self-supervise-sfm_amd"), HERE):
         if p not in sys.path:
             sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(rank)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     from goldens import load_npz, rule_state_dict
     from sailrecon_amd.models.aggregator import shard_range
     from sailrecon_amd.utils.pose_enc import pose_encoding_to_extri_intri
@@ -60,8 +62,15 @@ def _worker(rank, world, port, out_dir, golden, mode, overlap):
         layers = (0, 1)
     m = m.cuda()
     images = images.cuda()
-    m.aggregator.set_frame_sharding(dist.group.WORLD)
+    m.aggregator.set_frame_sharding(dist.group.WORLD)  # nccl: the seed broadcast as a device tensor
     m.aggregator.shard_overlap = overlap
+    if backend == "nccl":  # gather_rows' RCCL all_gather_into_tensor on the K/V row layout
+        from sailrecon_amd.models.aggregator import gather_rows
+        src = torch.randn(37, 2048, device="cuda", dtype=torch.bfloat16)
+        dst = torch.empty(37 * world, 2048, device="cuda", dtype=torch.bfloat16)
+        for w in gather_rows(dst, src, [37] * world, dist.group.WORLD, rank):
+            w.wait()
+        assert torch.equal(dst[rank * 37:(rank + 1) * 37], src)
     m.aggregator.generator.manual_seed(0)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=(mode == "bf16")):
         feats, psi, cam_last = m.aggregator(images, list(range(n)), list(range(n, 2 * n)), fix_rank=int(g["fix_rank"]))
@@ -88,11 +97,12 @@ def _worker(rank, world, port, out_dir, golden, mode, overlap):
     dist.destroy_process_group()
 
 
-def _run(tmp_path, world, golden, mode, overlap=True):
+def _run(tmp_path, world, golden, mode, overlap=True, backend="gloo"):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from goldens import load_npz, rel_l2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), golden, mode, overlap), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), golden, mode, overlap, backend), nprocs=world,
+             join=True)
     g = load_npz(golden)
     rs = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     tol = TOL[mode]
@@ -111,6 +121,15 @@ def _run(tmp_path, world, golden, mode, overlap=True):
         if "extrinsic" in g and "img" in g:
             assert rel_l2(r["ext"], g["extrinsic"]) < tol
             assert rel_l2(r["intr"], g["intrinsic"]) < tol
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_frame_sharded_rccl_world1(tmp_path, mode):
+    """The RCCL ("nccl") process group on the box's one GPU: set_frame_sharding's device-tensor
+    seed broadcast (aggregator.py set_frame_sharding), gather_rows' all_gather_into_tensor and the
+    sharded forward at world 1 against the reference golden (RCCL refuses two ranks on one
+    device, so world 2+ over RCCL is the driver's multi-GPU run)."""
+    _run(tmp_path, 1, "g1_small_56.npz", mode, backend="nccl")
 
 
 def test_frame_sharded_two_ranks_one_gpu(tmp_path):

@@ -26,6 +26,20 @@ def test_dpt_small_matches_reference(kind):
     assert rel_l2(conf.cpu().numpy(), g[f"{kind}_conf"]) < TOL
 
 
+def test_dpt_feature_only_matches_reference():
+    """DPTHead(feature_only=True) (dpt_head.py:123-126,286-287): the fused, upsampled,
+    position-embedded feature map [B, S, features, H, W] against the reference's output."""
+    from goldens import dpt_feat_model_sd
+    g = load_npz("g6_dpt_feat_small.npz")
+    m, sd = dpt_feat_model_sd()
+    m.load_state_dict(sd)
+    m = m.to(DEV)
+    toks = {l: torch.from_numpy(g[f"tok_{l}"]).to(DEV) for l in DPT_SMALL["intermediate_layer_idx"]}
+    feat = m(toks, images=torch.from_numpy(g["images"]).to(DEV), patch_start_idx=5, frames_chunk_size=2)
+    assert tuple(feat.shape) == g["feat"].shape
+    assert rel_l2(feat.cpu().numpy(), g["feat"]) < TOL
+
+
 def test_dpt_224_matches_reference():
     from sailrecon_amd.heads.dpt_head import DPTHead
     from sailrecon_amd.utils.synth_weights import synth_state_dict_like

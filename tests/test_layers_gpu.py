@@ -33,7 +33,7 @@ def _seeded(m, seed):
 
 
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
-@pytest.mark.parametrize("case", ["aggregator", "dino", "camera_mask"])
+@pytest.mark.parametrize("case", ["aggregator", "dino", "camera_mask", "bool_mask", "float_mask"])
 def test_attention_forward(dev, mode, case):
     from oracle import sfm_oracle as O
     from sailrecon_amd.heads.camera_head import build_lr_mask
@@ -52,11 +52,27 @@ def test_attention_forward(dev, mode, case):
         C, H = 384, 6
         m = MemEffAttention(C, num_heads=H)
         N, pos, kw, mask = 37, None, {}, None
-    else:  # camera trunk (camera_head.py:51-61,165): D = 128, ~build_lr_mask
+    elif case == "camera_mask":  # camera trunk (camera_head.py:51-61,165): D = 128, ~build_lr_mask
         C, H = 2048, 16
         m = Attention(C, num_heads=H)
         B, N, pos, kw = 1, 10, None, {}
         mask = ~build_lr_mask(N, list(range(6)))
+    elif case == "bool_mask":  # any SDPA bool mask (attention.py:103-109): per item + head, True = attend
+        C, H = 1024, 16
+        m = Attention(C, num_heads=H, qk_norm=True, rope=RotaryPositionEmbedding2D(100))
+        N = gh * gw + 5
+        pos = PositionGetter()(B, gh, gw, "cpu") + 1
+        pos = torch.cat([torch.zeros(B, 5, 2, dtype=pos.dtype), pos], 1)
+        kw = dict(qk_norm=True, rope_base=100.0)
+        mask = torch.rand(B, H, N, N, generator=torch.Generator().manual_seed(9)) < 0.3
+        mask |= torch.eye(N, dtype=torch.bool)  # no fully masked row (SDPA: NaN)
+    else:  # float (additive) mask broadcast from [N, N], with -inf entries and a > 520-key row set
+        C, H = 384, 6
+        m = Attention(C, num_heads=H)
+        B, N, pos, kw = 2, 600, None, {}
+        mask = torch.randn(N, N, generator=torch.Generator().manual_seed(10))
+        mask[torch.rand(N, N, generator=torch.Generator().manual_seed(11)) < 0.5] = float("-inf")
+        mask.fill_diagonal_(0.0)
     sd = _seeded(m, 3)
     m = m.to(dev)
     x = torch.randn(B, N, C, generator=torch.Generator().manual_seed(4))
@@ -67,10 +83,11 @@ def test_attention_forward(dev, mode, case):
             y = m(x.to(dev), pos=None if pos is None else pos.to(dev),
                   attn_mask=None if mask is None else mask.to(dev))
     ref = O.attention(sd, "", x, H, pos=pos, mask=mask, **kw)
-    tol = 1e-5 if mode == "fp32" or case == "camera_mask" else 2e-2
+    exact = mode == "fp32" or mask is not None
+    tol = 1e-5 if exact else 2e-2
     assert y.shape == (B, N, C)
-    # the masked / head_dim-128 camera case always runs the exact fp32 kernel
-    assert y.dtype == (torch.float32 if mode == "fp32" or case == "camera_mask" else torch.bfloat16)
+    # masked attention always runs the exact fp32 kernel
+    assert y.dtype == (torch.float32 if exact else torch.bfloat16)
     assert rel(y.float(), ref) < tol
 
 
@@ -125,3 +142,24 @@ def test_layer_scale_forward(dev, dtype, inplace):
     if inplace:
         assert y is x
     assert rel(y.float(), ref) < (1e-7 if dtype == torch.float32 else 4e-3)
+
+
+@pytest.mark.parametrize("short", [True, False])
+def test_block_forward_with_mask(dev, short):
+    """Block.forward(x, pos, attn_mask) with a per-item bool mask [B, 1, N, N] (block.py:86-112 ->
+    attention.py:103-109) against the oracle's Block; short = the one-wave-per-row kernel
+    (<= 512 keys), otherwise the tiled fp32 kernel."""
+    from oracle import sfm_oracle as O
+    from sailrecon_amd.layers.block import Block
+    C, H = 384, 6
+    B, N = 2, (40 if short else 700)
+    m = Block(C, H, init_values=0.1)
+    sd = _seeded(m, 5)
+    m = m.to(dev)
+    x = torch.randn(B, N, C, generator=torch.Generator().manual_seed(6))
+    mask = torch.rand(B, 1, N, N, generator=torch.Generator().manual_seed(7)) < 0.5
+    mask |= torch.eye(N, dtype=torch.bool)
+    with torch.no_grad():
+        y = m(x.to(dev), attn_mask=mask.to(dev))
+    ref = O.block(sd, "", x, H, 1e-5, mask=mask)
+    assert rel(y, ref) < 1e-5

@@ -134,6 +134,17 @@ def test_dpt_small_matches_reference(kind):
     assert rel_l2(conf.numpy(), g[f"{kind}_conf"]) < 1e-5
 
 
+def test_dpt_feature_only_matches_reference():
+    from goldens import DPT_SMALL, dpt_feat_model_sd
+    g = load_npz("g6_dpt_feat_small.npz")
+    _, sd = dpt_feat_model_sd()
+    toks = {l: torch.from_numpy(g[f"tok_{l}"]) for l in DPT_SMALL["intermediate_layer_idx"]}
+    feat = O.dpt_forward(sd, "", toks, torch.from_numpy(g["images"]), 5, layers=DPT_SMALL["intermediate_layer_idx"],
+                         feature_only=True)
+    assert feat.shape == g["feat"].shape
+    assert rel_l2(feat.numpy(), g["feat"]) < 1e-5
+
+
 def test_dpt_224_matches_reference():
     from goldens import DPT_HEADS, dpt_224_inputs, rule_state_dict
     g = load_npz("g6_dpt_224.npz")

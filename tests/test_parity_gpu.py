@@ -130,7 +130,9 @@ def full_model():
     return m.to(DEV)
 
 
-def _check_full(model, fname, mode):
+def _full_errors(model, fname, mode):
+    """rel-L2 of every checked quantity of a full-size golden (feature maps per layer: row norms,
+    camera columns, sampled rows; camera tokens; pose encodings; extrinsic / intrinsic)."""
     g = load_npz(fname)
     n, img = int(g["n_views"]), int(g["img"])
     gen = torch.Generator().manual_seed(n)
@@ -138,18 +140,24 @@ def _check_full(model, fname, mode):
     images = torch.cat([x, x])[None].to(DEV)
     feats, psi, cam_last, poses, ext, intr = run(model, images, n, 300, mode)
     assert np.array_equal(model.aggregator.last_subsample_indices[:, 0].numpy(), g["sub_idx"])
-    tol = TOL[mode]
     rows = torch.from_numpy(g["sample_rows"])
+    err = {}
     for layer in (4, 11, 17, 23):
         v = feats[layer][0].cpu()
-        assert rel_l2(v.norm(dim=-1).numpy(), g[f"feat_{layer}_rownorm"]) < tol
-        assert rel_l2(v[:, 0].numpy(), g[f"feat_{layer}_cam"]) < tol
-        assert rel_l2(v.reshape(-1, v.shape[-1])[rows].numpy(), g[f"feat_{layer}_rows"]) < tol
-    assert rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"]) < tol
-    pe = np.stack([p.cpu().numpy() for p in poses])
-    assert rel_l2(pe, g["pose_enc"]) < tol
-    assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
-    assert rel_l2(intr.cpu().numpy(), g["intrinsic"]) < tol
+        err[f"feat_{layer}_rownorm"] = rel_l2(v.norm(dim=-1).numpy(), g[f"feat_{layer}_rownorm"])
+        err[f"feat_{layer}_cam"] = rel_l2(v[:, 0].numpy(), g[f"feat_{layer}_cam"])
+        err[f"feat_{layer}_rows"] = rel_l2(v.reshape(-1, v.shape[-1])[rows].numpy(), g[f"feat_{layer}_rows"])
+    err["cam_token_last_layer"] = rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"])
+    err["pose_enc"] = rel_l2(np.stack([p.cpu().numpy() for p in poses]), g["pose_enc"])
+    err["extrinsic"] = rel_l2(ext.cpu().numpy(), g["extrinsic"])
+    err["intrinsic"] = rel_l2(intr.cpu().numpy(), g["intrinsic"])
+    return err
+
+
+def _check_full(model, fname, mode):
+    err = _full_errors(model, fname, mode)
+    bad = {k: v for k, v in err.items() if not v < TOL[mode]}
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
@@ -172,3 +180,25 @@ def test_full_c2_518_n8(full_model, mode):
 def test_full_c3_518_n32(full_model, mode):
     """BASELINE config 3, the headline workload: N=32 views @518 (S=64 frames, L_g = 43,968)."""
     _check_full(full_model, "g10_518_n32.npz", mode)
+
+
+# fp8 global attention (BASELINE C5's precision, opt-in: Aggregator.set_fp8_global) at the C3
+# headline scene against the reference's fp32 golden.  No reference output pins an fp8 contract
+# (the reference runs bf16 SDPA); the tolerances below are the measured errors with headroom
+# (measured on MI355X, round 3: printed by the test), next to bf16's 3e-2.
+FP8_TOL = {"qk": {"feat": 5e-2, "pose": 5e-2}, "qkv": {"feat": 8e-2, "pose": 8e-2}}
+
+
+@pytest.mark.parametrize("fp8", ["qk", "qkv"])
+def test_full_c3_518_n32_fp8_global(full_model, fp8):
+    full_model.aggregator.set_fp8_global(True, fp8_v=(fp8 == "qkv"))
+    try:
+        err = _full_errors(full_model, "g10_518_n32.npz", "bf16")
+    finally:
+        full_model.aggregator.set_fp8_global(False)
+    print(f"C3 fp8 global ({fp8}) rel-L2 vs the reference fp32 golden:",
+          {k: float(f"{v:.3e}") for k, v in err.items()})
+    feat = max(v for k, v in err.items() if k.startswith("feat_") or k == "cam_token_last_layer")
+    pose = max(err["pose_enc"], err["extrinsic"], err["intrinsic"])
+    assert feat < FP8_TOL[fp8]["feat"], err
+    assert pose < FP8_TOL[fp8]["pose"], err

@@ -33,6 +33,9 @@ for step in "$@"; do
     bench)   run bench 600 python bench.py ;;
     benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench_c2) run bench_c2 400 python bench.py --views 8 --no-cpu-baseline ;;
+    bench64) run bench64 600 python bench.py --views 64 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof64)  run prof64 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof64 -o run --output-format csv -- \
+               python3 bench.py --views 64 --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
     bench_c5) run bench_c5 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench_c5q) run bench_c5q 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline --fp8-global qkv ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
