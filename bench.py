@@ -483,13 +483,24 @@ def main():
                     "traffic_source": os.path.relpath(tsrc, REPO) if traffic is not None else None,
                     "algorithmic_bytes": round(b["bytes_per_launch"]),
                     "avg_launch_ms": round(b["avg_ms"], 4), "flop_per_launch": b["flops_per_launch"]}
-        gems = [v for k, v in breakdown.items() if k.startswith("gemm_")]
-        if gems:
-            flop = sum(v["flops_per_launch"] * v["launches"] for v in gems)
-            ms = sum(v["total_ms"] for v in gems)
-            roofline["gemm_all_tflops"] = round(flop / (ms * 1e-3) / 1e12, 1)
-            gpeak = bf16_peak if use_bf16 else PEAK_F32_TFLOPS  # GEMMs stay bf16 in the fp8 modes
-            roofline["gemm_mfma_util"] = round(flop / (ms * 1e-3) / 1e12 / gpeak, 4)
+        def gemm_rate(tags):
+            sel = [breakdown[k] for k in tags if k in breakdown]
+            if not sel:
+                return None
+            flop = sum(v["flops_per_launch"] * v["launches"] for v in sel)
+            return flop / (sum(v["total_ms"] for v in sel) * 1e-3) / 1e12
+
+        gpeak = bf16_peak if use_bf16 else PEAK_F32_TFLOPS  # GEMMs stay bf16 in the fp8 modes
+        # north-star "MFMA peak on aggregator GEMMs": the aggregator's bf16 GEMM classes (patch embed,
+        # QKV, proj / fc2, fc1; _GEMM_N); the camera head's fp32 GEMMs (*_f32 classes) are reported apart
+        agg = gemm_rate(list(_GEMM_N))
+        if agg is not None:
+            roofline["gemm_agg_tflops"] = round(agg, 1)
+            roofline["gemm_mfma_util"] = round(agg / gpeak, 4)
+            roofline["gemm_mfma_util_scope"] = "aggregator GEMMs (" + ", ".join(k for k in _GEMM_N if k in breakdown) + ")"
+        allr = gemm_rate([k for k in breakdown if k.startswith("gemm_")])
+        if allr is not None:
+            roofline["gemm_all_tflops"] = round(allr, 1)
         print(json.dumps({"kernel_breakdown": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                                                    for kk, vv in v.items()} for k, v in breakdown.items()},
                           "step_ms": dt / args.steps * 1e3}), file=sys.stderr)
