@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "sr_common.h"
+#include "sr_attn_pipe.inc"
 
 namespace {
 
@@ -70,11 +71,14 @@ constexpr float RESCALE_LOG2 = 8.f;
 #ifndef SR_ATTN_DEFAULT_CFG
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
-template <int NW, int QB, int KIND, bool STAG = false>
-__global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf16_kernel(AttnArgs args) {
+template <int NW, int QB, int KIND, bool PIPE = false>
+__global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(AttnArgs args) {
+  static_assert(!PIPE || (NW == 4 && QB == 2), "the pipelined sweep pairs the two q-blocks of a wave");
   constexpr int QROWS = NW * 32 * QB;
-  constexpr int NBUF = STAG ? 8 : (NW >= 4 ? 4 : 2);  // ring depth (power of 2)
-  constexpr int LOOK = STAG ? 3 : NBUF - 1;           // stages in flight
+  // ring depth: PIPE keeps tile t-1's V alive through tile t (5 stages = 80 KB, two workgroups
+  // fill the CU's 160 KB); otherwise a power of two
+  constexpr int NBUF = PIPE ? 5 : (NW >= 4 ? 4 : 2);
+  constexpr int LOOK = PIPE ? 3 : NBUF - 1;  // stages issued ahead
   constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
@@ -133,8 +137,9 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   const char* sp = sb0 + (srb0 + grow0) * sld0 * 2;  // row grow0 of the next tile to stage
   int64_t sstep = (int64_t)KT * sld0 * 2, s8 = 8 * sld0 * 2;
   uint32_t sva = voA0, svb = voB0;
+  auto slot = [](int t) { return NBUF == 5 ? t % 5 : t & (NBUF - 1); };
   auto stage = [&](int t) {  // t = 0, 1, 2, ... in order
-    const int buf = t & (NBUF - 1);
+    const int buf = slot(t);
     const bool s1 = t >= nt0;
     if (t == nt0) {  // first tile of segment 1
       sp = sb1 + (srb1 + grow0) * sld1 * 2;
@@ -276,7 +281,7 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   f32x16 sc[QB][2];  // [q-block][key block]: S' of the tile between qk_tile and pv_tile
   // S'^T of tile t, its ragged-tail mask and (until the offset is fixed) the row-max update
   auto qk_tile = [&](int t) __attribute__((always_inline)) {
-    const char* kt_lds = smem + (t & (NBUF - 1)) * STAGE_B;
+    const char* kt_lds = smem + slot(t) * STAGE_B;
     // ---- S'^T = K (cQ)^T - m for every q-block (2 blocks of 32 keys each); once every row of
     // the wave runs the fixed offset m = 0, the -m fold MFMAs are skipped (uniform branch)
     const f32x16 zero = {};
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
   };
   // P = exp2(S') of tile t, its row sums, O^T += V^T P^T
   auto pv_tile = [&](int t) __attribute__((always_inline)) {
-    const char* vt_lds = smem + (t & (NBUF - 1)) * STAGE_B + TILE_B;
+    const char* vt_lds = smem + slot(t) * STAGE_B + TILE_B;
     // ---- P = exp2(S') (B operand), O^T += V^T P^T; each V^T fragment feeds every q-block
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -411,37 +416,81 @@ __global__ __launch_bounds__(NW * 64, STAG ? 2 : (NW >= 8 ? 4 : 2)) void attn_bf
         }
       }
   };
-  // STAG (8 waves, one workgroup per CU): waves 4-7 run the sweep half a tile behind their SIMD
-  // partners (waves 0-3): in each barrier interval a partner's q.k^T MFMAs pair with this wave's
-  // exp2 / P.V stretch and vice versa (MI355X_MICROARCH.md "Two waves per SIMD" 9).  S' of the
-  // late waves' tile t crosses the barrier in registers; the ring keeps tile t-1 (8 stages,
-  // 3 in flight), and every wave runs ntiles + 1 barrier intervals.
-  auto sweep = [&](auto late_c) __attribute__((always_inline)) {
-    constexpr bool LATE = decltype(late_c)::value;
-    for (int t = 0; t < ntiles + (STAG ? 1 : 0); ++t) {
-      // tile t must have landed (up to LOOK-1 later stages stay in flight); everyone is done
-      // with the buffer the next stage overwrites
+  // one tile of the plain path: wait (tile t; PIPE: t + 1), barrier (everyone is done with the
+  // buffer the next stage overwrites), stage, compute.  A wave whose rows all lie past lq (the
+  // ragged last q-tile: 1374 = 5 x 256 + 94 leaves two of its four waves empty) keeps staging and
+  // barriers but leaves its SIMD to the other waves.
+  auto plain_tile = [&](int t) __attribute__((always_inline)) {
+    if constexpr (PIPE) {
+      if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
       if (LOOK >= 3 && t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
       else if (LOOK >= 2 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sr::barrier_raw();
-      if (t + LOOK < ntiles) stage(t + LOOK);
-      // a wave whose rows all lie past lq (the ragged last q-tile: 1374 = 5 x 256 + 94 leaves two
-      // of its four waves empty) keeps staging and barriers but leaves its SIMD to the other waves
-      if (!wave_active) continue;
-      if constexpr (LATE) {
-        if (t > 0) pv_tile(t - 1);
-        if (t < ntiles) qk_tile(t);
-      } else {
-        if (t < ntiles) {
-          qk_tile(t);
-          pv_tile(t);
-        }
-      }
+    }
+    sr::barrier_raw();
+    if (t + LOOK < ntiles) stage(t + LOOK);
+    if (wave_active) {
+      qk_tile(t);
+      pv_tile(t);
     }
   };
-  if (STAG && wave_u >= 4) sweep(std::true_type{});
-  else sweep(std::false_type{});
+
+  // ---- PIPE: the sweep with the wave's two q-blocks half a tile apart (cdna_hip_programming.md
+  // App. B "Fused attention prefill"; MI355X_MICROARCH.md "Two waves per SIMD" 1-3: with both
+  // q-blocks in step the matrix pipe idles while the wave's own exp2 / pack stretch runs).  Per
+  // tile t:
+  //   X(t): q.k^T of q-block 1 on tile t, P.V of q-block 1 on tile t-1  ||  P = exp2(S') of q-block 0
+  //   Y(t): q.k^T of q-block 0 on tile t+1, P.V of q-block 0 on tile t   ||  P of q-block 1
+  // so each phase holds 20 MFMAs against 32 v_exp + 16 packs.  The sweep is one hand-scheduled
+  // inline-asm statement generated by tools/gen_attn_pipe.py (sr_attn_pipe.inc): scores and P
+  // live in named registers (P written in place over its scores), O / Q / row sums stay operands.
+  // It covers a wave whose every row has its Cauchy-Schwarz bound qb <= 50, i.e. the fixed offset
+  // m = 0 that the plain path also settles on after tile 0 for such rows, over one key segment of
+  // full tiles (>= 4); any other wave runs the plain loop, which keeps the same wait, barrier and
+  // stage per tile, so the waves of a workgroup may take different paths.  V of tile t-1 is read
+  // during tile t, hence the 5-stage ring (stage t+3 overwrites tile t-2).
+  bool asm_ok = false;
+  if constexpr (PIPE) {
+    // (the asm derives every fragment address from koff[0] / voff0 by XOR: lds0 % 128 == 0)
+    bool ok = wave_active && use_bound && args.allow_mzero && args.ntile1 == 0 && len0 % KT == 0 && ntiles >= 4 &&
+              (lds0 & 127) == 0;
+#pragma unroll
+    for (int b = 0; b < QB; ++b) ok = ok && qb[b] <= 50.f;
+    asm_ok = __builtin_amdgcn_readfirstlane(__all(ok)) != 0;
+  }
+  if (asm_ok) {
+    m_zero = fixed_m = true;  // m_run = 0, m_b = 0 as initialised
+    const uint64_t spu = (uint64_t)(uintptr_t)sp;  // tile 3 (the prologue staged tiles 0-2)
+    // (readfirstlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends into
+    // the high word)
+    const uint32_t sp_lo = __builtin_amdgcn_readfirstlane((uint32_t)spu);
+    const uint32_t sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(spu >> 32));
+    const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
+    const char* spb2 = spb + 2 * s8;  // pieces 2, 3
+    uint32_t dm[2] = {sva, svb + (uint32_t)s8};  // pieces 0 / 2 and 1 / 3: rows +0 / +16 and +8 / +24
+    int nn = __builtin_amdgcn_readfirstlane(ntiles - 4);
+    uint32_t slotb = 0;
+    const uint32_t l0u = __builtin_amdgcn_readfirstlane(lds0);
+    const uint32_t ldsv = __builtin_amdgcn_readfirstlane(lds0 + (stage_v ? TILE_B : 0) + ((wave_u * DPW) & 7) * 1024);
+    const uint32_t sst32 = __builtin_amdgcn_readfirstlane((uint32_t)sstep);
+    uint32_t x0, x1, x2, x3;
+    asm volatile(SR_ATTN_PIPE_ASM
+                 // every output early-clobber: the asm writes them while it still reads inputs (an
+                 // input of equal value may otherwise share a tied output's register)
+                 : [o00] "+&v"(o[0][0]), [o01] "+&v"(o[0][1]), [o10] "+&v"(o[1][0]), [o11] "+&v"(o[1][1]),
+                   [l0] "+&v"(lacc[0]), [l1] "+&v"(lacc[1]), [dma0] "+&v"(dm[0]), [dma1] "+&v"(dm[1]),
+                   [n] "+&s"(nn), [slot] "+&s"(slotb), [sst] "=&s"(x0),
+                   [sk] "=&s"(x1), [sv] "=&s"(x2), [stmp] "=&s"(x3)
+                 : [q00] "v"(qf[0][0]), [q01] "v"(qf[0][1]), [q02] "v"(qf[0][2]), [q03] "v"(qf[0][3]),
+                   [q10] "v"(qf[1][0]), [q11] "v"(qf[1][1]), [q12] "v"(qf[1][2]), [q13] "v"(qf[1][3]),
+                   [suma] "v"(sum_a), [koff0] "v"(koff[0]), [voff0] "v"(voff0), [sp] "s"(spb), [sp2] "s"(spb2),
+                   [sstep] "s"(sst32), [lds0] "s"(l0u), [ldsv] "s"(ldsv)
+                 : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc");
+  } else {
+    for (int t = 0; t < ntiles; ++t) plain_tile(t);
+  }
 
   // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training)
 #pragma unroll
@@ -1256,7 +1305,6 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : (d.l1 > 0 ? 1 : 0);
     // Workgroup shapes (waves x 32-row q-blocks per wave):
     //   0: 4 x 2 = 256 rows    1: 8 x 1 = 256 rows    2: 2 x 2 = 128 rows
-    //   3: 8 x 2 = 512 rows, waves 4-7 staggered by half a tile (one workgroup per CU)
     // 256-row tiles unless they would leave CUs idle (fewer than 2 workgroups per CU, e.g. the
     // per-rank query slice of a frame-sharded global block).  SR_ATTN_CFG=0|1|2 overrides
     // (tuning experiments).
@@ -1266,7 +1314,12 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     }();
     const long wgs256 = (long)((d.lq + 255) / 256) * d.heads * d.batch;
     const int cfg = force_cfg >= 0 ? force_cfg : (wgs256 >= 512 ? SR_ATTN_DEFAULT_CFG : 2);
-    const int rows = cfg == 2 ? 128 : (cfg == 3 ? 512 : 256);
+    const int rows = cfg == 2 ? 128 : 256;
+    // the pipelined sweep (PIPE) for the 4 x 2 shape; SR_ATTN_PIPE=0 runs the plain one (A/B)
+    static const bool pipe = [] {
+      const char* e = getenv("SR_ATTN_PIPE");
+      return e ? atoi(e) != 0 : false;
+    }();
     dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
 #define SR_ATTN_LAUNCH(NW_, QB_, ST_)                                                                           \
   do {                                                                                                        \
@@ -1276,7 +1329,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   } while (0)
     if (cfg == 1) SR_ATTN_LAUNCH(8, 1, false);
     else if (cfg == 2) SR_ATTN_LAUNCH(2, 2, false);
-    else if (cfg == 3) SR_ATTN_LAUNCH(8, 2, true);
+    else if (pipe) SR_ATTN_LAUNCH(4, 2, true);
     else SR_ATTN_LAUNCH(4, 2, false);
 #undef SR_ATTN_LAUNCH
     return sr::check_launch("sr_attention(bf16)");

@@ -46,6 +46,17 @@ for step in "$@"; do
     kio)     run kio 300 python tools/kbench.py io ;;
     io_tests) run io_tests 600 python -m pytest tests/test_io_gpu.py -q -x ;;
     kattn)   run kattn 300 python tools/kbench.py attn ;;
+    dbg_pipe) run dbg_pipe 300 env SR_ATTN_PIPE=1 python tools/dbg_attn_pipe.py 1024 8192 8256 16384 43968 ;;
+    kattn_ab) run kattn_ab0 300 env SR_ATTN_PIPE=0 SR_KB_STATIC=1 python tools/kbench.py attn && \
+              run kattn_ab1 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 python tools/kbench.py attn && \
+              run kattn_ab2 300 env SR_ATTN_PIPE=0 SR_KB_STATIC=1 python tools/kbench.py attn && \
+              run kattn_ab3 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 python tools/kbench.py attn ;;
+    attn_pipe_tests) run attn_pipe_tests 900 env SR_ATTN_PIPE=1 python -u -m pytest tests/test_baseline_shapes_gpu.py \
+              tests/test_kernels_gpu.py -x -q -m gpu -k "attention or attn" --timeout 600 --timeout-method thread ;;
+    attn_shape_tests) run attn_shape_tests 900 python -u -m pytest tests/test_baseline_shapes_gpu.py tests/test_kernels_gpu.py \
+              -x -q -m gpu -k "attention or attn" --timeout 600 --timeout-method thread ;;
+    c4test)  run c4test 900 python -u -m pytest tests/test_c4_golden_gpu.py -x -v -s -m gpu --timeout 900 --timeout-method thread ;;
+    fp8test) run fp8test 900 python -u -m pytest tests/test_parity_gpu.py -x -v -s -m gpu -k fp8 --timeout 600 --timeout-method thread ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
