@@ -72,13 +72,11 @@ constexpr float RESCALE_LOG2 = 8.f;
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
 template <int NW, int QB, int KIND, bool PIPE = false>
-__global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(AttnArgs args) {
+__global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf16_kernel(AttnArgs args) {
   static_assert(!PIPE || (NW == 4 && QB == 2), "the pipelined sweep pairs the two q-blocks of a wave");
   constexpr int QROWS = NW * 32 * QB;
-  // ring depth: PIPE keeps tile t-1's V alive through tile t (5 stages = 80 KB, two workgroups
-  // fill the CU's 160 KB); otherwise a power of two
-  constexpr int NBUF = PIPE ? 5 : (NW >= 4 ? 4 : 2);
-  constexpr int LOOK = PIPE ? 3 : NBUF - 1;  // stages issued ahead
+  constexpr int NBUF = NW >= 4 ? 4 : 2;  // K/V ring stages
+  constexpr int LOOK = NBUF - 1;         // stages issued ahead
   constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
@@ -137,7 +135,7 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
   const char* sp = sb0 + (srb0 + grow0) * sld0 * 2;  // row grow0 of the next tile to stage
   int64_t sstep = (int64_t)KT * sld0 * 2, s8 = 8 * sld0 * 2;
   uint32_t sva = voA0, svb = voB0;
-  auto slot = [](int t) { return NBUF == 5 ? t % 5 : t & (NBUF - 1); };
+  auto slot = [](int t) { return t & (NBUF - 1); };
   auto stage = [&](int t) {  // t = 0, 1, 2, ... in order
     const int buf = slot(t);
     const bool s1 = t >= nt0;
@@ -416,19 +414,14 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
         }
       }
   };
-  // one tile of the plain path: wait (tile t; PIPE: t + 1), barrier (everyone is done with the
-  // buffer the next stage overwrites), stage, compute.  A wave whose rows all lie past lq (the
+  // one tile of the plain path: wait (tile t), barrier (everyone is done with the buffer the next
+  // stage overwrites), stage, compute.  A wave whose rows all lie past lq (the
   // ragged last q-tile: 1374 = 5 x 256 + 94 leaves two of its four waves empty) keeps staging and
   // barriers but leaves its SIMD to the other waves.
   auto plain_tile = [&](int t) __attribute__((always_inline)) {
-    if constexpr (PIPE) {
-      if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (LOOK >= 3 && t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
-      else if (LOOK >= 2 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (LOOK >= 3 && t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+    else if (LOOK >= 2 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sr::barrier_raw();
     if (t + LOOK < ntiles) stage(t + LOOK);
     if (wave_active) {
@@ -437,20 +430,20 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     }
   };
 
-  // ---- PIPE: the sweep with the wave's two q-blocks half a tile apart (cdna_hip_programming.md
-  // App. B "Fused attention prefill"; MI355X_MICROARCH.md "Two waves per SIMD" 1-3: with both
-  // q-blocks in step the matrix pipe idles while the wave's own exp2 / pack stretch runs).  Per
-  // tile t:
+  // ---- PIPE: one wave per SIMD (launch_bounds(256, 1), the whole register file), the wave's two
+  // q-blocks half a tile apart (cdna_hip_programming.md App. B "Fused attention prefill";
+  // MI355X_MICROARCH.md constants: at head_dim 64 the loop is vector-issue-bound, and two waves
+  // per SIMD share one issue port).  Per tile t:
   //   X(t): q.k^T of q-block 1 on tile t, P.V of q-block 1 on tile t-1  ||  P = exp2(S') of q-block 0
   //   Y(t): q.k^T of q-block 0 on tile t+1, P.V of q-block 0 on tile t   ||  P of q-block 1
-  // so each phase holds 20 MFMAs against 32 v_exp + 16 packs.  The sweep is one hand-scheduled
+  // so each phase holds 20 MFMAs against 32 v_exp + 16 packs, and every K / V fragment is read
+  // from LDS once (AGPR sets by tile parity) for both q-blocks.  The sweep is one hand-scheduled
   // inline-asm statement generated by tools/gen_attn_pipe.py (sr_attn_pipe.inc): scores and P
-  // live in named registers (P written in place over its scores), O / Q / row sums stay operands.
+  // live in named VGPRs (P written in place over its scores), O / Q / row sums are AGPR operands.
   // It covers a wave whose every row has its Cauchy-Schwarz bound qb <= 50, i.e. the fixed offset
   // m = 0 that the plain path also settles on after tile 0 for such rows, over one key segment of
   // full tiles (>= 4); any other wave runs the plain loop, which keeps the same wait, barrier and
-  // stage per tile, so the waves of a workgroup may take different paths.  V of tile t-1 is read
-  // during tile t, hence the 5-stage ring (stage t+3 overwrites tile t-2).
+  // stage per tile, so the waves of a workgroup may take different paths.
   bool asm_ok = false;
   if constexpr (PIPE) {
     // (the asm derives every fragment address from koff[0] / voff0 by XOR: lds0 % 128 == 0)
@@ -470,7 +463,8 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
     const char* spb2 = spb + 2 * s8;  // pieces 2, 3
     uint32_t dm[2] = {sva, svb + (uint32_t)s8};  // pieces 0 / 2 and 1 / 3: rows +0 / +16 and +8 / +24
-    int nn = __builtin_amdgcn_readfirstlane(ntiles - 4);
+    int nn = __builtin_amdgcn_readfirstlane((ntiles - 4) >> 1);  // (odd, even) tile pairs
+    const int rem = __builtin_amdgcn_readfirstlane((ntiles - 4) & 1);
     uint32_t slotb = 0;
     const uint32_t l0u = __builtin_amdgcn_readfirstlane(lds0);
     const uint32_t ldsv = __builtin_amdgcn_readfirstlane(lds0 + (stage_v ? TILE_B : 0) + ((wave_u * DPW) & 7) * 1024);
@@ -479,14 +473,14 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 4 : 2) void attn_bf16_kernel(Att
     asm volatile(SR_ATTN_PIPE_ASM
                  // every output early-clobber: the asm writes them while it still reads inputs (an
                  // input of equal value may otherwise share a tied output's register)
-                 : [o00] "+&v"(o[0][0]), [o01] "+&v"(o[0][1]), [o10] "+&v"(o[1][0]), [o11] "+&v"(o[1][1]),
-                   [l0] "+&v"(lacc[0]), [l1] "+&v"(lacc[1]), [dma0] "+&v"(dm[0]), [dma1] "+&v"(dm[1]),
+                 : [o00] "+&a"(o[0][0]), [o01] "+&a"(o[0][1]), [o10] "+&a"(o[1][0]), [o11] "+&a"(o[1][1]),
+                   [l0] "+&a"(lacc[0]), [l1] "+&a"(lacc[1]), [dma0] "+&v"(dm[0]), [dma1] "+&v"(dm[1]),
                    [n] "+&s"(nn), [slot] "+&s"(slotb), [sst] "=&s"(x0),
-                   [sk] "=&s"(x1), [sv] "=&s"(x2), [stmp] "=&s"(x3)
-                 : [q00] "v"(qf[0][0]), [q01] "v"(qf[0][1]), [q02] "v"(qf[0][2]), [q03] "v"(qf[0][3]),
-                   [q10] "v"(qf[1][0]), [q11] "v"(qf[1][1]), [q12] "v"(qf[1][2]), [q13] "v"(qf[1][3]),
+                   [sk] "=&s"(x1), [sv] "=&s"(x2), [sdma] "=&s"(x3)
+                 : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
+                   [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
                    [suma] "v"(sum_a), [koff0] "v"(koff[0]), [voff0] "v"(voff0), [sp] "s"(spb), [sp2] "s"(spb2),
-                   [sstep] "s"(sst32), [lds0] "s"(l0u), [ldsv] "s"(ldsv)
+                   [sstep] "s"(sst32), [lds0] "s"(l0u), [ldsv] "s"(ldsv), [rem] "s"(rem)
                  : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc");
   } else {
     for (int t = 0; t < ntiles; ++t) plain_tile(t);
@@ -1329,7 +1323,8 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   } while (0)
     if (cfg == 1) SR_ATTN_LAUNCH(8, 1, false);
     else if (cfg == 2) SR_ATTN_LAUNCH(2, 2, false);
-    else if (pipe) SR_ATTN_LAUNCH(4, 2, true);
+    else if (pipe && d.l1 == 0 && d.l0 % KT == 0 && (d.key_bound || d.key_norm_max > 0.f))
+      SR_ATTN_LAUNCH(4, 2, true);  // one key segment of full tiles with a key bound (the asm sweep)
     else SR_ATTN_LAUNCH(4, 2, false);
 #undef SR_ATTN_LAUNCH
     return sr::check_launch("sr_attention(bf16)");

@@ -99,7 +99,7 @@ def main():
     t1 = time.time()
     with torch.autocast("cpu", dtype=torch.bfloat16, enabled=bf16):
         feats, psi, cam_last = m.aggregator(images, na, nq, fix_rank=FIX_RANK)
-    feats = [f.float() for f in feats]
+    feats = {k: v.float() for k, v in feats.items()}  # output_dict: layer -> [B, S, P, 2C]
     poses = m.camera_head(feats, cam_last.float())
     enc = poses[-1][0]
     enc.retain_grad()

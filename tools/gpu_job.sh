@@ -75,6 +75,10 @@ for step in "$@"; do
     counters) run counters 120 rocprofv3 -L ;;
     pmc_attn1) run pmc_attn1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_attn1 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
     pmc_attn2) run pmc_attn2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_attn2 -o run --output-format csv -- python3 tools/kbench.py attn gemm ;;
+    pmc_attnp1) run pmc_attnp1 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_attnp1 -o run --output-format csv -- python3 tools/kbench.py attn ;;
+    pmc_attnp2) run pmc_attnp2 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_attnp2 -o run --output-format csv -- python3 tools/kbench.py attn ;;
+    pmc_attnp3) run pmc_attnp3 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 rocprofv3 --pmc SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VMEM SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d gpurun_out/pmc_attnp3 -o run --output-format csv -- python3 tools/kbench.py attn ;;
+    pmc_attn0) run pmc_attn0 300 env SR_ATTN_PIPE=0 SR_KB_STATIC=1 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_attn0 -o run --output-format csv -- python3 tools/kbench.py attn ;;
     kattnb)  run kattnb 300 python tools/kbench.py attn_bwd ;;
     ktrain)  run ktrain 900 python tools/kbench.py train ;;
     prof_train) run prof_train 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- \
