@@ -379,6 +379,9 @@ def main():
     ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
                     help="BASELINE C5: the global blocks' q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 "
                          "e4m3; everything else bf16")
+    ap.add_argument("--extra-c5", choices=["off", "qk", "qkv"], default="off",
+                    help="opt-in SECOND JSON object after the headline line: BASELINE C5 (N=128 @518, global "
+                         "attention in fp8: qk or qkv) timed on the same model")
     ap.add_argument("--launch-only", action="store_true",
                     help="launcher / process-group / ranks_seen check without the model (gloo if no GPU)")
     args = ap.parse_args()
@@ -537,8 +540,68 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
+    if args.extra_c5 != "off" and use_bf16:
+        extra = c5_line(model, device, args, world, use_pg, seen)
+        if rank == 0:
+            print(json.dumps(extra))
     if use_pg:
         dist.destroy_process_group()
+
+
+def c5_line(model, device, args, world, use_pg, seen, n=128):
+    """BASELINE config 5 (N=128 @518, 256 frames, L_g = 175,872) with the global blocks' attention in
+    fp8 (Aggregator.set_fp8_global): a second, opt-in bench object beside the headline line."""
+    from sailrecon_amd import ops
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(n, 3, args.img, args.img, generator=g)
+    images = torch.cat([x, x])[None].to(device)
+    no_reloc, reloc = list(range(n)), list(range(n, 2 * n))
+    model.aggregator.set_fp8_global(True, fp8_v=args.extra_c5 == "qkv")
+    steps = max(1, args.steps // 2)
+
+    def step():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            return model(images, no_reloc_list=no_reloc, reloc_list=reloc, fix_rank=300)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    try:
+        step()
+        barrier()
+        ops.TIMER = ops.KernelTimer()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        barrier()
+        dt = time.perf_counter() - t0
+        timer, ops.TIMER = ops.TIMER, None
+    finally:
+        model.aggregator.set_fp8_global(False)
+    dt_t = torch.tensor([dt], device=device)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    summ = timer.summary()
+    att = summ.get("attn_global")
+    tflop = algorithmic_tflop(n, args.img)
+    return {
+        "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px (BASELINE C5, fp8 global attention)",
+        "value": n * steps / dt, "unit": "views/s", "n_gpus": dist.get_world_size() if use_pg else 1,
+        "steps": steps, "warmup": 1, "ms_per_step": dt / steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+        "dtype": f"bf16, global {'q.k^T' if args.extra_c5 == 'qk' else 'q.k^T + P.V'} fp8-e4m3",
+        "data": "synthetic (seeded U[0,1) images, seeded synthetic weights)",
+        "config": {"workload": f"N={n} views @{args.img}px duplicated to {2 * n} frames, fix_rank=300",
+                   "views": n, "img": args.img, "frames": 2 * n, "algorithmic_tflop_per_step": round(tflop, 2),
+                   "achieved_tflops_whole_step": round(tflop * steps / dt, 1)},
+        "attn_global": None if att is None else {"avg_launch_ms": round(att["avg_ms"], 4),
+                                                 "tflops": round(att["tflops"], 1)},
+        "ranks_seen": seen,
+    }
 
 
 if __name__ == "__main__":

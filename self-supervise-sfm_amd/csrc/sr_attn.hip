@@ -463,24 +463,24 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
     const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
     const char* spb2 = spb + 2 * s8;  // pieces 2, 3
     uint32_t dm[2] = {sva, svb + (uint32_t)s8};  // pieces 0 / 2 and 1 / 3: rows +0 / +16 and +8 / +24
-    int nn = __builtin_amdgcn_readfirstlane((ntiles - 4) >> 1);  // (odd, even) tile pairs
-    const int rem = __builtin_amdgcn_readfirstlane((ntiles - 4) & 1);
-    uint32_t slotb = 0;
-    const uint32_t l0u = __builtin_amdgcn_readfirstlane(lds0);
+    int nn = __builtin_amdgcn_readfirstlane((ntiles - 4) >> 2);  // groups of four staging tiles
+    const int rem = __builtin_amdgcn_readfirstlane((ntiles - 4) & 3);
     const uint32_t ldsv = __builtin_amdgcn_readfirstlane(lds0 + (stage_v ? TILE_B : 0) + ((wave_u * DPW) & 7) * 1024);
     const uint32_t sst32 = __builtin_amdgcn_readfirstlane((uint32_t)sstep);
-    uint32_t x0, x1, x2, x3;
+    // fragment lane addresses (ring slot and block offsets ride in the instructions' offset field)
+    const uint32_t ka0 = lds0 + koff[0], ka1 = lds0 + koff[1], ka2 = lds0 + koff[2], ka3 = lds0 + koff[3];
+    const uint32_t va0 = lds0 + voff0, va1 = lds0 + voff1;
     asm volatile(SR_ATTN_PIPE_ASM
                  // every output early-clobber: the asm writes them while it still reads inputs (an
                  // input of equal value may otherwise share a tied output's register)
                  : [o00] "+&a"(o[0][0]), [o01] "+&a"(o[0][1]), [o10] "+&a"(o[1][0]), [o11] "+&a"(o[1][1]),
                    [l0] "+&a"(lacc[0]), [l1] "+&a"(lacc[1]), [dma0] "+&v"(dm[0]), [dma1] "+&v"(dm[1]),
-                   [n] "+&s"(nn), [slot] "+&s"(slotb), [sst] "=&s"(x0),
-                   [sk] "=&s"(x1), [sv] "=&s"(x2), [sdma] "=&s"(x3)
+                   [n] "+&s"(nn)
                  : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
                    [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
-                   [suma] "v"(sum_a), [koff0] "v"(koff[0]), [voff0] "v"(voff0), [sp] "s"(spb), [sp2] "s"(spb2),
-                   [sstep] "s"(sst32), [lds0] "s"(l0u), [ldsv] "s"(ldsv), [rem] "s"(rem)
+                   [suma] "v"(sum_a), [ka0] "v"(ka0), [ka1] "v"(ka1), [ka2] "v"(ka2), [ka3] "v"(ka3),
+                   [va0] "v"(va0), [va1] "v"(va1), [sp] "s"(spb), [sp2] "s"(spb2), [sstep] "s"(sst32),
+                   [ldsv] "s"(ldsv), [rem] "s"(rem)
                  : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc");
   } else {
     for (int t = 0; t < ntiles; ++t) plain_tile(t);
@@ -1309,10 +1309,12 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     const long wgs256 = (long)((d.lq + 255) / 256) * d.heads * d.batch;
     const int cfg = force_cfg >= 0 ? force_cfg : (wgs256 >= 512 ? SR_ATTN_DEFAULT_CFG : 2);
     const int rows = cfg == 2 ? 128 : 256;
-    // the pipelined sweep (PIPE) for the 4 x 2 shape; SR_ATTN_PIPE=0 runs the plain one (A/B)
+    // the hand-scheduled sweep (PIPE, one wave per SIMD) for the 4 x 2 shape over one key segment
+    // of full tiles; SR_ATTN_PIPE=0 runs the compiled two-waves-per-SIMD sweep instead (A/B:
+    // global L = 43,968 6.27-6.29 vs 6.78-6.83 ms, kbench on one box)
     static const bool pipe = [] {
       const char* e = getenv("SR_ATTN_PIPE");
-      return e ? atoi(e) != 0 : false;
+      return e ? atoi(e) != 0 : true;
     }();
     dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
 #define SR_ATTN_LAUNCH(NW_, QB_, ST_)                                                                           \

@@ -184,9 +184,11 @@ def test_full_c3_518_n32(full_model, mode):
 
 # fp8 global attention (BASELINE C5's precision, opt-in: Aggregator.set_fp8_global) at the C3
 # headline scene against the reference's fp32 golden.  No reference output pins an fp8 contract
-# (the reference runs bf16 SDPA); the tolerances below are the measured errors with headroom
-# (measured on MI355X, round 3: printed by the test), next to bf16's 3e-2.
-FP8_TOL = {"qk": {"feat": 5e-2, "pose": 5e-2}, "qkv": {"feat": 8e-2, "pose": 8e-2}}
+# (the reference runs bf16 SDPA); the tolerances below are the measured errors with ~2-4x headroom,
+# next to bf16's 3e-2.  Measured on MI355X (round 3, printed by the test): qk feature maps / camera
+# tokens <= 4.4e-3, pose encoding / extrinsic / intrinsic <= 6.3e-4; qkv 4.6e-3 / 6.9e-4 -- the fp8
+# global attention adds little to the bf16 path's own gap at this scene.
+FP8_TOL = {"qk": {"feat": 1e-2, "pose": 3e-3}, "qkv": {"feat": 1e-2, "pose": 3e-3}}
 
 
 @pytest.mark.parametrize("fp8", ["qk", "qkv"])

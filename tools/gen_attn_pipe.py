@@ -16,9 +16,11 @@ tile apart so that one q-block's MFMAs always have the other's VALU beside them:
 Every K and V fragment of a tile is read from LDS ONCE (into AGPR sets, double-buffered by tile
 parity) and used by both q-blocks.  Scores S_b (32 VGPRs per q-block) are named VGPRs; P
 overwrites its own scores in place (S_b[16:31], EXP order (1,0),(1,1),(0,0),(0,1)).  O, Q and
-the row sums are compiler-allocated AGPR operands.  The loop is unrolled by two (register sets by
-tile parity); two tails (by the parity of ntiles) end the sweep.  K/V ring: 4 stages of 16 KB,
-tile t+3 staged during tile t (its slot last read in X(t-1)).
+the row sums are compiler-allocated AGPR operands.  K/V ring: 4 stages of 16 KB, tile t+3 staged
+during tile t (its slot last read in X(t-1)).  The loop is unrolled by the ring depth, so every
+tile's slot (and register parity) is static: LDS fragment addresses are six lane-offset operands
+plus the instruction's 16-bit offset, with no per-tile address arithmetic; four tail variants (by
+(ntiles - 4) % 4) end the sweep.
 
 Hazards handled here: lgkmcnt counted per fragment read (LDS returns in order), MFMA -> VALU
 (scores) and VALU -> MFMA (P) distances, M0 -> LDS-DMA s_nop 0, and the trailing pad before the
@@ -33,17 +35,32 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "self-supervise-sfm_amd", "csrc", "sr_attn_pipe.inc")
 
 S = {0: 160, 1: 192}          # S_b: 32 VGPRs, kb block k at S_b + 16k
-KA, VA, AT = 224, 225, 226    # K base address (tile t+1), V base address (tile t), temporary
-NAMED_V = list(range(160, 227))
+NAMED_V = list(range(160, 224))
+# LDS addresses are lane offsets in operands (%[ka0..3] = lds0 + koff[s], %[va0..1] = lds0 +
+# voff[db]); the ring slot of a tile is static per body (the loop is unrolled by the ring depth),
+# so slot, K-block and V row offsets all ride in the instructions' 16-bit offset field
 KSET = [0, 32]                # AGPR bases: K fragment (kb, s) at KSET[p] + 4 (4 kb + s)
 VSET = [64, 96]               # AGPR bases: V^T fragment (i, db) at VSET[p] + 4 (2 i + db)
 NAMED_A = list(range(0, 128))
 EXP_ORDER = [(1, 0), (1, 1), (0, 0), (0, 1)]  # (kb, s2) in EXP / P-fragment order
 TILE_B = 8192
 STAGE_B = 2 * TILE_B
-RING_MASK = 4 * STAGE_B - 1   # 4-stage ring of 64 KB
 # issue cost weights (cycles of the SIMD's vector issue; MI355X_MICROARCH.md constants table)
-COST = {"exp": 8, "cvt": 5, "read": 8, "dma": 16}
+COST = {"exp": int(os.environ.get("SR_PIPE_EXP_COST", "8")), "cvt": 5, "read": 8, "dma": 16}
+# tuning knobs (A/B builds; the defaults are the measured best):
+#   SR_PIPE_DMA_IN_X=1: LDS-DMA of tile t+3 in X and V(t) reads at the head of Y (measured slower:
+#   global 6.52-6.57 vs 6.39-6.41 ms with V(t) in X and the DMA in Y)
+#   SR_PIPE_X_READS / SR_PIPE_Y_DMA: share of a phase's MFMA gaps the reads / DMA pieces spread over
+DMA_IN_X = os.environ.get("SR_PIPE_DMA_IN_X", "0") != "0"
+X_READS = float(os.environ.get("SR_PIPE_X_READS", "0.6"))
+Y_DMA = float(os.environ.get("SR_PIPE_Y_DMA", "0.8"))
+# XDL write -> VALU read of the same VGPR needs 11 wait states (8-pass 32x32x16): X's first exp2
+# reads the scores Y's last MFMA chain wrote ~10 instructions earlier, so pad
+X_LEAD_NOP = int(os.environ.get("SR_PIPE_X_LEAD_NOP", "2"))
+# timing-only experiments (WRONG results: they race the K/V ring): no per-tile barrier / a vmcnt
+# wait one tile looser
+NO_BARRIER = os.environ.get("SR_PIPE_EXP_NO_BARRIER") == "1"
+VM_SLACK = int(os.environ.get("SR_PIPE_EXP_VM_SLACK", "0"))
 
 
 def vr(a, n=1):
@@ -89,12 +106,6 @@ class Emit:
             self.waited = self.reads - 1
 
 
-def slot_derive(e, dst, k):
-    """dst = ring offset of tile t+k from %[slot] (tile t)."""
-    e.op(f"s_add_u32 {dst}, %[slot], {k * STAGE_B}")
-    e.op(f"s_and_b32 {dst}, {dst}, {RING_MASK}")
-
-
 class Phase:
     """One X or Y phase: an ordered MFMA list interleaved with filler units (VALU, LDS reads,
     LDS-DMA pieces), spread over the MFMA gaps by issue cost."""
@@ -128,38 +139,30 @@ class Phase:
                 self.valu.append((COST["cvt"], [f"v_cvt_pk_bf16_f32 {vr(dst + jj)}, {vr(src + 2 * jj)}, "
                                                 f"{vr(src + 2 * jj + 1)}"]))
 
-    def read_k(self, p, seqs):
-        """K fragments of the tile at KA into Kset[p] (8 ds_read_b128)."""
+    def read_k(self, p, slot, seqs):
+        """K fragments of the tile in ring slot `slot` into Kset[p] (8 ds_read_b128)."""
         for kb in range(2):
             for s in range(4):
-                lines = []
-                if s:
-                    lines.append(f"v_xor_b32 {vr(AT)}, {32 * s}, {vr(KA)}")
-                lines.append(("ds", f"ds_read_b128 {ar(kfrag(p, kb, s), 4)}, {vr(AT if s else KA)} "
-                                    f"offset:{kb * 4096}", seqs, (p, kb, s)))
+                lines = [("ds", f"ds_read_b128 {ar(kfrag(p, kb, s), 4)}, %[ka{s}] "
+                                f"offset:{slot * STAGE_B + kb * 4096}", seqs, (p, kb, s))]
                 self.other.append((COST["read"], lines, "read"))
 
-    def read_v(self, p, seqs):
-        """V^T fragments of the tile at VA into Vset[p] (16 ds_read_b64_tr_b16)."""
+    def read_v(self, p, slot, seqs):
+        """V^T fragments of the tile in ring slot `slot` into Vset[p] (16 ds_read_b64_tr_b16)."""
         for i, (kb, s2) in enumerate(EXP_ORDER):
             for db in range(2):
-                off = TILE_B + (kb * 32 + 16 * s2) * 128
-                a = vr(AT if db else VA)
+                off = slot * STAGE_B + TILE_B + (kb * 32 + 16 * s2) * 128
                 f = vfrag(p, i, db)
-                lines = []
-                if db:
-                    lines.append(f"v_xor_b32 {vr(AT)}, 64, {vr(VA)}")
-                lines.append(("ds", f"ds_read_b64_tr_b16 {ar(f, 2)}, {a} offset:{off}", None, None))
-                lines.append(("ds", f"ds_read_b64_tr_b16 {ar(f + 2, 2)}, {a} offset:{off + 1024}", seqs, (p, i, db)))
+                lines = [("ds", f"ds_read_b64_tr_b16 {ar(f, 2)}, %[va{db}] offset:{off}", None, None),
+                         ("ds", f"ds_read_b64_tr_b16 {ar(f + 2, 2)}, %[va{db}] offset:{off + 1024}", seqs, (p, i, db))]
                 self.other.append((2 * COST["read"], lines, "read"))
 
-    def dma(self):
-        """LDS-DMA of tile t+3 (4 pieces of 8 rows per wave) into slot (t+3) mod 4."""
-        first = ["s_add_u32 %[sst], %[sdma], %[ldsv]"]
+    def dma(self, slot):
+        """LDS-DMA of tile t+3 (4 pieces of 8 rows per wave) into ring slot `slot`; the per-lane
+        source offsets then step one tile."""
         for i in range(4):
-            lines = (first if i == 0 else []) + [
-                f"s_add_u32 m0, %[sst], {i * 1024}", "s_nop 0",
-                f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"]
+            lines = [f"s_add_u32 m0, %[ldsv], {slot * STAGE_B + i * 1024}", "s_nop 0",
+                     f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"]
             if i == 3:
                 lines += ["v_add_u32 %[dma0], %[sstep], %[dma0]", "v_add_u32 %[dma1], %[sstep], %[dma1]"]
             self.other.append((COST["dma"], lines, "dma"))
@@ -230,46 +233,44 @@ class Phase:
                 self._emit_unit(unit)
 
 
-def body(par, fill=False, drain=False, stage=True, vm=4):
-    """Tile t of parity par: K(t) in Kset[par] (read during X(t-1)), V(t-1) in Vset[par^1]."""
+def body(t4, fill=False, drain=False, stage=True, vm=4):
+    """Tile t with t % 4 == t4 (ring slot t4, register parity t4 & 1): K(t) in Kset[par] (read
+    during X(t-1)), V(t-1) in Vset[par ^ 1]."""
     e = Emit()
-    q = par ^ 1
-    e.op(f"; ---- tile body parity={par} fill={int(fill)} drain={int(drain)} stage={int(stage)} vmcnt={vm}")
+    par, q = t4 & 1, (t4 & 1) ^ 1
+    s_cur, s_next, s_stage = t4, (t4 + 1) & 3, (t4 + 3) & 3
+    e.op(f"; ---- tile body t%4={t4} fill={int(fill)} drain={int(drain)} stage={int(stage)} vmcnt={vm}")
     # tile t+1 landed (tile t+2's pieces may stay in flight); every wave is done with slot t-1
-    e.op(f"s_waitcnt vmcnt({vm})")
-    e.op("s_barrier")
+    e.op(f"s_waitcnt vmcnt({min(vm + VM_SLACK, 63)})")
+    if not NO_BARRIER:
+        e.op("s_barrier")
     kseqs, vseqs = {}, {}
     if fill:
         # K(0) into Kset[0], then q-block 0's scores of tile 0
-        e.op("s_add_u32 %[sk], %[slot], %[lds0]")
-        e.op(f"v_add_u32 {vr(KA)}, %[sk], %[koff0]")
         p = Phase(e)
-        p.read_k(par, kseqs)
+        p.read_k(par, s_cur, kseqs)
         p.qk(0, 0, par)
         p.qk(0, 1, par)
         p.emit(kseqs, vseqs, other_frac=0.01)
         e.wait_all_reads()
-    # addresses for X's reads: K of tile t+1, V of tile t
-    if not drain:
-        slot_derive(e, "%[sk]", 1)
-        e.op("s_add_u32 %[sk], %[sk], %[lds0]")
-        e.op(f"v_add_u32 {vr(KA)}, %[sk], %[koff0]")
-    e.op("s_add_u32 %[sv], %[slot], %[lds0]")
-    e.op(f"v_add_u32 {vr(VA)}, %[sv], %[voff0]")
-    # X(t)
+    # X(t): the LDS-DMA of tile t+3 first (its slot was freed by the barrier; the earlier it goes
+    # out, the longer it has to land), then K(t+1)
     p = Phase(e)
     p.qk(1, 0, par)
     if not fill:
         p.pv(1, q)
     p.qk(1, 1, par)
     p.exp(0)
+    if stage and DMA_IN_X:
+        p.dma(s_stage)
     if not drain:
-        p.read_k(q, kseqs)
-    p.read_v(par, vseqs)
-    p.emit(kseqs, vseqs, valu_lead=2 if fill else 1, lead_nop=15 if fill else 0)
-    # Y(t)
-    if stage:
-        slot_derive(e, "%[sdma]", 3)
+        p.read_k(q, s_next, kseqs)
+    if DMA_IN_X:
+        p.emit(kseqs, vseqs, valu_lead=2 if fill else 1, lead_nop=15 if fill else 0, other_frac=0.5)
+    else:
+        p.read_v(par, s_cur, vseqs)
+        p.emit(kseqs, vseqs, valu_lead=2 if fill else 1, lead_nop=15 if fill else X_LEAD_NOP, other_frac=X_READS)
+    # Y(t): V(t) early (P.V of q-block 0 starts after q.k^T's first chain)
     p = Phase(e)
     if not drain:
         p.qk(0, 0, q)
@@ -277,10 +278,12 @@ def body(par, fill=False, drain=False, stage=True, vm=4):
     if not drain:
         p.qk(0, 1, q)
     p.exp(1)
-    if stage:
-        p.dma()
+    if DMA_IN_X:
+        p.read_v(par, s_cur, vseqs)
+    elif stage:
+        p.dma(s_stage)
     # EXP1 reads S1 from X's last chain: two MFMAs and a pad first
-    p.emit(kseqs, vseqs, valu_lead=2, lead_nop=7, other_frac=0.8)
+    p.emit(kseqs, vseqs, valu_lead=2, lead_nop=7, other_frac=0.2 if DMA_IN_X else Y_DMA)
     if drain:
         # PV1(t): P1 was just written in place by EXP1 (VALU -> MFMA operand)
         e.op("s_nop 4")
@@ -288,42 +291,47 @@ def body(par, fill=False, drain=False, stage=True, vm=4):
         p.pv(1, par)
         p.emit(kseqs, vseqs)
     e.wait_all_reads()
-    slot_derive(e, "%[slot]", 1)
     return e.lines
 
 
 def main():
-    # tile 0 (fill, stages 3); pairs (odd, even) of staging tiles; an odd staging tile when
-    # ntiles - 4 is odd; then the last three tiles (no stage; vmcnt 4 / 0 / 0; the last drains),
-    # whose parities follow ntiles.  ntiles >= 4.
+    # tile 0 (fill, stages 3); groups of four staging tiles (t % 4 = 1, 2, 3, 0); the rem4 =
+    # (ntiles - 4) % 4 remaining staging tiles; then the last three tiles (no stage; vmcnt 4 / 0 / 0;
+    # the last one drains).  ntiles >= 4.
     L = lambda n: f"{n}_%="  # noqa: E731  (%= : a number unique to the asm statement instance)
     lines = body(0, fill=True)
-    lines += [f"{L('Lpair')}:", "s_cmp_eq_u32 %[n], 0", f"s_cbranch_scc1 {L('Lrem')}"]
-    loop = body(1) + body(0)
+    lines += [f"{L('Lgrp')}:", "s_cmp_eq_u32 %[n], 0", f"s_cbranch_scc1 {L('Lrem')}"]
+    loop = body(1) + body(2) + body(3) + body(0)
     lines += loop
-    lines += ["s_sub_u32 %[n], %[n], 1", f"s_branch {L('Lpair')}", f"{L('Lrem')}:"]
-    lines += ["s_cmp_eq_u32 %[rem], 0", f"s_cbranch_scc1 {L('Ltodd')}"]
-    # ntiles - 4 odd: tile ntiles-4 is odd, the tail starts on an even tile
-    lines += body(1)
-    lines += body(0, stage=False, vm=4) + body(1, stage=False, vm=0) + body(0, drain=True, stage=False, vm=0)
-    lines += [f"s_branch {L('Ldone')}", f"{L('Ltodd')}:"]
-    lines += body(1, stage=False, vm=4) + body(0, stage=False, vm=0) + body(1, drain=True, stage=False, vm=0)
+    lines += ["s_sub_u32 %[n], %[n], 1", f"s_branch {L('Lgrp')}", f"{L('Lrem')}:"]
+    for r in range(4):
+        lines += [f"s_cmp_eq_u32 %[rem], {r}", f"s_cbranch_scc1 {L(f'Lr{r}')}"]
+    for r in range(4):
+        lines += [f"{L(f'Lr{r}')}:"]
+        for k in range(r):  # staging tiles t % 4 = 1 .. r
+            lines += body(1 + k)
+        t0 = 1 + r          # first tail tile (mod 4)
+        lines += body(t0 & 3, stage=False, vm=4) + body((t0 + 1) & 3, stage=False, vm=0)
+        lines += body((t0 + 2) & 3, drain=True, stage=False, vm=0)
+        lines += [f"s_branch {L('Ldone')}"]
     lines += [f"{L('Ldone')}:"]
     # the compiler reads O / row sums right after the statement (XDL write -> read): pad
     lines += ["s_nop 15", "s_nop 15"]
     text = " \\\n".join("  \"" + l + "\\n\\t\"" for l in lines)
     clob = ", ".join([f'"v{r}"' for r in NAMED_V] + [f'"a{r}"' for r in NAMED_A])
-    n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 2
-    n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_cvt"))) // 2
-    n_ds = sum(1 for l in loop if l.startswith("ds_")) // 2
+    n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
+    n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_cvt"))) // 4
+    n_ds = sum(1 for l in loop if l.startswith("ds_")) // 4
+    n_all = sum(1 for l in loop if not l.startswith(";")) // 4
     with open(OUT, "w") as f:
         f.write("// GENERATED by tools/gen_attn_pipe.py — do not edit by hand.\n")
-        f.write(f"// per tile: {n_mfma} MFMA, {n_valu} exp/pack VALU, {n_ds} LDS fragment reads;\n")
+        f.write(f"// per tile: {n_mfma} MFMA, {n_valu} exp/pack VALU, {n_ds} LDS fragment reads, {n_all} instructions;\n")
         f.write(f"// {len(lines)} asm lines in all\n")
         f.write("#define SR_ATTN_PIPE_ASM \\\n")
         f.write(text + "\n")
         f.write("#define SR_ATTN_PIPE_CLOBBERS " + clob + "\n")
-    print(f"wrote {OUT}: per tile {n_mfma} MFMA / {n_valu} VALU / {n_ds} ds reads, {len(lines)} asm lines")
+    print(f"wrote {OUT}: per tile {n_mfma} MFMA / {n_valu} VALU / {n_ds} ds reads / {n_all} instructions, "
+          f"{len(lines)} asm lines")
 
 
 if __name__ == "__main__":

@@ -19,7 +19,7 @@ for step in "$@"; do
   case $step in
     kernels) run kernels 600 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu ;;
     parity)  run parity 900 python -m pytest tests/test_parity_gpu.py -x -q -m gpu ;;
-    gputests) run gputests 1200 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread ;;
+    gputests) run gputests 1200 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ;;
     newtests) run newtests 900 python -u -m pytest tests/test_baseline_shapes_gpu.py tests/test_layers_gpu.py \
                 tests/test_demo_entry_gpu.py tests/test_parity_gpu.py tests/test_train_graph_gpu.py -x -v -m gpu \
                 --timeout 600 --timeout-method thread ;;
@@ -36,6 +36,7 @@ for step in "$@"; do
     bench64) run bench64 600 python bench.py --views 64 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof64)  run prof64 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof64 -o run --output-format csv -- \
                python3 bench.py --views 64 --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing ;;
+    bench_extra) run bench_extra 600 python bench.py --steps 4 --warmup 1 --no-cpu-baseline --extra-c5 qkv ;;
     bench_c5) run bench_c5 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench_c5q) run bench_c5q 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline --fp8-global qkv ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
@@ -46,7 +47,7 @@ for step in "$@"; do
     kio)     run kio 300 python tools/kbench.py io ;;
     io_tests) run io_tests 600 python -m pytest tests/test_io_gpu.py -q -x ;;
     kattn)   run kattn 300 python tools/kbench.py attn ;;
-    dbg_pipe) run dbg_pipe 300 env SR_ATTN_PIPE=1 python tools/dbg_attn_pipe.py 1024 8192 8256 16384 43968 ;;
+    dbg_pipe) run dbg_pipe 300 env SR_ATTN_PIPE=1 python tools/dbg_attn_pipe.py 1024 8192 8256 16384 16448 16512 16576 43968 ;;
     kattn_ab) run kattn_ab0 300 env SR_ATTN_PIPE=0 SR_KB_STATIC=1 python tools/kbench.py attn && \
               run kattn_ab1 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 python tools/kbench.py attn && \
               run kattn_ab2 300 env SR_ATTN_PIPE=0 SR_KB_STATIC=1 python tools/kbench.py attn && \
@@ -57,6 +58,16 @@ for step in "$@"; do
               -x -q -m gpu -k "attention or attn" --timeout 600 --timeout-method thread ;;
     c4test)  run c4test 900 python -u -m pytest tests/test_c4_golden_gpu.py -x -v -s -m gpu --timeout 900 --timeout-method thread ;;
     fp8test) run fp8test 900 python -u -m pytest tests/test_parity_gpu.py -x -v -s -m gpu -k fp8 --timeout 600 --timeout-method thread ;;
+    kattn_var) for i in 1 2; do
+                 run kattn_v0_$i 300 env SR_ATTN_PIPE=0 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
+                 for v in $PIPE_VARIANTS; do
+                   run kattn_${v}_$i 300 env SFM_AMD_LIB=variants/libsfm_$v.so SR_ATTN_PIPE=1 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
+                 done
+                 run kattn_main_$i 300 env SR_ATTN_PIPE=1 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
+               done ;;
+    dbg_var) for v in $PIPE_VARIANTS; do
+               run dbg_$v 300 env SFM_AMD_LIB=variants/libsfm_$v.so SR_ATTN_PIPE=1 python tools/dbg_attn_pipe.py 8192 8256 16384 16448 43968 || exit 1
+             done ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
