@@ -105,8 +105,9 @@ def host_cpu():
 
 # timer class -> the kernel instantiation it launches at the N=32@518 workload
 # (rocprofv3 row names; see DESIGN.md "Kernels").
+_PIPE = "true" if os.environ.get("SR_ATTN_PIPE", "1") != "0" else "false"  # sr_attn.hip: the asm sweep
 KERNEL_OF_TAG = {
-    "attn_global": "attn_bf16_kernel<4, 2, 2, false>", "attn_reloc": "attn_bf16_kernel<4, 2, 1, false>",
+    "attn_global": f"attn_bf16_kernel<4, 2, 2, {_PIPE}>", "attn_reloc": "attn_bf16_kernel<4, 2, 1, false>",
     "attn_frame": "attn_bf16_kernel<4, 2, 0, false>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
     "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
 }

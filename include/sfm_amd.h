@@ -169,6 +169,10 @@ typedef struct sr_attn_desc {
      SDPA's math path. */
   const void* mask;
   int64_t mask_bstride, mask_hstride, mask_ld;
+  int32_t tail_rows_readable; /* optional (bf16 path): >= 64 = the caller guarantees at least 64
+                  readable rows of finite values past the end of every key segment (K and V; e.g.
+                  the next frame's rows or zeroed workspace padding), so the hand-scheduled sweep
+                  may stage a ragged last tile whole and mask its extra keys; 0 = unset */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */

@@ -447,8 +447,11 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
   bool asm_ok = false;
   if constexpr (PIPE) {
     // (the asm derives every fragment address from koff[0] / voff0 by XOR: lds0 % 128 == 0)
-    bool ok = wave_active && use_bound && args.allow_mzero && args.ntile1 == 0 && len0 % KT == 0 && ntiles >= 4 &&
-              (lds0 & 127) == 0;
+    // one segment of full tiles: SR_ATTN_PIPE_ASM; two segments or ragged tails: the _SEG variant,
+    // which stages a ragged tile whole (caller-guaranteed readable rows past each segment's end)
+    const bool simple = args.ntile1 == 0 && len0 % KT == 0;
+    bool ok = wave_active && use_bound && args.allow_mzero && ntiles >= 4 && (lds0 & 127) == 0 &&
+              (simple || d.tail_rows_readable >= KT);
 #pragma unroll
     for (int b = 0; b < QB; ++b) ok = ok && qb[b] <= 50.f;
     asm_ok = __builtin_amdgcn_readfirstlane(__all(ok)) != 0;
@@ -470,6 +473,39 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
     // fragment lane addresses (ring slot and block offsets ride in the instructions' offset field)
     const uint32_t ka0 = lds0 + koff[0], ka1 = lds0 + koff[1], ka2 = lds0 + koff[2], ka3 = lds0 + koff[3];
     const uint32_t va0 = lds0 + voff0, va1 = lds0 + voff1;
+    if (!(args.ntile1 == 0 && len0 % KT == 0)) {
+      // segment switch when tile nt0 is staged (the asm stages tile t+3 during tile t); a switch
+      // inside the C++ prologue (nt0 <= 2) already left sp / sstep on segment 1
+      const uint32_t nsw = nt0 >= LOOK && args.ntile1 > 0 ? (uint32_t)(nt0 - LOOK) : 0xffffffffu;
+      const char* p1 = (const char*)d.k1 != nullptr ? sb1 + (srb1 + grow0) * sld1 * 2 : spb;
+      const uint64_t p1u = (uint64_t)(uintptr_t)p1;
+      const uint32_t p1lo = __builtin_amdgcn_readfirstlane((uint32_t)p1u);
+      const uint32_t p1hi = __builtin_amdgcn_readfirstlane((uint32_t)(p1u >> 32));
+      const char* sp1 = (const char*)(uintptr_t)(((uint64_t)p1hi << 32) | p1lo);
+      const int64_t s8_1 = 8 * sld1 * 2;
+      const char* sp1b = sp1 + 2 * s8_1;
+      const uint32_t dm10 = voA1, dm11 = voB1 + (uint32_t)s8_1;
+      const uint32_t sstep1 = __builtin_amdgcn_readfirstlane((uint32_t)(KT * sld1 * 2));
+      uint32_t sstc = sst32;
+      // ragged tails: the tile index and the per-lane valid-key threshold (valid - 4 hi; a score's
+      // key within the tile is kb*32 + (r&3) + 8(r>>2) + 4 hi)
+      const uint32_t trag0 = len0 % KT ? (uint32_t)(nt0 - 1) : 0xffffffffu;
+      const uint32_t trag1 = args.ntile1 > 0 && len1 % KT ? (uint32_t)(ntiles - 1) : 0xffffffffu;
+      const int vk0 = len0 % KT - 4 * hi, vk1 = len1 % KT - 4 * hi;
+      const float ninf = -INFINITY;
+      uint32_t tcur = 0;
+      asm volatile(SR_ATTN_PIPE_ASM_SEG
+                   : [o00] "+&a"(o[0][0]), [o01] "+&a"(o[0][1]), [o10] "+&a"(o[1][0]), [o11] "+&a"(o[1][1]),
+                     [l0] "+&a"(lacc[0]), [l1] "+&a"(lacc[1]), [dma0] "+&v"(dm[0]), [dma1] "+&v"(dm[1]),
+                     [n] "+&s"(nn), [sp] "+&s"(spb), [sp2] "+&s"(spb2), [sstc] "+&s"(sstc), [tcur] "+&s"(tcur)
+                   : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
+                     [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
+                     [suma] "v"(sum_a), [ka0] "v"(ka0), [ka1] "v"(ka1), [ka2] "v"(ka2), [ka3] "v"(ka3),
+                     [va0] "v"(va0), [va1] "v"(va1), [ldsv] "s"(ldsv), [rem] "s"(rem), [nsw] "s"(nsw),
+                     [sp1] "s"(sp1), [sp1b] "s"(sp1b), [sstep1] "s"(sstep1), [dm10] "v"(dm10), [dm11] "v"(dm11),
+                     [trag0] "s"(trag0), [trag1] "s"(trag1), [vk0] "v"(vk0), [vk1] "v"(vk1), [ninf] "v"(ninf)
+                   : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc", "vcc");
+    } else
     asm volatile(SR_ATTN_PIPE_ASM
                  // every output early-clobber: the asm writes them while it still reads inputs (an
                  // input of equal value may otherwise share a tied output's register)
@@ -1316,6 +1352,16 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
       const char* e = getenv("SR_ATTN_PIPE");
       return e ? atoi(e) != 0 : true;
     }();
+    // ... and, opt-in (SR_ATTN_PIPE_SEG=1), for two-segment / ragged launches (reloc, frame, DINO)
+    // whose rows past each segment's end are readable.  Correct (the production-shape tests run it)
+    // but not faster: at one workgroup per CU the ragged last q-tile of each 1,374-row frame leaves
+    // two of its four SIMDs idle for the whole sweep (a second workgroup fills them in the compiled
+    // kernel), and a frame's 22-tile sweep does not hide the workgroup's prologue / epilogue
+    // (kbench: reloc 1.835-1.846 vs 1.828-1.852 ms, frame 0.609-0.611 vs 0.559-0.576 ms)
+    static const bool pipe_seg = [] {
+      const char* e = getenv("SR_ATTN_PIPE_SEG");
+      return e ? atoi(e) != 0 : false;
+    }();
     dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
 #define SR_ATTN_LAUNCH(NW_, QB_, ST_)                                                                           \
   do {                                                                                                        \
@@ -1325,8 +1371,9 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   } while (0)
     if (cfg == 1) SR_ATTN_LAUNCH(8, 1, false);
     else if (cfg == 2) SR_ATTN_LAUNCH(2, 2, false);
-    else if (pipe && d.l1 == 0 && d.l0 % KT == 0 && (d.key_bound || d.key_norm_max > 0.f))
-      SR_ATTN_LAUNCH(4, 2, true);  // one key segment of full tiles with a key bound (the asm sweep)
+    else if (pipe && (d.key_bound || d.key_norm_max > 0.f) &&
+             ((d.l1 == 0 && d.l0 % KT == 0) || (pipe_seg && d.tail_rows_readable >= KT)))
+      SR_ATTN_LAUNCH(4, 2, true);  // the asm sweep: one segment of full tiles, or (_SEG) two / ragged
     else SR_ATTN_LAUNCH(4, 2, false);
 #undef SR_ATTN_LAUNCH
     return sr::check_launch("sr_attention(bf16)");

@@ -44,6 +44,10 @@ struct GemmArgs {
   int kt_per_split;  // split-K (gemm_kernel, gridDim.y slices): k-tiles per slice
   float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
   int group_m;       // 256x256 kernels: tile order in groups of group_m row tiles (<= 1: row-major)
+  // 256x256 RESID kernels, stream-K tail: the first sk_dp tiles run data-parallel (whole rounds);
+  // sk_wgs > 0 workgroups split the remaining tiles' k-iterations evenly and add their partial
+  // products with fp32 atomics (the residual update is linear in the accumulator)
+  int sk_dp, sk_wgs;
   sr_gemm_epi ep;
   // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
   // (n, yo, xo) of the NHWC fp32 input x [n][H][W][C], A column k = (ky, kx, ci) — exactly
@@ -350,6 +354,32 @@ __device__ __forceinline__ void resid_full(const GemmArgs& g, f32x4 (&acc)[8][4]
   }
 }
 
+// Stream-K piece of a RESID tile: x += gamma * (acc (+ bias)) as fp32 atomics (no read of x;
+// the pieces of one tile add in any order).  Vector atomics (global_atomic_add_f32), rows < M.
+__device__ __forceinline__ void resid_atomic(const GemmArgs& g, f32x4 (&acc)[8][4], int rowbase, int colw, int lr,
+                                             int lg, bool with_bias) {
+  const sr_gemm_epi& ep = g.ep;
+  f32x4 gm[4], bs[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col = colw + ni * 16 + 4 * lg;
+    gm[ni] = *(const f32x4*)(ep.gamma + col);
+    bs[ni] = with_bias && ep.bias ? *(const f32x4*)(ep.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int row = rowbase + mi * 16 + lr;
+    if (row >= g.M) continue;
+    float* xr = (float*)g.out + (int64_t)row * g.ldo + colw + 4 * lg;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const f32x4 v = (acc[mi][ni] + bs[ni]) * gm[ni];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) unsafeAtomicAdd(xr + ni * 16 + r, v[r]);
+    }
+  }
+}
+
 // bias (+ erf-GELU) -> bf16 for a full 256x256 tile (every row < M; N % 256 == 0 here; no aux):
 // the guarded produce/emit form compiles to an exec branch around every one of the 32 stores
 // per lane; here they are plain stores with the math of the next vectors in between.
@@ -616,12 +646,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
 constexpr int BIG = 256;
 constexpr int STAGE_BIG = 2 * BIG * ROWB;  // 64 KiB
 
+// One output tile over k-tiles [kb, ke).  sk_part: a stream-K piece of a RESID tile, whose
+// x += gamma * (acc (+ bias on the piece holding k-tile 0)) goes out as fp32 atomics.
 template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+__device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke,
+                                             bool sk_part) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = g.N / BIG, ntm = (g.M + BIG - 1) / BIG;
-  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
   int tm, tn;
   if (g.group_m > 1) {  // column-major inside groups of group_m row tiles
     const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
@@ -683,11 +714,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   {
-    stage(0);
-    for (int kt = 0; kt < g.ktiles; ++kt) {
+    stage(kb);
+    for (int kt = kb; kt < ke; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
       sr::barrier_raw();                                  // ... every wave's; all done with kt-1
-      const bool more = kt + 1 < g.ktiles;
+      const bool more = kt + 1 < ke;
       // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
       // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
       // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
@@ -742,6 +773,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     }
   }
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    if (sk_part) {
+      resid_atomic(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg, kb == 0);
+      return;
+    }
     if (m0 + BIG <= g.M && !g.lds_epi) {
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
       return;
@@ -758,6 +793,32 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 }
 
 template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
+  if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    if (g.sk_wgs > 0 && (int)blockIdx.x >= g.sk_dp) {
+      // stream-K: workgroup j takes k-iterations [j*per, (j+1)*per) of the tail tiles, one
+      // contiguous run per tile it touches (at most a few), each with its own atomic epilogue
+      const int j = blockIdx.x - g.sk_dp;
+      const int total = (nt - g.sk_dp) * g.ktiles;
+      const int per = (total + g.sk_wgs - 1) / g.sk_wgs;
+      int it = j * per;
+      const int end = min(total, it + per);
+      while (it < end) {
+        const int tl = it / g.ktiles, k0 = it - tl * g.ktiles;
+        const int k1 = min(g.ktiles, k0 + (end - it));
+        gemm256_tile<EPI>(g, smem, g.sk_dp + tl, k0, k1, true);
+        it += k1 - k0;
+        if (it < end) sr::barrier_raw();  // every wave done with the LDS stages before the next run
+      }
+      return;
+    }
+  }
+  gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, g.sk_wgs > 0 ? g.sk_dp : nt), 0, g.ktiles, false);
+}
+
+template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
   // tile order: column-major inside groups of 4 row tiles for the wide outputs (fc1, QKV:
@@ -768,7 +829,33 @@ int launch256(GemmArgs a, hipStream_t s) {
     return e ? atoi(e) : -1;
   }();
   a.group_m = group_m >= 0 ? group_m : (a.N >= 3072 ? 4 : 0);
-  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
+  a.sk_dp = nwg;
+  a.sk_wgs = 0;
+  int grid = nwg;
+  if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    // stream-K tail, opt-in (SR_GEMM_SK=1): whole rounds stay data-parallel; a last round that
+    // fills less than ~85 % of the CUs is split over every CU by k-iterations (>= 4 per piece).
+    // Correct (test_gemm256_tiles) but much slower: the pieces' fp32 atomics cost more than the
+    // idle CUs of the tail (kbench, same box: proj M=87,936 0.50 vs 0.30 ms, fc2 0.88 vs 0.72,
+    // proj M=43,968 0.42 vs 0.14) -- see DESIGN.md "GEMM" for why a fixup pass would not pay either
+    static const int sk_mode = [] {
+      const char* e = getenv("SR_GEMM_SK");
+      return e ? atoi(e) : 0;
+    }();
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return n > 0 ? n : 256;
+    }();
+    const int tail = nwg % cus;
+    if (sk_mode && nwg > cus && tail > 0 && tail * 100 < cus * 85) {
+      a.sk_dp = nwg - tail;
+      a.sk_wgs = std::min(cus, tail * a.ktiles / 4);
+      grid = a.sk_dp + a.sk_wgs;
+    }
+  }
+  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
   return sr::check_launch("sr_gemm(256)");
 }
 

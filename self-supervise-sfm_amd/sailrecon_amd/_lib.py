@@ -59,6 +59,7 @@ class AttnDesc(ctypes.Structure):
         ("key_norm_max", _f32),
         ("o_bstride", _i64),
         ("mask", _vp), ("mask_bstride", _i64), ("mask_hstride", _i64), ("mask_ld", _i64),
+        ("tail_rows_readable", _i32),
     ]
 
 

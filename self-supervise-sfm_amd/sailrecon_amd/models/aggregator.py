@@ -245,7 +245,7 @@ class Aggregator(nn.Module):
             ops.set_special_tokens(x, F_, P, dtab, zero_t)
             for blk in dino.blocks:
                 pb = blk.packed(dtype)
-                runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P), None)
+                runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True), None)
             ops.layernorm(x, dino.norm.weight, dino.norm.bias, dino.norm.eps, x)  # in place (row-local)
 
         # ---- aggregator special tokens, aggregator.py:287-299 (type by ORIGINAL frame index)
@@ -348,7 +348,7 @@ class Aggregator(nn.Module):
         # ---- alternating layers, aggregator.py:339-423
         for l in range(self.depth):
             pb = self.frame_blocks[l].packed(dtype)
-            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P),
+            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True),
                               runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
             if l in out_maps and Nq_l > 0:  # frame half of the intermediate, :403-413
                 for b in range(B):
@@ -439,7 +439,7 @@ class Aggregator(nn.Module):
         out_maps = {l: torch.empty(1, S, P, 2 * C, device=dev, dtype=torch.float32) for l in self.intermediate_layer_idx}
         for l in range(self.depth):
             pb = self.frame_blocks[l].packed(dtype)
-            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P),
+            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True),
                               runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
             if l in out_maps:
                 ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, :C], x, R)
@@ -516,7 +516,7 @@ class Aggregator(nn.Module):
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
                               k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                              key_norm_max=runtime.key_norm_bound(pr))
+                              key_norm_max=runtime.key_norm_bound(pr), tail_readable=True)
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
                 with torch.cuda.stream(side):

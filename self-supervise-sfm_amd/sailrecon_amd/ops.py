@@ -242,7 +242,7 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
               scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
-              key_norm_max: float = 0.0, mask: Optional[Tensor] = None) -> None:
+              key_norm_max: float = 0.0, mask: Optional[Tensor] = None, tail_readable: bool = False) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``mask``
     (mask_mode SR_MASK_DENSE: bool / uint8, nonzero = attend; SR_MASK_ADD: fp32 added to the
     scores) is a [batch, heads, lq, l0 + l1] view (broadcast dims may have stride 0, the last dim
@@ -250,7 +250,10 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd.
     ``key_norm_max`` > 0: a static bound of every key's per-head 2-norm (runtime.key_norm_bound),
     which replaces the key scan of the fixed-offset sweep.  A bf16 single query set too short to
-    fill the chip runs key-split (key_split_parts, attention_partials + attn_merge_n)."""
+    fill the chip runs key-split (key_split_parts, attention_partials + attn_merge_n).
+    ``tail_readable``: at least 64 rows of finite values follow every key segment in memory
+    (runtime.Workspace buffers: zero-initialised, 64 rows of padding), which lets the
+    hand-scheduled sweep take ragged and two-segment launches (sr_attn_desc.tail_rows_readable)."""
     parts = key_split_parts(dtype=q.dtype, batch=batch, lq=lq, heads=heads, l0=l0, l1=l1, mask_mode=mask_mode)
     if parts > 1:
         if lse is not None and (lse.dtype != torch.float32 or not lse.is_contiguous() or lse.numel() != heads * lq):
@@ -263,6 +266,8 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
                    n_anchor=n_anchor, scale=scale, lse=lse)
+    if tail_readable:
+        d.tail_rows_readable = 64
     if mask_mode in (_lib.SR_MASK_DENSE, _lib.SR_MASK_ADD):
         want = torch.float32 if mask_mode == _lib.SR_MASK_ADD else (torch.bool, torch.uint8)
         if mask is None or mask.dim() != 4 or tuple(mask.shape) != (batch, heads, lq, l0 + l1) or \

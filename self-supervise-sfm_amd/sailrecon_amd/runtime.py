@@ -134,7 +134,12 @@ def pack_attention(a, dtype: torch.dtype) -> PackedBlock:
 
 
 class Workspace:
-    """Grow-only device scratch, keyed by name (reused across forwards)."""
+    """Grow-only device scratch, keyed by name (reused across forwards).  Buffers are zeroed when
+    allocated and carry PAD_ROWS rows of padding, so every row past a view's end is readable and
+    finite (ops.attention(tail_readable=True): the hand-scheduled attention sweep stages a ragged
+    last key tile whole)."""
+
+    PAD_ROWS = 64
 
     def __init__(self):
         self._bufs: Dict[str, Tensor] = {}
@@ -142,8 +147,9 @@ class Workspace:
     def get(self, name: str, rows: int, cols: int, dtype: torch.dtype, device) -> Tensor:
         t = self._bufs.get(name)
         need = rows * cols
-        if t is None or t.dtype != dtype or t.device != torch.device(device) or t.numel() < need:
-            t = torch.empty(max(need, 1), dtype=dtype, device=device)
+        if t is None or t.dtype != dtype or t.device != torch.device(device) or \
+                t.numel() < need + self.PAD_ROWS * cols:
+            t = torch.zeros(need + self.PAD_ROWS * max(cols, 1), dtype=dtype, device=device)
             self._bufs[name] = t
         return t[:need].view(rows, cols)
 
@@ -209,13 +215,14 @@ def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
              tag="gemm")
 
 
-def frame_attend(pb: PackedBlock, frames: int, tokens: int) -> Callable[[Tensor, Tensor], None]:
-    """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C])."""
+def frame_attend(pb: PackedBlock, frames: int, tokens: int, tail_readable: bool = False) -> Callable[[Tensor, Tensor], None]:
+    """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C]).
+    ``tail_readable``: the qkv buffers come from a Workspace (rows past the last frame readable)."""
     C, D = pb.dim, pb.head_dim
     kb = key_norm_bound(pb)
 
     def attend(qkv: Tensor, o: Tensor) -> None:
         ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads, head_dim=D,
                       batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_frame",
-                      key_norm_max=kb)
+                      key_norm_max=kb, tail_readable=tail_readable)
     return attend

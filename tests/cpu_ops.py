@@ -81,7 +81,7 @@ def _positions(qkv, M):
 
 def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None, lse=None,
-              key_norm_max=0.0):
+              key_norm_max=0.0, mask=None, tail_readable=False):
     D = head_dim
     scale = D ** -0.5 if scale is None else scale
     for b in range(batch):

@@ -314,17 +314,29 @@ def test_global_attention_fp8_production(ops, L, fp8_v, bound):
     assert e_exact < 0.15
 
 
+def _padded(t, rows=64):
+    """t with `rows` zero rows after it in memory (a runtime.Workspace buffer's padding)."""
+    buf = torch.zeros(t.shape[0] + rows, *t.shape[1:], device=t.device, dtype=t.dtype)
+    buf[:t.shape[0]] = t
+    return buf[:t.shape[0]]
+
+
+@pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
 @pytest.mark.parametrize("nq,nsub", [(8, 8 * PP), (32, 32 * PP), (4, 32 * PP), (8, 32 * PP)],
                          ids=["C2", "C3", "C3-8rk", "C3-4rk"])
-def test_reloc_attention_production(ops, nq, nsub):
+def test_reloc_attention_production(ops, nq, nsub, tail):
     """global_reloc (aggregator.py:672-741): every query frame attends to the shared anchor
     subsample (segment 0, batch stride 0) and to its own frame (segment 1); C3-8rk / C3-4rk are
-    the per-rank shapes of the frame-sharded C3 forward (4 / 8 query frames)."""
+    the per-rank shapes of the frame-sharded C3 forward (4 / 8 query frames).  asm-seg: readable
+    rows past each segment (tail_readable, as the aggregator's workspace buffers) send the launch
+    through the hand-scheduled sweep's two-segment / ragged-tail variant."""
     q, k, v = _make(nq * P, 3, spikes=(nq * P - 11,))
     ks, _, vs = _make(nsub, 4, spikes=(nsub - 3,))
+    if tail:
+        k, v, ks, vs = _padded(k), _padded(v), _padded(ks), _padded(vs)
     o = torch.empty(nq * P, C, device=DEV, dtype=torch.bfloat16)
     ops.attention(q, ks, vs, o, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
-                  k1=k, v1=v, l1=P, k1_bstride=P)
+                  k1=k, v1=v, l1=P, k1_bstride=P, tail_readable=tail)
     frames = sorted(set([0, nq - 1] + torch.randperm(nq, generator=torch.Generator().manual_seed(nq))[:6].tolist()))
     scale = D ** -0.5
     for j in frames:
@@ -336,12 +348,17 @@ def test_reloc_attention_production(ops, nq, nsub):
         assert _rel(o[fr][rows].float(), ref) < 1e-2, j
 
 
-def test_frame_attention_production(ops):
-    """frame / DINO stacks at C3: 64 frames x 1374 tokens, keys = own frame."""
+@pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
+def test_frame_attention_production(ops, tail):
+    """frame / DINO stacks at C3: 64 frames x 1374 tokens, keys = own frame (asm-seg: the ragged
+    last key tile staged whole from readable rows and masked in the hand-scheduled sweep)."""
     S = 64
     q, k, v = _make(S * P, 5, spikes=(S * P - 2,))
+    if tail:
+        k, v = _padded(k), _padded(v)
     o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
-    ops.attention(q, k, v, o, heads=H, head_dim=D, batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P)
+    ops.attention(q, k, v, o, heads=H, head_dim=D, batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P,
+                  tail_readable=tail)
     scale = D ** -0.5
     for j in (0, 17, 40, S - 1):
         fr = slice(j * P, (j + 1) * P)

@@ -52,11 +52,12 @@ def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
     assert rel(out.float(), F.gelu(ref)) < tol
 
 
-@pytest.mark.parametrize("M,N,K", [(8300, 4096, 128), (33000, 1024, 192), (32769, 1024, 64)])
+@pytest.mark.parametrize("M,N,K", [(8300, 4096, 128), (33000, 1024, 192), (32769, 1024, 64), (87936, 1024, 1024),
+                                   (43968, 1024, 4096)])
 def test_gemm256_tiles(ops, M, N, K):
     """>= 512 256x256 tiles select the 256x256 bf16 kernel (the production path):
     ragged last M tile (including slabs that start past row M-1), every bf16 epilogue that
-    runs on it at this width."""
+    runs on it at this width (the C3 frame / global proj and fc2 shapes included)."""
     L = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N)
     a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
@@ -73,6 +74,35 @@ def test_gemm256_tiles(ops, M, N, K):
     ops.gemm(a, w, x[32:32 + M], L.SR_EPI_BIAS_RESID, bias=b, gamma=gam)
     assert torch.equal(x[:32], x0[:32]) and torch.equal(x[32 + M:], x0[32 + M:])
     assert rel(x[32:32 + M] - x0[32:32 + M], ref * gam) < 1e-5
+
+
+def test_gemm256_streamk_tail(ops):
+    """The opt-in stream-K tail of the RESID 256x256 GEMM (SR_GEMM_SK=1): a last round under ~85 %
+    of the CUs is split by k-iterations over every CU, the pieces adding x += gamma (acc (+ b)) with
+    fp32 atomics.  8300 / 33000 / 32769 rows give pieces spanning 2-4 tiles; the C3 frame (87,936)
+    and global (43,968) proj / fc2 shapes 6- and 11-iteration pieces."""
+    import subprocess
+    import sys
+    code = (
+        "import math, torch, sys\n"
+        "sys.path.insert(0, 'self-supervise-sfm_amd')\n"
+        "from sailrecon_amd import ops, _lib as L\n"
+        "for M, N, K in [(8300, 4096, 128), (33000, 1024, 192), (32769, 1024, 64), (87936, 1024, 1024), (43968, 1024, 4096)]:\n"
+        "    g = torch.Generator().manual_seed(M + N)\n"
+        "    a = torch.randn(M, K, generator=g).cuda().bfloat16()\n"
+        "    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).cuda().bfloat16()\n"
+        "    b, gam = torch.randn(N, generator=g).cuda(), torch.randn(N, generator=g).cuda()\n"
+        "    ref = a.float() @ w.float().t() + b\n"
+        "    x = torch.randn(M + 64, N, device='cuda'); x0 = x.clone()\n"
+        "    ops.gemm(a, w, x[32:32 + M], L.SR_EPI_BIAS_RESID, bias=b, gamma=gam)\n"
+        "    assert torch.equal(x[:32], x0[:32]) and torch.equal(x[32 + M:], x0[32 + M:])\n"
+        "    d = (x[32:32 + M] - x0[32:32 + M]).double(); r = (ref * gam).double()\n"
+        "    e = float((d - r).norm() / r.norm()); print(M, N, K, e); assert e < 1e-5, (M, N, K, e)\n")
+    import os
+    env = dict(os.environ, SR_GEMM_SK="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
 
 
 @pytest.mark.parametrize("dtype,tol", DT)

@@ -57,6 +57,20 @@ Y_DMA = float(os.environ.get("SR_PIPE_Y_DMA", "0.8"))
 # XDL write -> VALU read of the same VGPR needs 11 wait states (8-pass 32x32x16): X's first exp2
 # reads the scores Y's last MFMA chain wrote ~10 instructions earlier, so pad
 X_LEAD_NOP = int(os.environ.get("SR_PIPE_X_LEAD_NOP", "2"))
+# SR_ATTN_PIPE_ASM_SEG (generated with SEG = True): two key segments (the DMA source switches to
+# segment 1's base, offsets and tile stride when tile nt0 is staged: %[nsw] = nt0 - 3) and ragged
+# segment tails (scores of keys past a segment's end -> -inf before their exp2: tiles %[trag0] /
+# %[trag1], per-lane valid-key thresholds %[vk0] / %[vk1] = valid - 4 hi).  The staging then reads
+# up to 63 rows past a segment's end: the caller guarantees them readable and finite.
+SEG = False
+_LABEL = [0]
+
+
+def _label(stem):
+    _LABEL[0] += 1
+    return f"L{stem}{_LABEL[0]}_%="
+
+
 # timing-only experiments (WRONG results: they race the K/V ring): no per-tile barrier / a vmcnt
 # wait one tile looser
 NO_BARRIER = os.environ.get("SR_PIPE_EXP_NO_BARRIER") == "1"
@@ -160,11 +174,18 @@ class Phase:
     def dma(self, slot):
         """LDS-DMA of tile t+3 (4 pieces of 8 rows per wave) into ring slot `slot`; the per-lane
         source offsets then step one tile."""
+        step = "%[sstc]" if SEG else "%[sstep]"
         for i in range(4):
-            lines = [f"s_add_u32 m0, %[ldsv], {slot * STAGE_B + i * 1024}", "s_nop 0",
-                     f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"]
+            lines = []
+            if SEG and i == 0:
+                sk = _label("sw")
+                lines += ["s_cmp_eq_u32 %[tcur], %[nsw]", f"s_cbranch_scc0 {sk}",
+                          "s_mov_b64 %[sp], %[sp1]", "s_mov_b64 %[sp2], %[sp1b]", "s_mov_b32 %[sstc], %[sstep1]",
+                          "v_mov_b32 %[dma0], %[dm10]", "v_mov_b32 %[dma1], %[dm11]", f"{sk}:"]
+            lines += [f"s_add_u32 m0, %[ldsv], {slot * STAGE_B + i * 1024}", "s_nop 0",
+                      f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"]
             if i == 3:
-                lines += ["v_add_u32 %[dma0], %[sstep], %[dma0]", "v_add_u32 %[dma1], %[sstep], %[dma1]"]
+                lines += [f"v_add_u32 %[dma0], {step}, %[dma0]", f"v_add_u32 %[dma1], {step}, %[dma1]"]
             self.other.append((COST["dma"], lines, "dma"))
 
     # ---- emission
@@ -233,6 +254,23 @@ class Phase:
                 self._emit_unit(unit)
 
 
+def mask_scores(e, b):
+    """SEG: if the current tile is a ragged segment tail, S_b of its keys past the segment's end
+    -> -inf (rare path; the scores were just written by MFMAs: pad first)."""
+    for j in range(2):
+        lab = _label("m")
+        e.op(f"s_cmp_eq_u32 %[tcur], %[trag{j}]")
+        e.op(f"s_cbranch_scc0 {lab}")
+        e.op("s_nop 15")
+        for kb in range(2):
+            for r in range(16):
+                c = kb * 32 + (r & 3) + 8 * (r >> 2)  # key of S_b[16 kb + r] in the tile is c + 4 hi
+                reg = vr(S[b] + 16 * kb + r)
+                e.op(f"v_cmp_ge_i32 vcc, {c}, %[vk{j}]")
+                e.op(f"v_cndmask_b32 {reg}, {reg}, %[ninf], vcc")
+        e.op(f"{lab}:")
+
+
 def body(t4, fill=False, drain=False, stage=True, vm=4):
     """Tile t with t % 4 == t4 (ring slot t4, register parity t4 & 1): K(t) in Kset[par] (read
     during X(t-1)), V(t-1) in Vset[par ^ 1]."""
@@ -253,6 +291,8 @@ def body(t4, fill=False, drain=False, stage=True, vm=4):
         p.qk(0, 1, par)
         p.emit(kseqs, vseqs, other_frac=0.01)
         e.wait_all_reads()
+    if SEG:
+        mask_scores(e, 0)  # S0(t): EXP0 runs in X
     # X(t): the LDS-DMA of tile t+3 first (its slot was freed by the barrier; the earlier it goes
     # out, the longer it has to land), then K(t+1)
     p = Phase(e)
@@ -270,6 +310,8 @@ def body(t4, fill=False, drain=False, stage=True, vm=4):
     else:
         p.read_v(par, s_cur, vseqs)
         p.emit(kseqs, vseqs, valu_lead=2 if fill else 1, lead_nop=15 if fill else X_LEAD_NOP, other_frac=X_READS)
+    if SEG:
+        mask_scores(e, 1)  # S1(t) (X's chains): EXP1 runs in Y
     # Y(t): V(t) early (P.V of q-block 0 starts after q.k^T's first chain)
     p = Phase(e)
     if not drain:
@@ -291,10 +333,12 @@ def body(t4, fill=False, drain=False, stage=True, vm=4):
         p.pv(1, par)
         p.emit(kseqs, vseqs)
     e.wait_all_reads()
+    if SEG:
+        e.op("s_add_u32 %[tcur], %[tcur], 1")
     return e.lines
 
 
-def main():
+def sweep():
     # tile 0 (fill, stages 3); groups of four staging tiles (t % 4 = 1, 2, 3, 0); the rem4 =
     # (ntiles - 4) % 4 remaining staging tiles; then the last three tiles (no stage; vmcnt 4 / 0 / 0;
     # the last one drains).  ntiles >= 4.
@@ -317,21 +361,29 @@ def main():
     lines += [f"{L('Ldone')}:"]
     # the compiler reads O / row sums right after the statement (XDL write -> read): pad
     lines += ["s_nop 15", "s_nop 15"]
-    text = " \\\n".join("  \"" + l + "\\n\\t\"" for l in lines)
+    return lines, loop
+
+
+def main():
+    global SEG
+    out = ["// GENERATED by tools/gen_attn_pipe.py — do not edit by hand."]
+    for seg, name in ((False, "SR_ATTN_PIPE_ASM"), (True, "SR_ATTN_PIPE_ASM_SEG")):
+        SEG = seg
+        lines, loop = sweep()
+        n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
+        n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_cvt"))) // 4
+        n_ds = sum(1 for l in loop if l.startswith("ds_")) // 4
+        n_all = sum(1 for l in loop if not l.startswith((";", "L")) and not l.endswith(":")) // 4
+        out.append(f"// {name}: per tile {n_mfma} MFMA, {n_valu} exp/pack VALU, {n_ds} LDS fragment reads, "
+                   f"{n_all} instructions (incl. the rare-path mask / switch blocks); {len(lines)} asm lines")
+        out.append(f"#define {name} \\")
+        out.append(" \\\n".join("  \"" + l + "\\n\\t\"" for l in lines))
+        print(f"{name}: per tile {n_mfma} MFMA / {n_valu} VALU / {n_ds} ds reads / {n_all} instructions, "
+              f"{len(lines)} asm lines")
     clob = ", ".join([f'"v{r}"' for r in NAMED_V] + [f'"a{r}"' for r in NAMED_A])
-    n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
-    n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_cvt"))) // 4
-    n_ds = sum(1 for l in loop if l.startswith("ds_")) // 4
-    n_all = sum(1 for l in loop if not l.startswith(";")) // 4
+    out.append("#define SR_ATTN_PIPE_CLOBBERS " + clob)
     with open(OUT, "w") as f:
-        f.write("// GENERATED by tools/gen_attn_pipe.py — do not edit by hand.\n")
-        f.write(f"// per tile: {n_mfma} MFMA, {n_valu} exp/pack VALU, {n_ds} LDS fragment reads, {n_all} instructions;\n")
-        f.write(f"// {len(lines)} asm lines in all\n")
-        f.write("#define SR_ATTN_PIPE_ASM \\\n")
-        f.write(text + "\n")
-        f.write("#define SR_ATTN_PIPE_CLOBBERS " + clob + "\n")
-    print(f"wrote {OUT}: per tile {n_mfma} MFMA / {n_valu} VALU / {n_ds} ds reads / {n_all} instructions, "
-          f"{len(lines)} asm lines")
+        f.write("\n".join(out) + "\n")
 
 
 if __name__ == "__main__":

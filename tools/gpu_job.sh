@@ -41,6 +41,10 @@ for step in "$@"; do
     bench_c5q) run bench_c5q 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline --fp8-global qkv ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
     kgemm)   run kgemm 300 python tools/kbench.py gemm ln ;;
+    kgemm_sk) for i in 1 2; do
+                run kgemm_sk0_$i 300 env SR_GEMM_SK=0 python tools/kbench.py gemm gemm_rank || exit 1
+                run kgemm_sk1_$i 300 env SR_GEMM_SK=1 python tools/kbench.py gemm gemm_rank || exit 1
+              done ;;
     kgemm_reg) run kgemm_reg 300 env SR_GEMM_REG_EPI=1 python tools/kbench.py gemm ;;
     kdpt)    run kdpt 600 python tools/kbench.py dpt ;;
     kreloc)  run kreloc 600 python tools/kbench.py reloc ;;
@@ -68,6 +72,10 @@ for step in "$@"; do
     dbg_var) for v in $PIPE_VARIANTS; do
                run dbg_$v 300 env SFM_AMD_LIB=variants/libsfm_$v.so SR_ATTN_PIPE=1 python tools/dbg_attn_pipe.py 8192 8256 16384 16448 43968 || exit 1
              done ;;
+    kattn_seg) for i in 1 2; do
+                 run kattn_seg0_$i 300 env SR_ATTN_PIPE_SEG=0 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
+                 run kattn_seg1_$i 300 env SR_ATTN_PIPE_SEG=1 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
+               done ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \

@@ -45,28 +45,34 @@ def attn():
     # SR_KB_STATIC=1: pass the keys' true max norm as the static bound (runtime.key_norm_bound's
     # role for qk-norm blocks) instead of the key scan
     static = os.environ.get("SR_KB_STATIC", "0") == "1"
+    # SR_KB_TAIL=1 (default): buffers with 64 readable rows after them, as the aggregator's
+    # workspace (ops.attention tail_readable: ragged / two-segment launches may take the asm sweep)
+    tail = os.environ.get("SR_KB_TAIL", "1") == "1"
+    pad = 64 if tail else 0
     for name, c in cases.items():
-        qkv = torch.randn(c["rows"], 3 * C, device=DEV, dtype=torch.bfloat16)
+        qkv = torch.randn(c["rows"] + pad, 3 * C, device=DEV, dtype=torch.bfloat16)[:c["rows"]]
         o = torch.empty(c["rows"], C, device=DEV, dtype=torch.bfloat16)
         kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max()) if static else 0.0
 
         def f():
             ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=c["batch"],
-                          lq=c["lq"], q_bstride=c["lq"], l0=c["l0"], k0_bstride=c["kb"], key_norm_max=kb)
+                          lq=c["lq"], q_bstride=c["lq"], l0=c["l0"], k0_bstride=c["kb"], key_norm_max=kb,
+                          tail_readable=tail)
         ms = timeit(f, reps=5 if c["batch"] == 1 else 10)
         fl = 4.0 * c["batch"] * H * c["lq"] * c["l0"] * D
         print(f"attn {name:18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
     # reloc: 32 query frames x (32*305 subsample + own 1374)
     nsub = N * 305
-    qkv = torch.randn(N * P, 3 * C, device=DEV, dtype=torch.bfloat16)
-    kv = torch.randn(nsub, 2 * C, device=DEV, dtype=torch.bfloat16)
+    qkv = torch.randn(N * P + pad, 3 * C, device=DEV, dtype=torch.bfloat16)[:N * P]
+    kv = torch.randn(nsub + pad, 2 * C, device=DEV, dtype=torch.bfloat16)[:nsub]
     o = torch.empty(N * P, C, device=DEV, dtype=torch.bfloat16)
     kb = max(float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max()),
              float(kv[:, :C].float().view(-1, H, D).norm(dim=-1).max())) if static else 0.0
 
     def f():
         ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], o, heads=H, head_dim=D, batch=N, lq=P, q_bstride=P, l0=nsub,
-                      k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P, key_norm_max=kb)
+                      k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P, k1_bstride=P, key_norm_max=kb,
+                      tail_readable=tail)
     ms = timeit(f)
     fl = 4.0 * N * H * P * (nsub + P) * D
     print(f"attn {'reloc 32x(9760+1374)':18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
