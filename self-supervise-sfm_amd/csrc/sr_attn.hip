@@ -1358,7 +1358,8 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     // two of its four SIMDs idle for the whole sweep (a second workgroup fills them in the compiled
     // kernel), and a frame's 22-tile sweep does not hide the workgroup's prologue / epilogue
     // (kbench: reloc 1.835-1.846 vs 1.828-1.852 ms, frame 0.609-0.611 vs 0.559-0.576 ms)
-    static const bool pipe_seg = [] {
+    // (read per launch: the tests switch it on for their asm-seg cases)
+    const bool pipe_seg = [] {
       const char* e = getenv("SR_ATTN_PIPE_SEG");
       return e ? atoi(e) != 0 : false;
     }();

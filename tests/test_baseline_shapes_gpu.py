@@ -324,7 +324,7 @@ def _padded(t, rows=64):
 @pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
 @pytest.mark.parametrize("nq,nsub", [(8, 8 * PP), (32, 32 * PP), (4, 32 * PP), (8, 32 * PP)],
                          ids=["C2", "C3", "C3-8rk", "C3-4rk"])
-def test_reloc_attention_production(ops, nq, nsub, tail):
+def test_reloc_attention_production(ops, nq, nsub, tail, monkeypatch):
     """global_reloc (aggregator.py:672-741): every query frame attends to the shared anchor
     subsample (segment 0, batch stride 0) and to its own frame (segment 1); C3-8rk / C3-4rk are
     the per-rank shapes of the frame-sharded C3 forward (4 / 8 query frames).  asm-seg: readable
@@ -334,6 +334,7 @@ def test_reloc_attention_production(ops, nq, nsub, tail):
     ks, _, vs = _make(nsub, 4, spikes=(nsub - 3,))
     if tail:
         k, v, ks, vs = _padded(k), _padded(v), _padded(ks), _padded(vs)
+        monkeypatch.setenv("SR_ATTN_PIPE_SEG", "1")  # the opt-in variant (read per launch)
     o = torch.empty(nq * P, C, device=DEV, dtype=torch.bfloat16)
     ops.attention(q, ks, vs, o, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
                   k1=k, v1=v, l1=P, k1_bstride=P, tail_readable=tail)
@@ -349,13 +350,14 @@ def test_reloc_attention_production(ops, nq, nsub, tail):
 
 
 @pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
-def test_frame_attention_production(ops, tail):
+def test_frame_attention_production(ops, tail, monkeypatch):
     """frame / DINO stacks at C3: 64 frames x 1374 tokens, keys = own frame (asm-seg: the ragged
     last key tile staged whole from readable rows and masked in the hand-scheduled sweep)."""
     S = 64
     q, k, v = _make(S * P, 5, spikes=(S * P - 2,))
     if tail:
         k, v = _padded(k), _padded(v)
+        monkeypatch.setenv("SR_ATTN_PIPE_SEG", "1")
     o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
     ops.attention(q, k, v, o, heads=H, head_dim=D, batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P,
                   tail_readable=tail)

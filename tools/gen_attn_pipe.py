@@ -57,6 +57,10 @@ Y_DMA = float(os.environ.get("SR_PIPE_Y_DMA", "0.8"))
 # XDL write -> VALU read of the same VGPR needs 11 wait states (8-pass 32x32x16): X's first exp2
 # reads the scores Y's last MFMA chain wrote ~10 instructions earlier, so pad
 X_LEAD_NOP = int(os.environ.get("SR_PIPE_X_LEAD_NOP", "2"))
+#   SR_PIPE_K1_IN_Y=1: K(t+1)'s kb1 fragments read at the head of Y (its chain is Y's last) instead of in X
+#   SR_PIPE_DMA_SPLIT=k: the first k DMA pieces in X, the rest in Y
+K1_IN_Y = os.environ.get("SR_PIPE_K1_IN_Y", "0") == "1"
+DMA_SPLIT = int(os.environ.get("SR_PIPE_DMA_SPLIT", "0"))
 # SR_ATTN_PIPE_ASM_SEG (generated with SEG = True): two key segments (the DMA source switches to
 # segment 1's base, offsets and tile stride when tile nt0 is staged: %[nsw] = nt0 - 3) and ragged
 # segment tails (scores of keys past a segment's end -> -inf before their exp2: tiles %[trag0] /
@@ -153,9 +157,9 @@ class Phase:
                 self.valu.append((COST["cvt"], [f"v_cvt_pk_bf16_f32 {vr(dst + jj)}, {vr(src + 2 * jj)}, "
                                                 f"{vr(src + 2 * jj + 1)}"]))
 
-    def read_k(self, p, slot, seqs):
+    def read_k(self, p, slot, seqs, kbs=(0, 1)):
         """K fragments of the tile in ring slot `slot` into Kset[p] (8 ds_read_b128)."""
-        for kb in range(2):
+        for kb in kbs:
             for s in range(4):
                 lines = [("ds", f"ds_read_b128 {ar(kfrag(p, kb, s), 4)}, %[ka{s}] "
                                 f"offset:{slot * STAGE_B + kb * 4096}", seqs, (p, kb, s))]
@@ -171,11 +175,11 @@ class Phase:
                          ("ds", f"ds_read_b64_tr_b16 {ar(f + 2, 2)}, %[va{db}] offset:{off + 1024}", seqs, (p, i, db))]
                 self.other.append((2 * COST["read"], lines, "read"))
 
-    def dma(self, slot):
+    def dma(self, slot, pieces=range(4)):
         """LDS-DMA of tile t+3 (4 pieces of 8 rows per wave) into ring slot `slot`; the per-lane
         source offsets then step one tile."""
         step = "%[sstc]" if SEG else "%[sstep]"
-        for i in range(4):
+        for i in pieces:
             lines = []
             if SEG and i == 0:
                 sk = _label("sw")
@@ -303,8 +307,10 @@ def body(t4, fill=False, drain=False, stage=True, vm=4):
     p.exp(0)
     if stage and DMA_IN_X:
         p.dma(s_stage)
+    elif stage and DMA_SPLIT:
+        p.dma(s_stage, range(DMA_SPLIT))
     if not drain:
-        p.read_k(q, s_next, kseqs)
+        p.read_k(q, s_next, kseqs, (0,) if K1_IN_Y else (0, 1))
     if DMA_IN_X:
         p.emit(kseqs, vseqs, valu_lead=2 if fill else 1, lead_nop=15 if fill else 0, other_frac=0.5)
     else:
@@ -320,10 +326,12 @@ def body(t4, fill=False, drain=False, stage=True, vm=4):
     if not drain:
         p.qk(0, 1, q)
     p.exp(1)
+    if K1_IN_Y and not drain:
+        p.read_k(q, s_next, kseqs, (1,))
     if DMA_IN_X:
         p.read_v(par, s_cur, vseqs)
     elif stage:
-        p.dma(s_stage)
+        p.dma(s_stage, range(DMA_SPLIT, 4))
     # EXP1 reads S1 from X's last chain: two MFMAs and a pad first
     p.emit(kseqs, vseqs, valu_lead=2, lead_nop=7, other_frac=0.2 if DMA_IN_X else Y_DMA)
     if drain:
