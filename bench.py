@@ -129,7 +129,7 @@ def kernel_of_tag(tag: str, views: int, img: int):
 
 
 TRAFFIC_FILES = [os.path.join(REPO, "profiles", f) for f in
-                 ("r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
+                 ("r03_pmc_traffic.json", "r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
 
 
 def pmc_traffic(kernel: str, views: int, img: int, fp8: str = "off"):
