@@ -818,6 +818,142 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, g.sk_wgs > 0 ? g.sk_dp : nt), 0, g.ktiles, false);
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x128 bf16 GEMM, TWO workgroups per CU ("pair"): the same 128x64 wave tile as gemm256_kernel
+// (acc[8][4], the same register epilogues), but 4 waves (2 M x 2 N) per workgroup and a 72 KiB
+// LDS ring (3 stages of 32-deep k-tiles, 64-B rows: A 256 rows | W 128 rows), so two workgroups
+// share a CU and one's epilogue (the stores and the residual read-modify-write) runs beside the
+// other's MFMAs -- the per-CU epilogue serialisation that caps the 256x256 kernel (DESIGN.md GEMM).
+//   * LDS rows of 64 B = 4 16-B chunks; chunk c of row r sits at c ^ ((r >> 2) & 3): a b128 read
+//     of 16 rows x 1 chunk touches 64 distinct banks; the LDS-DMA pieces (16 rows x 64 B) fetch
+//     the source chunk (l & 3) ^ ((l >> 4) & 3) for lane l, the same for every piece;
+//   * per k-tile each wave stages 4 A pieces (rows 64w..) and 2 W pieces (rows 32w..); tile kt+2
+//     goes out right after the barrier of tile kt (3-stage ring), the wait is vmcnt(6);
+//   * 32 MFMAs (16x16x32) per wave per k-tile in 4 quadrant phases, fragments of the next
+//     quadrant read before the current one's cluster.
+constexpr int PBM = 256, PBN = 128, PKT = 32, PROWB = 64;
+constexpr int PSTAGE = (PBM + PBN) * PROWB;  // 24 KiB
+constexpr int PNBUF = 3;
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_pair_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[PNBUF * PSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = g.N / PBN, ntm = (g.M + PBM - 1) / PBM;
+  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
+  int tm, tn;
+  if (g.group_m > 1) {
+    const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
+    const int gm = min(g.group_m, ntm - first), r = tile - grp * per;
+    tm = first + r % gm;
+    tn = r / gm;
+  } else {
+    tm = tile / ntn;
+    tn = tile - tm * ntn;
+  }
+  const int m0 = tm * PBM, n0 = tn * PBN;
+  const int ktiles = g.K / PKT;
+
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int csrc = (lane & 3) ^ ((lane >> 4) & 3);
+  const uint32_t voA = (uint32_t)((lane >> 2) * g.lda_b + csrc * 16);
+  const uint32_t voW = (uint32_t)((lane >> 2) * g.ldw_b + csrc * 16);
+  const int arow0 = m0 + wave_u * 64;  // this wave's first staged A row
+  const bool ragged = m0 + PBM > g.M;
+  const char* const sA = g.A + (int64_t)min(arow0, g.M - 1) * g.lda_b;
+  const char* const sW = g.W + (int64_t)(n0 + wave_u * 32) * g.ldw_b;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem));
+  const uint32_t dA = lds0 + wave_u * 64 * PROWB, dW = lds0 + (PBM + wave_u * 32) * PROWB;
+  auto stage = [&](int kt) {
+    const uint32_t sb = (uint32_t)((kt % PNBUF) * PSTAGE);
+    const int64_t ko = (int64_t)kt * PKT * 2;
+    if (!ragged) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sr::dma16_s(sA + ko + (int64_t)j * 16 * g.lda_b, voA, dA + sb + j * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = min(arow0 + 16 * j + (lane >> 2), g.M - 1);
+        sr::dma16(g.A + (int64_t)r * g.lda_b + ko + csrc * 16, dA + sb + j * 1024);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) sr::dma16_s(sW + ko + (int64_t)j * 16 * g.ldw_b, voW, dW + sb + j * 1024);
+  };
+
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int coff = ((lg ^ ((lr >> 2) & 3)) << 4);
+  const int arow = (wr * 128 + lr) * PROWB + coff;        // + (qm*64 + mi*16) * PROWB
+  const int brow = (PBM + wc * 64 + lr) * PROWB + coff;   // + (qn*32 + ni*16) * PROWB
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  if (ktiles > 1) stage(1);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    if (kt + 1 < ktiles) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile kt landed, kt+1 in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sr::barrier_raw();  // every wave's pieces of tile kt; everyone done with tile kt-1's stage
+    if (kt + 2 < ktiles) stage(kt + 2);
+    const char* sb = smem + (kt % PNBUF) * PSTAGE;
+    uint4 aX[4], aY[4], bX[2], bY[2];
+    auto load_a = [&](uint4 (&a)[4], int qm) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + arow + (qm * 64 + mi * 16) * PROWB);
+    };
+    auto load_b = [&](uint4 (&b)[2], int qn) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b[ni] = *(const uint4*)(sb + brow + (qn * 32 + ni * 16) * PROWB);
+    };
+    auto mma = [&](const uint4 (&a)[4], const uint4 (&b)[2], int qm, int qn) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni], a[mi], acc[qm * 4 + mi][qn * 2 + ni]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    load_a(aX, 0);
+    load_b(bX, 0);
+    load_b(bY, 1);
+    mma(aX, bX, 0, 0);
+    load_a(aY, 1);
+    mma(aX, bY, 0, 1);
+    mma(aY, bY, 1, 1);
+    mma(aY, bX, 1, 0);
+  }
+  if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    if (m0 + PBM <= g.M) {
+      resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+      return;
+    }
+  }
+  if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
+    if (m0 + PBM <= g.M && !g.ep.aux) {
+      bias_full<EPI>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+      return;
+    }
+  }
+  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+}
+
+template <int EPI>
+int launch_pair(GemmArgs a, hipStream_t s) {
+  const int nwg = (a.N / PBN) * ((a.M + PBM - 1) / PBM);
+  static const int group_m = [] {
+    const char* e = getenv("SR_GEMM_GROUP_M");
+    return e ? atoi(e) : -1;
+  }();
+  a.group_m = group_m >= 0 ? group_m : (a.N >= 3072 ? 4 : 0);
+  hipLaunchKernelGGL((gemm_pair_kernel<EPI>), dim3(nwg), dim3(256), 0, s, a);
+  return sr::check_launch("sr_gemm(pair)");
+}
+
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
@@ -879,6 +1015,21 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
     // 256x256 tiles (one WG per CU) only when they still give >= 2 WGs per CU; smaller
     // problems (frame-sharded ranks, small scenes) keep 4x more 128x128 workgroups.
     const long tiles256 = (long)(a.N / BIG) * ((a.M + BIG - 1) / BIG);
+    // 256x128 tiles, two workgroups per CU (SR_GEMM_PAIR=1; A/B against the 256x256 kernel)
+    static const bool pair = [] {
+      const char* e = getenv("SR_GEMM_PAIR");
+      return e ? atoi(e) != 0 : false;
+    }();
+    if (pair && !no_big && a.N % BIG == 0 && a.K % PKT == 0 && tiles256 >= 512 && epi != SR_EPI_PATCH &&
+        epi != SR_EPI_GELU_BWD) {
+      switch (epi) {
+        case SR_EPI_BIAS: return launch_pair<SR_EPI_BIAS>(a, s);
+        case SR_EPI_BIAS_GELU: return launch_pair<SR_EPI_BIAS_GELU>(a, s);
+        case SR_EPI_BIAS_RESID: return launch_pair<SR_EPI_BIAS_RESID>(a, s);
+        case SR_EPI_QKV: return launch_pair<SR_EPI_QKV>(a, s);
+        case SR_EPI_F32: return launch_pair<SR_EPI_F32>(a, s);
+      }
+    }
     if (!no_big && a.N % BIG == 0 && tiles256 >= 512) {
       switch (epi) {
         case SR_EPI_BIAS: return launch256<SR_EPI_BIAS>(a, s);

@@ -29,6 +29,9 @@ for step in "$@"; do
     attn_tests) run attn_tests 300 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k attention ;;
     attn_tests1) run attn_tests1 300 env SR_ATTN_CFG=1 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k attention ;;
     kattn_cfg1) run kattn_cfg1 300 env SR_ATTN_CFG=1 python tools/kbench.py attn ;;
+    kattn_cfgs) for i in 1 2; do
+                  for c in 0 1 2; do run kattn_cfg${c}_$i 300 env SR_ATTN_CFG=$c SR_KB_STATIC=1 python tools/kbench.py attn || exit 1; done
+                done ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py ;;
     benchq)  run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
@@ -41,6 +44,15 @@ for step in "$@"; do
     bench_c5q) run bench_c5q 600 python bench.py --views 128 --steps 2 --warmup 1 --no-cpu-baseline --fp8-global qkv ;;
     kbench)  run kbench 300 python tools/kbench.py ;;
     kgemm)   run kgemm 300 python tools/kbench.py gemm ln ;;
+    kgemm_128) for i in 1 2; do
+                run kgemm_256_$i 300 python tools/kbench.py gemm || exit 1
+                run kgemm_128_$i 300 env SR_GEMM_NO256=1 python tools/kbench.py gemm || exit 1
+              done ;;
+    gemm_pair_tests) run gemm_pair_tests 600 env SR_GEMM_PAIR=1 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm" --timeout 300 --timeout-method thread ;;
+    kgemm_pair) for i in 1 2; do
+                run kgemm_p0_$i 300 env SR_GEMM_PAIR=0 python tools/kbench.py gemm gemm_rank || exit 1
+                run kgemm_p1_$i 300 env SR_GEMM_PAIR=1 python tools/kbench.py gemm gemm_rank || exit 1
+              done ;;
     kgemm_sk) for i in 1 2; do
                 run kgemm_sk0_$i 300 env SR_GEMM_SK=0 python tools/kbench.py gemm gemm_rank || exit 1
                 run kgemm_sk1_$i 300 env SR_GEMM_SK=1 python tools/kbench.py gemm gemm_rank || exit 1
