@@ -513,10 +513,28 @@ class Aggregator(nn.Module):
         if Nq_l > 0:
             def attend_reloc(qkv, o):
                 _wait(work_sub)
+                rows = Nq_l * P
+                kb = runtime.key_norm_bound(pr)
+                if self._split_reloc(dtype, rows, n_sub_all):
+                    # two passes + LSE merge (the union of the two key sets, exactly): every query row
+                    # against the shared anchor subsample as ONE long query set (the hand-scheduled
+                    # sweep, sr_attn.hip), then each query frame against itself (the compiled sweep)
+                    o_parts, lse_parts = ops.key_split_workspace(dev, 2, rows, C, pr.heads, name="reloc_split")
+                    ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o_parts[:rows],
+                                  heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows, q_bstride=0,
+                                  l0=n_sub_all, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
+                                  lse=lse_parts[0].view(-1), tail_readable=True)
+                    ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o_parts[rows:],
+                                  heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=P,
+                                  k0_bstride=P, tag="attn_reloc", key_norm_max=kb, lse=lse_parts[1].view(-1),
+                                  tail_readable=True)
+                    ops.attn_merge_n(o_parts, lse_parts, o, parts=2, rows=rows, heads=pr.heads,
+                                     head_dim=pr.head_dim, seg_rows=[rows, P])
+                    return
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
                               k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                              key_norm_max=runtime.key_norm_bound(pr), tail_readable=True)
+                              key_norm_max=kb, tail_readable=True)
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
                 with torch.cuda.stream(side):
@@ -599,6 +617,16 @@ class Aggregator(nn.Module):
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
                           k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg))
+
+    @staticmethod
+    def _split_reloc(dtype, rows: int, n_sub: int) -> bool:
+        """Opt-in (SR_RELOC_SPLIT=1, bf16, a query set that fills the chip without key splitting):
+        the reloc attention as two passes + LSE merge, the shared-subsample pass over all query
+        rows on the hand-scheduled sweep.  Correct (C3 parity under it) but not faster end to end:
+        the attention classes 42.7-42.9 vs 43.0 ms per C3 step, the whole step 413 vs 409.5 ms (the
+        merge pass and the second launch cost more than the sweep saves)."""
+        return (os.environ.get("SR_RELOC_SPLIT") == "1" and dtype == torch.bfloat16 and
+                (rows + 255) // 256 * 16 >= 2048 and n_sub >= 64)
 
     def _side_stream(self, dev):
         """Second HIP stream for the concurrent reloc block (opt-in: SR_CONCURRENT_STACKS=1)."""

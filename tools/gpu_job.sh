@@ -53,6 +53,11 @@ for step in "$@"; do
                 run kgemm_p0_$i 300 env SR_GEMM_PAIR=0 python tools/kbench.py gemm gemm_rank || exit 1
                 run kgemm_p1_$i 300 env SR_GEMM_PAIR=1 python tools/kbench.py gemm gemm_rank || exit 1
               done ;;
+    reloc_split_ab) for i in 1 2; do
+                run bench_rs0_$i 400 env SR_RELOC_SPLIT=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
+                run bench_rs1_$i 400 env SR_RELOC_SPLIT=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
+              done ;;
+    parity_c3) run parity_c3 900 python -u -m pytest tests/test_parity_gpu.py -x -v -m gpu -k "c3 or c2" --timeout 600 --timeout-method thread ;;
     kgemm_sk) for i in 1 2; do
                 run kgemm_sk0_$i 300 env SR_GEMM_SK=0 python tools/kbench.py gemm gemm_rank || exit 1
                 run kgemm_sk1_$i 300 env SR_GEMM_SK=1 python tools/kbench.py gemm gemm_rank || exit 1
