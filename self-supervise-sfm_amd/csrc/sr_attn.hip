@@ -156,15 +156,14 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
         sr::dma16_s(sp + i * s8, (gi & 1) ? svb : sva, ldsb + (gi & 7) * 1024);
       }
     } else {
-      const char* base = s1 ? sb1 : sb0;
+      // (sp points at row tt*KT + grow0 of the segment: rows are addressed relative to it)
       const int64_t ld = s1 ? sld1 : sld0;
-      const int64_t rbase = s1 ? srb1 : srb0;
 #pragma unroll
       for (int i = 0; i < DPW; ++i) {
         const int gi = wave_u * DPW + i;
         const int r = (gi & 7) * 8 + lrow;  // key row inside the tile
-        const int key = min(tt * KT + r, len - 1);
-        sr::dma16(base + ((rbase + key) * ld + ((gi & 1) ? chB : chA) * 8) * 2, ldsb + (gi & 7) * 1024);
+        const int rel = min(r, len - 1 - tt * KT) - grow0;
+        sr::dma16(sp + (rel * ld + ((gi & 1) ? chB : chA) * 8) * 2, ldsb + (gi & 7) * 1024);
       }
     }
     sp += sstep;
@@ -225,6 +224,14 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
     }
   }
   bool fixed_m = false, m_zero = false;
+  if (use_bound && args.allow_mzero) {
+    // every row's bound qb <= 50: the fixed offset m = 0 holds from tile 0 (what the tile-0 max
+    // pass would settle on), so the sweep skips that pass and the -m fold MFMAs from the start
+    bool z = true;
+#pragma unroll
+    for (int b = 0; b < QB; ++b) z &= qb[b] <= 50.f;
+    fixed_m = m_zero = __all(z);
+  }
 
   // Running row max m (exp2 domain) enters the MFMA chain as one extra k-step:
   //   S'[key][q] = sum_k K[key][k] (cQ)[q][k] + 1 * (-m_hi[q]) + 1 * (-m_lo[q])

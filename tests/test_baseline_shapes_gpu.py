@@ -367,3 +367,32 @@ def test_frame_attention_production(ops, tail, monkeypatch):
         rows = _sample_rows(P, 64, j).to(DEV)
         ref = _ref_rows(q[fr][rows], k[fr], v[fr], scale)
         assert _rel(o[fr][rows].float(), ref) < 1e-2, j
+
+
+@pytest.mark.parametrize("S,L,static", [(16, P, True), (16, P, False), (40, 300, True), (5, P, False),
+                                        (24, 777, True)],
+                         ids=["16x1374", "16x1374-keyscan", "40x300", "5x1374-keyscan", "24x777"])
+def test_frame_attention_shapes_lse(ops, S, L, static):
+    """Frame launches of other sizes: ragged q- and key tiles, the static key bound and the
+    per-frame key scan (DINO), a spike key forcing the running-max path in two frames, O and the
+    log2-domain LSE the training backward reads, against fp64 on every frame's sampled rows
+    (LSE: 3e-3 relative + 1e-2, the bf16 rounding of c*q)."""
+    q, k, v = _make(S * L, 7 + S, spikes=(S * L - 5, L // 2))
+    kn = 1.01 * float(k.float().view(-1, H, D).norm(dim=-1).max()) if static else 0.0
+    o = torch.empty(S * L, C, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(S, H, L, device=DEV, dtype=torch.float32)
+    ops.attention(q, k, v, o, heads=H, head_dim=D, batch=S, lq=L, q_bstride=L, l0=L, k0_bstride=L,
+                  key_norm_max=kn, lse=lse)
+    scale = D ** -0.5
+    for j in range(S):
+        fr = slice(j * L, (j + 1) * L)
+        rows = _sample_rows(L, 24, j).to(DEV)
+        ref = _ref_rows(q[fr][rows], k[fr], v[fr], scale)
+        assert _rel(o[fr][rows].float(), ref) < 1e-2, j
+        for h in (0, H - 1):
+            c = slice(h * D, (h + 1) * D)
+            sc = (q[fr][rows][:, c].double() @ k[fr][:, c].double().T) * scale
+            ref_lse = torch.logsumexp(sc, -1) / math.log(2.0)
+            # c*q enters the MFMAs rounded to bf16: scores (and so the LSE) carry ~2^-9 relative error
+            err = (lse[j, h, rows].double() - ref_lse).abs() - 3e-3 * ref_lse.abs()
+            assert float(err.max()) < 1e-2, (j, h)

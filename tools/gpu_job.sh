@@ -93,6 +93,8 @@ for step in "$@"; do
                  run kattn_seg0_$i 300 env SR_ATTN_PIPE_SEG=0 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
                  run kattn_seg1_$i 300 env SR_ATTN_PIPE_SEG=1 SR_KB_STATIC=1 python tools/kbench.py attn || exit 1
                done ;;
+    kfdiag)  run kfdiag0 300 python tools/kbench.py attn_frame_diag && \
+             run kfdiag1 300 env SR_ATTN_PIPE_SEG=1 python tools/kbench.py attn_frame_diag ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \

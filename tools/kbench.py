@@ -78,6 +78,28 @@ def attn():
     print(f"attn {'reloc 32x(9760+1374)':18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
 
 
+def attn_frame_diag():
+    """Where the frame attention loses against the long sweep: the same launch with no ragged
+    q-tile (lq = 1280 = 5 x 256), with full key tiles (l0 = 1408), and with 4x longer key sweeps
+    (l0 = 5496, the neighbouring frames' keys), 16 heads, static key bound."""
+    C, H, D, P = 1024, 16, 64, 1374
+    B = 64
+    qkv = torch.randn(B * P + 8 * P, 3 * C, device=DEV, dtype=torch.bfloat16)
+    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
+    kb = 1.01 * float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())
+    warm = torch.randn(8192, 8192, device=DEV, dtype=torch.bfloat16)
+    for _ in range(20):  # clocks up before the first timed case
+        warm @ warm
+    for lq, l0, b in ((P, P, B), (1280, P, B), (P, 1408, B), (1280, 1408, B), (1280, 4 * P, B),
+                      (P, 4 * P, B), (1024, P, B), (768, P, B), (512, P, B), (256, P, B)):
+        def f():
+            ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=b, lq=lq,
+                          q_bstride=P, l0=l0, k0_bstride=P, key_norm_max=kb, tail_readable=True)
+        ms = timeit(f)
+        fl = 4.0 * b * H * lq * l0 * D
+        print(f"attn frame-diag b={b} lq={lq:5d} l0={l0:5d} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s", flush=True)
+
+
 def attn_rank():
     """Per-rank global attention of the frame-sharded C3 forward: 32/G anchors' queries against
     all 43,968 anchor keys (one pass), G = 2, 4, 8."""
