@@ -1293,6 +1293,51 @@ __global__ __launch_bounds__(256) void attn_merge_n_kernel(const T* __restrict__
   }
 }
 
+// bf16, 8 columns (16 B) per thread, 32-bit index math (the split reloc / key-split merges run
+// at the HBM rate: the generic form's 64-bit divisions and 2-byte loads held it near 1.8 TB/s)
+__global__ __launch_bounds__(256) void attn_merge_n_bf16_kernel(const bf16* __restrict__ op, int64_t ld,
+                                                                int64_t pstride, const float* __restrict__ lse,
+                                                                MergeSegRows segrows, int parts, bf16* out,
+                                                                int64_t ldo, float* __restrict__ lout, int rows,
+                                                                int heads, int head_dim) {
+  const int chunks = head_dim >> 3, per_row = heads * chunks;
+  const int total = rows * per_row, lstride = heads * rows;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int r = e / per_row, rem = e - r * per_row;
+    const int h = rem / chunks, c = rem - h * chunks;
+    float lp[SR_ATTN_MERGE_MAX_PARTS];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < SR_ATTN_MERGE_MAX_PARTS; ++p) {
+      if (p < parts) {
+        const int sg = segrows.n[p], q = r / sg;
+        lp[p] = lse[p * lstride + (q * heads + h) * sg + (r - q * sg)];
+        mx = fmaxf(mx, lp[p]);
+      }
+    }
+    const int col = h * head_dim + 8 * c;
+    float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sum = 0.f;
+    if (mx != -INFINITY) {
+#pragma unroll
+      for (int p = 0; p < SR_ATTN_MERGE_MAX_PARTS; ++p) {
+        if (p < parts) {
+          const float w = exp2f(lp[p] - mx);
+          sum += w;
+          const bf16x8 v = *(const bf16x8*)(op + p * pstride + (int64_t)r * ld + col);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] = fmaf(w, (float)v[j], y[j]);
+        }
+      }
+    }
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)(y[j] * inv);
+    *(bf16x8*)(out + (int64_t)r * ldo + col) = o;
+    if (lout && c == 0) lout[h * rows + r] = mx == -INFINITY ? mx : mx + log2f(sum);
+  }
+}
+
 }  // namespace
 
 extern "C" int sr_attention_bound_floats(const sr_attn_desc* desc) {
@@ -1428,7 +1473,14 @@ extern "C" int sr_attn_merge_n(sr_stream_t stream, int dtype, int parts, int row
   const int64_t total = (int64_t)rows * heads * (head_dim / 4);
   const dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 65536));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == SR_BF16)
+  const bool fast = dtype == SR_BF16 && head_dim % 8 == 0 && ld % 8 == 0 && ldo % 8 == 0 && (part_rows * ld) % 8 == 0 &&
+                    (((uintptr_t)o_parts | (uintptr_t)out) & 15) == 0 && (int64_t)rows * heads * head_dim < (1LL << 31);
+  if (fast) {
+    const int64_t t8 = (int64_t)rows * heads * (head_dim / 8);
+    hipLaunchKernelGGL(attn_merge_n_bf16_kernel, dim3((unsigned)std::min<int64_t>((t8 + 255) / 256, 65536)), dim3(256), 0, s,
+                       (const bf16*)o_parts, ld, part_rows * ld, lse_parts, sg, parts, (bf16*)out, ldo, lse_out, rows,
+                       heads, head_dim);
+  } else if (dtype == SR_BF16)
     hipLaunchKernelGGL(attn_merge_n_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)o_parts, ld, part_rows * ld,
                        lse_parts, sg, parts, (bf16*)out, ldo, lse_out, rows, heads, head_dim);
   else {

@@ -517,17 +517,27 @@ class Aggregator(nn.Module):
                 kb = runtime.key_norm_bound(pr)
                 if self._split_reloc(dtype, rows, n_sub_all):
                     # two passes + LSE merge (the union of the two key sets, exactly): every query row
-                    # against the shared anchor subsample as ONE long query set (the hand-scheduled
-                    # sweep, sr_attn.hip), then each query frame against itself (the compiled sweep)
+                    # against the shared anchor subsample's whole 64-key tiles as ONE long query set
+                    # (the hand-scheduled sweep, sr_attn.hip), then each query frame against the
+                    # subsample's last partial tile (shared segment 0) and itself (segment 1) on the
+                    # compiled sweep
+                    n_full = n_sub_all // 64 * 64
                     o_parts, lse_parts = ops.key_split_workspace(dev, 2, rows, C, pr.heads, name="reloc_split")
-                    ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o_parts[:rows],
-                                  heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows, q_bstride=0,
-                                  l0=n_sub_all, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
+                    ops.attention(qkv[:, 0:C], kv_sub_all[:n_full, 0:C], kv_sub_all[:n_full, C:2 * C],
+                                  o_parts[:rows], heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows,
+                                  q_bstride=0, l0=n_full, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
                                   lse=lse_parts[0].view(-1), tail_readable=True)
-                    ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o_parts[rows:],
-                                  heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=P,
-                                  k0_bstride=P, tag="attn_reloc", key_norm_max=kb, lse=lse_parts[1].view(-1),
-                                  tail_readable=True)
+                    if n_full < n_sub_all:
+                        ops.attention(qkv[:, 0:C], kv_sub_all[n_full:, 0:C], kv_sub_all[n_full:, C:2 * C],
+                                      o_parts[rows:], heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P,
+                                      q_bstride=P, l0=n_sub_all - n_full, k0_bstride=0, k1=qkv[:, C:2 * C],
+                                      v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
+                                      key_norm_max=kb, lse=lse_parts[1].view(-1), tail_readable=True)
+                    else:
+                        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o_parts[rows:],
+                                      heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=P,
+                                      k0_bstride=P, tag="attn_reloc", key_norm_max=kb,
+                                      lse=lse_parts[1].view(-1), tail_readable=True)
                     ops.attn_merge_n(o_parts, lse_parts, o, parts=2, rows=rows, heads=pr.heads,
                                      head_dim=pr.head_dim, seg_rows=[rows, P])
                     return
@@ -621,10 +631,10 @@ class Aggregator(nn.Module):
     @staticmethod
     def _split_reloc(dtype, rows: int, n_sub: int) -> bool:
         """Opt-in (SR_RELOC_SPLIT=1, bf16, a query set that fills the chip without key splitting):
-        the reloc attention as two passes + LSE merge, the shared-subsample pass over all query
-        rows on the hand-scheduled sweep.  Correct (C3 parity under it) but not faster end to end:
-        the attention classes 42.7-42.9 vs 43.0 ms per C3 step, the whole step 413 vs 409.5 ms (the
-        merge pass and the second launch cost more than the sweep saves)."""
+        the reloc attention as two passes + LSE merge, the shared subsample's whole tiles over all
+        query rows on the hand-scheduled sweep.  Correct (C2 / C3 parity under it) but break-even
+        (kbench, one box: 1.424 + 0.285 + merge 0.074 = 1.783 ms vs 1.792 ms in one launch; whole C3
+        step 402.4 / 403.1 vs 404.2 / 402.7 ms), so the one-launch form stays the default."""
         return (os.environ.get("SR_RELOC_SPLIT") == "1" and dtype == torch.bfloat16 and
                 (rows + 255) // 256 * 16 >= 2048 and n_sub >= 64)
 

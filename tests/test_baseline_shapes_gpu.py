@@ -349,6 +349,36 @@ def test_reloc_attention_production(ops, nq, nsub, tail, monkeypatch):
         assert _rel(o[fr][rows].float(), ref) < 1e-2, j
 
 
+@pytest.mark.parametrize("nq", [8, 32], ids=["C2", "C3"])
+def test_reloc_attention_split_production(ops, nq):
+    """global_reloc as the aggregator's opt-in split (SR_RELOC_SPLIT=1): every query row against the
+    shared subsample's whole 64-key tiles as one long query set (the hand-scheduled sweep), each
+    frame against the subsample's last partial tile + itself, merged by LSE with mixed layouts in
+    the bf16 merge kernel; equal to the one-launch kernel and to fp64 on sampled rows."""
+    nsub = 32 * PP
+    q, k, v = _make(nq * P, 3, spikes=(nq * P - 11,))
+    ks, _, vs = _make(nsub, 4, spikes=(nsub - 3, 100))
+    rows, nf = nq * P, nsub // 64 * 64
+    o_parts, lse_parts = ops.key_split_workspace(DEV, 2, rows, C, H, name="test_reloc_split")
+    ops.attention(q, ks[:nf], vs[:nf], o_parts[:rows], heads=H, head_dim=D, batch=1, lq=rows, q_bstride=0, l0=nf,
+                  k0_bstride=0, lse=lse_parts[0].view(-1))
+    ops.attention(q, ks[nf:], vs[nf:], o_parts[rows:], heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P,
+                  l0=nsub - nf, k0_bstride=0, k1=k, v1=v, l1=P, k1_bstride=P, lse=lse_parts[1].view(-1))
+    o = torch.empty(rows, C, device=DEV, dtype=torch.bfloat16)
+    ops.attn_merge_n(o_parts, lse_parts, o, parts=2, rows=rows, heads=H, head_dim=D, seg_rows=[rows, P])
+    one = torch.empty_like(o)
+    ops.attention(q, ks, vs, one, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
+                  k1=k, v1=v, l1=P, k1_bstride=P)
+    torch.cuda.synchronize()
+    assert _rel(o.float(), one.float()) < 1e-2
+    scale = D ** -0.5
+    for j in sorted({0, nq // 2, nq - 1}):
+        fr = slice(j * P, (j + 1) * P)
+        rws = _sample_rows(P, 40, j).to(DEV)
+        ref = _ref_rows(q[fr][rws], torch.cat([ks, k[fr]]), torch.cat([vs, v[fr]]), scale)
+        assert _rel(o[fr][rws].float(), ref) < 1e-2, j
+
+
 @pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
 def test_frame_attention_production(ops, tail, monkeypatch):
     """frame / DINO stacks at C3: 64 frames x 1374 tokens, keys = own frame (asm-seg: the ragged

@@ -95,6 +95,7 @@ for step in "$@"; do
                done ;;
     kfdiag)  run kfdiag0 300 python tools/kbench.py attn_frame_diag && \
              run kfdiag1 300 env SR_ATTN_PIPE_SEG=1 python tools/kbench.py attn_frame_diag ;;
+    parity_split) run parity_split 900 env SR_RELOC_SPLIT=1 python -u -m pytest tests/test_parity_gpu.py -x -v -m gpu -k "c3 or c2" --timeout 600 --timeout-method thread ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \

@@ -76,6 +76,27 @@ def attn():
     ms = timeit(f)
     fl = 4.0 * N * H * P * (nsub + P) * D
     print(f"attn {'reloc 32x(9760+1374)':18s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+    # the same reloc attention split (aggregator SR_RELOC_SPLIT=1): all 43,968 query rows against the
+    # subsample's 152 whole tiles (one long query set), each frame against the last 32 subsample
+    # keys + itself, LSE merge
+    rows, nf = N * P, nsub // 64 * 64
+    o_parts, lse_parts = ops.key_split_workspace(DEV, 2, rows, C, H, name="kb_reloc_split")
+
+    def pa():
+        ops.attention(qkv[:, :C], kv[:nf, :C], kv[:nf, C:], o_parts[:rows], heads=H, head_dim=D, batch=1, lq=rows,
+                      q_bstride=0, l0=nf, k0_bstride=0, key_norm_max=kb, lse=lse_parts[0].view(-1), tail_readable=tail)
+
+    def pb():
+        ops.attention(qkv[:, :C], kv[nf:, :C], kv[nf:, C:], o_parts[rows:], heads=H, head_dim=D, batch=N, lq=P,
+                      q_bstride=P, l0=nsub - nf, k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P,
+                      k1_bstride=P, key_norm_max=kb, lse=lse_parts[1].view(-1), tail_readable=tail)
+
+    def pm():
+        ops.attn_merge_n(o_parts, lse_parts, o, parts=2, rows=rows, heads=H, head_dim=D, seg_rows=[rows, P])
+    ta, tb, tm = timeit(pa), timeit(pb), timeit(pm)
+    print(f"attn reloc split: subsample pass {ta:.3f} ms ({4.0 * H * rows * nf * D / ta / 1e9:.1f} TF/s), "
+          f"tail+own pass {tb:.3f} ms, merge {tm:.3f} ms, total {ta + tb + tm:.3f} ms  "
+          f"{fl / (ta + tb + tm) / 1e9:8.1f} TF/s")
 
 
 def attn_frame_diag():
