@@ -418,6 +418,17 @@ int sr_imc_loss(sr_stream_t stream, const sr_imc_loss_desc* desc);
 int sr_layernorm(sr_stream_t stream, int out_dtype, const float* x, int64_t ldx, const int32_t* rowmap,
                  const float* w, const float* b, float eps, void* out, int64_t ldo, int rows, int cols);
 
+/* ------------------------------------------------------------------------
+ * Residual update + LayerNorm (block.py:86-89: x = x + ls1(attn(norm1(x))) then norm2(x)):
+ *   x[r] += gamma * y[r]   (fp32 x updated in place; y in `dtype` = the compute dtype, the
+ *                           projection GEMM's SR_EPI_BIAS output; gamma NULL = 1)
+ *   out[r] = LN(x[r]) * w + b   (out in `dtype`; w/b may both be NULL)
+ * cols in {256, 512, 768, 1024, 1536, 2048}; y / out must not alias x.
+ * ---------------------------------------------------------------------- */
+int sr_residual_layernorm(sr_stream_t stream, int dtype, float* x, int64_t ldx, const void* y, int64_t ldy,
+                          const float* gamma, const float* w, const float* b, float eps, void* out, int64_t ldo,
+                          int rows, int cols);
+
 /* image normalisation (aggregator.py:267) + 14x14 patch im2col, K zero-padded
  * to kpad: out[(f*gh+py)*gw+px][c*ps*ps + ky*ps + kx]  (patch_embed.py:78) */
 int sr_im2col_normalize(sr_stream_t stream, int dtype, const float* img, int frames, int H, int W,

@@ -116,6 +116,122 @@ int layernorm_dispatch(hipStream_t s, const float* x, int64_t ldx, const int32_t
   return SR_EUNSUPPORTED;
 }
 
+// ------------------------------------------------------------------ residual + LayerNorm
+// x += gamma * y (y = the projection GEMM's bias-epilogue output, in the compute dtype as the
+// reference's autocast Linear returns it), then out = LN(x): block.py:86-89's `x + ls1(attn(..))`
+// followed by norm2, in one pass over the rows (the GEMM's fp32 residual read-modify-write
+// epilogue ran serialized behind each CU's MFMAs; here it streams at the HBM rate).  One wave per
+// row, ln_rows_per_wave rows in flight, 4-wide vectors.
+template <int NPL, int RPW, typename TY, typename TO>
+__global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64_t ldx, const TY* __restrict__ y,
+                                                                 int64_t ldy, const float* __restrict__ gamma,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ b, float eps,
+                                                                 TO* __restrict__ out, int64_t ldo, int rows) {
+  constexpr int NV = NPL / 4;
+  constexpr int COLS = NPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  float v[RPW][NPL];
+  float yv[RPW][NPL];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = min(row0 + r, rows - 1);
+    const float* xr = x + (int64_t)row * ldx;
+    const TY* yr = y + (int64_t)row * ldy;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      const float4 t = *(const float4*)(xr + col);
+      v[r][i * 4 + 0] = t.x; v[r][i * 4 + 1] = t.y; v[r][i * 4 + 2] = t.z; v[r][i * 4 + 3] = t.w;
+      if constexpr (sr::is_bf16<TY>::value) {
+        const bf16x4 u = *(const bf16x4*)(yr + col);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yv[r][i * 4 + j] = (float)u[j];
+      } else {
+        const float4 u = *(const float4*)(yr + col);
+        yv[r][i * 4 + 0] = u.x; yv[r][i * 4 + 1] = u.y; yv[r][i * 4 + 2] = u.z; yv[r][i * 4 + 3] = u.w;
+      }
+    }
+  }
+  float gv[NPL], wv[NPL], bv[NPL];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int col = (i * 64 + lane) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      gv[i * 4 + j] = gamma ? gamma[col + j] : 1.f;
+      wv[i * 4 + j] = w ? w[col + j] : 1.f;
+      bv[i * 4 + j] = w ? b[col + j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    float* xr = x + (int64_t)row * ldx;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) v[r][i] = fmaf(gv[i], yv[r][i], v[r][i]);
+    if (row < rows) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        *(float4*)(xr + (i * 64 + lane) * 4) = make_float4(v[r][i * 4], v[r][i * 4 + 1], v[r][i * 4 + 2], v[r][i * 4 + 3]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) s += v[r][i];
+    const float mean = sr::wave_sum(s) * (1.f / COLS);
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      v[r][i] -= mean;
+      s2 += v[r][i] * v[r][i];
+    }
+    const float rstd = rsqrtf(sr::wave_sum(s2) * (1.f / COLS) + eps);
+    if (row >= rows) break;
+    TO* orow = out + (int64_t)row * ldo;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      float o4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o4[j] = fmaf(v[r][i * 4 + j] * rstd, wv[i * 4 + j], bv[i * 4 + j]);
+      if constexpr (sr::is_bf16<TO>::value) {
+        const bf16x4 o = {(bf16)o4[0], (bf16)o4[1], (bf16)o4[2], (bf16)o4[3]};
+        *(bf16x4*)(orow + col) = o;
+      } else {
+        *(float4*)(orow + col) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+      }
+    }
+  }
+}
+
+template <typename TY, typename TO>
+int residual_layernorm_dispatch(hipStream_t s, float* x, int64_t ldx, const TY* y, int64_t ldy, const float* gamma,
+                                const float* w, const float* b, float eps, TO* out, int64_t ldo, int rows, int cols) {
+  // rows in flight per wave as the LayerNorm (kbench M = 87,936, C = 1024: 1 row 3.5 TB/s, 2 rows
+  // 4.86, 4 rows 4.96 TB/s of the 12 B per element moved)
+#define RLN_LAUNCH(C, R)                                                                                        \
+  hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), \
+                     0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows)
+#define RLN_CASE(C)                                                                                             \
+  case C:                                                                                                       \
+    RLN_LAUNCH(C, ln_rows_per_wave(C / 64));                                                                    \
+    return sr::check_launch("sr_residual_layernorm");
+  switch (cols) {
+    RLN_CASE(256)
+    RLN_CASE(512)
+    RLN_CASE(768)
+    RLN_CASE(1024)
+    RLN_CASE(1536)
+    RLN_CASE(2048)
+  }
+#undef RLN_CASE
+#undef RLN_LAUNCH
+  sr::set_error("sr_residual_layernorm: unsupported cols=%d", cols);
+  return SR_EUNSUPPORTED;
+}
+
 // ------------------------------------------------------------------ im2col
 template <typename T>
 __global__ void im2col_kernel(const float* __restrict__ img, int frames, int H, int W, int ps, float m0, float m1,
@@ -271,6 +387,23 @@ inline dim3 grid_for(int64_t n, int block = 256) {
 }
 
 }  // namespace
+
+extern "C" int sr_residual_layernorm(sr_stream_t stream, int dtype, float* x, int64_t ldx, const void* y, int64_t ldy,
+                                     const float* gamma, const float* w, const float* b, float eps, void* out,
+                                     int64_t ldo, int rows, int cols) {
+  SR_CHECK(x && y && out && rows > 0 && cols > 0, SR_EINVAL, "sr_residual_layernorm: bad args");
+  SR_CHECK((w == nullptr) == (b == nullptr), SR_EINVAL, "sr_residual_layernorm: w and b must both be set or both NULL");
+  SR_CHECK(ldx % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)x & 15) == 0, SR_EINVAL,
+           "sr_residual_layernorm: leading dims must be multiples of 4, x 16-B aligned");
+  SR_CHECK((const void*)x != y && (const void*)x != out, SR_EINVAL, "sr_residual_layernorm: y / out alias x");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    return residual_layernorm_dispatch<bf16, bf16>(s, x, ldx, (const bf16*)y, ldy, gamma, w, b, eps, (bf16*)out, ldo,
+                                                   rows, cols);
+  SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_residual_layernorm: bad dtype");
+  return residual_layernorm_dispatch<float, float>(s, x, ldx, (const float*)y, ldy, gamma, w, b, eps, (float*)out, ldo,
+                                                   rows, cols);
+}
 
 extern "C" int sr_layernorm(sr_stream_t stream, int out_dtype, const float* x, int64_t ldx, const int32_t* rowmap,
                             const float* w, const float* b, float eps, void* out, int64_t ldo, int rows, int cols) {

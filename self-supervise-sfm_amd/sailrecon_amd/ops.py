@@ -526,6 +526,23 @@ def layernorm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float, o
     check(rc, "sr_layernorm")
 
 
+RESIDUAL_LN_COLS = (256, 512, 768, 1024, 1536, 2048)
+
+
+def residual_layernorm(x: Tensor, y: Tensor, gamma: Optional[Tensor], w: Optional[Tensor], b: Optional[Tensor],
+                       eps: float, out: Tensor) -> None:
+    """x += gamma * y (fp32 x in place; y in the compute dtype), then out = LayerNorm(x) (block.py:86-89:
+    the attention branch's residual update followed by norm2); see sr_residual_layernorm."""
+    if x.dtype != torch.float32 or y.dtype != out.dtype or x.shape != y.shape or x.shape != out.shape:
+        raise ValueError("residual_layernorm: x fp32 [rows, cols]; y and out [rows, cols] of one dtype")
+    if x.shape[1] not in RESIDUAL_LN_COLS:
+        raise ValueError(f"residual_layernorm: cols must be one of {RESIDUAL_LN_COLS}")
+    rc = _lib.load().sr_residual_layernorm(_stream(x), dtype_code(out.dtype), _p(x), _rowmajor(x, "x"), _p(y),
+                                           _rowmajor(y, "y"), _p(gamma), _p(w), _p(b), eps, _p(out),
+                                           _rowmajor(out, "out"), x.shape[0], x.shape[1])
+    check(rc, "sr_residual_layernorm")
+
+
 _MEAN = (0.485, 0.456, 0.406)  # aggregator.py:31-32
 _STD = (0.229, 0.224, 0.225)
 

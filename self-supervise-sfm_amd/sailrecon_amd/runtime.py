@@ -15,6 +15,7 @@ ranges (global anchors vs reloc queries) never share scratch.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Dict, Optional, Tuple
 
@@ -184,6 +185,31 @@ def qkv_params(pb: PackedBlock, rope: Optional[Tuple[Tensor, Tensor]], **pos) ->
     return d
 
 
+# SR_FUSED_RESID_LN=1 (opt-in, read at import): the projection GEMM's plain bias epilogue +
+# sr_residual_layernorm instead of its fp32 residual epilogue + sr_layernorm.  Correct (the GPU suite
+# and the C2 / C3 goldens pass under it) and it lifts the GEMMs' MFMA utilisation (0.378 -> 0.391 at
+# C3), but the step does not get faster (409.9 / 409.9 vs 409.1 / 408.6 ms, one box, interleaved):
+# the fused pass moves 12 B per element at 4.96 TB/s (0.218 ms at M = 87,936 against LayerNorm's
+# 0.104 ms), which is what the GEMM epilogue saved, and fc1 then reads xn from HBM rather than MALL.
+_FUSED_RESID_LN = os.environ.get("SR_FUSED_RESID_LN", "0") == "1"
+
+
+def proj_residual_ln2(pb: PackedBlock, xs: Tensor, o: Tensor, qkv: Tensor, xn: Tensor) -> None:
+    """xs += g1 * proj(o); xn = norm2(xs) (block.py:86-89).  Default: the projection GEMM's fp32
+    bias*gamma + residual epilogue, then LayerNorm.  Opt-in (SR_FUSED_RESID_LN=1): the GEMM writes
+    its bias output in the compute dtype into the dead q slot of ``qkv`` (the reference's autocast
+    Linear returns bf16 too) and sr_residual_layernorm streams the residual update and LN2 in one
+    pass."""
+    C = pb.w_proj.shape[0]
+    if _FUSED_RESID_LN and C in ops.RESIDUAL_LN_COLS and qkv.shape[1] >= C:
+        y = qkv[:, :C]
+        ops.gemm(o, pb.w_proj, y, _lib.SR_EPI_BIAS, bias=pb.b_proj, tag="gemm")
+        ops.residual_layernorm(xs, y, pb.g1, pb.ln2_w, pb.ln2_b, pb.eps, xn)
+    else:
+        ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
+        ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
+
+
 def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
               attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict], tag: str = "blk") -> None:
     """x[r0:r1] <- Block(x[r0:r1]); ``attend(qkv_rows, o_rows)`` launches the attention.
@@ -196,8 +222,7 @@ def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
     else:
         ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
     attend(qkv, o)
-    ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
-    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
+    proj_residual_ln2(pb, xs, o, qkv, xn)
     ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
     ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2,
              tag="gemm")
@@ -208,8 +233,7 @@ def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
     output sc.o[r0:r1] was produced separately (frame-sharded global block)."""
     xs = x[r0:r1]
     xn, o, h = sc.xn[r0:r1], sc.o[r0:r1], sc.h[r0:r1]
-    ops.gemm(o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
-    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
+    proj_residual_ln2(pb, xs, o, sc.qkv[r0:r1], xn)
     ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
     ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2,
              tag="gemm")

@@ -149,6 +149,11 @@ def layernorm(x, w, b, eps, out, rowmap=None, rows=None):
     out[:n] = F.layer_norm(src, (x.shape[1],), w, b, eps).to(out.dtype)
 
 
+def residual_layernorm(x, y, gamma, w, b, eps, out):
+    x += (y.float() * (gamma if gamma is not None else 1.0))
+    out.copy_(F.layer_norm(x, (x.shape[1],), w, b, eps).to(out.dtype))
+
+
 def im2col_normalize(img, patch, out, kpad):
     mean = torch.tensor(real_ops._MEAN).view(1, 3, 1, 1)
     std = torch.tensor(real_ops._STD).view(1, 3, 1, 1)
@@ -198,7 +203,8 @@ def pose_decode(enc, hw, ext, intr):
     intr.copy_(i[0])
 
 
-_NAMES = ["gemm", "attention", "attn_merge", "attention_partials", "attn_merge_n", "layernorm", "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
+_NAMES = ["gemm", "attention", "attn_merge", "attention_partials", "attn_merge_n", "layernorm", "residual_layernorm",
+          "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
           "silu", "adaln_modulate", "pose_update", "pose_decode"]
 
 

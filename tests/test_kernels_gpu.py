@@ -363,6 +363,30 @@ def test_layernorm_rowmap(ops, cols, dtype):
     assert rel(out2, F.layer_norm(x, (cols,), eps=1e-6)) < 1e-6
 
 
+@pytest.mark.parametrize("cols", [256, 768, 1024, 2048])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_residual_layernorm(ops, cols, dtype):
+    """x += gamma * y (y strided inside a wider buffer, as the projection output in the qkv slot),
+    out = LN(x): x exact against the fp32 update, out against F.layer_norm; gamma None = 1; ragged
+    row counts (the 4-rows-per-wave tail)."""
+    for rows in (1, 7, 301):
+        x = torch.randn(rows, cols, device=DEV) * 3 + 1
+        ybuf = torch.randn(rows, 3 * cols, device=DEV).to(dtype)
+        y = ybuf[:, cols:2 * cols]
+        g, w, b = (torch.randn(cols, device=DEV) for _ in range(3))
+        for gamma in (g, None):
+            x0 = x.clone()
+            out = torch.empty(rows, cols, device=DEV, dtype=dtype)
+            ops.residual_layernorm(x, y, gamma, w, b, 1e-6, out)
+            xr = x0 + y.float() * (gamma if gamma is not None else 1.0)
+            assert rel(x, xr) < 1e-6
+            ref = F.layer_norm(xr, (cols,), w, b, 1e-6)
+            assert rel(out.float(), ref) < (1e-6 if dtype == torch.float32 else 5e-3)
+            x = x0
+    with pytest.raises(ValueError):
+        ops.residual_layernorm(x, torch.empty(rows, 320, device=DEV, dtype=dtype), None, w, b, 1e-6, out)
+
+
 def test_im2col_and_tokens(ops):
     img = torch.rand(2, 3, 28, 42, device=DEV)
     out = torch.empty(2 * 6, 640, device=DEV)

@@ -95,12 +95,16 @@ def test_small_interleaved_lists(small_model, mode):
     assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
 
 
-def test_block_kats_fp32():
+@pytest.mark.parametrize("fused", [False, True], ids=["resid-epilogue", "fused-resid-ln"])
+def test_block_kats_fp32(fused, monkeypatch):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from sailrecon_amd.layers.block import Block
     from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    from sailrecon_amd import runtime
     from functools import partial
+    # fused: the projection's bias epilogue + sr_residual_layernorm (SR_FUSED_RESID_LN=1)
+    monkeypatch.setattr(runtime, "_FUSED_RESID_LN", fused)
     g = load_npz("g2_blocks.npz")
     blk = Block(dim=1024, num_heads=16, init_values=0.01, qk_norm=True, rope=RotaryPositionEmbedding2D(100))
     blk.load_state_dict(rule_state_dict("block_state_dict_keys.json", "agg"))

@@ -96,6 +96,11 @@ for step in "$@"; do
     kfdiag)  run kfdiag0 300 python tools/kbench.py attn_frame_diag && \
              run kfdiag1 300 env SR_ATTN_PIPE_SEG=1 python tools/kbench.py attn_frame_diag ;;
     parity_split) run parity_split 900 env SR_RELOC_SPLIT=1 python -u -m pytest tests/test_parity_gpu.py -x -v -m gpu -k "c3 or c2" --timeout 600 --timeout-method thread ;;
+    resln_ab) for i in 1 2; do
+                run bench_rl0_$i 400 env SR_FUSED_RESID_LN=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
+                run bench_rl1_$i 400 env SR_FUSED_RESID_LN=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
+              done ;;
+    kln)     run kln 300 python tools/kbench.py ln ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \

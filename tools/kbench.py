@@ -230,6 +230,12 @@ def ln():
     ms = timeit(lambda: ops.layernorm(x, w, b, 1e-5, out))
     gb = M * C * 6 / 1e9
     print(f"layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s")
+    # x += g * y; out = LN(x) (runtime.proj_residual_ln2), y strided in the qkv slot
+    ybuf = torch.randn(M, 3 * C, device=DEV).bfloat16()
+    g = torch.randn(C, device=DEV) * 0.01
+    ms = timeit(lambda: ops.residual_layernorm(x, ybuf[:, :C], g, w, b, 1e-5, out))
+    gb = M * C * 12 / 1e9
+    print(f"residual_layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s", flush=True)
 
 
 def dpt():
