@@ -101,6 +101,13 @@ for step in "$@"; do
                 run bench_rl1_$i 400 env SR_FUSED_RESID_LN=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
               done ;;
     kln)     run kln 300 python tools/kbench.py ln ;;
+    kln)     run kln 300 python tools/kbench.py ln ;;
+    kgemm_var) for i in 1 2; do
+                 run kgemm_v0_$i 300 python tools/kbench.py gemm || exit 1
+                 for v in $GEMM_VARIANTS; do
+                   run kgemm_${v}_$i 300 env SFM_AMD_LIB=variants/libsfm_$v.so python tools/kbench.py gemm || exit 1
+                 done
+               done ;;
     kattn4)  run kattn4 300 env SR_ATTN_WAVES=4 python tools/kbench.py attn ;;
     kattn2)  run kattn2 300 env SR_ATTN_WAVES=2 python tools/kbench.py attn ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
