@@ -32,7 +32,7 @@ compiler reads O / l.
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-OUT = os.path.join(HERE, "..", "self-supervise-sfm_amd", "csrc", "sr_attn_pipe.inc")
+OUT = os.environ.get("SR_PIPE_OUT") or os.path.join(HERE, "..", "self-supervise-sfm_amd", "csrc", "sr_attn_pipe.inc")
 
 S = {0: 160, 1: 192}          # S_b: 32 VGPRs, kb block k at S_b + 16k
 NAMED_V = list(range(160, 224))
@@ -79,6 +79,10 @@ def _label(stem):
 # wait one tile looser
 NO_BARRIER = os.environ.get("SR_PIPE_EXP_NO_BARRIER") == "1"
 VM_SLACK = int(os.environ.get("SR_PIPE_EXP_VM_SLACK", "0"))
+# timing-only (WRONG results): V fragments as one conflict-free ds_read_b128 each (what a V^T tile
+# would cost) / two LDS-DMA pieces per wave and tile instead of four
+EXP_VB128 = os.environ.get("SR_PIPE_EXP_VB128") == "1"
+EXP_DMA2 = os.environ.get("SR_PIPE_EXP_DMA2") == "1"
 
 
 def vr(a, n=1):
@@ -171,6 +175,11 @@ class Phase:
             for db in range(2):
                 off = slot * STAGE_B + TILE_B + (kb * 32 + 16 * s2) * 128
                 f = vfrag(p, i, db)
+                if EXP_VB128:
+                    lines = [("ds", f"ds_read_b128 {ar(f, 4)}, %[ka{(2 * i + db) & 3}] "
+                                    f"offset:{slot * STAGE_B + TILE_B + (i >> 1) * 4096}", seqs, (p, i, db))]
+                    self.other.append((COST["read"], lines, "read"))
+                    continue
                 lines = [("ds", f"ds_read_b64_tr_b16 {ar(f, 2)}, %[va{db}] offset:{off}", None, None),
                          ("ds", f"ds_read_b64_tr_b16 {ar(f + 2, 2)}, %[va{db}] offset:{off + 1024}", seqs, (p, i, db))]
                 self.other.append((2 * COST["read"], lines, "read"))
@@ -179,6 +188,8 @@ class Phase:
         """LDS-DMA of tile t+3 (4 pieces of 8 rows per wave) into ring slot `slot`; the per-lane
         source offsets then step one tile."""
         step = "%[sstc]" if SEG else "%[sstep]"
+        if EXP_DMA2:
+            pieces = [i for i in pieces if i in (0, 3)]
         for i in pieces:
             lines = []
             if SEG and i == 0:
