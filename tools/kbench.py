@@ -197,6 +197,25 @@ def gemm(M=2 * 32 * 1374):
         print(f"gemm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
 
 
+def gemm_k():
+    """Per-tile fixed cost of the 256x256 GEMM: exactly 5 rounds of 256 tiles (M = 81,920, N = 1024)
+    at K = 256 ... 4096; time = fixed + K * per-k, the intercept is the prologue / epilogue / tile
+    start cost of one round."""
+    M, N = 81920, 1024
+    for epi, ename in ((_lib.SR_EPI_BIAS, "bias"), (_lib.SR_EPI_BIAS_RESID, "resid")):
+        for K in (256, 512, 1024, 2048, 4096):
+            a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+            w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / 32
+            b = torch.randn(N, device=DEV)
+            g = torch.randn(N, device=DEV)
+            out = torch.zeros(M, N, device=DEV) if epi == _lib.SR_EPI_BIAS_RESID else \
+                torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=g))
+            fl = 2.0 * M * N * K
+            print(f"gemm_k {ename:5s} M={M} N={N} K={K:5d} {ms:8.4f} ms  {ms / 5 * 1e3:7.2f} us/round  "
+                  f"{fl / ms / 1e9:8.1f} TF/s")
+
+
 def gemm_f32():
     """The exact-fp32 GEMM at DPT conv shapes (im2col'd 3x3 convs, 8 frames per chunk)."""
     for name, (M, N, K) in {"rn1 3x3 256->256 @148": (8 * 148 * 148, 256, 2304),
