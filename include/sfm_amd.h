@@ -173,6 +173,15 @@ typedef struct sr_attn_desc {
                   readable rows of finite values past the end of every key segment (K and V; e.g.
                   the next frame's rows or zeroed workspace padding), so the hand-scheduled sweep
                   may stage a ragged last tile whole and mask its extra keys; 0 = unset */
+  /* optional merge-in (sr_attention, bf16 path): merge_o holds a result of the SAME query rows over
+     a DISJOINT key set, row-normalised bf16 (row r at merge_o + r*ld_merge_o, the head's columns at
+     head*head_dim), and merge_lse its log2-domain LSE ([heads][merge_rows]); the row of (item,
+     query row i) is item*q_bstride + i.  o then receives the softmax over the union of the key
+     sets (sr_attn_merge's formula) and lse, if set, the union's LSE.  NULL = off */
+  const void* merge_o;
+  int64_t ld_merge_o;
+  const float* merge_lse;
+  int64_t merge_rows;
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */

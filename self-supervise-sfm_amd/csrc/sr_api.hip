@@ -29,4 +29,4 @@ int check_launch(const char* what) {
 }  // namespace sr
 
 extern "C" const char* sr_last_error(void) { return g_err; }
-extern "C" int sr_version(void) { return (0 << 16) | 1; }
+extern "C" int sr_version(void) { return (0 << 16) | 2; }

@@ -529,18 +529,40 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
     for (int t = 0; t < ntiles; ++t) plain_tile(t);
   }
 
-  // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training)
+  // ---- epilogue: O[q][hcol + d] = O^T[d][q] / l  (+ the row's log2-domain LSE for training).
+  // Merge-in (d.merge_o): the row's result over a DISJOINT key set, row-normalised, with its LSE
+  // la, is folded in exactly as sr_attn_merge does:  out = (2^(la-M) o_a + 2^(lb-M) o / l) /
+  // (2^(la-M) + 2^(lb-M)),  lb = this sweep's LSE, M = max(la, lb)  (the split reloc attention
+  // ends in its second pass instead of a separate merge launch).
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const float s0 = __shfl(lacc[b][0], l32 & 15), s1 = __shfl(lacc[b][1], l32 & 15);
     const float lsum = l32 < 16 ? s0 : s1;
-    const float inv = 1.f / lsum;
     const bool wide_o = d.ldo % 8 == 0 && ((uintptr_t)d.o & 15) == 0;
     const int qrow = qrow0 + 32 * b;
-    if (d.lse && hi == 0 && qrow < d.lq)
-      d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m_run[b] + log2f(lsum);
+    float inv = 1.f / lsum, sa = 0.f;
+    float lse_row = m_run[b] + log2f(lsum);
+    const bf16* mo = nullptr;
+    if (d.merge_o && qrow < d.lq) {
+      const int64_t rg = (int64_t)item * d.q_bstride + qrow;
+      const float la = d.merge_lse[(int64_t)head * d.merge_rows + rg];
+      const float mx = fmaxf(la, lse_row);
+      const float wa = exp2f(la - mx), wb = exp2f(lse_row - mx);
+      const float rw = 1.f / (wa + wb);
+      sa = wa * rw;
+      inv *= wb * rw;
+      lse_row = mx + log2f(wa + wb);
+      mo = (const bf16*)d.merge_o + rg * d.ld_merge_o + hcol;
+    }
+    if (d.lse && hi == 0 && qrow < d.lq) d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = lse_row;
     if (qrow < d.lq) {
       bf16* op = (bf16*)d.o + (item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol;
+      // the merge partial's 4 columns at c (8-B load; zero weight when there is none)
+      auto part = [&](int c) -> f32x4 {
+        if (!mo) return f32x4{0.f, 0.f, 0.f, 0.f};
+        const bf16x4 v = *(const bf16x4*)(mo + c);
+        return f32x4{sa * (float)v[0], sa * (float)v[1], sa * (float)v[2], sa * (float)v[3]};
+      };
       if (wide_o) {
         // lane halves hold columns 8g..8g+3 (hi = 0) and 8g+4..8g+7 (hi = 1) of the row: one
         // permlane32 swap per dword joins groups (2k, 2k+1) into 16 contiguous bytes per lane,
@@ -550,10 +572,11 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
 #pragma unroll
           for (int k = 0; k < 2; ++k) {
             bf16x4 va, vb;
+            const f32x4 pa = part(db * 32 + 16 * k + 4 * hi), pb = part(db * 32 + 16 * k + 8 + 4 * hi);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              va[j] = (bf16)(o[b][db][8 * k + j] * inv);
-              vb[j] = (bf16)(o[b][db][8 * k + 4 + j] * inv);
+              va[j] = (bf16)(o[b][db][8 * k + j] * inv + pa[j]);
+              vb[j] = (bf16)(o[b][db][8 * k + 4 + j] * inv + pb[j]);
             }
             const uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
             const auto x = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
@@ -566,8 +589,9 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             bf16x4 v;
+            const f32x4 pv = part(db * 32 + 8 * g + 4 * hi);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv);
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[b][db][4 * g + j] * inv + pv[j]);
             *(bf16x4*)(op + db * 32 + 8 * g + 4 * hi) = v;
           }
       }
@@ -1359,6 +1383,9 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   AttnArgs a;
   a.d = d;
   hipStream_t s = (hipStream_t)stream;
+  SR_CHECK(!d.merge_o || (dtype == SR_BF16 && d.merge_lse && d.merge_rows > 0 && d.ld_merge_o % 4 == 0 &&
+                          ((uintptr_t)d.merge_o & 7) == 0),
+           SR_EINVAL, "sr_attention: merge_o needs the bf16 path, merge_lse, merge_rows and 8-B aligned rows");
   if (dtype == SR_BF16) {
     SR_CHECK(d.head_dim == 64, SR_EUNSUPPORTED, "sr_attention(bf16): head_dim must be 64 (got %d)", d.head_dim);
     SR_CHECK(d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED, "sr_attention(bf16): masks need the f32 kernel");
@@ -1531,7 +1558,7 @@ extern "C" int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* desc, co
   const sr_attn_desc& d = *desc;
   SR_CHECK(d.v0 && d.o && d.batch > 0 && d.heads > 0 && d.lq > 0 && d.l0 > 0, SR_EINVAL,
            "sr_attention_qk8: bad v0/o/sizes");
-  SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED,
+  SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE && !d.merge_o, SR_EUNSUPPORTED,
            "sr_attention_qk8: head_dim 64, one key segment, no mask");
   SR_CHECK(ldq8 % 16 == 0 && ldk8 % 16 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0, SR_EINVAL,
            "sr_attention_qk8: leading dims (fp8 rows 16-B aligned, bf16 multiples of 8)");
@@ -1573,7 +1600,7 @@ extern "C" int sr_attention_qkv8(sr_stream_t stream, const sr_attn_desc* desc, c
   const sr_attn_desc& d = *desc;
   SR_CHECK(d.o && d.batch == 1 && d.heads > 0 && d.lq > 0 && d.l0 > 0, SR_EINVAL,
            "sr_attention_qkv8: o / sizes (one item: the global block)");
-  SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED,
+  SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE && !d.merge_o, SR_EUNSUPPORTED,
            "sr_attention_qkv8: head_dim 64, one key segment, no mask");
   SR_CHECK(ldq8 % 16 == 0 && ldk8 % 16 == 0 && d.ldo % 4 == 0, SR_EINVAL, "sr_attention_qkv8: leading dims");
   AttnArgs a;

@@ -60,6 +60,7 @@ class AttnDesc(ctypes.Structure):
         ("o_bstride", _i64),
         ("mask", _vp), ("mask_bstride", _i64), ("mask_hstride", _i64), ("mask_ld", _i64),
         ("tail_rows_readable", _i32),
+        ("merge_o", _vp), ("ld_merge_o", _i64), ("merge_lse", _vp), ("merge_rows", _i64),
     ]
 
 

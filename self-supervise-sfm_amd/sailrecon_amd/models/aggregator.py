@@ -516,30 +516,29 @@ class Aggregator(nn.Module):
                 rows = Nq_l * P
                 kb = runtime.key_norm_bound(pr)
                 if self._split_reloc(dtype, rows, n_sub_all):
-                    # two passes + LSE merge (the union of the two key sets, exactly): every query row
-                    # against the shared anchor subsample's whole 64-key tiles as ONE long query set
-                    # (the hand-scheduled sweep, sr_attn.hip), then each query frame against the
-                    # subsample's last partial tile (shared segment 0) and itself (segment 1) on the
-                    # compiled sweep
+                    # two passes merged by their LSEs (the union of the two key sets, exactly): every
+                    # query row against the shared anchor subsample's whole 64-key tiles as ONE long
+                    # query set (the hand-scheduled sweep, sr_attn.hip), then each query frame against
+                    # the subsample's last partial tile (shared segment 0) and itself (segment 1) on
+                    # the compiled sweep, whose epilogue folds the first pass in (sr_attn_desc.merge_o)
                     n_full = n_sub_all // 64 * 64
-                    o_parts, lse_parts = ops.key_split_workspace(dev, 2, rows, C, pr.heads, name="reloc_split")
+                    o_a, lse_a = ops.key_split_workspace(dev, 1, rows, C, pr.heads, name="reloc_split")
+                    lse_a = lse_a[0]
                     ops.attention(qkv[:, 0:C], kv_sub_all[:n_full, 0:C], kv_sub_all[:n_full, C:2 * C],
-                                  o_parts[:rows], heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows,
+                                  o_a, heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows,
                                   q_bstride=0, l0=n_full, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
-                                  lse=lse_parts[0].view(-1), tail_readable=True)
+                                  lse=lse_a.view(-1), tail_readable=True)
                     if n_full < n_sub_all:
                         ops.attention(qkv[:, 0:C], kv_sub_all[n_full:, 0:C], kv_sub_all[n_full:, C:2 * C],
-                                      o_parts[rows:], heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P,
+                                      o, heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P,
                                       q_bstride=P, l0=n_sub_all - n_full, k0_bstride=0, k1=qkv[:, C:2 * C],
                                       v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                                      key_norm_max=kb, lse=lse_parts[1].view(-1), tail_readable=True)
+                                      key_norm_max=kb, tail_readable=True, merge_o=o_a, merge_lse=lse_a)
                     else:
-                        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o_parts[rows:],
+                        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o,
                                       heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=P,
-                                      k0_bstride=P, tag="attn_reloc", key_norm_max=kb,
-                                      lse=lse_parts[1].view(-1), tail_readable=True)
-                    ops.attn_merge_n(o_parts, lse_parts, o, parts=2, rows=rows, heads=pr.heads,
-                                     head_dim=pr.head_dim, seg_rows=[rows, P])
+                                      k0_bstride=P, tag="attn_reloc", key_norm_max=kb, tail_readable=True,
+                                      merge_o=o_a, merge_lse=lse_a)
                     return
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
@@ -630,12 +629,13 @@ class Aggregator(nn.Module):
 
     @staticmethod
     def _split_reloc(dtype, rows: int, n_sub: int) -> bool:
-        """Opt-in (SR_RELOC_SPLIT=1, bf16, a query set that fills the chip without key splitting):
-        the reloc attention as two passes + LSE merge, the shared subsample's whole tiles over all
-        query rows on the hand-scheduled sweep.  Correct (C2 / C3 parity under it) but break-even
-        (kbench, one box: 1.424 + 0.285 + merge 0.074 = 1.783 ms vs 1.792 ms in one launch; whole C3
-        step 402.4 / 403.1 vs 404.2 / 402.7 ms), so the one-launch form stays the default."""
-        return (os.environ.get("SR_RELOC_SPLIT") == "1" and dtype == torch.bfloat16 and
+        """The reloc attention as two passes (bf16, a query set that fills the chip without key
+        splitting; SR_RELOC_SPLIT=0 turns it off): the shared subsample's whole tiles over all query
+        rows on the hand-scheduled sweep, then the own-frame pass whose epilogue folds the first in
+        (sr_attn_desc.merge_o).  Measured (one box, kbench): 1.505 + 0.332 = 1.837 ms against 1.883 ms
+        in one launch; whole C3 step 417.8 / 418.2 vs 419.5 / 418.9 ms (interleaved).  With a separate
+        merge launch instead (round 3, first form) it was break-even."""
+        return (os.environ.get("SR_RELOC_SPLIT", "1") == "1" and dtype == torch.bfloat16 and
                 (rows + 255) // 256 * 16 >= 2048 and n_sub >= 64)
 
     def _side_stream(self, dev):

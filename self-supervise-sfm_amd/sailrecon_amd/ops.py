@@ -242,7 +242,8 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
               q_bstride: int, l0: int, k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
               scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
-              key_norm_max: float = 0.0, mask: Optional[Tensor] = None, tail_readable: bool = False) -> None:
+              key_norm_max: float = 0.0, mask: Optional[Tensor] = None, tail_readable: bool = False,
+              merge_o: Optional[Tensor] = None, merge_lse: Optional[Tensor] = None) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``mask``
     (mask_mode SR_MASK_DENSE: bool / uint8, nonzero = attend; SR_MASK_ADD: fp32 added to the
     scores) is a [batch, heads, lq, l0 + l1] view (broadcast dims may have stride 0, the last dim
@@ -253,8 +254,19 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     fill the chip runs key-split (key_split_parts, attention_partials + attn_merge_n).
     ``tail_readable``: at least 64 rows of finite values follow every key segment in memory
     (runtime.Workspace buffers: zero-initialised, 64 rows of padding), which lets the
-    hand-scheduled sweep take ragged and two-segment launches (sr_attn_desc.tail_rows_readable)."""
+    hand-scheduled sweep take ragged and two-segment launches (sr_attn_desc.tail_rows_readable).
+    ``merge_o`` / ``merge_lse`` (bf16 only): a row-normalised result of the same query rows over a
+    DISJOINT key set ([R, >= heads*head_dim] bf16, row item*q_bstride + i) and its log2-domain LSE
+    (fp32 [heads, R]); o then receives the softmax over the union (sr_attn_desc.merge_o)."""
     parts = key_split_parts(dtype=q.dtype, batch=batch, lq=lq, heads=heads, l0=l0, l1=l1, mask_mode=mask_mode)
+    if merge_o is not None:
+        if q.dtype != torch.bfloat16 or merge_o.dtype != torch.bfloat16 or merge_o.stride(1) != 1 or \
+                merge_lse is None or merge_lse.dtype != torch.float32 or not merge_lse.is_contiguous() or \
+                merge_lse.dim() != 2 or merge_lse.shape[0] != heads or merge_o.shape[1] < heads * head_dim or \
+                merge_o.shape[0] < merge_lse.shape[1] or merge_lse.shape[1] < (batch - 1) * q_bstride + lq:
+            raise ValueError("attention: merge_o must be bf16 [R, heads*head_dim] rows and merge_lse fp32 "
+                             "[heads, R] covering every query row")
+        parts = 1
     if parts > 1:
         if lse is not None and (lse.dtype != torch.float32 or not lse.is_contiguous() or lse.numel() != heads * lq):
             raise ValueError("attention: lse must be contiguous fp32 [batch, heads, lq]")
@@ -268,6 +280,9 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
                    n_anchor=n_anchor, scale=scale, lse=lse)
     if tail_readable:
         d.tail_rows_readable = 64
+    if merge_o is not None:
+        d.merge_o, d.ld_merge_o = _p(merge_o), merge_o.stride(0)
+        d.merge_lse, d.merge_rows = _p(merge_lse), merge_lse.shape[1]
     if mask_mode in (_lib.SR_MASK_DENSE, _lib.SR_MASK_ADD):
         want = torch.float32 if mask_mode == _lib.SR_MASK_ADD else (torch.bool, torch.uint8)
         if mask is None or mask.dim() != 4 or tuple(mask.shape) != (batch, heads, lq, l0 + l1) or \

@@ -351,7 +351,7 @@ def test_reloc_attention_production(ops, nq, nsub, tail, monkeypatch):
 
 @pytest.mark.parametrize("nq", [8, 32], ids=["C2", "C3"])
 def test_reloc_attention_split_production(ops, nq):
-    """global_reloc as the aggregator's opt-in split (SR_RELOC_SPLIT=1): every query row against the
+    """global_reloc as the aggregator's split (default; SR_RELOC_SPLIT=0 = one launch): every query row against the
     shared subsample's whole 64-key tiles as one long query set (the hand-scheduled sweep), each
     frame against the subsample's last partial tile + itself, merged by LSE with mixed layouts in
     the bf16 merge kernel; equal to the one-launch kernel and to fp64 on sampled rows."""
@@ -369,14 +369,28 @@ def test_reloc_attention_split_production(ops, nq):
     one = torch.empty_like(o)
     ops.attention(q, ks, vs, one, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
                   k1=k, v1=v, l1=P, k1_bstride=P)
+    # the aggregator's form: the second pass folds the first in (sr_attn_desc.merge_o) and writes the
+    # union's LSE; the one-launch kernel's LSE is the reference for it
+    om = torch.empty_like(o)
+    lse_m = torch.empty(nq, H, P, device=DEV)
+    ops.attention(q, ks[nf:], vs[nf:], om, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub - nf,
+                  k0_bstride=0, k1=k, v1=v, l1=P, k1_bstride=P, lse=lse_m.view(-1), merge_o=o_parts[:rows],
+                  merge_lse=lse_parts[0])
+    lse_one = torch.empty(nq, H, P, device=DEV)
+    ops.attention(q, ks, vs, one, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
+                  k1=k, v1=v, l1=P, k1_bstride=P, lse=lse_one.view(-1))
     torch.cuda.synchronize()
     assert _rel(o.float(), one.float()) < 1e-2
+    assert _rel(om.float(), one.float()) < 1e-2
+    assert _rel(om.float(), o.float()) < 5e-3  # same partials, the merge in fp32 either way
+    assert float((lse_m - lse_one).abs().max()) < 1e-2
     scale = D ** -0.5
     for j in sorted({0, nq // 2, nq - 1}):
         fr = slice(j * P, (j + 1) * P)
         rws = _sample_rows(P, 40, j).to(DEV)
         ref = _ref_rows(q[fr][rws], torch.cat([ks, k[fr]]), torch.cat([vs, v[fr]]), scale)
         assert _rel(o[fr][rws].float(), ref) < 1e-2, j
+        assert _rel(om[fr][rws].float(), ref) < 1e-2, j
 
 
 @pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])

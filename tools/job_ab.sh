@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# One-off A/B job: GPU steps in order, each under its own time limit; stops at the first failure.
+set -u
+mkdir -p gpurun_out
+run() { local name=$1 secs=$2; shift 2; echo "=== $name" >> gpurun_out/job.log; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc" >> gpurun_out/job.log; [ $rc -eq 0 ] || exit $rc; }
+T="--timeout 600 --timeout-method thread"
+case ${1:-} in
+  split)
+    run split_test 600 python -u -m pytest tests/test_baseline_shapes_gpu.py -x -q -m gpu -k "split or reloc" $T
+    run kreloc 300 python tools/kbench.py attn
+    run parity_split 900 env SR_RELOC_SPLIT=1 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "c3 or c2" $T
+    for i in 1 2; do
+      run bench_rs0_$i 400 env SR_RELOC_SPLIT=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+      run bench_rs1_$i 400 env SR_RELOC_SPLIT=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+    done ;;
+  *) echo "unknown job ${1:-}"; exit 2 ;;
+esac

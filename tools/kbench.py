@@ -93,10 +93,17 @@ def attn():
 
     def pm():
         ops.attn_merge_n(o_parts, lse_parts, o, parts=2, rows=rows, heads=H, head_dim=D, seg_rows=[rows, P])
-    ta, tb, tm = timeit(pa), timeit(pb), timeit(pm)
+
+    def pbm():  # the aggregator's form: the second pass merges the first in its epilogue
+        ops.attention(qkv[:, :C], kv[nf:, :C], kv[nf:, C:], o, heads=H, head_dim=D, batch=N, lq=P,
+                      q_bstride=P, l0=nsub - nf, k0_bstride=0, k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:], l1=P,
+                      k1_bstride=P, key_norm_max=kb, tail_readable=tail, merge_o=o_parts[:rows],
+                      merge_lse=lse_parts[0])
+    ta, tb, tm, tbm = timeit(pa), timeit(pb), timeit(pm), timeit(pbm)
     print(f"attn reloc split: subsample pass {ta:.3f} ms ({4.0 * H * rows * nf * D / ta / 1e9:.1f} TF/s), "
           f"tail+own pass {tb:.3f} ms, merge {tm:.3f} ms, total {ta + tb + tm:.3f} ms  "
-          f"{fl / (ta + tb + tm) / 1e9:8.1f} TF/s")
+          f"{fl / (ta + tb + tm) / 1e9:8.1f} TF/s; merge-in pass {tbm:.3f} ms, total {ta + tbm:.3f} ms  "
+          f"{fl / (ta + tbm) / 1e9:8.1f} TF/s")
 
 
 def attn_frame_diag():
