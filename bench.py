@@ -107,7 +107,7 @@ def host_cpu():
 # (rocprofv3 row names; see DESIGN.md "Kernels").
 _PIPE = "true" if os.environ.get("SR_ATTN_PIPE", "1") != "0" else "false"  # sr_attn.hip: the asm sweep
 KERNEL_OF_TAG = {
-    "attn_global": f"attn_bf16_kernel<4, 2, 2, {_PIPE}>", "attn_reloc": "attn_bf16_kernel<4, 2, 1, false>",
+    "attn_global": f"attn_bf16_kernel<4, 2, 2, {_PIPE}>", "attn_reloc": f"attn_bf16_kernel<4, 2, 3, {_PIPE}>",
     "attn_frame": "attn_bf16_kernel<4, 2, 0, false>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
     "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
 }
@@ -129,7 +129,7 @@ def kernel_of_tag(tag: str, views: int, img: int):
 
 
 TRAFFIC_FILES = [os.path.join(REPO, "profiles", f) for f in
-                 ("r03_pmc_traffic.json", "r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
+                 ("r03b_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
 
 
 def pmc_traffic(kernel: str, views: int, img: int, fp8: str = "off"):

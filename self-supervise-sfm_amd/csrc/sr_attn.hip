@@ -57,7 +57,7 @@ __device__ __forceinline__ float sum_x32(float v) {
 }
 
 // NW waves x QB 32-row q-blocks per wave; KIND only names the call site in profiles
-// (0 frame, 1 global_reloc, 2 global).
+// (0 frame, 1 global_reloc, 2 global, 3 the split reloc's subsample pass).
 //
 // Tile loop (K/V ring of NBUF=4 stages, up to 3 in flight, one barrier per tile):
 //   S_b = K Q_b^T                  (8 MFMA per q-block; each K fragment read once, used QB times)
@@ -1411,7 +1411,9 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     }
     // one long query item = the global block (also its two-segment remote-anchor pass under frame
     // sharding); otherwise a second segment = global_reloc
-    const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : (d.l1 > 0 ? 1 : 0);
+    // (3: one long query set against a SHORTER shared key set, the split reloc block's subsample
+    // pass -- the same code as 2, its own name in the profiles)
+    const int kind = d.batch == 1 && d.lq >= 4096 ? (d.l1 == 0 && d.l0 < d.lq ? 3 : 2) : (d.l1 > 0 ? 1 : 0);
     // Workgroup shapes (waves x 32-row q-blocks per wave):
     //   0: 4 x 2 = 256 rows    1: 8 x 1 = 256 rows    2: 2 x 2 = 128 rows
     // 256-row tiles unless they would leave CUs idle (fewer than 2 workgroups per CU, e.g. the
@@ -1445,7 +1447,8 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
 #define SR_ATTN_LAUNCH(NW_, QB_, ST_)                                                                           \
   do {                                                                                                        \
-    if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 2, ST_>), grid, dim3(NW_ * 64), 0, s, a);     \
+    if (kind == 3) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 3, ST_>), grid, dim3(NW_ * 64), 0, s, a);     \
+    else if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 2, ST_>), grid, dim3(NW_ * 64), 0, s, a); \
     else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 1, ST_>), grid, dim3(NW_ * 64), 0, s, a); \
     else hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 0, ST_>), grid, dim3(NW_ * 64), 0, s, a);               \
   } while (0)

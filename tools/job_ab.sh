@@ -13,5 +13,11 @@ case ${1:-} in
       run bench_rs0_$i 400 env SR_RELOC_SPLIT=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
       run bench_rs1_$i 400 env SR_RELOC_SPLIT=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
     done ;;
+  conc)
+    for i in 1 2; do
+      run bench_cs0_$i 400 env SR_CONCURRENT_STACKS=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+      run bench_cs1_$i 400 env SR_CONCURRENT_STACKS=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+    done
+    run parity_conc 900 env SR_CONCURRENT_STACKS=1 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "c3 or c2" $T ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac
