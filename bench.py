@@ -117,8 +117,27 @@ _GEMM_N = {"gemm_bias": 3072, "gemm_gelu": 4096, "gemm_resid": 1024, "gemm_qkv":
 _GEMM_EPI = {"gemm_bias": 0, "gemm_gelu": 1, "gemm_resid": 2, "gemm_qkv": 3, "gemm_patch": 4}
 
 
+_PAIR = os.environ.get("SR_ATTN_PAIR", "1") != "0"  # aggregator: global + reloc subsample attention paired
+
+
+def _paired(views: int, img: int) -> bool:
+    """Whether the single-GPU forward pairs the global attention with the split reloc's subsample
+    pass (aggregator._paired_attention at this workload)."""
+    rows = views * ((img // 14) ** 2 + 5)
+    return (_PAIR and _PIPE == "true" and rows % 64 == 0 and (rows + 255) // 256 * 16 >= 2048 and
+            os.environ.get("SR_RELOC_SPLIT", "1") == "1")
+
+
 def kernel_of_tag(tag: str, views: int, img: int):
     """rocprofv3 row name of the kernel a timer class launches at this workload."""
+    if tag in ("attn_global", "attn_reloc") and _paired(views, img):
+        # attn_global: one sr_attention_pair launch (the global attention + the split reloc's
+        # subsample pass); attn_reloc: the reloc own-frame pass that folds the subsample pass in
+        return "attn_bf16_pair_kernel<2>" if tag == "attn_global" else "attn_bf16_kernel<4, 2, 1, false>"
+    if tag == "attn_reloc":  # split reloc (subsample pass = the larger launch) only for long query sets
+        rows = views * ((img // 14) ** 2 + 5)
+        split = (rows + 255) // 256 * 16 >= 2048 and os.environ.get("SR_RELOC_SPLIT", "1") == "1"
+        return f"attn_bf16_kernel<4, 2, 3, {_PIPE}>" if split else "attn_bf16_kernel<4, 2, 1, false>"
     if tag in _GEMM_N:
         rows = 2 * views * ((img // 14) ** 2 + 5)
         if tag == "gemm_patch":

@@ -189,6 +189,16 @@ int sr_attention_bound_floats(const sr_attn_desc* d);
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 
+/* Two independent single-query-set bf16 attentions in ONE launch of the hand-scheduled sweep:
+ * d0's workgroups are dispatched first, d1's fill the CUs d0 leaves idle in its last round (the
+ * C3 global block's anchors against themselves and the split reloc block's queries against the
+ * anchor subsample, 10.75 workgroup rounds each).  Each desc as sr_attention's bf16 path with
+ * batch 1, one key segment of whole 64-key tiles (>= 4), a static key_norm_max, no mask or
+ * merge_o (lse optional), equal head counts; SR_EUNSUPPORTED otherwise (the caller then launches them apart).
+ * Replaces the two F.scaled_dot_product_attention calls of one layer's global and global_reloc
+ * blocks (attention.py:103-109; aggregator.py:672-769). */
+int sr_attention_pair(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1);
+
 /* Merge two attention results of the same query rows over DISJOINT key sets, given each one's
  * log2-domain LSE ([heads][rows] fp32, as sr_attention writes for batch 1):
  *   out = (2^(la-m) o_a + 2^(lb-m) o_b) / (2^(la-m) + 2^(lb-m)),  m = max(la, lb)

@@ -71,8 +71,9 @@ constexpr float RESCALE_LOG2 = 8.f;
 #ifndef SR_ATTN_DEFAULT_CFG
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
-template <int NW, int QB, int KIND, bool PIPE = false>
-__global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf16_kernel(AttnArgs args) {
+// One workgroup's work: q-tile qt of (head, item) against every key of the item's segments.
+template <int NW, int QB, int KIND, bool PIPE>
+__device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int qt, const int head, const int item) {
   static_assert(!PIPE || (NW == 4 && QB == 2), "the pipelined sweep pairs the two q-blocks of a wave");
   constexpr int QROWS = NW * 32 * QB;
   constexpr int NBUF = NW >= 4 ? 4 : 2;  // K/V ring stages
@@ -81,29 +82,6 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int qt = blockIdx.x, head = blockIdx.y, item = blockIdx.z;
-  {
-    // Blocks are dealt round-robin over the 8 XCDs (each with its own L2); the bijective remap
-    // hands each XCD a contiguous range of tiles instead, so the q-tiles that read the same K/V
-    // run on one XCD:
-    //   global (one item): the 172 q-tiles of a head (C3) sweep its 11 MB K/V together;
-    //   frame: the 6 q-tiles of a (frame, head) share its 350 KB K/V (3.5x -> ~1x HBM traffic);
-    //   global_reloc: head-major, every query frame of a head reads the same anchor-subsample
-    //   K/V (segment 0, 2.5 MB per head at C3).
-    const int nq = gridDim.x, nh = gridDim.y, nb = gridDim.z;
-    const int lin = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
-    {
-      const int tile = sr::xcd_remap(lin, nq * nh * nb);
-      qt = tile % nq;
-      if constexpr (KIND == 1) {
-        item = (tile / nq) % nb;
-        head = tile / (nq * nb);
-      } else {
-        head = (tile / nq) % nh;
-        item = tile / (nq * nh);
-      }
-    }
-  }
   const int hcol = head * 64;
   const int l32 = lane & 31, hi = lane >> 5;
   const int ntiles = args.ntile0 + args.ntile1;
@@ -597,6 +575,52 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
       }
     }
   }
+}
+
+template <int NW, int QB, int KIND, bool PIPE = false>
+__global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf16_kernel(AttnArgs args) {
+  // Blocks are dealt round-robin over the 8 XCDs (each with its own L2); the bijective remap
+  // hands each XCD a contiguous range of tiles instead, so the q-tiles that read the same K/V
+  // run on one XCD:
+  //   global (one item): the 172 q-tiles of a head (C3) sweep its 11 MB K/V together;
+  //   frame: the 6 q-tiles of a (frame, head) share its 350 KB K/V (3.5x -> ~1x HBM traffic);
+  //   global_reloc: head-major, every query frame of a head reads the same anchor-subsample
+  //   K/V (segment 0, 2.5 MB per head at C3).
+  const int nq = gridDim.x, nh = gridDim.y, nb = gridDim.z;
+  const int lin = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
+  const int tile = sr::xcd_remap(lin, nq * nh * nb);
+  const int qt = tile % nq;
+  int head, item;
+  if constexpr (KIND == 1) {
+    item = (tile / nq) % nb;
+    head = tile / (nq * nb);
+  } else {
+    head = (tile / nq) % nh;
+    item = tile / (nq * nh);
+  }
+  attn_bf16_body<NW, QB, KIND, PIPE>(args, qt, head, item);
+}
+
+// Two single-query-set problems of the hand-scheduled sweep in ONE launch (sr_attention_pair):
+// the global block's anchors against themselves and the split reloc block's queries against the
+// shared anchor subsample.  Problem 0's workgroups come first in dispatch order (its count padded
+// to a multiple of 8, so problem 1's ids keep their XCD), each problem XCD-remapped within itself:
+// the second, shorter problem's workgroups fill the CUs the first leaves idle in its last round.
+struct AttnPair {
+  AttnArgs a[2];
+  int nwg0p;     // problem 0's workgroups rounded up to 8
+  int nq[2], nh;  // q-tiles per problem, heads (both)
+};
+
+template <int KIND>
+__global__ __launch_bounds__(256, 1) void attn_bf16_pair_kernel(AttnPair p) {
+  int lin = blockIdx.x;
+  const int sel = lin >= p.nwg0p ? 1 : 0;
+  if (sel) lin -= p.nwg0p;
+  const int nq = p.nq[sel], nwg = nq * p.nh;
+  if (lin >= nwg) return;  // problem 0's padding
+  const int tile = sr::xcd_remap(lin, nwg);
+  attn_bf16_body<4, 2, KIND, true>(p.a[sel], tile % nq, tile / nq, 0);
 }
 
 // ------------------------------------------------------------------ fp8 Q.K^T (BASELINE C5)
@@ -1368,6 +1392,47 @@ extern "C" int sr_attention_bound_floats(const sr_attn_desc* desc) {
   if (!desc || desc->head_dim != 64 || desc->mask_mode != SR_MASK_NONE || desc->heads > 32) return 0;
   int n0;
   return bound_instances(*desc, n0) * desc->heads;
+}
+
+// The hand-scheduled sweep's launch conditions for one problem of sr_attention_pair (bf16, one
+// long query set against one segment of whole key tiles, a static key bound).
+static int pair_args(const sr_attn_desc& d, AttnArgs& a, const char* which) {
+  SR_CHECK(d.q && d.o && d.k0 && d.v0 && !d.merge_o, SR_EINVAL, "sr_attention_pair(%s): null q/k0/v0/o, or merge_o set", which);
+  SR_CHECK(d.batch == 1 && d.heads > 0 && d.head_dim == 64 && d.lq > 0 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE,
+           SR_EUNSUPPORTED, "sr_attention_pair(%s): one query set, head_dim 64, one key segment, no mask", which);
+  SR_CHECK(d.l0 >= 4 * KT && d.l0 % KT == 0 && d.key_norm_max > 0.f, SR_EUNSUPPORTED,
+           "sr_attention_pair(%s): whole key tiles (>= 4) and a static key bound", which);
+  SR_CHECK(d.ldq % 8 == 0 && d.ldk0 % 8 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0, SR_EINVAL,
+           "sr_attention_pair(%s): leading dims must be multiples of 8", which);
+  a.d = d;
+  a.ntile0 = d.l0 / KT;
+  a.ntile1 = 0;
+  a.kb_n0 = 1;
+  static const int allow_mz = [] {
+    const char* e = getenv("SR_ATTN_MZERO");
+    return e ? atoi(e) : 1;
+  }();
+  a.allow_mzero = allow_mz;
+  return SR_OK;
+}
+
+extern "C" int sr_attention_pair(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1) {
+  SR_CHECK(d0 && d1, SR_EINVAL, "sr_attention_pair: null desc");
+  SR_CHECK(dtype == SR_BF16, SR_EUNSUPPORTED, "sr_attention_pair: bf16 only");
+  SR_CHECK(d0->heads == d1->heads, SR_EINVAL, "sr_attention_pair: both problems need the same head count");
+  AttnPair p;
+  int rc = pair_args(*d0, p.a[0], "0");
+  if (rc != SR_OK) return rc;
+  rc = pair_args(*d1, p.a[1], "1");
+  if (rc != SR_OK) return rc;
+  p.nh = d0->heads;
+  p.nq[0] = (d0->lq + 255) / 256;
+  p.nq[1] = (d1->lq + 255) / 256;
+  const int nwg0 = p.nq[0] * p.nh;
+  p.nwg0p = (nwg0 + 7) / 8 * 8;
+  const int grid = p.nwg0p + p.nq[1] * p.nh;
+  hipLaunchKernelGGL((attn_bf16_pair_kernel<2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  return sr::check_launch("sr_attention_pair");
 }
 
 extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* desc) {

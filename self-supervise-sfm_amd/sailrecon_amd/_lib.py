@@ -93,6 +93,7 @@ _PROTOS = {
     "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
+    "sr_attention_pair": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnDesc)]),
     "sr_attention_bound_floats": (_i32, [ctypes.POINTER(AttnDesc)]),
     "sr_attn_merge_n": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "sr_attn_merge": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp]),

@@ -505,10 +505,37 @@ class Aggregator(nn.Module):
                          tag="gemm")
             self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
             work_kv = gather_rows(kv_all, kv_loc, [c * P for c in a_counts], group, r)
+        if G == 1 and self._paired_attention(pr, pg, dtype, Nq_l * P, q0 - a0, n_sub_all):
+            # G == 1, bf16: the global block's attention (anchors against themselves) and the split
+            # reloc block's subsample pass (queries against the anchor subsample) in ONE launch of the
+            # hand-scheduled sweep (sr_attention_pair), so that the reloc pass fills the CUs the global
+            # attention's last workgroup round leaves idle; then the reloc own-frame pass folds the
+            # subsample pass in, and both blocks' projection / MLP tails follow
+            rows, La = Nq_l * P, q0 - a0
+            n_full = n_sub_all // 64 * 64
+            runtime.run_block_head(pr, x, q0, q1, sc, runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
+            runtime.run_block_head(pg, x, a0, q0, sc, runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx))
+            qkv_r, qkv_g = sc.qkv[q0:q1], sc.qkv[a0:q0]
+            o_a, lse_a = ops.key_split_workspace(dev, 1, rows, C, pr.heads, name="reloc_split")
+            lse_a = lse_a[0]
+            ops.attention_pair(
+                dict(q=qkv_g[:, 0:C], k0=qkv_g[:, C:2 * C], v0=qkv_g[:, 2 * C:3 * C], o=sc.o[a0:q0], lq=La, l0=La,
+                     key_norm_max=runtime.key_norm_bound(pg)),
+                dict(q=qkv_r[:, 0:C], k0=kv_sub_all[:n_full, 0:C], v0=kv_sub_all[:n_full, C:2 * C], o=o_a, lq=rows,
+                     l0=n_full, key_norm_max=runtime.key_norm_bound(pr), lse=lse_a.view(-1)),
+                heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
+            self._reloc_own_pass(pr, qkv_r, kv_sub_all, sc.o[q0:q1], o_a, lse_a, Nq_l, P, n_sub_all, n_full)
+            runtime.run_block_tail(pr, x, q0, q1, sc)
+            runtime.run_block_tail(pg, x, a0, q0, sc)
+            return
         # G == 1: the reloc block (query rows) and the global block (anchor rows) are independent.
         # SR_CONCURRENT_STACKS=1 runs the reloc block on a side stream so that each could fill the
-        # other's last partial wave; measured 3% SLOWER at N=32 (68.7 -> 66.7 views/s: the two
-        # streams' kernels interfere more than the tails cost), so it is off by default.
+        # other's last partial wave.  Round 1: 3% SLOWER at N=32 (68.7 -> 66.7 views/s).  Round 3,
+        # with the one-workgroup-per-CU asm attention and the split reloc: 0.8 % faster (409.4 / 409.1
+        # vs 411.9 / 413.2 ms, one box, interleaved; C2 / C3 goldens pass), but the kernels of the two
+        # streams then overlap, so no per-kernel time (HIP events or rocprofv3) measures a kernel any
+        # more -- the roofline of the dominant kernel reads 0.40 instead of 0.50.  Off by default,
+        # so that the bench's roofline stays a measurement of the kernel.
         side = self._side_stream(dev) if (G == 1 and Nq_l > 0 and a0 < q0) else None
         if Nq_l > 0:
             def attend_reloc(qkv, o):
@@ -528,17 +555,7 @@ class Aggregator(nn.Module):
                                   o_a, heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows,
                                   q_bstride=0, l0=n_full, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
                                   lse=lse_a.view(-1), tail_readable=True)
-                    if n_full < n_sub_all:
-                        ops.attention(qkv[:, 0:C], kv_sub_all[n_full:, 0:C], kv_sub_all[n_full:, C:2 * C],
-                                      o, heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P,
-                                      q_bstride=P, l0=n_sub_all - n_full, k0_bstride=0, k1=qkv[:, C:2 * C],
-                                      v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                                      key_norm_max=kb, tail_readable=True, merge_o=o_a, merge_lse=lse_a)
-                    else:
-                        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o,
-                                      heads=pr.heads, head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=P,
-                                      k0_bstride=P, tag="attn_reloc", key_norm_max=kb, tail_readable=True,
-                                      merge_o=o_a, merge_lse=lse_a)
+                    self._reloc_own_pass(pr, qkv, kv_sub_all, o, o_a, lse_a, Nq_l, P, n_sub_all, n_full)
                     return
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
@@ -626,6 +643,35 @@ class Aggregator(nn.Module):
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
                           k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg))
+
+    @staticmethod
+    def _reloc_own_pass(pr, qkv, kv_sub_all, o, o_a, lse_a, nq: int, P: int, n_sub_all: int, n_full: int) -> None:
+        """Second pass of the split reloc attention: each query frame against the subsample's last
+        partial tile (shared segment 0) and itself (segment 1), folding the subsample pass's
+        (o_a, lse_a) in at its epilogue (sr_attn_desc.merge_o) -> o."""
+        C, kb = pr.dim, runtime.key_norm_bound(pr)
+        if n_full < n_sub_all:
+            ops.attention(qkv[:, 0:C], kv_sub_all[n_full:, 0:C], kv_sub_all[n_full:, C:2 * C], o, heads=pr.heads,
+                          head_dim=pr.head_dim, batch=nq, lq=P, q_bstride=P, l0=n_sub_all - n_full, k0_bstride=0,
+                          k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
+                          key_norm_max=kb, tail_readable=True, merge_o=o_a, merge_lse=lse_a)
+        else:
+            ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pr.heads, head_dim=pr.head_dim,
+                          batch=nq, lq=P, q_bstride=P, l0=P, k0_bstride=P, tag="attn_reloc", key_norm_max=kb,
+                          tail_readable=True, merge_o=o_a, merge_lse=lse_a)
+
+    def _paired_attention(self, pr, pg, dtype, rows: int, La: int, n_sub: int) -> bool:
+        """Single GPU, bf16, split reloc, a global query set that fills the chip without key
+        splitting: the global attention and the reloc subsample pass in one launch
+        (ops.attention_pair; SR_ATTN_PAIR=0 launches them apart)."""
+        if not self._split_reloc(dtype, rows, n_sub) or self.fp8_global or La <= 0 or pg.heads != pr.heads:
+            return False
+        if os.environ.get("SR_CONCURRENT_STACKS", "0") == "1":
+            return False
+        if ops.key_split_parts(dtype=dtype, batch=1, lq=La, heads=pg.heads, l0=La, l1=0, mask_mode=0) != 1:
+            return False
+        return (ops.pair_eligible(dtype, La, pg.head_dim, runtime.key_norm_bound(pg)) and
+                ops.pair_eligible(dtype, n_sub // 64 * 64, pr.head_dim, runtime.key_norm_bound(pr)))
 
     @staticmethod
     def _split_reloc(dtype, rows: int, n_sub: int) -> bool:

@@ -300,6 +300,43 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
                       (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)))
 
 
+def pair_eligible(dtype: torch.dtype, l0: int, head_dim: int, key_norm_max: float) -> bool:
+    """Whether a single-query-set attention may go into attention_pair (sr_attention_pair's
+    conditions: bf16, head_dim 64, whole 64-key tiles (>= 4), a static key bound; SR_ATTN_PAIR=0
+    turns pairing off)."""
+    return (_ATTN_PAIR and dtype == torch.bfloat16 and head_dim == 64 and l0 >= 256 and l0 % 64 == 0 and
+            key_norm_max > 0.0 and _ATTN_BOUND)
+
+
+_ATTN_PAIR = os.environ.get("SR_ATTN_PAIR", "1") != "0"
+
+
+def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional[str] = None) -> None:
+    """Two single-query-set bf16 attentions in ONE launch (sr_attention_pair): ``a`` / ``b`` are
+    dicts with q, k0, v0, o, lq, l0, key_norm_max and optionally lse (keys as attention()'s, batch
+    1, one segment).
+    a's workgroups run first and b's fill the CUs a's last round leaves idle.  Both must pass
+    pair_eligible (checked)."""
+    descs = []
+    flops = nbytes = 0.0
+    for p in (a, b):
+        if not pair_eligible(p["q"].dtype, p["l0"], head_dim, p["key_norm_max"]):
+            raise ValueError("attention_pair: a problem does not qualify (see pair_eligible)")
+        d = _attn_desc(p["q"], p["k0"], p["v0"], p["o"], heads=heads, head_dim=head_dim, batch=1, lq=p["lq"],
+                       q_bstride=0, l0=p["l0"], k0_bstride=0, lse=p.get("lse"))
+        d.key_norm_max = float(p["key_norm_max"])
+        descs.append(d)
+        flops += 4.0 * heads * p["lq"] * p["l0"] * head_dim
+        nbytes += p["q"].element_size() * heads * head_dim * (2 * p["lq"] + 2 * p["l0"])
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    rc = _lib.load().sr_attention_pair(_stream(a["q"]), dtype_code(a["q"].dtype), ctypes.byref(descs[0]),
+                                       ctypes.byref(descs[1]))
+    check(rc, "sr_attention_pair")
+    if timed:
+        TIMER.stop(tag, ev0, flops, nbytes)
+
+
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,
                       nbytes: float) -> None:
     if q.dtype == torch.bfloat16 and _ATTN_BOUND and key_norm_max > 0.0:

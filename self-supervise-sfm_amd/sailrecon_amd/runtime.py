@@ -228,6 +228,18 @@ def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
              tag="gemm")
 
 
+def run_block_head(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch, qkv_epi: Optional[dict]) -> None:
+    """First half of run_block (LN1 + the QKV GEMM) when the attention is launched separately
+    (the global and reloc blocks' attentions paired in one launch)."""
+    xs = x[r0:r1]
+    xn, qkv = sc.xn[r0:r1], sc.qkv[r0:r1]
+    ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, xn)
+    if qkv_epi is None:
+        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
+    else:
+        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
+
+
 def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch) -> None:
     """Second half of run_block (proj + residual, LN2, MLP + residual) when the attention
     output sc.o[r0:r1] was produced separately (frame-sharded global block)."""

@@ -92,6 +92,57 @@ def test_global_attention_production(ops, L):
     assert _rel(o[rows].float(), ref) < 1e-2
 
 
+def _kbound(k, heads=H):
+    return 1.01 * float(k.float().view(k.shape[0], heads, -1).norm(dim=-1).max())
+
+
+@pytest.mark.parametrize("case", ["C3", "padded"])
+def test_attention_pair(ops, case):
+    """sr_attention_pair (ops.attention_pair): the global block's attention and the split reloc's
+    subsample pass in ONE launch of the hand-scheduled sweep -- bit-identical to the two launches
+    apart (outputs and the second problem's LSE), and equal to fp64 on sampled rows.  'padded': 3
+    heads, so the first problem's 63 workgroups are padded to 64 (the padding workgroups exit)."""
+    if case == "C3":
+        heads, La, rows, nk = H, 32 * P, 32 * P, 32 * PP // 64 * 64
+        qg, kg, vg = _make(La, 11, spikes=(La - 5, 77))
+        qr, _, _ = _make(rows, 12)
+        _, ks, vs = _make(nk, 13, spikes=(nk - 1,))
+    else:
+        heads, La, rows, nk = 3, 21 * 256 - 128, 9 * 256 + 7, 40 * 64  # 21 q-tiles x 3 heads = 63 workgroups
+        g = torch.Generator(device=DEV).manual_seed(5)
+        mk = lambda n: (torch.randn(n, heads * D, device=DEV, generator=g) * 0.5).bfloat16()  # noqa: E731
+        qg, kg, vg, qr, ks, vs = mk(La), mk(La), mk(La), mk(rows), mk(nk), mk(nk)
+    cols = heads * D
+    kbg, kbr = _kbound(kg, heads), _kbound(ks, heads)
+    og, orr = (torch.empty(n, cols, device=DEV, dtype=torch.bfloat16) for n in (La, rows))
+    lse = torch.empty(heads, rows, device=DEV)
+    ops.attention_pair(dict(q=qg, k0=kg, v0=vg, o=og, lq=La, l0=La, key_norm_max=kbg),
+                       dict(q=qr, k0=ks, v0=vs, o=orr, lq=rows, l0=nk, key_norm_max=kbr, lse=lse.view(-1)),
+                       heads=heads, head_dim=D)
+    if case == "C3":  # apart, both launches take the same hand-scheduled sweep (2,752 workgroups each)
+        og1, or1 = torch.empty_like(og), torch.empty_like(orr)
+        lse1 = torch.empty_like(lse)
+        ops.attention(qg, kg, vg, og1, heads=heads, head_dim=D, batch=1, lq=La, q_bstride=0, l0=La, k0_bstride=0,
+                      key_norm_max=kbg)
+        ops.attention(qr, ks, vs, or1, heads=heads, head_dim=D, batch=1, lq=rows, q_bstride=0, l0=nk,
+                      k0_bstride=0, key_norm_max=kbr, lse=lse1.view(-1))
+        torch.cuda.synchronize()
+        assert torch.equal(og, og1) and torch.equal(orr, or1) and torch.equal(lse, lse1)
+    scale = D ** -0.5
+    for q_, k_, v_, o_, n in ((qg, kg, vg, og, La), (qr, ks, vs, orr, rows)):
+        rws = _sample_rows(n, 64, n).to(DEV)
+        ref = torch.empty(rws.numel(), cols, dtype=torch.float64, device=DEV)
+        for h in range(heads):
+            c = slice(h * D, (h + 1) * D)
+            sc = (q_[rws][:, c].double() @ k_[:, c].double().T) * scale
+            ref[:, c] = torch.softmax(sc, -1) @ v_[:, c].double()
+            if o_ is orr:  # the LSE (log2 domain) of the second problem; the kernel sums the bf16-rounded
+                # P that P.V uses (matrix-pipe row sums), 2^-9 relative per term: 1.5e-2 measured here
+                l2 = torch.logsumexp(sc, -1) / math.log(2.0)
+                assert float((lse[h, rws].double() - l2).abs().max()) < 3e-2
+        assert _rel(o_[rws].float(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("loose", [1.0, 3.0])
 @pytest.mark.parametrize("case", ["global-C3", "frame-C3"])
 def test_attention_static_key_bound(ops, case, loose):

@@ -19,5 +19,13 @@ case ${1:-} in
       run bench_cs1_$i 400 env SR_CONCURRENT_STACKS=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
     done
     run parity_conc 900 env SR_CONCURRENT_STACKS=1 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "c3 or c2" $T ;;
+  pair)
+    run pair_test 600 python -u -m pytest tests/test_baseline_shapes_gpu.py -x -q -m gpu -k "pair or split" $T
+    run kpair 300 python tools/kbench.py attn_pair
+    run parity_pair 900 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "c3 or c2" $T
+    for i in 1 2; do
+      run bench_pr0_$i 400 env SR_ATTN_PAIR=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+      run bench_pr1_$i 400 env SR_ATTN_PAIR=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+    done ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac

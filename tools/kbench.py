@@ -106,6 +106,35 @@ def attn():
           f"{fl / (ta + tbm) / 1e9:8.1f} TF/s")
 
 
+def attn_pair():
+    """C3 global attention + the split reloc's subsample pass: apart vs one sr_attention_pair launch."""
+    C, H, D, P, N = 1024, 16, 64, 1374, 32
+    L, nf = N * P, N * 305 // 64 * 64
+    qkv = torch.randn(L + 64, 3 * C, device=DEV, dtype=torch.bfloat16)[:L]
+    qr = torch.randn(L, C, device=DEV, dtype=torch.bfloat16)
+    kv = torch.randn(nf, 2 * C, device=DEV, dtype=torch.bfloat16)
+    og, oa = (torch.empty(L, C, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    lse = torch.empty(H, L, device=DEV)
+    kb = lambda k: 1.01 * float(k.float().view(-1, H, D).norm(dim=-1).max())  # noqa: E731
+    kbg, kbr = kb(qkv[:, C:2 * C]), kb(kv[:, :C])
+
+    def apart():
+        ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], og, heads=H, head_dim=D, batch=1, lq=L,
+                      q_bstride=0, l0=L, k0_bstride=0, key_norm_max=kbg)
+        ops.attention(qr, kv[:, :C], kv[:, C:], oa, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=nf,
+                      k0_bstride=0, key_norm_max=kbr, lse=lse.view(-1))
+
+    def paired():
+        ops.attention_pair(dict(q=qkv[:, :C], k0=qkv[:, C:2 * C], v0=qkv[:, 2 * C:], o=og, lq=L, l0=L, key_norm_max=kbg),
+                           dict(q=qr, k0=kv[:, :C], v0=kv[:, C:], o=oa, lq=L, l0=nf, key_norm_max=kbr,
+                                lse=lse.view(-1)), heads=H, head_dim=D)
+    fl = 4.0 * H * L * (L + nf) * D
+    for i in range(2):
+        ta, tp = timeit(apart, reps=5), timeit(paired, reps=5)
+        print(f"attn pair C3 global + reloc subsample: apart {ta:.3f} ms ({fl / ta / 1e9:.1f} TF/s), "
+              f"paired {tp:.3f} ms ({fl / tp / 1e9:.1f} TF/s)", flush=True)
+
+
 def attn_frame_diag():
     """Where the frame attention loses against the long sweep: the same launch with no ragged
     q-tile (lq = 1280 = 5 x 256), with full key tiles (l0 = 1408), and with 4x longer key sweeps
