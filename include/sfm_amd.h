@@ -99,6 +99,25 @@ typedef struct sr_gemm_epi {
 int sr_gemm(sr_stream_t stream, int dtype, int epilogue, const void* A, int64_t lda, const void* W,
             int64_t ldw, void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep);
 
+/* One problem of sr_gemm_group: the arguments of sr_gemm. */
+typedef struct sr_gemm_problem {
+  const void* A;
+  int64_t lda;
+  const void* W;
+  int64_t ldw;
+  void* out;
+  int64_t ldo;
+  int M, N, K;
+  sr_gemm_epi ep;
+} sr_gemm_problem;
+
+/* 1..4 independent bf16 GEMMs of one epilogue kind (BIAS, QKV, BIAS_GELU, BIAS_RESID; N % 256 == 0)
+ * in ONE launch of the 256x256 kernel, so that their last partial workgroup rounds merge (the
+ * layer's query, anchor and anchor-subsample QKV projections after a frame block).  Each problem
+ * exactly as sr_gemm would compute it.  Replaces the qkv nn.Linear calls of one layer's
+ * global_reloc and global blocks (attention.py:73; aggregator.py:672-769). */
+int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, const sr_gemm_problem* problems);
+
 /* Split-K form of sr_gemm for few rows and long K (the camera trunk: M = 2N views against
  * 2048 x 8192 weights, camera_head.py:163-168).  `splits` workgroup slices of K write fp32
  * partial tiles to `workspace` (>= splits * M * N floats, 16-B aligned, caller-owned; no

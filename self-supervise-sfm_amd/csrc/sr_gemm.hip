@@ -818,6 +818,31 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, g.sk_wgs > 0 ? g.sk_dp : nt), 0, g.ktiles, false);
 }
 
+// Up to 4 independent 256x256 GEMMs of one epilogue kind in ONE launch (sr_gemm_group): problem
+// p owns workgroups [start[p], start[p+1]), each range a multiple of 8 (padding workgroups exit) so
+// that the XCD remap within a problem keeps its tiles on one XCD as a launch of its own would.
+// The problems' last partial rounds merge: the layer's three QKV GEMMs after a frame block
+// (queries, anchors, anchor subsample: 2,064 + 2,064 + 312 tiles at C3) run in 18 rounds, not 20.
+constexpr int GROUP_MAX = 4;
+struct GemmGroup {
+  GemmArgs g[GROUP_MAX];
+  int start[GROUP_MAX + 1];
+  int n;
+};
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < GROUP_MAX; ++i) p += (i < gg.n && (int)blockIdx.x >= gg.start[i]) ? 1 : 0;
+  const GemmArgs& g = gg.g[p];
+  const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
+  const int lin = blockIdx.x - gg.start[p];
+  if (lin >= nt) return;  // padding
+  gemm256_tile<EPI>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, false);
+}
+
 // ---------------------------------------------------------------------------------------
 // 256x128 bf16 GEMM, TWO workgroups per CU ("pair"): the same 128x64 wave tile as gemm256_kernel
 // (acc[8][4], the same register epilogues), but 4 waves (2 M x 2 N) per workgroup and a 72 KiB
@@ -1162,9 +1187,8 @@ int launch_conv(const GemmArgs& a, hipStream_t s) {
 
 }  // namespace
 
-static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
-                       int64_t ldw, void* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,
-                       const sr_gemm_epi* ep) {
+static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda, const void* W, int64_t ldw,
+                     void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep) {
   SR_CHECK(A && W && out && ep, SR_EINVAL, "sr_gemm: null pointer");
   SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_gemm: bad dtype %d", dtype);
   SR_CHECK(M > 0 && N > 0 && K > 0, SR_EINVAL, "sr_gemm: bad shape M=%d N=%d K=%d", M, N, K);
@@ -1193,7 +1217,7 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
                    (ep->pos_yx || (ep->tokens_per_frame > ep->patch_start && ep->grid_w > 0)),
                SR_EINVAL, "sr_gemm: QKV rope params");
   }
-  GemmArgs a{};
+  a = GemmArgs{};
   a.A = (const char*)A;
   a.lda_b = lda * esz;
   a.W = (const char*)W;
@@ -1212,6 +1236,15 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
   a.ep = *ep;
   a.partial = nullptr;
   a.kt_per_split = a.ktiles;
+  return SR_OK;
+}
+
+static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,
+                       int64_t ldw, void* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,
+                       const sr_gemm_epi* ep) {
+  GemmArgs a;
+  const int rc = gemm_args(a, dtype, epi, A, lda, W, ldw, out, ldo, M, N, K, ep);
+  if (rc != SR_OK) return rc;
   hipStream_t s = (hipStream_t)stream;
   if (splits > 1) {
     SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID, SR_EUNSUPPORTED,
@@ -1231,6 +1264,39 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
     }
   }
   return dtype == SR_BF16 ? dispatch<bf16>(epi, a, s) : dispatch<float>(epi, a, s);
+}
+
+extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, const sr_gemm_problem* pr) {
+  SR_CHECK(pr && n >= 1 && n <= GROUP_MAX, SR_EINVAL, "sr_gemm_group: 1..%d problems (got %d)", GROUP_MAX, n);
+  SR_CHECK(dtype == SR_BF16, SR_EUNSUPPORTED, "sr_gemm_group: bf16 only");
+  SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_QKV || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID,
+           SR_EUNSUPPORTED, "sr_gemm_group: epilogue %d not supported", epi);
+  GemmGroup gg{};
+  gg.n = n;
+  gg.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const sr_gemm_problem& q = pr[i];
+    const int rc = gemm_args(gg.g[i], dtype, epi, q.A, q.lda, q.W, q.ldw, q.out, q.ldo, q.M, q.N, q.K, &q.ep);
+    if (rc != SR_OK) return rc;
+    SR_CHECK(q.N % BIG == 0, SR_EUNSUPPORTED, "sr_gemm_group: N=%d must be a multiple of %d", q.N, BIG);
+    GemmArgs& a = gg.g[i];
+    a.group_m = a.N >= 3072 ? 4 : 0;  // launch256's tile order
+    a.sk_dp = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
+    a.sk_wgs = 0;
+    gg.start[i + 1] = gg.start[i] + (a.sk_dp + 7) / 8 * 8;
+  }
+  for (int i = n + 1; i <= GROUP_MAX; ++i) gg.start[i] = gg.start[n];
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case SR_EPI_BIAS: hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS>), dim3(gg.start[n]), dim3(512), 0, s, gg); break;
+    case SR_EPI_QKV: hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_QKV>), dim3(gg.start[n]), dim3(512), 0, s, gg); break;
+    case SR_EPI_BIAS_GELU:
+      hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS_GELU>), dim3(gg.start[n]), dim3(512), 0, s, gg);
+      break;
+    default:
+      hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS_RESID>), dim3(gg.start[n]), dim3(512), 0, s, gg);
+  }
+  return sr::check_launch("sr_gemm_group");
 }
 
 extern "C" int sr_gemm(sr_stream_t stream, int dtype, int epi, const void* A, int64_t lda, const void* W,

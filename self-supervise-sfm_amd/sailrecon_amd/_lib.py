@@ -42,6 +42,13 @@ class GemmEpi(ctypes.Structure):
     ]
 
 
+class GemmProblem(ctypes.Structure):
+    _fields_ = [
+        ("A", _vp), ("lda", _i64), ("W", _vp), ("ldw", _i64), ("out", _vp), ("ldo", _i64),
+        ("M", _i32), ("N", _i32), ("K", _i32), ("ep", GemmEpi),
+    ]
+
+
 class AttnDesc(ctypes.Structure):
     _fields_ = [
         ("q", _vp), ("ldq", _i64),
@@ -94,6 +101,7 @@ _PROTOS = {
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_attention_pair": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnDesc)]),
+    "sr_gemm_group": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(GemmProblem)]),
     "sr_attention_bound_floats": (_i32, [ctypes.POINTER(AttnDesc)]),
     "sr_attn_merge_n": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "sr_attn_merge": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp]),

@@ -475,6 +475,10 @@ class Aggregator(nn.Module):
         n_sub = (q0 - a0) // P * Pp    # local anchor-subsample rows
         n_sub_all = sum(a_counts) * Pp
         work_sub, work_kv = [], []
+        paired = G == 1 and self._paired_attention(pr, pg, dtype, Nq_l * P, q0 - a0, n_sub_all)
+        # paired: the subsample K/V projection joins the queries' and anchors' QKV GEMMs in one
+        # grouped launch below (its LayerNorm still reads x here, before the global block updates it)
+        defer_kv = paired and cache_layer is None and need_sub
         if need_sub:
             # anchor-subsample K/V (reads x before the global block updates the anchors)
             xn_sub = ws.get("xn_sub", n_sub, C, dtype, dev)
@@ -484,7 +488,8 @@ class Aggregator(nn.Module):
             else:
                 kv_sub = kv_sub_all = ws.get("kv_sub", n_sub, 2 * C, dtype, dev)
             ops.layernorm(x, pr.ln1_w, pr.ln1_b, pr.eps, xn_sub, rowmap=rowmap, rows=n_sub)
-            self._kv_gemm(pr, xn_sub, kv_sub, rope, dict(pos_rowmap=rowmap, **posctx))
+            if not defer_kv:
+                self._kv_gemm(pr, xn_sub, kv_sub, rope, dict(pos_rowmap=rowmap, **posctx))
             if G > 1:
                 work_sub = gather_rows(kv_sub_all, kv_sub, [c * Pp for c in a_counts], group, r)
             if cache_layer is not None:  # two-phase reloc: every anchor's subsample K|V of this layer
@@ -505,16 +510,33 @@ class Aggregator(nn.Module):
                          tag="gemm")
             self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
             work_kv = gather_rows(kv_all, kv_loc, [c * P for c in a_counts], group, r)
-        if G == 1 and self._paired_attention(pr, pg, dtype, Nq_l * P, q0 - a0, n_sub_all):
-            # G == 1, bf16: the global block's attention (anchors against themselves) and the split
-            # reloc block's subsample pass (queries against the anchor subsample) in ONE launch of the
-            # hand-scheduled sweep (sr_attention_pair), so that the reloc pass fills the CUs the global
-            # attention's last workgroup round leaves idle; then the reloc own-frame pass folds the
-            # subsample pass in, and both blocks' projection / MLP tails follow
+        if paired:
+            # G == 1, bf16: the queries' and anchors' QKV projections (and the anchor-subsample K/V
+            # one) as ONE grouped GEMM launch, then the global block's attention (anchors against
+            # themselves) and the split reloc block's subsample pass (queries against the anchor
+            # subsample) in ONE launch of the hand-scheduled sweep (sr_attention_pair): each time the
+            # second problem fills the CUs the first one's last workgroup round leaves idle; then the
+            # reloc own-frame pass folds the subsample pass in, and both blocks' tails follow
             rows, La = Nq_l * P, q0 - a0
             n_full = n_sub_all // 64 * 64
-            runtime.run_block_head(pr, x, q0, q1, sc, runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
-            runtime.run_block_head(pg, x, a0, q0, sc, runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx))
+            epi_r = runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx)
+            epi_g = runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx)
+            epi_s = runtime.qkv_params(pr, rope, pos_rowmap=rowmap, **posctx) if defer_kv else None
+            if epi_s is not None:
+                epi_s["col_offset"] = C
+            probs = [dict(a=sc.xn[q0:q1], w=pr.w_qkv, out=sc.qkv[q0:q1], bias=pr.b_qkv, qkv=epi_r),
+                     dict(a=sc.xn[a0:q0], w=pg.w_qkv, out=sc.qkv[a0:q0], bias=pg.b_qkv, qkv=epi_g)]
+            if defer_kv:
+                probs.append(dict(a=xn_sub, w=pr.w_qkv[C:], out=kv_sub_all, bias=_sl(pr.b_qkv, C, 3 * C), qkv=epi_s))
+            if all(p_["qkv"] is not None for p_ in probs) and ops.gemm_group_eligible(probs):
+                ops.layernorm(x[q0:q1], pr.ln1_w, pr.ln1_b, pr.eps, sc.xn[q0:q1])
+                ops.layernorm(x[a0:q0], pg.ln1_w, pg.ln1_b, pg.eps, sc.xn[a0:q0])
+                ops.gemm_group(probs, _lib.SR_EPI_QKV, tag="gemm")
+            else:
+                runtime.run_block_head(pr, x, q0, q1, sc, epi_r)
+                runtime.run_block_head(pg, x, a0, q0, sc, epi_g)
+                if defer_kv:
+                    self._kv_gemm(pr, xn_sub, kv_sub_all, rope, dict(pos_rowmap=rowmap, **posctx))
             qkv_r, qkv_g = sc.qkv[q0:q1], sc.qkv[a0:q0]
             o_a, lse_a = ops.key_split_workspace(dev, 1, rows, C, pr.heads, name="reloc_split")
             lse_a = lse_a[0]

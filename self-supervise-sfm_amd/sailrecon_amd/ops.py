@@ -200,6 +200,49 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         TIMER.stop(tag, ev0, 2.0 * M * N * K, nb)
 
 
+GEMM_GROUP_MAX = 4
+_GEMM_GROUP = os.environ.get("SR_GEMM_GROUP", "1") != "0"
+
+
+def gemm_group_eligible(problems) -> bool:
+    """Whether gemm_group can take these problems (bf16, N % 256 == 0, 1..4 of them; SR_GEMM_GROUP=0
+    turns grouping off)."""
+    return (_GEMM_GROUP and 1 <= len(problems) <= GEMM_GROUP_MAX and
+            all(p["a"].dtype == torch.bfloat16 and p["w"].shape[0] % 256 == 0 for p in problems))
+
+
+def gemm_group(problems, epi: int, tag: Optional[str] = None) -> None:
+    """Several independent gemm() calls of one epilogue kind in ONE launch of the 256x256 kernel
+    (sr_gemm_group): each problem a dict with a, w, out and gemm()'s bias / gamma / qkv keywords;
+    their last partial workgroup rounds merge."""
+    if not gemm_group_eligible(problems):
+        raise ValueError("gemm_group: bf16 problems with N % 256 == 0, at most 4")
+    arr = (_lib.GemmProblem * len(problems))()
+    flops = nbytes = 0.0
+    for i, p in enumerate(problems):
+        a, w, out = p["a"], p["w"], p["out"]
+        N, K = w.shape
+        if a.shape[1] != K or a.dtype != w.dtype:
+            raise ValueError("gemm_group: a / w shapes or dtypes differ")
+        q = arr[i]
+        q.A, q.lda, q.W, q.ldw = _p(a), _rowmajor(a, "a"), _p(w), _rowmajor(w, "w")
+        q.out, q.ldo = _p(out), _rowmajor(out, "out")
+        q.M, q.N, q.K = a.shape[0], N, K
+        q.ep.bias, q.ep.gamma = _p(p.get("bias")), _p(p.get("gamma"))
+        if p.get("qkv") is not None:
+            _fill_qkv_epi(q.ep, p["qkv"])
+        flops += 2.0 * a.shape[0] * N * K
+        nbytes += (a.shape[0] * K + N * K) * a.element_size() + a.shape[0] * N * out.element_size()
+    if tag == "gemm":
+        tag = f"gemm_{_EPI_NAME.get(epi, epi)}"
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    rc = _lib.load().sr_gemm_group(_stream(problems[0]["a"]), dtype_code(torch.bfloat16), epi, len(problems), arr)
+    check(rc, "sr_gemm_group")
+    if timed:
+        TIMER.stop(tag, ev0, flops, nbytes)
+
+
 # fixed-offset softmax sweep (sr_attn_desc.key_bound); SR_ATTN_BOUND=0 keeps the per-tile row max
 _ATTN_BOUND = os.environ.get("SR_ATTN_BOUND", "1") != "0"
 # key-split attention: SR_ATTN_KSPLIT=0 disables it, =S forces S chunks where they divide the keys

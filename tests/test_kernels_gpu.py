@@ -437,3 +437,46 @@ def test_small_fp32_ops(ops):
     ops.pose_decode(enc[0].to(DEV), (224, 300), ext, intr)
     re, ri = pose_encoding_to_extri_intri(enc, (224, 300))
     assert rel(ext.cpu(), re[0]) < 1e-6 and rel(intr.cpu(), ri[0]) < 1e-6
+
+
+@pytest.mark.parametrize("epi_name", ["QKV", "BIAS", "BIAS_RESID"])
+def test_gemm_group(ops, epi_name):
+    """sr_gemm_group: 3 independent bf16 GEMMs of one epilogue in ONE 256x256 launch (different M
+    and N, one problem's workgroup count not a multiple of 8) are bit-identical to the same
+    problems launched apart on the 256x256 kernel (>= 512 tiles each) -- and, QKV, the layer's
+    query / anchor / subsample-K|V projections with the qk-LayerNorm + RoPE epilogue."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    L = _lib()
+    epi = getattr(L, "SR_EPI_" + epi_name)
+    C, H, D, P, gw = 1024, 16, 64, 21, 4
+    g = torch.Generator(device=DEV).manual_seed(3)
+    rope = RotaryPositionEmbedding2D(100).tables(D, 5, DEV)
+    probs, plain = [], []
+    # (rows, N): 2,064 / 516 / 552 tiles of 256x256, all >= 512 (the 256x256 kernel when apart); 516 is
+    # not a multiple of 8 (4 padding workgroups); ragged last row tiles in the second and third
+    for i, (M, N) in enumerate(((172 * 256, 3072), (43 * 256 - 100, 3072), (69 * 256 - 5, 2048))):
+        a = torch.randn(M, C, device=DEV, generator=g).bfloat16()
+        w = (torch.randn(3 * C, C, device=DEV, generator=g) / 32).bfloat16()[3 * C - N:]
+        b = torch.randn(N, device=DEV, generator=g)
+        gm = torch.randn(N, device=DEV, generator=g)
+        p = dict(a=a, w=w, bias=b)
+        if epi_name == "QKV":
+            qn = [torch.randn(D, device=DEV, generator=g) for _ in range(4)]
+            p["qkv"] = dict(embed_dim=C, head_dim=D, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
+                            rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=P, patch_start=5, grid_w=gw,
+                            pos_row_base=7 * i, col_offset=3 * C - N)
+        if epi_name == "BIAS_RESID":
+            p["gamma"] = gm
+            x0 = torch.randn(M, N, device=DEV, generator=g)
+            p["out"], ref_out = x0.clone(), x0.clone()
+        else:
+            p["out"] = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ref_out = torch.empty_like(p["out"])
+        probs.append(p)
+        plain.append(ref_out)
+    ops.gemm_group(probs, epi)
+    for p, ref_out in zip(probs, plain):
+        ops.gemm(p["a"], p["w"], ref_out, epi, bias=p["bias"], gamma=p.get("gamma"), qkv=p.get("qkv"), splits=1)
+    torch.cuda.synchronize()
+    for p, ref_out in zip(probs, plain):
+        assert torch.equal(p["out"], ref_out)

@@ -27,5 +27,12 @@ case ${1:-} in
       run bench_pr0_$i 400 env SR_ATTN_PAIR=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
       run bench_pr1_$i 400 env SR_ATTN_PAIR=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
     done ;;
+  group)
+    run group_test 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_baseline_shapes_gpu.py -x -q -m gpu -k "group or pair" $T
+    run parity_group 900 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "c3 or c2" $T
+    for i in 1 2; do
+      run bench_gg0_$i 400 env SR_GEMM_GROUP=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+      run bench_gg1_$i 400 env SR_GEMM_GROUP=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+    done ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac
