@@ -71,15 +71,17 @@ constexpr float RESCALE_LOG2 = 8.f;
 #ifndef SR_ATTN_DEFAULT_CFG
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
-// One workgroup's work: q-tile qt of (head, item) against every key of the item's segments.
+// One workgroup's work: the NW*32*QB query rows from row0 of (head, item) against every key of
+// the item's segments.
+template <int NW> constexpr int attn_nbuf() { return NW >= 4 ? 4 : 2; }  // K/V ring stages
+
 template <int NW, int QB, int KIND, bool PIPE>
-__device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int qt, const int head, const int item) {
+__device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int row0, const int head, const int item,
+                                               char* smem) {
   static_assert(!PIPE || (NW == 4 && QB == 2), "the pipelined sweep pairs the two q-blocks of a wave");
-  constexpr int QROWS = NW * 32 * QB;
-  constexpr int NBUF = NW >= 4 ? 4 : 2;  // K/V ring stages
+  constexpr int NBUF = attn_nbuf<NW>();
   constexpr int LOOK = NBUF - 1;         // stages issued ahead
   constexpr int DPW = 16 / NW;  // LDS-DMA wave-instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE_B];
   const sr_attn_desc& d = args.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hcol = head * 64;
@@ -153,8 +155,8 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int q
   // ---- Q fragments (B operand of S^T = K Q^T): lane holds c*Q[row][16s + 8hi .. +8], with
   // c = scale*log2(e) folded in so that the MFMA chain yields scores in the exp2 domain
   const float c = d.scale * 1.4426950408889634f;
-  const int qrow0 = qt * QROWS + wave * 32 * QB + l32;  // q-block b: row qrow0 + 32b
-  const bool wave_active = qt * QROWS + wave_u * 32 * QB < d.lq;
+  const int qrow0 = row0 + wave * 32 * QB + l32;  // q-block b: row qrow0 + 32b
+  const bool wave_active = row0 + wave_u * 32 * QB < d.lq;
   bf16x8 qf[QB][4];
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
@@ -586,6 +588,8 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
   //   frame: the 6 q-tiles of a (frame, head) share its 350 KB K/V (3.5x -> ~1x HBM traffic);
   //   global_reloc: head-major, every query frame of a head reads the same anchor-subsample
   //   K/V (segment 0, 2.5 MB per head at C3).
+  constexpr int QROWS = NW * 32 * QB;
+  __shared__ __attribute__((aligned(16))) char smem[attn_nbuf<NW>() * STAGE_B];
   const int nq = gridDim.x, nh = gridDim.y, nb = gridDim.z;
   const int lin = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
   const int tile = sr::xcd_remap(lin, nq * nh * nb);
@@ -598,7 +602,7 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
     head = (tile / nq) % nh;
     item = tile / (nq * nh);
   }
-  attn_bf16_body<NW, QB, KIND, PIPE>(args, qt, head, item);
+  attn_bf16_body<NW, QB, KIND, PIPE>(args, qt * QROWS, head, item, smem);
 }
 
 // Two single-query-set problems of the hand-scheduled sweep in ONE launch (sr_attention_pair):
@@ -620,7 +624,8 @@ __global__ __launch_bounds__(256, 1) void attn_bf16_pair_kernel(AttnPair p) {
   const int nq = p.nq[sel], nwg = nq * p.nh;
   if (lin >= nwg) return;  // problem 0's padding
   const int tile = sr::xcd_remap(lin, nwg);
-  attn_bf16_body<4, 2, KIND, true>(p.a[sel], tile % nq, tile / nq, 0);
+  __shared__ __attribute__((aligned(16))) char smem[attn_nbuf<4>() * STAGE_B];
+  attn_bf16_body<4, 2, KIND, true>(p.a[sel], (tile % nq) * 256, tile / nq, 0, smem);
 }
 
 // ------------------------------------------------------------------ fp8 Q.K^T (BASELINE C5)
@@ -1445,7 +1450,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   SR_CHECK(d.mask_mode == SR_MASK_NONE || (d.mask_mode == SR_MASK_CAMERA && d.l1 == 0) ||
                ((d.mask_mode == SR_MASK_DENSE || d.mask_mode == SR_MASK_ADD) && d.mask && d.mask_ld >= 0),
            SR_EINVAL, "sr_attention: bad mask_mode %d (or mask / mask_ld)", d.mask_mode);
-  AttnArgs a;
+  AttnArgs a{};
   a.d = d;
   hipStream_t s = (hipStream_t)stream;
   SR_CHECK(!d.merge_o || (dtype == SR_BF16 && d.merge_lse && d.merge_rows > 0 && d.ld_merge_o % 4 == 0 &&
@@ -1630,7 +1635,7 @@ extern "C" int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* desc, co
            "sr_attention_qk8: head_dim 64, one key segment, no mask");
   SR_CHECK(ldq8 % 16 == 0 && ldk8 % 16 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0, SR_EINVAL,
            "sr_attention_qk8: leading dims (fp8 rows 16-B aligned, bf16 multiples of 8)");
-  AttnArgs a;
+  AttnArgs a{};
   a.d = d;
   a.ntile0 = (d.l0 + KT - 1) / KT;
   a.ntile1 = 0;
@@ -1671,7 +1676,7 @@ extern "C" int sr_attention_qkv8(sr_stream_t stream, const sr_attn_desc* desc, c
   SR_CHECK(d.head_dim == 64 && d.l1 == 0 && d.mask_mode == SR_MASK_NONE && !d.merge_o, SR_EUNSUPPORTED,
            "sr_attention_qkv8: head_dim 64, one key segment, no mask");
   SR_CHECK(ldq8 % 16 == 0 && ldk8 % 16 == 0 && d.ldo % 4 == 0, SR_EINVAL, "sr_attention_qkv8: leading dims");
-  AttnArgs a;
+  AttnArgs a{};
   a.d = d;
   a.ntile0 = (d.l0 + KT - 1) / KT;
   a.ntile1 = 0;

@@ -146,6 +146,95 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs g) {
       }
 }
 
+// The same G = A^T B over 256 (n) x 256 (k) output tiles: 8 waves as 2 (n) x 4 (k), each 128 x 64 =
+// 4 x 2 tiles of v_mfma_f32_32x32x16_bf16 (128 accumulator VGPRs), one workgroup per CU (128 KiB of
+// LDS: two 64 KiB stages of eight 64-row x 64-col sub-tiles, A columns n0.. in sub-tiles 0-3 and B
+// columns k0.. in 4-7, one per wave, same swizzle and transposed reads as wgrad_kernel).  Half the
+// staged bytes per FLOP of the 128 x 128 tile; the reduction over M splits into gridDim.y slices
+// whose fp32 partials wgrad_reduce_kernel sums.
+constexpr int WT2 = 256;
+constexpr int WSTAGE2 = 8 * SUB;  // 64 KiB
+
+__global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * WSTAGE2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int ntk = g.K / WT2, ntiles = (g.N / WT2) * ntk;
+  const int tile = sr::xcd_remap(blockIdx.x, ntiles);
+  const int tn = tile / ntk, tk = tile - tn * ntk;
+  const int n0 = tn * WT2, k0 = tk * WT2;
+
+  // wave w fills sub-tile w (0-3: A columns n0 + 64w; 4-7: B columns k0 + 64(w-4)), 8 DMAs of 8 rows
+  const char* base = wave < 4 ? g.A + (int64_t)(n0 + 64 * wave) * 2 : g.B + (int64_t)(k0 + 64 * (wave - 4)) * 2;
+  const int64_t ld = wave < 4 ? g.lda_b : g.ldb_b;
+  const int rsub = lane >> 3, slot = lane & 7;
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * SUB);
+  auto stage = [&](int mt, int buf) {
+    const uint32_t db = dst0 + buf * WSTAGE2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 8 * i + rsub;
+      const int chunk = slot ^ (((r >> 1) & 1) << 2);
+      const int row = min(mt * 64 + r, g.M - 1);
+      sr::dma16(base + (int64_t)row * ld + chunk * 16, db + i * 1024);
+    }
+  };
+
+  const int wr = wave >> 2, wc = wave & 3;
+  const TrOff tro = tr_offsets(lane);
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int mt0 = blockIdx.y * g.mt_per_split;
+  const int mt1 = min(mt0 + g.mt_per_split, g.mtiles);
+  if (mt0 < mt1) stage(mt0, 0);
+  for (int mt = mt0; mt < mt1; ++mt) {
+    const int buf = (mt - mt0) & 1;
+    sr::wait_vmcnt0();   // this wave's part of stage mt landed
+    sr::barrier_raw();   // ... every wave's; every wave is done reading the other buffer
+    if (mt + 1 < mt1) stage(mt + 1, buf ^ 1);
+    char* sb = smem + buf * WSTAGE2;
+    const int valid = g.M - mt * 64;
+    if (valid < 64) {  // ragged last m-tile: zero the clamped rows (uniform branch)
+      for (int e = tid; e < 8 * 64 * 8; e += 512) {
+        const int st = e >> 9, r = (e >> 3) & 63, c = e & 7;
+        if (r >= valid) *(uint4*)(sb + st * SUB + r * 128 + c * 16) = uint4{0u, 0u, 0u, 0u};
+      }
+      __syncthreads();
+    }
+    const char* tb = sb + (4 + wc) * SUB;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = tr_frag(sb + (2 * wr + (i >> 1)) * SUB, 16 * s, tro.off[i & 1]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = tr_frag(tb, 16 * s, tro.off[j]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // lane: column k = k0 + 64 wc + 32 j + l32, rows n = n0 + 128 wr + 32 i + acc_row(e, hi)
+  float* part = g.part + (int64_t)blockIdx.y * g.N * g.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + 128 * wr + 32 * i + acc_row(e, hi), k = k0 + 64 * wc + 32 * j + l32;
+        part[(int64_t)n * g.K + k] = acc[i][j][e];
+      }
+}
+
 // per output row n (one workgroup): slices summed in order, then scale / accumulate / rowdot
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int N, int K,
                                                            float* dW, int64_t lddw, int accumulate,
@@ -784,7 +873,15 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   g.mt_per_split = (g.mtiles + splits - 1) / splits;
   splits = (g.mtiles + g.mt_per_split - 1) / g.mt_per_split;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wgrad_kernel, dim3((N / WT) * (K / WT), splits), dim3(256), 0, s, g);
+  // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
+  static const bool big = [] {
+    const char* e = getenv("SR_WGRAD256");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (big && N % WT2 == 0 && K % WT2 == 0)
+    hipLaunchKernelGGL(wgrad256_kernel, dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL(wgrad_kernel, dim3((N / WT) * (K / WT), splits), dim3(256), 0, s, g);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, workspace, splits, N, K, dW, lddw, accumulate,
                      rowscale, wdot, ldwd, rowdot);
   return sr::check_launch("sr_gemm_wgrad");

@@ -860,11 +860,19 @@ def _train_ws(device, name: str, numel: int) -> Tensor:
     return ws
 
 
+_WGRAD256 = os.environ.get("SR_WGRAD256", "1") != "0"
+
+
 def _wgrad_splits(M: int, N: int, K: int) -> int:
-    """Reduction slices so that the 128x128-tile grid has >= 512 workgroups (2 per CU) while
-    every slice keeps >= 8 m-tiles of 64 rows; the fp32 partials stay <= 16x the output."""
-    tiles = (N // 128) * (K // 128)
+    """Reduction slices.  256x256 tiles (sr_gemm_wgrad's one-workgroup-per-CU kernel when N and K
+    are multiples of 256): the most slices that still fit one round of 256 workgroups, each slice
+    >= 8 m-tiles of 64 rows, at most 16.  128x128 tiles: >= 512 workgroups (2 per CU), powers of 2;
+    the fp32 partials stay <= 16x the output."""
     mt = -(-M // 64)
+    if _WGRAD256 and N % 256 == 0 and K % 256 == 0:
+        tiles = (N // 256) * (K // 256)
+        return max(1, min(256 // tiles, 16, mt // 8))
+    tiles = (N // 128) * (K // 128)
     s = 1
     while tiles * s < 512 and mt // (2 * s) >= 8 and 2 * s <= 16:
         s *= 2

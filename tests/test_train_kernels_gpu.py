@@ -35,8 +35,11 @@ def L():
     return _lib
 
 
+# N, K multiples of 256 run the 256 x 256 kernel (wgrad256_kernel), the others the 128 x 128 one
 @pytest.mark.parametrize("M,N,K,splits", [(64, 128, 128, 1), (1000, 256, 384, 1), (4397, 384, 256, 3),
-                                          (43968 // 8, 1024, 1024, None), (130, 3072, 128, 2)])
+                                          (43968 // 8, 1024, 1024, None), (130, 3072, 128, 2),
+                                          (4397, 512, 256, 3), (200, 256, 256, 1), (21984, 3072, 1024, None),
+                                          (43968, 1024, 4096, None)])
 def test_gemm_wgrad(ops, M, N, K, splits):
     torch.manual_seed(0)
     dy = torch.randn(M, N, device=DEV).bfloat16()
@@ -47,11 +50,12 @@ def test_gemm_wgrad(ops, M, N, K, splits):
     assert rel(dw, ref) < 1e-5
 
 
-def test_gemm_wgrad_strided_accumulate_rowscale_rowdot(ops):
+@pytest.mark.parametrize("K", [128, 256])
+def test_gemm_wgrad_strided_accumulate_rowscale_rowdot(ops, K):
     """Row-strided operands (column slices of wider buffers), accumulate, per-row scale
     (LayerScale gamma folded into dW) and rowdot (the gamma gradient)."""
     torch.manual_seed(1)
-    M, N, K = 777, 256, 128
+    M, N = 777, 256
     big_dy = torch.randn(M, N + 128, device=DEV).bfloat16()
     big_x = torch.randn(M, 3 * K, device=DEV).bfloat16()
     dy, x = big_dy[:, 128:], big_x[:, K:2 * K]

@@ -34,15 +34,11 @@ case ${1:-} in
       run bench_gg0_$i 400 env SR_GEMM_GROUP=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
       run bench_gg1_$i 400 env SR_GEMM_GROUP=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
     done ;;
-  half)
-    run half_test 600 python -u -m pytest tests/test_baseline_shapes_gpu.py tests/test_kernels_gpu.py -x -q -m gpu -k "frame or reloc or attention" $T
+  wgrad)
+    run wgrad_test 600 python -u -m pytest tests/test_train_kernels_gpu.py tests/test_train_block_gpu.py -x -q -m gpu $T
     for i in 1 2; do
-      run kattn_ht0_$i 300 env SR_ATTN_HALF_TAIL=0 python tools/kbench.py attn
-      run kattn_ht1_$i 300 env SR_ATTN_HALF_TAIL=1 python tools/kbench.py attn
-    done
-    for i in 1 2; do
-      run bench_ht0_$i 400 env SR_ATTN_HALF_TAIL=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
-      run bench_ht1_$i 400 env SR_ATTN_HALF_TAIL=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+      run ktrain_w0_$i 600 env SR_WGRAD256=0 python tools/kbench.py train
+      run ktrain_w1_$i 600 env SR_WGRAD256=1 python tools/kbench.py train
     done ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac
