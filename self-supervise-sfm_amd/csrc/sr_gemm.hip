@@ -44,10 +44,6 @@ struct GemmArgs {
   int kt_per_split;  // split-K (gemm_kernel, gridDim.y slices): k-tiles per slice
   float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
   int group_m;       // 256x256 kernels: tile order in groups of group_m row tiles (<= 1: row-major)
-  // 256x256 RESID kernels, stream-K tail: the first sk_dp tiles run data-parallel (whole rounds);
-  // sk_wgs > 0 workgroups split the remaining tiles' k-iterations evenly and add their partial
-  // products with fp32 atomics (the residual update is linear in the accumulator)
-  int sk_dp, sk_wgs;
   sr_gemm_epi ep;
   // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
   // (n, yo, xo) of the NHWC fp32 input x [n][H][W][C], A column k = (ky, kx, ci) — exactly
@@ -354,32 +350,6 @@ __device__ __forceinline__ void resid_full(const GemmArgs& g, f32x4 (&acc)[8][4]
   }
 }
 
-// Stream-K piece of a RESID tile: x += gamma * (acc (+ bias)) as fp32 atomics (no read of x;
-// the pieces of one tile add in any order).  Vector atomics (global_atomic_add_f32), rows < M.
-__device__ __forceinline__ void resid_atomic(const GemmArgs& g, f32x4 (&acc)[8][4], int rowbase, int colw, int lr,
-                                             int lg, bool with_bias) {
-  const sr_gemm_epi& ep = g.ep;
-  f32x4 gm[4], bs[4];
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int col = colw + ni * 16 + 4 * lg;
-    gm[ni] = *(const f32x4*)(ep.gamma + col);
-    bs[ni] = with_bias && ep.bias ? *(const f32x4*)(ep.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int row = rowbase + mi * 16 + lr;
-    if (row >= g.M) continue;
-    float* xr = (float*)g.out + (int64_t)row * g.ldo + colw + 4 * lg;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const f32x4 v = (acc[mi][ni] + bs[ni]) * gm[ni];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) unsafeAtomicAdd(xr + ni * 16 + r, v[r]);
-    }
-  }
-}
-
 // bias (+ erf-GELU) -> bf16 for a full 256x256 tile (every row < M; N % 256 == 0 here; no aux):
 // the guarded produce/emit form compiles to an exec branch around every one of the 32 stores
 // per lane; here they are plain stores with the math of the next vectors in between.
@@ -646,11 +616,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
 constexpr int BIG = 256;
 constexpr int STAGE_BIG = 2 * BIG * ROWB;  // 64 KiB
 
-// One output tile over k-tiles [kb, ke).  sk_part: a stream-K piece of a RESID tile, whose
-// x += gamma * (acc (+ bias on the piece holding k-tile 0)) goes out as fp32 atomics.
+// One output tile over k-tiles [kb, ke).
 template <int EPI>
-__device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke,
-                                             bool sk_part) {
+__device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = g.N / BIG, ntm = (g.M + BIG - 1) / BIG;
   int tm, tn;
@@ -773,10 +741,6 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
     }
   }
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
-    if (sk_part) {
-      resid_atomic(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg, kb == 0);
-      return;
-    }
     if (m0 + BIG <= g.M && !g.lds_epi) {
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
       return;
@@ -796,26 +760,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
-  if constexpr (EPI == SR_EPI_BIAS_RESID) {
-    if (g.sk_wgs > 0 && (int)blockIdx.x >= g.sk_dp) {
-      // stream-K: workgroup j takes k-iterations [j*per, (j+1)*per) of the tail tiles, one
-      // contiguous run per tile it touches (at most a few), each with its own atomic epilogue
-      const int j = blockIdx.x - g.sk_dp;
-      const int total = (nt - g.sk_dp) * g.ktiles;
-      const int per = (total + g.sk_wgs - 1) / g.sk_wgs;
-      int it = j * per;
-      const int end = min(total, it + per);
-      while (it < end) {
-        const int tl = it / g.ktiles, k0 = it - tl * g.ktiles;
-        const int k1 = min(g.ktiles, k0 + (end - it));
-        gemm256_tile<EPI>(g, smem, g.sk_dp + tl, k0, k1, true);
-        it += k1 - k0;
-        if (it < end) sr::barrier_raw();  // every wave done with the LDS stages before the next run
-      }
-      return;
-    }
-  }
-  gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, g.sk_wgs > 0 ? g.sk_dp : nt), 0, g.ktiles, false);
+  gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles);
 }
 
 // Up to 4 independent 256x256 GEMMs of one epilogue kind in ONE launch (sr_gemm_group): problem
@@ -840,144 +785,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
   const int lin = blockIdx.x - gg.start[p];
   if (lin >= nt) return;  // padding
-  gemm256_tile<EPI>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, false);
+  gemm256_tile<EPI>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles);
 }
 
-// ---------------------------------------------------------------------------------------
-// 256x128 bf16 GEMM, TWO workgroups per CU ("pair"): the same 128x64 wave tile as gemm256_kernel
-// (acc[8][4], the same register epilogues), but 4 waves (2 M x 2 N) per workgroup and a 72 KiB
-// LDS ring (3 stages of 32-deep k-tiles, 64-B rows: A 256 rows | W 128 rows), so two workgroups
-// share a CU and one's epilogue (the stores and the residual read-modify-write) runs beside the
-// other's MFMAs -- the per-CU epilogue serialisation that caps the 256x256 kernel (DESIGN.md GEMM).
-//   * LDS rows of 64 B = 4 16-B chunks; chunk c of row r sits at c ^ ((r >> 2) & 3): a b128 read
-//     of 16 rows x 1 chunk touches 64 distinct banks; the LDS-DMA pieces (16 rows x 64 B) fetch
-//     the source chunk (l & 3) ^ ((l >> 4) & 3) for lane l, the same for every piece;
-//   * per k-tile each wave stages 4 A pieces (rows 64w..) and 2 W pieces (rows 32w..); tile kt+2
-//     goes out right after the barrier of tile kt (3-stage ring), the wait is vmcnt(6);
-//   * 32 MFMAs (16x16x32) per wave per k-tile in 4 quadrant phases, fragments of the next
-//     quadrant read before the current one's cluster.
-constexpr int PBM = 256, PBN = 128, PKT = 32, PROWB = 64;
-constexpr int PSTAGE = (PBM + PBN) * PROWB;  // 24 KiB
-constexpr int PNBUF = 3;
-
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_pair_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[PNBUF * PSTAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = g.N / PBN, ntm = (g.M + PBM - 1) / PBM;
-  const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
-  int tm, tn;
-  if (g.group_m > 1) {
-    const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
-    const int gm = min(g.group_m, ntm - first), r = tile - grp * per;
-    tm = first + r % gm;
-    tn = r / gm;
-  } else {
-    tm = tile / ntn;
-    tn = tile - tm * ntn;
-  }
-  const int m0 = tm * PBM, n0 = tn * PBN;
-  const int ktiles = g.K / PKT;
-
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int csrc = (lane & 3) ^ ((lane >> 4) & 3);
-  const uint32_t voA = (uint32_t)((lane >> 2) * g.lda_b + csrc * 16);
-  const uint32_t voW = (uint32_t)((lane >> 2) * g.ldw_b + csrc * 16);
-  const int arow0 = m0 + wave_u * 64;  // this wave's first staged A row
-  const bool ragged = m0 + PBM > g.M;
-  const char* const sA = g.A + (int64_t)min(arow0, g.M - 1) * g.lda_b;
-  const char* const sW = g.W + (int64_t)(n0 + wave_u * 32) * g.ldw_b;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem));
-  const uint32_t dA = lds0 + wave_u * 64 * PROWB, dW = lds0 + (PBM + wave_u * 32) * PROWB;
-  auto stage = [&](int kt) {
-    const uint32_t sb = (uint32_t)((kt % PNBUF) * PSTAGE);
-    const int64_t ko = (int64_t)kt * PKT * 2;
-    if (!ragged) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) sr::dma16_s(sA + ko + (int64_t)j * 16 * g.lda_b, voA, dA + sb + j * 1024);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = min(arow0 + 16 * j + (lane >> 2), g.M - 1);
-        sr::dma16(g.A + (int64_t)r * g.lda_b + ko + csrc * 16, dA + sb + j * 1024);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) sr::dma16_s(sW + ko + (int64_t)j * 16 * g.ldw_b, voW, dW + sb + j * 1024);
-  };
-
-  const int wr = wave >> 1, wc = wave & 1;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int coff = ((lg ^ ((lr >> 2) & 3)) << 4);
-  const int arow = (wr * 128 + lr) * PROWB + coff;        // + (qm*64 + mi*16) * PROWB
-  const int brow = (PBM + wc * 64 + lr) * PROWB + coff;   // + (qn*32 + ni*16) * PROWB
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0);
-  if (ktiles > 1) stage(1);
-  for (int kt = 0; kt < ktiles; ++kt) {
-    if (kt + 1 < ktiles) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile kt landed, kt+1 in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    sr::barrier_raw();  // every wave's pieces of tile kt; everyone done with tile kt-1's stage
-    if (kt + 2 < ktiles) stage(kt + 2);
-    const char* sb = smem + (kt % PNBUF) * PSTAGE;
-    uint4 aX[4], aY[4], bX[2], bY[2];
-    auto load_a = [&](uint4 (&a)[4], int qm) {
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + arow + (qm * 64 + mi * 16) * PROWB);
-    };
-    auto load_b = [&](uint4 (&b)[2], int qn) {
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) b[ni] = *(const uint4*)(sb + brow + (qn * 32 + ni * 16) * PROWB);
-    };
-    auto mma = [&](const uint4 (&a)[4], const uint4 (&b)[2], int qm, int qn) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni], a[mi], acc[qm * 4 + mi][qn * 2 + ni]);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    load_a(aX, 0);
-    load_b(bX, 0);
-    load_b(bY, 1);
-    mma(aX, bX, 0, 0);
-    load_a(aY, 1);
-    mma(aX, bY, 0, 1);
-    mma(aY, bY, 1, 1);
-    mma(aY, bX, 1, 0);
-  }
-  if constexpr (EPI == SR_EPI_BIAS_RESID) {
-    if (m0 + PBM <= g.M) {
-      resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-      return;
-    }
-  }
-  if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
-    if (m0 + PBM <= g.M && !g.ep.aux) {
-      bias_full<EPI>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-      return;
-    }
-  }
-  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-}
-
-template <int EPI>
-int launch_pair(GemmArgs a, hipStream_t s) {
-  const int nwg = (a.N / PBN) * ((a.M + PBM - 1) / PBM);
-  static const int group_m = [] {
-    const char* e = getenv("SR_GEMM_GROUP_M");
-    return e ? atoi(e) : -1;
-  }();
-  a.group_m = group_m >= 0 ? group_m : (a.N >= 3072 ? 4 : 0);
-  hipLaunchKernelGGL((gemm_pair_kernel<EPI>), dim3(nwg), dim3(256), 0, s, a);
-  return sr::check_launch("sr_gemm(pair)");
-}
 
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
@@ -990,32 +800,7 @@ int launch256(GemmArgs a, hipStream_t s) {
     return e ? atoi(e) : -1;
   }();
   a.group_m = group_m >= 0 ? group_m : (a.N >= 3072 ? 4 : 0);
-  a.sk_dp = nwg;
-  a.sk_wgs = 0;
-  int grid = nwg;
-  if constexpr (EPI == SR_EPI_BIAS_RESID) {
-    // stream-K tail, opt-in (SR_GEMM_SK=1): whole rounds stay data-parallel; a last round that
-    // fills less than ~85 % of the CUs is split over every CU by k-iterations (>= 4 per piece).
-    // Correct (test_gemm256_tiles) but much slower: the pieces' fp32 atomics cost more than the
-    // idle CUs of the tail (kbench, same box: proj M=87,936 0.50 vs 0.30 ms, fc2 0.88 vs 0.72,
-    // proj M=43,968 0.42 vs 0.14) -- see DESIGN.md "GEMM" for why a fixup pass would not pay either
-    static const int sk_mode = [] {
-      const char* e = getenv("SR_GEMM_SK");
-      return e ? atoi(e) : 0;
-    }();
-    static const int cus = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        n = 256;
-      return n > 0 ? n : 256;
-    }();
-    const int tail = nwg % cus;
-    if (sk_mode && nwg > cus && tail > 0 && tail * 100 < cus * 85) {
-      a.sk_dp = nwg - tail;
-      a.sk_wgs = std::min(cus, tail * a.ktiles / 4);
-      grid = a.sk_dp + a.sk_wgs;
-    }
-  }
+  const int grid = nwg;
   hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
   return sr::check_launch("sr_gemm(256)");
 }
@@ -1040,21 +825,6 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
     // 256x256 tiles (one WG per CU) only when they still give >= 2 WGs per CU; smaller
     // problems (frame-sharded ranks, small scenes) keep 4x more 128x128 workgroups.
     const long tiles256 = (long)(a.N / BIG) * ((a.M + BIG - 1) / BIG);
-    // 256x128 tiles, two workgroups per CU (SR_GEMM_PAIR=1; A/B against the 256x256 kernel)
-    static const bool pair = [] {
-      const char* e = getenv("SR_GEMM_PAIR");
-      return e ? atoi(e) != 0 : false;
-    }();
-    if (pair && !no_big && a.N % BIG == 0 && a.K % PKT == 0 && tiles256 >= 512 && epi != SR_EPI_PATCH &&
-        epi != SR_EPI_GELU_BWD) {
-      switch (epi) {
-        case SR_EPI_BIAS: return launch_pair<SR_EPI_BIAS>(a, s);
-        case SR_EPI_BIAS_GELU: return launch_pair<SR_EPI_BIAS_GELU>(a, s);
-        case SR_EPI_BIAS_RESID: return launch_pair<SR_EPI_BIAS_RESID>(a, s);
-        case SR_EPI_QKV: return launch_pair<SR_EPI_QKV>(a, s);
-        case SR_EPI_F32: return launch_pair<SR_EPI_F32>(a, s);
-      }
-    }
     if (!no_big && a.N % BIG == 0 && tiles256 >= 512) {
       switch (epi) {
         case SR_EPI_BIAS: return launch256<SR_EPI_BIAS>(a, s);
@@ -1281,9 +1051,8 @@ extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, cons
     SR_CHECK(q.N % BIG == 0, SR_EUNSUPPORTED, "sr_gemm_group: N=%d must be a multiple of %d", q.N, BIG);
     GemmArgs& a = gg.g[i];
     a.group_m = a.N >= 3072 ? 4 : 0;  // launch256's tile order
-    a.sk_dp = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
-    a.sk_wgs = 0;
-    gg.start[i + 1] = gg.start[i] + (a.sk_dp + 7) / 8 * 8;
+    const int nt = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
+    gg.start[i + 1] = gg.start[i] + (nt + 7) / 8 * 8;
   }
   for (int i = n + 1; i <= GROUP_MAX; ++i) gg.start[i] = gg.start[n];
   hipStream_t s = (hipStream_t)stream;

@@ -76,45 +76,6 @@ def test_gemm256_tiles(ops, M, N, K):
     assert rel(x[32:32 + M] - x0[32:32 + M], ref * gam) < 1e-5
 
 
-_OPT_IN_GEMM = (
-    "import math, torch, sys\n"
-    "import torch.nn.functional as F\n"
-    "sys.path.insert(0, 'self-supervise-sfm_amd')\n"
-    "from sailrecon_amd import ops, _lib as L\n"
-    "def rel(a, b): return float((a.double() - b.double()).norm() / b.double().norm())\n"
-    "for M, N, K in [(8300, 4096, 128), (33000, 1024, 192), (32769, 1024, 64), (87936, 1024, 1024), (43968, 1024, 4096)]:\n"
-    "    g = torch.Generator().manual_seed(M + N)\n"
-    "    a = torch.randn(M, K, generator=g).cuda().bfloat16()\n"
-    "    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).cuda().bfloat16()\n"
-    "    b, gam = torch.randn(N, generator=g).cuda(), torch.randn(N, generator=g).cuda()\n"
-    "    ref = a.float() @ w.float().t() + b\n"
-    "    if EPIS != ('resid',):\n"
-    "        out = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)\n"
-    "        ops.gemm(a, w, out, L.SR_EPI_BIAS, bias=b); e = rel(out.float(), ref); assert e < 8e-3, (M, N, K, e)\n"
-    "        ops.gemm(a, w, out, L.SR_EPI_BIAS_GELU, bias=b); e = rel(out.float(), F.gelu(ref)); assert e < 8e-3, (M, N, K, e)\n"
-    "    x = torch.randn(M + 64, N, device='cuda'); x0 = x.clone()\n"
-    "    ops.gemm(a, w, x[32:32 + M], L.SR_EPI_BIAS_RESID, bias=b, gamma=gam)\n"
-    "    assert torch.equal(x[:32], x0[:32]) and torch.equal(x[32 + M:], x0[32 + M:])\n"
-    "    e = rel(x[32:32 + M] - x0[32:32 + M], ref * gam); print(M, N, K, e); assert e < 1e-5, (M, N, K, e)\n")
-
-
-@pytest.mark.parametrize("env,epis", [("SR_GEMM_SK", "('resid',)"), ("SR_GEMM_PAIR", "('bias', 'gelu', 'resid')")],
-                         ids=["streamk", "pair"])
-def test_gemm256_opt_in_variants(ops, env, epis):
-    """The opt-in 256-kernel variants (switches read once per process: run in a subprocess):
-    SR_GEMM_SK=1, RESID's stream-K tail (a last round under ~85 % of the CUs split by k-iterations,
-    fp32 atomics; 8300 / 33000 / 32769 rows give pieces spanning 2-4 tiles, the C3 frame / global
-    proj and fc2 shapes 6- and 11-iteration pieces); SR_GEMM_PAIR=1, the 256x128 two-workgroups-
-    per-CU kernel with the BIAS / GELU / RESID epilogues, ragged last row tiles included."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", f"EPIS = {epis}\n" + _OPT_IN_GEMM], env=dict(os.environ, **{env: "1"}),
-                       cwd=root, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-
-
 @pytest.mark.parametrize("dtype,tol", DT)
 @pytest.mark.parametrize("M,N,K,splits", [(64, 2048, 2048, None), (64, 1024, 8192, None), (37, 256, 1024, 4)])
 def test_gemm_splitk(ops, dtype, tol, M, N, K, splits):

@@ -48,20 +48,11 @@ for step in "$@"; do
                 run kgemm_256_$i 300 python tools/kbench.py gemm || exit 1
                 run kgemm_128_$i 300 env SR_GEMM_NO256=1 python tools/kbench.py gemm || exit 1
               done ;;
-    gemm_pair_tests) run gemm_pair_tests 600 env SR_GEMM_PAIR=1 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm" --timeout 300 --timeout-method thread ;;
-    kgemm_pair) for i in 1 2; do
-                run kgemm_p0_$i 300 env SR_GEMM_PAIR=0 python tools/kbench.py gemm gemm_rank || exit 1
-                run kgemm_p1_$i 300 env SR_GEMM_PAIR=1 python tools/kbench.py gemm gemm_rank || exit 1
-              done ;;
     reloc_split_ab) for i in 1 2; do
                 run bench_rs0_$i 400 env SR_RELOC_SPLIT=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
                 run bench_rs1_$i 400 env SR_RELOC_SPLIT=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
               done ;;
     parity_c3) run parity_c3 900 python -u -m pytest tests/test_parity_gpu.py -x -v -m gpu -k "c3 or c2" --timeout 600 --timeout-method thread ;;
-    kgemm_sk) for i in 1 2; do
-                run kgemm_sk0_$i 300 env SR_GEMM_SK=0 python tools/kbench.py gemm gemm_rank || exit 1
-                run kgemm_sk1_$i 300 env SR_GEMM_SK=1 python tools/kbench.py gemm gemm_rank || exit 1
-              done ;;
     kgemm_reg) run kgemm_reg 300 env SR_GEMM_REG_EPI=1 python tools/kbench.py gemm ;;
     kdpt)    run kdpt 600 python tools/kbench.py dpt ;;
     kreloc)  run kreloc 600 python tools/kbench.py reloc ;;
@@ -100,7 +91,6 @@ for step in "$@"; do
                 run bench_rl0_$i 400 env SR_FUSED_RESID_LN=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
                 run bench_rl1_$i 400 env SR_FUSED_RESID_LN=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
               done ;;
-    kln)     run kln 300 python tools/kbench.py ln ;;
     kln)     run kln 300 python tools/kbench.py ln ;;
     kgemm_var) for i in 1 2; do
                  run kgemm_v0_$i 300 python tools/kbench.py gemm || exit 1
