@@ -121,8 +121,8 @@ int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, const sr_gemm_p
 /* Split-K form of sr_gemm for few rows and long K (the camera trunk: M = 2N views against
  * 2048 x 8192 weights, camera_head.py:163-168).  `splits` workgroup slices of K write fp32
  * partial tiles to `workspace` (>= splits * M * N floats, 16-B aligned, caller-owned; no
- * allocation inside), then one reduction applies the epilogue.  Epilogues BIAS, BIAS_GELU
- * and BIAS_RESID; deterministic (fixed summation order).  K/splits must be a multiple of
+ * allocation inside), then one reduction applies the epilogue.  Epilogues BIAS, BIAS_GELU,
+ * BIAS_RESID and F32 (the camera trunk's dgrad); deterministic (fixed summation order).  K/splits must be a multiple of
  * the k-tile (64 bf16 | 32 f32). */
 int sr_gemm_splitk(sr_stream_t stream, int dtype, int epilogue, const void* A, int64_t lda, const void* W,
                    int64_t ldw, void* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,

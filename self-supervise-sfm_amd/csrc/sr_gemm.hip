@@ -454,25 +454,32 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4
   }
 }
 
-template <typename T, int EPI, bool CONV = false>
+// TBM x TBN output tile, 4 waves of 64 x 64 (128 x 128 as 2 x 2; few-row problems, M <= 64, as
+// 64 x 256 = 1 x 4, so that no wave computes padding rows: the camera trunk's fp32 GEMMs at M = 2N)
+template <typename T, int EPI, bool CONV = false, int TBM = BM, int TBN = BN>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  static_assert(TBM % 64 == 0 && TBN % 64 == 0 && (TBM / 64) * (TBN / 64) == 4, "4 waves of 64 x 64");
+  static_assert(!CONV || (TBM == 128 && TBN == 128), "the implicit conv stages A with waves 0-1");
+  constexpr int STAGE = (TBM + TBN) * ROWB;
+  constexpr int NPW = (TBM + TBN) / 32;  // LDS-DMA pieces (8 rows of 128 B) per wave per stage
+  constexpr int WC = TBN / 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;  // N % 4 == 0; last column tile ragged
+  const int ntn = (g.N + TBN - 1) / TBN, ntm = (g.M + TBM - 1) / TBM;  // N % 4 == 0; last column tile ragged
   const int tile = sr::xcd_remap(blockIdx.x, ntn * ntm);
   const int tm = tile / ntn, tn = tile - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * TBM, n0 = tn * TBN;
 
-  // LDS-DMA sources: instruction i of wave w fills tile rows (w*8+i)*8 .. +8 (rows < BM: A, else W).
-  const char* src[8];
+  // LDS-DMA sources: instruction i of wave w fills tile rows (w*NPW+i)*8 .. +8 (rows < TBM: A, else W).
+  const char* src[NPW];
   // CONV: A rows come from the 3x3 window of output pixel m (waves 0-1 stage A, 2-3 stage W)
   const bool a_wave = __builtin_amdgcn_readfirstlane(wave) < 2;
-  int cy[8], cx[8];  // CONV: window top-left (yo*s - 1, xo*s - 1) of this lane's pixel per piece
+  int cy[NPW], cx[NPW];  // CONV: window top-left (yo*s - 1, xo*s - 1) of this lane's pixel per piece
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int tr = (wave * 8 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < NPW; ++i) {
+    const int tr = (wave * NPW + i) * 8 + (lane >> 3);
     const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
-    if (tr < BM) {
+    if (tr < TBM) {
       const int r = min(m0 + tr, g.M - 1);
       if constexpr (CONV) {
         const int hw = g.conv.Ho * g.conv.Wo;
@@ -485,13 +492,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
         src[i] = g.A + (int64_t)r * g.lda_b + chunk * 16;
       }
     } else {
-      const int r = min(n0 + tr - BM, g.N - 1);  // ragged last column tile: re-read the last W row
+      const int r = min(n0 + tr - TBM, g.N - 1);  // ragged last column tile: re-read the last W row
       src[i] = g.W + (int64_t)r * g.ldw_b + chunk * 16;
     }
   }
-  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * NPW * 1024);
   auto stage = [&](int kt, int buf) {
-    const uint32_t base = dst0 + buf * STAGE_BYTES;
+    const uint32_t base = dst0 + buf * STAGE;
     if (CONV && a_wave) {
       // k-tile kt = 32 channels [ci0, ci0 + 32) of tap (ky, kx): C % 32 == 0, no tile straddles taps
       const int k0 = kt * 32, tap = k0 / g.conv.C, ci0 = k0 - tap * g.conv.C;
@@ -505,11 +512,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
+      for (int i = 0; i < NPW; ++i) sr::dma16(src[i] + (int64_t)kt * ROWB, base + i * 1024);
     }
   };
 
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WC, wc = wave % WC;
   const int lr = lane & 15, lg = lane >> 4;
   const int swz = lr >> 1;  // (row>>1)&7 for every fragment row of this lane
   f32x4 acc[4][4];
@@ -526,12 +533,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
     const int buf = (kt - kt0) & 1;
     if (kt + 1 < kt1) {
       stage(kt + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     sr::barrier_raw();
-    const char* sb = smem + buf * STAGE_BYTES;
+    const char* sb = smem + buf * STAGE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int coff = (((ks * 4 + lg) ^ swz) * 16);
@@ -539,7 +546,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) a[mi] = *(const uint4*)(sb + (wr * 64 + mi * 16 + lr) * ROWB + coff);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) b[ni] = *(const uint4*)(sb + (BM + wc * 64 + ni * 16 + lr) * ROWB + coff);
+      for (int ni = 0; ni < 4; ++ni) b[ni] = *(const uint4*)(sb + (TBM + wc * 64 + ni * 16 + lr) * ROWB + coff);
       if constexpr (CONV) {
         if (g.conv.relu) {  // the RCU's ReLU on the conv input (zero padding stays zero)
 #pragma unroll
@@ -595,6 +602,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
     f32x4* xp = (f32x4*)((float*)g.out + (int64_t)row * g.ldo + col);
     *xp += v * *(const f32x4*)(g.ep.gamma + col);
+  } else if constexpr (EPI == SR_EPI_F32) {  // fp32 output whatever the operand type
+    *(f32x4*)((float*)g.out + (int64_t)row * g.ldo + col) = v;
   } else if constexpr (sr::is_bf16<T>::value) {
     const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
     *(bf16x4*)((T*)g.out + (int64_t)row * g.ldo + col) = o;
@@ -807,9 +816,20 @@ int launch256(GemmArgs a, hipStream_t s) {
 
 template <typename T, int EPI>
 int launch(const GemmArgs& a, hipStream_t s) {
-  const int nwg = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
   const int slices = a.partial ? (a.ktiles + a.kt_per_split - 1) / a.kt_per_split : 1;
-  hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
+  // few rows (the camera trunk, M = 2N views): 64 x 256 tiles, no padding rows computed
+  // (SR_GEMM_SMALLM=0: 128 x 128)
+  static const bool small_m = [] {
+    const char* e = getenv("SR_GEMM_SMALLM");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (small_m && a.M <= 64 && a.N > 128) {
+    const int nwg = (a.N + 255) / 256;
+    hipLaunchKernelGGL((gemm_kernel<T, EPI, false, 64, 256>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
+  } else {
+    const int nwg = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
+    hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
+  }
   if (a.partial) {
     const int64_t nq = (int64_t)a.M * (a.N / 4);
     hipLaunchKernelGGL((splitk_reduce_kernel<T, EPI>), dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, a,
@@ -1017,8 +1037,8 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
   if (rc != SR_OK) return rc;
   hipStream_t s = (hipStream_t)stream;
   if (splits > 1) {
-    SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID, SR_EUNSUPPORTED,
-             "sr_gemm_splitk: epilogue %d not supported", epi);
+    SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID || epi == SR_EPI_F32,
+             SR_EUNSUPPORTED, "sr_gemm_splitk: epilogue %d not supported", epi);
     SR_CHECK(workspace && ((uintptr_t)workspace % 16) == 0 && ((uintptr_t)out % 16) == 0 && ldo % 4 == 0 && N % 4 == 0,
              SR_EINVAL, "sr_gemm_splitk: workspace / out must be 16-B aligned");
     SR_CHECK(a.ktiles % splits == 0, SR_EUNSUPPORTED, "sr_gemm_splitk: %d k-tiles not divisible into %d slices",
@@ -1029,6 +1049,7 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
       case SR_EPI_BIAS: return dtype == SR_BF16 ? launch<bf16, SR_EPI_BIAS>(a, s) : launch<float, SR_EPI_BIAS>(a, s);
       case SR_EPI_BIAS_GELU:
         return dtype == SR_BF16 ? launch<bf16, SR_EPI_BIAS_GELU>(a, s) : launch<float, SR_EPI_BIAS_GELU>(a, s);
+      case SR_EPI_F32: return dtype == SR_BF16 ? launch<bf16, SR_EPI_F32>(a, s) : launch<float, SR_EPI_F32>(a, s);
       default:
         return dtype == SR_BF16 ? launch<bf16, SR_EPI_BIAS_RESID>(a, s) : launch<float, SR_EPI_BIAS_RESID>(a, s);
     }

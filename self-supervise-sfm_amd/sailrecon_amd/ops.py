@@ -97,13 +97,17 @@ def _rowmajor(t: Tensor, name: str) -> int:
 _SPLITK_WS = {}  # (device, stream) -> fp32 workspace of sr_gemm_splitk
 
 
+_GEMM_SMALLM = os.environ.get("SR_GEMM_SMALLM", "1") != "0"
+
+
 def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
     """K slices for few-row GEMMs (the camera trunk, M = 2N views): enough 128x128-tile
     workgroups to spread the weight stream over the CUs; 1 = plain sr_gemm."""
-    if M > 256 or epi not in (_lib.SR_EPI_BIAS, _lib.SR_EPI_BIAS_GELU, _lib.SR_EPI_BIAS_RESID):
+    if M > 256 or epi not in (_lib.SR_EPI_BIAS, _lib.SR_EPI_BIAS_GELU, _lib.SR_EPI_BIAS_RESID, _lib.SR_EPI_F32):
         return 1
     ktiles = K // (64 if dtype == torch.bfloat16 else 32)
-    wgs = -(-M // 128) * (N // 128)
+    # sr_gemm's tiles: 64 x 256 for M <= 64 (SR_GEMM_SMALLM), else 128 x 128
+    wgs = -(-N // 256) if (M <= 64 and N > 128 and _GEMM_SMALLM) else -(-M // 128) * (N // 128)
     cap = max(1, K // (4 * M))  # partial-tile traffic (2 * splits * M * N) <= half the weight stream (N * K)
     splits = 1
     while (wgs * splits * 2 <= 1024 and splits * 2 <= cap and ktiles % (splits * 2) == 0

@@ -96,6 +96,9 @@ def test_gemm_splitk(ops, dtype, tol, M, N, K, splits):
     x0 = x.clone()
     ops.gemm(a, w, x, L.SR_EPI_BIAS_RESID, bias=b, gamma=gam, splits=splits)
     assert rel(x - x0, ref * gam) < max(tol, 1e-5)
+    o32 = torch.empty(M, N + 4, device=DEV)[:, :N]  # F32: fp32 output for either operand type (dgrad)
+    ops.gemm(a, w, o32, L.SR_EPI_F32, bias=b, splits=splits)
+    assert rel(o32, ref) < max(tol, 1e-5)
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-5)])

@@ -40,5 +40,18 @@ case ${1:-} in
       run ktrain_w0_$i 600 env SR_WGRAD256=0 python tools/kbench.py train
       run ktrain_w1_$i 600 env SR_WGRAD256=1 python tools/kbench.py train
     done ;;
+  evidence)
+    run pmc_pair1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_pair1 -o run --output-format csv -- python3 tools/kbench.py attn_pair
+    run pmc_pair2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_pair2 -o run --output-format csv -- python3 tools/kbench.py attn_pair
+    run ktrain 900 python tools/kbench.py train
+    run prof_train 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/kbench.py train ;;
+  smallm)
+    run smallm_test 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_layers_gpu.py -x -q -m gpu -k "gemm or camera or block" $T
+    run parity_smallm 900 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu $T
+    for i in 1 2; do
+      run bench_sm0_$i 400 env SR_GEMM_SMALLM=0 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+      run bench_sm1_$i 400 env SR_GEMM_SMALLM=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
+    done
+    run ktrain 900 python tools/kbench.py train ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac
