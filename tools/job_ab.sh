@@ -53,5 +53,18 @@ case ${1:-} in
       run bench_sm1_$i 400 env SR_GEMM_SMALLM=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline
     done
     run ktrain 900 python tools/kbench.py train ;;
+  final)
+    run gputests 1200 python -u -m pytest tests -x -q -m gpu $T
+    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+    run bench 600 python bench.py
+    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing
+    run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
+      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing
+    run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
+      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing
+    run pmc_pair1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_pair1 -o run --output-format csv -- python3 tools/kbench.py attn_pair
+    run pmc_pair2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_pair2 -o run --output-format csv -- python3 tools/kbench.py attn_pair
+    run prof_train 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/kbench.py train ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac
