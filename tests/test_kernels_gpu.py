@@ -36,8 +36,10 @@ DT = [(torch.float32, 2e-6), (torch.bfloat16, 8e-3)]
 
 
 @pytest.mark.parametrize("dtype,tol", DT)
+# M <= 64 and N > 128 take the few-row 64 x 256 tiles (ragged N included)
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 256, 1024), (1374, 384, 128), (77, 3072, 1024),
-                                   (2500, 512, 256), (4100, 1024, 1024), (2048, 256, 4096)])
+                                   (2500, 512, 256), (4100, 1024, 1024), (2048, 256, 4096),
+                                   (64, 388, 256), (9, 2052, 128), (40, 200, 64)])
 def test_gemm_bias_gelu(ops, dtype, tol, M, N, K):
     L = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
