@@ -182,6 +182,49 @@ def attn_rank():
         ops._KSPLIT_ENV = saved
 
 
+def attn_rank_seg():
+    """attn_rank's key-split launches (auto S) with the chunks' tails readable: the compiled sweep
+    vs the hand-scheduled _SEG sweep (SR_ATTN_PIPE_SEG=1), which masks each chunk's ragged last
+    key tile (43,968 / S keys are not whole 64-key tiles for S = 2, 4, 8)."""
+    C, H, D, P, N = 1024, 16, 64, 1374, 32
+    L = N * P
+    qkv = torch.randn(L + 64, 3 * C, device=DEV, dtype=torch.bfloat16)[:L]
+    kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())
+    for G in (2, 4, 8):
+        lq = L // G
+        S = ops.key_split_parts(dtype=torch.bfloat16, batch=1, lq=lq, heads=H, l0=L, l1=0, mask_mode=0)
+        o_parts, lse_parts = ops.key_split_workspace(qkv.device, S, lq, C, H)
+        chunk = L // S
+        d = ops._attn_desc(qkv[:lq, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o_parts, heads=H, head_dim=D, batch=S,
+                           lq=lq, q_bstride=0, l0=chunk, k0_bstride=chunk, lse=lse_parts)
+        d.o_bstride = lq
+        d.key_norm_max = kb
+        d.tail_rows_readable = 64
+        fl = 4.0 * H * lq * L * D
+
+        def f():
+            ops.check(_lib.load().sr_attention(ops._stream(qkv), ops.dtype_code(qkv.dtype), ops.ctypes.byref(d)),
+                      "sr_attention")
+        res = {}
+        for seg in ("0", "1", "0", "1"):
+            os.environ["SR_ATTN_PIPE_SEG"] = seg
+            ms = timeit(f, reps=10)
+            res.setdefault(seg, []).append(ms)
+        outs = []
+        for seg in ("0", "1"):
+            os.environ["SR_ATTN_PIPE_SEG"] = seg
+            o_parts.zero_()
+            f()
+            torch.cuda.synchronize()
+            outs.append((o_parts[:S * lq].float().clone(), lse_parts.clone()))
+        os.environ.pop("SR_ATTN_PIPE_SEG")
+        print(f"attn rank seg G={G} max |o| diff {float((outs[0][0] - outs[1][0]).abs().max()):.3e} "
+              f"max |lse| diff {float((outs[0][1] - outs[1][1]).abs().max()):.3e}")
+        for seg, v in res.items():
+            print(f"attn rank seg G={G} S={S} chunk={chunk} pipe_seg={seg} "
+                  + " ".join(f"{m:7.3f} ms ({fl / m / 1e9:7.1f} TF/s)" for m in v))
+
+
 def attn_rank_small():
     """Per-rank reloc (32/G query frames x [9760 shared subsample + own 1374]) and frame
     (64/G frames x 1374) attention of the frame-sharded C3 forward, G = 1, 2, 4, 8."""
