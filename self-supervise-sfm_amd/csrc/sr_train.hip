@@ -363,20 +363,25 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
       dws[i * VEC + j] = 0.f;
       dbs[i * VEC + j] = 0.f;
     }
-  for (int row = gw; row < rows; row += nw) {
-    const int64_t xr = rowmap ? (int64_t)rowmap[row] : row;
-    float v[NPL], g[NPL];
+  // Two rows per wave per iteration, and the dx each adds into loaded with x and dy: all loads of
+  // both rows are in flight before the first reduction (one memory latency per two rows, not two
+  // per row -- 1,024 waves alone do not cover HBM latency).
+  auto load = [&](int64_t xr, int row, float* v, float* g, float* a) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int col = (i * 64 + lane) * VEC;
       const float* xp = x + xr * ldx + col;
       const TD* gp = dy + (int64_t)row * lddy + col;
+      const float* ap = dx + xr * lddx + col;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         v[i * VEC + j] = xp[j];
         g[i * VEC + j] = sr::to_f32(gp[j]);
+        if constexpr (NPL <= 32) a[i * VEC + j] = ap[j];
       }
     }
+  };
+  auto finish = [&](int64_t xr, int row, float* v, float* g, const float* a) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NPL; ++i) s += v[i];
@@ -407,7 +412,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
       float* dp = dx + xr * lddx + col;
       float o[VEC];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) o[j] = dp[j] + rstd * (g[i * VEC + j] - mg - v[i * VEC + j] * mgx);
+      for (int j = 0; j < VEC; ++j)
+        o[j] = (NPL <= 32 ? a[i * VEC + j] : dp[j]) + rstd * (g[i * VEC + j] - mg - v[i * VEC + j] * mgx);
       if constexpr (VEC == 4) {
         *(float4*)dp = make_float4(o[0], o[1], o[2], o[3]);
         if (dxb) *(bf16x4*)(dxb + (int64_t)row * lddxb + col) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
@@ -420,6 +426,24 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
         }
       }
     }
+  };
+  if constexpr (NPL > 32) {  // 4,096 columns: one row per iteration, dx read late (register file)
+    for (int row = gw; row < rows; row += nw) {
+      const int64_t xr = rowmap ? (int64_t)rowmap[row] : row;
+      float v[NPL], g[NPL];
+      load(xr, row, v, g, nullptr);
+      finish(xr, row, v, g, nullptr);
+    }
+  } else for (int row = gw; row < rows; row += 2 * nw) {
+    const int rowb = row + nw;
+    const bool has_b = rowb < rows;  // wave-uniform
+    const int64_t xa = rowmap ? (int64_t)rowmap[row] : row;
+    const int64_t xb = has_b ? (rowmap ? (int64_t)rowmap[rowb] : rowb) : xa;
+    float va[NPL], ga[NPL], aa[NPL], vb[NPL], gb[NPL], ab[NPL];
+    load(xa, row, va, ga, aa);
+    load(xb, has_b ? rowb : row, vb, gb, ab);
+    finish(xa, row, va, ga, aa);
+    if (has_b) finish(xb, rowb, vb, gb, ab);
   }
   if (want_params) {
     float* pw = part + (int64_t)gw * 2 * COLS;

@@ -66,5 +66,14 @@ case ${1:-} in
     run pmc_pair1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_pair1 -o run --output-format csv -- python3 tools/kbench.py attn_pair
     run pmc_pair2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_pair2 -o run --output-format csv -- python3 tools/kbench.py attn_pair
     run prof_train 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/kbench.py train ;;
+  lnb)
+    run lnb_test 600 python -u -m pytest tests/test_train_kernels_gpu.py tests/test_train_block_gpu.py -x -q -m gpu $T
+    for i in 1 2; do
+      run ktrain_lnb0_$i 600 env SFM_AMD_LIB=variants/libsfm_lnb0.so python tools/kbench.py train
+      run ktrain_lnb1_$i 600 python tools/kbench.py train
+    done
+    run prof_lnb1 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lnb1 -o run --output-format csv -- python3 tools/kbench.py train
+    run prof_lnb0 900 env SFM_AMD_LIB=variants/libsfm_lnb0.so rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lnb0 -o run --output-format csv -- python3 tools/kbench.py train
+    run c4_golden 900 python -u -m pytest tests/test_c4_golden_gpu.py -x -q -m gpu $T ;;
   *) echo "unknown job ${1:-}"; exit 2 ;;
 esac
