@@ -103,48 +103,17 @@ def host_cpu():
         pass
     return model, len(cores) or (os.cpu_count() or 1), os.cpu_count()
 
-# timer class -> the kernel instantiation it launches at the N=32@518 workload
-# (rocprofv3 row names; see DESIGN.md "Kernels").
-_PIPE = "true" if os.environ.get("SR_ATTN_PIPE", "1") != "0" else "false"  # sr_attn.hip: the asm sweep
-KERNEL_OF_TAG = {
-    "attn_global": f"attn_bf16_kernel<4, 2, 2, {_PIPE}>", "attn_reloc": f"attn_bf16_kernel<4, 2, 3, {_PIPE}>",
-    "attn_frame": "attn_bf16_kernel<4, 2, 0, false>", "gemm_bias": "gemm256_kernel<0>", "gemm_gelu": "gemm256_kernel<1>",
-    "gemm_resid": "gemm256_kernel<2>", "gemm_qkv": "gemm256_kernel<3>", "gemm_patch": "gemm256_kernel<4>",
-}
-# GEMM output width per timer class: the 256x256 kernel runs only when it yields >= 512 tiles
-# (sr_gemm.hip dispatch); smaller row counts (C2) run the 128x128 gemm_kernel
-_GEMM_N = {"gemm_bias": 3072, "gemm_gelu": 4096, "gemm_resid": 1024, "gemm_qkv": 3072, "gemm_patch": 1024}
-_GEMM_EPI = {"gemm_bias": 0, "gemm_gelu": 1, "gemm_resid": 2, "gemm_qkv": 3, "gemm_patch": 4}
+# the aggregator's bf16 GEMM timer classes (patch embed, QKV, proj / fc2, fc1): the scope of the
+# north-star "MFMA peak on aggregator GEMMs"; the camera head's fp32 GEMMs (*_f32) are reported apart
+AGG_GEMM_TAGS = ("gemm_bias", "gemm_gelu", "gemm_resid", "gemm_qkv", "gemm_patch")
 
 
-_PAIR = os.environ.get("SR_ATTN_PAIR", "1") != "0"  # aggregator: global + reloc subsample attention paired
-
-
-def _paired(views: int, img: int) -> bool:
-    """Whether the single-GPU forward pairs the global attention with the split reloc's subsample
-    pass (aggregator._paired_attention at this workload)."""
-    rows = views * ((img // 14) ** 2 + 5)
-    return (_PAIR and _PIPE == "true" and rows % 64 == 0 and (rows + 255) // 256 * 16 >= 2048 and
-            os.environ.get("SR_RELOC_SPLIT", "1") == "1")
-
-
-def kernel_of_tag(tag: str, views: int, img: int):
-    """rocprofv3 row name of the kernel a timer class launches at this workload."""
-    if tag in ("attn_global", "attn_reloc") and _paired(views, img):
-        # attn_global: one sr_attention_pair launch (the global attention + the split reloc's
-        # subsample pass); attn_reloc: the reloc own-frame pass that folds the subsample pass in
-        return "attn_bf16_pair_kernel<2>" if tag == "attn_global" else "attn_bf16_kernel<4, 2, 1, false>"
-    if tag == "attn_reloc":  # split reloc (subsample pass = the larger launch) only for long query sets
-        rows = views * ((img // 14) ** 2 + 5)
-        split = (rows + 255) // 256 * 16 >= 2048 and os.environ.get("SR_RELOC_SPLIT", "1") == "1"
-        return f"attn_bf16_kernel<4, 2, 3, {_PIPE}>" if split else "attn_bf16_kernel<4, 2, 1, false>"
-    if tag in _GEMM_N:
-        rows = 2 * views * ((img // 14) ** 2 + 5)
-        if tag == "gemm_patch":
-            rows = 2 * views * (img // 14) ** 2
-        if (_GEMM_N[tag] // 256) * ((rows + 255) // 256) < 512:
-            return f"gemm_kernel<__bf16, {_GEMM_EPI[tag]}, false>"
-    return KERNEL_OF_TAG.get(tag)
+def kernel_of_class(entry):
+    """rocprofv3 name of the kernel a timer class launched, as the library itself reported it
+    (ops.KernelTimer records sr_last_kernel per launch: the C dispatch is the single source of
+    truth); the most-launched one if a class ran several.  None if unreported."""
+    ks = entry.get("kernels") or {}
+    return max(ks, key=ks.get) if ks else None
 
 
 TRAFFIC_FILES = [os.path.join(REPO, "profiles", f) for f in
@@ -490,15 +459,16 @@ def main():
         dom = max(breakdown, key=lambda k: breakdown[k]["total_ms"])
         b = breakdown[dom]
         achieved = b["tflops"]
-        kern = kernel_of_tag(dom, n, args.img) if use_bf16 else None
+        kern = kernel_of_class(b)
         if fp8 and dom == "attn_global":
             # half the attention flops (q.k^T) at the fp8 rate (2x bf16), half (P.V) at the bf16 rate
             if args.fp8_global == "qkv":  # every attention flop at the fp8 rate
-                kern, peak = "attn_qk8_kernel<2, true>", 2 * bf16_peak
+                peak = 2 * bf16_peak
             else:
-                kern, peak = "attn_qk8_kernel<2, false>", 1.0 / (0.5 / (2 * bf16_peak) + 0.5 / bf16_peak)
+                peak = 1.0 / (0.5 / (2 * bf16_peak) + 0.5 / bf16_peak)
         traffic, tsrc = pmc_traffic(kern, n, args.img, args.fp8_global if fp8 else "off") if kern else (None, None)
-        roofline = {"bound": "mfma", "kernel": kern or dom, "timer_class": dom, "achieved": round(achieved, 2),
+        roofline = {"bound": "mfma", "kernel": kern or dom, "kernel_source": "sr_last_kernel" if kern else None,
+                    "timer_class": dom, "achieved": round(achieved, 2),
                     "peak": round(peak, 1), "peak_source": peak_src, "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4),
                     "traffic": None if traffic is None else round(traffic),
@@ -514,13 +484,12 @@ def main():
             return flop / (sum(v["total_ms"] for v in sel) * 1e-3) / 1e12
 
         gpeak = bf16_peak if use_bf16 else PEAK_F32_TFLOPS  # GEMMs stay bf16 in the fp8 modes
-        # north-star "MFMA peak on aggregator GEMMs": the aggregator's bf16 GEMM classes (patch embed,
-        # QKV, proj / fc2, fc1; _GEMM_N); the camera head's fp32 GEMMs (*_f32 classes) are reported apart
-        agg = gemm_rate(list(_GEMM_N))
+        agg = gemm_rate(list(AGG_GEMM_TAGS))
         if agg is not None:
             roofline["gemm_agg_tflops"] = round(agg, 1)
             roofline["gemm_mfma_util"] = round(agg / gpeak, 4)
-            roofline["gemm_mfma_util_scope"] = "aggregator GEMMs (" + ", ".join(k for k in _GEMM_N if k in breakdown) + ")"
+            roofline["gemm_mfma_util_scope"] = "aggregator GEMMs (" + ", ".join(k for k in AGG_GEMM_TAGS
+                                                                                  if k in breakdown) + ")"
         allr = gemm_rate([k for k in breakdown if k.startswith("gemm_")])
         if allr is not None:
             roofline["gemm_all_tflops"] = round(allr, 1)

@@ -12,8 +12,9 @@
  *   - leading dimensions / strides are in ELEMENTS of the pointed-to type;
  *   - launches are asynchronous on the caller's stream (hipStream_t, NULL = default);
  *   - return 0 (SR_OK) or a negative sr_status; sr_last_error() explains it;
- *   - no global mutable state, no allocation, no synchronisation inside a call
- *     (safe to capture into a hipGraph).
+ *   - no allocation, no synchronisation inside a call (safe to capture into a hipGraph);
+ *     the only process-wide mutable state is the tuning switches (sr_set_tuning), whose
+ *     SR_TUNE_SYNC_CHECK debug mode is the one exception to "no synchronisation".
  */
 #ifndef SFM_AMD_H
 #define SFM_AMD_H
@@ -39,6 +40,48 @@ enum sr_status {
 const char* sr_last_error(void);
 /* ABI version: (major << 16) | minor. */
 int sr_version(void);
+
+/* The main device kernel (the one its time goes to) of the most recent launching call on this
+ * thread, named as rocprofv3 names it (e.g. "attn_bf16_pair_kernel<2>", "gemm256_kernel<2>"): the library's
+ * own dispatch decision, for profilers and benchmarks that attribute time to kernels ("" if
+ * none yet).  Per thread, like sr_last_error. */
+const char* sr_last_kernel(void);
+
+/* ------------------------------------------------------------------------
+ * Tuning switches: the library's one piece of process-wide mutable state (besides the
+ * per-thread strings above).  Each switch selects between kernels or schedules that compute
+ * the same function (A/B experiments; the defaults are the measured best).  Values
+ * start from the environment variable sr_tuning_name(key) (read once, at the first use), and
+ * are read at every launch, so sr_set_tuning takes effect for the next call on any thread.
+ * Not synchronised with launches in flight on other threads.
+ * ---------------------------------------------------------------------- */
+enum sr_tuning_key {
+  SR_TUNE_ATTN_MZERO = 0,   /* 1: a fixed softmax offset of 0 drops the -m fold MFMAs, and the
+                               hand-scheduled sweep may run (0: neither)               default 1 */
+  SR_TUNE_ATTN_CFG = 1,     /* -1 auto; 0 | 1 | 2: force the bf16 attention workgroup shape
+                               (4x2 | 8x1 | 2x2 waves x q-blocks)                      default -1 */
+  SR_TUNE_ATTN_PIPE = 2,    /* 1: the hand-scheduled (asm) sweep where it applies    default 1 */
+  SR_TUNE_ATTN_PIPE_SEG = 3,/* 1: its two-segment / ragged variant for every launch with
+                               readable tails (0: only for one long query set)         default 0 */
+  SR_TUNE_ATTN_NO_SHORT = 4,/* 1: no short-sequence fp32 attention kernel             default 0 */
+  SR_TUNE_GEMM_GROUP_M = 5, /* -1 auto (4 for N >= 3072, else row-major); g: tile order in groups
+                               of g row tiles for sr_gemm's and sr_gemm_group's 256x256 tiles */
+  SR_TUNE_GEMM_SMALLM = 6,  /* 1: 64x256 tiles for M <= 64                             default 1 */
+  SR_TUNE_GEMM_NO256 = 7,   /* 1: never the 256x256 GEMM kernel                        default 0 */
+  SR_TUNE_GEMM_REG_EPI = 8, /* 1: register (not LDS-staged) bf16 epilogue              default 0 */
+  SR_TUNE_CONV_NO_NARROW = 9,/* 1: no narrow (Cout <= 32) conv kernel                  default 0 */
+  SR_TUNE_WGRAD256 = 10,    /* 1: 256x256 weight-gradient tiles where they fit         default 1 */
+  SR_TUNE_SYNC_CHECK = 11,  /* 1: debug mode -- every launching call synchronises the device and
+                               returns SR_ELAUNCH with the runtime's message if a kernel faulted
+                               (HIP_LAUNCH_BLOCKING-style attribution; not graph-capturable) */
+  SR_TUNE_COUNT = 12
+};
+/* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
+int sr_set_tuning(int key, int value);
+/* Current value of a switch (SR_EINVAL for an unknown key). */
+int sr_get_tuning(int key);
+/* The environment variable a switch starts from (e.g. "SR_ATTN_PIPE"); NULL for an unknown key. */
+const char* sr_tuning_name(int key);
 
 /* ------------------------------------------------------------------------
  * GEMM with fused epilogue:  out = epilogue(A[M,K] . W[N,K]^T)
@@ -113,8 +156,11 @@ typedef struct sr_gemm_problem {
 
 /* 1..4 independent bf16 GEMMs of one epilogue kind (BIAS, QKV, BIAS_GELU, BIAS_RESID; N % 256 == 0)
  * in ONE launch of the 256x256 kernel, so that their last partial workgroup rounds merge (the
- * layer's query, anchor and anchor-subsample QKV projections after a frame block).  Each problem
- * exactly as sr_gemm would compute it.  Replaces the qkv nn.Linear calls of one layer's
+ * layer's query, anchor and anchor-subsample QKV projections after a frame block).  Every problem
+ * runs on the 256x256 kernel with sr_gemm's tile order, so it is bit-identical to sr_gemm only
+ * where sr_gemm also picks that kernel (>= 512 tiles of 256x256); a smaller problem (the C3
+ * anchor-subsample K/V projection: ~312 tiles) differs from sr_gemm's 128x128 kernel by
+ * accumulation order (fp32 accumulate, rel ~1e-6).  Replaces the qkv nn.Linear calls of one layer's
  * global_reloc and global blocks (attention.py:73; aggregator.py:672-769). */
 int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, const sr_gemm_problem* problems);
 
@@ -170,7 +216,11 @@ typedef struct sr_attn_desc {
                   aligned): per key-segment instance and head, max |k| over the keys.  With it a
                   query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^100 of its first
                   tile's max runs the sweep with a FIXED softmax offset (no per-tile row max,
-                  no rescale; every P <= 2^50, no overflow, same precision); NULL = per-tile max */
+                  no rescale; every P <= 2^50, no overflow, same precision); NULL = per-tile max.
+                  The hand-scheduled sweep (bf16, 256-row workgroups) fixes m = max(0, bound - 64)
+                  for every row whose bound is within 2^174 of its max over the first three key
+                  tiles (every P <= 2^64, the row's largest P >= 2^-110); other waves run the
+                  compiled loop above */
   float key_norm_max; /* optional (bf16 path): > 0 = a static upper bound of |k| (2-norm per head)
                   for every key, used INSTEAD of key_bound (no key scan).  For keys that come out of
                   the qk LayerNorm (attention.py:49-50,78) and RoPE (a rotation), |k| <=
@@ -184,8 +234,8 @@ typedef struct sr_attn_desc {
      (item b, head h, query row i, key j; j the logical key index: segment 0 then segment 1) at
      mask + b*mask_bstride + h*mask_hstride + i*mask_ld + j (element strides; 0 = broadcast).
      DENSE: uint8, nonzero = attend (SDPA's bool mask); ADD: fp32 added to scale*q.k before the
-     softmax (SDPA's float mask; -inf = masked).  A row with no attended key yields NaN like
-     SDPA's math path. */
+     softmax (SDPA's float mask; -inf = masked).  A row with no attended key yields zeros (and
+     LSE -inf), as torch's SDPA does since 2.5 (safe softmax). */
   const void* mask;
   int64_t mask_bstride, mask_hstride, mask_ld;
   int32_t tail_rows_readable; /* optional (bf16 path): >= 64 = the caller guarantees at least 64
@@ -201,6 +251,11 @@ typedef struct sr_attn_desc {
   int64_t ld_merge_o;
   const float* merge_lse;
   int64_t merge_rows;
+  int32_t* sweep_stats; /* optional (bf16 path, diagnostics): two int32 counters the launch ADDS to
+                  (atomically, caller zeroes): [0] waves with query rows that ran the hand-scheduled
+                  sweep, [1] such waves that ran the compiled loop (a row whose fixed softmax offset
+                  falls outside the sweep's 2^174 window, or a launch the sweep does not cover).
+                  NULL = off (no extra work) */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */

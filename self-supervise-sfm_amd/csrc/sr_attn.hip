@@ -427,11 +427,25 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // from LDS once (AGPR sets by tile parity) for both q-blocks.  The sweep is one hand-scheduled
   // inline-asm statement generated by tools/gen_attn_pipe.py (sr_attn_pipe.inc): scores and P
   // live in named VGPRs (P written in place over its scores), O / Q / row sums are AGPR operands.
-  // It covers a wave whose every row has its Cauchy-Schwarz bound qb <= 50, i.e. the fixed offset
-  // m = 0 that the plain path also settles on after tile 0 for such rows, over one key segment of
-  // full tiles (>= 4); any other wave runs the plain loop, which keeps the same wait, barrier and
+  // Every row runs a FIXED offset m (exp2 domain) for the whole sweep, entering each q.k^T chain
+  // as its accumulator operand (-m broadcast over the lane's 16 entries, all scores of one row).
+  // With the row's Cauchy-Schwarz bound qb (every score <= qb):
+  //   m = max(0, qb - PIPE_HI):  every P = 2^(S - m) <= 2^PIPE_HI (O, l: no overflow in fp32 /
+  //                              bf16 for any key count the ABI takes);
+  //   m <= mx0 + PIPE_LO:        mx0 = the row's max over the first three tiles (the prologue's
+  //                              stages) <= its true max, so the row's largest P >= 2^-PIPE_LO
+  //                              stays a normal number in fp32 and bf16 (as do its products with
+  //                              every V entry above 2^-16).
+  // m = 0 (qb <= PIPE_HI) needs no check (the true max >= -qb); larger bounds (trained qk-norm
+  // gains: qb grows as the square of the q_norm / k_norm weights) take mx0 from a pre-pass over
+  // the staged tiles.  The window is 2^174 wide: qb - mx0 <= 174 (qk-gain 4 on LayerNorm'd random
+  // q / k: qb ~ 196 against scores of sigma ~ 23, so mx0 >= 22 for all but ~1e-16 of the rows);
+  // a wave with any row outside it runs the plain loop, which keeps the same wait, barrier and
   // stage per tile, so the waves of a workgroup may take different paths.
+  // One key segment of full tiles (>= 4) or, with readable tails, the _SEG variant.
+  constexpr float PIPE_HI = 64.f, PIPE_LO = 110.f;
   bool asm_ok = false;
+  float m_fix[QB];
   if constexpr (PIPE) {
     // (the asm derives every fragment address from koff[0] / voff0 by XOR: lds0 % 128 == 0)
     // one segment of full tiles: SR_ATTN_PIPE_ASM; two segments or ragged tails: the _SEG variant,
@@ -439,12 +453,48 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
     const bool simple = args.ntile1 == 0 && len0 % KT == 0;
     bool ok = wave_active && use_bound && args.allow_mzero && ntiles >= 4 && (lds0 & 127) == 0 &&
               (simple || d.tail_rows_readable >= KT);
+    bool need_mx = false;
 #pragma unroll
-    for (int b = 0; b < QB; ++b) ok = ok && qb[b] <= 50.f;
+    for (int b = 0; b < QB; ++b) {
+      m_fix[b] = fmaxf(qb[b] - PIPE_HI, 0.f);
+      need_mx |= m_fix[b] > 0.f;
+    }
+    if (use_bound && args.allow_mzero && ntiles >= 4) {  // workgroup-uniform: every wave takes the barrier
+      // the prologue's stages (tiles 0-2) landed and visible to every wave
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sr::barrier_raw();
+      if (__builtin_amdgcn_readfirstlane(__any(ok && need_mx))) {
+        const bool mz = m_zero, fm = fixed_m;
+        m_zero = fixed_m = true;  // plain scores (ragged tails masked), no max tracking
+        float mx[QB];
+#pragma unroll
+        for (int b = 0; b < QB; ++b) mx[b] = -INFINITY;
+        for (int t = 0; t < LOOK; ++t) {
+          qk_tile(t);
+#pragma unroll
+          for (int b = 0; b < QB; ++b)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              mx[b] = fmaxf(mx[b], fmaxf(fmaxf(sc[b][0][i], sc[b][0][i + 8]), fmaxf(sc[b][1][i], sc[b][1][i + 8])));
+        }
+        m_zero = mz;
+        fixed_m = fm;
+#pragma unroll
+        for (int b = 0; b < QB; ++b) ok = ok && m_fix[b] - max_x32(mx[b]) <= PIPE_LO;  // (false for -inf)
+      }
+    }
     asm_ok = __builtin_amdgcn_readfirstlane(__all(ok)) != 0;
   }
+  if (d.sweep_stats && wave_active && lane == 0) atomicAdd(d.sweep_stats + (asm_ok ? 0 : 1), 1);
   if (asm_ok) {
-    m_zero = fixed_m = true;  // m_run = 0, m_b = 0 as initialised
+    m_zero = fixed_m = true;
+    f32x16 mneg[QB];  // chain-start operands: -m broadcast
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      m_run[b] = m_fix[b];  // the LSE below is m + log2(l)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mneg[b][i] = -m_fix[b];
+    }
     const uint64_t spu = (uint64_t)(uintptr_t)sp;  // tile 3 (the prologue staged tiles 0-2)
     // (readfirstlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends into
     // the high word)
@@ -490,7 +540,8 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
                      [suma] "v"(sum_a), [ka0] "v"(ka0), [ka1] "v"(ka1), [ka2] "v"(ka2), [ka3] "v"(ka3),
                      [va0] "v"(va0), [va1] "v"(va1), [ldsv] "s"(ldsv), [rem] "s"(rem), [nsw] "s"(nsw),
                      [sp1] "s"(sp1), [sp1b] "s"(sp1b), [sstep1] "s"(sstep1), [dm10] "v"(dm10), [dm11] "v"(dm11),
-                     [trag0] "s"(trag0), [trag1] "s"(trag1), [vk0] "v"(vk0), [vk1] "v"(vk1), [ninf] "v"(ninf)
+                     [trag0] "s"(trag0), [trag1] "s"(trag1), [vk0] "v"(vk0), [vk1] "v"(vk1), [ninf] "v"(ninf),
+                     [mn0] "v"(mneg[0]), [mn1] "v"(mneg[1])
                    : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc", "vcc");
     } else
     asm volatile(SR_ATTN_PIPE_ASM
@@ -503,7 +554,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
                    [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
                    [suma] "v"(sum_a), [ka0] "v"(ka0), [ka1] "v"(ka1), [ka2] "v"(ka2), [ka3] "v"(ka3),
                    [va0] "v"(va0), [va1] "v"(va1), [sp] "s"(spb), [sp2] "s"(spb2), [sstep] "s"(sst32),
-                   [ldsv] "s"(ldsv), [rem] "s"(rem)
+                   [ldsv] "s"(ldsv), [rem] "s"(rem), [mn0] "v"(mneg[0]), [mn1] "v"(mneg[1])
                  : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc");
   } else {
     for (int t = 0; t < ntiles; ++t) plain_tile(t);
@@ -527,11 +578,16 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
       const int64_t rg = (int64_t)item * d.q_bstride + qrow;
       const float la = d.merge_lse[(int64_t)head * d.merge_rows + rg];
       const float mx = fmaxf(la, lse_row);
-      const float wa = exp2f(la - mx), wb = exp2f(lse_row - mx);
-      const float rw = 1.f / (wa + wb);
-      sa = wa * rw;
-      inv *= wb * rw;
-      lse_row = mx + log2f(wa + wb);
+      if (mx == -INFINITY) {  // both key sets empty for this row: sr_attn_merge's convention
+        sa = 0.f;
+        inv = 0.f;
+      } else {
+        const float wa = exp2f(la - mx), wb = exp2f(lse_row - mx);
+        const float rw = 1.f / (wa + wb);
+        sa = wa * rw;
+        inv *= wb * rw;
+        lse_row = mx + log2f(wa + wb);
+      }
       mo = (const bf16*)d.merge_o + rg * d.ld_merge_o + hcol;
     }
     if (d.lse && hi == 0 && qrow < d.lq) d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = lse_row;
@@ -1157,7 +1213,9 @@ __global__ __launch_bounds__(F32_THREADS) void attn_f32_kernel(AttnArgs args) {
   }
   if (qrow < d.lq) {
     float* op = (float*)d.o + (item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol;
-    const float inv = 1.f / l;
+    // a row with no attended key (all-False SR_MASK_DENSE / all -inf SR_MASK_ADD) gives zeros, as
+    // torch's SDPA does (2.5+: the math path's safe softmax; torch 2.10 here), and LSE -inf
+    const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
     for (int i = 0; i < D; ++i) op[i] = o[i] * inv;
     // same log2-domain convention as the bf16 kernel: log2(sum_j 2^(scale*log2e*q.k_j))
@@ -1248,7 +1306,7 @@ __global__ __launch_bounds__(256) void attn_f32_short_kernel(AttnArgs args) {
   }
   float* op = (float*)d.o + ((int64_t)item * (d.o_bstride ? d.o_bstride : d.q_bstride) + qrow) * d.ldo + hcol +
               lane * DL;
-  const float inv = 1.f / l;
+  const float inv = l > 0.f ? 1.f / l : 0.f;  // no attended key: zeros, as attn_f32_kernel
 #pragma unroll
   for (int t = 0; t < DL; ++t) op[t] = o[t] * inv;
   if (d.lse && lane == 0) d.lse[((int64_t)item * d.heads + head) * d.lq + qrow] = m * 1.4426950408889634f + log2f(l);
@@ -1413,11 +1471,7 @@ static int pair_args(const sr_attn_desc& d, AttnArgs& a, const char* which) {
   a.ntile0 = d.l0 / KT;
   a.ntile1 = 0;
   a.kb_n0 = 1;
-  static const int allow_mz = [] {
-    const char* e = getenv("SR_ATTN_MZERO");
-    return e ? atoi(e) : 1;
-  }();
-  a.allow_mzero = allow_mz;
+  a.allow_mzero = sr::tune(SR_TUNE_ATTN_MZERO);
   return SR_OK;
 }
 
@@ -1437,6 +1491,7 @@ extern "C" int sr_attention_pair(sr_stream_t stream, int dtype, const sr_attn_de
   p.nwg0p = (nwg0 + 7) / 8 * 8;
   const int grid = p.nwg0p + p.nq[1] * p.nh;
   hipLaunchKernelGGL((attn_bf16_pair_kernel<2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  sr::note_kernel("attn_bf16_pair_kernel<2>");
   return sr::check_launch("sr_attention_pair");
 }
 
@@ -1465,11 +1520,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     a.ntile0 = (d.l0 + KT - 1) / KT;
     a.ntile1 = (d.l1 + KT - 1) / KT;
     const int n_inst = bound_instances(d, a.kb_n0);
-    static const int allow_mz = [] {
-      const char* e = getenv("SR_ATTN_MZERO");
-      return e ? atoi(e) : 1;
-    }();
-    a.allow_mzero = allow_mz;
+    a.allow_mzero = sr::tune(SR_TUNE_ATTN_MZERO);
     if (d.key_bound && !(d.key_norm_max > 0.f)) {
       SR_CHECK(d.heads <= 32 && ((uintptr_t)d.key_bound & 3) == 0, SR_EINVAL, "sr_attention: key_bound needs heads <= 32");
       SR_CHECK(hipMemsetAsync(d.key_bound, 0, sizeof(float) * n_inst * d.heads, s) == hipSuccess, SR_ELAUNCH,
@@ -1489,34 +1540,25 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     // 256-row tiles unless they would leave CUs idle (fewer than 2 workgroups per CU, e.g. the
     // per-rank query slice of a frame-sharded global block).  SR_ATTN_CFG=0|1|2 overrides
     // (tuning experiments).
-    static const int force_cfg = [] {
-      const char* e = getenv("SR_ATTN_CFG");
-      return e ? atoi(e) : -1;
-    }();
+    const int force_cfg = sr::tune(SR_TUNE_ATTN_CFG);
     const long wgs256 = (long)((d.lq + 255) / 256) * d.heads * d.batch;
     const int cfg = force_cfg >= 0 ? force_cfg : (wgs256 >= 512 ? SR_ATTN_DEFAULT_CFG : 2);
     const int rows = cfg == 2 ? 128 : 256;
     // the hand-scheduled sweep (PIPE, one wave per SIMD) for the 4 x 2 shape over one key segment
     // of full tiles; SR_ATTN_PIPE=0 runs the compiled two-waves-per-SIMD sweep instead (A/B:
     // global L = 43,968 6.27-6.29 vs 6.78-6.83 ms, kbench on one box)
-    static const bool pipe = [] {
-      const char* e = getenv("SR_ATTN_PIPE");
-      return e ? atoi(e) != 0 : true;
-    }();
+    const bool pipe = sr::tune(SR_TUNE_ATTN_PIPE) != 0;
     // ... and, opt-in (SR_ATTN_PIPE_SEG=1), for two-segment / ragged launches (reloc, frame, DINO)
     // whose rows past each segment's end are readable.  Correct (the production-shape tests run it)
     // but not faster: at one workgroup per CU the ragged last q-tile of each 1,374-row frame leaves
     // two of its four SIMDs idle for the whole sweep (a second workgroup fills them in the compiled
     // kernel), and a frame's 22-tile sweep does not hide the workgroup's prologue / epilogue
     // (kbench: reloc 1.835-1.846 vs 1.828-1.852 ms, frame 0.609-0.611 vs 0.559-0.576 ms)
-    // (read per launch: the tests switch it on for their asm-seg cases)
-    const bool pipe_seg = [] {
-      const char* e = getenv("SR_ATTN_PIPE_SEG");
-      return e ? atoi(e) != 0 : false;
-    }();
+    const bool pipe_seg = sr::tune(SR_TUNE_ATTN_PIPE_SEG) != 0;
     dim3 grid((d.lq + rows - 1) / rows, d.heads, d.batch);
 #define SR_ATTN_LAUNCH(NW_, QB_, ST_)                                                                           \
   do {                                                                                                        \
+    sr::note_kernel("attn_bf16_kernel<%d, %d, %d, %s>", NW_, QB_, kind, ST_ ? "true" : "false");             \
     if (kind == 3) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 3, ST_>), grid, dim3(NW_ * 64), 0, s, a);     \
     else if (kind == 2) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 2, ST_>), grid, dim3(NW_ * 64), 0, s, a); \
     else if (kind == 1) hipLaunchKernelGGL((attn_bf16_kernel<NW_, QB_, 1, ST_>), grid, dim3(NW_ * 64), 0, s, a); \
@@ -1537,20 +1579,23 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   }
   SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attention: bad dtype %d", dtype);
   a.ntile0 = a.ntile1 = 0;
-  static const bool no_short = getenv("SR_ATTN_NO_SHORT") != nullptr;  // tuning A/B switch
+  const bool no_short = sr::tune(SR_TUNE_ATTN_NO_SHORT) != 0;
   const bool al16 = (((uintptr_t)d.q | (uintptr_t)d.k0 | (uintptr_t)(d.l1 ? d.k1 : d.k0)) & 15) == 0;
   if (!no_short && al16 && d.l0 + d.l1 <= 512 && (d.head_dim == 64 || d.head_dim == 128) && d.ldq % 4 == 0 &&
       d.ldk0 % 4 == 0 && (d.l1 == 0 || d.ldk1 % 4 == 0)) {
     dim3 g4((d.lq + 3) / 4, d.heads, d.batch);
     if (d.head_dim == 64) hipLaunchKernelGGL(attn_f32_short_kernel<64>, g4, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(attn_f32_short_kernel<128>, g4, dim3(256), 0, s, a);
+    sr::note_kernel("attn_f32_short_kernel<%d>", d.head_dim);
     return sr::check_launch("sr_attention(f32 short)");
   }
   dim3 grid((d.lq + F32_THREADS - 1) / F32_THREADS, d.heads, d.batch);
   if (d.head_dim == 64) {
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(F32_THREADS), 0, s, a);
+    sr::note_kernel("attn_f32_kernel<64>");
   } else if (d.head_dim == 128) {
     hipLaunchKernelGGL(attn_f32_kernel<128>, grid, dim3(F32_THREADS), 0, s, a);
+    sr::note_kernel("attn_f32_kernel<128>");
   } else {
     sr::set_error("sr_attention(f32): head_dim must be 64 or 128 (got %d)", d.head_dim);
     return SR_EUNSUPPORTED;
@@ -1643,6 +1688,7 @@ extern "C" int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* desc, co
   dim3 grid((d.lq + 255) / 256, d.heads, d.batch);
   const int kind = d.batch == 1 && d.lq >= 4096 ? 2 : 0;
   const uint8_t* nov = nullptr;
+  sr::note_kernel("attn_qk8_kernel<%d, false>", kind);
   if (kind == 2)
     hipLaunchKernelGGL((attn_qk8_kernel<2, false>), grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8,
                        (const uint8_t*)k8, ldk8, nov, qk_exp);
@@ -1683,5 +1729,6 @@ extern "C" int sr_attention_qkv8(sr_stream_t stream, const sr_attn_desc* desc, c
   dim3 grid((d.lq + 255) / 256, d.heads, 1);
   hipLaunchKernelGGL((attn_qk8_kernel<2, true>), grid, dim3(256), 0, (hipStream_t)stream, a, (const uint8_t*)q8, ldq8,
                      (const uint8_t*)k8, ldk8, (const uint8_t*)v8t, qkv_exp);
+  sr::note_kernel("attn_qk8_kernel<2, true>");
   return sr::check_launch("sr_attention_qkv8");
 }

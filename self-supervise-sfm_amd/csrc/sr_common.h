@@ -19,7 +19,13 @@ namespace sr {
 
 // thread-local error message; set by host wrappers on failure
 void set_error(const char* fmt, ...);
+// after a call's launches: the runtime's launch error (and, under SR_TUNE_SYNC_CHECK, a
+// device synchronisation's) -> SR_ELAUNCH with the message
 int check_launch(const char* what);
+// thread-local name of the kernel a call launched (sr_last_kernel), as rocprofv3 prints it
+void note_kernel(const char* fmt, ...);
+// current value of a tuning switch (sfm_amd.h sr_tuning_key)
+int tune(int key);
 
 template <typename T> struct is_bf16 { static constexpr bool value = false; };
 template <> struct is_bf16<bf16> { static constexpr bool value = true; };

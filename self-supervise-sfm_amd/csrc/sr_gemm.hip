@@ -798,19 +798,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
 }
 
 
+// 256x256 tile order (sr_gemm and sr_gemm_group): column-major inside groups of 4 row tiles for
+// the wide outputs (fc1, QKV: N >= 3072; kbench A/B fc1 -3 %, qkv -1.5 %), row-major for N = 1024
+// (proj / fc2, where grouping measured neutral to +1-2 % slower).  SR_TUNE_GEMM_GROUP_M = g >= 0
+// overrides (<= 1: row-major).
+static int tile_group_m(int N) {
+  const int g = sr::tune(SR_TUNE_GEMM_GROUP_M);
+  return g >= 0 ? g : (N >= 3072 ? 4 : 0);
+}
+
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
-  // tile order: column-major inside groups of 4 row tiles for the wide outputs (fc1, QKV:
-  // N >= 3072; kbench A/B fc1 -3 %, qkv -1.5 %), row-major for N = 1024 (proj / fc2, where
-  // grouping measured neutral to +1-2 % slower).  SR_GEMM_GROUP_M=g overrides (<= 1: row-major).
-  static const int group_m = [] {
-    const char* e = getenv("SR_GEMM_GROUP_M");
-    return e ? atoi(e) : -1;
-  }();
-  a.group_m = group_m >= 0 ? group_m : (a.N >= 3072 ? 4 : 0);
+  a.group_m = tile_group_m(a.N);
   const int grid = nwg;
   hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
+  sr::note_kernel("gemm256_kernel<%d>", EPI);
   return sr::check_launch("sr_gemm(256)");
 }
 
@@ -819,16 +822,16 @@ int launch(const GemmArgs& a, hipStream_t s) {
   const int slices = a.partial ? (a.ktiles + a.kt_per_split - 1) / a.kt_per_split : 1;
   // few rows (the camera trunk, M = 2N views): 64 x 256 tiles, no padding rows computed
   // (SR_GEMM_SMALLM=0: 128 x 128)
-  static const bool small_m = [] {
-    const char* e = getenv("SR_GEMM_SMALLM");
-    return e ? atoi(e) != 0 : true;
-  }();
+  const bool small_m = sr::tune(SR_TUNE_GEMM_SMALLM) != 0;
+  const char* tn = sr::is_bf16<T>::value ? "__bf16" : "float";
   if (small_m && a.M <= 64 && a.N > 128) {
     const int nwg = (a.N + 255) / 256;
     hipLaunchKernelGGL((gemm_kernel<T, EPI, false, 64, 256>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
+    sr::note_kernel("gemm_kernel<%s, %d, false, 64, 256>", tn, EPI);
   } else {
     const int nwg = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM);
     hipLaunchKernelGGL((gemm_kernel<T, EPI>), dim3(nwg, slices), dim3(NTHREADS), 0, s, a);
+    sr::note_kernel("gemm_kernel<%s, %d, false>", tn, EPI);
   }
   if (a.partial) {
     const int64_t nq = (int64_t)a.M * (a.N / 4);
@@ -841,7 +844,7 @@ int launch(const GemmArgs& a, hipStream_t s) {
 template <typename T>
 int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
   if constexpr (sr::is_bf16<T>::value) {
-    static const bool no_big = getenv("SR_GEMM_NO256") != nullptr;  // tuning A/B switch
+    const bool no_big = sr::tune(SR_TUNE_GEMM_NO256) != 0;
     // 256x256 tiles (one WG per CU) only when they still give >= 2 WGs per CU; smaller
     // problems (frame-sharded ranks, small scenes) keep 4x more 128x128 workgroups.
     const long tiles256 = (long)(a.N / BIG) * ((a.M + BIG - 1) / BIG);
@@ -1020,7 +1023,7 @@ static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda
   a.ktiles = K / kt;
   // LDS-staged epilogue (256x256 tiles): measured +8 % on bf16 BIAS / QKV outputs, -7 % on the
   // fp32 residual update and -2 % with GELU (DESIGN.md "GEMM"), so only the former use it.
-  static const bool no_lds_epi = getenv("SR_GEMM_REG_EPI") != nullptr;  // tuning A/B switch
+  const bool no_lds_epi = sr::tune(SR_TUNE_GEMM_REG_EPI) != 0;
   a.lds_epi = !no_lds_epi && (epi == SR_EPI_BIAS || (epi == SR_EPI_QKV && !ep->aux)) &&
               ((uintptr_t)out % 16) == 0 && (ldo * esz) % 16 == 0;
   a.ep = *ep;
@@ -1071,7 +1074,7 @@ extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, cons
     if (rc != SR_OK) return rc;
     SR_CHECK(q.N % BIG == 0, SR_EUNSUPPORTED, "sr_gemm_group: N=%d must be a multiple of %d", q.N, BIG);
     GemmArgs& a = gg.g[i];
-    a.group_m = a.N >= 3072 ? 4 : 0;  // launch256's tile order
+    a.group_m = tile_group_m(a.N);  // launch256's tile order
     const int nt = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
     gg.start[i + 1] = gg.start[i] + (nt + 7) / 8 * 8;
   }
@@ -1086,6 +1089,7 @@ extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, cons
     default:
       hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS_RESID>), dim3(gg.start[n]), dim3(512), 0, s, gg);
   }
+  sr::note_kernel("gemm256_group_kernel<%d>", epi);
   return sr::check_launch("sr_gemm_group");
 }
 
@@ -1139,7 +1143,7 @@ extern "C" int sr_conv3x3_f32(sr_stream_t stream, const float* x, int n, int h, 
   a.conv.stride = stride;
   a.conv.relu = relu_in;
   hipStream_t s = (hipStream_t)stream;
-  static const bool no_narrow = getenv("SR_CONV_NO_NARROW") != nullptr;  // tuning A/B switch
+  const bool no_narrow = sr::tune(SR_TUNE_CONV_NO_NARROW) != 0;
   if (!no_narrow && epi == SR_EPI_BIAS && cout <= NBN) {
     hipLaunchKernelGGL(conv_narrow_kernel, dim3((a.M + NBM - 1) / NBM), dim3(256), 0, s, a);
     return sr::check_launch("sr_conv3x3_f32(narrow)");

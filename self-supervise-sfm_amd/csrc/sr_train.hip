@@ -898,14 +898,14 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   splits = (g.mtiles + g.mt_per_split - 1) / g.mt_per_split;
   hipStream_t s = (hipStream_t)stream;
   // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
-  static const bool big = [] {
-    const char* e = getenv("SR_WGRAD256");
-    return e ? atoi(e) != 0 : true;
-  }();
-  if (big && N % WT2 == 0 && K % WT2 == 0)
+  const bool big = sr::tune(SR_TUNE_WGRAD256) != 0;
+  if (big && N % WT2 == 0 && K % WT2 == 0) {
     hipLaunchKernelGGL(wgrad256_kernel, dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
-  else
+    sr::note_kernel("wgrad256_kernel");
+  } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3((N / WT) * (K / WT), splits), dim3(256), 0, s, g);
+    sr::note_kernel("wgrad_kernel");
+  }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, workspace, splits, N, K, dW, lddw, accumulate,
                      rowscale, wdot, ldwd, rowdot);
   return sr::check_launch("sr_gemm_wgrad");

@@ -68,6 +68,7 @@ class AttnDesc(ctypes.Structure):
         ("mask", _vp), ("mask_bstride", _i64), ("mask_hstride", _i64), ("mask_ld", _i64),
         ("tail_rows_readable", _i32),
         ("merge_o", _vp), ("ld_merge_o", _i64), ("merge_lse", _vp), ("merge_rows", _i64),
+        ("sweep_stats", _vp),
     ]
 
 
@@ -96,6 +97,10 @@ class ImcLossDesc(ctypes.Structure):
 _PROTOS = {
     "sr_last_error": (ctypes.c_char_p, []),
     "sr_version": (_i32, []),
+    "sr_last_kernel": (ctypes.c_char_p, []),
+    "sr_set_tuning": (_i32, [_i32, _i32]),
+    "sr_get_tuning": (_i32, [_i32]),
+    "sr_tuning_name": (ctypes.c_char_p, [_i32]),
     "sr_gemm": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, ctypes.POINTER(GemmEpi)]),
     "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                               ctypes.POINTER(GemmEpi)]),

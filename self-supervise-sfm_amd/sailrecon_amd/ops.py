@@ -7,6 +7,7 @@ place).  No function here computes anything on the host.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Optional
@@ -29,6 +30,7 @@ class KernelTimer:
     def __init__(self, tags=None):
         self.tags = None if tags is None else set(tags)
         self.records = {}
+        self.kernels = {}  # tag -> {kernel name: launches}
 
     def wants(self, tag: Optional[str]) -> bool:
         return tag is not None and (self.tags is None or tag in self.tags)
@@ -38,13 +40,19 @@ class KernelTimer:
         ev.record()
         return ev
 
-    def stop(self, tag: str, ev0, work: float, nbytes: float = 0.0):
+    def stop(self, tag: str, ev0, work: float, nbytes: float = 0.0, kernel: Optional[str] = None):
+        """``kernel``: the rocprof name of the launch's kernel, as the library reports it
+        (last_kernel(), sr_last_kernel) -- the library's own dispatch decision."""
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
         self.records.setdefault(tag, []).append((ev0, ev1, work, nbytes))
+        if kernel:
+            k = self.kernels.setdefault(tag, {})
+            k[kernel] = k.get(kernel, 0) + 1
 
     def summary(self):
-        """tag -> dict(launches, total_ms, avg_ms, flops_per_launch, tflops, bytes_per_launch, gbs)
+        """tag -> dict(launches, total_ms, avg_ms, flops_per_launch, tflops, bytes_per_launch, gbs,
+        kernels = {rocprof kernel name: launches} as the library reported them)
 
         ``bytes_per_launch`` is the algorithmic (compulsory) HBM traffic of a launch:
         every operand read once, every output written once."""
@@ -58,11 +66,63 @@ class KernelTimer:
             sec = tot * 1e-3
             out[tag] = dict(launches=len(recs), total_ms=tot, avg_ms=tot / len(recs),
                             flops_per_launch=work / len(recs), tflops=(work / sec / 1e12) if tot else 0.0,
-                            bytes_per_launch=nbytes / len(recs), gbs=(nbytes / sec / 1e9) if tot else 0.0)
+                            bytes_per_launch=nbytes / len(recs), gbs=(nbytes / sec / 1e9) if tot else 0.0,
+                            kernels=dict(self.kernels.get(tag, {})))
         return out
 
 
 TIMER: Optional[KernelTimer] = None
+
+
+# ---- the library's tuning switches (sfm_amd.h sr_tuning_key), by environment-variable name
+_TUNE_KEYS: dict = {}
+
+
+def _tune_key(name: str) -> int:
+    if not _TUNE_KEYS:
+        lib = _lib.load()
+        k = 0
+        while True:
+            n = lib.sr_tuning_name(k)
+            if n is None:
+                break
+            _TUNE_KEYS[n.decode()] = k
+            k += 1
+    if name not in _TUNE_KEYS:
+        raise KeyError(f"unknown tuning switch {name!r} (known: {sorted(_TUNE_KEYS)})")
+    return _TUNE_KEYS[name]
+
+
+def tuning_names():
+    """Every switch the library has (sr_tuning_name), e.g. 'SR_ATTN_PIPE'."""
+    _tune_key("SR_ATTN_PIPE")
+    return sorted(_TUNE_KEYS, key=_TUNE_KEYS.get)
+
+
+def get_tuning(name: str) -> int:
+    """Current value of a library tuning switch (sr_get_tuning); it starts from the environment."""
+    return int(_lib.load().sr_get_tuning(_tune_key(name)))
+
+
+def set_tuning(name: str, value: int) -> int:
+    """Sets a library tuning switch (sr_set_tuning) for every later launch; returns the old value."""
+    return int(_lib.load().sr_set_tuning(_tune_key(name), int(value)))
+
+
+@contextlib.contextmanager
+def tuning(**switches):
+    """with ops.tuning(SR_ATTN_PIPE_SEG=1): ... -- switches set for the block, restored after."""
+    old = {k: set_tuning(k, v) for k, v in switches.items()}
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            set_tuning(k, v)
+
+
+def last_kernel() -> str:
+    """The main kernel the last library call on this thread launched (sr_last_kernel)."""
+    return _lib.load().sr_last_kernel().decode()
 
 _EPI_NAME = {_lib.SR_EPI_BIAS: "bias", _lib.SR_EPI_BIAS_GELU: "gelu", _lib.SR_EPI_BIAS_RESID: "resid",
              _lib.SR_EPI_QKV: "qkv", _lib.SR_EPI_PATCH: "patch", _lib.SR_EPI_F32: "f32",
@@ -97,9 +157,6 @@ def _rowmajor(t: Tensor, name: str) -> int:
 _SPLITK_WS = {}  # (device, stream) -> fp32 workspace of sr_gemm_splitk
 
 
-_GEMM_SMALLM = os.environ.get("SR_GEMM_SMALLM", "1") != "0"
-
-
 def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
     """K slices for few-row GEMMs (the camera trunk, M = 2N views): enough 128x128-tile
     workgroups to spread the weight stream over the CUs; 1 = plain sr_gemm."""
@@ -107,7 +164,7 @@ def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
         return 1
     ktiles = K // (64 if dtype == torch.bfloat16 else 32)
     # sr_gemm's tiles: 64 x 256 for M <= 64 (SR_GEMM_SMALLM), else 128 x 128
-    wgs = -(-N // 256) if (M <= 64 and N > 128 and _GEMM_SMALLM) else -(-M // 128) * (N // 128)
+    wgs = -(-N // 256) if (M <= 64 and N > 128 and get_tuning("SR_GEMM_SMALLM")) else -(-M // 128) * (N // 128)
     cap = max(1, K // (4 * M))  # partial-tile traffic (2 * splits * M * N) <= half the weight stream (N * K)
     splits = 1
     while (wgs * splits * 2 <= 1024 and splits * 2 <= cap and ktiles % (splits * 2) == 0
@@ -201,7 +258,7 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
     if timed:
         es, eo = a.element_size(), out.element_size()
         nb = (M * K + N * K) * es + M * N * eo * (2 if epi == _lib.SR_EPI_BIAS_RESID else 1)
-        TIMER.stop(tag, ev0, 2.0 * M * N * K, nb)
+        TIMER.stop(tag, ev0, 2.0 * M * N * K, nb, kernel=last_kernel())
 
 
 GEMM_GROUP_MAX = 4
@@ -244,7 +301,7 @@ def gemm_group(problems, epi: int, tag: Optional[str] = None) -> None:
     rc = _lib.load().sr_gemm_group(_stream(problems[0]["a"]), dtype_code(torch.bfloat16), epi, len(problems), arr)
     check(rc, "sr_gemm_group")
     if timed:
-        TIMER.stop(tag, ev0, flops, nbytes)
+        TIMER.stop(tag, ev0, flops, nbytes, kernel=last_kernel())
 
 
 # fixed-offset softmax sweep (sr_attn_desc.key_bound); SR_ATTN_BOUND=0 keeps the per-tile row max
@@ -290,7 +347,8 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
               l1: int = 0, k1_bstride: int = 0, mask_mode: int = _lib.SR_MASK_NONE, n_anchor: int = 0,
               scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
               key_norm_max: float = 0.0, mask: Optional[Tensor] = None, tail_readable: bool = False,
-              merge_o: Optional[Tensor] = None, merge_lse: Optional[Tensor] = None) -> None:
+              merge_o: Optional[Tensor] = None, merge_lse: Optional[Tensor] = None,
+              sweep_stats: Optional[Tensor] = None) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``mask``
     (mask_mode SR_MASK_DENSE: bool / uint8, nonzero = attend; SR_MASK_ADD: fp32 added to the
     scores) is a [batch, heads, lq, l0 + l1] view (broadcast dims may have stride 0, the last dim
@@ -304,8 +362,12 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     hand-scheduled sweep take ragged and two-segment launches (sr_attn_desc.tail_rows_readable).
     ``merge_o`` / ``merge_lse`` (bf16 only): a row-normalised result of the same query rows over a
     DISJOINT key set ([R, >= heads*head_dim] bf16, row item*q_bstride + i) and its log2-domain LSE
-    (fp32 [heads, R]); o then receives the softmax over the union (sr_attn_desc.merge_o)."""
+    (fp32 [heads, R]); o then receives the softmax over the union (sr_attn_desc.merge_o).
+    ``sweep_stats`` (int32 [2], caller-zeroed, bf16): the launch adds its waves on the
+    hand-scheduled sweep / on the compiled loop (sr_attn_desc.sweep_stats); it forces one launch."""
     parts = key_split_parts(dtype=q.dtype, batch=batch, lq=lq, heads=heads, l0=l0, l1=l1, mask_mode=mask_mode)
+    if sweep_stats is not None:
+        parts = 1
     if merge_o is not None:
         if q.dtype != torch.bfloat16 or merge_o.dtype != torch.bfloat16 or merge_o.stride(1) != 1 or \
                 merge_lse is None or merge_lse.dtype != torch.float32 or not merge_lse.is_contiguous() or \
@@ -327,6 +389,7 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
                    n_anchor=n_anchor, scale=scale, lse=lse)
     if tail_readable:
         d.tail_rows_readable = 64
+    _set_sweep_stats(d, sweep_stats)
     if merge_o is not None:
         d.merge_o, d.ld_merge_o = _p(merge_o), merge_o.stride(0)
         d.merge_lse, d.merge_rows = _p(merge_lse), merge_lse.shape[1]
@@ -345,6 +408,14 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * (l0 + l1) * head_dim,
                       q.element_size() * heads * head_dim *
                       (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)))
+
+
+def _set_sweep_stats(d: AttnDesc, stats: Optional[Tensor]) -> None:
+    if stats is None:
+        return
+    if stats.dtype != torch.int32 or stats.numel() < 2 or not stats.is_cuda or not stats.is_contiguous():
+        raise ValueError("sweep_stats must be a contiguous int32 device tensor of >= 2 elements")
+    d.sweep_stats = _p(stats)
 
 
 def pair_eligible(dtype: torch.dtype, l0: int, head_dim: int, key_norm_max: float) -> bool:
@@ -372,6 +443,7 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
         d = _attn_desc(p["q"], p["k0"], p["v0"], p["o"], heads=heads, head_dim=head_dim, batch=1, lq=p["lq"],
                        q_bstride=0, l0=p["l0"], k0_bstride=0, lse=p.get("lse"))
         d.key_norm_max = float(p["key_norm_max"])
+        _set_sweep_stats(d, p.get("sweep_stats"))
         descs.append(d)
         flops += 4.0 * heads * p["lq"] * p["l0"] * head_dim
         nbytes += p["q"].element_size() * heads * head_dim * (2 * p["lq"] + 2 * p["l0"])
@@ -381,7 +453,7 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
                                        ctypes.byref(descs[1]))
     check(rc, "sr_attention_pair")
     if timed:
-        TIMER.stop(tag, ev0, flops, nbytes)
+        TIMER.stop(tag, ev0, flops, nbytes, kernel=last_kernel())
 
 
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,
@@ -397,7 +469,7 @@ def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: 
     rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))
     check(rc, "sr_attention")
     if timed:
-        TIMER.stop(tag, ev0, flops, nbytes)
+        TIMER.stop(tag, ev0, flops, nbytes, kernel=last_kernel())
 
 
 def key_split_workspace(device, parts: int, rows: int, cols: int, heads: int, name: str = "attn_ksplit"):
@@ -555,7 +627,7 @@ def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, b
     if timed:
         kv_rows = l0 if k0_bstride == 0 else batch * l0
         nb = heads * head_dim * (2 * batch * lq + kv_rows) + 2 * heads * head_dim * (batch * lq + kv_rows)
-        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * l0 * head_dim, nb)
+        TIMER.stop(tag, ev0, 4.0 * batch * heads * lq * l0 * head_dim, nb, kernel=last_kernel())
 
 
 def _attn_desc(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
@@ -864,16 +936,13 @@ def _train_ws(device, name: str, numel: int) -> Tensor:
     return ws
 
 
-_WGRAD256 = os.environ.get("SR_WGRAD256", "1") != "0"
-
-
 def _wgrad_splits(M: int, N: int, K: int) -> int:
     """Reduction slices.  256x256 tiles (sr_gemm_wgrad's one-workgroup-per-CU kernel when N and K
     are multiples of 256): the most slices that still fit one round of 256 workgroups, each slice
     >= 8 m-tiles of 64 rows, at most 16.  128x128 tiles: >= 512 workgroups (2 per CU), powers of 2;
     the fp32 partials stay <= 16x the output."""
     mt = -(-M // 64)
-    if _WGRAD256 and N % 256 == 0 and K % 256 == 0:
+    if get_tuning("SR_WGRAD256") and N % 256 == 0 and K % 256 == 0:
         tiles = (N // 256) * (K // 256)
         return max(1, min(256 // tiles, 16, mt // 8))
     tiles = (N // 128) * (K // 128)

@@ -47,3 +47,51 @@ def test_abi_validation_errors_without_gpu():
     assert rc == -3 and b"multiple of 4" in lib.sr_last_error()
     d = _lib.AttnDesc()
     assert lib.sr_attention(None, _lib.SR_BF16, ctypes.byref(d)) == -1
+
+
+def test_tuning_switches_without_gpu():
+    """sr_set_tuning / sr_get_tuning / sr_tuning_name: every A/B switch the
+    kernels read is one documented entry of sfm_amd.h's sr_tuning_key, starting from its
+    environment variable; set returns the old value, unknown keys fail with SR_EINVAL."""
+    from sailrecon_amd import _lib, ops
+    lib = _lib.load()
+    src = open(HEADER).read()
+    keys = re.findall(r"^\s*(SR_TUNE_\w+)\s*=\s*(\d+)", src, flags=re.M)
+    count = dict(keys).pop("SR_TUNE_COUNT")
+    assert len(keys) - 1 == int(count) == len(ops.tuning_names())
+    for name, k in keys:
+        if name == "SR_TUNE_COUNT":
+            assert lib.sr_tuning_name(int(k)) is None
+            continue
+        env = lib.sr_tuning_name(int(k)).decode()
+        assert name.replace("SR_TUNE_", "SR_") == env
+    assert ops.get_tuning("SR_ATTN_PIPE") == int(os.environ.get("SR_ATTN_PIPE", "1"))
+    with ops.tuning(SR_ATTN_PIPE_SEG=1, SR_GEMM_GROUP_M=2):
+        assert ops.get_tuning("SR_ATTN_PIPE_SEG") == 1 and ops.get_tuning("SR_GEMM_GROUP_M") == 2
+    assert ops.get_tuning("SR_ATTN_PIPE_SEG") == int(os.environ.get("SR_ATTN_PIPE_SEG", "0"))
+    assert lib.sr_set_tuning(99, 1) == -1 and b"unknown key" in lib.sr_last_error()
+    assert lib.sr_get_tuning(-1) == -1
+    assert lib.sr_last_kernel() == b""  # nothing launched on this thread
+
+
+def test_no_getenv_outside_the_tuning_table():
+    """The kernels' switches live in one table (sr_api.hip); no other translation unit reads the
+    environment."""
+    csrc = os.path.join(REPO, "self-supervise-sfm_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h", ".inc")) and f != "sr_api.hip":
+            assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+
+
+def test_generated_asm_sweep_matches_generator(tmp_path):
+    """csrc/sr_attn_pipe.inc is what tools/gen_attn_pipe.py emits with its default
+    knobs (no stale or hand-edited variant ships)."""
+    import subprocess
+    import sys
+    out = tmp_path / "pipe.inc"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("SR_PIPE_")}
+    env["SR_PIPE_OUT"] = str(out)
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "gen_attn_pipe.py")], env=env, check=True,
+                   capture_output=True)
+    shipped = open(os.path.join(REPO, "self-supervise-sfm_amd", "csrc", "sr_attn_pipe.inc")).read()
+    assert out.read_text() == shipped

@@ -375,7 +375,7 @@ def _padded(t, rows=64):
 @pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
 @pytest.mark.parametrize("nq,nsub", [(8, 8 * PP), (32, 32 * PP), (4, 32 * PP), (8, 32 * PP)],
                          ids=["C2", "C3", "C3-8rk", "C3-4rk"])
-def test_reloc_attention_production(ops, nq, nsub, tail, monkeypatch):
+def test_reloc_attention_production(ops, nq, nsub, tail):
     """global_reloc (aggregator.py:672-741): every query frame attends to the shared anchor
     subsample (segment 0, batch stride 0) and to its own frame (segment 1); C3-8rk / C3-4rk are
     the per-rank shapes of the frame-sharded C3 forward (4 / 8 query frames).  asm-seg: readable
@@ -385,10 +385,15 @@ def test_reloc_attention_production(ops, nq, nsub, tail, monkeypatch):
     ks, _, vs = _make(nsub, 4, spikes=(nsub - 3,))
     if tail:
         k, v, ks, vs = _padded(k), _padded(v), _padded(ks), _padded(vs)
-        monkeypatch.setenv("SR_ATTN_PIPE_SEG", "1")  # the opt-in variant (read per launch)
     o = torch.empty(nq * P, C, device=DEV, dtype=torch.bfloat16)
-    ops.attention(q, ks, vs, o, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
-                  k1=k, v1=v, l1=P, k1_bstride=P, tail_readable=tail)
+    with ops.tuning(SR_ATTN_PIPE_SEG=int(tail)):  # the opt-in variant (sr_set_tuning)
+        ops.attention(q, ks, vs, o, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
+                      k1=k, v1=v, l1=P, k1_bstride=P, tail_readable=tail)
+        # the library's dispatch: 256-row workgroups with the asm variant, or 128-row ones below 512
+        # workgroups (the 4-query-frame rank shape)
+        big = (P + 255) // 256 * H * nq >= 512
+        assert ops.last_kernel() == (f"attn_bf16_kernel<4, 2, 1, {'true' if tail else 'false'}>" if big
+                                     else "attn_bf16_kernel<2, 2, 1, false>")
     frames = sorted(set([0, nq - 1] + torch.randperm(nq, generator=torch.Generator().manual_seed(nq))[:6].tolist()))
     scale = D ** -0.5
     for j in frames:
@@ -445,17 +450,18 @@ def test_reloc_attention_split_production(ops, nq):
 
 
 @pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
-def test_frame_attention_production(ops, tail, monkeypatch):
+def test_frame_attention_production(ops, tail):
     """frame / DINO stacks at C3: 64 frames x 1374 tokens, keys = own frame (asm-seg: the ragged
     last key tile staged whole from readable rows and masked in the hand-scheduled sweep)."""
     S = 64
     q, k, v = _make(S * P, 5, spikes=(S * P - 2,))
     if tail:
         k, v = _padded(k), _padded(v)
-        monkeypatch.setenv("SR_ATTN_PIPE_SEG", "1")
     o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
-    ops.attention(q, k, v, o, heads=H, head_dim=D, batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P,
-                  tail_readable=tail)
+    with ops.tuning(SR_ATTN_PIPE_SEG=int(tail)):
+        ops.attention(q, k, v, o, heads=H, head_dim=D, batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P,
+                      tail_readable=tail)
+        assert ops.last_kernel() == f"attn_bf16_kernel<4, 2, 0, {'true' if tail else 'false'}>"
     scale = D ** -0.5
     for j in (0, 17, 40, S - 1):
         fr = slice(j * P, (j + 1) * P)
@@ -491,3 +497,116 @@ def test_frame_attention_shapes_lse(ops, S, L, static):
             # c*q enters the MFMAs rounded to bf16: scores (and so the LSE) carry ~2^-9 relative error
             err = (lse[j, h, rows].double() - ref_lse).abs() - 3e-3 * ref_lse.abs()
             assert float(err.max()) < 1e-2, (j, h)
+
+
+def _qk_gain(rows, g, gen):
+    """[rows, C] bf16 as the aggregator's qk-norm makes q / k (attention.py:49-50,78): per-head
+    LayerNorm of a gaussian times w + b with w = g (1 + 0.02 n), b = 0.02 n -- the synthetic rule's
+    affine scaled by the qk-gain g (trained q_norm / k_norm weights sit around 2-3).  Returns it and
+    runtime.key_norm_bound's static bound sqrt(D) max|w| + |b| (x 1 + 2^-6)."""
+    x = torch.randn(rows, H, D, device=DEV, generator=gen)
+    x = (x - x.mean(-1, keepdim=True)) / x.std(-1, keepdim=True, unbiased=False)
+    w = g * (1.0 + 0.02 * torch.randn(D, device=DEV, generator=gen))
+    b = 0.02 * torch.randn(D, device=DEV, generator=gen)
+    kb = (D ** 0.5 * float(w.abs().max()) + float(b.norm())) * (1.0 + 2.0 ** -6)
+    return (x * w + b).reshape(rows, C).bfloat16(), kb
+
+
+@pytest.mark.parametrize("g", [1.0, 2.0, 4.0, 8.0])
+def test_global_attention_qk_gain(ops, g):
+    """the hand-scheduled global sweep under trained-like qk-norm gains.  The
+    Cauchy-Schwarz bound qb = c |q| k_bound grows as g^2 (~12 at g = 1, ~196 at g = 4); the sweep
+    fixes m = max(0, qb - 64) per row, checked against the rows' max over the first three key tiles
+    (sr_attn.hip PIPE_HI / PIPE_LO).  g <= 4: EVERY wave runs the hand-scheduled sweep
+    (sr_attn_desc.sweep_stats), alone and paired with the reloc subsample pass; g = 8 (qb ~ 780,
+    outside the window) falls to the compiled loop.  Each against fp64 on sampled rows, and the
+    pair bit-identical to the two launches apart."""
+    L, nf = 32 * P, 32 * PP // 64 * 64
+    gen = torch.Generator(device=DEV).manual_seed(int(g * 10))
+    q, _ = _qk_gain(L, g, gen)
+    k, kb = _qk_gain(L, g, gen)
+    v = torch.randn(L, C, device=DEV, generator=gen).bfloat16()
+    qr, _ = _qk_gain(L, g, gen)
+    ks, kbs = _qk_gain(nf, g, gen)
+    vs = torch.randn(nf, C, device=DEV, generator=gen).bfloat16()
+    st = torch.zeros(2, dtype=torch.int32, device=DEV)
+    o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+    ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                  key_norm_max=kb, sweep_stats=st)
+    sp = torch.zeros(2, dtype=torch.int32, device=DEV)
+    og, orr = torch.empty_like(o), torch.empty_like(o)
+    lse = torch.empty(H, L, device=DEV)
+    ops.attention_pair(dict(q=q, k0=k, v0=v, o=og, lq=L, l0=L, key_norm_max=kb, sweep_stats=sp),
+                       dict(q=qr, k0=ks, v0=vs, o=orr, lq=L, l0=nf, key_norm_max=kbs, lse=lse.view(-1),
+                            sweep_stats=sp), heads=H, head_dim=D)
+    or1 = torch.empty_like(o)
+    lse1 = torch.empty_like(lse)
+    ops.attention(qr, ks, vs, or1, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=nf, k0_bstride=0,
+                  key_norm_max=kbs, lse=lse1.view(-1))
+    torch.cuda.synchronize()
+    waves = (L + 63) // 64 * H  # waves with query rows: 64 rows each
+    s1, s2 = st.tolist(), sp.tolist()
+    print(f"qk-gain {g}: asm / compiled waves: global {s1}, pair {s2}")
+    assert sum(s1) == waves and sum(s2) == 2 * waves
+    if g <= 4.0:
+        assert s1[1] == 0 and s2[1] == 0
+    else:
+        assert s1[1] > 0
+    assert torch.equal(og, o) and torch.equal(orr, or1) and torch.equal(lse, lse1)
+    scale = D ** -0.5
+    for q_, k_, v_, o_ in ((q, k, v, o), (qr, ks, vs, orr)):
+        rows = _sample_rows(L, 128, int(g)).to(DEV)
+        ref = _ref_rows(q_[rows], k_, v_, scale)
+        assert _rel(o_[rows].float(), ref) < 1e-2
+    # the second problem's LSE (log2 domain), as test_attention_pair
+    rws = _sample_rows(L, 32, 3).to(DEV)
+    for h in (0, H - 1):
+        c = slice(h * D, (h + 1) * D)
+        sc = (qr[rws][:, c].double() @ ks[:, c].double().T) * scale
+        l2 = torch.logsumexp(sc, -1) / math.log(2.0)
+        assert float(((lse[h, rws].double() - l2).abs() - 3e-3 * l2.abs()).max()) < 3e-2
+
+
+def test_attention_dma_base_bit31(ops):
+    """The round-3 fault's cause (readfirstlane returns int, and the widened low
+    word of the LDS-DMA base sign-extended into the high word when bit 31 was set; fixed at
+    sr_attn.hip's sp_lo / sp_hi): q / k / v placed so that every DMA base address the asm sweep
+    forms has bit 31 of its low word set.  The global attention and the pair launch there are
+    bit-identical to the same data at an ordinary address."""
+    L, nf = 171 * 64, 8 * PP // 64 * 64  # whole key tiles: the pair and the plain asm variant
+    q, k, v = _make(L, 21, spikes=(L - 9,))
+    ks, _, vs = _make(nf, 22)
+    kb, kbs = _kbound(k), _kbound(ks)
+    slab = 3 * L * C * 2 + 2 * nf * C * 2
+    big = torch.empty(slab + (1 << 32) + 4096, dtype=torch.uint8, device=DEV)
+    base = big.data_ptr()
+    off = ((0x90000000 - (base & 0xFFFFFFFF)) % (1 << 32) + 255) // 256 * 256
+    region = big[off:off + slab]
+    assert ((base + off) & 0xFFFFFFFF) >= 0x80000000 and ((base + off + slab) & 0xFFFFFFFF) >= 0x80000000
+
+    def at(t, start):
+        n = t.numel() * 2
+        dst = region[start:start + n].view(torch.bfloat16).view(t.shape)
+        dst.copy_(t)
+        return dst, start + n
+    s = 0
+    q2, s = at(q, s)
+    k2, s = at(k, s)
+    v2, s = at(v, s)
+    ks2, s = at(ks, s)
+    vs2, s = at(vs, s)
+    outs = []
+    for (qq, kk, vv, kks, vvs) in ((q, k, v, ks, vs), (q2, k2, v2, ks2, vs2)):
+        o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+        og, orr = torch.empty_like(o), torch.empty_like(o)
+        st = torch.zeros(2, dtype=torch.int32, device=DEV)
+        ops.attention(qq, kk, vv, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                      key_norm_max=kb, sweep_stats=st)
+        ops.attention_pair(dict(q=qq, k0=kk, v0=vv, o=og, lq=L, l0=L, key_norm_max=kb),
+                           dict(q=qq, k0=kks, v0=vvs, o=orr, lq=L, l0=nf, key_norm_max=kbs), heads=H, head_dim=D)
+        torch.cuda.synchronize()
+        assert st.tolist()[1] == 0  # every wave on the hand-scheduled sweep
+        outs.append((o, og, orr))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    del big

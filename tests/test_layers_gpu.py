@@ -163,3 +163,37 @@ def test_block_forward_with_mask(dev, short):
         y = m(x.to(dev), attn_mask=mask.to(dev))
     ref = O.block(sd, "", x, H, 1e-5, mask=mask)
     assert rel(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("N", [40, 600], ids=["short-kernel", "long-kernel"])
+@pytest.mark.parametrize("kind", ["bool", "float"])
+def test_attention_fully_masked_rows(dev, N, kind):
+    """ADVICE/VERDICT r3: a query row with no attended key (an all-False bool row, an all -inf
+    additive row) against torch's own SDPA (attention.py:103-109) on the same inputs: torch 2.10
+    returns zeros for such rows (safe softmax), and so does the fp32 kernel (both the short-key
+    and the tiled form); every other row matches to fp32 rounding."""
+    from sailrecon_amd import ops
+    import torch.nn.functional as F
+    B, H, D = 2, 3, 64
+    g = torch.Generator().manual_seed(21)
+    q, k, v = (torch.randn(B, H, N, D, generator=g) for _ in range(3))
+    if kind == "bool":
+        mask = torch.rand(B, H, N, N, generator=g) < 0.4
+        mask[0, 1, 3] = False
+        mask[1, :, N - 1] = False
+    else:
+        mask = torch.randn(B, H, N, N, generator=g)
+        mask[torch.rand(B, H, N, N, generator=g) < 0.4] = float("-inf")
+        mask[0, 1, 3] = float("-inf")
+        mask[1, :, N - 1] = float("-inf")
+    ref = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+    flat = lambda t: t.permute(0, 2, 1, 3).reshape(B * N, H * D).contiguous().to(dev)  # noqa: E731
+    o = torch.empty(B * N, H * D, device=dev)
+    mm = mask.to(dev) if kind == "float" else mask.to(dev).to(torch.uint8)
+    ops.attention(flat(q), flat(k), flat(v), o, heads=H, head_dim=D, batch=B, lq=N, q_bstride=N, l0=N,
+                  k0_bstride=N, mask_mode=ops._lib.SR_MASK_ADD if kind == "float" else ops._lib.SR_MASK_DENSE,
+                  mask=mm)
+    y = o.view(B, N, H, D).permute(0, 2, 1, 3).cpu()
+    assert torch.isfinite(y).all()
+    assert float(y[0, 1, 3].abs().max()) == 0.0 and float(y[1, :, N - 1].abs().max()) == 0.0
+    assert float((y - ref).abs().max()) < 1e-5

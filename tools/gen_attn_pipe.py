@@ -13,6 +13,11 @@ tile apart so that one q-block's MFMAs always have the other's VALU beside them:
   X(t): MFMA  QK1(t) kb0 | PV1(t-1) | QK1(t) kb1     VALU EXP0(t)   LDS K(t+1) -> Kset[t+1], V(t) -> Vset[t]
   Y(t): MFMA  QK0(t+1) kb0 | PV0(t) | QK0(t+1) kb1   VALU EXP1(t)   LDS-DMA of tile t+3
 
+Fixed offset m per query row (exp2 domain): every q.k^T chain starts from the accumulator
+operand %[mn<b>] = -m broadcast (16 VGPRs per q-block), so P = exp2(S) needs no max tracking;
+the C++ side picks m from the row's Cauchy-Schwarz bound (m = 0 when it is <= 64) and checks it
+against tile 0's row max.
+
 Every K and V fragment of a tile is read from LDS ONCE (into AGPR sets, double-buffered by tile
 parity) and used by both q-blocks.  Scores S_b (32 VGPRs per q-block) are named VGPRs; P
 overwrites its own scores in place (S_b[16:31], EXP order (1,0),(1,1),(0,0),(0,1)).  O, Q and
@@ -211,7 +216,10 @@ class Phase:
             b, kb, s, ps = p
             e.wait_read(kseqs.get((ps, kb, s)))
             acc = vr(S[b] + 16 * kb, 16)
-            c = "0" if s == 0 else acc
+            # the chain starts from -m (the row's fixed offset, broadcast over the lane's 16
+            # accumulator entries: every entry of a lane is a score of ONE query row), so the
+            # chain returns c q.k - m with no fold MFMA and no per-score subtraction
+            c = f"%[mn{b}]" if s == 0 else acc
             e.op(f"v_mfma_f32_32x32x16_bf16 {acc}, {ar(kfrag(ps, kb, s), 4)}, %[q{b}{s}], {c}")
         elif kind == "rs":
             b, i = p

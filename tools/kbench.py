@@ -135,6 +135,62 @@ def attn_pair():
               f"paired {tp:.3f} ms ({fl / tp / 1e9:.1f} TF/s)", flush=True)
 
 
+def qk_normed(rows, g, gen, H=16, D=64):
+    """[rows, H*D] bf16 as the aggregator's qk-norm produces it (attention.py:49-50,78): per-head
+    LayerNorm of a gaussian times w + b, w = g (1 + 0.02 n), b = 0.02 n (the synthetic rule's LN
+    affine scaled by the qk-gain g; trained q_norm / k_norm gains sit around 2-3).  Returns the
+    tensor and runtime.key_norm_bound's static bound sqrt(D) max|w| + |b| (x 1 + 2^-6)."""
+    x = torch.randn(rows, H, D, device=DEV, generator=gen)
+    x = (x - x.mean(-1, keepdim=True)) / x.std(-1, keepdim=True, unbiased=False)
+    w = g * (1.0 + 0.02 * torch.randn(D, device=DEV, generator=gen))
+    b = 0.02 * torch.randn(D, device=DEV, generator=gen)
+    kb = (D ** 0.5 * float(w.abs().max()) + float(b.norm())) * (1.0 + 2.0 ** -6)
+    return (x * w + b).reshape(rows, H * D).bfloat16(), kb
+
+
+def attn_gain():
+    """the hand-scheduled global sweep at qk-norm gains g = 1, 2, 4 (the bound
+    qb grows as g^2).  Global L = 43,968 alone and paired with the reloc subsample pass, with the
+    waves that ran the asm sweep / the compiled loop (sr_attn_desc.sweep_stats)."""
+    C, H, D, P, N = 1024, 16, 64, 1374, 32
+    L, nf = N * P, N * 305 // 64 * 64
+    fl1 = 4.0 * H * L * L * D
+    fl2 = 4.0 * H * L * (L + nf) * D
+    gains = [float(x) for x in os.environ.get("SR_QK_GAINS", "1,2,3,4").split(",")]
+    for g in gains:
+        gen = torch.Generator(device=DEV).manual_seed(1)
+        q, _ = qk_normed(L, g, gen)
+        k, kb = qk_normed(L, g, gen)
+        v = torch.randn(L, C, device=DEV, dtype=torch.bfloat16)
+        qr, _ = qk_normed(L, g, gen)
+        ks, kbs = qk_normed(nf, g, gen)
+        vs = torch.randn(nf, C, device=DEV, dtype=torch.bfloat16)
+        o, orr = torch.empty_like(q), torch.empty_like(q)
+        lse = torch.empty(H, L, device=DEV)
+        st = torch.zeros(2, dtype=torch.int32, device=DEV)
+
+        def glob(stats=None):
+            ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                          key_norm_max=kb, sweep_stats=stats)
+
+        def pair(stats=None):
+            ops.attention_pair(dict(q=q, k0=k, v0=v, o=o, lq=L, l0=L, key_norm_max=kb, sweep_stats=stats),
+                               dict(q=qr, k0=ks, v0=vs, o=orr, lq=L, l0=nf, key_norm_max=kbs, lse=lse.view(-1),
+                                    sweep_stats=stats), heads=H, head_dim=D)
+        glob(st)
+        torch.cuda.synchronize()
+        sg = st.tolist()
+        st.zero_()
+        pair(st)
+        torch.cuda.synchronize()
+        sp = st.tolist()
+        tg, tp = timeit(glob, reps=5), timeit(pair, reps=5)
+        qb = 1.4426950408889634 / 8 * kb * kb
+        print(f"attn qk-gain {g:.1f} (bound qb ~ {qb:6.1f}): global {tg:.3f} ms ({fl1 / tg / 1e9:.1f} TF/s, asm waves "
+              f"{sg[0]}/{sg[0] + sg[1]}); pair {tp:.3f} ms ({fl2 / tp / 1e9:.1f} TF/s, asm waves {sp[0]}/{sp[0] + sp[1]})",
+              flush=True)
+
+
 def attn_frame_diag():
     """Where the frame attention loses against the long sweep: the same launch with no ragged
     q-tile (lq = 1280 = 5 x 256), with full key tiles (l0 = 1408), and with 4x longer key sweeps
@@ -207,17 +263,17 @@ def attn_rank_seg():
                       "sr_attention")
         res = {}
         for seg in ("0", "1", "0", "1"):
-            os.environ["SR_ATTN_PIPE_SEG"] = seg
+            ops.set_tuning("SR_ATTN_PIPE_SEG", int(seg))
             ms = timeit(f, reps=10)
             res.setdefault(seg, []).append(ms)
         outs = []
         for seg in ("0", "1"):
-            os.environ["SR_ATTN_PIPE_SEG"] = seg
+            ops.set_tuning("SR_ATTN_PIPE_SEG", int(seg))
             o_parts.zero_()
             f()
             torch.cuda.synchronize()
             outs.append((o_parts[:S * lq].float().clone(), lse_parts.clone()))
-        os.environ.pop("SR_ATTN_PIPE_SEG")
+        ops.set_tuning("SR_ATTN_PIPE_SEG", 0)
         print(f"attn rank seg G={G} max |o| diff {float((outs[0][0] - outs[1][0]).abs().max()):.3e} "
               f"max |lse| diff {float((outs[0][1] - outs[1][1]).abs().max()):.3e}")
         for seg, v in res.items():
