@@ -188,6 +188,8 @@ class Aggregator(nn.Module):
         rank (broadcast from rank 0) so the draws do not depend on the world size.
         ``group=None`` disables sharding."""
         self._shard_group = group
+        if isinstance(group, RankSim):  # one rank's workload without peers (timing rehearsal)
+            return
         if group is not None:
             seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
             dist = torch.distributed
@@ -201,6 +203,8 @@ class Aggregator(nn.Module):
         g = getattr(self, "_shard_group", None)
         if g is None:
             return None, 1, 0
+        if isinstance(g, RankSim):
+            return g, g.world, g.rank
         return g, torch.distributed.get_world_size(g), torch.distributed.get_rank(g)
 
     # ------------------------------------------------------------------ forward
@@ -751,6 +755,10 @@ def gather_rows(dst: torch.Tensor, src: torch.Tensor, counts: List[int], group, 
     rank straight into that rank's slot of ``dst`` — the rows land compact, so no padding row
     can reach a softmax.  Returns the works to wait on."""
     dist = torch.distributed
+    if isinstance(group, RankSim):  # no peers: this rank's rows land in its slot, the others stay as they are
+        off = sum(counts[:rank])
+        dst[off:off + counts[rank]].copy_(src)
+        return []
     if len(set(counts)) == 1:
         return [dist.all_gather_into_tensor(dst, src, group=group, async_op=True)]
     offs = np.concatenate([[0], np.cumsum(counts)]).tolist()
@@ -758,3 +766,19 @@ def gather_rows(dst: torch.Tensor, src: torch.Tensor, counts: List[int], group, 
         dst[offs[rank]:offs[rank + 1]].copy_(src)
     return [dist.broadcast(dst[offs[j]:offs[j + 1]], src=dist.get_global_rank(group, j), group=group, async_op=True)
             for j in range(len(counts)) if counts[j]]
+
+
+class RankSim:
+    """Stand-in process group for ONE rank of a ``world``-rank frame-sharded forward, run alone on
+    one GPU (``Aggregator.set_frame_sharding(RankSim(8, 0))``): the rank computes exactly its
+    share -- its frames' DINO / frame / MLP work, the global block's local and remote attention
+    passes over every anchor's keys, the reloc block against the whole anchor subsample, the
+    replicated camera head -- but the gathers move nothing (the peers' slots of the gathered K/V
+    buffers keep whatever they hold).  Its outputs are therefore NOT the model's; it exists to time
+    a rank's step and host submit cost before a multi-GPU run (tools/rank_sim.py)."""
+
+    def __init__(self, world: int, rank: int):
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside a world of {world}")
+        self.world, self.rank = int(world), int(rank)
+

@@ -81,7 +81,15 @@ def _positions(qkv, M):
 
 def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None, lse=None,
-              key_norm_max=0.0, mask=None, tail_readable=False):
+              key_norm_max=0.0, mask=None, tail_readable=False, merge_o=None, merge_lse=None, sweep_stats=None):
+    """sr_attention's semantics (include/sfm_amd.h sr_attn_desc): the camera mask, SR_MASK_DENSE
+    (nonzero = attend) / SR_MASK_ADD masks with zeros for a row without attended keys, and the
+    merge-in of a disjoint key set's (merge_o, merge_lse).  sweep_stats (device diagnostics) is
+    rejected: there is no sweep here."""
+    if sweep_stats is not None:
+        raise NotImplementedError("cpu_ops.attention: sweep_stats counts GPU waves")
+    if mask_mode in (_lib.SR_MASK_DENSE, _lib.SR_MASK_ADD) and mask is None:
+        raise ValueError("cpu_ops.attention: dense / additive mask_mode without a mask")
     D = head_dim
     scale = D ** -0.5 if scale is None else scale
     for b in range(batch):
@@ -92,6 +100,7 @@ def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bst
             ks.append(k1[b * k1_bstride:b * k1_bstride + l1].float())
             vs.append(v1[b * k1_bstride:b * k1_bstride + l1].float())
         kk, vv = torch.cat(ks), torch.cat(vs)
+        rows = slice(b * q_bstride, b * q_bstride + lq)
         for h in range(heads):
             sl = slice(h * D, (h + 1) * D)
             s = (qs[:, sl] @ kk[:, sl].t()) * scale
@@ -99,9 +108,23 @@ def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bst
                 i = torch.arange(lq)[:, None]
                 j = torch.arange(kk.shape[0])[None]
                 s = s.masked_fill(~((j < n_anchor) | (j == i)), float("-inf"))
-            o[b * q_bstride:b * q_bstride + lq, sl] = (torch.softmax(s, -1) @ vv[:, sl]).to(o.dtype)
+            elif mask_mode == _lib.SR_MASK_DENSE:
+                s = s.masked_fill(mask[b, h].to(torch.bool).logical_not(), float("-inf"))
+            elif mask_mode == _lib.SR_MASK_ADD:
+                s = s + mask[b, h].float()
+            l2 = torch.logsumexp(s, -1) * (1.0 / math.log(2.0))
+            p = torch.softmax(s, -1).nan_to_num(0.0)  # a row without attended keys: zeros (torch SDPA)
+            y = p @ vv[:, sl]
+            if merge_o is not None:  # sr_attn_merge's formula over the two disjoint key sets
+                la = merge_lse[h, rows].float()
+                m = torch.maximum(la, l2)
+                wa, wb = torch.exp2(la - m), torch.exp2(l2 - m)
+                tot = wa + wb
+                y = (merge_o[rows, sl].float() * (wa / tot)[:, None] + y * (wb / tot)[:, None])
+                l2 = m + torch.log2(tot)
+            o[rows, sl] = y.to(o.dtype)
             if lse is not None:
-                lse.view(batch, heads, lq)[b, h] = torch.logsumexp(s, -1) * (1.0 / math.log(2.0))
+                lse.view(batch, heads, lq)[b, h] = l2
 
 
 def attn_merge(o_a, lse_a, o_b, lse_b, out, *, heads, head_dim, lse_out=None, tag=None):

@@ -153,3 +153,32 @@ def test_sharded_global_partials_plan(G, r, force):
                           lq=lq, q_bstride=0, l0=La, k0_bstride=0)
     err = float((o.float() - ref).norm() / ref.norm())
     assert err < 1e-2, err
+
+
+def test_rank_sim_rehearsal_matches_shard_shapes():
+    """aggregator.RankSim (tools/rank_sim.py): one rank of a 3-rank frame-sharded forward run
+    alone, gathers replaced by the rank's own slot -- its local frame work and outputs have the
+    sharded rank's shapes, and its frame-block half of the intermediate maps (which needs no
+    peer) equals the real 3-rank run's rank 1 (the reference golden's rows of that rank)."""
+    for p in (REPO, os.path.join(REPO, "self-supervise-sfm_amd"), HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import cpu_ops
+    from goldens import load_npz
+    from test_host_cpu import small_model
+    from sailrecon_amd.models.aggregator import RankSim, shard_range
+
+    g = load_npz("g1_small_56_n5.npz")
+    images = torch.from_numpy(g["images"])
+    no_reloc, reloc = _lists(g)
+    m = small_model()
+    m.aggregator.set_frame_sharding(RankSim(3, 1))
+    m.aggregator.generator.manual_seed(0)
+    with cpu_ops.installed(), torch.no_grad():
+        feats, psi, cam_last = m.aggregator(images, no_reloc, reloc, fix_rank=int(g["fix_rank"]))
+    q0, nq = shard_range(len(reloc), 3, 1)
+    assert feats[1].shape[1] == nq and cam_last.shape[1] == len(no_reloc)
+    ref = g["feat_0"][0][q0:q0 + nq]
+    C = ref.shape[-1] // 2
+    # layer 0's frame half: frame block 0 of this rank's own query frames, no exchange involved
+    assert np.abs(feats[0][0].numpy()[..., :C] - ref[..., :C]).max() < 1e-4

@@ -28,7 +28,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo"):
+def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo", shard=True):
     for p in (REPO, os.path.join(REPO, "self-supervise-sfm_amd"), HERE):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -42,7 +42,11 @@ def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo"):
     from sailrecon_amd.utils.pose_enc import pose_encoding_to_extri_intri
     from test_parity_gpu import Hot
 
-    g = load_npz(golden)
+    if isinstance(golden, dict):  # no reference golden at this size: the synthetic scene's spec
+        g = dict(golden)
+        g["sample_rows"] = np.sort(np.random.default_rng(5).choice(g["n_views"] * 1374, 512, replace=False))
+    else:
+        g = load_npz(golden)
     n = int(g["n_views"])
     full = "img" in g
     torch.manual_seed(0)
@@ -62,7 +66,8 @@ def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo"):
         layers = (0, 1)
     m = m.cuda()
     images = images.cuda()
-    m.aggregator.set_frame_sharding(dist.group.WORLD)  # nccl: the seed broadcast as a device tensor
+    if shard:
+        m.aggregator.set_frame_sharding(dist.group.WORLD)  # nccl: the seed broadcast as a device tensor
     m.aggregator.shard_overlap = overlap
     if backend == "nccl":  # gather_rows' RCCL all_gather_into_tensor on the K/V row layout
         from sailrecon_amd.models.aggregator import gather_rows
@@ -97,12 +102,17 @@ def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo"):
     dist.destroy_process_group()
 
 
+def _spawn(tmp_path, world, golden, mode, overlap=True, backend="gloo", shard=True):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), golden, mode, overlap, backend, shard),
+             nprocs=world, join=True)
+    return [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+
+
 def _run(tmp_path, world, golden, mode, overlap=True, backend="gloo"):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from goldens import load_npz, rel_l2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), golden, mode, overlap, backend), nprocs=world,
-             join=True)
+    _spawn(tmp_path, world, golden, mode, overlap, backend)
     g = load_npz(golden)
     rs = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     tol = TOL[mode]
@@ -149,3 +159,40 @@ def test_frame_sharded_c2_518_n8_two_ranks(tmp_path, mode):
     """BASELINE config 2 (N=8 views @518) split over 2 ranks: 4 anchors + 4 queries each; the
     global block's local pass runs on 5,496 keys, the remote pass on the other 5,496."""
     _run(tmp_path, 2, "g9_518_n8.npz", mode)
+
+
+@pytest.mark.parametrize("world,mode", [(2, "fp32"), (3, "bf16"), (3, "fp32")], ids=["2rk-fp32", "3rk-bf16", "3rk-fp32"])
+def test_frame_sharded_c3_518_n32(tmp_path, world, mode):
+    """BASELINE config 3 (the headline scene, N=32 views @518) frame-sharded
+    over 2 ranks (16 / 16 anchors + queries) and 3 ranks (the uneven 11 / 11 / 10 split; the
+    middle rank's remote global-attention pass has two key segments), every rank's features,
+    camera tokens and poses against the reference golden g10 (fp32 1e-4, bf16 3e-2)."""
+    _run(tmp_path, world, "g10_518_n32.npz", mode)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_frame_sharded_n64_matches_one_rank(tmp_path, world):
+    """The north-star scaling workload (64 views @518, global L = 87,936) sharded over 2 / 3
+    ranks against the same scene on one rank without sharding (no reference golden exists at
+    this size: the reference needs hours and 30 GB of dense mask on the CPU).  bf16: the sharded
+    run splits the global softmax into local / remote passes merged by LSE and key-split
+    partials, so it differs from the one-rank run by bf16 rounding only (measured values printed)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from goldens import rel_l2
+    spec = {"n_views": 64, "img": 518, "fix_rank": 300}
+    (tmp_path / "one").mkdir()
+    one = _spawn(tmp_path / "one", 1, spec, "bf16", shard=False)[0]
+    rs = _spawn(tmp_path, world, spec, "bf16")
+    errs = {}
+    for layer in (4, 11, 17, 23):
+        for key in ("rownorm", "cam", "rows"):
+            full = np.concatenate([r[f"feat_{layer}_{key}"] for r in rs], axis=0)
+            errs[f"{layer}_{key}"] = rel_l2(full, one[f"feat_{layer}_{key}"])
+    for i, r in enumerate(rs):
+        for k in ("cam_last", "pose", "ext"):
+            errs[f"rank{i}_{k}"] = rel_l2(r[k], one[k])
+    print(f"N=64 sharded over {world} vs one rank (bf16, rel-L2):", {k: float(f"{v:.2e}") for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items() if not v < 2e-2}
+    assert not bad, bad
+
