@@ -122,13 +122,16 @@ int layernorm_dispatch(hipStream_t s, const float* x, int64_t ldx, const int32_t
 // followed by norm2, in one pass over the rows (the GEMM's fp32 residual read-modify-write
 // epilogue ran serialized behind each CU's MFMAs; here it streams at the HBM rate).  One wave per
 // row, ln_rows_per_wave rows in flight, 4-wide vectors.
-template <int NPL, int RPW, typename TY, typename TO>
+// W = columns per lane-vector: 4 (float4 x, 8-B bf16 y / out) or 8 (two float4 of x, ONE 16-B
+// bf16x8 of y and of out: every load and store of the row is 16 B wide).
+template <int NPL, int RPW, typename TY, typename TO, int W = 4>
 __global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64_t ldx, const TY* __restrict__ y,
                                                                  int64_t ldy, const float* __restrict__ gamma,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ b, float eps,
                                                                  TO* __restrict__ out, int64_t ldo, int rows) {
-  constexpr int NV = NPL / 4;
+  static_assert(W == 4 || W == 8, "lane vector width");
+  constexpr int NV = NPL / W;
   constexpr int COLS = NPL * 64;
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -142,28 +145,40 @@ __global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64
     const TY* yr = y + (int64_t)row * ldy;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      const float4 t = *(const float4*)(xr + col);
-      v[r][i * 4 + 0] = t.x; v[r][i * 4 + 1] = t.y; v[r][i * 4 + 2] = t.z; v[r][i * 4 + 3] = t.w;
-      if constexpr (sr::is_bf16<TY>::value) {
+      const int col = (i * 64 + lane) * W;
+#pragma unroll
+      for (int h = 0; h < W / 4; ++h) {
+        const float4 t = *(const float4*)(xr + col + 4 * h);
+        v[r][i * W + 4 * h + 0] = t.x; v[r][i * W + 4 * h + 1] = t.y;
+        v[r][i * W + 4 * h + 2] = t.z; v[r][i * W + 4 * h + 3] = t.w;
+      }
+      if constexpr (sr::is_bf16<TY>::value && W == 8) {
+        const bf16x8 u = *(const bf16x8*)(yr + col);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) yv[r][i * 8 + j] = (float)u[j];
+      } else if constexpr (sr::is_bf16<TY>::value) {
         const bf16x4 u = *(const bf16x4*)(yr + col);
 #pragma unroll
         for (int j = 0; j < 4; ++j) yv[r][i * 4 + j] = (float)u[j];
       } else {
-        const float4 u = *(const float4*)(yr + col);
-        yv[r][i * 4 + 0] = u.x; yv[r][i * 4 + 1] = u.y; yv[r][i * 4 + 2] = u.z; yv[r][i * 4 + 3] = u.w;
+#pragma unroll
+        for (int h = 0; h < W / 4; ++h) {
+          const float4 u = *(const float4*)(yr + col + 4 * h);
+          yv[r][i * W + 4 * h + 0] = u.x; yv[r][i * W + 4 * h + 1] = u.y;
+          yv[r][i * W + 4 * h + 2] = u.z; yv[r][i * W + 4 * h + 3] = u.w;
+        }
       }
     }
   }
   float gv[NPL], wv[NPL], bv[NPL];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int col = (i * 64 + lane) * 4;
+    const int col = (i * 64 + lane) * W;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      gv[i * 4 + j] = gamma ? gamma[col + j] : 1.f;
-      wv[i * 4 + j] = w ? w[col + j] : 1.f;
-      bv[i * 4 + j] = w ? b[col + j] : 0.f;
+    for (int j = 0; j < W; ++j) {
+      gv[i * W + j] = gamma ? gamma[col + j] : 1.f;
+      wv[i * W + j] = w ? w[col + j] : 1.f;
+      bv[i * W + j] = w ? b[col + j] : 0.f;
     }
   }
 #pragma unroll
@@ -175,7 +190,11 @@ __global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64
     if (row < rows) {
 #pragma unroll
       for (int i = 0; i < NV; ++i)
-        *(float4*)(xr + (i * 64 + lane) * 4) = make_float4(v[r][i * 4], v[r][i * 4 + 1], v[r][i * 4 + 2], v[r][i * 4 + 3]);
+#pragma unroll
+        for (int h = 0; h < W / 4; ++h) {
+          const int k = i * W + 4 * h;
+          *(float4*)(xr + (i * 64 + lane) * W + 4 * h) = make_float4(v[r][k], v[r][k + 1], v[r][k + 2], v[r][k + 3]);
+        }
     }
     float s = 0.f;
 #pragma unroll
@@ -192,15 +211,22 @@ __global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64
     TO* orow = out + (int64_t)row * ldo;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      float o4[4];
+      const int col = (i * 64 + lane) * W;
+      float ow[W];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o4[j] = fmaf(v[r][i * 4 + j] * rstd, wv[i * 4 + j], bv[i * 4 + j]);
-      if constexpr (sr::is_bf16<TO>::value) {
-        const bf16x4 o = {(bf16)o4[0], (bf16)o4[1], (bf16)o4[2], (bf16)o4[3]};
+      for (int j = 0; j < W; ++j) ow[j] = fmaf(v[r][i * W + j] * rstd, wv[i * W + j], bv[i * W + j]);
+      if constexpr (sr::is_bf16<TO>::value && W == 8) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)ow[j];
+        *(bf16x8*)(orow + col) = o;
+      } else if constexpr (sr::is_bf16<TO>::value) {
+        const bf16x4 o = {(bf16)ow[0], (bf16)ow[1], (bf16)ow[2], (bf16)ow[3]};
         *(bf16x4*)(orow + col) = o;
       } else {
-        *(float4*)(orow + col) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+#pragma unroll
+        for (int h = 0; h < W / 4; ++h)
+          *(float4*)(orow + col + 4 * h) = make_float4(ow[4 * h], ow[4 * h + 1], ow[4 * h + 2], ow[4 * h + 3]);
       }
     }
   }
@@ -211,9 +237,21 @@ int residual_layernorm_dispatch(hipStream_t s, float* x, int64_t ldx, const TY* 
                                 const float* w, const float* b, float eps, TO* out, int64_t ldo, int rows, int cols) {
   // rows in flight per wave as the LayerNorm (kbench M = 87,936, C = 1024: 1 row 3.5 TB/s, 2 rows
   // 4.86, 4 rows 4.96 TB/s of the 12 B per element moved)
-#define RLN_LAUNCH(C, R)                                                                                        \
-  hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), \
-                     0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows)
+  // 16-B lane vectors (W = 8) where every row is 512-column blocks and 16-B aligned
+  const bool w8 = cols % 512 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && ldx % 4 == 0 &&
+                  (((uintptr_t)y | (uintptr_t)out | (uintptr_t)x) & 15) == 0;
+#define RLN_LAUNCH(C, R)                                                                                          \
+  do {                                                                                                            \
+    if constexpr (C % 512 == 0) {                                                                                 \
+      if (w8) {                                                                                                   \
+        hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO, 8>), dim3((rows + 4 * R - 1) / (4 * R)), \
+                           dim3(256), 0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows);                    \
+        break;                                                                                                    \
+      }                                                                                                           \
+    }                                                                                                             \
+    hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO, 4>), dim3((rows + 4 * R - 1) / (4 * R)),     \
+                       dim3(256), 0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows);                        \
+  } while (0)
 #define RLN_CASE(C)                                                                                             \
   case C:                                                                                                       \
     RLN_LAUNCH(C, ln_rows_per_wave(C / 64));                                                                    \

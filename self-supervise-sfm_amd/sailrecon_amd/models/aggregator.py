@@ -247,9 +247,15 @@ class Aggregator(nn.Module):
             dtab = dtab.detach().float().contiguous()[None]
             zero_t = ws.get("frame_type0", F_, 1, torch.int32, dev).zero_()
             ops.set_special_tokens(x, F_, P, dtab, zero_t)
-            for blk in dino.blocks:
+            pending = []  # fc2 residual of block i folded into block i+1's LN1 (runtime.Pending)
+            nblk = len(dino.blocks)
+            for i, blk in enumerate(dino.blocks):
                 pb = blk.packed(dtype)
-                runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True), None)
+                p = runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True), None,
+                                      pending=pending, defer=i < nblk - 1)
+                if p is not None:
+                    pending.append(p)
+            assert not pending
             ops.layernorm(x, dino.norm.weight, dino.norm.bias, dino.norm.eps, x)  # in place (row-local)
 
         # ---- aggregator special tokens, aggregator.py:287-299 (type by ORIGINAL frame index)
@@ -350,10 +356,11 @@ class Aggregator(nn.Module):
         cam_flat = cam_loc.view(B * Na_l, 2 * C)
 
         # ---- alternating layers, aggregator.py:339-423
+        pending = []  # the global / reloc blocks' fc2 residuals, folded into the next frame block's LN1
         for l in range(self.depth):
             pb = self.frame_blocks[l].packed(dtype)
             runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True),
-                              runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
+                              runtime.qkv_params(pb, rope, pos_row_base=0, **posctx), pending=pending)
             if l in out_maps and Nq_l > 0:  # frame half of the intermediate, :403-413
                 for b in range(B):
                     ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, :C],
@@ -362,11 +369,15 @@ class Aggregator(nn.Module):
                 ops.copy_rows(cam_flat[:, :C], x, B * Na_l, rowmap=anchor_rows0)
             pr = self.global_reloc_blocks[l].packed(dtype)
             pg = self.global_blocks[l].packed(dtype)
+            # the next reader of x after this layer's global / reloc blocks is the next frame block's LN1,
+            # unless an output map or the camera tokens copy x first
+            defer = l + 1 < self.depth and l not in out_maps and not fill_cache and \
+                os.environ.get("SR_CONCURRENT_STACKS", "0") != "1"
             for b in range(B):
                 a0, q0, q1 = b * S_l * P, b * S_l * P + Na_l * P, (b + 1) * S_l * P
-                self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if need_sub else None, Pp, a0, q0, q1,
-                                   Nq_l, P, rope, posctx, dtype, dev, group, G, r, a_counts, need_sub,
-                                   cache_layer=l if fill_cache else None)
+                pending += self._layer_global(pr, pg, x, sc, rowmap_t[l, b] if need_sub else None, Pp, a0, q0, q1,
+                                              Nq_l, P, rope, posctx, dtype, dev, group, G, r, a_counts, need_sub,
+                                              cache_layer=l if fill_cache else None, defer=defer)
             if l in out_maps and Nq_l > 0:  # reloc half
                 for b in range(B):
                     ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, C:],
@@ -466,12 +477,18 @@ class Aggregator(nn.Module):
 
     # ------------------------------------------------------------------ stacks
     def _layer_global(self, pr, pg, x, sc, rowmap, Pp, a0, q0, q1, Nq_l, P, rope, posctx, dtype, dev,
-                      group, G, r, a_counts, need_sub, cache_layer=None):
+                      group, G, r, a_counts, need_sub, cache_layer=None, defer=False) -> list:
         """global_reloc (queries, aggregator.py:672-741) + global (anchors, :743-769) blocks of
         one layer for one batch item.  With G > 1 the anchor K/V and the anchor-subsample K/V
         are gathered asynchronously (``gather_rows``; ``a_counts`` = anchor frames per rank):
         the subsample K/V behind the query-side QKV GEMM, the anchor K/V behind the whole reloc
-        block and the local-anchor attention pass."""
+        block and the local-anchor attention pass.  ``defer``: the two blocks' fc2 residuals are
+        returned as runtime.Pending updates for the next frame block's LN1 (else [])."""
+        out = []
+
+        def keep(p):
+            if p is not None:
+                out.append(p)
         C = pg.dim
         ws = self._ws
         La_l = q0 - a0                 # local anchor tokens
@@ -551,9 +568,9 @@ class Aggregator(nn.Module):
                      l0=n_full, key_norm_max=runtime.key_norm_bound(pr), lse=lse_a.view(-1)),
                 heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
             self._reloc_own_pass(pr, qkv_r, kv_sub_all, sc.o[q0:q1], o_a, lse_a, Nq_l, P, n_sub_all, n_full)
-            runtime.run_block_tail(pr, x, q0, q1, sc)
-            runtime.run_block_tail(pg, x, a0, q0, sc)
-            return
+            keep(runtime.run_block_tail(pr, x, q0, q1, sc, defer=defer))
+            keep(runtime.run_block_tail(pg, x, a0, q0, sc, defer=defer))
+            return out
         # G == 1: the reloc block (query rows) and the global block (anchor rows) are independent.
         # SR_CONCURRENT_STACKS=1 runs the reloc block on a side stream so that each could fill the
         # other's last partial wave.  Round 1: 3% SLOWER at N=32 (68.7 -> 66.7 views/s).  Round 3,
@@ -593,8 +610,8 @@ class Aggregator(nn.Module):
                     runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
                                       runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
             else:
-                runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
-                                  runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
+                keep(runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
+                                       runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx), defer=defer))
         _wait(work_sub)  # a rank without query frames still fed the others (send buffer reuse)
         if G > 1:
             o, q = sc.o[a0:q0], sc.qkv[a0:q0, 0:C]
@@ -604,14 +621,15 @@ class Aggregator(nn.Module):
             else:
                 _wait(work_kv)
                 self._global_attention(q, kv_all[:, 0:C], kv_all[:, C:2 * C], o, pg, La_l, La)
-            runtime.run_block_tail(pg, x, a0, q0, sc)
+            keep(runtime.run_block_tail(pg, x, a0, q0, sc, defer=defer))
         else:
             def attend_global(qkv, o):
                 self._global_attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, pg, La, La)
-            runtime.run_block(pg, x, a0, q0, sc, attend_global, runtime.qkv_params(pg, rope, pos_row_base=a0,
-                                                                                    **posctx))
+            keep(runtime.run_block(pg, x, a0, q0, sc, attend_global,
+                                   runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx), defer=defer))
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)  # join before the next frame block
+        return out
 
     def set_fp8_global(self, enabled: bool = True, fp8_v: bool = False):
         """Global blocks' q.k^T in block-scaled fp8 (BASELINE C5); with ``fp8_v`` also V and P.V.

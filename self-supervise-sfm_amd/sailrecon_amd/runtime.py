@@ -185,21 +185,59 @@ def qkv_params(pb: PackedBlock, rope: Optional[Tuple[Tensor, Tensor]], **pos) ->
     return d
 
 
-# SR_FUSED_RESID_LN=1 (opt-in, read at import): the projection GEMM's plain bias epilogue +
-# sr_residual_layernorm instead of its fp32 residual epilogue + sr_layernorm.  Correct (the GPU suite
-# and the C2 / C3 goldens pass under it) and it lifts the GEMMs' MFMA utilisation (0.378 -> 0.391 at
-# C3), but the step does not get faster (409.9 / 409.9 vs 409.1 / 408.6 ms, one box, interleaved):
-# the fused pass moves 12 B per element at 4.96 TB/s (0.218 ms at M = 87,936 against LayerNorm's
-# 0.104 ms), which is what the GEMM epilogue saved, and fc1 then reads xn from HBM rather than MALL.
+# Residual updates folded into the next LayerNorm.  The reference's autocast
+# Linear returns bf16 and LayerScale / the residual add happen outside it (block.py:86-112,
+# layer_scale.py:22-23); so the proj / fc2 GEMMs may end in the plain bias epilogue (their output
+# in the compute dtype, as the reference has it) and x += gamma * y streams through
+# sr_residual_layernorm together with the LayerNorm that reads x next:
+#   SR_FUSED_RESID_LN=1: proj -> LN2 of the same block;
+#   SR_DEFER_RESID=1:    fc2 -> LN1 of the next block over the same rows (DINO block i -> i+1; the
+#                        global / reloc blocks of layer l -> the frame block of layer l+1), where no
+#                        other reader of x comes in between (Pending / run_block's ``pending``).
+# Measured (round 3, proj only): the GEMMs' MFMA utilisation 0.378 -> 0.391 at C3 and the step even
+# (409.9 / 409.9 vs 409.1 / 408.6 ms): the fused pass moves 12 B per element where LayerNorm moves 6.
 _FUSED_RESID_LN = os.environ.get("SR_FUSED_RESID_LN", "0") == "1"
+_DEFER_RESID = os.environ.get("SR_DEFER_RESID", "0") == "1"
+
+
+@dataclass
+class Pending:
+    """A residual update x[r0:r1] += gamma * y deferred to the next LayerNorm over those rows
+    (y [r1 - r0, C] in the compute dtype: a GEMM's bias-epilogue output)."""
+    r0: int
+    r1: int
+    y: Tensor
+    gamma: Tensor
+
+
+def defer_enabled(pb: PackedBlock) -> bool:
+    return _DEFER_RESID and pb.w_fc2 is not None and pb.w_fc2.shape[0] in ops.RESIDUAL_LN_COLS
+
+
+def layernorm_pending(x: Tensor, r0: int, r1: int, w, b, eps: float, xn: Tensor, pending) -> None:
+    """xn = LN(x[r0:r1]) after applying the ``pending`` residual updates that cover these rows
+    (each one exactly once: applied updates are removed from the list)."""
+    if not pending:
+        ops.layernorm(x[r0:r1], w, b, eps, xn)
+        return
+    cur = r0
+    for p in sorted([p for p in pending if p.r0 < r1 and p.r1 > r0], key=lambda p: p.r0):
+        if p.r0 < r0 or p.r1 > r1:
+            raise RuntimeError("a pending residual update straddles the LayerNorm's rows")
+        if cur < p.r0:
+            ops.layernorm(x[cur:p.r0], w, b, eps, xn[cur - r0:p.r0 - r0])
+        ops.residual_layernorm(x[p.r0:p.r1], p.y, p.gamma, w, b, eps, xn[p.r0 - r0:p.r1 - r0])
+        pending.remove(p)
+        cur = p.r1
+    if cur < r1:
+        ops.layernorm(x[cur:r1], w, b, eps, xn[cur - r0:])
 
 
 def proj_residual_ln2(pb: PackedBlock, xs: Tensor, o: Tensor, qkv: Tensor, xn: Tensor) -> None:
     """xs += g1 * proj(o); xn = norm2(xs) (block.py:86-89).  Default: the projection GEMM's fp32
-    bias*gamma + residual epilogue, then LayerNorm.  Opt-in (SR_FUSED_RESID_LN=1): the GEMM writes
-    its bias output in the compute dtype into the dead q slot of ``qkv`` (the reference's autocast
-    Linear returns bf16 too) and sr_residual_layernorm streams the residual update and LN2 in one
-    pass."""
+    bias*gamma + residual epilogue, then LayerNorm.  SR_FUSED_RESID_LN=1: the GEMM writes its bias
+    output in the compute dtype into the dead q slot of ``qkv`` and sr_residual_layernorm streams
+    the residual update and LN2 in one pass."""
     C = pb.w_proj.shape[0]
     if _FUSED_RESID_LN and C in ops.RESIDUAL_LN_COLS and qkv.shape[1] >= C:
         y = qkv[:, :C]
@@ -210,22 +248,37 @@ def proj_residual_ln2(pb: PackedBlock, xs: Tensor, o: Tensor, qkv: Tensor, xn: T
         ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
 
 
+def mlp_residual(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch, defer: bool) -> Optional[Pending]:
+    """fc1 (+GELU) and fc2 with the LayerScale residual: x[r0:r1] += g2 * fc2(gelu(fc1(xn))).
+    ``defer``: fc2 ends in the bias epilogue into the block's dead attention-output rows sc.o and
+    the update is returned as a Pending for the next LayerNorm over these rows."""
+    xs, xn, h, o = x[r0:r1], sc.xn[r0:r1], sc.h[r0:r1], sc.o[r0:r1]
+    hid = pb.w_fc1.shape[0]
+    ops.gemm(xn, pb.w_fc1, h[:, :hid], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
+    if defer and defer_enabled(pb) and o.shape[1] >= pb.w_fc2.shape[0]:
+        y = o[:, :pb.w_fc2.shape[0]]
+        ops.gemm(h[:, :hid], pb.w_fc2, y, _lib.SR_EPI_BIAS, bias=pb.b_fc2, tag="gemm")
+        return Pending(r0, r1, y, pb.g2)
+    ops.gemm(h[:, :hid], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2, tag="gemm")
+    return None
+
+
 def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
-              attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict], tag: str = "blk") -> None:
+              attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict], tag: str = "blk",
+              pending: Optional[list] = None, defer: bool = False) -> Optional[Pending]:
     """x[r0:r1] <- Block(x[r0:r1]); ``attend(qkv_rows, o_rows)`` launches the attention.
-    ``tag`` prefixes the kernel-timer tags of the four GEMMs (e.g. "global.qkv")."""
+    ``pending``: deferred residual updates of earlier blocks, applied by this block's LN1 (the list
+    is consumed).  ``defer``: leave this block's fc2 residual pending (returned; see mlp_residual)."""
     xs = x[r0:r1]
-    xn, qkv, o, h = sc.xn[r0:r1], sc.qkv[r0:r1], sc.o[r0:r1], sc.h[r0:r1]
-    ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, xn)
+    xn, qkv, o = sc.xn[r0:r1], sc.qkv[r0:r1], sc.o[r0:r1]
+    layernorm_pending(x, r0, r1, pb.ln1_w, pb.ln1_b, pb.eps, xn, pending)
     if qkv_epi is None:
         ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
     else:
         ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
     attend(qkv, o)
     proj_residual_ln2(pb, xs, o, qkv, xn)
-    ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
-    ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2,
-             tag="gemm")
+    return mlp_residual(pb, x, r0, r1, sc, defer)
 
 
 def run_block_head(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch, qkv_epi: Optional[dict]) -> None:
@@ -240,15 +293,14 @@ def run_block_head(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
         ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
 
 
-def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch) -> None:
+def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
+                   defer: bool = False) -> Optional[Pending]:
     """Second half of run_block (proj + residual, LN2, MLP + residual) when the attention
     output sc.o[r0:r1] was produced separately (frame-sharded global block)."""
     xs = x[r0:r1]
-    xn, o, h = sc.xn[r0:r1], sc.o[r0:r1], sc.h[r0:r1]
+    xn, o = sc.xn[r0:r1], sc.o[r0:r1]
     proj_residual_ln2(pb, xs, o, sc.qkv[r0:r1], xn)
-    ops.gemm(xn, pb.w_fc1, h[:, : pb.w_fc1.shape[0]], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
-    ops.gemm(h[:, : pb.w_fc1.shape[0]], pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2,
-             tag="gemm")
+    return mlp_residual(pb, x, r0, r1, sc, defer)
 
 
 def frame_attend(pb: PackedBlock, frames: int, tokens: int, tail_readable: bool = False) -> Callable[[Tensor, Tensor], None]:

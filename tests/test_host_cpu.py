@@ -96,3 +96,43 @@ def test_product_path_refuses_cpu_tensors():
     m = small_model()
     with pytest.raises(RuntimeError, match="HIP path only"):
         m.aggregator(torch.from_numpy(g["images"]), [0, 1], [2, 3], fix_rank=10)
+
+
+def test_deferred_residuals_equal_fused_epilogues(monkeypatch):
+    """the proj residual folded into LN2 (SR_FUSED_RESID_LN) and the fc2
+    residual deferred to the next LayerNorm over the same rows (SR_DEFER_RESID: DINO block i ->
+    i + 1, the global / reloc blocks of layer l -> the frame block of layer l + 1 when no output
+    map or camera-token copy reads x in between) give the same forward as the GEMMs' residual
+    epilogues: the host bookkeeping of runtime.Pending (which rows, which gamma, applied once)."""
+    from sailrecon_amd import ops, runtime
+    from sailrecon_amd.heads.camera_head import CameraHead
+    from sailrecon_amd.models.aggregator import Aggregator
+    g = load_npz("g1_small_56_n5.npz")
+    images = torch.from_numpy(g["images"])
+    n = int(g["n_views"])
+    torch.manual_seed(3)
+    agg = Aggregator(img_size=56, patch_size=14, embed_dim=384, depth=4, num_heads=6,
+                     patch_embed="dinov2_vits14_reg", intermediate_layer_idx=[1, 3]).eval()
+    cam = CameraHead(dim_in=768, trunk_depth=2, num_heads=6).eval()
+    for mod in (agg, cam):  # LayerScale gammas of 1e-2 would hide a mis-applied residual
+        for name, prm in mod.named_parameters():
+            if name.endswith(("gamma", "ls1.gamma", "ls2.gamma")):
+                prm.data.uniform_(0.5, 1.5)
+    outs = []
+    orig = cpu_ops.residual_layernorm
+    for on in (False, True):
+        monkeypatch.setattr(runtime, "_DEFER_RESID", on)
+        monkeypatch.setattr(runtime, "_FUSED_RESID_LN", on)
+        monkeypatch.setattr(ops, "RESIDUAL_LN_COLS", ops.RESIDUAL_LN_COLS + ((384,) if on else ()))
+        agg.generator.manual_seed(0)
+        calls = []
+        monkeypatch.setattr(cpu_ops, "residual_layernorm", lambda *a, **k: (calls.append(1), orig(*a, **k)))
+        with cpu_ops.installed(), torch.no_grad():
+            feats, _, cam_last = agg(images, list(range(n)), list(range(n, 2 * n)), fix_rank=int(g["fix_rank"]))
+            poses = cam(feats, cam_last)
+        # on: 11 DINO LN1s + 12 DINO LN2s + 3 x 4 aggregator LN2s + the frame LN1s of layers 1 and 3
+        # (two row ranges each: anchors, queries) + the camera trunk's 2 blocks x 4 iterations of LN2
+        assert len(calls) == (0 if not on else 11 + 12 + 3 * 4 + 2 * 2 + 8), len(calls)
+        outs.append((feats[1].clone(), feats[3].clone(), cam_last.clone(), poses[-1].clone()))
+    for a, b in zip(*outs):
+        assert rel_l2(b.numpy(), a.numpy()) < 1e-6

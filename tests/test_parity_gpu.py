@@ -186,6 +186,19 @@ def test_full_c3_518_n32(full_model, mode):
     _check_full(full_model, "g10_518_n32.npz", mode)
 
 
+@pytest.mark.parametrize("fname", ["g9_518_n8.npz", "g10_518_n32.npz"], ids=["C2", "C3"])
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_full_deferred_residuals(full_model, fname, mode, monkeypatch):
+    """proj / fc2 in the plain bias epilogue (their output in the compute dtype,
+    as the reference's autocast Linear returns it) with the residual updates folded into the next
+    LayerNorm (runtime: SR_FUSED_RESID_LN + SR_DEFER_RESID) -- against the reference goldens at
+    the BASELINE workloads."""
+    from sailrecon_amd import runtime
+    monkeypatch.setattr(runtime, "_FUSED_RESID_LN", True)
+    monkeypatch.setattr(runtime, "_DEFER_RESID", True)
+    _check_full(full_model, fname, mode)
+
+
 # fp8 global attention (BASELINE C5's precision, opt-in: Aggregator.set_fp8_global) at the C3
 # headline scene against the reference's fp32 golden.  No reference output pins an fp8 contract
 # (the reference runs bf16 SDPA); the tolerances below are the measured errors with ~2-4x headroom,
