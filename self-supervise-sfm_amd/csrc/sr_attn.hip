@@ -1566,12 +1566,12 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
   } while (0)
     if (cfg == 1) SR_ATTN_LAUNCH(8, 1, false);
     else if (cfg == 2) SR_ATTN_LAUNCH(2, 2, false);
-    // the _SEG variant by default only for ONE long query set (one ragged q-tile in the whole
-    // launch): the reloc block's shared-subsample pass (aggregator.py split reloc) and ragged
-    // global segments
+    // the _SEG variant by default only for ONE long query set (one ragged q-tile per item): the
+    // reloc block's shared-subsample pass (aggregator.py split reloc), ragged global segments and
+    // the key-split items of one query set (q_bstride 0) whose chunk tails are readable
     else if (pipe && (d.key_bound || d.key_norm_max > 0.f) &&
              ((d.l1 == 0 && d.l0 % KT == 0) ||
-              ((pipe_seg || (d.batch == 1 && d.lq >= 4096)) && d.tail_rows_readable >= KT)))
+              ((pipe_seg || ((d.batch == 1 || d.q_bstride == 0) && d.lq >= 4096)) && d.tail_rows_readable >= KT)))
       SR_ATTN_LAUNCH(4, 2, true);  // the asm sweep: one segment of full tiles, or (_SEG) two / ragged
     else SR_ATTN_LAUNCH(4, 2, false);
 #undef SR_ATTN_LAUNCH

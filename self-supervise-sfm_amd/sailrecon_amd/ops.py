@@ -381,7 +381,7 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
             raise ValueError("attention: lse must be contiguous fp32 [batch, heads, lq]")
         o_parts, lse_parts = key_split_workspace(q.device, parts, lq, heads * head_dim, heads)
         attention_partials(q, k0, v0, o_parts, lse_parts, heads=heads, head_dim=head_dim, lq=lq, l0=l0, parts=parts,
-                           scale=scale, tag=tag, key_norm_max=key_norm_max)
+                           scale=scale, tag=tag, key_norm_max=key_norm_max, tail_readable=tail_readable)
         attn_merge_n(o_parts, lse_parts, o, parts=parts, rows=lq, heads=heads, head_dim=head_dim, lse_out=lse)
         return
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
@@ -483,7 +483,7 @@ def key_split_workspace(device, parts: int, rows: int, cols: int, heads: int, na
 
 def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_parts: Tensor, *, heads: int,
                        head_dim: int, lq: int, l0: int, parts: int, scale: Optional[float] = None,
-                       tag: Optional[str] = None, key_norm_max: float = 0.0) -> None:
+                       tag: Optional[str] = None, key_norm_max: float = 0.0, tail_readable: bool = False) -> None:
     """One bf16 launch of ``parts`` items over equal key chunks of k0/v0 (item s: keys
     [s*l0/parts, (s+1)*l0/parts)) against the same lq queries: item s writes its normalised
     partial output at rows s*lq of o_parts and its LSE to lse_parts[s] ([heads, lq]).  The parts
@@ -497,6 +497,8 @@ def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_p
     d = _attn_desc(q, k0, v0, o_parts, heads=heads, head_dim=head_dim, batch=parts, lq=lq, q_bstride=0, l0=chunk,
                    k0_bstride=chunk, scale=scale, lse=lse_parts)
     d.o_bstride = lq
+    if tail_readable:  # rows past k0/v0's end readable: each chunk's ragged tile may go to the asm sweep
+        d.tail_rows_readable = 64
     _launch_attention(d, q, tag, key_norm_max, 4.0 * heads * lq * l0 * head_dim,
                       q.element_size() * heads * head_dim * (lq + 2 * parts * lq + 2 * l0))
 

@@ -49,10 +49,16 @@ class BlockTape:
     h: Tensor            # dtype [R, H]
 
 
+TAIL_ROWS = 64
+
+
 def alloc_tape(rows: int, dim: int, hidden: int, dtype: torch.dtype, device, lse_numel: int,
                separate_raw: bool) -> BlockTape:
     e = lambda r, c, dt=dtype: torch.empty(r, c, device=device, dtype=dt)  # noqa: E731
-    qkv = e(rows, 3 * dim)
+    # q|k|v with TAIL_ROWS zeroed rows after it: every key segment's tail is readable, so the
+    # forward attention may take the hand-scheduled sweep's ragged variant (ops.attention
+    # tail_readable; the C4 global block's 21,984 keys are 343.5 tiles)
+    qkv = torch.zeros(rows + TAIL_ROWS, 3 * dim, device=device, dtype=dtype)[:rows]
     return BlockTape(x0=e(rows, dim, torch.float32), x1=e(rows, dim, torch.float32), xn1=e(rows, dim),
                      raw=e(rows, 3 * dim) if separate_raw else qkv, qkv=qkv, o=e(rows, dim),
                      lse=torch.empty(lse_numel, device=device, dtype=torch.float32) if lse_numel else None,
@@ -245,7 +251,7 @@ def frame_attend_train(pb: runtime.PackedBlock, frames: int, tokens: int):
     def fwd(qkv, o, lse):
         ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=pb.heads, head_dim=pb.head_dim,
                       batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, lse=lse,
-                      tag="attn_frame")
+                      tag="attn_frame", tail_readable=True)
 
     def bwd(tape, dO, dqkv):
         q = tape.qkv

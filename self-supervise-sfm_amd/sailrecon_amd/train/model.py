@@ -243,8 +243,12 @@ class TrainGraph:
         C = pg.dim
 
         def fwd(qkv, o, lse):
+            # the tape's q|k|v has readable tail rows (engine.alloc_tape): the hand-scheduled sweep's
+            # ragged variant covers L = 21,984 (C4); the key bound comes from the per-launch key scan
+            # (the weights move every step)
             ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=pg.heads, head_dim=pg.head_dim,
-                          batch=1, lq=La, q_bstride=0, l0=La, k0_bstride=0, lse=lse, tag="attn_global")
+                          batch=1, lq=La, q_bstride=0, l0=La, k0_bstride=0, lse=lse, tag="attn_global",
+                          tail_readable=True)
 
         def bwd(tape, dO, dqkv):
             q = tape.qkv
