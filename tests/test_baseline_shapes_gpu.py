@@ -554,10 +554,14 @@ def test_global_attention_qk_gain(ops, g):
         assert s1[1] > 0
     assert torch.equal(og, o) and torch.equal(orr, or1) and torch.equal(lse, lse1)
     scale = D ** -0.5
+    # the kernels (asm and compiled alike) take c*q rounded to bf16 (c = scale*log2 e), a relative
+    # error of 2^-9 on every score: at g = 8 the scores reach |s| ~ 300 (log2 domain), so the peaked
+    # softmax moves by ~1.5e-2 against fp64 on the unscaled bf16 q (measured); 1e-2 up to g = 4
+    tol = 1e-2 if g <= 4.0 else 3e-2
     for q_, k_, v_, o_ in ((q, k, v, o), (qr, ks, vs, orr)):
         rows = _sample_rows(L, 128, int(g)).to(DEV)
         ref = _ref_rows(q_[rows], k_, v_, scale)
-        assert _rel(o_[rows].float(), ref) < 1e-2
+        assert _rel(o_[rows].float(), ref) < tol
     # the second problem's LSE (log2 domain), as test_attention_pair
     rws = _sample_rows(L, 32, 3).to(DEV)
     for h in (0, H - 1):
