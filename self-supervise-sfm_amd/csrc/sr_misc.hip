@@ -237,8 +237,9 @@ int residual_layernorm_dispatch(hipStream_t s, float* x, int64_t ldx, const TY* 
                                 const float* w, const float* b, float eps, TO* out, int64_t ldo, int rows, int cols) {
   // rows in flight per wave as the LayerNorm (kbench M = 87,936, C = 1024: 1 row 3.5 TB/s, 2 rows
   // 4.86, 4 rows 4.96 TB/s of the 12 B per element moved)
-  // 16-B lane vectors (W = 8) where every row is 512-column blocks and 16-B aligned
-  const bool w8 = cols % 512 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && ldx % 4 == 0 &&
+  // 16-B lane vectors (W = 8) where every row is 512-column blocks and 16-B aligned: opt-in
+  // (SR_TUNE_RLN_WIDE; kbench M = 87,936: 0.242 ms against round 3's 0.218 ms for W = 4)
+  const bool w8 = sr::tune(SR_TUNE_RLN_WIDE) && cols % 512 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && ldx % 4 == 0 &&
                   (((uintptr_t)y | (uintptr_t)out | (uintptr_t)x) & 15) == 0;
 #define RLN_LAUNCH(C, R)                                                                                          \
   do {                                                                                                            \

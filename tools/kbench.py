@@ -391,8 +391,11 @@ def ln():
     gb = M * C * 12 / 1e9
     print(f"residual_layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s", flush=True)
     yc = torch.randn(M, C, device=DEV).bfloat16()  # the deferred fc2 residual: y in the o slot (ld = C)
-    ms = timeit(lambda: ops.residual_layernorm(x, yc, g, w, b, 1e-5, out))
-    print(f"residual_layernorm (y ld=C) M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s", flush=True)
+    for wide in (0, 1, 0, 1):
+        with ops.tuning(SR_RLN_WIDE=wide):
+            ms = timeit(lambda: ops.residual_layernorm(x, yc, g, w, b, 1e-5, out))
+        print(f"residual_layernorm (y ld=C, 16-B lanes {wide}) M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s",
+              flush=True)
 
 
 def dpt():
