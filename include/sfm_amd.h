@@ -74,7 +74,7 @@ enum sr_tuning_key {
   SR_TUNE_SYNC_CHECK = 11,  /* 1: debug mode -- every launching call synchronises the device and
                                returns SR_ELAUNCH with the runtime's message if a kernel faulted
                                (HIP_LAUNCH_BLOCKING-style attribution; not graph-capturable) */
-  SR_TUNE_RLN_WIDE = 12,    /* 1: sr_residual_layernorm with 16-B lane vectors            default 0 */
+  SR_TUNE_RLN_WIDE = 12,    /* sr_residual_layernorm variant bits: 1 16-B lanes, 2 two rows per wave, 4 nt x stores (0) */
   SR_TUNE_COUNT = 13
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */

@@ -124,7 +124,7 @@ int layernorm_dispatch(hipStream_t s, const float* x, int64_t ldx, const int32_t
 // row, ln_rows_per_wave rows in flight, 4-wide vectors.
 // W = columns per lane-vector: 4 (float4 x, 8-B bf16 y / out) or 8 (two float4 of x, ONE 16-B
 // bf16x8 of y and of out: every load and store of the row is 16 B wide).
-template <int NPL, int RPW, typename TY, typename TO, int W = 4>
+template <int NPL, int RPW, typename TY, typename TO, int W = 4, bool NT = false>
 __global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64_t ldx, const TY* __restrict__ y,
                                                                  int64_t ldy, const float* __restrict__ gamma,
                                                                  const float* __restrict__ w,
@@ -193,7 +193,12 @@ __global__ __launch_bounds__(256) void residual_layernorm_kernel(float* x, int64
 #pragma unroll
         for (int h = 0; h < W / 4; ++h) {
           const int k = i * W + 4 * h;
-          *(float4*)(xr + (i * 64 + lane) * W + 4 * h) = make_float4(v[r][k], v[r][k + 1], v[r][k + 2], v[r][k + 3]);
+          if constexpr (NT) {
+            const f32x4 xv = {v[r][k], v[r][k + 1], v[r][k + 2], v[r][k + 3]};
+            __builtin_nontemporal_store(xv, (f32x4*)(xr + (i * 64 + lane) * W + 4 * h));
+          } else {
+            *(float4*)(xr + (i * 64 + lane) * W + 4 * h) = make_float4(v[r][k], v[r][k + 1], v[r][k + 2], v[r][k + 3]);
+          }
         }
     }
     float s = 0.f;
@@ -237,21 +242,28 @@ int residual_layernorm_dispatch(hipStream_t s, float* x, int64_t ldx, const TY* 
                                 const float* w, const float* b, float eps, TO* out, int64_t ldo, int rows, int cols) {
   // rows in flight per wave as the LayerNorm (kbench M = 87,936, C = 1024: 1 row 3.5 TB/s, 2 rows
   // 4.86, 4 rows 4.96 TB/s of the 12 B per element moved)
-  // 16-B lane vectors (W = 8) where every row is 512-column blocks and 16-B aligned: opt-in
-  // (SR_TUNE_RLN_WIDE; kbench M = 87,936: 0.242 ms against round 3's 0.218 ms for W = 4)
-  const bool w8 = sr::tune(SR_TUNE_RLN_WIDE) && cols % 512 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && ldx % 4 == 0 &&
+  // Variants (SR_TUNE_RLN_WIDE, a kbench A/B switch; default 0): bit 0 = 16-B lane vectors (W = 8:
+  // rows of 512-column blocks, 16-B aligned; kbench M = 87,936: 0.242 ms against round 3's
+  // 0.218 ms for W = 4), bit 1 = 2 rows in flight per wave instead of 4, bit 2 = non-temporal x stores
+  const int var = sr::tune(SR_TUNE_RLN_WIDE);
+  const bool w8 = (var & 1) && cols % 512 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && ldx % 4 == 0 &&
                   (((uintptr_t)y | (uintptr_t)out | (uintptr_t)x) & 15) == 0;
+  const bool r2 = (var & 2) != 0, nt = (var & 4) != 0;
+#define RLN_GO(C, R, W_, NT_)                                                                                     \
+  hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO, W_, NT_>), dim3((rows + 4 * R - 1) / (4 * R)), \
+                     dim3(256), 0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows)
 #define RLN_LAUNCH(C, R)                                                                                          \
   do {                                                                                                            \
-    if constexpr (C % 512 == 0) {                                                                                 \
-      if (w8) {                                                                                                   \
-        hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO, 8>), dim3((rows + 4 * R - 1) / (4 * R)), \
-                           dim3(256), 0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows);                    \
+    if constexpr (C % 512 == 0 && R == 4) {                                                                       \
+      if (w8 || r2 || nt) {                                                                                       \
+        if (w8 && r2) { if (nt) RLN_GO(C, 2, 8, true); else RLN_GO(C, 2, 8, false); }                           \
+        else if (w8) { if (nt) RLN_GO(C, 4, 8, true); else RLN_GO(C, 4, 8, false); }                           \
+        else if (r2) { if (nt) RLN_GO(C, 2, 4, true); else RLN_GO(C, 2, 4, false); }                           \
+        else RLN_GO(C, 4, 4, true);                                                                               \
         break;                                                                                                    \
       }                                                                                                           \
     }                                                                                                             \
-    hipLaunchKernelGGL((residual_layernorm_kernel<C / 64, R, TY, TO, 4>), dim3((rows + 4 * R - 1) / (4 * R)),     \
-                       dim3(256), 0, s, x, ldx, y, ldy, gamma, w, b, eps, out, ldo, rows);                        \
+    RLN_GO(C, R, 4, false);                                                                                       \
   } while (0)
 #define RLN_CASE(C)                                                                                             \
   case C:                                                                                                       \
@@ -267,6 +279,7 @@ int residual_layernorm_dispatch(hipStream_t s, float* x, int64_t ldx, const TY* 
   }
 #undef RLN_CASE
 #undef RLN_LAUNCH
+#undef RLN_GO
   sr::set_error("sr_residual_layernorm: unsupported cols=%d", cols);
   return SR_EUNSUPPORTED;
 }

@@ -446,3 +446,21 @@ def test_gemm_group(ops, epi_name):
     torch.cuda.synchronize()
     for p, ref_out in zip(probs, plain):
         assert torch.equal(p["out"], ref_out)
+
+
+@pytest.mark.parametrize("var", range(8))
+def test_residual_layernorm_variants(ops, var):
+    """Every sr_residual_layernorm variant of the SR_RLN_WIDE switch (16-B lanes, two rows per
+    wave, non-temporal x stores) computes the same update and LayerNorm (bit-identical x, out
+    within bf16 rounding of the reference)."""
+    rows, cols = 301, 1024
+    x = torch.randn(rows, cols, device=DEV) * 3 + 1
+    y = torch.randn(rows, cols, device=DEV).bfloat16()
+    g, w, b = (torch.randn(cols, device=DEV) for _ in range(3))
+    xr = x + y.float() * g
+    out = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+    with ops.tuning(SR_RLN_WIDE=var):
+        ops.residual_layernorm(x, y, g, w, b, 1e-6, out)
+    torch.cuda.synchronize()
+    assert torch.equal(x, xr)
+    assert rel(out.float(), F.layer_norm(xr, (cols,), w, b, 1e-6)) < 5e-3

@@ -391,10 +391,11 @@ def ln():
     gb = M * C * 12 / 1e9
     print(f"residual_layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s", flush=True)
     yc = torch.randn(M, C, device=DEV).bfloat16()  # the deferred fc2 residual: y in the o slot (ld = C)
-    for wide in (0, 1, 0, 1):
-        with ops.tuning(SR_RLN_WIDE=wide):
-            ms = timeit(lambda: ops.residual_layernorm(x, yc, g, w, b, 1e-5, out))
-        print(f"residual_layernorm (y ld=C, 16-B lanes {wide}) M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s",
+    # SR_RLN_WIDE variants: bit 0 16-B lanes, bit 1 two rows in flight per wave, bit 2 nt x stores
+    for var in (0, 1, 2, 3, 4, 6, 0, 1, 2, 3, 4, 6):
+        with ops.tuning(SR_RLN_WIDE=var):
+            ms = timeit(lambda: ops.residual_layernorm(x, yc, g, w, b, 1e-5, out), reps=20)
+        print(f"residual_layernorm (y ld=C, variant {var}) M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s",
               flush=True)
 
 

@@ -14,5 +14,6 @@ run() {  # name seconds cmd...
 run dist 900 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeout 800 --timeout-method thread -k "c3 or n64"
 run ranksim 400 python tools/rank_sim.py --views 32 --worlds 1,2,4,8 --steps 4
 run ranksim64 400 python tools/rank_sim.py --views 64 --worlds 1,8 --steps 2
+run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
 run kln 200 python tools/kbench.py ln
 run ktrain 600 python tools/kbench.py train
