@@ -191,6 +191,23 @@ def attn_gain():
               flush=True)
 
 
+def attn_frame_cfg():
+    """Frame / DINO attention (64 frames x 1374 tokens, static key bound) under each bf16 workgroup
+    shape (SR_ATTN_CFG: 0 = 4 waves x 2 q-blocks, 1 = 8 x 1, 2 = 2 x 2 = 128 rows), interleaved."""
+    C, H, D, P, S = 1024, 16, 64, 1374, 64
+    qkv = torch.randn(S * P + 64, 3 * C, device=DEV, dtype=torch.bfloat16)[:S * P]
+    o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
+    kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())
+    fl = 4.0 * S * H * P * P * D
+    for cfg in (0, 1, 2, 0, 1, 2):
+        with ops.tuning(SR_ATTN_CFG=cfg):
+            ms = timeit(lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
+                                              batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P, key_norm_max=kb,
+                                              tail_readable=True), reps=20)
+            kern = ops.last_kernel()
+        print(f"attn frame cfg {cfg} ({kern}): {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s", flush=True)
+
+
 def attn_frame_diag():
     """Where the frame attention loses against the long sweep: the same launch with no ragged
     q-tile (lq = 1280 = 5 x 256), with full key tiles (l0 = 1408), and with 4x longer key sweeps

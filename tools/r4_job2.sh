@@ -15,5 +15,5 @@ run dist 900 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeou
 run ranksim 400 python tools/rank_sim.py --views 32 --worlds 1,2,4,8 --steps 4
 run ranksim64 400 python tools/rank_sim.py --views 64 --worlds 1,8 --steps 2
 run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
-run kln 200 python tools/kbench.py ln
+run kln 200 python tools/kbench.py ln attn_frame_cfg
 run ktrain 600 python tools/kbench.py train
