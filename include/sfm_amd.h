@@ -215,13 +215,13 @@ typedef struct sr_attn_desc {
                   domain), saved for sr_attention_bwd and for sr_attn_merge */
   float* key_bound; /* optional scratch (bf16 path, >= sr_attention_bound_floats(d) floats, 4-B
                   aligned): per key-segment instance and head, max |k| over the keys.  With it a
-                  query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^100 of its first
-                  tile's max runs the sweep with a FIXED softmax offset (no per-tile row max,
-                  no rescale; every P <= 2^50, no overflow, same precision); NULL = per-tile max.
-                  The hand-scheduled sweep (bf16, 256-row workgroups) fixes m = max(0, bound - 64)
-                  for every row whose bound is within 2^174 of its max over the first three key
-                  tiles (every P <= 2^64, the row's largest P >= 2^-110); other waves run the
-                  compiled loop above */
+                  query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^174 of its first
+                  tile's max runs the sweep with a FIXED softmax offset m = max(tile max, bound - 64)
+                  (m = 0 for a bound <= 64): no per-tile row max, no rescale; every P <= 2^64 and the
+                  row's largest P >= 2^-110, so no overflow and the same precision.  The
+                  hand-scheduled sweep (bf16, 256-row workgroups) fixes m = max(0, bound - 64) for
+                  every row whose bound is within 2^174 of its max over the first three key tiles;
+                  other waves run the compiled loop; NULL (and no key_norm_max) = per-tile max */
   float key_norm_max; /* optional (bf16 path): > 0 = a static upper bound of |k| (2-norm per head)
                   for every key, used INSTEAD of key_bound (no key scan).  For keys that come out of
                   the qk LayerNorm (attention.py:49-50,78) and RoPE (a rotation), |k| <=

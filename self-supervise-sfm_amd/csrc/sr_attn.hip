@@ -68,6 +68,12 @@ __device__ __forceinline__ float sum_x32(float v) {
 //   P = exp2(S*c - m) -> bf16; O^T += V^T P^T  (8 MFMA per q-block)
 // Two workgroups per CU interleave their MFMA / VALU phases freely.
 constexpr float RESCALE_LOG2 = 8.f;
+// Fixed-offset window (both sweeps of the bf16 kernel): with a row's Cauchy-Schwarz bound qb and a
+// lower bound mx0 of its true max (exp2 domain), an offset m with qb - FIX_HI <= m <= mx0 + FIX_LO
+// keeps every P = 2^(S - m) <= 2^FIX_HI (no overflow of O or l in fp32 for any key count the ABI
+// takes) and the row's largest P >= 2^-FIX_LO (normal in fp32 and bf16, as are its products with
+// every V entry above 2^-16).
+constexpr float FIX_HI = 64.f, FIX_LO = 110.f;
 #ifndef SR_ATTN_DEFAULT_CFG
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
@@ -177,9 +183,9 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
       for (int j = 0; j < 8; ++j) qf[b][s][j] = (bf16)((float)qf[b][s][j] * c);
 
   // Fixed-offset sweep (d.key_bound set): qb = |cq| max|k| bounds every score of the row
-  // (Cauchy-Schwarz).  After tile 0 a wave whose rows all satisfy qb - max_tile0 <= 100 fixes
-  // m = max(max_tile0, qb - 50) for the whole sweep: every later S' = c q.k - m <= 50 (P <= 2^50,
-  // no overflow in fp32 / bf16) and the row's true max stays >= m - 50 (l >= 2^-50), so the
+  // (Cauchy-Schwarz).  After tile 0 a wave whose rows all satisfy qb - max_tile0 <= FIX_HI + FIX_LO
+  // fixes m = max(max_tile0, qb - FIX_HI) for the whole sweep: every later S' = c q.k - m <= FIX_HI
+  // (no overflow in fp32 / bf16) and the row's true max stays >= m - FIX_LO, so the
   // per-tile row max, its lane exchange and the rescale test are skipped.  P keeps bf16's
   // relative precision at any magnitude, O and l are fp32: the result equals the per-tile-max
   // sweep's up to rounding.
@@ -209,7 +215,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
     // pass would settle on), so the sweep skips that pass and the -m fold MFMAs from the start
     bool z = true;
 #pragma unroll
-    for (int b = 0; b < QB; ++b) z &= qb[b] <= 50.f;
+    for (int b = 0; b < QB; ++b) z &= qb[b] <= FIX_HI;
     fixed_m = m_zero = __all(z);
   }
 
@@ -326,16 +332,16 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
       if (t == 0 && use_bound) {
         bool ok = true;
 #pragma unroll
-        for (int b = 0; b < QB; ++b) ok &= qb[b] - mx[b] <= 100.f;
+        for (int b = 0; b < QB; ++b) ok &= qb[b] - mx[b] <= FIX_HI + FIX_LO;
         fixed_m = __all(ok);
       }
       if (__any(grow)) {
 #pragma unroll
         for (int b = 0; b < QB; ++b) {
           // new max (rows that did not grow keep theirs), split into bf16 hi + lo
-          // fixed offset: m = 0 when the row's bound allows it (every score <= qb <= 50 and the
-          // true max >= -qb >= -50), else max(tile-0 max, qb - 50)
-          const float target = t == 0 ? (fixed_m ? (qb[b] <= 50.f ? 0.f : fmaxf(mx[b], qb[b] - 50.f)) : mx[b])
+          // fixed offset: m = 0 when the row's bound allows it (every score <= qb <= FIX_HI and the
+          // true max >= -qb), else max(tile-0 max, qb - FIX_HI)
+          const float target = t == 0 ? (fixed_m ? (qb[b] <= FIX_HI ? 0.f : fmaxf(mx[b], qb[b] - FIX_HI)) : mx[b])
                                       : m_run[b] + fmaxf(mx[b], 0.f);
           const bf16 nhi = (bf16)target;
           const bf16 nlo = (bf16)(target - (float)nhi);
@@ -443,7 +449,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // a wave with any row outside it runs the plain loop, which keeps the same wait, barrier and
   // stage per tile, so the waves of a workgroup may take different paths.
   // One key segment of full tiles (>= 4) or, with readable tails, the _SEG variant.
-  constexpr float PIPE_HI = 64.f, PIPE_LO = 110.f;
+  constexpr float PIPE_HI = FIX_HI, PIPE_LO = FIX_LO;
   bool asm_ok = false;
   float m_fix[QB];
   if constexpr (PIPE) {

@@ -189,6 +189,16 @@ def attn_gain():
         print(f"attn qk-gain {g:.1f} (bound qb ~ {qb:6.1f}): global {tg:.3f} ms ({fl1 / tg / 1e9:.1f} TF/s, asm waves "
               f"{sg[0]}/{sg[0] + sg[1]}); pair {tp:.3f} ms ({fl2 / tp / 1e9:.1f} TF/s, asm waves {sp[0]}/{sp[0] + sp[1]})",
               flush=True)
+        # frame / DINO attention (64 frames x 1374, compiled two-workgroups-per-CU sweep) at the same gain
+        S = 64
+        qf = torch.cat([q, qr])[:S * P] if 2 * L >= S * P else None
+        kf, kbf = qk_normed(S * P, g, gen)
+        vf = torch.randn(S * P, C, device=DEV, dtype=torch.bfloat16)
+        of = torch.empty_like(vf)
+        tf = timeit(lambda: ops.attention(qf, kf, vf, of, heads=H, head_dim=D, batch=S, lq=P, q_bstride=P, l0=P,
+                                          k0_bstride=P, key_norm_max=kbf), reps=10)
+        ff = 4.0 * S * H * P * P * D
+        print(f"attn qk-gain {g:.1f} frame 64x1374: {tf:.3f} ms ({ff / tf / 1e9:.1f} TF/s)", flush=True)
 
 
 def attn_frame_cfg():
