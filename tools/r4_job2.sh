@@ -17,3 +17,4 @@ run ranksim64 400 python tools/rank_sim.py --views 64 --worlds 1,8 --steps 2
 run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
 run kln 200 python tools/kbench.py ln attn_frame_cfg
 run ktrain 600 python tools/kbench.py train
+run k2 300 python tools/kbench.py attn_gain
