@@ -182,7 +182,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
 #pragma unroll
   for (int i = 0; i < 16; ++i) dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f;
 
-  for (int t = 0, cq = 0; t < ntiles; ++t, cq = cq + 1 == ntq ? 0 : cq + 1) {
+  // One tile of the sweep.  MASKED (the last, ragged query tile of an item) is a separate
+  // instantiation, so the full-tile body is one basic block: the compiler interleaves one q-block's
+  // S / dP chains with the other's exp2 / pack / dV / dK work (a uniform branch between the chains
+  // and the softmax split them apart).
+  auto tile_body = [&](int t, int cq, auto masked) __attribute__((always_inline)) {
     // tile t has landed (later stages stay in flight: 5 DMA wave-instructions per stage on
     // waves 0-1, 4 on waves 2-3); every wave is done with tile t-1, whose buffer stage t+3 reuses
     if (t + 2 < ntiles) {
@@ -221,8 +225,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
         sc[qb2] = mfma32(row_frag(qt, qb2 * 32 + l32, s, hi), kf[s], sc[qb2]);
         dp[qb2] = mfma32(row_frag(ot, qb2 * 32 + l32, s, hi), vf[s], dp[qb2]);
       }
-    const int qv = f.lq - cq * 64;  // valid query rows of this tile
-    if (qv < 64) {  // ragged last tile (uniform branch): clamped duplicate rows get P = 0
+    if constexpr (decltype(masked)::value) {  // clamped duplicate rows of the ragged tile get P = 0
+      const int qv = f.lq - cq * 64;  // valid query rows of this tile
 #pragma unroll
       for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
@@ -249,6 +253,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
           dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
         }
       }
+  };
+  // tiles item by item; the last query tile of an item is the only one that can be ragged
+  const bool ragged = f.lq % 64 != 0;
+  for (int t = 0; t < ntiles;) {
+    const int full = ragged ? ntq - 1 : ntq;
+    for (int cq = 0; cq < full; ++cq, ++t) tile_body(t, cq, std::false_type{});
+    if (ragged) {
+      tile_body(t, ntq - 1, std::true_type{});
+      ++t;
+    }
   }
   // dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key l32, d = 32 db + acc_row(r))
   if (key < len) {
@@ -324,49 +338,54 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
   f32x16 dq[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) dq[0][i] = dq[1][i] = 0.f;
-  for (int t = 0; t < ntiles; ++t) {
-    {
-      if (t + 2 < ntiles) wait_vm<8>();  // tile t landed; t+1, t+2 stay in flight (4 per stage)
-      else if (t + 1 < ntiles) wait_vm<4>();
-      else wait_vm<0>();
-      sr::barrier_raw();  // every wave is done with tile t-1, whose buffer stage t+3 reuses
-      if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
-      const char* kt = smem + (t & (NBUF - 1)) * 2 * TB;
-      const char* vt = kt + TB;
+  // one key tile; MASKED (a segment's ragged last tile) is its own instantiation, so the full-tile
+  // body is one basic block the compiler can interleave (see attn_bwd_dkdv_kernel)
+  auto tile_body = [&](int t, auto masked) __attribute__((always_inline)) {
+    if (t + 2 < ntiles) wait_vm<8>();  // tile t landed; t+1, t+2 stay in flight (4 per stage)
+    else if (t + 1 < ntiles) wait_vm<4>();
+    else wait_vm<0>();
+    sr::barrier_raw();  // every wave is done with tile t-1, whose buffer stage t+3 reuses
+    if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
+    const char* kt = smem + (t & (NBUF - 1)) * 2 * TB;
+    const char* vt = kt + TB;
+    f32x16 sc[2], dp[2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        sc[kb] = mfma32(row_frag(kt, kb * 32 + l32, s, hi), qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
+        dp[kb] = mfma32(row_frag(vt, kb * 32 + l32, s, hi), of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
+      }
+    if constexpr (decltype(masked)::value) {  // partial key tile: keys >= valid get S' = -inf, P = 0
       const int seg = t >= nt0;
       const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
-      f32x16 sc[2], dp[2];
-#pragma unroll
-      for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          sc[kb] = mfma32(row_frag(kt, kb * 32 + l32, s, hi), qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
-          dp[kb] = mfma32(row_frag(vt, kb * 32 + l32, s, hi), of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
-        }
-      if (valid < 64) {  // partial key tile (uniform branch): keys >= valid get S' = -inf, P = 0
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kb * 32 + acc_row(r, hi) >= valid) sc[kb][r] = -INFINITY;
-      }
-      // one code path for every tile: a masked copy of the dS / dQ block made the compiler join
-      // two register assignments of dq with 64 v_mov per tile
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 df;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int r = 8 * s2 + j;
-            df[j] = (bf16)(__builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r]);
-          }
-          const int row0 = kb * 32 + 16 * s2;
-#pragma unroll
-          for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
-        }
+        for (int r = 0; r < 16; ++r)
+          if (kb * 32 + acc_row(r, hi) >= valid) sc[kb][r] = -INFINITY;
     }
+    // one code path for every tile: a masked copy of the dS / dQ block made the compiler join
+    // two register assignments of dq with 64 v_mov per tile
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 df;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * s2 + j;
+          df[j] = (bf16)(__builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r]);
+        }
+        const int row0 = kb * 32 + 16 * s2;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
+      }
+  };
+  const int rag0 = f.l0 % 64 ? nt0 - 1 : -1, rag1 = nt1 > 0 && f.l1 % 64 ? ntiles - 1 : -1;
+  for (int t = 0; t < ntiles; ++t) {
+    if (t == rag0 || t == rag1) tile_body(t, std::true_type{});
+    else tile_body(t, std::false_type{});
   }
   if (qrow < f.lq) {
     float* dqp = b.dq + ((int64_t)item * f.q_bstride + qrow) * b.lddq + hcol;
