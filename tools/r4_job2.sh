@@ -16,5 +16,6 @@ run ranksim 400 python tools/rank_sim.py --views 32 --worlds 1,2,4,8 --steps 4
 run ranksim64 400 python tools/rank_sim.py --views 64 --worlds 1,8 --steps 2
 run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
 run kln 200 python tools/kbench.py ln attn_frame_cfg
+run tbwd 600 python -u -m pytest tests/test_attn_bwd_gpu.py tests/test_train_block_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread
 run ktrain 600 python tools/kbench.py train
 run k2 300 python tools/kbench.py attn_gain
