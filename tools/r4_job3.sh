@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# round-4 GPU job 2: frame-sharded C3 / N=64 tests, per-rank rehearsal, training kbench
+# round-4 GPU job 3: residual-LN variants, frame cfg, backward tests + training kbench, gain kbench
 set -u
 mkdir -p gpurun_out
 run() {  # name seconds cmd...
@@ -12,6 +12,8 @@ run() {  # name seconds cmd...
   if [ "$rc" -ne 0 ]; then echo "=== $name failed (rc=$rc): stopping"; exit "$rc"; fi
 }
 run dist 900 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeout 800 --timeout-method thread -k "c3 or n64"
-run dist 900 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeout 800 --timeout-method thread -k "c3 or n64"
-run ranksim 300 python tools/rank_sim.py --views 32 --worlds 1,2,4,8 --steps 4
-run ranksim64 200 python tools/rank_sim.py --views 64 --worlds 1,8 --steps 2
+run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
+run kln 200 python tools/kbench.py ln attn_frame_cfg
+run tbwd 600 python -u -m pytest tests/test_attn_bwd_gpu.py tests/test_train_block_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread
+run ktrain 600 python tools/kbench.py train
+run k2 300 python tools/kbench.py attn_gain
