@@ -11,7 +11,6 @@ run() {  # name seconds cmd...
   tail -n 4 "gpurun_out/$name.log"
   if [ "$rc" -ne 0 ]; then echo "=== $name failed (rc=$rc): stopping"; exit "$rc"; fi
 }
-run dist 900 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeout 800 --timeout-method thread -k "c3 or n64"
 run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
 run kln 200 python tools/kbench.py ln attn_frame_cfg
 run tbwd 600 python -u -m pytest tests/test_attn_bwd_gpu.py tests/test_train_block_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread
