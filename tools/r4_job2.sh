@@ -11,6 +11,6 @@ run() {  # name seconds cmd...
   tail -n 4 "gpurun_out/$name.log"
   if [ "$rc" -ne 0 ]; then echo "=== $name failed (rc=$rc): stopping"; exit "$rc"; fi
 }
-run dist 900 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeout 800 --timeout-method thread -k "c3 or n64"
-run ranksim 300 python tools/rank_sim.py --views 32 --worlds 1,2,4,8 --steps 4
+run dist 700 python -u -m pytest tests/test_dist_gpu.py -x -v -s -m gpu --timeout 600 --timeout-method thread -k "c3 or n64"
+run ranksim 250 python tools/rank_sim.py --views 32 --worlds 1,2,4,8 --steps 4
 run ranksim64 200 python tools/rank_sim.py --views 64 --worlds 1,8 --steps 2
