@@ -659,7 +659,7 @@ class Aggregator(nn.Module):
                     _wait(work_kv)  # the remote anchors' K/V
                 ops.attention_partials(q, kv[:, 0:C], kv[:, C:2 * C], o_parts[p0 * lq:(p0 + p) * lq],
                                        lse_parts[p0:p0 + p], heads=H, head_dim=D, lq=lq, l0=kv.shape[0], parts=p,
-                                       tag="attn_global", key_norm_max=kb)
+                                       tag="attn_global", key_norm_max=kb, tail_readable=_SHARD_TAIL)
                 p0 += p
             ops.attn_merge_n(o_parts, lse_parts, o, parts=total, rows=lq, heads=H, head_dim=D)
             return
@@ -747,6 +747,13 @@ class Aggregator(nn.Module):
         else:
             epi["col_offset"] = C
             ops.gemm(xn, pb.w_qkv[C:], out, _lib.SR_EPI_QKV, bias=_sl(pb.b_qkv, C, 3 * C), qkv=epi, tag="gemm")
+
+
+# SR_SHARD_TAIL=1 (opt-in): the frame-sharded global block's key-split passes declare their chunk
+# tails readable (kv_loc / kv_all are Workspace buffers with 64 padding rows), which sends them to the
+# hand-scheduled sweep's ragged variant (round 3 measured it level with the compiled sweep per rank:
+# DESIGN.md section 5)
+_SHARD_TAIL = os.environ.get("SR_SHARD_TAIL", "0") == "1"
 
 
 def _sl(t, a, b):
