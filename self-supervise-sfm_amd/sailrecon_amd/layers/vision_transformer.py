@@ -77,27 +77,36 @@ class DinoVisionTransformer(nn.Module):
         if key in self._pos_cache:
             return self._pos_cache[key]
         pe = self.pos_embed.detach()
-        n0 = pe.shape[1] - 1
-        if npatch == n0 and w_img == h_img:
+        if not self.pos_resampled(h_img, w_img):
             out = pe[0].float().contiguous()
         else:
-            pe = pe.float()
-            dim = pe.shape[-1]
-            m = int(math.sqrt(n0))
-            assert n0 == m * m
-            kw = {}
-            if self.interpolate_offset:
-                kw["scale_factor"] = (float(h_img // self.patch_size + self.interpolate_offset) / m,
-                                      float(w_img // self.patch_size + self.interpolate_offset) / m)
-            else:
-                kw["size"] = (h_img // self.patch_size, w_img // self.patch_size)
             # bicubic resampling of a parameter table (not a per-forward op): run on the host
-            src = pe[:, 1:].cpu().reshape(1, m, m, dim).permute(0, 3, 1, 2)
-            pp = F.interpolate(src, mode="bicubic", antialias=self.interpolate_antialias, **kw)
-            pp = pp.permute(0, 2, 3, 1).reshape(-1, dim)
+            pe = pe.float()
+            pp = self.resample_patch_pos(pe[0, 1:].cpu(), h_img, w_img)
             out = torch.cat([pe[0, :1].cpu(), pp], dim=0).to(pe.device).contiguous()
         self._pos_cache = {key: out}
         return out
+
+    def pos_resampled(self, h_img: int, w_img: int) -> bool:
+        npatch = (h_img // self.patch_size) * (w_img // self.patch_size)
+        return not (npatch == self.pos_embed.shape[1] - 1 and w_img == h_img)
+
+    def resample_patch_pos(self, patch_pe: torch.Tensor, h_img: int, w_img: int) -> torch.Tensor:
+        """[n0, C] patch part of pos_embed -> [npatch, C] for an h_img x w_img input: the bicubic
+        resampling of interpolate_pos_encoding (vision_transformer.py:219-238).  Linear in
+        ``patch_pe``, so the training backward takes its adjoint by autograd (TrainGraph)."""
+        n0, dim = patch_pe.shape
+        m = int(math.sqrt(n0))
+        assert n0 == m * m
+        kw = {}
+        if self.interpolate_offset:
+            kw["scale_factor"] = (float(h_img // self.patch_size + self.interpolate_offset) / m,
+                                  float(w_img // self.patch_size + self.interpolate_offset) / m)
+        else:
+            kw["size"] = (h_img // self.patch_size, w_img // self.patch_size)
+        src = patch_pe.reshape(1, m, m, dim).permute(0, 3, 1, 2)
+        pp = F.interpolate(src, mode="bicubic", antialias=self.interpolate_antialias, **kw)
+        return pp.permute(0, 2, 3, 1).reshape(-1, dim)
 
 
 def vit_small(patch_size=16, num_register_tokens=0, **kwargs):

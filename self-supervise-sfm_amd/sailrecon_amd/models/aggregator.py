@@ -726,7 +726,7 @@ class Aggregator(nn.Module):
         in one launch; whole C3 step 417.8 / 418.2 vs 419.5 / 418.9 ms (interleaved).  With a separate
         merge launch instead (round 3, first form) it was break-even."""
         return (os.environ.get("SR_RELOC_SPLIT", "1") == "1" and dtype == torch.bfloat16 and
-                (rows + 255) // 256 * 16 >= 2048 and n_sub >= 64)
+                (rows + 255) // 256 * 16 >= _RELOC_SPLIT_MIN_WG and n_sub >= 64)
 
     def _side_stream(self, dev):
         """Second HIP stream for the concurrent reloc block (opt-in: SR_CONCURRENT_STACKS=1)."""
@@ -754,6 +754,8 @@ class Aggregator(nn.Module):
 # hand-scheduled sweep's ragged variant (round 3 measured it level with the compiled sweep per rank:
 # DESIGN.md section 5)
 _SHARD_TAIL = os.environ.get("SR_SHARD_TAIL", "0") == "1"
+# smallest query set (in 256-row x head workgroups) whose reloc attention runs split (A/B switch)
+_RELOC_SPLIT_MIN_WG = int(os.environ.get("SR_RELOC_SPLIT_MIN_WG", "2048"))
 
 
 def _sl(t, a, b):

@@ -158,9 +158,15 @@ class TrainGraph:
         is_dino = hasattr(agg.patch_embed, "blocks")
         if is_dino:
             dino = agg.patch_embed
-            if n_patch != dino.pos_embed.shape[1] - 1 or H != W:
-                raise NotImplementedError("training at a resolution that resamples DINO's pos_embed")
-            pos_tab = dino.pos_embed_for(H, W)
+            st["pos_resampled"] = dino.pos_resampled(H, W)
+            if st["pos_resampled"]:
+                # interpolate_pos_encoding (vision_transformer.py:206-240) of the live parameter, every
+                # step (the optimizer updates it in place): a 5 MB table transform on the device;
+                # backward() applies its adjoint to the patch rows' colsum
+                pe = dino.pos_embed.detach()[0]
+                pos_tab = torch.cat([pe[:1], dino.resample_patch_pos(pe[1:], H, W)], 0).contiguous()
+            else:
+                pos_tab = dino.pos_embed_for(H, W)
             row_add = pos_tab[1:]
         else:
             row_add = self._buf("zeros_pos", n_patch, C, F32).zero_()
@@ -514,8 +520,18 @@ class TrainGraph:
             ops.colsum(dx.as_strided((S, C), (P * C, 1)), dino.pos_embed.grad[0, 0], accumulate=True)
             ops.colsum(dx[1:].as_strided((S, 4 * C), (P * C, 1)), dino.register_tokens.grad.reshape(-1),
                        accumulate=True)
-            ops.colsum(dx[psi:].as_strided((S, n_patch * C), (P * C, 1)), dino.pos_embed.grad[0, 1:].reshape(-1),
-                       accumulate=True)
+            if st.get("pos_resampled"):
+                # adjoint of the bicubic resampling: d(pos_embed[1:]) += R^T d(table[1:])
+                dtab = self._buf("dpos_tab", n_patch, C, F32)
+                ops.colsum(dx[psi:].as_strided((S, n_patch * C), (P * C, 1)), dtab.reshape(-1))
+                H, W = st["H"], st["W"]
+                with torch.enable_grad():
+                    src = dino.pos_embed.detach()[0, 1:].clone().requires_grad_(True)
+                    dsrc, = torch.autograd.grad(dino.resample_patch_pos(src, H, W), src, dtab)
+                ops.copy2d(dino.pos_embed.grad[0, 1:], dsrc.contiguous(), accumulate=True)
+            else:
+                ops.colsum(dx[psi:].as_strided((S, n_patch * C), (P * C, 1)),
+                           dino.pos_embed.grad[0, 1:].reshape(-1), accumulate=True)
             conv = dino.patch_embed.proj
         else:
             conv = agg.patch_embed.proj

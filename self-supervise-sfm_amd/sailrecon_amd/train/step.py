@@ -15,6 +15,7 @@ zero grads on every rank and are not reduced (their mean is zero either way).
 
 from __future__ import annotations
 
+from pathlib import Path
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -33,6 +34,23 @@ def prepare_model_input(rgb: Tensor) -> Tuple[Tensor, List[int], List[int]]:
     return torch.cat([rgb, rgb], 0)[None], list(range(n)), list(range(n, 2 * n))
 
 
+def save_checkpoint(model, optimizer, scheduler, scaler, step: int, loss, checkpoint_dir,
+                    is_distributed: bool = False) -> Path:
+    """train_imc.py:272-286: model weights only, as ``model_step_<step>.pt`` and ``model_latest.pt``
+    (a plain state_dict with the reference's keys, so the reference's own loader and
+    ``SailRecon.load_state_dict`` both read it).  The trainer's parameters are views into its flat
+    fp32 buffer (train.params.FlatParams), so ``state_dict()`` already holds the updated weights.
+    ``optimizer`` / ``scheduler`` / ``scaler`` / ``loss`` are accepted and unused, as in the reference."""
+    del optimizer, scheduler, scaler, loss
+    checkpoint_dir = Path(checkpoint_dir)
+    checkpoint_dir.mkdir(parents=True, exist_ok=True)
+    sd = model.module.state_dict() if is_distributed else model.state_dict()
+    path = checkpoint_dir / f"model_step_{step}.pt"
+    torch.save(sd, path)
+    torch.save(sd, checkpoint_dir / "model_latest.pt")
+    return path
+
+
 class Trainer:
     def __init__(self, model, *, max_lr: float = 2e-4, warmup_steps: int = 2000, max_steps: int = 100_000,
                  group=None, grad_scaler: bool = True, cdf: Optional[CDFLossIndexPytorch] = None):
@@ -47,6 +65,7 @@ class Trainer:
         self.group = group
         self.world = dist.get_world_size(group) if group is not None else 1
         self._works = []
+        self.steps_done = 0
         self._reduced: Dict[int, Tuple[int, int]] = {}
         self._slices = self._module_slices(model)
         self._skip = self._no_grad_slices(model)
@@ -131,4 +150,10 @@ class Trainer:
         if not found:
             self.graph.refresh_packs()
         lr = self.sched.step()
+        self.steps_done += 1
         return {"loss": float(loss.item()), "lr": lr, "skipped": found}
+
+    def save_checkpoint(self, checkpoint_dir, loss=None) -> Path:
+        """Rank 0 saves (train_imc.py:426-428 guards the call with is_main_process)."""
+        return save_checkpoint(self.graph.model, self.opt, self.sched, self.scaler, self.steps_done, loss,
+                               checkpoint_dir)

@@ -136,3 +136,23 @@ def test_deferred_residuals_equal_fused_epilogues(monkeypatch):
         outs.append((feats[1].clone(), feats[3].clone(), cam_last.clone(), poses[-1].clone()))
     for a, b in zip(*outs):
         assert rel_l2(b.numpy(), a.numpy()) < 1e-6
+
+
+def test_save_checkpoint_writes_flat_trained_weights(tmp_path):
+    """train.step.save_checkpoint (train_imc.py:272-286): model_step_<k>.pt + model_latest.pt,
+    weights only, holding the values in the trainer's flat fp32 buffer (parameters are views into
+    it), loadable with torch.load(weights_only=True) and the reference's key names."""
+    import torch
+    from sailrecon_amd.train.params import FlatParams
+    from sailrecon_amd.train.step import save_checkpoint
+    from sailrecon_amd.layers.block import Block
+    torch.manual_seed(0)
+    m = Block(dim=128, num_heads=2, qk_norm=True, init_values=0.01)
+    flat = FlatParams(m)
+    flat.data.add_(0.5)  # an "optimizer step" on the flat buffer
+    path = save_checkpoint(m, None, None, None, 7, 1.25, tmp_path / "ck")
+    assert path.name == "model_step_7.pt" and (tmp_path / "ck" / "model_latest.pt").exists()
+    sd = torch.load(path, weights_only=True)
+    assert set(sd) == set(m.state_dict())
+    for n, p in m.named_parameters():
+        assert torch.equal(sd[n], flat.view(flat.data, n)), n
