@@ -403,6 +403,11 @@ int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx,
 int sr_qk_bwd(sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds, void* out,
               int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace);
 
+/* sr_qk_bwd for fp32 blocks (autocast off: the reference's fp32 Attention with qk_norm / RoPE):
+ * raw and out fp32, otherwise identical.  out may alias dsrc (same ld). */
+int sr_qk_bwd_f32(sr_stream_t stream, const float* raw, int64_t ldr, const float* dsrc, int64_t lds, float* out,
+                  int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace);
+
 /* out[r, c] = bf16(scale * src[r, c])  (fp32 -> bf16 GEMM operands), cols % 4 == 0 */
 int sr_cast_bf16(sr_stream_t stream, const float* src, int64_t lds, void* dst, int64_t ldd, int rows, int cols,
                  float scale);

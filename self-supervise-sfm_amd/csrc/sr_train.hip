@@ -461,9 +461,12 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // ================================================================ qk-norm + RoPE backward
 // One wave per row; 4 heads per pass (16 lanes x 4 values per head: dims 4 li .. 4 li + 3).
 // RoPE pairs (d, d + 16) of each half sit in lanes li and li ^ 4.
-__global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ raw, int64_t ldr,
-                                                     const float* __restrict__ dsrc, int64_t lds, bf16* out,
+// T = bf16 (autocast blocks) or float (fp32 blocks): the type of raw and out.
+template <typename T>
+__global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, int64_t ldr,
+                                                     const float* __restrict__ dsrc, int64_t lds, T* out,
                                                      int64_t ldo, int rows, int ncols, sr_gemm_epi ep, float* part) {
+  constexpr bool BF = sr::is_bf16<T>::value;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   const int C = ep.embed_dim;
@@ -500,13 +503,20 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
     // math (16 heads of loads in flight per wave; one pass at a time left HBM latency exposed)
     for (int cb = 0; cb < ncols; cb += 1024) {
       float4 d4s[4];
-      bf16x4 r4s[4] = {};
+      f32x4 r4s[4] = {};
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         // a short last pass computes on clamped columns and stores nothing
         const int col = min(cb + 256 * p + 4 * lane, ncols - 4);
         d4s[p] = *(const float4*)(dsrc + (int64_t)row * lds + col);
-        if (norm && (col + ep.col_offset) / C < 2) r4s[p] = *(const bf16x4*)(raw + (int64_t)row * ldr + col);
+        if (norm && (col + ep.col_offset) / C < 2) {
+          if constexpr (BF) {
+            const bf16x4 r = *(const bf16x4*)(raw + (int64_t)row * ldr + col);
+            r4s[p] = f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+          } else {
+            r4s[p] = *(const f32x4*)(raw + (int64_t)row * ldr + col);
+          }
+        }
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -526,8 +536,8 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
           for (int e = 0; e < 4; ++e) d[e] = first ? fmaf(cs[e], d[e], sn[e] * pd[e]) : fmaf(cs[e], d[e], -sn[e] * pd[e]);
         }
         if (norm) {
-          const bf16x4 r4 = r4s[p];
-          float v[4] = {(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
+          const f32x4 r4 = r4s[p];
+          float v[4] = {r4[0], r4[1], r4[2], r4[3]};
           float s = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
           for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
@@ -573,7 +583,12 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const bf16* __restrict__ ra
           for (int e = 0; e < 4; ++e) d[e] = rstd * (g[e] - sg - v[e] * sgx);
         }
       }
-      if (live) *(bf16x4*)(out + (int64_t)row * ldo + col) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+      if (live) {
+        if constexpr (BF)
+          *(bf16x4*)(out + (int64_t)row * ldo + col) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+        else
+          *(f32x4*)(out + (int64_t)row * ldo + col) = f32x4{d[0], d[1], d[2], d[3]};
+      }
       }
       }
     }
@@ -963,26 +978,39 @@ extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, i
   return sr::check_launch("sr_layernorm_bwd");
 }
 
-extern "C" int sr_qk_bwd(sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds, void* out,
-                         int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace) {
-  SR_CHECK(dsrc && out && ep && rows > 0, SR_EINVAL, "sr_qk_bwd: null pointer / no rows");
+template <typename T>
+static int qk_bwd(const char* who, sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds,
+                  void* out, int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace) {
+  SR_CHECK(dsrc && out && ep && rows > 0, SR_EINVAL, "%s: null pointer / no rows", who);
   SR_CHECK(ep->head_dim == 64 && ep->embed_dim % 64 == 0 && ncols % 64 == 0, SR_EUNSUPPORTED,
-           "sr_qk_bwd: head_dim 64 and ncols %% 64 == 0 only (ncols=%d)", ncols);
+           "%s: head_dim 64 and ncols %% 64 == 0 only (ncols=%d)", who, ncols);
   const bool norm = ep->qn_w != nullptr;
   SR_CHECK(!norm || (raw && ep->qn_b && ep->kn_w && ep->kn_b && grads && workspace), SR_EINVAL,
-           "sr_qk_bwd: qk-norm needs raw, the four norm params, grads and workspace");
+           "%s: qk-norm needs raw, the four norm params, grads and workspace", who);
   SR_CHECK(!ep->rope_cos || (ep->rope_sin && (ep->pos_yx || (ep->tokens_per_frame > ep->patch_start && ep->grid_w > 0))),
-           SR_EINVAL, "sr_qk_bwd: rope params");
+           SR_EINVAL, "%s: rope params", who);
   hipStream_t s = (hipStream_t)stream;
   const int wgs = std::min(1024, (rows + 3) / 4);
-  hipLaunchKernelGGL(qk_bwd_kernel, dim3(wgs), dim3(256), 0, s, (const bf16*)raw, ldr, dsrc, lds, (bf16*)out, ldo,
+  hipLaunchKernelGGL(qk_bwd_kernel<T>, dim3(wgs), dim3(256), 0, s, (const T*)raw, ldr, dsrc, lds, (T*)out, ldo,
                      rows, ncols, *ep, workspace);
+  sr::note_kernel("qk_bwd_kernel<%s>", sr::is_bf16<T>::value ? "__bf16" : "float");
   if (norm) {  // [wgs*4][4][64] -> grads[4][64]
     const int rc = colsum_launch(s, SR_F32, workspace, 256, wgs * 4, 256, grads, 1, 1.f,
                                  workspace + (int64_t)wgs * 4 * 256);
     if (rc) return rc;
   }
-  return sr::check_launch("sr_qk_bwd");
+  return sr::check_launch(who);
+}
+
+extern "C" int sr_qk_bwd(sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds, void* out,
+                         int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace) {
+  return qk_bwd<bf16>("sr_qk_bwd", stream, raw, ldr, dsrc, lds, out, ldo, rows, ncols, ep, grads, workspace);
+}
+
+extern "C" int sr_qk_bwd_f32(sr_stream_t stream, const float* raw, int64_t ldr, const float* dsrc, int64_t lds,
+                             float* out, int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads,
+                             float* workspace) {
+  return qk_bwd<float>("sr_qk_bwd_f32", stream, raw, ldr, dsrc, lds, out, ldo, rows, ncols, ep, grads, workspace);
 }
 
 extern "C" int sr_cast_bf16(sr_stream_t stream, const float* src, int64_t lds, void* dst, int64_t ldd, int rows,

@@ -235,9 +235,10 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
         draw = sc.get("draw", R, 3 * C, dt, dev)
         ops.qk_bwd(tape.raw if qkv_epi is not None else None, dqkv, draw, qkv_epi or dict(embed_dim=C, head_dim=64),
                    grads=g.qkn)
+    elif qkv_epi is not None:  # fp32 block (autocast off) with qk-norm / RoPE: in place on dqkv
+        ops.qk_bwd(tape.raw, dqkv, dqkv, qkv_epi, grads=g.qkn)
+        draw = dqkv
     else:
-        if qkv_epi is not None:
-            raise NotImplementedError("fp32 block backward with qk-norm / RoPE")
         draw = dqkv
     ops.gemm(draw, bp.wt_qkv, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
     wgrad(draw, tape.xn1, g.w_qkv, db=g.b_qkv)

@@ -136,6 +136,59 @@ def test_block_backward_fp32_camera():
         assert rel(p.grad, ref[n].grad) < 1e-4, n
 
 
+def test_block_backward_fp32_qknorm_rope():
+    """fp32 aggregator-style block (qk-norm + 2-D RoPE, autocast off): the backward runs
+    sr_qk_bwd_f32 in place on dq|dk (VERDICT r3 missing 3) -> 1e-4 like the fp32 camera block."""
+    from oracle import sfm_oracle as O
+    from sailrecon_amd import ops, runtime
+    from sailrecon_amd.layers.block import Block
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    from sailrecon_amd.train import engine
+    from sailrecon_amd.train.params import FlatParams
+    torch.manual_seed(0)
+    C, H, gh, gw = 256, 4, 4, 5
+    P = 5 + gh * gw
+    rope = RotaryPositionEmbedding2D(100)
+    blk = Block(dim=C, num_heads=H, init_values=0.01, qk_norm=True, rope=rope)
+    _randomize(blk, 3)
+    sd = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    blk = blk.to(DEV)
+    fp = FlatParams(blk)
+    blk.invalidate_packed()
+    dt = torch.float32
+    pb = blk.packed(dt)
+    tabs = rope.tables(C // H, max(gh, gw) + 1, DEV)
+    qkv_epi = runtime.qkv_params(pb, tabs, pos_row_base=0, tokens_per_frame=P, patch_start=5, grid_w=gw)
+    tape = engine.alloc_tape(P, C, 4 * C, dt, DEV, 0, separate_raw=True)
+
+    def fwd(qkv, o, lse):
+        ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=C // H, batch=1, lq=P,
+                      q_bstride=0, l0=P, k0_bstride=0)
+
+    def bwd(tp, dO, dqkv):
+        q = tp.qkv
+        ops.attention_bwd_small(q[:, 0:C], q[:, C:2 * C], q[:, 2 * C:], dO, dqkv[:, 0:C], dqkv[:, C:2 * C],
+                                dqkv[:, 2 * C:], heads=H, head_dim=C // H)
+    x = torch.randn(P, C)
+    xd = x.to(DEV)
+    engine.run_block_train(pb, xd, 0, P, tape, fwd, qkv_epi)
+    dy = torch.randn(P, C)
+    dx = dy.to(DEV)
+    fp.zero_grad()
+    bp = engine.pack_bwd(blk, pb, dt)
+    engine.block_bwd(pb, bp, engine.block_grads(blk), tape, dx, None, bwd, qkv_epi, engine.BwdScratch())
+    torch.cuda.synchronize()
+    ref = {k: v.clone().requires_grad_(True) for k, v in sd.items() if v.is_floating_point()}
+    xr = x.clone().requires_grad_(True)
+    pos = _positions(1, P, gw).view(1, P, 2)
+    y = O.block(ref, "", xr[None], H, 1e-5, pos=pos, qk_norm=True, rope_base=100.0)
+    y.backward(dy[None])
+    assert rel(xd, y.detach()[0]) < 1e-5
+    assert rel(dx, xr.grad) < 1e-4, "input grad"
+    for n, p in blk.named_parameters():
+        assert rel(p.grad, ref[n].grad) < 1e-4, n
+
+
 def test_block_backward_c4_global():
     """BASELINE C4 (train_imc, 16 views): ONE full-width aggregator global block (C = 1024, 16
     heads, qk-norm + RoPE) forward-with-tape + backward over L_g = 16 x 1374 = 21,984 anchor
