@@ -31,6 +31,10 @@ Prints ONE JSON line on rank 0 (contract in the task statement) with a
 ``roofline`` object for the dominant kernel class (live HIP-event timing inside
 the timed region) and a ``cpu_baseline`` object (the CPU oracle on a bounded
 sample, rank 0 at N=1 only).  A per-kernel-class breakdown goes to stderr.
+After the headline's timed region the same model also times the ``extra_configs`` (--extras):
+N=64 @518 (the north star's 64-view scaling workload, sharded like the headline) and, on one GPU,
+BASELINE C5 (N=128 @518 with fp8 global attention); they ride inside the one line and are
+never its ``value``.
 """
 
 from __future__ import annotations
@@ -368,9 +372,13 @@ def main():
     ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
                     help="BASELINE C5: the global blocks' q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 "
                          "e4m3; everything else bf16")
-    ap.add_argument("--extra-c5", choices=["off", "qk", "qkv"], default="off",
-                    help="opt-in SECOND JSON object after the headline line: BASELINE C5 (N=128 @518, global "
-                         "attention in fp8: qk or qkv) timed on the same model")
+    ap.add_argument("--extras", default="n64,c5",
+                    help="comma list of extra workloads timed after the headline on the same model and reported "
+                         "inside its line as extra_configs (not the metric): n64 = N=64 @518 bf16 (the north "
+                         "star's 64-view scaling workload, sharded like the headline), c5 = BASELINE C5 (N=128 "
+                         "@518, global attention in fp8; one GPU only); '' or 'none' to skip")
+    ap.add_argument("--c5-fp8", choices=["qk", "qkv"], default="qk",
+                    help="C5 extra: q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 e4m3")
     ap.add_argument("--launch-only", action="store_true",
                     help="launcher / process-group / ranks_seen check without the model (gloo if no GPU)")
     args = ap.parse_args()
@@ -497,6 +505,15 @@ def main():
                                                    for kk, vv in v.items()} for k, v in breakdown.items()},
                           "step_ms": dt / args.steps * 1e3}), file=sys.stderr)
 
+    extras = []
+    if use_bf16 and not fp8:
+        for name in [e for e in args.extras.split(",") if e and e != "none"]:
+            if name == "c5" and world > 1:
+                continue
+            if name not in ("n64", "c5"):
+                raise SystemExit(f"bench.py: unknown extra workload {name!r}")
+            extras.append(extra_config(model, device, args, world, name))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline({k: v for k, v in sd.items()}, args.img, n, args.cpu_views)
@@ -527,26 +544,32 @@ def main():
                        "achieved_tflops_whole_step": round(tflop * args.steps / dt, 1)},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "extra_configs": extras,
         }
         print(json.dumps(line))
-    if args.extra_c5 != "off" and use_bf16:
-        extra = c5_line(model, device, args, world, use_pg, seen)
-        if rank == 0:
-            print(json.dumps(extra))
     if use_pg:
         dist.destroy_process_group()
 
 
-def c5_line(model, device, args, world, use_pg, seen, n=128):
-    """BASELINE config 5 (N=128 @518, 256 frames, L_g = 175,872) with the global blocks' attention in
-    fp8 (Aggregator.set_fp8_global): a second, opt-in bench object beside the headline line."""
+def extra_config(model, device, args, world, name):
+    """An extra workload timed on the same model after the headline (reported inside the headline
+    line's ``extra_configs``, never as its value): ``n64`` = N=64 @518 bf16, the north star's
+    64-view scaling workload (frame-sharded like the headline when world > 1); ``c5`` = BASELINE
+    config 5 (N=128 @518, 256 frames, L_g = 175,872) with the global blocks' attention in fp8
+    (Aggregator.set_fp8_global), one GPU.  One untimed warmup, then a few steps between barriers +
+    synchronize, max over ranks.  A Python error is reported in the object, not raised."""
     from sailrecon_amd import ops
+    n = 64 if name == "n64" else 128
+    fp8 = name == "c5"
+    steps = 3 if name == "n64" else 2
     g = torch.Generator().manual_seed(n)
     x = torch.rand(n, 3, args.img, args.img, generator=g)
     images = torch.cat([x, x])[None].to(device)
     no_reloc, reloc = list(range(n)), list(range(n, 2 * n))
-    model.aggregator.set_fp8_global(True, fp8_v=args.extra_c5 == "qkv")
-    steps = max(1, args.steps // 2)
+    dtype = (f"bf16, global {'q.k^T' if args.c5_fp8 == 'qk' else 'q.k^T + P.V'} fp8-e4m3" if fp8 else "bf16")
+    out = {"name": name, "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px" + (
+        " (BASELINE C5, fp8 global attention)" if fp8 else " (north-star 64-view workload)"),
+           "unit": "views/s", "dtype": dtype, "views": n, "frames": 2 * n, "steps": steps, "warmup": 1}
 
     def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
@@ -557,7 +580,10 @@ def c5_line(model, device, args, world, use_pg, seen, n=128):
             dist.barrier()
         torch.cuda.synchronize()
 
+    timer = None
     try:
+        if fp8:
+            model.aggregator.set_fp8_global(True, fp8_v=args.c5_fp8 == "qkv")
         step()
         barrier()
         ops.TIMER = ops.KernelTimer()
@@ -567,30 +593,28 @@ def c5_line(model, device, args, world, use_pg, seen, n=128):
             step()
         barrier()
         dt = time.perf_counter() - t0
-        timer, ops.TIMER = ops.TIMER, None
+        timer = ops.TIMER
+    except Exception as e:  # noqa: BLE001  (reported, the headline stands)
+        out["error"] = f"{type(e).__name__}: {e}"
+        return out
     finally:
-        model.aggregator.set_fp8_global(False)
+        ops.TIMER = None
+        if fp8:
+            model.aggregator.set_fp8_global(False)
     dt_t = torch.tensor([dt], device=device)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
-    summ = timer.summary()
-    att = summ.get("attn_global")
+    att = timer.summary().get("attn_global") if timer is not None else None
     tflop = algorithmic_tflop(n, args.img)
-    return {
-        "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px (BASELINE C5, fp8 global attention)",
-        "value": n * steps / dt, "unit": "views/s", "n_gpus": dist.get_world_size() if use_pg else 1,
-        "steps": steps, "warmup": 1, "ms_per_step": dt / steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
-        "dtype": f"bf16, global {'q.k^T' if args.extra_c5 == 'qk' else 'q.k^T + P.V'} fp8-e4m3",
-        "data": "synthetic (seeded U[0,1) images, seeded synthetic weights)",
-        "config": {"workload": f"N={n} views @{args.img}px duplicated to {2 * n} frames, fix_rank=300",
-                   "views": n, "img": args.img, "frames": 2 * n, "algorithmic_tflop_per_step": round(tflop, 2),
-                   "achieved_tflops_whole_step": round(tflop * steps / dt, 1)},
-        "attn_global": None if att is None else {"avg_launch_ms": round(att["avg_ms"], 4),
-                                                 "tflops": round(att["tflops"], 1)},
-        "ranks_seen": seen,
-    }
+    out.update({"value": n * steps / dt, "ms_per_step": dt / steps * 1e3,
+                "algorithmic_tflop_per_step": round(tflop, 2),
+                "achieved_tflops_whole_step": round(tflop * steps / dt, 1),
+                "attn_global": None if att is None else {"avg_launch_ms": round(att["avg_ms"], 4),
+                                                         "tflops": round(att["tflops"], 1),
+                                                         "kernels": att.get("kernels")}})
+    del images
+    return out
 
 
 if __name__ == "__main__":

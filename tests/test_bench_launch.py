@@ -70,10 +70,13 @@ def test_bench_rccl_world1():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(29500 + os.getpid() % 1000))
     r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--steps", "1", "--warmup", "1", "--views", "2",
-                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+                        "--no-cpu-baseline", "--extras", "n64"], capture_output=True, text=True, timeout=600, env=env,
+                       cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _json_line(r.stdout)
     assert line["n_gpus"] == 1 and line["backend"] == "nccl"
     assert line["value"] > 0
+    (x,) = line["extra_configs"]  # the 64-view extra workload rides inside the one line
+    assert x["name"] == "n64" and "error" not in x and x["value"] > 0
     (seen,) = line["ranks_seen"]
     assert seen["rank"] == 0 and seen["device"].startswith("cuda") and "pci_bus" in seen
