@@ -21,3 +21,4 @@ run ktrain 600 python tools/kbench.py train
 run tln 200 python -m pytest tests/test_kernels_gpu.py -q -m gpu -k residual_layernorm
 run kln 200 python tools/kbench.py ln attn_frame_cfg
 run k2 300 python tools/kbench.py attn_gain
+run bench 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
