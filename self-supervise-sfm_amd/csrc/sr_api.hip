@@ -21,7 +21,7 @@ constexpr TuneDef kTune[SR_TUNE_COUNT] = {
     {"SR_ATTN_MZERO", 1},   {"SR_ATTN_CFG", -1},      {"SR_ATTN_PIPE", 1},       {"SR_ATTN_PIPE_SEG", 0},
     {"SR_ATTN_NO_SHORT", 0}, {"SR_GEMM_GROUP_M", -1}, {"SR_GEMM_SMALLM", 1},     {"SR_GEMM_NO256", 0},
     {"SR_GEMM_REG_EPI", 0},  {"SR_CONV_NO_NARROW", 0}, {"SR_WGRAD256", 1},       {"SR_SYNC_CHECK", 0},
-    {"SR_RLN_WIDE", 0},
+    {"SR_RLN_WIDE", 0},      {"SR_GEMM_TAIL", 0},
 };
 std::atomic<int> g_tune[SR_TUNE_COUNT];
 std::once_flag g_tune_once;
@@ -56,6 +56,18 @@ void note_kernel(const char* fmt, ...) {
 int tune(int key) {
   tune_init();
   return g_tune[key].load(std::memory_order_relaxed);
+}
+
+int cu_count() {
+  static std::once_flag once;
+  static int n = 256;
+  std::call_once(once, [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+  });
+  return n;
 }
 
 int check_launch(const char* what) {

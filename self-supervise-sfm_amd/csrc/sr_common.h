@@ -26,6 +26,8 @@ int check_launch(const char* what);
 void note_kernel(const char* fmt, ...);
 // current value of a tuning switch (sfm_amd.h sr_tuning_key)
 int tune(int key);
+// compute units of the current device (read once; 256 on MI355X)
+int cu_count();
 
 template <typename T> struct is_bf16 { static constexpr bool value = false; };
 template <> struct is_bf16<bf16> { static constexpr bool value = true; };

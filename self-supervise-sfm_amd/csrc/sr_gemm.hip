@@ -841,6 +841,48 @@ int launch(const GemmArgs& a, hipStream_t s) {
   return sr::check_launch("sr_gemm");
 }
 
+// Rows [r0, r0 + rows) of a GEMM as a GEMM of its own: A / out / aux and the QKV epilogue's row
+// positions advanced by r0 (every epilogue but PATCH, whose row remap is absolute).
+static GemmArgs row_slice(const GemmArgs& a, int epi, int r0, int rows) {
+  GemmArgs b = a;
+  b.A += (int64_t)r0 * a.lda_b;
+  const int oes = (epi == SR_EPI_BIAS_RESID || epi == SR_EPI_F32) ? 4 : 2;  // bf16 GEMMs only
+  b.out = (char*)a.out + (int64_t)r0 * a.ldo * oes;
+  if (a.ep.aux) b.ep.aux = (char*)a.ep.aux + (int64_t)r0 * a.ep.ld_aux * 2;
+  if (a.ep.pos_yx) b.ep.pos_yx += 2 * (int64_t)r0;
+  else if (a.ep.pos_rowmap) b.ep.pos_rowmap += r0;
+  else b.ep.pos_row_base += r0;
+  b.M = rows;
+  return b;
+}
+
+template <int EPI>
+int launch256_tail(GemmArgs a, hipStream_t s) {
+  // Last-round quantisation (SR_TUNE_GEMM_TAIL): with T tiles of 256x256 on C CUs (one workgroup
+  // each) the last round runs T % C tiles while the rest of the chip idles.  When the rows past the
+  // last whole round fit ONE round of the 128x128 kernel (two workgroups per CU), they go there as a
+  // second launch: the frame QKV at C3 is 4,128 tiles = 16 rounds + 32 tiles, so 341 row tiles run
+  // in 16 rounds and the last 640 rows in 120 small tiles.  Same MFMA and k order per output tile.
+  if (sr::tune(SR_TUNE_GEMM_TAIL) && EPI != SR_EPI_PATCH) {
+    const int ntn = a.N / BIG, cus = sr::cu_count();
+    const long tiles = (long)ntn * ((a.M + BIG - 1) / BIG);
+    const long whole = tiles / cus * cus;
+    const int main_rows = (int)(whole / ntn) * BIG;
+    const int rest = a.M - main_rows;
+    const long small = (long)((rest + BM - 1) / BM) * (a.N / BN);
+    if (tiles % cus != 0 && main_rows > 0 && rest > 0 && small <= 2L * cus) {
+      GemmArgs head = a;
+      head.M = main_rows;
+      int rc = launch256<EPI>(head, s);
+      if (rc != SR_OK) return rc;
+      rc = launch<bf16, EPI>(row_slice(a, EPI, main_rows, rest), s);
+      sr::note_kernel("gemm256_kernel<%d>", EPI);  // the launch the time goes to
+      return rc;
+    }
+  }
+  return launch256<EPI>(a, s);
+}
+
 template <typename T>
 int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
   if constexpr (sr::is_bf16<T>::value) {
@@ -850,13 +892,13 @@ int dispatch(int epi, const GemmArgs& a, hipStream_t s) {
     const long tiles256 = (long)(a.N / BIG) * ((a.M + BIG - 1) / BIG);
     if (!no_big && a.N % BIG == 0 && tiles256 >= 512) {
       switch (epi) {
-        case SR_EPI_BIAS: return launch256<SR_EPI_BIAS>(a, s);
-        case SR_EPI_BIAS_GELU: return launch256<SR_EPI_BIAS_GELU>(a, s);
-        case SR_EPI_BIAS_RESID: return launch256<SR_EPI_BIAS_RESID>(a, s);
-        case SR_EPI_QKV: return launch256<SR_EPI_QKV>(a, s);
+        case SR_EPI_BIAS: return launch256_tail<SR_EPI_BIAS>(a, s);
+        case SR_EPI_BIAS_GELU: return launch256_tail<SR_EPI_BIAS_GELU>(a, s);
+        case SR_EPI_BIAS_RESID: return launch256_tail<SR_EPI_BIAS_RESID>(a, s);
+        case SR_EPI_QKV: return launch256_tail<SR_EPI_QKV>(a, s);
         case SR_EPI_PATCH: return launch256<SR_EPI_PATCH>(a, s);
-        case SR_EPI_F32: return launch256<SR_EPI_F32>(a, s);
-        case SR_EPI_GELU_BWD: return launch256<SR_EPI_GELU_BWD>(a, s);
+        case SR_EPI_F32: return launch256_tail<SR_EPI_F32>(a, s);
+        case SR_EPI_GELU_BWD: return launch256_tail<SR_EPI_GELU_BWD>(a, s);
       }
     }
   }

@@ -441,8 +441,10 @@ def test_gemm_group(ops, epi_name):
         probs.append(p)
         plain.append(ref_out)
     ops.gemm_group(probs, epi)
-    for p, ref_out in zip(probs, plain):
-        ops.gemm(p["a"], p["w"], ref_out, epi, bias=p["bias"], gamma=p.get("gamma"), qkv=p.get("qkv"), splits=1)
+    with ops.tuning(SR_GEMM_TAIL=0):  # sr_gemm on the 256x256 kernel alone (no 128x128 tail launch)
+        for p, ref_out in zip(probs, plain):
+            ops.gemm(p["a"], p["w"], ref_out, epi, bias=p["bias"], gamma=p.get("gamma"), qkv=p.get("qkv"),
+                     splits=1)
     torch.cuda.synchronize()
     for p, ref_out in zip(probs, plain):
         assert torch.equal(p["out"], ref_out)
@@ -464,3 +466,50 @@ def test_residual_layernorm_variants(ops, var):
     torch.cuda.synchronize()
     assert torch.equal(x, xr)
     assert rel(out.float(), F.layer_norm(xr, (cols,), w, b, 1e-6)) < 5e-3
+
+
+@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])
+@pytest.mark.parametrize("M,N", [(43 * 256 - 100, 3072), (87936, 1024), (2 * 5496, 4096)])
+def test_gemm_tail_split(ops, epi_name, M, N):
+    """SR_GEMM_TAIL: the rows past the 256x256 kernel's last whole workgroup round run on the
+    128x128 kernel in a second launch (frame-sharded ranks' and C3's QKV / proj / fc2 sizes: 516
+    tiles = 2 rounds + 4; 1,376 = 5 + 96; 688 = 2 + 176).  Same function as the one-kernel launch:
+    within 1e-6 rel (fp32 accumulation in the same k order; the epilogues may contract differently);
+    the time-dominant kernel is still reported."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    L = _lib()
+    epi = getattr(L, "SR_EPI_" + epi_name)
+    K, C = 1024, 1024
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) / 32).bfloat16()
+    kw = dict(bias=torch.randn(N, device=DEV, generator=g))
+    if epi_name == "QKV":
+        if N % C:
+            pytest.skip("QKV needs whole q|k|v blocks")
+        rope = RotaryPositionEmbedding2D(100).tables(64, 40, DEV)
+        qn = [torch.randn(64, device=DEV, generator=g) for _ in range(4)]
+        kw["qkv"] = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
+                         rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37,
+                         pos_row_base=11, col_offset=3 * C - N)
+    if epi_name == "BIAS_RESID":
+        kw["gamma"] = torch.randn(N, device=DEV, generator=g)
+    if epi_name == "GELU_BWD":
+        kw = dict(aux=torch.randn(M, N, device=DEV, generator=g).bfloat16())
+    if epi_name in ("BIAS_RESID", "F32"):
+        x0 = torch.randn(M, N, device=DEV, generator=g)
+        out1, out0 = x0.clone(), x0.clone()
+    else:
+        out1 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        out0 = torch.zeros_like(out1)
+    with ops.tuning(SR_GEMM_TAIL=1):
+        ops.gemm(a, w, out1, epi, splits=1, **kw)
+        k1 = ops.last_kernel()
+    with ops.tuning(SR_GEMM_TAIL=0):
+        ops.gemm(a, w, out0, epi, splits=1, **kw)
+        k0 = ops.last_kernel()
+    torch.cuda.synchronize()
+    assert k1 == k0 and k0.startswith("gemm256_kernel"), (k1, k0)
+    same = torch.equal(out1, out0)
+    print(f"{epi_name} M={M} N={N}: bit-identical={same} rel={rel(out1.float(), out0.float()):.2e}")
+    assert rel(out1.float(), out0.float()) < 1e-6
