@@ -52,6 +52,14 @@ __device__ __forceinline__ void dma_rows(const bf16* base, int64_t ld, int row0,
   const int r = 8 * g + (lane >> 3);
   sr::dma16(base + (int64_t)min(row0 + r, nrows - 1) * ld + swz(r, lane & 7) * 8, lds_tile + g * 1024);
 }
+// Full tiles take the wave-uniform form (sr::dma16_s): a scalar row pointer + one of two per-lane
+// 32-bit byte offsets (row lane/8 of the piece, its swizzled chunk; the swizzle depends only on the
+// parity of the row group g, as 4g + lane/16 mod 8).  The per-lane form above (64-bit row multiply
+// and clamp per piece: ~60 VALU per tile, 12 of them quarter-rate) is kept for ragged tiles.
+__device__ __forceinline__ uint32_t piece_off(int64_t ld, int parity, int lane) {
+  const int r = 8 * parity + (lane >> 3);
+  return (uint32_t)(((lane >> 3) * ld + swz(r, lane & 7) * 8) * 2);
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -108,16 +116,17 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 #pragma unroll
       for (int j = 0; j < 8; ++j) s = fmaf((float)ov[j], (float)gv[j], s);
     }
-    b.delta[e] = s;
+    b.delta[e] = -s;  // stored negated: it seeds the dP chains as is
   }
 }
 
 // ---------------------------------------------------------------- dK, dV
 // grid (key tiles of 128, heads, SHARED ? 1 : batch); wave w owns keys tile*128 + 32 w + l32.
-// Q / dO tiles and their lse / delta stream through the LDS-DMA ring.  The resident K and V
-// fragments are negated (K also scaled by c) and the S / dP chains are seeded with +lse / +delta
-// straight from LDS, so the chains return -(c q.k - lse) and -(dO.v - delta): P = exp2(-S'),
-// dS = -P dP', the signs folding into the VALU source modifiers.
+// Q / dO tiles and their lse / delta stream through the LDS-DMA ring.  The resident K fragment is
+// negated and scaled by c and the S chain is seeded with +lse straight from LDS, so it returns
+// -(c q.k - lse) and P = exp2(-S') (the sign is a source modifier of v_exp); the dP chain is seeded
+// with the stored -delta (attn_bwd_delta_kernel) and returns dO.v - delta, so dS = P dP' with no
+// sign flips (a negated V turned into 24 v_xor per tile before the packed multiplies).
 template <int SEG>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
@@ -147,13 +156,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
   const float* const lsrc = wave_u == 0 ? f.lse : b.delta;
   // tile t = (item - it0) * ntq + query tile; cursors instead of divisions (the compiler
   // expands an integer division into ~15 VALU)
+  const int g0 = 4 * (wave_u & 1);
+  const uint32_t offA = piece_off(sld, 0, lane), offB = piece_off(sld, 1, lane);
   auto stage = [&](int t, int item, int q0) {
     const uint32_t sb = lds0 + (t & (NBUF - 1)) * STG;
     const bf16* tb = sbase + (int64_t)item * f.q_bstride * sld;
+    const float* lb = lsrc + ((int64_t)item * f.heads + head) * f.lq + q0;
+    if (q0 + 64 <= f.lq) {  // full tile: scalar pointers
+      const char* p = (const char*)(tb + (int64_t)(q0 + 8 * g0) * sld);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma_rows(tb, sld, q0, f.lq, 4 * (wave_u & 1) + i, lane, sb + (stage_o ? TB : 0));
-    if (wave_u < 2)
-      sr::dma4(lsrc + ((int64_t)item * f.heads + head) * f.lq + min(q0 + lane, f.lq - 1), sb + 2 * TB + wave_u * 256);
+      for (int i = 0; i < 4; ++i)
+        sr::dma16_s(p + (int64_t)8 * i * sld * 2, (i & 1) ? offB : offA, sb + (stage_o ? TB : 0) + (g0 + i) * 1024);
+      if (wave_u < 2) sr::dma4_s(lb, (uint32_t)lane * 4, sb + 2 * TB + wave_u * 256);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma_rows(tb, sld, q0, f.lq, g0 + i, lane, sb + (stage_o ? TB : 0));
+      if (wave_u < 2) sr::dma4(lb + min(lane, f.lq - 1 - q0), sb + 2 * TB + wave_u * 256);
+    }
   };
   int s_item = it0, s_q = 0;  // next tile to stage
   for (int i = 0; i < NBUF - 1 && i < ntiles; ++i) {
@@ -171,12 +190,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
   // would otherwise carry them into the loop, and a vmcnt wait there drains the ring
   __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < 4; ++s) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       kf[s][j] = (bf16)(-(float)kf[s][j] * c);
-      vf[s][j] = (bf16)(-(float)vf[s][j]);
     }
+    // keep the negated fragment in registers: otherwise the compiler re-derives it inside the
+    // tile loop (16 v_xor + 8 v_perm per tile and fragment set)
+    asm volatile("" : "+v"(kf[s]));
+  }
   const TrOff tro = tr_offsets(lane);
   f32x16 dk[2], dv[2];
 #pragma unroll
@@ -238,14 +260,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
     for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf, df;
+        f32x8 pv, dv8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int r = 8 * s2 + j;
-          const float p = __builtin_amdgcn_exp2f(-sc[qb2][r]);
-          pf[j] = (bf16)p;
-          df[j] = (bf16)(-(p * dp[qb2][r]));
+          pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
+          dv8[j] = pv[j] * dp[qb2][r];
         }
+        const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
         const int row0 = qb2 * 32 + 16 * s2;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -303,13 +325,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
   const bf16* const sb1 = f.l1 > 0 ? (const bf16*)(stage_v ? f.v1 : f.k1) + (int64_t)item * f.k1_bstride * (stage_v ? f.ldv1 : f.ldk1) + hcol
                                    : sb0;
   const int64_t sld0 = stage_v ? f.ldv0 : f.ldk0, sld1 = stage_v ? f.ldv1 : f.ldk1;
+  const int g0 = 4 * (wave_u & 1);
+  const uint32_t offA0 = piece_off(sld0, 0, lane), offB0 = piece_off(sld0, 1, lane);
+  const uint32_t offA1 = piece_off(sld1, 0, lane), offB1 = piece_off(sld1, 1, lane);
   auto stage = [&](int t) {
     const bool s1 = t >= nt0;
     const uint32_t sb = lds0 + (t & (NBUF - 1)) * 2 * TB + (stage_v ? TB : 0);
+    const bf16* base = s1 ? sb1 : sb0;
+    const int64_t ld = s1 ? sld1 : sld0;
+    const int r0 = (s1 ? t - nt0 : t) * 64, len = s1 ? f.l1 : f.l0;
+    if (r0 + 64 <= len) {  // full tile: scalar pointers
+      const char* p = (const char*)(base + (int64_t)(r0 + 8 * g0) * ld);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dma_rows(s1 ? sb1 : sb0, s1 ? sld1 : sld0, (s1 ? t - nt0 : t) * 64, s1 ? f.l1 : f.l0, 4 * (wave_u & 1) + i,
-               lane, sb);
+      for (int i = 0; i < 4; ++i)
+        sr::dma16_s(p + (int64_t)8 * i * ld * 2, (i & 1) ? (s1 ? offB1 : offB0) : (s1 ? offA1 : offA0),
+                    sb + (g0 + i) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma_rows(base, ld, r0, len, g0 + i, lane, sb);
+    }
   };
   for (int i = 0; i < NBUF - 1 && i < ntiles; ++i) stage(i);
 
@@ -327,12 +361,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * c);
   // the S / dP chains of every tile start from -lse / -delta (this lane's query row in every
-  // accumulator entry), so they return S' = c q.k - lse and dP' = dO.v - delta
+  // accumulator entry; delta is stored negated), so they return S' = c q.k - lse and dP' = dO.v - delta
   f32x16 nl, nd;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     nl[i] = -lse;
-    nd[i] = -dlt;
+    nd[i] = dlt;  // the stored -delta
   }
   const TrOff tro = tr_offsets(lane);
   f32x16 dq[2];
@@ -371,12 +405,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 df;
+        f32x8 d8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int r = 8 * s2 + j;
-          df[j] = (bf16)(__builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r]);
+          d8[j] = __builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r];
         }
+        const bf16x8 df = __builtin_convertvector(d8, bf16x8);
         const int row0 = kb * 32 + 16 * s2;
 #pragma unroll
         for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T

@@ -11,6 +11,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
@@ -139,6 +140,14 @@ __device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, uint32
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
   sbase = (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base)
+               : "memory", "m0");
+}
+// 4-byte form of dma16_s (lane l's dword at sbase + voff to LDS[lds_base + 4*l]).
+__device__ __forceinline__ void dma4_s(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  const uint64_t a = (uint64_t)(uintptr_t)sbase;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  sbase = (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base)
                : "memory", "m0");
 }
 
