@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 // -(c q.k - lse) and P = exp2(-S') (the sign is a source modifier of v_exp); the dP chain is seeded
 // with the stored -delta (attn_bwd_delta_kernel) and returns dO.v - delta, so dS = P dP' with no
 // sign flips (a negated V turned into 24 v_xor per tile before the packed multiplies).
-template <int SEG>
+template <int SEG, bool SP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
@@ -240,13 +240,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
         sc[qb2][4 * g] = l4.x; sc[qb2][4 * g + 1] = l4.y; sc[qb2][4 * g + 2] = l4.z; sc[qb2][4 * g + 3] = l4.w;
         dp[qb2][4 * g] = d4.x; dp[qb2][4 * g + 1] = d4.y; dp[qb2][4 * g + 2] = d4.z; dp[qb2][4 * g + 3] = d4.w;
       }
+    bf16x8 fq[4][2], fo[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int qb2 = 0; qb2 < 2; ++qb2) {
+        fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
+        fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
+      }
 #pragma unroll
     for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
 #pragma unroll
       for (int qb2 = 0; qb2 < 2; ++qb2) {
-        sc[qb2] = mfma32(row_frag(qt, qb2 * 32 + l32, s, hi), kf[s], sc[qb2]);
-        dp[qb2] = mfma32(row_frag(ot, qb2 * 32 + l32, s, hi), vf[s], dp[qb2]);
+        sc[qb2] = mfma32(fq[s][qb2], kf[s], sc[qb2]);
+        dp[qb2] = mfma32(fo[s][qb2], vf[s], dp[qb2]);
       }
+    if constexpr (SP) {
+      // software pipeline of the S / dP chains (SR_TUNE_BWD_SCHED): the 16 seed reads and k-step
+      // 0's four fragments, then k-step s+1's fragment reads in flight under k-step s's four MFMAs
+      // (the default schedule puts every read right before its MFMA behind an lgkmcnt(0))
+      __builtin_amdgcn_sched_group_barrier(0x100, 20, 0);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
     if constexpr (decltype(masked)::value) {  // clamped duplicate rows of the ragged tile get P = 0
       const int qv = f.lq - cq * 64;  // valid query rows of this tile
 #pragma unroll
@@ -304,6 +324,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
 
 // ---------------------------------------------------------------- dQ
 // grid (query tiles of 128, heads, batch); wave w owns query rows tile*128 + 32 w + l32.
+template <bool SP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b) {
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TB];  // ring of K tile | V tile stages
   const sr_attn_desc& f = b.f;
@@ -383,13 +404,30 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
     const char* kt = smem + (t & (NBUF - 1)) * 2 * TB;
     const char* vt = kt + TB;
     f32x16 sc[2], dp[2];
+    bf16x8 fk[4][2], fv[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        fk[s][kb] = row_frag(kt, kb * 32 + l32, s, hi);
+        fv[s][kb] = row_frag(vt, kb * 32 + l32, s, hi);
+      }
 #pragma unroll
     for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        sc[kb] = mfma32(row_frag(kt, kb * 32 + l32, s, hi), qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
-        dp[kb] = mfma32(row_frag(vt, kb * 32 + l32, s, hi), of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
+        sc[kb] = mfma32(fk[s][kb], qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
+        dp[kb] = mfma32(fv[s][kb], of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
       }
+    if constexpr (SP) {  // the dK / dV kernel's pipeline of the S / dP fragment reads
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
     if constexpr (decltype(masked)::value) {  // partial key tile: keys >= valid get S' = -inf, P = 0
       const int seg = t >= nt0;
       const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
@@ -454,11 +492,18 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   const int64_t nrows = (int64_t)f.batch * f.heads * f.lq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<0>, dim3((f.l0 + 127) / 128, f.heads, f.k0_bstride == 0 ? 1 : f.batch),
-                     dim3(256), 0, s, b);
-  if (f.l1 > 0)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, dim3((f.l1 + 127) / 128, f.heads, f.k1_bstride == 0 ? 1 : f.batch),
-                       dim3(256), 0, s, b);
+  const dim3 gq((f.lq + 127) / 128, f.heads, f.batch);
+  if (sr::tune(SR_TUNE_BWD_SCHED)) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, gq, dim3(256), 0, s, b);
+  else hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, gq, dim3(256), 0, s, b);
+  const dim3 g0((f.l0 + 127) / 128, f.heads, f.k0_bstride == 0 ? 1 : f.batch);
+  const dim3 g1((f.l1 + 127) / 128, f.heads, f.k1_bstride == 0 ? 1 : f.batch);
+  if (sr::tune(SR_TUNE_BWD_SCHED)) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, true>), g0, dim3(256), 0, s, b);
+    if (f.l1 > 0) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), g1, dim3(256), 0, s, b);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, false>), g0, dim3(256), 0, s, b);
+    if (f.l1 > 0) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), g1, dim3(256), 0, s, b);
+  }
+  sr::note_kernel("attn_bwd_dkdv_kernel<0, %s>", sr::tune(SR_TUNE_BWD_SCHED) ? "true" : "false");
   return sr::check_launch("sr_attention_bwd");
 }
