@@ -76,7 +76,7 @@ enum sr_tuning_key {
                                (HIP_LAUNCH_BLOCKING-style attribution; not graph-capturable) */
   SR_TUNE_RLN_WIDE = 12,    /* sr_residual_layernorm variant bits: 1 16-B lanes, 2 two rows per wave, 4 nt x stores (0) */
   SR_TUNE_GEMM_TAIL = 13,   /* 1: a 256x256 GEMM whose last workgroup round would run few tiles computes
-                               the rows past its last whole round on the 128x128 kernel (second launch)  (0) */
+                               the rows past its last whole round on the 128x128 kernel (second launch)  (1) */
   SR_TUNE_BWD_SCHED = 14,   /* 1: attention backward dK/dV kernel with its S / dP fragment reads software-
                                pipelined under the MFMAs (sched_group_barrier)                           (0) */
   SR_TUNE_COUNT = 15
