@@ -275,26 +275,69 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
         for (int r = 0; r < 16; ++r)
           if (qb2 * 32 + acc_row(r, hi) >= qv) sc[qb2][r] = INFINITY;
     }
-    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
+    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS,
+    // in four groups g = (qb2, s2) of 16 query rows
+    auto group = [&](int g, const bf16x8 (&to)[2], const bf16x8 (&tq)[2]) __attribute__((always_inline)) {
+      const int qb2 = g >> 1, s2 = g & 1;
+      f32x8 pv, dv8;
 #pragma unroll
-    for (int qb2 = 0; qb2 < 2; ++qb2)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        f32x8 pv, dv8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = 8 * s2 + j;
-          pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
-          dv8[j] = pv[j] * dp[qb2][r];
-        }
-        const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
-        const int row0 = qb2 * 32 + 16 * s2;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
-          dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
-        }
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * s2 + j;
+        pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
+        dv8[j] = pv[j] * dp[qb2][r];
       }
+      const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dv[db] = mfma32(to[db], pf, dv[db]);
+        dk[db] = mfma32(tq[db], df, dk[db]);
+      }
+    };
+    auto load = [&](int g, bf16x8 (&to)[2], bf16x8 (&tq)[2]) __attribute__((always_inline)) {
+      const int row0 = (g >> 1) * 32 + 16 * (g & 1);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        to[db] = tr_frag(ot, row0, tro.off[db]);
+        tq[db] = tr_frag(qt, row0, tro.off[db]);
+      }
+    };
+    if constexpr (SP) {
+      // group g+1's eight transposed reads issued in the stage that computes group g (stages
+      // fenced by sched_barrier, so each MFMA waits only for reads of the stage before)
+      bf16x8 toA[2], tqA[2], toB[2], tqB[2];
+      load(0, toA, tqA);
+      __builtin_amdgcn_sched_barrier(0);
+      load(1, toB, tqB);
+      group(0, toA, tqA);
+      __builtin_amdgcn_sched_barrier(0);
+      load(2, toA, tqA);
+      group(1, toB, tqB);
+      __builtin_amdgcn_sched_barrier(0);
+      load(3, toB, tqB);
+      group(2, toA, tqA);
+      __builtin_amdgcn_sched_barrier(0);
+      group(3, toB, tqB);
+    } else {
+#pragma unroll
+      for (int qb2 = 0; qb2 < 2; ++qb2)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          f32x8 pv, dv8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int r = 8 * s2 + j;
+            pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
+            dv8[j] = pv[j] * dp[qb2][r];
+          }
+          const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
+          const int row0 = qb2 * 32 + 16 * s2;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
+            dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
+          }
+        }
+    }
   };
   // tiles item by item; the last query tile of an item is the only one that can be ragged
   const bool ragged = f.lq % 64 != 0;
