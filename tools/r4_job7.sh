@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# round-4 GPU job 7: every GPU test + smoke (final tree), then attention-backward counters
+set -u
+mkdir -p gpurun_out
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/job.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/job.log
+  grep -v amdgpu.ids "gpurun_out/$name.log" | tail -n 4
+  if [ "$rc" -ne 0 ]; then echo "=== $name failed (rc=$rc): stopping"; exit "$rc"; fi
+}
+T="--timeout 600 --timeout-method thread"
+run gputests 900 python -u -m pytest tests -x -q -m gpu $T
+run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+run kbwd_stats 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bwd -o run --output-format csv -- python3 tools/kbench.py attn_bwd
+run pmc_bwd1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_bwd1 -o run --output-format csv -- python3 tools/kbench.py attn_bwd
+run pmc_bwd2 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_bwd2 -o run --output-format csv -- python3 tools/kbench.py attn_bwd
