@@ -264,12 +264,20 @@ def test_global_attention_key_split(ops, G):
         ops._KSPLIT_ENV = saved
     torch.cuda.synchronize()
     assert _rel(outs[1].float(), outs[0].float()) < 1e-2
-    assert float((lses[1] - lses[0]).abs().max()) < 1e-2
     rows = _sample_rows(lq, 256, G).to(DEV)
     ref = _ref_rows(qs[rows], k, v, D ** -0.5)
+    # fp64 log2-domain LSE of the sampled rows; the kernels round c*q to bf16, an error that grows
+    # with |S| (the spike keys score ~30 in log2 units here), so the LSE bound is 2e-2 against fp64
+    s_ref = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double()) * D ** -0.5
+    ref_lse = torch.logsumexp(s_ref, -1) / math.log(2.0)
+    e_split = float((lses[1][:, rows].double() - ref_lse).abs().max())
+    e_one = float((lses[0][:, rows].double() - ref_lse).abs().max())
+    e_pair = float((lses[1] - lses[0]).abs().max())
     print(f"key split S={parts}: rel {_rel(outs[1][rows].float(), ref):.2e} (unsplit "
-          f"{_rel(outs[0][rows].float(), ref):.2e})")
+          f"{_rel(outs[0][rows].float(), ref):.2e}); LSE vs fp64 {e_split:.2e} (unsplit {e_one:.2e}), "
+          f"split vs unsplit {e_pair:.2e}")
     assert _rel(outs[1][rows].float(), ref) < 1e-2
+    assert e_split < 2e-2 and e_one < 2e-2 and e_pair < 2e-2
 
 
 def test_attn_merge_n_seg_rows_fp32(ops):

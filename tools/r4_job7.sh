@@ -12,7 +12,8 @@ run() {  # name seconds cmd...
   if [ "$rc" -ne 0 ]; then echo "=== $name failed (rc=$rc): stopping"; exit "$rc"; fi
 }
 T="--timeout 600 --timeout-method thread"
-run gputests 900 python -u -m pytest tests -x -q -m gpu $T
+run gputests 900 python -u -m pytest tests --maxfail 5 -q -m gpu $T
+run keysplit 120 python -u -m pytest tests/test_baseline_shapes_gpu.py -q -s -m gpu -k key_split $T
 run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 run kbwd_stats 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bwd -o run --output-format csv -- python3 tools/kbench.py attn_bwd
 run pmc_bwd1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_bwd1 -o run --output-format csv -- python3 tools/kbench.py attn_bwd
