@@ -240,84 +240,103 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
         sc[qb2][4 * g] = l4.x; sc[qb2][4 * g + 1] = l4.y; sc[qb2][4 * g + 2] = l4.z; sc[qb2][4 * g + 3] = l4.w;
         dp[qb2][4 * g] = d4.x; dp[qb2][4 * g + 1] = d4.y; dp[qb2][4 * g + 2] = d4.z; dp[qb2][4 * g + 3] = d4.w;
       }
-    bf16x8 fq[4][2], fo[4][2];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2) {
-        fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
-        fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
-      }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
-#pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2) {
-        sc[qb2] = mfma32(fq[s][qb2], kf[s], sc[qb2]);
-        dp[qb2] = mfma32(fo[s][qb2], vf[s], dp[qb2]);
-      }
-    if constexpr (SP) {
-      // software pipeline of the S / dP chains (SR_TUNE_BWD_SCHED): the 16 seed reads and k-step
-      // 0's four fragments, then k-step s+1's fragment reads in flight under k-step s's four MFMAs
-      // (the default schedule puts every read right before its MFMA behind an lgkmcnt(0))
-      __builtin_amdgcn_sched_group_barrier(0x100, 20, 0);
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
-    if constexpr (decltype(masked)::value) {  // clamped duplicate rows of the ragged tile get P = 0
-      const int qv = f.lq - cq * 64;  // valid query rows of this tile
-#pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2)
+    // clamped duplicate rows of the ragged tile get P = 0
+    auto mask_rows = [&](int qb2) __attribute__((always_inline)) {
+      if constexpr (decltype(masked)::value) {
+        const int qv = f.lq - cq * 64;  // valid query rows of this tile
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           if (qb2 * 32 + acc_row(r, hi) >= qv) sc[qb2][r] = INFINITY;
-    }
-    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS,
-    // in four groups g = (qb2, s2) of 16 query rows
-    auto group = [&](int g, const bf16x8 (&to)[2], const bf16x8 (&tq)[2]) __attribute__((always_inline)) {
-      const int qb2 = g >> 1, s2 = g & 1;
-      f32x8 pv, dv8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = 8 * s2 + j;
-        pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
-        dv8[j] = pv[j] * dp[qb2][r];
-      }
-      const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        dv[db] = mfma32(to[db], pf, dv[db]);
-        dk[db] = mfma32(tq[db], df, dk[db]);
-      }
-    };
-    auto load = [&](int g, bf16x8 (&to)[2], bf16x8 (&tq)[2]) __attribute__((always_inline)) {
-      const int row0 = (g >> 1) * 32 + 16 * (g & 1);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        to[db] = tr_frag(ot, row0, tro.off[db]);
-        tq[db] = tr_frag(qt, row0, tro.off[db]);
       }
     };
     if constexpr (SP) {
-      // group g+1's eight transposed reads issued in the stage that computes group g (stages
-      // fenced by sched_barrier, so each MFMA waits only for reads of the stage before)
-      bf16x8 toA[2], tqA[2], toB[2], tqB[2];
-      load(0, toA, tqA);
-      __builtin_amdgcn_sched_barrier(0);
-      load(1, toB, tqB);
-      group(0, toA, tqA);
-      __builtin_amdgcn_sched_barrier(0);
-      load(2, toA, tqA);
-      group(1, toB, tqB);
-      __builtin_amdgcn_sched_barrier(0);
-      load(3, toB, tqB);
-      group(2, toA, tqA);
-      __builtin_amdgcn_sched_barrier(0);
-      group(3, toB, tqB);
+      // SR_TUNE_BWD_SCHED: a hand-ordered tile.  Stage A0 runs q-block 0's S / dP chains; in stage
+      // A1 each of q-block 1's eight chain MFMAs is followed by two elements of q-block 0's
+      // exp / multiply / bf16 pack, and in stage B0 each of q-block 0's eight dV / dK products by
+      // two elements of q-block 1's; B1 runs q-block 1's products.  Every MFMA's operand reads are
+      // issued one MFMA ahead.  sched_barrier fences after each MFMA keep this order (the compiler
+      // otherwise runs all 16 chain MFMAs, then all exps, then all products).
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 pw[4], dw[4];  // packed bf16 P / dS of group g = (q-block, 16-row half)
+      auto soft2 = [&](int g, int j) __attribute__((always_inline)) {  // elements j, j+1 of group g
+        const int qb2 = g >> 1, r = 8 * (g & 1) + j;
+        const f32x2 p = {__builtin_amdgcn_exp2f(-sc[qb2][r]), __builtin_amdgcn_exp2f(-sc[qb2][r + 1])};
+        const f32x2 d = {p[0] * dp[qb2][r], p[1] * dp[qb2][r + 1]};
+        pw[g][j >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2));
+        dw[g][j >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(d, bf16x2));
+      };
+      auto fence = [] __attribute__((always_inline)) { __builtin_amdgcn_sched_barrier(0); };
+      // A0
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc[0] = mfma32(row_frag(qt, l32, s, hi), kf[s], sc[0]);
+        dp[0] = mfma32(row_frag(ot, l32, s, hi), vf[s], dp[0]);
+      }
+      bf16x8 fa = row_frag(qt, 32 + l32, 0, hi);  // A1's first operand
+      fence();
+      mask_rows(0);
+      // A1: MFMA k = 2s + (0: S, 1: dP); soft elements 2k, 2k+1 of q-block 0 (groups 0, 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int s = k >> 1;
+        const bf16x8 cur = fa;
+        if (k < 7) fa = (k & 1) ? row_frag(qt, 32 + l32, s + 1, hi) : row_frag(ot, 32 + l32, s, hi);
+        if (k & 1) dp[1] = mfma32(cur, vf[s], dp[1]);
+        else sc[1] = mfma32(cur, kf[s], sc[1]);
+        soft2(k >> 2, 2 * (k & 3));
+        fence();
+      }
+      // B0: products of groups 0, 1 (MFMA k: group k >> 2, db (k >> 1) & 1, dV if k even else dK);
+      // soft elements of q-block 1 (groups 2, 3)
+      mask_rows(1);
+      auto prod_frag = [&](int k) __attribute__((always_inline)) {
+        const int g = k >> 2, db = (k >> 1) & 1;
+        const int row0 = (g >> 1) * 32 + 16 * (g & 1);
+        return tr_frag((k & 1) ? qt : ot, row0, tro.off[db]);
+      };
+      auto prod = [&](int k, const bf16x8& a) __attribute__((always_inline)) {
+        const int g = k >> 2, db = (k >> 1) & 1;
+        if (k & 1) dk[db] = mfma32(a, __builtin_bit_cast(bf16x8, dw[g]), dk[db]);
+        else dv[db] = mfma32(a, __builtin_bit_cast(bf16x8, pw[g]), dv[db]);
+      };
+      bf16x8 fb = prod_frag(0);
+      fence();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bf16x8 cur = fb;
+        fb = prod_frag(k + 1);  // k = 7 reads B1's first operand
+        prod(k, cur);
+        soft2(2 + (k >> 2), 2 * (k & 3));
+        fence();
+      }
+      // B1: products of groups 2, 3
+#pragma unroll
+      for (int k = 8; k < 16; ++k) {
+        const bf16x8 cur = fb;
+        if (k < 15) fb = prod_frag(k + 1);
+        prod(k, cur);
+      }
     } else {
+      bf16x8 fq[4][2], fo[4][2];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int qb2 = 0; qb2 < 2; ++qb2) {
+          fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
+          fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
+        }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
+#pragma unroll
+        for (int qb2 = 0; qb2 < 2; ++qb2) {
+          sc[qb2] = mfma32(fq[s][qb2], kf[s], sc[qb2]);
+          dp[qb2] = mfma32(fo[s][qb2], vf[s], dp[qb2]);
+        }
+      mask_rows(0);
+      mask_rows(1);
+      // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
 #pragma unroll
       for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
