@@ -17,4 +17,5 @@ run kb_s0 120 env SR_BWD_SCHED=0 python tools/kbench.py attn_bwd
 run kb_s1 120 env SR_BWD_SCHED=1 python tools/kbench.py attn_bwd
 run kb_s0b 120 env SR_BWD_SCHED=0 python tools/kbench.py attn_bwd
 run kb_s1b 120 env SR_BWD_SCHED=1 python tools/kbench.py attn_bwd
-run pmc_s1a 120 env SR_BWD_SCHED=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_s1a -o run --output-format csv -- python3 tools/kbench.py attn_bwd
+export SR_BWD_SCHED=1
+run pmc_s1a 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_s1a -o run --output-format csv -- python3 tools/kbench.py attn_bwd
