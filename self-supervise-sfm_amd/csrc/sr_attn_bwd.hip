@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 // -(c q.k - lse) and P = exp2(-S') (the sign is a source modifier of v_exp); the dP chain is seeded
 // with the stored -delta (attn_bwd_delta_kernel) and returns dO.v - delta, so dS = P dP' with no
 // sign flips (a negated V turned into 24 v_xor per tile before the packed multiplies).
-template <int SEG, bool SP>
+template <int SEG>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
@@ -249,114 +249,43 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
           if (qb2 * 32 + acc_row(r, hi) >= qv) sc[qb2][r] = INFINITY;
       }
     };
-    if constexpr (SP) {
-      // SR_TUNE_BWD_SCHED: a hand-ordered tile.  Stage A0 runs q-block 0's S / dP chains; in stage
-      // A1 each of q-block 1's eight chain MFMAs is followed by two elements of q-block 0's
-      // exp / multiply / bf16 pack, and in stage B0 each of q-block 0's eight dV / dK products by
-      // two elements of q-block 1's; B1 runs q-block 1's products.  Every MFMA's operand reads are
-      // issued one MFMA ahead.  sched_barrier fences after each MFMA keep this order (the compiler
-      // otherwise runs all 16 chain MFMAs, then all exps, then all products).
-      typedef float f32x2 __attribute__((ext_vector_type(2)));
-      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 pw[4], dw[4];  // packed bf16 P / dS of group g = (q-block, 16-row half)
-      auto soft2 = [&](int g, int j) __attribute__((always_inline)) {  // elements j, j+1 of group g
-        const int qb2 = g >> 1, r = 8 * (g & 1) + j;
-        const f32x2 p = {__builtin_amdgcn_exp2f(-sc[qb2][r]), __builtin_amdgcn_exp2f(-sc[qb2][r + 1])};
-        const f32x2 d = {p[0] * dp[qb2][r], p[1] * dp[qb2][r + 1]};
-        pw[g][j >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2));
-        dw[g][j >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(d, bf16x2));
-      };
-      auto fence = [] __attribute__((always_inline)) { __builtin_amdgcn_sched_barrier(0); };
-      // A0
+    bf16x8 fq[4][2], fo[4][2];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sc[0] = mfma32(row_frag(qt, l32, s, hi), kf[s], sc[0]);
-        dp[0] = mfma32(row_frag(ot, l32, s, hi), vf[s], dp[0]);
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int qb2 = 0; qb2 < 2; ++qb2) {
+        fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
+        fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
       }
-      bf16x8 fa = row_frag(qt, 32 + l32, 0, hi);  // A1's first operand
-      fence();
-      mask_rows(0);
-      // A1: MFMA k = 2s + (0: S, 1: dP); soft elements 2k, 2k+1 of q-block 0 (groups 0, 1)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int s = k >> 1;
-        const bf16x8 cur = fa;
-        if (k < 7) fa = (k & 1) ? row_frag(qt, 32 + l32, s + 1, hi) : row_frag(ot, 32 + l32, s, hi);
-        if (k & 1) dp[1] = mfma32(cur, vf[s], dp[1]);
-        else sc[1] = mfma32(cur, kf[s], sc[1]);
-        soft2(k >> 2, 2 * (k & 3));
-        fence();
+    for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
+#pragma unroll
+      for (int qb2 = 0; qb2 < 2; ++qb2) {
+        sc[qb2] = mfma32(fq[s][qb2], kf[s], sc[qb2]);
+        dp[qb2] = mfma32(fo[s][qb2], vf[s], dp[qb2]);
       }
-      // B0: products of groups 0, 1 (MFMA k: group k >> 2, db (k >> 1) & 1, dV if k even else dK);
-      // soft elements of q-block 1 (groups 2, 3)
-      mask_rows(1);
-      auto prod_frag = [&](int k) __attribute__((always_inline)) {
-        const int g = k >> 2, db = (k >> 1) & 1;
-        const int row0 = (g >> 1) * 32 + 16 * (g & 1);
-        return tr_frag((k & 1) ? qt : ot, row0, tro.off[db]);
-      };
-      auto prod = [&](int k, const bf16x8& a) __attribute__((always_inline)) {
-        const int g = k >> 2, db = (k >> 1) & 1;
-        if (k & 1) dk[db] = mfma32(a, __builtin_bit_cast(bf16x8, dw[g]), dk[db]);
-        else dv[db] = mfma32(a, __builtin_bit_cast(bf16x8, pw[g]), dv[db]);
-      };
-      bf16x8 fb = prod_frag(0);
-      fence();
+    mask_rows(0);
+    mask_rows(1);
+    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bf16x8 cur = fb;
-        fb = prod_frag(k + 1);  // k = 7 reads B1's first operand
-        prod(k, cur);
-        soft2(2 + (k >> 2), 2 * (k & 3));
-        fence();
-      }
-      // B1: products of groups 2, 3
+    for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
-      for (int k = 8; k < 16; ++k) {
-        const bf16x8 cur = fb;
-        if (k < 15) fb = prod_frag(k + 1);
-        prod(k, cur);
-      }
-    } else {
-      bf16x8 fq[4][2], fo[4][2];
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f32x8 pv, dv8;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int qb2 = 0; qb2 < 2; ++qb2) {
-          fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
-          fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * s2 + j;
+          pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
+          dv8[j] = pv[j] * dp[qb2][r];
         }
+        const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
+        const int row0 = qb2 * 32 + 16 * s2;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
-#pragma unroll
-        for (int qb2 = 0; qb2 < 2; ++qb2) {
-          sc[qb2] = mfma32(fq[s][qb2], kf[s], sc[qb2]);
-          dp[qb2] = mfma32(fo[s][qb2], vf[s], dp[qb2]);
+        for (int db = 0; db < 2; ++db) {
+          dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
+          dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
         }
-      mask_rows(0);
-      mask_rows(1);
-      // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
-#pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          f32x8 pv, dv8;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int r = 8 * s2 + j;
-            pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
-            dv8[j] = pv[j] * dp[qb2][r];
-          }
-          const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
-          const int row0 = qb2 * 32 + 16 * s2;
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
-            dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
-          }
-        }
-    }
+      }
   };
   // tiles item by item; the last query tile of an item is the only one that can be ragged
   const bool ragged = f.lq % 64 != 0;
@@ -386,7 +315,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
 
 // ---------------------------------------------------------------- dQ
 // grid (query tiles of 128, heads, batch); wave w owns query rows tile*128 + 32 w + l32.
-template <bool SP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b) {
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TB];  // ring of K tile | V tile stages
   const sr_attn_desc& f = b.f;
@@ -481,15 +409,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
         sc[kb] = mfma32(fk[s][kb], qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
         dp[kb] = mfma32(fv[s][kb], of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
       }
-    if constexpr (SP) {  // the dK / dV kernel's pipeline of the S / dP fragment reads
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
     if constexpr (decltype(masked)::value) {  // partial key tile: keys >= valid get S' = -inf, P = 0
       const int seg = t >= nt0;
       const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
@@ -554,18 +473,12 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   const int64_t nrows = (int64_t)f.batch * f.heads * f.lq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
-  const dim3 gq((f.lq + 127) / 128, f.heads, f.batch);
-  if (sr::tune(SR_TUNE_BWD_SCHED)) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, gq, dim3(256), 0, s, b);
-  else hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, gq, dim3(256), 0, s, b);
-  const dim3 g0((f.l0 + 127) / 128, f.heads, f.k0_bstride == 0 ? 1 : f.batch);
-  const dim3 g1((f.l1 + 127) / 128, f.heads, f.k1_bstride == 0 ? 1 : f.batch);
-  if (sr::tune(SR_TUNE_BWD_SCHED)) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, true>), g0, dim3(256), 0, s, b);
-    if (f.l1 > 0) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), g1, dim3(256), 0, s, b);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, false>), g0, dim3(256), 0, s, b);
-    if (f.l1 > 0) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), g1, dim3(256), 0, s, b);
-  }
-  sr::note_kernel("attn_bwd_dkdv_kernel<0, %s>", sr::tune(SR_TUNE_BWD_SCHED) ? "true" : "false");
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<0>, dim3((f.l0 + 127) / 128, f.heads, f.k0_bstride == 0 ? 1 : f.batch),
+                     dim3(256), 0, s, b);
+  if (f.l1 > 0)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, dim3((f.l1 + 127) / 128, f.heads, f.k1_bstride == 0 ? 1 : f.batch),
+                       dim3(256), 0, s, b);
+  sr::note_kernel("attn_bwd_dkdv_kernel<0>");
   return sr::check_launch("sr_attention_bwd");
 }
