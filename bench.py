@@ -296,6 +296,18 @@ def cpu_baseline(sd, img: int, n_views: int, cross_views: int = 4):
                      f"mask, camera head and pose decode once: {est:.1f} s per forward estimated from {wall:.1f} s "
                      f"of CPU work on {threads} threads",
            "seconds_per_part": {k: round(v, 3) for k, v in parts.items()}}
+    # the full N-view oracle forward, timed whole once on a GPU box's host (tools/cpu_full.py; too long
+    # for every bench run): the check of the per-layer estimate at the headline size
+    full = os.path.join(REPO, "profiles", "r04_cpu_full.json")
+    try:
+        with open(full) as f:
+            d = json.load(f)
+        if (d.get("views"), d.get("img")) == (n_views, img):
+            out["full_forward_check"] = {k: d[k] for k in ("full_forward_s", "per_layer_estimate_s", "estimate_over_full",
+                                                           "views_per_s_full_forward", "cpu_model", "threads")}
+            out["full_forward_check"]["source"] = os.path.relpath(full, REPO) + " (tools/cpu_full.py, a separate run)"
+    except (OSError, ValueError, KeyError):
+        pass
     if cross_views:
         dt = cpu_full_forward(sd, img, cross_views)
         est_small, _ = cpu_forward_by_layer(sd, img, cross_views)
