@@ -169,6 +169,23 @@ def build_model(device, seed_rule=True):
     return model.to(device), sd
 
 
+def scale_qk_gain(model, g: float) -> int:
+    """Multiply every q_norm / k_norm weight (attention.py:78, qk_norm=True blocks) by g and drop
+    the blocks' packed-weight caches; returns the number of norms scaled."""
+    n = 0
+    with torch.no_grad():
+        for m in model.modules():
+            for name in ("q_norm", "k_norm"):
+                ln = getattr(m, name, None)
+                if ln is not None and getattr(ln, "weight", None) is not None:
+                    ln.weight.mul_(g)
+                    n += 1
+        for m in model.modules():
+            if hasattr(m, "invalidate_packed"):
+                m.invalidate_packed()
+    return n
+
+
 def _cpu_threads():
     model, phys, logical = host_cpu()
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
@@ -391,6 +408,10 @@ def main():
                          "@518, global attention in fp8; one GPU only); '' or 'none' to skip")
     ap.add_argument("--c5-fp8", choices=["qk", "qkv"], default="qk",
                     help="C5 extra: q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 e4m3")
+    ap.add_argument("--qk-gain", type=float, default=1.0,
+                    help="scale every q_norm / k_norm weight of the aggregator by this factor (trained models carry "
+                         "gains of ~2-3; the synthetic weights ~1): the attention softmax's peakedness, for A/B of "
+                         "the kernels' behaviour under trained-weight statistics; reported in config")
     ap.add_argument("--launch-only", action="store_true",
                     help="launcher / process-group / ranks_seen check without the model (gloo if no GPU)")
     args = ap.parse_args()
@@ -427,6 +448,8 @@ def main():
     from sailrecon_amd import ops
 
     model, sd = build_model(device)
+    if args.qk_gain != 1.0:
+        scale_qk_gain(model, args.qk_gain)
     if world > 1:
         model.aggregator.set_frame_sharding(dist.group.WORLD)
     n = args.views
@@ -550,7 +573,7 @@ def main():
             "data": "synthetic (seeded U[0,1) images, seeded synthetic weights)",
             "config": {"workload": f"N={n} views @{args.img}px duplicated to {2 * n} frames (anchors+queries), "
                                    "fix_rank=300: Aggregator + CameraHead + pose decode",
-                       "views": n, "img": args.img, "frames": 2 * n, "fix_rank": 300,
+                       "views": n, "img": args.img, "frames": 2 * n, "fix_rank": 300, "qk_gain": args.qk_gain,
                        "parallelism": f"frame-sharded x{world} (RCCL K/V all-gather)" if world > 1 else "single GPU",
                        "algorithmic_tflop_per_step": round(tflop, 2),
                        "achieved_tflops_whole_step": round(tflop * args.steps / dt, 1)},
