@@ -519,3 +519,33 @@ def test_gemm_tail_split(ops, epi_name, M, N):
     same = torch.equal(out1, out0)
     print(f"{epi_name} M={M} N={N}: bit-identical={same} rel={rel(out1.float(), out0.float()):.2e}")
     assert rel(out1.float(), out0.float()) < 1e-6
+
+
+def test_merge_with_empty_partial(ops):
+    """a merge partial with LSE = -inf (no key of that part attended) contributes
+    nothing -- in the attention's merge-in epilogue (sr_attn_desc.merge_o) and in sr_attn_merge_n
+    alike (mx == -inf guard): the result is the other part's, finite, not NaN."""
+    H, D, lq, L = 4, 64, 300, 256
+    C = H * D
+    g = torch.Generator(device=DEV).manual_seed(31)
+    q, k, v = (torch.randn(n, C, device=DEV, generator=g).bfloat16() for n in (lq, L, L))
+    o_ref = torch.empty(lq, C, device=DEV, dtype=torch.bfloat16)
+    lse_ref = torch.empty(H, lq, device=DEV)
+    ops.attention(q, k, v, o_ref, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0, lse=lse_ref)
+    junk = torch.randn(lq, C, device=DEV, generator=g).bfloat16()
+    empty = torch.full((H, lq), float("-inf"), device=DEV)
+    # merge-in epilogue: every row's other part is empty
+    o = torch.empty_like(o_ref)
+    ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0,
+                  merge_o=junk, merge_lse=empty)
+    # N-way merge: part 1 empty
+    parts = torch.cat([o_ref, junk])
+    lse_parts = torch.stack([lse_ref, empty]).contiguous()
+    out = torch.empty_like(o_ref)
+    lse_out = torch.empty(H, lq, device=DEV)
+    ops.attn_merge_n(parts, lse_parts, out, parts=2, rows=lq, heads=H, head_dim=D, lse_out=lse_out)
+    torch.cuda.synchronize()
+    for t in (o, out):
+        assert torch.isfinite(t.float()).all()
+        assert rel(t.float(), o_ref.float()) < 1e-2
+    assert torch.equal(out, o_ref) and torch.equal(lse_out, lse_ref)
