@@ -259,10 +259,24 @@ typedef struct sr_attn_desc {
                   sweep, [1] such waves that ran the compiled loop (a row whose fixed softmax offset
                   falls outside the sweep's 2^174 window, or a launch the sweep does not cover).
                   NULL = off (no extra work) */
+  const float* key_box; /* optional (bf16 path, with key_bound or key_norm_max): per key-segment
+                  instance and head the per-dimension max and min of the keys, [inst][heads][2][64]
+                  fp32 (sr_attention_key_box; instances as key_bound's).  Each row's bound then becomes
+                  min(c|q| max|k|, sum_d max(cq_d kmax_d, cq_d kmin_d)) -- far tighter when the keys
+                  share a direction (all scores of a row well below the 2-norm bound, which otherwise
+                  sends the row outside the fixed-offset window).  NULL = the 2-norm bound alone */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */
 int sr_attention_bound_floats(const sr_attn_desc* d);
+
+/* out[inst][h][0][d] / out[inst][h][1][d] = max / min over rows r < rows of k[inst*inst_stride + r]
+ * [h*64 + d] (bf16 keys, head_dim 64; out fp32, n_inst*heads*128 floats): the key box of
+ * sr_attn_desc.key_box for one key segment (inst_stride 0 with n_inst 1: keys shared by every item).
+ * Replaces nothing in the reference: a bound the fixed-offset softmax of attention.py:103-109's
+ * replacement uses. */
+int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride, int n_inst,
+                         int heads, float* out);
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 

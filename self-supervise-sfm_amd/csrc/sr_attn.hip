@@ -189,7 +189,9 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // per-tile row max, its lane exchange and the rescale test are skipped.  P keeps bf16's
   // relative precision at any magnitude, O and l are fp32: the result equals the per-tile-max
   // sweep's up to rounding.
-  float qb[QB];
+  // qs: the 2-norm bound |S| <= qs (both sides); qb: the upper bound S <= qb, the box bound
+  // sum_d max(cq_d kmax_d, cq_d kmin_d) where d.key_box is set (min of the two)
+  float qb[QB], qs[QB];
   const bool use_bound = d.key_bound != nullptr || d.key_norm_max > 0.f;
   if (use_bound) {
     float kn = d.key_norm_max;
@@ -206,16 +208,47 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss = fmaf((float)qf[b][s][j], (float)qf[b][s][j], ss);
-      qb[b] = sqrtf(sum_x32(ss)) * kn * 1.0001f;  // margin for the fp32 sums
+      qs[b] = qb[b] = sqrtf(sum_x32(ss)) * kn * 1.0001f;  // margin for the fp32 sums
+    }
+    if (d.key_box) {
+      // this lane's 32 dims (16 s + 8 hi .. + 8) of the box, segment 1's merged in
+      const float* bx0 = d.key_box + ((int64_t)(d.k0_bstride == 0 ? 0 : item) * d.heads + head) * 128;
+      const float* bx1 = args.ntile1 > 0
+          ? d.key_box + ((int64_t)(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head) * 128 : bx0;
+      float ub[QB], ab[QB];
+#pragma unroll
+      for (int b = 0; b < QB; ++b) ub[b] = ab[b] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int h4 = 0; h4 < 2; ++h4) {
+          const int dd = 16 * s + 8 * hi + 4 * h4;
+          const f32x4 hi0 = *(const f32x4*)(bx0 + dd), lo0 = *(const f32x4*)(bx0 + 64 + dd);
+          const f32x4 hi1 = *(const f32x4*)(bx1 + dd), lo1 = *(const f32x4*)(bx1 + 64 + dd);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float kmax = fmaxf(hi0[e], hi1[e]), kmin = fminf(lo0[e], lo1[e]);
+#pragma unroll
+            for (int b = 0; b < QB; ++b) {
+              const float q = (float)qf[b][s][4 * h4 + e];
+              ub[b] += fmaxf(q * kmax, q * kmin);
+              ab[b] += fabsf(q) * fmaxf(fabsf(kmax), fabsf(kmin));
+            }
+          }
+        }
+#pragma unroll
+      for (int b = 0; b < QB; ++b)  // + a margin for the fp32 sums of the score and of the bound
+        qb[b] = fminf(qb[b], sum_x32(ub[b]) + 2e-4f * sum_x32(ab[b]));
     }
   }
   bool fixed_m = false, m_zero = false;
   if (use_bound && args.allow_mzero) {
-    // every row's bound qb <= 50: the fixed offset m = 0 holds from tile 0 (what the tile-0 max
-    // pass would settle on), so the sweep skips that pass and the -m fold MFMAs from the start
+    // every row's upper bound qb <= FIX_HI and 2-norm bound qs <= FIX_LO: the fixed offset m = 0
+    // holds from tile 0 (every P <= 2^FIX_HI, the row's max P >= 2^-qs), so the sweep skips the
+    // tile-0 max pass and the -m fold MFMAs from the start
     bool z = true;
 #pragma unroll
-    for (int b = 0; b < QB; ++b) z &= qb[b] <= FIX_HI;
+    for (int b = 0; b < QB; ++b) z &= qb[b] <= FIX_HI && qs[b] <= FIX_LO;
     fixed_m = m_zero = __all(z);
   }
 
@@ -341,7 +374,9 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
           // new max (rows that did not grow keep theirs), split into bf16 hi + lo
           // fixed offset: m = 0 when the row's bound allows it (every score <= qb <= FIX_HI and the
           // true max >= -qb), else max(tile-0 max, qb - FIX_HI)
-          const float target = t == 0 ? (fixed_m ? (qb[b] <= FIX_HI ? 0.f : fmaxf(mx[b], qb[b] - FIX_HI)) : mx[b])
+          const float target = t == 0 ? (fixed_m ? ((qb[b] <= FIX_HI && qs[b] <= FIX_LO) ? 0.f
+                                                                           : fmaxf(mx[b], qb[b] - FIX_HI))
+                                                 : mx[b])
                                       : m_run[b] + fmaxf(mx[b], 0.f);
           const bf16 nhi = (bf16)target;
           const bf16 nlo = (bf16)(target - (float)nhi);
@@ -463,7 +498,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       m_fix[b] = fmaxf(qb[b] - PIPE_HI, 0.f);
-      need_mx |= m_fix[b] > 0.f;
+      need_mx |= m_fix[b] + qs[b] > PIPE_LO;  // the true max >= -qs: no pre-pass needed when m + qs <= LO
     }
     if (use_bound && args.allow_mzero && ntiles >= 4) {  // workgroup-uniform: every wave takes the barrier
       // the prologue's stages (tiles 0-2) landed and visible to every wave
@@ -1146,6 +1181,66 @@ void launch_key_norm(hipStream_t s, const void* k, int64_t ldk, int rows, int64_
                      inst_stride, heads, (unsigned*)out);
 }
 
+// key box of sr_attention_key_box: per (instance, head, dim) max and min of the keys.  fp32 values
+// are reduced as order-preserving int32 keys (o(f) = bits ^ ((bits >> 31) & 0x7fffffff), its own
+// inverse) with the integer atomicMax / atomicMin: init, scan, decode.
+__device__ __forceinline__ int ord_key(float f) {
+  const int b = __float_as_int(f);
+  return b ^ ((b >> 31) & 0x7fffffff);
+}
+
+__global__ __launch_bounds__(256) void key_box_init_kernel(int* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = (i & 64) ? 0x7fffffff : (int)0x80000000;  // [.][.][0] max slots, [.][.][1] min slots
+}
+
+__global__ __launch_bounds__(256) void key_box_kernel(const bf16* __restrict__ k, int64_t ldk, int rows,
+                                                      int64_t inst_stride, int heads, int* __restrict__ out) {
+  __shared__ int red[32 * 128];
+  const int cpr = heads * 8;  // 8-dim column groups per row
+  const int rpi = blockDim.x / cpr;
+  const int t = threadIdx.x;
+  const int row_in = t / cpr, c = t - row_in * cpr, head = c >> 3, d0 = (c & 7) * 8;
+  const int64_t inst = blockIdx.y;
+  for (int i = t; i < heads * 128; i += blockDim.x) red[i] = (i & 64) ? 0x7fffffff : (int)0x80000000;
+  __syncthreads();
+  float mx[8], mn[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mx[j] = -INFINITY;
+    mn[j] = INFINITY;
+  }
+  if (row_in < rpi) {
+    for (int r = blockIdx.x * rpi + row_in; r < rows; r += gridDim.x * rpi) {
+      const bf16x8 v = *(const bf16x8*)(k + (inst * inst_stride + r) * ldk + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mx[j] = fmaxf(mx[j], (float)v[j]);
+        mn[j] = fminf(mn[j], (float)v[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicMax(&red[head * 128 + d0 + j], ord_key(mx[j]));
+      atomicMin(&red[head * 128 + 64 + d0 + j], ord_key(mn[j]));
+    }
+  }
+  __syncthreads();
+  int* o = out + inst * heads * 128;
+  for (int i = t; i < heads * 128; i += blockDim.x) {
+    if (i & 64) atomicMin(&o[i], red[i]);
+    else atomicMax(&o[i], red[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void key_box_decode_kernel(int* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const int b = out[i];
+    out[i] = b ^ ((b >> 31) & 0x7fffffff);  // back to the fp32 bits
+  }
+}
+
 // ------------------------------------------------------------------ f32 / VALU
 constexpr int F32_KT = 32;       // keys per LDS tile
 constexpr int F32_THREADS = 128;  // query rows per workgroup
@@ -1456,6 +1551,29 @@ __global__ __launch_bounds__(256) void attn_merge_n_bf16_kernel(const bf16* __re
 }
 
 }  // namespace
+
+extern "C" int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride,
+                                    int n_inst, int heads, float* out) {
+  SR_CHECK(k && out, SR_EINVAL, "sr_attention_key_box: null k / out");
+  SR_CHECK(rows > 0 && n_inst > 0 && heads > 0 && heads <= 32, SR_EINVAL,
+           "sr_attention_key_box: rows, instances > 0 and 1..32 heads (rows=%d n_inst=%d heads=%d)", rows, n_inst, heads);
+  SR_CHECK(ldk % 8 == 0 && ldk >= 64 * heads && ((uintptr_t)k & 15) == 0 && ((uintptr_t)out & 3) == 0 &&
+               (n_inst == 1 || inst_stride >= rows),
+           SR_EINVAL, "sr_attention_key_box: ldk a multiple of 8 covering the heads, 16-B aligned k, inst_stride >= rows");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = n_inst * heads * 128;
+  hipLaunchKernelGGL(key_box_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n);
+  const int cpr = heads * 8;
+  const int threads = std::max(64, (256 / cpr) * cpr);
+  const int rpi = std::max(1, threads / cpr);
+  const int want = std::max(1, 2048 / n_inst);
+  const int gx = std::max(1, std::min((rows + rpi - 1) / rpi, want));
+  hipLaunchKernelGGL(key_box_kernel, dim3(gx, n_inst), dim3(threads), 0, s, (const bf16*)k, ldk, rows, inst_stride, heads,
+                     (int*)out);
+  hipLaunchKernelGGL(key_box_decode_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n);
+  sr::note_kernel("key_box_kernel");
+  return sr::check_launch("sr_attention_key_box");
+}
 
 extern "C" int sr_attention_bound_floats(const sr_attn_desc* desc) {
   if (!desc || desc->head_dim != 64 || desc->mask_mode != SR_MASK_NONE || desc->heads > 32) return 0;

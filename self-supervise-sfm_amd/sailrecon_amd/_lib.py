@@ -69,6 +69,7 @@ class AttnDesc(ctypes.Structure):
         ("tail_rows_readable", _i32),
         ("merge_o", _vp), ("ld_merge_o", _i64), ("merge_lse", _vp), ("merge_rows", _i64),
         ("sweep_stats", _vp),
+        ("key_box", _vp),
     ]
 
 
@@ -147,6 +148,7 @@ _PROTOS = {
     "sr_layernorm_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _f32, _vp, _i64, _vp, _i64, _vp, _vp,
                                 _i32, _i32, _vp]),
     "sr_qk_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
+    "sr_attention_key_box": (_i32, [_vp, _vp, _i64, _i32, _i64, _i32, _i32, _vp]),
     "sr_qk_bwd_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
     "sr_cast_bf16": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _f32]),
     "sr_nonfinite_check": (_i32, [_vp, _vp, _i64, _vp, _vp]),

@@ -465,7 +465,8 @@ class Aggregator(nn.Module):
                 ops.attention(qkv[:, 0:C], kv[:, 0:C], kv[:, C:2 * C], o, heads=pr.heads, head_dim=pr.head_dim,
                               batch=F_, lq=P, q_bstride=P, l0=n_sub, k0_bstride=0, k1=qkv[:, C:2 * C],
                               v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                              key_norm_max=runtime.key_norm_bound(pr))
+                              key_norm_max=runtime.key_norm_bound(pr),
+                              query_norm_max=runtime.query_norm_bound(pr))
             runtime.run_block(pr, x, 0, R, sc, attend_cached, runtime.qkv_params(pr, rope, pos_row_base=0, **posctx))
             if l in out_maps:
                 ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, C:], x, R)
@@ -563,9 +564,10 @@ class Aggregator(nn.Module):
             lse_a = lse_a[0]
             ops.attention_pair(
                 dict(q=qkv_g[:, 0:C], k0=qkv_g[:, C:2 * C], v0=qkv_g[:, 2 * C:3 * C], o=sc.o[a0:q0], lq=La, l0=La,
-                     key_norm_max=runtime.key_norm_bound(pg)),
+                     key_norm_max=runtime.key_norm_bound(pg), query_norm_max=runtime.query_norm_bound(pg)),
                 dict(q=qkv_r[:, 0:C], k0=kv_sub_all[:n_full, 0:C], v0=kv_sub_all[:n_full, C:2 * C], o=o_a, lq=rows,
-                     l0=n_full, key_norm_max=runtime.key_norm_bound(pr), lse=lse_a.view(-1)),
+                     l0=n_full, key_norm_max=runtime.key_norm_bound(pr), query_norm_max=runtime.query_norm_bound(pr),
+                     lse=lse_a.view(-1)),
                 heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
             self._reloc_own_pass(pr, qkv_r, kv_sub_all, sc.o[q0:q1], o_a, lse_a, Nq_l, P, n_sub_all, n_full)
             keep(runtime.run_block_tail(pr, x, q0, q1, sc, defer=defer))
@@ -584,7 +586,7 @@ class Aggregator(nn.Module):
             def attend_reloc(qkv, o):
                 _wait(work_sub)
                 rows = Nq_l * P
-                kb = runtime.key_norm_bound(pr)
+                kb, qb = runtime.key_norm_bound(pr), runtime.query_norm_bound(pr)
                 if self._split_reloc(dtype, rows, n_sub_all):
                     # two passes merged by their LSEs (the union of the two key sets, exactly): every
                     # query row against the shared anchor subsample's whole 64-key tiles as ONE long
@@ -597,13 +599,14 @@ class Aggregator(nn.Module):
                     ops.attention(qkv[:, 0:C], kv_sub_all[:n_full, 0:C], kv_sub_all[:n_full, C:2 * C],
                                   o_a, heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows,
                                   q_bstride=0, l0=n_full, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
+                                  query_norm_max=qb,
                                   lse=lse_a.view(-1), tail_readable=True)
                     self._reloc_own_pass(pr, qkv, kv_sub_all, o, o_a, lse_a, Nq_l, P, n_sub_all, n_full)
                     return
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
                               k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                              key_norm_max=kb, tail_readable=True)
+                              key_norm_max=kb, query_norm_max=qb, tail_readable=True)
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
                 with torch.cuda.stream(side):
@@ -643,7 +646,7 @@ class Aggregator(nn.Module):
         while the gather of the others is in flight, then the remote anchors (kv_all rows outside
         [off, off + lq): up to two key segments), merged exactly by the passes' LSEs."""
         C, H, D = pg.dim, pg.heads, pg.head_dim
-        kb = runtime.key_norm_bound(pg)
+        kb, qb = runtime.key_norm_bound(pg), runtime.query_norm_bound(pg)
         segs = [(a, n) for a, n in ((0, off), (off + lq, lk - off - lq)) if n > 0]
         if q.dtype == torch.bfloat16:
             # every pass key-split as one slice of a stacked partials buffer (the per-rank query
@@ -659,7 +662,8 @@ class Aggregator(nn.Module):
                     _wait(work_kv)  # the remote anchors' K/V
                 ops.attention_partials(q, kv[:, 0:C], kv[:, C:2 * C], o_parts[p0 * lq:(p0 + p) * lq],
                                        lse_parts[p0:p0 + p], heads=H, head_dim=D, lq=lq, l0=kv.shape[0], parts=p,
-                                       tag="attn_global", key_norm_max=kb, tail_readable=_SHARD_TAIL)
+                                       tag="attn_global", key_norm_max=kb, query_norm_max=qb,
+                                       tail_readable=_SHARD_TAIL)
                 p0 += p
             ops.attn_merge_n(o_parts, lse_parts, o, parts=total, rows=lq, heads=H, head_dim=D)
             return
@@ -668,13 +672,13 @@ class Aggregator(nn.Module):
         lse_rem = ws.get("lse_rem", H, lq, torch.float32, q.device)
         o_rem = ws.get("o_rem", lq, C, o.dtype, q.device)
         ops.attention(q, kv_loc[:, 0:C], kv_loc[:, C:2 * C], o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0,
-                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc, key_norm_max=kb)
+                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc, key_norm_max=kb, query_norm_max=qb)
         _wait(work_kv)
         (s0, n0), (s1, n1) = segs[0], (segs[1] if len(segs) > 1 else (0, 0))
         ops.attention(q, kv_all[s0:s0 + n0, 0:C], kv_all[s0:s0 + n0, C:2 * C], o_rem, heads=H, head_dim=D, batch=1,
                       lq=lq, q_bstride=0, l0=n0, k0_bstride=0, k1=kv_all[s1:s1 + n1, 0:C] if n1 else None,
                       v1=kv_all[s1:s1 + n1, C:2 * C] if n1 else None, l1=n1, k1_bstride=0, tag="attn_global",
-                      lse=lse_rem, key_norm_max=kb)
+                      lse=lse_rem, key_norm_max=kb, query_norm_max=qb)
         ops.attn_merge(o, lse_loc, o_rem, lse_rem, o, heads=H, head_dim=D, tag="attn_merge")
 
     def _global_attention(self, q, k, v, o, pg, lq, lk):
@@ -686,22 +690,24 @@ class Aggregator(nn.Module):
                               key_norm_max=runtime.key_norm_bound(pg))
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
-                          k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg))
+                          k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg),
+                          query_norm_max=runtime.query_norm_bound(pg))
 
     @staticmethod
     def _reloc_own_pass(pr, qkv, kv_sub_all, o, o_a, lse_a, nq: int, P: int, n_sub_all: int, n_full: int) -> None:
         """Second pass of the split reloc attention: each query frame against the subsample's last
         partial tile (shared segment 0) and itself (segment 1), folding the subsample pass's
         (o_a, lse_a) in at its epilogue (sr_attn_desc.merge_o) -> o."""
-        C, kb = pr.dim, runtime.key_norm_bound(pr)
+        C, kb, qb = pr.dim, runtime.key_norm_bound(pr), runtime.query_norm_bound(pr)
         if n_full < n_sub_all:
             ops.attention(qkv[:, 0:C], kv_sub_all[n_full:, 0:C], kv_sub_all[n_full:, C:2 * C], o, heads=pr.heads,
                           head_dim=pr.head_dim, batch=nq, lq=P, q_bstride=P, l0=n_sub_all - n_full, k0_bstride=0,
                           k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                          key_norm_max=kb, tail_readable=True, merge_o=o_a, merge_lse=lse_a)
+                          key_norm_max=kb, query_norm_max=qb, tail_readable=True, merge_o=o_a, merge_lse=lse_a)
         else:
             ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pr.heads, head_dim=pr.head_dim,
                           batch=nq, lq=P, q_bstride=P, l0=P, k0_bstride=P, tag="attn_reloc", key_norm_max=kb,
+                          query_norm_max=qb,
                           tail_readable=True, merge_o=o_a, merge_lse=lse_a)
 
     def _paired_attention(self, pr, pg, dtype, rows: int, La: int, n_sub: int) -> bool:

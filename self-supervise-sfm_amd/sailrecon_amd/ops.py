@@ -348,14 +348,17 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
               scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
               key_norm_max: float = 0.0, mask: Optional[Tensor] = None, tail_readable: bool = False,
               merge_o: Optional[Tensor] = None, merge_lse: Optional[Tensor] = None,
-              sweep_stats: Optional[Tensor] = None) -> None:
+              sweep_stats: Optional[Tensor] = None, query_norm_max: float = 0.0) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``mask``
     (mask_mode SR_MASK_DENSE: bool / uint8, nonzero = attend; SR_MASK_ADD: fp32 added to the
     scores) is a [batch, heads, lq, l0 + l1] view (broadcast dims may have stride 0, the last dim
     stride 1), fp32 q / k / v only.  ``lse``
     (fp32 [batch, heads, lq]) receives the rows' log2-domain LSE for attention_bwd.
     ``key_norm_max`` > 0: a static bound of every key's per-head 2-norm (runtime.key_norm_bound),
-    which replaces the key scan of the fixed-offset sweep.  A bf16 single query set too short to
+    which replaces the key scan of the fixed-offset sweep.  ``query_norm_max`` > 0: the same bound
+    for the queries (runtime.query_norm_bound); where scale*log2(e)*|q|*|k| leaves the sweep's
+    window the launch first computes the per-dimension key box (sr_attention_key_box,
+    sr_attn_desc.key_box; SR_ATTN_KEY_BOX=1 always, =0 never).  A bf16 single query set too short to
     fill the chip runs key-split (key_split_parts, attention_partials + attn_merge_n).
     ``tail_readable``: at least 64 rows of finite values follow every key segment in memory
     (runtime.Workspace buffers: zero-initialised, 64 rows of padding), which lets the
@@ -381,7 +384,8 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
             raise ValueError("attention: lse must be contiguous fp32 [batch, heads, lq]")
         o_parts, lse_parts = key_split_workspace(q.device, parts, lq, heads * head_dim, heads)
         attention_partials(q, k0, v0, o_parts, lse_parts, heads=heads, head_dim=head_dim, lq=lq, l0=l0, parts=parts,
-                           scale=scale, tag=tag, key_norm_max=key_norm_max, tail_readable=tail_readable)
+                           scale=scale, tag=tag, key_norm_max=key_norm_max, tail_readable=tail_readable,
+                           query_norm_max=query_norm_max)
         attn_merge_n(o_parts, lse_parts, o, parts=parts, rows=lq, heads=heads, head_dim=head_dim, lse_out=lse)
         return
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
@@ -407,7 +411,8 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
         d.mask_bstride, d.mask_hstride, d.mask_ld = mask.stride(0), mask.stride(1), mask.stride(2)
     _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * (l0 + l1) * head_dim,
                       q.element_size() * heads * head_dim *
-                      (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)))
+                      (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)),
+                      query_norm_max=query_norm_max, k0=k0, k1=k1)
 
 
 def _set_sweep_stats(d: AttnDesc, stats: Optional[Tensor]) -> None:
@@ -431,8 +436,8 @@ _ATTN_PAIR = os.environ.get("SR_ATTN_PAIR", "1") != "0"
 
 def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional[str] = None) -> None:
     """Two single-query-set bf16 attentions in ONE launch (sr_attention_pair): ``a`` / ``b`` are
-    dicts with q, k0, v0, o, lq, l0, key_norm_max and optionally lse (keys as attention()'s, batch
-    1, one segment).
+    dicts with q, k0, v0, o, lq, l0, key_norm_max and optionally lse, query_norm_max (keys as
+    attention()'s, batch 1, one segment).
     a's workgroups run first and b's fill the CUs a's last round leaves idle.  Both must pass
     pair_eligible (checked)."""
     descs = []
@@ -444,6 +449,7 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
                        q_bstride=0, l0=p["l0"], k0_bstride=0, lse=p.get("lse"))
         d.key_norm_max = float(p["key_norm_max"])
         _set_sweep_stats(d, p.get("sweep_stats"))
+        _attach_key_box(d, p["k0"], None, p.get("query_norm_max", 0.0), "attn_key_box" + str(len(descs)))
         descs.append(d)
         flops += 4.0 * heads * p["lq"] * p["l0"] * head_dim
         nbytes += p["q"].element_size() * heads * head_dim * (2 * p["lq"] + 2 * p["l0"])
@@ -456,10 +462,40 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
         TIMER.stop(tag, ev0, flops, nbytes, kernel=last_kernel())
 
 
+_KEY_BOX = os.environ.get("SR_ATTN_KEY_BOX", "auto")  # auto | 1 (always) | 0 (never)
+_FIX_HI = 64.0  # sr_attn.hip FIX_HI: the fixed offset's headroom (log2 units)
+
+
+def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_max: float, name: str) -> None:
+    """Set d.key_box (bf16, static key bound set) when the 2-norm score bound scale*log2(e)*|q|*|k|
+    exceeds the sweep's headroom FIX_HI: one sr_attention_key_box pass per key segment into a
+    per-stream workspace, instances as sr_attention_bound_floats' (k0's, then k1's)."""
+    if _KEY_BOX == "0" or not (d.key_norm_max > 0.0) or d.head_dim != 64 or d.heads > 32:
+        return
+    if _KEY_BOX != "1" and not (query_norm_max > 0.0 and
+                                d.scale * 1.4426950408889634 * query_norm_max * d.key_norm_max > _FIX_HI):
+        return
+    n0 = 1 if d.k0_bstride == 0 else d.batch
+    n1 = (1 if d.k1_bstride == 0 else d.batch) if d.l1 > 0 else 0
+    per = d.heads * 128
+    ws = _train_ws(k0.device, name, (n0 + n1) * per)
+    lib = _lib.load()
+    stream = _stream(k0)
+    check(lib.sr_attention_key_box(stream, d.k0, d.ldk0, d.l0, d.k0_bstride, n0, d.heads, _p(ws)),
+          "sr_attention_key_box")
+    if n1:
+        check(lib.sr_attention_key_box(stream, d.k1, d.ldk1, d.l1, d.k1_bstride, n1, d.heads, _p(ws[n0 * per:])),
+              "sr_attention_key_box")
+    d.key_box = _p(ws)
+
+
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,
-                      nbytes: float) -> None:
+                      nbytes: float, query_norm_max: float = 0.0, k0: Optional[Tensor] = None,
+                      k1: Optional[Tensor] = None) -> None:
     if q.dtype == torch.bfloat16 and _ATTN_BOUND and key_norm_max > 0.0:
         d.key_norm_max = float(key_norm_max)
+        if k0 is not None:
+            _attach_key_box(d, k0, k1, query_norm_max, "attn_key_box")
     elif q.dtype == torch.bfloat16 and _ATTN_BOUND:
         nb = _lib.load().sr_attention_bound_floats(ctypes.byref(d))
         if nb > 0:
@@ -483,7 +519,8 @@ def key_split_workspace(device, parts: int, rows: int, cols: int, heads: int, na
 
 def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_parts: Tensor, *, heads: int,
                        head_dim: int, lq: int, l0: int, parts: int, scale: Optional[float] = None,
-                       tag: Optional[str] = None, key_norm_max: float = 0.0, tail_readable: bool = False) -> None:
+                       tag: Optional[str] = None, key_norm_max: float = 0.0, tail_readable: bool = False,
+                       query_norm_max: float = 0.0) -> None:
     """One bf16 launch of ``parts`` items over equal key chunks of k0/v0 (item s: keys
     [s*l0/parts, (s+1)*l0/parts)) against the same lq queries: item s writes its normalised
     partial output at rows s*lq of o_parts and its LSE to lse_parts[s] ([heads, lq]).  The parts
@@ -500,7 +537,8 @@ def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_p
     if tail_readable:  # rows past k0/v0's end readable: each chunk's ragged tile may go to the asm sweep
         d.tail_rows_readable = 64
     _launch_attention(d, q, tag, key_norm_max, 4.0 * heads * lq * l0 * head_dim,
-                      q.element_size() * heads * head_dim * (lq + 2 * parts * lq + 2 * l0))
+                      q.element_size() * heads * head_dim * (lq + 2 * parts * lq + 2 * l0),
+                      query_norm_max=query_norm_max, k0=k0)
 
 
 def attn_merge(o_a: Tensor, lse_a: Tensor, o_b: Tensor, lse_b: Tensor, out: Tensor, *, heads: int, head_dim: int,

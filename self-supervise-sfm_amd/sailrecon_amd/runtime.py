@@ -75,6 +75,7 @@ class PackedBlock:
     b_fc2: Optional[Tensor]
     g2: Tensor
     k_bound: float = -1.0  # key_norm_bound cache (-1: not computed yet)
+    q_bound: float = -1.0  # query_norm_bound cache
 
 
 def key_norm_bound(pb: PackedBlock) -> float:
@@ -90,6 +91,20 @@ def key_norm_bound(pb: PackedBlock) -> float:
             b = float(pb.kn_b.norm()) if pb.kn_b is not None else 0.0
             pb.k_bound = (pb.head_dim ** 0.5 * w + b) * (1.0 + 2.0 ** -6)
     return pb.k_bound
+
+
+def query_norm_bound(pb: PackedBlock) -> float:
+    """key_norm_bound's bound for the queries (q_norm, attention.py:49-50,77): with it the
+    attention sees the static score bound scale * |q| * |k| and computes the per-dimension key box
+    (ops.attention's query_norm_max) only when that bound leaves the fixed-offset window."""
+    if pb.q_bound < 0.0:
+        if not pb.qk_norm or pb.qn_w is None:
+            pb.q_bound = 0.0
+        else:
+            w = float(pb.qn_w.abs().max())
+            b = float(pb.qn_b.norm()) if pb.qn_b is not None else 0.0
+            pb.q_bound = (pb.head_dim ** 0.5 * w + b) * (1.0 + 2.0 ** -6)
+    return pb.q_bound
 
 
 def _f32(t: Optional[Tensor]) -> Optional[Tensor]:
@@ -307,10 +322,10 @@ def frame_attend(pb: PackedBlock, frames: int, tokens: int, tail_readable: bool 
     """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C]).
     ``tail_readable``: the qkv buffers come from a Workspace (rows past the last frame readable)."""
     C, D = pb.dim, pb.head_dim
-    kb = key_norm_bound(pb)
+    kb, qb = key_norm_bound(pb), query_norm_bound(pb)
 
     def attend(qkv: Tensor, o: Tensor) -> None:
         ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads, head_dim=D,
                       batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_frame",
-                      key_norm_max=kb, tail_readable=tail_readable)
+                      key_norm_max=kb, query_norm_max=qb, tail_readable=tail_readable)
     return attend

@@ -81,7 +81,8 @@ def _positions(qkv, M):
 
 def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None, lse=None,
-              key_norm_max=0.0, mask=None, tail_readable=False, merge_o=None, merge_lse=None, sweep_stats=None):
+              key_norm_max=0.0, mask=None, tail_readable=False, merge_o=None, merge_lse=None, sweep_stats=None,
+              query_norm_max=0.0):
     """sr_attention's semantics (include/sfm_amd.h sr_attn_desc): the camera mask, SR_MASK_DENSE
     (nonzero = attend) / SR_MASK_ADD masks with zeros for a row without attended keys, and the
     merge-in of a disjoint key set's (merge_o, merge_lse).  sweep_stats (device diagnostics) is
@@ -141,7 +142,7 @@ def attn_merge(o_a, lse_a, o_b, lse_b, out, *, heads, head_dim, lse_out=None, ta
 
 
 def attention_partials(q, k0, v0, o_parts, lse_parts, *, heads, head_dim, lq, l0, parts, scale=None, tag=None,
-                       key_norm_max=0.0, tail_readable=False):
+                       key_norm_max=0.0, tail_readable=False, query_norm_max=0.0):
     del tail_readable  # a memory-layout promise for the HIP sweep; no effect on the result
     assert l0 % parts == 0
     ch = l0 // parts

@@ -47,6 +47,11 @@ def test_abi_validation_errors_without_gpu():
     assert rc == -3 and b"multiple of 4" in lib.sr_last_error()
     d = _lib.AttnDesc()
     assert lib.sr_attention(None, _lib.SR_BF16, ctypes.byref(d)) == -1
+    # key box: 33 heads, an unaligned k, and an instance stride below the rows are rejected
+    for args in ((64, 10, 0, 1, 33), (64, 10, 0, 1, 1), (1024, 10, 5, 2, 16)):
+        k = ctypes.c_void_p(18 if args == (64, 10, 0, 1, 1) else 16)
+        assert lib.sr_attention_key_box(None, k, *args[:4], args[4], ctypes.c_void_p(16)) == -1, args
+        assert b"sr_attention_key_box" in lib.sr_last_error()
 
 
 def test_tuning_switches_without_gpu():

@@ -625,3 +625,68 @@ def test_attention_dma_base_bit31(ops):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     del big
+
+
+def _qk_gain_shared(rows, g, gen, u, spread):
+    """_qk_gain's rule on inputs u + spread * n (a direction u shared by every row): the keys of a
+    real forward cluster like this, so the rows' scores sit far below the 2-norm bound c|q||k|."""
+    x = u + spread * torch.randn(rows, H, D, device=DEV, generator=gen)
+    x = (x - x.mean(-1, keepdim=True)) / x.std(-1, keepdim=True, unbiased=False)
+    w = g * (1.0 + 0.02 * torch.randn(D, device=DEV, generator=gen))
+    b = 0.02 * torch.randn(D, device=DEV, generator=gen)
+    kb = (D ** 0.5 * float(w.abs().max()) + float(b.norm())) * (1.0 + 2.0 ** -6)
+    return (x * w + b).reshape(rows, C).bfloat16(), kb
+
+
+@pytest.mark.parametrize("g", [2.0, 4.0])
+def test_global_attention_key_box(ops, g):
+    """The per-dimension key box (sr_attention_key_box, sr_attn_desc.key_box): keys clustered
+    around one direction, queries spread, qk-gain g.  With the 2-norm bound alone (query_norm_max
+    0) the rows whose queries point away from the keys' direction lie > 174 below it and their waves
+    fall to the compiled loop (at g = 4); with query_norm_max the launch computes the box, whose
+    bound sits within the window, and every wave stays on the hand-scheduled sweep, alone and paired.
+    Both against fp64 on sampled rows; the box itself bit-exact against torch's amax / amin."""
+    L, nf = 32 * P, 32 * PP // 64 * 64
+    gen = torch.Generator(device=DEV).manual_seed(int(g * 100))
+    u = torch.randn(1, H, D, device=DEV, generator=gen)
+    q, qn = _qk_gain(L, g, gen)
+    k, kb = _qk_gain_shared(L, g, gen, u, 0.05)
+    v = torch.randn(L, C, device=DEV, generator=gen).bfloat16()
+    ks, kbs = _qk_gain_shared(nf, g, gen, u, 0.05)
+    vs = torch.randn(nf, C, device=DEV, generator=gen).bfloat16()
+    box = torch.empty(H, 2, D, device=DEV)
+    assert ops._lib.load().sr_attention_key_box(ops._stream(k), k.data_ptr(), C, L, 0, 1, H, box.data_ptr()) == 0
+    kh = k.float().view(L, H, D)
+    assert torch.equal(box[:, 0], kh.amax(0)) and torch.equal(box[:, 1], kh.amin(0))
+    outs = {}
+    for qnm in (0.0, qn):
+        st = torch.zeros(2, dtype=torch.int32, device=DEV)
+        o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                      key_norm_max=kb, query_norm_max=qnm, sweep_stats=st)
+        sp = torch.zeros(2, dtype=torch.int32, device=DEV)
+        og, orr = torch.empty_like(o), torch.empty_like(o)
+        ops.attention_pair(dict(q=q, k0=k, v0=v, o=og, lq=L, l0=L, key_norm_max=kb, query_norm_max=qnm,
+                                sweep_stats=sp),
+                           dict(q=q, k0=ks, v0=vs, o=orr, lq=L, l0=nf, key_norm_max=kbs, query_norm_max=qnm,
+                                sweep_stats=sp), heads=H, head_dim=D)
+        torch.cuda.synchronize()
+        print(f"qk-gain {g}, query_norm_max {qnm:.1f}: asm / compiled waves: global {st.tolist()}, "
+              f"pair {sp.tolist()}")
+        outs[qnm] = (st.tolist(), sp.tolist(), o, og, orr)
+    waves = (L + 63) // 64 * H
+    s_cs, p_cs = outs[0.0][:2]
+    s_bx, p_bx = outs[qn][:2]
+    assert sum(s_bx) == waves and sum(p_bx) == 2 * waves
+    assert s_bx[1] == 0 and p_bx[1] == 0
+    if g >= 4.0:
+        assert s_cs[1] > 0  # the 2-norm bound alone leaves the window
+    scale = D ** -0.5
+    rows = _sample_rows(L, 128, int(g)).to(DEV)
+    ref = _ref_rows(q[rows], k, v, scale)
+    refs = _ref_rows(q[rows], ks, vs, scale)
+    for qnm in (0.0, qn):
+        _, _, o, og, orr = outs[qnm]
+        assert _rel(o[rows].float(), ref) < 1e-2
+        assert torch.equal(og, o)
+        assert _rel(orr[rows].float(), refs) < 1e-2

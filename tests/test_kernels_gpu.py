@@ -474,6 +474,26 @@ def test_residual_layernorm_variants(ops, var):
     assert rel(out.float(), F.layer_norm(xr.float(), (cols,), w, b, 1e-6)) < 5e-3
 
 
+@pytest.mark.parametrize("rows,n_inst,heads,ld", [(1, 1, 1, 64), (1374, 1, 16, 3072), (305, 7, 16, 1024),
+                                                  (777, 3, 24, 1600), (4099, 2, 32, 2048), (64, 300, 8, 512)])
+def test_attention_key_box(ops, rows, n_inst, heads, ld):
+    """sr_attention_key_box: per (instance, head, dim) max / min of bf16 keys, bit-exact against
+    torch amax / amin, with signed zeros, infinities and ragged row counts; instances inst_stride
+    rows apart (here rows + 5) inside a wider row stride."""
+    stride = rows + 5
+    g = torch.Generator(device=DEV).manual_seed(rows + heads)
+    buf = (torch.randn(n_inst * stride, ld, device=DEV, generator=g) * 3).bfloat16()
+    buf[0, 0] = -0.0
+    buf[min(1, rows - 1), 1] = float("inf")
+    buf[0, 2] = float("-inf")
+    out = torch.empty(n_inst, heads, 2, 64, device=DEV)
+    rc = _lib().load().sr_attention_key_box(ops._stream(buf), buf.data_ptr(), ld, rows, stride, n_inst, heads,
+                                             out.data_ptr())
+    assert rc == 0
+    k = buf.float().view(n_inst, stride, ld)[:, :rows, :heads * 64].reshape(n_inst, rows, heads, 64)
+    assert torch.equal(out[:, :, 0], k.amax(1)) and torch.equal(out[:, :, 1], k.amin(1))
+
+
 @pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])
 @pytest.mark.parametrize("M,N", [(43 * 256 - 100, 3072), (87936, 1024), (2 * 5496, 4096)])
 def test_gemm_tail_split(ops, epi_name, M, N):
