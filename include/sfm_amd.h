@@ -265,6 +265,11 @@ typedef struct sr_attn_desc {
                   min(c|q| max|k|, sum_d max(cq_d kmax_d, cq_d kmin_d)) -- far tighter when the keys
                   share a direction (all scores of a row well below the 2-norm bound, which otherwise
                   sends the row outside the fixed-offset window).  NULL = the 2-norm bound alone */
+  const float* value_box; /* optional (same path and layout as key_box, sr_attention_key_box run on
+                  the values): with max|v| known the fixed-offset window's upper side widens from 2^64
+                  to what the launch's fp32 sums allow, 125 - ceil(log2(l0 + l1)) -
+                  ceil(log2 max|v|) (at most 100), so rows with a larger gap between their bound and
+                  their true score max stay on the hand-scheduled sweep.  NULL = the 2^64 side */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */
@@ -272,7 +277,8 @@ int sr_attention_bound_floats(const sr_attn_desc* d);
 
 /* out[inst][h][0][d] / out[inst][h][1][d] = max / min over rows r < rows of k[inst*inst_stride + r]
  * [h*64 + d] (bf16 keys, head_dim 64; out fp32, n_inst*heads*128 floats): the key box of
- * sr_attn_desc.key_box for one key segment (inst_stride 0 with n_inst 1: keys shared by every item).
+ * sr_attn_desc.key_box for one key segment (inst_stride 0 with n_inst 1: keys shared by every item);
+ * on the values, sr_attn_desc.value_box.
  * Replaces nothing in the reference: a bound the fixed-offset softmax of attention.py:103-109's
  * replacement uses. */
 int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride, int n_inst,

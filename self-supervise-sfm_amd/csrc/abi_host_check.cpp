@@ -72,7 +72,7 @@ void layout() {
           FIELD(sr_attn_desc, mask_hstride), FIELD(sr_attn_desc, mask_ld), FIELD(sr_attn_desc, tail_rows_readable),
           FIELD(sr_attn_desc, merge_o), FIELD(sr_attn_desc, ld_merge_o), FIELD(sr_attn_desc, merge_lse),
           FIELD(sr_attn_desc, merge_rows), FIELD(sr_attn_desc, sweep_stats),
-          FIELD(sr_attn_desc, key_box)));
+          FIELD(sr_attn_desc, key_box), FIELD(sr_attn_desc, value_box)));
   STRUCT(sr_attn_bwd_desc,
          (FIELD(sr_attn_bwd_desc, f), FIELD(sr_attn_bwd_desc, dout), FIELD(sr_attn_bwd_desc, lddo),
           FIELD(sr_attn_bwd_desc, delta), FIELD(sr_attn_bwd_desc, dq), FIELD(sr_attn_bwd_desc, lddq),

@@ -74,9 +74,30 @@ constexpr float RESCALE_LOG2 = 8.f;
 // takes) and the row's largest P >= 2^-FIX_LO (normal in fp32 and bf16, as are its products with
 // every V entry above 2^-16).
 constexpr float FIX_HI = 64.f, FIX_LO = 110.f;
+// With d.value_box (per-dimension max / min of V, sr_attention_key_box on V) the upper side
+// widens to what THIS launch's fp32 sums allow: |O| <= L 2^hi max|v| and l <= L 2^hi stay below
+// 2^125 for hi = 125 - ceil(log2 L) - ceil(log2 max(max|v|, 1)), clamped to [FIX_HI, FIX_HI_MAX]
+// (P itself <= 2^100: bf16 / fp32 normal, v_exp exact range).
+constexpr float FIX_HI_MAX = 100.f;
 #ifndef SR_ATTN_DEFAULT_CFG
 #define SR_ATTN_DEFAULT_CFG 0
 #endif
+// The window's upper side for (item, head) from d.value_box (see FIX_HI_MAX): wave-uniform.
+__device__ __forceinline__ float value_window_hi(const sr_attn_desc& d, const AttnArgs& args, int item, int head,
+                                                 int lane) {
+  const float* b0 = d.value_box + ((int64_t)(d.k0_bstride == 0 ? 0 : item) * d.heads + head) * 128;
+  float v = fmaxf(fabsf(b0[lane]), fabsf(b0[64 + lane]));
+  if (args.ntile1 > 0) {
+    const float* b1 = d.value_box + ((int64_t)(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head) * 128;
+    v = fmaxf(v, fmaxf(fabsf(b1[lane]), fabsf(b1[64 + lane])));
+  }
+  v = sr::wave_max(v);
+  if (!(v <= 3.0e38f)) return FIX_HI;  // inf / nan in V: the default window
+  const float lg_v = ceilf(log2f(fmaxf(v, 1.f)));
+  const float lg_l = ceilf(log2f((float)(d.l0 + d.l1)));
+  return fminf(fmaxf(125.f - lg_l - lg_v, FIX_HI), FIX_HI_MAX);
+}
+
 // One workgroup's work: the NW*32*QB query rows from row0 of (head, item) against every key of
 // the item's segments.
 template <int NW> constexpr int attn_nbuf() { return NW >= 4 ? 4 : 2; }  // K/V ring stages
@@ -192,6 +213,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // qs: the 2-norm bound |S| <= qs (both sides); qb: the upper bound S <= qb, the box bound
   // sum_d max(cq_d kmax_d, cq_d kmin_d) where d.key_box is set (min of the two)
   float qb[QB], qs[QB];
+  float fix_hi = FIX_HI;  // the window's upper side (wider with d.value_box: value_window_hi)
   const bool use_bound = d.key_bound != nullptr || d.key_norm_max > 0.f;
   if (use_bound) {
     float kn = d.key_norm_max;
@@ -240,6 +262,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
       for (int b = 0; b < QB; ++b)  // + a margin for the fp32 sums of the score and of the bound
         qb[b] = fminf(qb[b], sum_x32(ub[b]) + 2e-4f * sum_x32(ab[b]));
     }
+    if (d.value_box) fix_hi = value_window_hi(d, args, item, head, lane);
   }
   bool fixed_m = false, m_zero = false;
   if (use_bound && args.allow_mzero) {
@@ -248,7 +271,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
     // tile-0 max pass and the -m fold MFMAs from the start
     bool z = true;
 #pragma unroll
-    for (int b = 0; b < QB; ++b) z &= qb[b] <= FIX_HI && qs[b] <= FIX_LO;
+    for (int b = 0; b < QB; ++b) z &= qb[b] <= fix_hi && qs[b] <= FIX_LO;
     fixed_m = m_zero = __all(z);
   }
 
@@ -365,7 +388,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
       if (t == 0 && use_bound) {
         bool ok = true;
 #pragma unroll
-        for (int b = 0; b < QB; ++b) ok &= qb[b] - mx[b] <= FIX_HI + FIX_LO;
+        for (int b = 0; b < QB; ++b) ok &= qb[b] - mx[b] <= fix_hi + FIX_LO;
         fixed_m = __all(ok);
       }
       if (__any(grow)) {
@@ -374,8 +397,8 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
           // new max (rows that did not grow keep theirs), split into bf16 hi + lo
           // fixed offset: m = 0 when the row's bound allows it (every score <= qb <= FIX_HI and the
           // true max >= -qb), else max(tile-0 max, qb - FIX_HI)
-          const float target = t == 0 ? (fixed_m ? ((qb[b] <= FIX_HI && qs[b] <= FIX_LO) ? 0.f
-                                                                           : fmaxf(mx[b], qb[b] - FIX_HI))
+          const float target = t == 0 ? (fixed_m ? ((qb[b] <= fix_hi && qs[b] <= FIX_LO) ? 0.f
+                                                                           : fmaxf(mx[b], qb[b] - fix_hi))
                                                  : mx[b])
                                       : m_run[b] + fmaxf(mx[b], 0.f);
           const bf16 nhi = (bf16)target;
@@ -484,7 +507,8 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // a wave with any row outside it runs the plain loop, which keeps the same wait, barrier and
   // stage per tile, so the waves of a workgroup may take different paths.
   // One key segment of full tiles (>= 4) or, with readable tails, the _SEG variant.
-  constexpr float PIPE_HI = FIX_HI, PIPE_LO = FIX_LO;
+  const float PIPE_HI = fix_hi;
+  constexpr float PIPE_LO = FIX_LO;
   bool asm_ok = false;
   float m_fix[QB];
   if constexpr (PIPE) {

@@ -70,6 +70,7 @@ class AttnDesc(ctypes.Structure):
         ("merge_o", _vp), ("ld_merge_o", _i64), ("merge_lse", _vp), ("merge_rows", _i64),
         ("sweep_stats", _vp),
         ("key_box", _vp),
+        ("value_box", _vp),
     ]
 
 

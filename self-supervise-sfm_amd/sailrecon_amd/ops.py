@@ -357,8 +357,8 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     ``key_norm_max`` > 0: a static bound of every key's per-head 2-norm (runtime.key_norm_bound),
     which replaces the key scan of the fixed-offset sweep.  ``query_norm_max`` > 0: the same bound
     for the queries (runtime.query_norm_bound); where scale*log2(e)*|q|*|k| leaves the sweep's
-    window the launch first computes the per-dimension key box (sr_attention_key_box,
-    sr_attn_desc.key_box; SR_ATTN_KEY_BOX=1 always, =0 never).  A bf16 single query set too short to
+    window the launch first computes the per-dimension key and value boxes (sr_attention_key_box,
+    sr_attn_desc.key_box / value_box; SR_ATTN_KEY_BOX=1 always, =0 never).  A bf16 single query set too short to
     fill the chip runs key-split (key_split_parts, attention_partials + attn_merge_n).
     ``tail_readable``: at least 64 rows of finite values follow every key segment in memory
     (runtime.Workspace buffers: zero-initialised, 64 rows of padding), which lets the
@@ -467,9 +467,11 @@ _FIX_HI = 64.0  # sr_attn.hip FIX_HI: the fixed offset's headroom (log2 units)
 
 
 def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_max: float, name: str) -> None:
-    """Set d.key_box (bf16, static key bound set) when the 2-norm score bound scale*log2(e)*|q|*|k|
-    exceeds the sweep's headroom FIX_HI: one sr_attention_key_box pass per key segment into a
-    per-stream workspace, instances as sr_attention_bound_floats' (k0's, then k1's)."""
+    """Set d.key_box and d.value_box (bf16, static key bound set) when the 2-norm score bound
+    scale*log2(e)*|q|*|k| exceeds the sweep's default headroom FIX_HI: sr_attention_key_box over
+    each key and value segment into a per-stream workspace, instances as
+    sr_attention_bound_floats' (k0's, then k1's)."""
+    del k1
     if _KEY_BOX == "0" or not (d.key_norm_max > 0.0) or d.head_dim != 64 or d.heads > 32:
         return
     if _KEY_BOX != "1" and not (query_norm_max > 0.0 and
@@ -478,15 +480,19 @@ def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_ma
     n0 = 1 if d.k0_bstride == 0 else d.batch
     n1 = (1 if d.k1_bstride == 0 else d.batch) if d.l1 > 0 else 0
     per = d.heads * 128
-    ws = _train_ws(k0.device, name, (n0 + n1) * per)
+    ws = _train_ws(k0.device, name, 2 * (n0 + n1) * per)
     lib = _lib.load()
     stream = _stream(k0)
-    check(lib.sr_attention_key_box(stream, d.k0, d.ldk0, d.l0, d.k0_bstride, n0, d.heads, _p(ws)),
-          "sr_attention_key_box")
+    segs = [(d.k0, d.ldk0, d.v0, d.ldv0, d.l0, d.k0_bstride, n0, 0)]
     if n1:
-        check(lib.sr_attention_key_box(stream, d.k1, d.ldk1, d.l1, d.k1_bstride, n1, d.heads, _p(ws[n0 * per:])),
+        segs.append((d.k1, d.ldk1, d.v1, d.ldv1, d.l1, d.k1_bstride, n1, n0 * per))
+    vb = (n0 + n1) * per
+    for k, ldk, v, ldv, rows, bstride, n, off in segs:
+        check(lib.sr_attention_key_box(stream, k, ldk, rows, bstride, n, d.heads, _p(ws[off:])),
               "sr_attention_key_box")
-    d.key_box = _p(ws)
+        check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:])),
+              "sr_attention_key_box(values)")
+    d.key_box, d.value_box = _p(ws), _p(ws[vb:])
 
 
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,

@@ -690,3 +690,36 @@ def test_global_attention_key_box(ops, g):
         assert _rel(o[rows].float(), ref) < 1e-2
         assert torch.equal(og, o)
         assert _rel(orr[rows].float(), refs) < 1e-2
+
+
+@pytest.mark.parametrize("vscale", [1.0, 2.0 ** 30], ids=["v1", "v2e30"])
+def test_global_attention_value_window(ops, vscale):
+    """The value box (sr_attn_desc.value_box): qk-gain 4.5 on LayerNorm'd random q / k puts every
+    wave's gap between its bound and its max over the first three key tiles at ~195 > 174 (the
+    default 2^64 / 2^-110 window), so the 2-norm window alone sends every wave to the compiled loop.
+    With max|v| known the upper side widens to 125 - ceil(log2 L) - ceil(log2 max|v|) = 106 -> 100
+    (|v| ~ 4): every wave runs the hand-scheduled sweep.  V scaled by 2^30 narrows it to 76 (a
+    186-wide window): the waves fall back, correctly.  Against fp64 on sampled rows."""
+    g, L = 4.5, 32 * P
+    gen = torch.Generator(device=DEV).manual_seed(45)
+    q, qn = _qk_gain(L, g, gen)
+    k, kb = _qk_gain(L, g, gen)
+    v = (torch.randn(L, C, device=DEV, generator=gen) * vscale).bfloat16()
+    res = {}
+    for qnm in (0.0, qn):
+        st = torch.zeros(2, dtype=torch.int32, device=DEV)
+        o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                      key_norm_max=kb, query_norm_max=qnm, sweep_stats=st)
+        torch.cuda.synchronize()
+        print(f"v x {vscale:g}, query_norm_max {qnm:.1f}: asm / compiled waves {st.tolist()}")
+        res[qnm] = (st.tolist(), o)
+    waves = (L + 63) // 64 * H
+    assert res[0.0][0] == [0, waves]
+    assert res[qn][0] == ([waves, 0] if vscale == 1.0 else [0, waves])
+    rows = _sample_rows(L, 128, 45).to(DEV)
+    ref = _ref_rows(q[rows], k, v, D ** -0.5)
+    for qnm in (0.0, qn):
+        err = _rel(res[qnm][1][rows].float(), ref)
+        print(f"rel err vs fp64 (query_norm_max {qnm:.1f}): {err:.2e}")
+        assert err < 1.5e-2  # c*q in bf16 at |s| ~ 300: as test_global_attention_qk_gain

@@ -61,10 +61,21 @@ def main():
             cs.append(cq.norm(dim=-1) * kn - mx)
             kmax, kmin = kk.max(0).values, kk.min(0).values
             bx.append(torch.maximum(cq * kmax, cq * kmin).sum(-1) - mx)
+        # per wave (64 consecutive query rows): max over its rows of the 2-norm bound minus the
+        # row's max over the first three key tiles (the pre-pass the sweep's window is checked on)
+        starts = torch.randperm(q.shape[0] // 64, generator=torch.Generator().manual_seed(7))[:16] * 64
+        wrows = (starts[:, None] + torch.arange(64)[None]).reshape(-1).to(q.device)
+        wv = []
+        for h in range(heads):
+            sl = slice(64 * h, 64 * h + 64)
+            cq = (q[wrows, sl].float() * c)
+            mx0 = (cq @ k[:192, sl].float().T).max(-1).values
+            wv.append((cq.norm(dim=-1) * kn - mx0).view(16, 64).max(-1).values)
         qt = torch.tensor([0.5, 0.9, 0.99, 1.0], device=q.device)
         f = lambda v: [round(float(x), 1) for x in torch.quantile(torch.cat(v), qt)]  # noqa: E731
         diag.append({"tag": tag, "rows": q.shape[0], "keys": k.shape[0], "cs_gap_q50_90_99_100": f(cs),
-                     "box_gap_q50_90_99_100": f(bx)})
+                     "box_gap_q50_90_99_100": f(bx),
+                     "wave_cs_gap_mx0_q50_90_99_100": f(wv)})
 
     def attention(q, *a, **kw):
         if q.dtype == torch.bfloat16 and kw.get("sweep_stats") is None and kw.get("mask") is None:
