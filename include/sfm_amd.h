@@ -223,7 +223,10 @@ typedef struct sr_attn_desc {
                   row's largest P >= 2^-110, so no overflow and the same precision.  The
                   hand-scheduled sweep (bf16, 256-row workgroups) fixes m = max(0, bound - 64) for
                   every row whose bound is within 2^174 of its max over the first three key tiles;
-                  other waves run the compiled loop; NULL (and no key_norm_max) = per-tile max */
+                  other waves run the compiled loop; NULL (and no key_norm_max) = per-tile max.
+                  (The per-head value is max |k|^2.)  With key_norm_max > 0 a non-NULL key_bound is
+                  NOT scratch but caller-filled (sr_attention_key_box's norm2_out) and the bound uses
+                  the smaller of the two: the keys' actual max norm is often well below the static one */
   float key_norm_max; /* optional (bf16 path): > 0 = a static upper bound of |k| (2-norm per head)
                   for every key, used INSTEAD of key_bound (no key scan).  For keys that come out of
                   the qk LayerNorm (attention.py:49-50,78) and RoPE (a rotation), |k| <=
@@ -278,11 +281,13 @@ int sr_attention_bound_floats(const sr_attn_desc* d);
 /* out[inst][h][0][d] / out[inst][h][1][d] = max / min over rows r < rows of k[inst*inst_stride + r]
  * [h*64 + d] (bf16 keys, head_dim 64; out fp32, n_inst*heads*128 floats): the key box of
  * sr_attn_desc.key_box for one key segment (inst_stride 0 with n_inst 1: keys shared by every item);
- * on the values, sr_attn_desc.value_box.
+ * on the values, sr_attn_desc.value_box.  norm2_out (optional, n_inst*heads floats): max over the rows
+ * of |k|^2 per instance and head (fp32 sums of the bf16 squares), sr_attn_desc.key_bound's caller-
+ * filled form.
  * Replaces nothing in the reference: a bound the fixed-offset softmax of attention.py:103-109's
  * replacement uses. */
 int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride, int n_inst,
-                         int heads, float* out);
+                         int heads, float* out, float* norm2_out);
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 

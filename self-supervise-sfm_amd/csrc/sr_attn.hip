@@ -216,12 +216,14 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   float fix_hi = FIX_HI;  // the window's upper side (wider with d.value_box: value_window_hi)
   const bool use_bound = d.key_bound != nullptr || d.key_norm_max > 0.f;
   if (use_bound) {
-    float kn = d.key_norm_max;
-    if (!(kn > 0.f)) {
+    // static bound, scanned bound (scratch filled above), or the smaller of a static and a
+    // caller-filled one (sr_attention_key_box's norm2_out)
+    float kn = d.key_norm_max > 0.f ? d.key_norm_max : INFINITY;
+    if (d.key_bound) {
       float kn2 = d.key_bound[(d.k0_bstride == 0 ? 0 : item) * d.heads + head];
       if (args.ntile1 > 0)
         kn2 = fmaxf(kn2, d.key_bound[(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head]);
-      kn = sqrtf(kn2);
+      kn = fminf(kn, sqrtf(kn2) * 1.0001f);  // (+ the fp32 sums of the squares)
     }
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
@@ -1213,22 +1215,26 @@ __device__ __forceinline__ int ord_key(float f) {
   return b ^ ((b >> 31) & 0x7fffffff);
 }
 
-__global__ __launch_bounds__(256) void key_box_init_kernel(int* out, int n) {
+__global__ __launch_bounds__(256) void key_box_init_kernel(int* out, int n, int* norm2, int n_norm) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) out[i] = (i & 64) ? 0x7fffffff : (int)0x80000000;  // [.][.][0] max slots, [.][.][1] min slots
+  if (norm2 && i < n_norm) norm2[i] = 0;  // non-negative fp32 order as their bits
 }
 
 __global__ __launch_bounds__(256) void key_box_kernel(const bf16* __restrict__ k, int64_t ldk, int rows,
-                                                      int64_t inst_stride, int heads, int* __restrict__ out) {
+                                                      int64_t inst_stride, int heads, int* __restrict__ out,
+                                                      int* __restrict__ norm2) {
   __shared__ int red[32 * 128];
+  __shared__ int red_n[32];
   const int cpr = heads * 8;  // 8-dim column groups per row
   const int rpi = blockDim.x / cpr;
   const int t = threadIdx.x;
   const int row_in = t / cpr, c = t - row_in * cpr, head = c >> 3, d0 = (c & 7) * 8;
   const int64_t inst = blockIdx.y;
   for (int i = t; i < heads * 128; i += blockDim.x) red[i] = (i & 64) ? 0x7fffffff : (int)0x80000000;
+  if (t < 32) red_n[t] = 0;
   __syncthreads();
-  float mx[8], mn[8];
+  float mx[8], mn[8], nmax = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mx[j] = -INFINITY;
@@ -1237,12 +1243,21 @@ __global__ __launch_bounds__(256) void key_box_kernel(const bf16* __restrict__ k
   if (row_in < rpi) {
     for (int r = blockIdx.x * rpi + row_in; r < rows; r += gridDim.x * rpi) {
       const bf16x8 v = *(const bf16x8*)(k + (inst * inst_stride + r) * ldk + c * 8);
+      float ss = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         mx[j] = fmaxf(mx[j], (float)v[j]);
         mn[j] = fminf(mn[j], (float)v[j]);
+        ss = fmaf((float)v[j], (float)v[j], ss);
       }
+      // |k|^2 of this row and head: the 8 lanes of the head's columns are 8 consecutive lanes
+      // (cpr is a multiple of 8), all on the same row
+      ss += __shfl_xor(ss, 1, 64);
+      ss += __shfl_xor(ss, 2, 64);
+      ss += __shfl_xor(ss, 4, 64);
+      nmax = fmaxf(nmax, ss);
     }
+    if ((c & 7) == 0) atomicMax(&red_n[head], __float_as_int(nmax));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       atomicMax(&red[head * 128 + d0 + j], ord_key(mx[j]));
@@ -1255,6 +1270,7 @@ __global__ __launch_bounds__(256) void key_box_kernel(const bf16* __restrict__ k
     if (i & 64) atomicMin(&o[i], red[i]);
     else atomicMax(&o[i], red[i]);
   }
+  if (norm2 && t < heads) atomicMax(&norm2[inst * heads + t], red_n[t]);
 }
 
 __global__ __launch_bounds__(256) void key_box_decode_kernel(int* out, int n) {
@@ -1577,7 +1593,7 @@ __global__ __launch_bounds__(256) void attn_merge_n_bf16_kernel(const bf16* __re
 }  // namespace
 
 extern "C" int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride,
-                                    int n_inst, int heads, float* out) {
+                                    int n_inst, int heads, float* out, float* norm2_out) {
   SR_CHECK(k && out, SR_EINVAL, "sr_attention_key_box: null k / out");
   SR_CHECK(rows > 0 && n_inst > 0 && heads > 0 && heads <= 32, SR_EINVAL,
            "sr_attention_key_box: rows, instances > 0 and 1..32 heads (rows=%d n_inst=%d heads=%d)", rows, n_inst, heads);
@@ -1586,14 +1602,16 @@ extern "C" int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t l
            SR_EINVAL, "sr_attention_key_box: ldk a multiple of 8 covering the heads, 16-B aligned k, inst_stride >= rows");
   hipStream_t s = (hipStream_t)stream;
   const int n = n_inst * heads * 128;
-  hipLaunchKernelGGL(key_box_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n);
+  SR_CHECK(((uintptr_t)norm2_out & 3) == 0, SR_EINVAL, "sr_attention_key_box: norm2_out must be 4-B aligned");
+  hipLaunchKernelGGL(key_box_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n, (int*)norm2_out,
+                     n_inst * heads);
   const int cpr = heads * 8;
   const int threads = std::max(64, (256 / cpr) * cpr);
   const int rpi = std::max(1, threads / cpr);
   const int want = std::max(1, 2048 / n_inst);
   const int gx = std::max(1, std::min((rows + rpi - 1) / rpi, want));
   hipLaunchKernelGGL(key_box_kernel, dim3(gx, n_inst), dim3(threads), 0, s, (const bf16*)k, ldk, rows, inst_stride, heads,
-                     (int*)out);
+                     (int*)out, (int*)norm2_out);
   hipLaunchKernelGGL(key_box_decode_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n);
   sr::note_kernel("key_box_kernel");
   return sr::check_launch("sr_attention_key_box");

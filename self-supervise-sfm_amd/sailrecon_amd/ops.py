@@ -467,10 +467,10 @@ _FIX_HI = 64.0  # sr_attn.hip FIX_HI: the fixed offset's headroom (log2 units)
 
 
 def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_max: float, name: str) -> None:
-    """Set d.key_box and d.value_box (bf16, static key bound set) when the 2-norm score bound
-    scale*log2(e)*|q|*|k| exceeds the sweep's default headroom FIX_HI: sr_attention_key_box over
-    each key and value segment into a per-stream workspace, instances as
-    sr_attention_bound_floats' (k0's, then k1's)."""
+    """Set d.key_box, d.value_box and d.key_bound (the keys' actual max |k|^2, which tightens the
+    static key_norm_max) when the 2-norm score bound scale*log2(e)*|q|*|k| exceeds the sweep's
+    default headroom FIX_HI: sr_attention_key_box over each key and value segment into a
+    per-stream workspace, instances as sr_attention_bound_floats' (k0's, then k1's)."""
     del k1
     if _KEY_BOX == "0" or not (d.key_norm_max > 0.0) or d.head_dim != 64 or d.heads > 32:
         return
@@ -480,19 +480,19 @@ def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_ma
     n0 = 1 if d.k0_bstride == 0 else d.batch
     n1 = (1 if d.k1_bstride == 0 else d.batch) if d.l1 > 0 else 0
     per = d.heads * 128
-    ws = _train_ws(k0.device, name, 2 * (n0 + n1) * per)
+    ws = _train_ws(k0.device, name, (2 * per + d.heads) * (n0 + n1))
     lib = _lib.load()
     stream = _stream(k0)
     segs = [(d.k0, d.ldk0, d.v0, d.ldv0, d.l0, d.k0_bstride, n0, 0)]
     if n1:
         segs.append((d.k1, d.ldk1, d.v1, d.ldv1, d.l1, d.k1_bstride, n1, n0 * per))
-    vb = (n0 + n1) * per
+    vb, nb = (n0 + n1) * per, 2 * (n0 + n1) * per
     for k, ldk, v, ldv, rows, bstride, n, off in segs:
-        check(lib.sr_attention_key_box(stream, k, ldk, rows, bstride, n, d.heads, _p(ws[off:])),
-              "sr_attention_key_box")
-        check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:])),
+        check(lib.sr_attention_key_box(stream, k, ldk, rows, bstride, n, d.heads, _p(ws[off:]),
+                                       _p(ws[nb + off // 128:])), "sr_attention_key_box")
+        check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:]), None),
               "sr_attention_key_box(values)")
-    d.key_box, d.value_box = _p(ws), _p(ws[vb:])
+    d.key_box, d.value_box, d.key_bound = _p(ws), _p(ws[vb:]), _p(ws[nb:])
 
 
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,

@@ -692,14 +692,15 @@ def test_global_attention_key_box(ops, g):
         assert _rel(orr[rows].float(), refs) < 1e-2
 
 
-@pytest.mark.parametrize("vscale", [1.0, 2.0 ** 30], ids=["v1", "v2e30"])
+@pytest.mark.parametrize("vscale", [1.0, 2.0 ** 40], ids=["v1", "v2e40"])
 def test_global_attention_value_window(ops, vscale):
     """The value box (sr_attn_desc.value_box): qk-gain 4.5 on LayerNorm'd random q / k puts every
     wave's gap between its bound and its max over the first three key tiles at ~195 > 174 (the
     default 2^64 / 2^-110 window), so the 2-norm window alone sends every wave to the compiled loop.
     With max|v| known the upper side widens to 125 - ceil(log2 L) - ceil(log2 max|v|) = 106 -> 100
-    (|v| ~ 4): every wave runs the hand-scheduled sweep.  V scaled by 2^30 narrows it to 76 (a
-    186-wide window): most waves fall back (measured: 589 of 10992 stay), correctly.  Against fp64 on sampled rows."""
+    (|v| ~ 4): every wave runs the hand-scheduled sweep.  V scaled by 2^40 narrows it to 66 (a
+    176-wide window): most waves fall back, correctly.  (With the boxes the launch also scans the
+    keys' actual max norm, ~5 % below the static bound here.)  Against fp64 on sampled rows."""
     g, L = 4.5, 32 * P
     gen = torch.Generator(device=DEV).manual_seed(45)
     q, qn = _qk_gain(L, g, gen)

@@ -487,11 +487,17 @@ def test_attention_key_box(ops, rows, n_inst, heads, ld):
     buf[min(1, rows - 1), 1] = float("inf")
     buf[0, 2] = float("-inf")
     out = torch.empty(n_inst, heads, 2, 64, device=DEV)
+    n2 = torch.full((n_inst, heads), -1.0, device=DEV)
     rc = _lib().load().sr_attention_key_box(ops._stream(buf), buf.data_ptr(), ld, rows, stride, n_inst, heads,
-                                             out.data_ptr())
+                                             out.data_ptr(), n2.data_ptr())
     assert rc == 0
     k = buf.float().view(n_inst, stride, ld)[:, :rows, :heads * 64].reshape(n_inst, rows, heads, 64)
     assert torch.equal(out[:, :, 0], k.amax(1)) and torch.equal(out[:, :, 1], k.amin(1))
+    # max |k|^2 per instance and head (fp32 sums: summation order differs from torch's)
+    ref = k.double().square().sum(-1).amax(1)
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isinf(n2), ~fin)
+    assert torch.allclose(n2[fin].double(), ref[fin], rtol=1e-6, atol=0)
 
 
 @pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])
