@@ -283,11 +283,13 @@ int sr_attention_bound_floats(const sr_attn_desc* d);
  * sr_attn_desc.key_box for one key segment (inst_stride 0 with n_inst 1: keys shared by every item);
  * on the values, sr_attn_desc.value_box.  norm2_out (optional, n_inst*heads floats): max over the rows
  * of |k|^2 per instance and head (fp32 sums of the bf16 squares), sr_attn_desc.key_bound's caller-
- * filled form.
+ * filled form.  Two launches (per-workgroup partial boxes in scratch, then their reduction), no atomics.
  * Replaces nothing in the reference: a bound the fixed-offset softmax of attention.py:103-109's
  * replacement uses. */
 int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride, int n_inst,
-                         int heads, float* out, float* norm2_out);
+                         int heads, float* out, float* norm2_out, float* scratch);
+/* floats of scratch (4-B aligned, stream-ordered reuse) sr_attention_key_box needs for the shape */
+int sr_attention_key_box_scratch(int rows, int n_inst, int heads);
 
 int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
 

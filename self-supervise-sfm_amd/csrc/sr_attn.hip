@@ -1207,78 +1207,108 @@ void launch_key_norm(hipStream_t s, const void* k, int64_t ldk, int rows, int64_
                      inst_stride, heads, (unsigned*)out);
 }
 
-// key box of sr_attention_key_box: per (instance, head, dim) max and min of the keys.  fp32 values
-// are reduced as order-preserving int32 keys (o(f) = bits ^ ((bits >> 31) & 0x7fffffff), its own
-// inverse) with the integer atomicMax / atomicMin: init, scan, decode.
-__device__ __forceinline__ int ord_key(float f) {
-  const int b = __float_as_int(f);
-  return b ^ ((b >> 31) & 0x7fffffff);
-}
+// key box of sr_attention_key_box: per (instance, head, dim) max and min of the keys and the max
+// |k|^2 per (instance, head), in two passes without atomics: key_box_part_kernel reduces a
+// workgroup's rows to one partial box in the caller's scratch, key_box_reduce_kernel the partials.
+// Thread layout: cpr = heads * 8 threads cover one row (8 dims each: 16-B loads), rpi rows per pass.
+__host__ __device__ constexpr int key_box_threads(int heads) { return (256 / (heads * 8)) * (heads * 8); }
 
-__global__ __launch_bounds__(256) void key_box_init_kernel(int* out, int n, int* norm2, int n_norm) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] = (i & 64) ? 0x7fffffff : (int)0x80000000;  // [.][.][0] max slots, [.][.][1] min slots
-  if (norm2 && i < n_norm) norm2[i] = 0;  // non-negative fp32 order as their bits
-}
-
-__global__ __launch_bounds__(256) void key_box_kernel(const bf16* __restrict__ k, int64_t ldk, int rows,
-                                                      int64_t inst_stride, int heads, int* __restrict__ out,
-                                                      int* __restrict__ norm2) {
-  __shared__ int red[32 * 128];
-  __shared__ int red_n[32];
-  const int cpr = heads * 8;  // 8-dim column groups per row
-  const int rpi = blockDim.x / cpr;
-  const int t = threadIdx.x;
-  const int row_in = t / cpr, c = t - row_in * cpr, head = c >> 3, d0 = (c & 7) * 8;
+__global__ __launch_bounds__(256) void key_box_part_kernel(const bf16* __restrict__ k, int64_t ldk, int rows,
+                                                           int64_t inst_stride, int heads, float* __restrict__ part) {
+  __shared__ float red[256 * 16];  // [thread][8 max | 8 min]
+  __shared__ float red_n[256 / 8];
+  const int cpr = heads * 8, rpi = blockDim.x / cpr, t = threadIdx.x;
+  const int row_in = t / cpr, c = t - row_in * cpr, head = c >> 3;
   const int64_t inst = blockIdx.y;
-  for (int i = t; i < heads * 128; i += blockDim.x) red[i] = (i & 64) ? 0x7fffffff : (int)0x80000000;
-  if (t < 32) red_n[t] = 0;
-  __syncthreads();
+  const bf16* kb = k + inst * inst_stride * ldk + c * 8;
   float mx[8], mn[8], nmax = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mx[j] = -INFINITY;
     mn[j] = INFINITY;
   }
-  if (row_in < rpi) {
-    for (int r = blockIdx.x * rpi + row_in; r < rows; r += gridDim.x * rpi) {
-      const bf16x8 v = *(const bf16x8*)(k + (inst * inst_stride + r) * ldk + c * 8);
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        mx[j] = fmaxf(mx[j], (float)v[j]);
-        mn[j] = fminf(mn[j], (float)v[j]);
-        ss = fmaf((float)v[j], (float)v[j], ss);
-      }
-      // |k|^2 of this row and head: the 8 lanes of the head's columns are 8 consecutive lanes
-      // (cpr is a multiple of 8), all on the same row
-      ss += __shfl_xor(ss, 1, 64);
-      ss += __shfl_xor(ss, 2, 64);
-      ss += __shfl_xor(ss, 4, 64);
-      nmax = fmaxf(nmax, ss);
-    }
-    if ((c & 7) == 0) atomicMax(&red_n[head], __float_as_int(nmax));
+  auto take = [&](const bf16x8 v) {
+    float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      atomicMax(&red[head * 128 + d0 + j], ord_key(mx[j]));
-      atomicMin(&red[head * 128 + 64 + d0 + j], ord_key(mn[j]));
+      mx[j] = fmaxf(mx[j], (float)v[j]);
+      mn[j] = fminf(mn[j], (float)v[j]);
+      ss = fmaf((float)v[j], (float)v[j], ss);
     }
+    // |k|^2 of the row for this head: its 8 column threads are 8 consecutive lanes of one row
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    ss += __shfl_xor(ss, 4, 64);
+    nmax = fmaxf(nmax, ss);
+  };
+  const int step = gridDim.x * rpi;
+  int r = blockIdx.x * rpi + row_in;
+  for (; r + 3 * step < rows; r += 4 * step) {  // four independent 16-B loads in flight
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(kb + (int64_t)(r + u * step) * ldk);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) take(v[u]);
   }
+  for (; r < rows; r += step) take(*(const bf16x8*)(kb + (int64_t)r * ldk));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[t * 16 + j] = mx[j];
+    red[t * 16 + 8 + j] = mn[j];
+  }
+  if ((c & 7) == 0) red_n[row_in * heads + head] = nmax;
   __syncthreads();
-  int* o = out + inst * heads * 128;
+  // partial [heads][2][64] of this workgroup: column i = h*128 + side*64 + d
+  float* pb = part + ((int64_t)inst * gridDim.x + blockIdx.x) * heads * 128;
   for (int i = t; i < heads * 128; i += blockDim.x) {
-    if (i & 64) atomicMin(&o[i], red[i]);
-    else atomicMax(&o[i], red[i]);
+    const int h = i >> 7, side = (i >> 6) & 1, d = i & 63;
+    const int src = (h * 8 + (d >> 3)) * 16 + side * 8 + (d & 7);  // thread h*8 + d/8 of row 0
+    float a = red[src];
+    for (int q = 1; q < rpi; ++q) {
+      const float b = red[src + q * cpr * 16];
+      a = side ? fminf(a, b) : fmaxf(a, b);
+    }
+    pb[i] = a;
   }
-  if (norm2 && t < heads) atomicMax(&norm2[inst * heads + t], red_n[t]);
+  if (t < heads) {
+    float a = red_n[t];
+    for (int q = 1; q < rpi; ++q) a = fmaxf(a, red_n[q * heads + t]);
+    part[(int64_t)gridDim.y * gridDim.x * heads * 128 + ((int64_t)inst * gridDim.x + blockIdx.x) * heads + t] = a;
+  }
 }
 
-__global__ __launch_bounds__(256) void key_box_decode_kernel(int* out, int n) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    const int b = out[i];
-    out[i] = b ^ ((b >> 31) & 0x7fffffff);  // back to the fp32 bits
+// out[inst][h][side][d] over the nparts partials of each instance (64 columns x 4 part groups per
+// workgroup); workgroup x == 0 also reduces the norms
+__global__ __launch_bounds__(256) void key_box_reduce_kernel(const float* __restrict__ part, int nparts, int heads,
+                                                             int n_inst, float* __restrict__ out,
+                                                             float* __restrict__ norm2) {
+  __shared__ float red[4][64];
+  const int t = threadIdx.x, col = blockIdx.x * 64 + (t & 63), grp = t >> 6, side = (col >> 6) & 1;
+  const int64_t inst = blockIdx.y, cols = heads * 128;
+  float a = side ? INFINITY : -INFINITY;
+  for (int p = grp; p < nparts; p += 4) {
+    const float b = part[(inst * nparts + p) * cols + col];
+    a = side ? fminf(a, b) : fmaxf(a, b);
   }
+  red[grp][t & 63] = a;
+  __syncthreads();
+  if (grp == 0) {
+#pragma unroll
+    for (int g = 1; g < 4; ++g) a = side ? fminf(a, red[g][t]) : fmaxf(a, red[g][t]);
+    out[inst * cols + col] = a;
+  }
+  if (norm2 && blockIdx.x == 0 && t < heads) {
+    const float* pn = part + (int64_t)n_inst * nparts * cols + inst * nparts * heads;
+    float m = 0.f;
+    for (int p = 0; p < nparts; ++p) m = fmaxf(m, pn[p * heads + t]);
+    norm2[inst * heads + t] = m;
+  }
+}
+
+// workgroups per instance of key_box_part_kernel: >= 16 rows per thread, <= 1024 in total
+int key_box_parts(int rows, int n_inst, int heads) {
+  const int rpi = key_box_threads(heads) / (heads * 8);
+  return std::max(1, std::min((rows + rpi * 16 - 1) / (rpi * 16), std::max(1, 1024 / n_inst)));
 }
 
 // ------------------------------------------------------------------ f32 / VALU
@@ -1592,28 +1622,28 @@ __global__ __launch_bounds__(256) void attn_merge_n_bf16_kernel(const bf16* __re
 
 }  // namespace
 
+extern "C" int sr_attention_key_box_scratch(int rows, int n_inst, int heads) {
+  if (rows <= 0 || n_inst <= 0 || heads <= 0 || heads > 32) return 0;
+  return n_inst * key_box_parts(rows, n_inst, heads) * heads * 129;
+}
+
 extern "C" int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride,
-                                    int n_inst, int heads, float* out, float* norm2_out) {
-  SR_CHECK(k && out, SR_EINVAL, "sr_attention_key_box: null k / out");
+                                    int n_inst, int heads, float* out, float* norm2_out, float* scratch) {
+  SR_CHECK(k && out && scratch, SR_EINVAL, "sr_attention_key_box: null k / out / scratch");
   SR_CHECK(rows > 0 && n_inst > 0 && heads > 0 && heads <= 32, SR_EINVAL,
            "sr_attention_key_box: rows, instances > 0 and 1..32 heads (rows=%d n_inst=%d heads=%d)", rows, n_inst, heads);
   SR_CHECK(ldk % 8 == 0 && ldk >= 64 * heads && ((uintptr_t)k & 15) == 0 && ((uintptr_t)out & 3) == 0 &&
-               (n_inst == 1 || inst_stride >= rows),
-           SR_EINVAL, "sr_attention_key_box: ldk a multiple of 8 covering the heads, 16-B aligned k, inst_stride >= rows");
+               ((uintptr_t)norm2_out & 3) == 0 && ((uintptr_t)scratch & 3) == 0 && (n_inst == 1 || inst_stride >= rows),
+           SR_EINVAL, "sr_attention_key_box: ldk a multiple of 8 covering the heads, 16-B aligned k, 4-B aligned "
+                      "out / norm2_out / scratch, inst_stride >= rows");
+  SR_CHECK(n_inst <= 65535, SR_EINVAL, "sr_attention_key_box: at most 65535 instances");
   hipStream_t s = (hipStream_t)stream;
-  const int n = n_inst * heads * 128;
-  SR_CHECK(((uintptr_t)norm2_out & 3) == 0, SR_EINVAL, "sr_attention_key_box: norm2_out must be 4-B aligned");
-  hipLaunchKernelGGL(key_box_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n, (int*)norm2_out,
-                     n_inst * heads);
-  const int cpr = heads * 8;
-  const int threads = std::max(64, (256 / cpr) * cpr);
-  const int rpi = std::max(1, threads / cpr);
-  const int want = std::max(1, 2048 / n_inst);
-  const int gx = std::max(1, std::min((rows + rpi - 1) / rpi, want));
-  hipLaunchKernelGGL(key_box_kernel, dim3(gx, n_inst), dim3(threads), 0, s, (const bf16*)k, ldk, rows, inst_stride, heads,
-                     (int*)out, (int*)norm2_out);
-  hipLaunchKernelGGL(key_box_decode_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (int*)out, n);
-  sr::note_kernel("key_box_kernel");
+  const int gx = key_box_parts(rows, n_inst, heads);
+  hipLaunchKernelGGL(key_box_part_kernel, dim3(gx, n_inst), dim3(key_box_threads(heads)), 0, s, (const bf16*)k, ldk,
+                     rows, inst_stride, heads, scratch);
+  hipLaunchKernelGGL(key_box_reduce_kernel, dim3(heads * 2, n_inst), dim3(256), 0, s, (const float*)scratch, gx, heads,
+                     n_inst, out, norm2_out);
+  sr::note_kernel("key_box_part_kernel");
   return sr::check_launch("sr_attention_key_box");
 }
 

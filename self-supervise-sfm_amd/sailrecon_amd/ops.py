@@ -487,10 +487,12 @@ def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_ma
     if n1:
         segs.append((d.k1, d.ldk1, d.v1, d.ldv1, d.l1, d.k1_bstride, n1, n0 * per))
     vb, nb = (n0 + n1) * per, 2 * (n0 + n1) * per
+    sc = _train_ws(k0.device, "attn_box_scratch",
+                   max(lib.sr_attention_key_box_scratch(g[4], g[6], d.heads) for g in segs))
     for k, ldk, v, ldv, rows, bstride, n, off in segs:
         check(lib.sr_attention_key_box(stream, k, ldk, rows, bstride, n, d.heads, _p(ws[off:]),
-                                       _p(ws[nb + off // 128:])), "sr_attention_key_box")
-        check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:]), None),
+                                       _p(ws[nb + off // 128:]), _p(sc)), "sr_attention_key_box")
+        check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:]), None, _p(sc)),
               "sr_attention_key_box(values)")
     d.key_box, d.value_box, d.key_bound = _p(ws), _p(ws[vb:]), _p(ws[nb:])
 

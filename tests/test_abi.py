@@ -50,8 +50,10 @@ def test_abi_validation_errors_without_gpu():
     # key box: 33 heads, an unaligned k, and an instance stride below the rows are rejected
     for args in ((64, 10, 0, 1, 33), (64, 10, 0, 1, 1), (1024, 10, 5, 2, 16)):
         k = ctypes.c_void_p(18 if args == (64, 10, 0, 1, 1) else 16)
-        assert lib.sr_attention_key_box(None, k, *args[:4], args[4], ctypes.c_void_p(16), None) == -1, args
+        assert lib.sr_attention_key_box(None, k, *args[:4], args[4], ctypes.c_void_p(16), None,
+                                        ctypes.c_void_p(16)) == -1, args
         assert b"sr_attention_key_box" in lib.sr_last_error()
+    assert lib.sr_attention_key_box_scratch(43968, 1, 16) > 0 and lib.sr_attention_key_box_scratch(10, 1, 33) == 0
 
 
 def test_tuning_switches_without_gpu():

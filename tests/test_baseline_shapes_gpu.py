@@ -655,8 +655,10 @@ def test_global_attention_key_box(ops, g):
     ks, kbs = _qk_gain_shared(nf, g, gen, u, 0.05)
     vs = torch.randn(nf, C, device=DEV, generator=gen).bfloat16()
     box = torch.empty(H, 2, D, device=DEV)
-    assert ops._lib.load().sr_attention_key_box(ops._stream(k), k.data_ptr(), C, L, 0, 1, H, box.data_ptr(),
-                                                   None) == 0
+    lib = ops._lib.load()
+    sc = torch.empty(lib.sr_attention_key_box_scratch(L, 1, H), device=DEV)
+    assert lib.sr_attention_key_box(ops._stream(k), k.data_ptr(), C, L, 0, 1, H, box.data_ptr(), None,
+                                    sc.data_ptr()) == 0
     kh = k.float().view(L, H, D)
     assert torch.equal(box[:, 0], kh.amax(0)) and torch.equal(box[:, 1], kh.amin(0))
     outs = {}

@@ -479,7 +479,8 @@ def test_residual_layernorm_variants(ops, var):
 def test_attention_key_box(ops, rows, n_inst, heads, ld):
     """sr_attention_key_box: per (instance, head, dim) max / min of bf16 keys, bit-exact against
     torch amax / amin, with signed zeros, infinities and ragged row counts; instances inst_stride
-    rows apart (here rows + 5) inside a wider row stride."""
+    rows apart (here rows + 5) inside a wider row stride; scratch pre-filled with NaN (every
+    partial slot the reduction reads is written first)."""
     stride = rows + 5
     g = torch.Generator(device=DEV).manual_seed(rows + heads)
     buf = (torch.randn(n_inst * stride, ld, device=DEV, generator=g) * 3).bfloat16()
@@ -488,8 +489,10 @@ def test_attention_key_box(ops, rows, n_inst, heads, ld):
     buf[0, 2] = float("-inf")
     out = torch.empty(n_inst, heads, 2, 64, device=DEV)
     n2 = torch.full((n_inst, heads), -1.0, device=DEV)
-    rc = _lib().load().sr_attention_key_box(ops._stream(buf), buf.data_ptr(), ld, rows, stride, n_inst, heads,
-                                             out.data_ptr(), n2.data_ptr())
+    L = _lib().load()
+    sc = torch.full((L.sr_attention_key_box_scratch(rows, n_inst, heads),), float("nan"), device=DEV)
+    rc = L.sr_attention_key_box(ops._stream(buf), buf.data_ptr(), ld, rows, stride, n_inst, heads, out.data_ptr(),
+                                n2.data_ptr(), sc.data_ptr())
     assert rc == 0
     k = buf.float().view(n_inst, stride, ld)[:, :rows, :heads * 64].reshape(n_inst, rows, heads, 64)
     assert torch.equal(out[:, :, 0], k.amax(1)) and torch.equal(out[:, :, 1], k.amin(1))
