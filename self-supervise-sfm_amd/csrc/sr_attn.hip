@@ -1277,38 +1277,54 @@ __global__ __launch_bounds__(256) void key_box_part_kernel(const bf16* __restric
   }
 }
 
-// out[inst][h][side][d] over the nparts partials of each instance (64 columns x 4 part groups per
-// workgroup); workgroup x == 0 also reduces the norms
-__global__ __launch_bounds__(256) void key_box_reduce_kernel(const float* __restrict__ part, int nparts, int heads,
-                                                             int n_inst, float* __restrict__ out,
-                                                             float* __restrict__ norm2) {
-  __shared__ float red[4][64];
+// out[inst][h][side][d] over the nparts partials of each instance: 64 columns x 16 part groups per
+// workgroup, 8 loads in flight per thread; workgroup x == 0 also reduces the norms (32 head slots x
+// 32 part groups)
+__global__ __launch_bounds__(1024) void key_box_reduce_kernel(const float* __restrict__ part, int nparts, int heads,
+                                                              int n_inst, float* __restrict__ out,
+                                                              float* __restrict__ norm2) {
+  __shared__ float red[16][64];
+  __shared__ float red_n[32][33];
   const int t = threadIdx.x, col = blockIdx.x * 64 + (t & 63), grp = t >> 6, side = (col >> 6) & 1;
   const int64_t inst = blockIdx.y, cols = heads * 128;
+  const float* pc = part + inst * nparts * cols + col;
   float a = side ? INFINITY : -INFINITY;
-  for (int p = grp; p < nparts; p += 4) {
-    const float b = part[(inst * nparts + p) * cols + col];
-    a = side ? fminf(a, b) : fmaxf(a, b);
+  int p = grp;
+  for (; p + 7 * 16 < nparts; p += 8 * 16) {
+    float b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) b[u] = pc[(int64_t)(p + 16 * u) * cols];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a = side ? fminf(a, b[u]) : fmaxf(a, b[u]);
   }
+  for (; p < nparts; p += 16) a = side ? fminf(a, pc[(int64_t)p * cols]) : fmaxf(a, pc[(int64_t)p * cols]);
   red[grp][t & 63] = a;
+  if (norm2 && blockIdx.x == 0) {  // head t & 31, part group t >> 5
+    const float* pn = part + (int64_t)n_inst * nparts * cols + inst * nparts * heads;
+    const int h = t & 31, g = t >> 5;
+    float m = 0.f;
+    if (h < heads)
+      for (int q = g; q < nparts; q += 32) m = fmaxf(m, pn[(int64_t)q * heads + h]);
+    red_n[g][h] = m;
+  }
   __syncthreads();
   if (grp == 0) {
 #pragma unroll
-    for (int g = 1; g < 4; ++g) a = side ? fminf(a, red[g][t]) : fmaxf(a, red[g][t]);
+    for (int g = 1; g < 16; ++g) a = side ? fminf(a, red[g][t]) : fmaxf(a, red[g][t]);
     out[inst * cols + col] = a;
   }
   if (norm2 && blockIdx.x == 0 && t < heads) {
-    const float* pn = part + (int64_t)n_inst * nparts * cols + inst * nparts * heads;
-    float m = 0.f;
-    for (int p = 0; p < nparts; ++p) m = fmaxf(m, pn[p * heads + t]);
+    float m = red_n[0][t];
+    for (int g = 1; g < 32; ++g) m = fmaxf(m, red_n[g][t]);
     norm2[inst * heads + t] = m;
   }
 }
 
-// workgroups per instance of key_box_part_kernel: >= 16 rows per thread, <= 1024 in total
+// workgroups per instance of key_box_part_kernel: >= 16 rows per thread, <= 512 in total (2 per CU,
+// 4 loads in flight per thread: enough to stream at HBM rate, few partials to reduce)
 int key_box_parts(int rows, int n_inst, int heads) {
   const int rpi = key_box_threads(heads) / (heads * 8);
-  return std::max(1, std::min((rows + rpi * 16 - 1) / (rpi * 16), std::max(1, 1024 / n_inst)));
+  return std::max(1, std::min((rows + rpi * 16 - 1) / (rpi * 16), std::max(1, 512 / n_inst)));
 }
 
 // ------------------------------------------------------------------ f32 / VALU
@@ -1641,8 +1657,8 @@ extern "C" int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t l
   const int gx = key_box_parts(rows, n_inst, heads);
   hipLaunchKernelGGL(key_box_part_kernel, dim3(gx, n_inst), dim3(key_box_threads(heads)), 0, s, (const bf16*)k, ldk,
                      rows, inst_stride, heads, scratch);
-  hipLaunchKernelGGL(key_box_reduce_kernel, dim3(heads * 2, n_inst), dim3(256), 0, s, (const float*)scratch, gx, heads,
-                     n_inst, out, norm2_out);
+  hipLaunchKernelGGL(key_box_reduce_kernel, dim3(heads * 2, n_inst), dim3(1024), 0, s, (const float*)scratch, gx,
+                     heads, n_inst, out, norm2_out);
   sr::note_kernel("key_box_part_kernel");
   return sr::check_launch("sr_attention_key_box");
 }
