@@ -218,6 +218,16 @@ void check() {
   expect("sr_attention_pair head counts", sr_attention_pair(nullptr, SR_BF16, &a, &b), false);
   d = attn(1, 16, 43968, 43968, 0);
   std::printf("bound floats: %d\n", sr_attention_bound_floats(&d));
+  std::printf("key box scratch floats: %d\n", sr_attention_key_box_scratch(43968, 1, 16));
+  expect("sr_attention_key_box", sr_attention_key_box(nullptr, fake(0), 3072, 43968, 0, 1, 16, fake<float>(1),
+                                                      fake<float>(2), fake<float>(3)), true);
+  expect("sr_attention_key_box null scratch", sr_attention_key_box(nullptr, fake(0), 3072, 43968, 0, 1, 16,
+                                                                   fake<float>(1), nullptr, nullptr), false);
+  expect("sr_attention_key_box 33 heads", sr_attention_key_box(nullptr, fake(0), 3072, 100, 0, 1, 33, fake<float>(1),
+                                                               nullptr, fake<float>(3)), false);
+  expect("sr_attention_key_box overlapping instances", sr_attention_key_box(nullptr, fake(0), 1024, 1374, 1000, 64,
+                                                                             16, fake<float>(1), nullptr,
+                                                                             fake<float>(3)), false);
 
   // ---- merges
   const int seg[SR_ATTN_MERGE_MAX_PARTS] = {43968, 1374};
