@@ -32,9 +32,10 @@ Prints ONE JSON line on rank 0 (contract in the task statement) with a
 the timed region) and a ``cpu_baseline`` object (the CPU oracle on a bounded
 sample, rank 0 at N=1 only).  A per-kernel-class breakdown goes to stderr.
 After the headline's timed region the same model also times the ``extra_configs`` (--extras):
-N=64 @518 (the north star's 64-view scaling workload, sharded like the headline) and, on one GPU,
-BASELINE C5 (N=128 @518 with fp8 global attention); they ride inside the one line and are
-never its ``value``.
+N=64 @518 (the north star's 64-view scaling workload, sharded like the headline), on one GPU
+BASELINE C5 (N=128 @518 with fp8 global attention), and the headline workload at qk-norm gain 4
+(``g4``: trained-like q_norm / k_norm weights); they ride inside the one line and are never its
+``value``.
 """
 
 from __future__ import annotations
@@ -401,7 +402,7 @@ def main():
     ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
                     help="BASELINE C5: the global blocks' q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 "
                          "e4m3; everything else bf16")
-    ap.add_argument("--extras", default="n64,c5",
+    ap.add_argument("--extras", default="n64,c5,g4",
                     help="comma list of extra workloads timed after the headline on the same model and reported "
                          "inside its line as extra_configs (not the metric): n64 = N=64 @518 bf16 (the north "
                          "star's 64-view scaling workload, sharded like the headline), c5 = BASELINE C5 (N=128 "
@@ -545,8 +546,10 @@ def main():
         for name in [e for e in args.extras.split(",") if e and e != "none"]:
             if name == "c5" and world > 1:
                 continue
-            if name not in ("n64", "c5"):
+            if name not in ("n64", "c5", "g4"):
                 raise SystemExit(f"bench.py: unknown extra workload {name!r}")
+            if name == "g4" and args.qk_gain != 1.0:
+                continue  # the headline already runs at a scaled gain
             extras.append(extra_config(model, device, args, world, name))
 
     cpu = None
@@ -591,20 +594,25 @@ def extra_config(model, device, args, world, name):
     line's ``extra_configs``, never as its value): ``n64`` = N=64 @518 bf16, the north star's
     64-view scaling workload (frame-sharded like the headline when world > 1); ``c5`` = BASELINE
     config 5 (N=128 @518, 256 frames, L_g = 175,872) with the global blocks' attention in fp8
-    (Aggregator.set_fp8_global), one GPU.  One untimed warmup, then a few steps between barriers +
+    (Aggregator.set_fp8_global), one GPU; ``g4`` = the headline workload with every q_norm / k_norm
+weight x 4 (scale_qk_gain, undone after).  One untimed warmup, then a few steps between barriers +
     synchronize, max over ranks.  A Python error is reported in the object, not raised."""
     from sailrecon_amd import ops
-    n = 64 if name == "n64" else 128
+    n = {"n64": 64, "c5": 128}.get(name, args.views)
     fp8 = name == "c5"
-    steps = 3 if name == "n64" else 2
+    gain = 4.0 if name == "g4" else None
+    steps = 2 if name == "c5" else 3
     g = torch.Generator().manual_seed(n)
     x = torch.rand(n, 3, args.img, args.img, generator=g)
     images = torch.cat([x, x])[None].to(device)
     no_reloc, reloc = list(range(n)), list(range(n, 2 * n))
     dtype = (f"bf16, global {'q.k^T' if args.c5_fp8 == 'qk' else 'q.k^T + P.V'} fp8-e4m3" if fp8 else "bf16")
-    out = {"name": name, "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px" + (
-        " (BASELINE C5, fp8 global attention)" if fp8 else " (north-star 64-view workload)"),
+    what = {"n64": " (north-star 64-view workload)", "c5": " (BASELINE C5, fp8 global attention)",
+            "g4": " at qk-norm gain 4 (trained-like q_norm / k_norm weights: every one x 4)"}.get(name, "")
+    out = {"name": name, "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px" + what,
            "unit": "views/s", "dtype": dtype, "views": n, "frames": 2 * n, "steps": steps, "warmup": 1}
+    if gain is not None:
+        out["qk_gain"] = gain
 
     def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
@@ -619,6 +627,8 @@ def extra_config(model, device, args, world, name):
     try:
         if fp8:
             model.aggregator.set_fp8_global(True, fp8_v=args.c5_fp8 == "qkv")
+        if gain is not None:
+            scale_qk_gain(model, gain)
         step()
         barrier()
         ops.TIMER = ops.KernelTimer()
@@ -636,6 +646,8 @@ def extra_config(model, device, args, world, name):
         ops.TIMER = None
         if fp8:
             model.aggregator.set_fp8_global(False)
+        if gain is not None:
+            scale_qk_gain(model, 1.0 / gain)  # a power of two: the weights come back exactly
     dt_t = torch.tensor([dt], device=device)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
