@@ -730,3 +730,36 @@ def test_global_attention_value_window(ops, vscale):
         err = _rel(res[qnm][1][rows].float(), ref)
         print(f"rel err vs fp64 (query_norm_max {qnm:.1f}): {err:.2e}")
         assert err < 1.5e-2  # c*q in bf16 at |s| ~ 300: as test_global_attention_qk_gain
+
+
+@pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm_seg"])
+def test_global_attention_key_split_boxes(ops, tail):
+    """The data-derived bounds on the key-split path (attention_partials, one box / norm / value box
+    instance per key chunk): a G = 8 rank's query slice (5,496 rows) at qk-gain 4 against the C3
+    keys clustered around one direction, with (query_norm_max set) and without the boxes, each
+    against fp64.  ``tail``: the chunks' ragged tails readable (padded key buffer), so the chunks
+    may take the hand-scheduled _SEG sweep."""
+    g, L = 4.0, 32 * P
+    lq = 4 * P
+    gen = torch.Generator(device=DEV).manual_seed(404)
+    u = torch.randn(1, H, D, device=DEV, generator=gen)
+    q, qn = _qk_gain(lq, g, gen)
+    k, kb = _qk_gain_shared(L, g, gen, u, 0.05)
+    v = torch.randn(L, C, device=DEV, generator=gen).bfloat16()
+    if tail:
+        k, v = _padded(k), _padded(v)
+    parts = ops.key_split_parts(dtype=torch.bfloat16, batch=1, lq=lq, heads=H, l0=L, l1=0, mask_mode=0)
+    assert parts > 1
+    rows = _sample_rows(lq, 128, 404).to(DEV)
+    ref = _ref_rows(q[rows], k[:L], v[:L], D ** -0.5)
+    outs = []
+    for qnm in (0.0, qn):
+        o = torch.empty(lq, C, device=DEV, dtype=torch.bfloat16)
+        ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0,
+                      key_norm_max=kb, query_norm_max=qnm, tail_readable=tail)
+        torch.cuda.synchronize()
+        err = _rel(o[rows].float(), ref)
+        print(f"key split S={parts}, tail {tail}, query_norm_max {qnm:.1f}: rel {err:.2e}")
+        assert err < 1e-2
+        outs.append(o)
+    assert _rel(outs[1].float(), outs[0].float()) < 1e-2
