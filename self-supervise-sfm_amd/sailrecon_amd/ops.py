@@ -412,7 +412,7 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     _launch_attention(d, q, tag, key_norm_max, 4.0 * batch * heads * lq * (l0 + l1) * head_dim,
                       q.element_size() * heads * head_dim *
                       (2 * batch * lq + 2 * ((l0 if k0_bstride == 0 else batch * l0) + batch * l1)),
-                      query_norm_max=query_norm_max, k0=k0, k1=k1)
+                      query_norm_max=query_norm_max)
 
 
 def _set_sweep_stats(d: AttnDesc, stats: Optional[Tensor]) -> None:
@@ -449,7 +449,7 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
                        q_bstride=0, l0=p["l0"], k0_bstride=0, lse=p.get("lse"))
         d.key_norm_max = float(p["key_norm_max"])
         _set_sweep_stats(d, p.get("sweep_stats"))
-        _attach_key_box(d, p["k0"], None, p.get("query_norm_max", 0.0), "attn_key_box" + str(len(descs)))
+        _attach_key_box(d, p["k0"].device, p.get("query_norm_max", 0.0), "attn_key_box" + str(len(descs)))
         descs.append(d)
         flops += 4.0 * heads * p["lq"] * p["l0"] * head_dim
         nbytes += p["q"].element_size() * heads * head_dim * (2 * p["lq"] + 2 * p["l0"])
@@ -466,12 +466,11 @@ _KEY_BOX = os.environ.get("SR_ATTN_KEY_BOX", "auto")  # auto | 1 (always) | 0 (n
 _FIX_HI = 64.0  # sr_attn.hip FIX_HI: the fixed offset's headroom (log2 units)
 
 
-def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_max: float, name: str) -> None:
+def _attach_key_box(d: AttnDesc, device, query_norm_max: float, name: str) -> None:
     """Set d.key_box, d.value_box and d.key_bound (the keys' actual max |k|^2, which tightens the
     static key_norm_max) when the 2-norm score bound scale*log2(e)*|q|*|k| exceeds the sweep's
     default headroom FIX_HI: sr_attention_key_box over each key and value segment into a
     per-stream workspace, instances as sr_attention_bound_floats' (k0's, then k1's)."""
-    del k1
     if _KEY_BOX == "0" or not (d.key_norm_max > 0.0) or d.head_dim != 64 or d.heads > 32:
         return
     if _KEY_BOX != "1" and not (query_norm_max > 0.0 and
@@ -480,14 +479,14 @@ def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_ma
     n0 = 1 if d.k0_bstride == 0 else d.batch
     n1 = (1 if d.k1_bstride == 0 else d.batch) if d.l1 > 0 else 0
     per = d.heads * 128
-    ws = _train_ws(k0.device, name, (2 * per + d.heads) * (n0 + n1))
+    ws = _train_ws(device, name, (2 * per + d.heads) * (n0 + n1))
     lib = _lib.load()
-    stream = _stream(k0)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     segs = [(d.k0, d.ldk0, d.v0, d.ldv0, d.l0, d.k0_bstride, n0, 0)]
     if n1:
         segs.append((d.k1, d.ldk1, d.v1, d.ldv1, d.l1, d.k1_bstride, n1, n0 * per))
     vb, nb = (n0 + n1) * per, 2 * (n0 + n1) * per
-    sc = _train_ws(k0.device, "attn_box_scratch",
+    sc = _train_ws(device, "attn_box_scratch",
                    max(lib.sr_attention_key_box_scratch(g[4], g[6], d.heads) for g in segs))
     for k, ldk, v, ldv, rows, bstride, n, off in segs:
         check(lib.sr_attention_key_box(stream, k, ldk, rows, bstride, n, d.heads, _p(ws[off:]),
@@ -498,12 +497,10 @@ def _attach_key_box(d: AttnDesc, k0: Tensor, k1: Optional[Tensor], query_norm_ma
 
 
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,
-                      nbytes: float, query_norm_max: float = 0.0, k0: Optional[Tensor] = None,
-                      k1: Optional[Tensor] = None) -> None:
+                      nbytes: float, query_norm_max: float = 0.0) -> None:
     if q.dtype == torch.bfloat16 and _ATTN_BOUND and key_norm_max > 0.0:
         d.key_norm_max = float(key_norm_max)
-        if k0 is not None:
-            _attach_key_box(d, k0, k1, query_norm_max, "attn_key_box")
+        _attach_key_box(d, q.device, query_norm_max, "attn_key_box")
     elif q.dtype == torch.bfloat16 and _ATTN_BOUND:
         nb = _lib.load().sr_attention_bound_floats(ctypes.byref(d))
         if nb > 0:
@@ -546,7 +543,7 @@ def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_p
         d.tail_rows_readable = 64
     _launch_attention(d, q, tag, key_norm_max, 4.0 * heads * lq * l0 * head_dim,
                       q.element_size() * heads * head_dim * (lq + 2 * parts * lq + 2 * l0),
-                      query_norm_max=query_norm_max, k0=k0)
+                      query_norm_max=query_norm_max)
 
 
 def attn_merge(o_a: Tensor, lse_a: Tensor, o_b: Tensor, lse_b: Tensor, out: Tensor, *, heads: int, head_dim: int,
