@@ -77,7 +77,9 @@ enum sr_tuning_key {
   SR_TUNE_RLN_WIDE = 12,    /* sr_residual_layernorm variant bits: 1 16-B lanes, 2 two rows per wave, 4 nt x stores (0) */
   SR_TUNE_GEMM_TAIL = 13,   /* 1: a 256x256 GEMM whose last workgroup round would run few tiles computes
                                the rows past its last whole round on the 128x128 kernel (second launch)  (1) */
-  SR_TUNE_COUNT = 14
+  SR_TUNE_GEMM_PERSIST = 14,/* 1: the 256x256 GEMM as one persistent workgroup per CU walking its tiles,
+                               the next tile's first K stage staged under the current epilogue   default 0 */
+  SR_TUNE_COUNT = 15
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -625,13 +625,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
 constexpr int BIG = 256;
 constexpr int STAGE_BIG = 2 * BIG * ROWB;  // 64 KiB
 
-// One output tile over k-tiles [kb, ke).
-template <int EPI>
-__device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// Output tile -> (m0, n0): column-major inside groups of group_m row tiles, else row-major.
+__device__ __forceinline__ void tile_origin(const GemmArgs& g, int tile, int& m0, int& n0) {
   const int ntn = g.N / BIG, ntm = (g.M + BIG - 1) / BIG;
   int tm, tn;
-  if (g.group_m > 1) {  // column-major inside groups of group_m row tiles
+  if (g.group_m > 1) {
     const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
     const int gm = min(g.group_m, ntm - first), r = tile - grp * per;
     tm = first + r % gm;
@@ -640,7 +638,20 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
     tm = tile / ntn;
     tn = tile - tm * ntn;
   }
-  int m0 = tm * BIG, n0 = tn * BIG;
+  m0 = tm * BIG;
+  n0 = tn * BIG;
+}
+
+// One output tile over k-tiles [kb, ke).  ``staged``: stage kb already issued (by the previous
+// tile of a persistent workgroup).  ``next_tile`` >= 0 (persistent walk, kb = 0): this tile's
+// epilogue first issues the next tile's stage 0 into LDS buffer 0 (free once every wave is past
+// the k-loop), so that its DMA overlaps the epilogue; returns whether it did.
+template <int EPI>
+__device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke, bool staged = false,
+                                             int next_tile = -1) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int m0, n0;
+  tile_origin(g, tile, m0, n0);
 
   // LDS-DMA sources: wave w, instruction i fills stage rows (w*8 + i)*8 .. +8 of the 512-row
   // stage: waves 0-3 stage A rows m0 + 64w + 8i + lane/8, waves 4-7 W rows n0 + 64(w-4) + 8i +
@@ -650,22 +661,20 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const bool a_wave = wave_u < 4;
   const int64_t ld_b = a_wave ? g.lda_b : g.ldw_b;
-  // first staged row of this wave (A rows clamped to M - 1 for a ragged last row tile)
-  const int brow0 = a_wave ? min(m0 + wave_u * 64, g.M - 1) : n0 + (wave_u - 4) * 64;
-  const char* const sbase = (a_wave ? g.A : g.W) + (int64_t)brow0 * ld_b;
-  const bool ragged = a_wave && m0 + BIG > g.M;
-  const int rlim = g.M - 1 - brow0;  // ragged: last valid row relative to brow0
   const uint32_t voA = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (lane >> 4)) << 4));
   const uint32_t voB = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
   const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
-  // pieces [i0, i1) of stage kt (one wave-uniform branch per call)
-  auto dma_pieces = [&](int kt, int i0, int i1) {
+  // pieces [i0, i1) of stage kt of the tile at (m0_, n0_) (one wave-uniform branch per call):
+  // this wave's first staged row (A rows clamped to M - 1 for a ragged last row tile)
+  auto dma_tile = [&](int m0_, int n0_, int kt, int i0, int i1) {
+    const int brow0 = a_wave ? min(m0_ + wave_u * 64, g.M - 1) : n0_ + (wave_u - 4) * 64;
+    const char* sp = (a_wave ? g.A : g.W) + (int64_t)brow0 * ld_b + (int64_t)kt * ROWB;
     const uint32_t base = dst0 + (kt & 1) * STAGE_BIG;
-    const char* sp = sbase + (int64_t)kt * ROWB;
-    if (!ragged) {
+    if (!(a_wave && m0_ + BIG > g.M)) {
 #pragma unroll
       for (int i = i0; i < i1; ++i) sr::dma16_s(sp + (int64_t)i * 8 * ld_b, (i & 1) ? voB : voA, base + i * 1024);
     } else {
+      const int rlim = g.M - 1 - brow0;  // last valid row relative to brow0
 #pragma unroll
       for (int i = i0; i < i1; ++i) {
         const int r = min(i * 8 + (lane >> 3), rlim);
@@ -674,7 +683,17 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
       }
     }
   };
+  auto dma_pieces = [&](int kt, int i0, int i1) { dma_tile(m0, n0, kt, i0, i1); };
   auto stage = [&](int kt) { dma_pieces(kt, 0, 8); };
+  // the next tile's stage 0 into buffer 0 once every wave is done with this tile's LDS
+  auto prefetch_next = [&]() -> bool {
+    if (next_tile < 0) return false;
+    int nm0, nn0;
+    tile_origin(g, next_tile, nm0, nn0);
+    sr::barrier_raw();
+    dma_tile(nm0, nn0, 0, 0, 8);
+    return true;
+  };
 
   const int wr = wave >> 2, wc = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
@@ -691,7 +710,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   {
-    stage(kb);
+    if (!staged) stage(kb);
     for (int kt = kb; kt < ke; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
       sr::barrier_raw();                                  // ... every wave's; all done with kt-1
@@ -751,18 +770,27 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
   }
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
     if (m0 + BIG <= g.M && !g.lds_epi) {
+      const bool pf = prefetch_next();
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-      return;
+      return pf;
     }
   }
   if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
     if (m0 + BIG <= g.M && !g.lds_epi && !g.ep.aux) {
+      const bool pf = prefetch_next();
       bias_full<EPI>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-      return;
+      return pf;
     }
   }
-  if (g.lds_epi) epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
-  else epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+  if (g.lds_epi) {
+    // the LDS-staged epilogue uses both buffers: the next tile's stage goes out after it (every
+    // wave's copy-out reads are complete once it stores their data)
+    epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
+    return prefetch_next();
+  }
+  const bool pf = prefetch_next();
+  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+  return pf;
 }
 
 template <int EPI>
@@ -770,6 +798,21 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
   gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles);
+}
+
+// Persistent form (SR_TUNE_GEMM_PERSIST): one workgroup per CU walks tiles t = blockIdx.x + i *
+// gridDim.x (gridDim.x a multiple of 8, so every tile of a workgroup sits on its XCD's contiguous
+// xcd_remap range, as in the one-tile-per-workgroup launch); each tile's epilogue overlaps the
+// next tile's first K stage, and no workgroup is relaunched between tiles.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_persist_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
+  bool staged = false;
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int nxt = t + (int)gridDim.x < nt ? sr::xcd_remap(t + gridDim.x, nt) : -1;
+    staged = gemm256_tile<EPI>(g, smem, sr::xcd_remap(t, nt), 0, g.ktiles, staged, nxt);
+  }
 }
 
 // Up to 4 independent 256x256 GEMMs of one epilogue kind in ONE launch (sr_gemm_group): problem
@@ -807,12 +850,23 @@ static int tile_group_m(int N) {
   return g >= 0 ? g : (N >= 3072 ? 4 : 0);
 }
 
+// the persistent form applies (SR_TUNE_GEMM_PERSIST, more tiles than one round)
+static bool use_persist(int epi, long nwg) {
+  const int cus = sr::cu_count() / 8 * 8;
+  return sr::tune(SR_TUNE_GEMM_PERSIST) && epi != SR_EPI_PATCH && cus >= 8 && nwg > cus;
+}
+
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
   a.group_m = tile_group_m(a.N);
-  const int grid = nwg;
-  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
+  const int cus = sr::cu_count() / 8 * 8;
+  if (use_persist(EPI, nwg)) {
+    hipLaunchKernelGGL((gemm256_persist_kernel<EPI>), dim3(cus), dim3(512), 0, s, a);
+    sr::note_kernel("gemm256_persist_kernel<%d>", EPI);
+    return sr::check_launch("sr_gemm(256, persistent)");
+  }
+  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
   sr::note_kernel("gemm256_kernel<%d>", EPI);
   return sr::check_launch("sr_gemm(256)");
 }
@@ -876,7 +930,8 @@ int launch256_tail(GemmArgs a, hipStream_t s) {
       int rc = launch256<EPI>(head, s);
       if (rc != SR_OK) return rc;
       rc = launch<bf16, EPI>(row_slice(a, EPI, main_rows, rest), s);
-      sr::note_kernel("gemm256_kernel<%d>", EPI);  // the launch the time goes to
+      // the launch the time goes to
+      sr::note_kernel(use_persist(EPI, whole) ? "gemm256_persist_kernel<%d>" : "gemm256_kernel<%d>", EPI);
       return rc;
     }
   }

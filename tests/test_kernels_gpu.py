@@ -550,6 +550,51 @@ def test_gemm_tail_split(ops, epi_name, M, N):
     assert rel(out1.float(), out0.float()) < 1e-6
 
 
+@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])
+@pytest.mark.parametrize("M,N,K", [(43 * 256 - 100, 3072, 1024), (87936, 1024, 1024), (2 * 5496, 4096, 1024),
+                                   (43968, 1024, 4096)])
+def test_gemm_persistent(ops, epi_name, M, N, K):
+    """SR_GEMM_PERSIST: the 256x256 GEMM as one persistent workgroup per CU, each tile's epilogue
+    overlapping the next tile's first K stage (register and LDS-staged epilogues, ragged last row
+    tile, with and without the tail split).  Per output tile the same MFMA sequence as the
+    one-tile-per-workgroup kernel: bit-identical."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    L = _lib()
+    epi = getattr(L, "SR_EPI_" + epi_name)
+    C = 1024
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) / 32).bfloat16()
+    kw = dict(bias=torch.randn(N, device=DEV, generator=g))
+    if epi_name == "QKV":
+        if N % C or N > 3 * C:
+            pytest.skip("QKV needs whole q|k|v blocks")
+        rope = RotaryPositionEmbedding2D(100).tables(64, 40, DEV)
+        qn = [torch.randn(64, device=DEV, generator=g) for _ in range(4)]
+        kw["qkv"] = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
+                         rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37,
+                         pos_row_base=11, col_offset=3 * C - N)
+    if epi_name == "BIAS_RESID":
+        kw["gamma"] = torch.randn(N, device=DEV, generator=g)
+    if epi_name == "GELU_BWD":
+        kw = dict(aux=torch.randn(M, N, device=DEV, generator=g).bfloat16())
+    if epi_name in ("BIAS_RESID", "F32"):
+        x0 = torch.randn(M, N, device=DEV, generator=g)
+        outs = [x0.clone() for _ in range(4)]
+    else:
+        outs = [torch.zeros(M, N, device=DEV, dtype=torch.bfloat16) for _ in range(4)]
+    names = []
+    for i, (persist, tail) in enumerate(((0, 0), (1, 0), (0, 1), (1, 1))):
+        with ops.tuning(SR_GEMM_PERSIST=persist, SR_GEMM_TAIL=tail):
+            ops.gemm(a, w, outs[i], epi, splits=1, **kw)
+            names.append(ops.last_kernel())
+    torch.cuda.synchronize()
+    print(f"{epi_name} M={M} N={N} K={K}: {names}")
+    assert names[1].startswith("gemm256_persist_kernel") and names[0].startswith("gemm256_kernel"), names
+    assert torch.equal(outs[1], outs[0])
+    assert torch.equal(outs[3], outs[2])
+
+
 def test_merge_with_empty_partial(ops):
     """a merge partial with LSE = -inf (no key of that part attended) contributes
     nothing -- in the attention's merge-in epilogue (sr_attn_desc.merge_o) and in sr_attn_merge_n
