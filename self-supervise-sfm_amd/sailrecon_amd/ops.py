@@ -463,18 +463,21 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
 
 
 _KEY_BOX = os.environ.get("SR_ATTN_KEY_BOX", "auto")  # auto | 1 (always) | 0 (never)
-_FIX_HI = 64.0  # sr_attn.hip FIX_HI: the fixed offset's headroom (log2 units)
+# sr_attn.hip's default window: P <= 2^FIX_HI, the row's max P >= 2^-FIX_LO.  With every score in
+# [-qs, qs] and qs <= (FIX_HI + FIX_LO) / 2 = 87 the offset m = max(0, qs - FIX_HI) always fits it
+# (the row max >= -qs >= m - FIX_LO), so the boxes only pay above that
+_BOX_MIN_BOUND = (64.0 + 110.0) / 2
 
 
 def _attach_key_box(d: AttnDesc, device, query_norm_max: float, name: str) -> None:
     """Set d.key_box, d.value_box and d.key_bound (the keys' actual max |k|^2, which tightens the
-    static key_norm_max) when the 2-norm score bound scale*log2(e)*|q|*|k| exceeds the sweep's
-    default headroom FIX_HI: sr_attention_key_box over each key and value segment into a
+    static key_norm_max) when the 2-norm score bound scale*log2(e)*|q|*|k| exceeds 87, above which the
+    default window can miss: sr_attention_key_box over each key and value segment into a
     per-stream workspace, instances as sr_attention_bound_floats' (k0's, then k1's)."""
     if _KEY_BOX == "0" or not (d.key_norm_max > 0.0) or d.head_dim != 64 or d.heads > 32:
         return
     if _KEY_BOX != "1" and not (query_norm_max > 0.0 and
-                                d.scale * 1.4426950408889634 * query_norm_max * d.key_norm_max > _FIX_HI):
+                                d.scale * 1.4426950408889634 * query_norm_max * d.key_norm_max > _BOX_MIN_BOUND):
         return
     n0 = 1 if d.k0_bstride == 0 else d.batch
     n1 = (1 if d.k1_bstride == 0 else d.batch) if d.l1 > 0 else 0
