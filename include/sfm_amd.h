@@ -403,7 +403,7 @@ int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B,
 /* Column sums (bias / token / positional-embedding grads):
  *   out[c] = (accumulate ? out[c] : 0) + scale * sum_{r<M} X[r*ldx + c],  c < N (N % 4 == 0).
  * X is `dtype`; two deterministic passes through `workspace` (>= 1024 * N floats, or
- * ceil(M / 32) * N if smaller). */
+ * ceil(M / 16) * N if smaller). */
 int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
               float scale, float* workspace);
 

@@ -305,8 +305,19 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
   const int qi = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int64_t c = ((int64_t)blockIdx.x * 16 + qi) * 4;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (c < N)
-    for (int z = g; z < chunks; z += 16) s += *(const f32x4*)(part + (int64_t)z * N + c);
+  if (c < N) {
+    // four chunks in flight per step (independent sums, combined in a fixed order)
+    f32x4 s1 = s, s2 = s, s3 = s;
+    int z = g;
+    for (; z + 48 < chunks; z += 64) {
+      s += *(const f32x4*)(part + (int64_t)z * N + c);
+      s1 += *(const f32x4*)(part + (int64_t)(z + 16) * N + c);
+      s2 += *(const f32x4*)(part + (int64_t)(z + 32) * N + c);
+      s3 += *(const f32x4*)(part + (int64_t)(z + 48) * N + c);
+    }
+    for (; z < chunks; z += 16) s += *(const f32x4*)(part + (int64_t)z * N + c);
+    s = (s + s1) + (s2 + s3);
+  }
   red[g][qi] = s;
   __syncthreads();
   for (int w = 8; w > 0; w >>= 1) {
@@ -321,9 +332,9 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 
 int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
                   float scale, float* ws) {
-  // ~1024 partial workgroups of >= 32 rows, then the parallel final reduction
+  // ~1024 partial workgroups of >= 16 rows, then the parallel final reduction
   const int64_t gx = (N / 4 + 255) / 256;
-  int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 31) / 32));
+  int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 15) / 16));
   const int rpc = (M + chunks - 1) / chunks;
   chunks = (M + rpc - 1) / rpc;
   if (dtype == SR_BF16)
