@@ -413,12 +413,14 @@ int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, 
  *   dx  += rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w (w NULL: 1)
  *   dxb[r] = bf16(updated dx row)  (if dxb: the next GEMM operand)
  *   dw  += sum_r dy * xhat,  db += sum_r dy   (if dw / db; accumulate)
- * dy is `dtype` [rows][lddy].  `workspace` >= 3 * 1024 * cols floats.
+ *   dx_colsum[c] = sum_r updated dx[r][c]     (if dx_colsum: assigned; needs dw / db, cols <= 2048 --
+ *                  the bias grad of the residual branch that wrote x, without a second pass over dx)
+ * dy is `dtype` [rows][lddy].  `workspace` >= 4 * 1024 * cols floats (3 * without dx_colsum).
  * cols in {128,256,384,512,768,1024,1536,2048,4096}.  Rows of one call must map to distinct
  * dx rows. */
 int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx, const int32_t* rowmap,
                      const void* dy, int64_t lddy, const float* w, float eps, float* dx, int64_t lddx, void* dxb,
-                     int64_t lddxb, float* dw, float* db, int rows, int cols, float* workspace);
+                     int64_t lddxb, float* dw, float* db, int rows, int cols, float* workspace, float* dx_colsum);
 
 /* qk-norm + 2-D RoPE backward (attention.py:72-82, rope.py:165-207), the inverse of the
  * SR_EPI_QKV epilogue: raw = the saved pre-norm q|k|v (bf16, aux of the forward),

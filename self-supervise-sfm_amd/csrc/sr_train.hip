@@ -360,12 +360,15 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
                                                             const TD* __restrict__ dy, int64_t lddy,
                                                             const float* __restrict__ w, float eps, float* dx,
                                                             int64_t lddx, bf16* dxb, int64_t lddxb, int want_params,
-                                                            float* part, int rows) {
+                                                            int want_sum, float* part, int rows) {
   constexpr int NV = NPL / VEC;
   constexpr int COLS = NPL * 64;
+  // the column sum of the updated dx rows rides along as a third partial (cols <= 2048: the
+  // register file of the 4,096-column form has no room for it)
+  constexpr bool CAN_SUM = NPL <= 32;
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  float wv[NPL], dws[NPL], dbs[NPL];
+  float wv[NPL], dws[NPL], dbs[NPL], dss[CAN_SUM ? NPL : 1];
 #pragma unroll
   for (int i = 0; i < NV; ++i)
 #pragma unroll
@@ -373,6 +376,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
       wv[i * VEC + j] = w ? w[(i * 64 + lane) * VEC + j] : 1.f;
       dws[i * VEC + j] = 0.f;
       dbs[i * VEC + j] = 0.f;
+      if constexpr (CAN_SUM) dss[i * VEC + j] = 0.f;
     }
   // Two rows per wave per iteration, and the dx each adds into loaded with x and dy: all loads of
   // both rows are in flight before the first reduction (one memory latency per two rows, not two
@@ -423,8 +427,11 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
       float* dp = dx + xr * lddx + col;
       float o[VEC];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j)
+      for (int j = 0; j < VEC; ++j) {
         o[j] = (NPL <= 32 ? a[i * VEC + j] : dp[j]) + rstd * (g[i * VEC + j] - mg - v[i * VEC + j] * mgx);
+        if constexpr (CAN_SUM)
+          if (want_sum) dss[i * VEC + j] += o[j];
+      }
       if constexpr (VEC == 4) {
         *(float4*)dp = make_float4(o[0], o[1], o[2], o[3]);
         if (dxb) *(bf16x4*)(dxb + (int64_t)row * lddxb + col) = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
@@ -456,8 +463,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
     finish(xa, row, va, ga, aa);
     if (has_b) finish(xb, rowb, vb, gb, ab);
   }
-  if (want_params) {
-    float* pw = part + (int64_t)gw * 2 * COLS;
+  if (want_params) {  // [nw][2 or 3][COLS]: dw, db (, dx) partials
+    const int np = (CAN_SUM && want_sum) ? 3 : 2;
+    float* pw = part + (int64_t)gw * np * COLS;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
 #pragma unroll
@@ -465,6 +473,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
         const int col = (i * 64 + lane) * VEC + j;
         pw[col] = dws[i * VEC + j];
         pw[COLS + col] = dbs[i * VEC + j];
+        if constexpr (CAN_SUM)
+          if (want_sum) pw[2 * COLS + col] = dss[i * VEC + j];
       }
   }
 }
@@ -948,21 +958,28 @@ extern "C" int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t l
 
 extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx, const int32_t* rowmap,
                                 const void* dy, int64_t lddy, const float* w, float eps, float* dx, int64_t lddx,
-                                void* dxb, int64_t lddxb, float* dw, float* db, int rows, int cols, float* workspace) {
+                                void* dxb, int64_t lddxb, float* dw, float* db, int rows, int cols, float* workspace,
+                                float* dx_colsum) {
   SR_CHECK(x && dy && dx && rows > 0, SR_EINVAL, "sr_layernorm_bwd: null pointer / no rows");
   SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_layernorm_bwd: bad dtype");
   SR_CHECK(!(dw || db) || (dw && db && workspace), SR_EINVAL, "sr_layernorm_bwd: dw and db need workspace");
+  SR_CHECK(!dx_colsum || (dw && cols <= 2048), SR_EINVAL,
+           "sr_layernorm_bwd: dx_colsum needs dw / db (their workspace) and cols <= 2048");
   hipStream_t s = (hipStream_t)stream;
   const int want = dw != nullptr;
+  const int want_sum = dx_colsum != nullptr;
+  const int np = want_sum ? 3 : 2;
   const int wgs = std::min(LNB_WGS, (rows + 3) / 4);
 #define LNB_CASE(C, V)                                                                                          \
   case C:                                                                                                       \
     if (dtype == SR_BF16)                                                                                       \
       hipLaunchKernelGGL((layernorm_bwd_kernel<C / 64, V, bf16>), dim3(wgs), dim3(256), 0, s, x, ldx, rowmap,  \
-                         (const bf16*)dy, lddy, w, eps, dx, lddx, (bf16*)dxb, lddxb, want, workspace, rows);     \
+                         (const bf16*)dy, lddy, w, eps, dx, lddx, (bf16*)dxb, lddxb, want, want_sum, workspace, \
+                         rows);                                                                                \
     else                                                                                                        \
       hipLaunchKernelGGL((layernorm_bwd_kernel<C / 64, V, float>), dim3(wgs), dim3(256), 0, s, x, ldx, rowmap, \
-                         (const float*)dy, lddy, w, eps, dx, lddx, (bf16*)dxb, lddxb, want, workspace, rows);    \
+                         (const float*)dy, lddy, w, eps, dx, lddx, (bf16*)dxb, lddxb, want, want_sum, workspace, \
+                         rows);                                                                                \
     break;
   switch (cols) {
     LNB_CASE(128, 2)
@@ -979,12 +996,16 @@ extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, i
       return SR_EUNSUPPORTED;
   }
 #undef LNB_CASE
-  if (want) {  // partial rows [wgs*4][2*cols] -> dw | db
-    float* tail = workspace + (int64_t)wgs * 4 * 2 * cols;
-    int rc = colsum_launch(s, SR_F32, workspace, 2 * cols, wgs * 4, cols, dw, 1, 1.f, tail);
+  if (want) {  // partial rows [wgs*4][np*cols] -> dw | db (| dx_colsum, assigned)
+    float* tail = workspace + (int64_t)wgs * 4 * np * cols;
+    int rc = colsum_launch(s, SR_F32, workspace, np * cols, wgs * 4, cols, dw, 1, 1.f, tail);
     if (rc) return rc;
-    rc = colsum_launch(s, SR_F32, workspace + cols, 2 * cols, wgs * 4, cols, db, 1, 1.f, tail);
+    rc = colsum_launch(s, SR_F32, workspace + cols, np * cols, wgs * 4, cols, db, 1, 1.f, tail);
     if (rc) return rc;
+    if (want_sum) {
+      rc = colsum_launch(s, SR_F32, workspace + 2 * cols, np * cols, wgs * 4, cols, dx_colsum, 0, 1.f, tail);
+      if (rc) return rc;
+    }
   }
   return sr::check_launch("sr_layernorm_bwd");
 }

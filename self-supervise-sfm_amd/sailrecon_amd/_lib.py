@@ -147,7 +147,7 @@ _PROTOS = {
                              _i32, _vp]),
     "sr_colsum": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i32, _f32, _vp]),
     "sr_layernorm_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _f32, _vp, _i64, _vp, _i64, _vp, _vp,
-                                _i32, _i32, _vp]),
+                                _i32, _i32, _vp, _vp]),
     "sr_qk_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
     "sr_attention_key_box": (_i32, [_vp, _vp, _i64, _i32, _i64, _i32, _i32, _vp, _vp, _vp]),
     "sr_attention_key_box_scratch": (_i32, [_i32, _i32, _i32]),

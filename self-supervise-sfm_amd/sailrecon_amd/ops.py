@@ -1038,14 +1038,20 @@ def colsum(x: Tensor, out: Tensor, *, rows: Optional[int] = None, cols: Optional
 
 def layernorm_bwd(x: Tensor, dy: Tensor, w: Optional[Tensor], eps: float, dx: Tensor, *,
                   dxb: Optional[Tensor] = None, dw: Optional[Tensor] = None, db: Optional[Tensor] = None,
-                  rowmap: Optional[Tensor] = None, rows: Optional[int] = None) -> None:
-    """dx[rows] += LayerNorm backward (see sr_layernorm_bwd); dxb = bf16 copy of the updated rows."""
+                  rowmap: Optional[Tensor] = None, rows: Optional[int] = None,
+                  dx_sum: Optional[Tensor] = None) -> None:
+    """dx[rows] += LayerNorm backward (see sr_layernorm_bwd); dxb = bf16 copy of the updated rows;
+    dx_sum (fp32 [cols], with dw / db, cols <= 2048) = the column sum of the updated rows."""
     n = dy.shape[0] if rows is None else rows
     cols = x.shape[1]
-    ws = _train_ws(x.device, "lnbwd", 3 * 1024 * cols) if dw is not None else None
+    if dx_sum is not None and (dw is None or dx_sum.dtype != torch.float32 or dx_sum.numel() < cols or
+                               not dx_sum.is_contiguous()):
+        raise ValueError("layernorm_bwd: dx_sum needs dw / db and a contiguous fp32 [cols] output")
+    ws = _train_ws(x.device, "lnbwd", 4 * 1024 * cols) if dw is not None else None
     rc = _lib.load().sr_layernorm_bwd(_stream(x), dtype_code(dy.dtype), _p(x), _rowmajor(x, "x"), _p(rowmap), _p(dy),
                                       _rowmajor(dy, "dy"), _p(w), eps, _p(dx), _rowmajor(dx, "dx"), _p(dxb),
-                                      0 if dxb is None else _rowmajor(dxb, "dxb"), _p(dw), _p(db), n, cols, _p(ws))
+                                      0 if dxb is None else _rowmajor(dxb, "dxb"), _p(dw), _p(db), n, cols, _p(ws),
+                                      _p(dx_sum))
     check(rc, "sr_layernorm_bwd")
 
 

@@ -174,13 +174,19 @@ class BwdScratch:
         return self.ws.get(name, rows, cols, dtype, device)
 
 
+def _resid_wants_sum(bias: Optional[Tensor], g_bias: Optional[Tensor], g_gamma: Optional[Tensor]) -> bool:
+    return g_bias is not None or (g_gamma is not None and bias is not None)
+
+
 def _resid_param_grads(dx: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor], g_bias: Optional[Tensor],
-                       g_gamma: Optional[Tensor], tmp: Tensor) -> None:
+                       g_gamma: Optional[Tensor], tmp: Tensor, summed: bool = False) -> None:
     """Bias and LayerScale-gamma grads of ``x += gamma * (a W^T + b)`` from colsum(dx):
-    db += gamma * s, dgamma += b * s (the <W, G> part comes from the wgrad row dots)."""
-    if g_bias is None and (g_gamma is None or bias is None):
+    db += gamma * s, dgamma += b * s (the <W, G> part comes from the wgrad row dots).
+    ``summed``: tmp already holds colsum(dx) (layernorm_bwd's dx_sum)."""
+    if not _resid_wants_sum(bias, g_bias, g_gamma):
         return
-    ops.colsum(dx, tmp)
+    if not summed:
+        ops.colsum(dx, tmp)
     if g_bias is not None:
         if gamma is None:
             raise RuntimeError("bias grad without gamma")
@@ -221,14 +227,17 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
     dxn = sc.get("dxn", R, C, torch.float32, dev)
     ops.gemm(dU, bp.wt_fc1, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
     wgrad(dU, tape.xn2, g.w_fc1, db=g.b_fc1)
-    ops.layernorm_bwd(tape.x1, dxn, pb.ln2_w, pb.eps, dx, dxb=dxb, dw=g.ln2_w, db=g.ln2_b)
+    # (LN2's backward also sums the updated dx over the rows: proj's bias / gamma grads below)
+    fused_sum = g.ln2_w is not None and C <= 2048 and _resid_wants_sum(bp.b_proj, g.b_proj, g.g1)
+    ops.layernorm_bwd(tape.x1, dxn, pb.ln2_w, pb.eps, dx, dxb=dxb, dw=g.ln2_w, db=g.ln2_b,
+                      dx_sum=tmp[:C] if fused_sum else None)
 
     # ---- attention: x1 = x0 + g1 * proj(attn(qk(qkv(LN1(x0)))))
     dO = sc.get("dO", R, C, dt, dev)
     ops.gemm(a_op, bp.wt_proj, dO, _lib.SR_EPI_BIAS, tag=tag + ".dgrad")
     wgrad(a_op, tape.o, g.w_proj, rowscale=pb.g1, wdot=bp.w_proj if g.g1 is not None else None,
           rowdot=g.g1 if g.g1 is not None else None)
-    _resid_param_grads(dx, bp.b_proj, pb.g1, g.b_proj, g.g1, tmp[:C])
+    _resid_param_grads(dx, bp.b_proj, pb.g1, g.b_proj, g.g1, tmp[:C], summed=fused_sum)
     dqkv = sc.get("dqkv", R, 3 * C, torch.float32, dev)
     attend_bwd(tape, dO, dqkv)
     if bf:

@@ -152,11 +152,14 @@ def test_layernorm_bwd(ops, cols, dy_dtype):
     dxb = torch.empty(R, cols, device=DEV, dtype=torch.bfloat16)
     dw = torch.zeros(cols, device=DEV)
     db = torch.zeros(cols, device=DEV)
-    ops.layernorm_bwd(x, dy, w, 1e-5, dx, dxb=dxb, dw=dw, db=db)
+    dsum = torch.full((cols,), float("nan"), device=DEV) if cols <= 2048 else None
+    ops.layernorm_bwd(x, dy, w, 1e-5, dx, dxb=dxb, dw=dw, db=db, dx_sum=dsum)
     gx, gw, gb = _ln_ref(x, dy.float(), w, b, 1e-5)
     assert rel(dx - dx0, gx) < 1e-5
     assert rel(dxb.float(), dx) < 8e-3
     assert rel(dw, gw) < 1e-5 and rel(db, gb) < 1e-5
+    if dsum is not None:  # the fused column sum of the updated rows (proj's bias grad in block_bwd)
+        assert rel(dsum, dx.double().sum(0)) < 1e-5
 
 
 def test_layernorm_bwd_rowmap(ops):
@@ -170,13 +173,15 @@ def test_layernorm_bwd_rowmap(ops):
     dx = torch.zeros(R, cols, device=DEV)
     dw = torch.zeros(cols, device=DEV)
     db = torch.zeros(cols, device=DEV)
-    ops.layernorm_bwd(x, dy, w, 1e-6, dx, rowmap=rowmap, dw=dw, db=db)
+    dsum = torch.empty(cols, device=DEV)
+    ops.layernorm_bwd(x, dy, w, 1e-6, dx, rowmap=rowmap, dw=dw, db=db, dx_sum=dsum)
     xs = x[rowmap.long()]
     gx, gw, gb = _ln_ref(xs, dy.float(), w, torch.zeros_like(w), 1e-6)
     ref = torch.zeros_like(dx)
     ref[rowmap.long()] = gx
     assert rel(dx, ref) < 1e-5
     assert rel(dw, gw) < 1e-5 and rel(db, gb) < 1e-5
+    assert rel(dsum, dx[rowmap.long()].double().sum(0)) < 1e-5  # over the mapped rows only
 
 
 def _qk_fwd_ref(raw, C, D, qkv, pos):
