@@ -549,6 +549,10 @@ int sr_imc_loss(sr_stream_t stream, const sr_imc_loss_desc* desc);
  * ---------------------------------------------------------------------- */
 int sr_layernorm(sr_stream_t stream, int out_dtype, const float* x, int64_t ldx, const int32_t* rowmap,
                  const float* w, const float* b, float eps, void* out, int64_t ldo, int rows, int cols);
+/* sr_layernorm (no rowmap) that also writes each fp32 input row to x_copy (row stride ldc): the
+ * training tape's saved block input (engine.run_block_train) without a separate copy pass. */
+int sr_layernorm_copy(sr_stream_t stream, int out_dtype, const float* x, int64_t ldx, const float* w, const float* b,
+                      float eps, void* out, int64_t ldo, float* x_copy, int64_t ldc, int rows, int cols);
 
 /* ------------------------------------------------------------------------
  * Residual update + LayerNorm (block.py:86-89: x = x + ls1(attn(norm1(x))) then norm2(x)):

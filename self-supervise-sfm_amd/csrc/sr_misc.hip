@@ -16,7 +16,8 @@ template <int NPL, int VEC, typename TO>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t ldx,
                                                         const int32_t* __restrict__ rowmap,
                                                         const float* __restrict__ w, const float* __restrict__ b,
-                                                        float eps, TO* __restrict__ out, int64_t ldo, int rows) {
+                                                        float eps, TO* __restrict__ out, int64_t ldo, int rows,
+                                                        float* __restrict__ xc, int64_t ldc) {
   // one wave per row pair (RPW rows in flight per wave: every load issued before the first
   // reduction); VEC-wide vector loads of x, w, b and VEC-wide stores
   constexpr int RPW = ln_rows_per_wave(NPL);
@@ -37,9 +38,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
       if constexpr (VEC == 4) {
         const float4 t = *(const float4*)(xr + col);
         v[r][i * 4 + 0] = t.x; v[r][i * 4 + 1] = t.y; v[r][i * 4 + 2] = t.z; v[r][i * 4 + 3] = t.w;
+        if (xc) *(float4*)(xc + (int64_t)row * ldc + col) = t;  // the row's fp32 copy (training tape)
       } else {
         const float2 t = *(const float2*)(xr + col);
         v[r][i * 2 + 0] = t.x; v[r][i * 2 + 1] = t.y;
+        if (xc) *(float2*)(xc + (int64_t)row * ldc + col) = t;
       }
     }
   }
@@ -92,13 +95,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 
 template <typename TO>
 int layernorm_dispatch(hipStream_t s, const float* x, int64_t ldx, const int32_t* rowmap, const float* w,
-                       const float* b, float eps, TO* out, int64_t ldo, int rows, int cols) {
+                       const float* b, float eps, TO* out, int64_t ldo, int rows, int cols, float* xc = nullptr,
+                       int64_t ldc = 0) {
   const dim3 block(256);  // 4 waves x ln_rows_per_wave rows
 #define LN_CASE(C, V)                                                                                    \
   case C:                                                                                                \
     hipLaunchKernelGGL((layernorm_kernel<C / 64, V, TO>),                                                \
                        dim3((rows + 4 * ln_rows_per_wave(C / 64) - 1) / (4 * ln_rows_per_wave(C / 64))), block, \
-                       0, s, x, ldx, rowmap, w, b, eps, out, ldo, rows);                                  \
+                       0, s, x, ldx, rowmap, w, b, eps, out, ldo, rows, xc, ldc);                         \
     return sr::check_launch("sr_layernorm");
   switch (cols) {
     LN_CASE(128, 2)
@@ -467,6 +471,20 @@ extern "C" int sr_layernorm(sr_stream_t stream, int out_dtype, const float* x, i
     return layernorm_dispatch<bf16>(s, x, ldx, rowmap, w, b, eps, (bf16*)out, ldo, rows, cols);
   SR_CHECK(out_dtype == SR_F32, SR_EINVAL, "sr_layernorm: bad dtype");
   return layernorm_dispatch<float>(s, x, ldx, rowmap, w, b, eps, (float*)out, ldo, rows, cols);
+}
+
+extern "C" int sr_layernorm_copy(sr_stream_t stream, int out_dtype, const float* x, int64_t ldx, const float* w,
+                                 const float* b, float eps, void* out, int64_t ldo, float* x_copy, int64_t ldc,
+                                 int rows, int cols) {
+  SR_CHECK(x && out && x_copy && rows > 0 && cols > 0, SR_EINVAL, "sr_layernorm_copy: bad args");
+  SR_CHECK((w == nullptr) == (b == nullptr), SR_EINVAL, "sr_layernorm_copy: w and b must both be set or both NULL");
+  SR_CHECK(ldx % 4 == 0 && ldc % 4 == 0 && ldc >= cols && ((uintptr_t)x_copy & 15) == 0, SR_EINVAL,
+           "sr_layernorm_copy: ldx / ldc multiples of 4, ldc >= cols, 16-B aligned x_copy");
+  hipStream_t s = (hipStream_t)stream;
+  if (out_dtype == SR_BF16)
+    return layernorm_dispatch<bf16>(s, x, ldx, nullptr, w, b, eps, (bf16*)out, ldo, rows, cols, x_copy, ldc);
+  SR_CHECK(out_dtype == SR_F32, SR_EINVAL, "sr_layernorm_copy: bad dtype");
+  return layernorm_dispatch<float>(s, x, ldx, nullptr, w, b, eps, (float*)out, ldo, rows, cols, x_copy, ldc);
 }
 
 extern "C" int sr_im2col_normalize(sr_stream_t stream, int dtype, const float* img, int frames, int H, int W,

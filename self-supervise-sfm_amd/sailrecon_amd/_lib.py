@@ -131,6 +131,7 @@ _PROTOS = {
     "sr_pil_resample_v_f32": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _f32, _vp,
                                      _i64, _i64, _i64]),
     "sr_layernorm": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _f32, _vp, _i64, _i32, _i32]),
+    "sr_layernorm_copy": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _i64, _i32, _i32]),
     "sr_residual_layernorm": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _f32, _vp, _i64, _i32, _i32]),
     "sr_im2col_normalize": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, ctypes.POINTER(_f32),
                                    ctypes.POINTER(_f32), _vp, _i32]),

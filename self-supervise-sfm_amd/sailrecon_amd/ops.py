@@ -734,12 +734,21 @@ def attention_bwd(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, lse: Tensor, dou
 
 
 def layernorm(x: Tensor, w: Optional[Tensor], b: Optional[Tensor], eps: float, out: Tensor,
-              rowmap: Optional[Tensor] = None, rows: Optional[int] = None) -> None:
+              rowmap: Optional[Tensor] = None, rows: Optional[int] = None, x_copy: Optional[Tensor] = None) -> None:
+    """out = LayerNorm(x rows) (sr_layernorm); ``x_copy`` (fp32, no rowmap): also the input rows
+    copied there in the same pass (sr_layernorm_copy)."""
     ldx = _rowmajor(x, "x")
     ldo = _rowmajor(out, "out")
     if x.dtype != torch.float32:
         raise TypeError("layernorm input must be fp32")
     n = out.shape[0] if rows is None else rows
+    if x_copy is not None:
+        if rowmap is not None or x_copy.dtype != torch.float32 or x_copy.shape[0] < n or x_copy.shape[1] != x.shape[1]:
+            raise ValueError("layernorm: x_copy must be fp32 [>= rows, cols] and takes no rowmap")
+        rc = _lib.load().sr_layernorm_copy(_stream(x), dtype_code(out.dtype), _p(x), ldx, _p(w), _p(b), eps, _p(out),
+                                           ldo, _p(x_copy), _rowmajor(x_copy, "x_copy"), n, x.shape[1])
+        check(rc, "sr_layernorm_copy")
+        return
     rc = _lib.load().sr_layernorm(_stream(x), dtype_code(out.dtype), _p(x), ldx, _p(rowmap), _p(w), _p(b),
                                   eps, _p(out), ldo, n, x.shape[1])
     check(rc, "sr_layernorm")

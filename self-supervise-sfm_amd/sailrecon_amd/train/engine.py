@@ -4,9 +4,9 @@ mlp.py:34-40 / layer_scale.py:22-23 that ``loss.backward()`` runs in train_imc.p
 
 Forward (run_block_train) is run_block's kernel sequence with the backward's inputs kept:
 
-    x0 = x (copy)  LN1 -> xn1   GEMM qkv -> qkv  (+ aux: pre-norm q|k|v = raw)
+    LN1 -> xn1 (+ x0 = x, the same pass)   GEMM qkv -> qkv  (+ aux: pre-norm q|k|v = raw)
     attention(qkv) -> o (+ lse)   GEMM proj + gamma1 + residual (in place on x)
-    x1 = x (copy)  LN2 -> xn2   GEMM fc1 + GELU -> h (+ aux: pre-activation u)
+    LN2 -> xn2 (+ x1 = x)   GEMM fc1 + GELU -> h (+ aux: pre-activation u)
     GEMM fc2 + gamma2 + residual
 
 Backward (block_bwd) takes dx (fp32 residual grad of the block output, updated in place to the
@@ -69,17 +69,14 @@ def run_block_train(pb: runtime.PackedBlock, x: Tensor, r0: int, r1: int, tape: 
                     attend: Callable[[Tensor, Tensor, Optional[Tensor]], None], qkv_epi: Optional[dict]) -> None:
     """x[r0:r1] <- Block(x[r0:r1]) keeping the backward's inputs in ``tape``."""
     xs = x[r0:r1]
-    R = r1 - r0
-    ops.copy_rows(tape.x0, xs, R)
-    ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, tape.xn1)
+    ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, tape.xn1, x_copy=tape.x0)  # x0 = x in the same pass
     if qkv_epi is None:
         ops.gemm(tape.xn1, pb.w_qkv, tape.qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
     else:
         ops.gemm(tape.xn1, pb.w_qkv, tape.qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, aux=tape.raw, tag="gemm")
     attend(tape.qkv, tape.o, tape.lse)
     ops.gemm(tape.o, pb.w_proj, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_proj, gamma=pb.g1, tag="gemm")
-    ops.copy_rows(tape.x1, xs, R)
-    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, tape.xn2)
+    ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, tape.xn2, x_copy=tape.x1)  # x1 = x likewise
     ops.gemm(tape.xn2, pb.w_fc1, tape.h, _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, aux=tape.u, tag="gemm")
     ops.gemm(tape.h, pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2, tag="gemm")
 

@@ -168,9 +168,11 @@ def attn_merge_n(o_parts, lse_parts, out, *, parts, rows, heads, head_dim, lse_o
         lse_out.view(heads, rows).copy_((m + torch.log2(tot)).t())
 
 
-def layernorm(x, w, b, eps, out, rowmap=None, rows=None):
+def layernorm(x, w, b, eps, out, rowmap=None, rows=None, x_copy=None):
     n = out.shape[0] if rows is None else rows
     src = x[rowmap.long()[:n]] if rowmap is not None else x[:n]
+    if x_copy is not None:
+        x_copy[:n] = src
     out[:n] = F.layer_norm(src, (x.shape[1],), w, b, eps).to(out.dtype)
 
 

@@ -314,6 +314,23 @@ def test_attention_softmax_spike(ops):
         assert rel(o.float(), ref) < tol
 
 
+@pytest.mark.parametrize("cols", [384, 1024, 4096])
+def test_layernorm_copy(ops, cols):
+    """sr_layernorm_copy (the training tape's x0 / x1 in the LayerNorm pass): the normalised rows
+    bit-identical to sr_layernorm's and the copy equal to the input rows, at a padded row stride."""
+    torch.manual_seed(cols)
+    R = 1377
+    x = torch.randn(R, cols, device=DEV) * 3 + 1
+    w, b = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV)
+    o0 = torch.empty(R, cols, device=DEV, dtype=torch.bfloat16)
+    o1 = torch.empty_like(o0)
+    xc = torch.full((R, cols + 64), float("nan"), device=DEV)[:, :cols]
+    ops.layernorm(x, w, b, 1e-6, o0)
+    ops.layernorm(x, w, b, 1e-6, o1, x_copy=xc)
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1) and torch.equal(xc, x)
+
+
 @pytest.mark.parametrize("cols", [384, 768, 1024, 2048])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_layernorm_rowmap(ops, cols, dtype):
