@@ -763,3 +763,39 @@ def test_global_attention_key_split_boxes(ops, tail):
         assert err < 1e-2
         outs.append(o)
     assert _rel(outs[1].float(), outs[0].float()) < 1e-2
+
+
+@pytest.mark.parametrize("tail", [False, True], ids=["compiled", "asm-seg"])
+def test_reloc_attention_two_segment_boxes(ops, tail):
+    """The data-derived bounds on a two-segment launch (global_reloc at qk-gain 4): the shared
+    subsample (segment 0, one box / norm / value-box instance) and each query frame's own keys
+    (segment 1, one instance per frame, at kb_n0 + item), both clustered around one direction so
+    that the boxes change the bound.  With and without them, against fp64 per frame."""
+    g, nq, nsub = 4.0, 8, 8 * PP
+    gen = torch.Generator(device=DEV).manual_seed(77)
+    u = torch.randn(1, H, D, device=DEV, generator=gen)
+    q, qn = _qk_gain(nq * P, g, gen)
+    k, kb = _qk_gain_shared(nq * P, g, gen, u, 0.05)
+    ks, kbs = _qk_gain_shared(nsub, g, gen, u, 0.05)
+    v = torch.randn(nq * P, C, device=DEV, generator=gen).bfloat16()
+    vs = torch.randn(nsub, C, device=DEV, generator=gen).bfloat16()
+    if tail:
+        k, v, ks, vs = _padded(k), _padded(v), _padded(ks), _padded(vs)
+    kbound = max(kb, kbs)
+    outs = []
+    for qnm in (0.0, qn):
+        o = torch.empty(nq * P, C, device=DEV, dtype=torch.bfloat16)
+        with ops.tuning(SR_ATTN_PIPE_SEG=int(tail)):
+            ops.attention(q, ks, vs, o, heads=H, head_dim=D, batch=nq, lq=P, q_bstride=P, l0=nsub, k0_bstride=0,
+                          k1=k, v1=v, l1=P, k1_bstride=P, tail_readable=tail, key_norm_max=kbound,
+                          query_norm_max=qnm)
+        torch.cuda.synchronize()
+        outs.append(o)
+    scale = D ** -0.5
+    for j in (0, 3, nq - 1):
+        fr = slice(j * P, (j + 1) * P)
+        rows = _sample_rows(P, 40, j).to(DEV)
+        ref = _ref_rows(q[fr][rows], torch.cat([ks, k[fr]]), torch.cat([vs, v[fr]]), scale)
+        for o in outs:
+            assert _rel(o[fr][rows].float(), ref) < 1e-2, j
+    assert _rel(outs[1].float(), outs[0].float()) < 1e-2
