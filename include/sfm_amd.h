@@ -457,6 +457,24 @@ int sr_nonfinite_check(sr_stream_t stream, const float* g, int64_t n, const floa
 int sr_adam_f32(sr_stream_t stream, float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                 float beta2, float eps, float weight_decay, int step, const float* scale, const int* found_inf);
 
+/* Per-optimizer-step weight refresh of one block (train/model.py refresh_packs): for each item the
+ * fp32 weight src [rows][cols] is read once and written as (cast, if set) its bf16 copy [rows][cols]
+ * and (trans, if set) its transposed bf16 copy [cols][rows] with rowscale[r] (if set) folded in --
+ * the forward GEMM operand and the dgrad GEMM operand in one launch for up to
+ * SR_WEIGHT_REFRESH_MAX weights. */
+#define SR_WEIGHT_REFRESH_MAX 4
+typedef struct sr_weight_item {
+  const float* src;
+  int64_t lds;
+  int rows, cols;
+  const float* rowscale;
+  void* cast;
+  int64_t ldc;
+  void* trans;
+  int64_t ldt;
+} sr_weight_item;
+int sr_weight_refresh_bf16(sr_stream_t stream, int n, const sr_weight_item* items);
+
 /* dst[c][r] = out_dtype(rowscale[r] * src[r][c])  (fp32 src [rows][lds]; W^T packs of the dgrad
  * GEMMs with LayerScale gamma folded into W's rows; rowscale may be NULL) */
 int sr_transpose_f32(sr_stream_t stream, int out_dtype, const float* src, int64_t lds, int rows, int cols,

@@ -89,6 +89,10 @@ void layout() {
           FIELD(sr_imc_loss_desc, max_val), FIELD(sr_imc_loss_desc, num_bins), FIELD(sr_imc_loss_desc, smooth_w),
           FIELD(sr_imc_loss_desc, smooth_radius), FIELD(sr_imc_loss_desc, grad_scale), FIELD(sr_imc_loss_desc, loss),
           FIELD(sr_imc_loss_desc, d_enc), FIELD(sr_imc_loss_desc, workspace)));
+  STRUCT(sr_weight_item,
+         (FIELD(sr_weight_item, src), FIELD(sr_weight_item, lds), FIELD(sr_weight_item, rows),
+          FIELD(sr_weight_item, cols), FIELD(sr_weight_item, rowscale), FIELD(sr_weight_item, cast),
+          FIELD(sr_weight_item, ldc), FIELD(sr_weight_item, trans), FIELD(sr_weight_item, ldt)));
   std::printf("}\n");
 }
 
@@ -252,6 +256,18 @@ void check() {
   expect("sr_pose_decode_f32 null", sr_pose_decode_f32(nullptr, nullptr, 9, 0, 518, 518, nullptr, nullptr), false);
   expect("sr_copy_rows_f32 null", sr_copy_rows_f32(nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0), false);
   expect("sr_conv3x3_f32 null", sr_conv3x3_f32(nullptr, nullptr, 1, 8, 8, 32, 1, 0, nullptr, 32, SR_EPI_BIAS, &ep, nullptr, 32, nullptr), false);
+  sr_weight_item wi{};
+  expect("sr_weight_refresh_bf16 0 items", sr_weight_refresh_bf16(nullptr, 0, &wi), false);
+  expect("sr_weight_refresh_bf16 no outputs", sr_weight_refresh_bf16(nullptr, 1, &wi), false);
+  wi.src = fake<float>(0);
+  wi.lds = 1024;
+  wi.rows = 3072;
+  wi.cols = 1024;
+  wi.cast = fake(1);
+  wi.ldc = 1024;
+  wi.trans = fake(2);
+  wi.ldt = 3072;
+  expect("sr_weight_refresh_bf16", sr_weight_refresh_bf16(nullptr, 1, &wi), true);
   expect("sr_im2col_normalize null", sr_im2col_normalize(nullptr, SR_BF16, nullptr, 0, 518, 518, 14, nullptr, nullptr, nullptr, 0), false);
 }
 

@@ -1074,6 +1074,63 @@ extern "C" int sr_adam_f32(sr_stream_t stream, float* p, const float* g, float* 
   return sr::check_launch("sr_adam_f32");
 }
 
+// sr_weight_refresh_bf16: up to SR_WEIGHT_REFRESH_MAX fp32 weights in one launch, each 64 x 64
+// source tile read once and written as its bf16 cast (same layout) and its transposed bf16 copy
+// with the row scale folded in.  Workgroup -> (item, tile) by the tile-count prefix.
+struct WeightRefresh {
+  sr_weight_item it[SR_WEIGHT_REFRESH_MAX];
+  int start[SR_WEIGHT_REFRESH_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void weight_refresh_kernel(WeightRefresh wr) {
+  __shared__ float tile[64][65];
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < SR_WEIGHT_REFRESH_MAX; ++i) p += (i < wr.n && (int)blockIdx.x >= wr.start[i]) ? 1 : 0;
+  const sr_weight_item& w = wr.it[p];
+  const int t = blockIdx.x - wr.start[p], ntc = (w.cols + 63) / 64;
+  const int r0 = (t / ntc) * 64, c0 = (t % ntc) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    float v = 0.f;
+    if (r < w.rows && c < w.cols) {
+      v = w.src[(int64_t)r * w.lds + c];
+      if (w.cast) ((bf16*)w.cast)[(int64_t)r * w.ldc + c] = (bf16)v;
+      if (w.rowscale) v *= w.rowscale[r];
+    }
+    tile[i][tx] = v;
+  }
+  if (!w.trans) return;  // workgroup-uniform
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < w.cols && r < w.rows) ((bf16*)w.trans)[(int64_t)c * w.ldt + r] = (bf16)tile[tx][i];
+  }
+}
+
+extern "C" int sr_weight_refresh_bf16(sr_stream_t stream, int n, const sr_weight_item* items) {
+  SR_CHECK(items && n > 0 && n <= SR_WEIGHT_REFRESH_MAX, SR_EINVAL, "sr_weight_refresh_bf16: 1..%d items (got %d)",
+           SR_WEIGHT_REFRESH_MAX, n);
+  WeightRefresh wr{};
+  wr.n = n;
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const sr_weight_item& w = items[i];
+    SR_CHECK(w.src && w.rows > 0 && w.cols > 0 && w.lds >= w.cols && (w.cast || w.trans) &&
+                 (!w.cast || w.ldc >= w.cols) && (!w.trans || w.ldt >= w.rows),
+             SR_EINVAL, "sr_weight_refresh_bf16: item %d: bad shape / pointers", i);
+    wr.it[i] = w;
+    wr.start[i] = tiles;
+    tiles += ((w.rows + 63) / 64) * ((w.cols + 63) / 64);
+  }
+  wr.start[n] = tiles;
+  hipLaunchKernelGGL(weight_refresh_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, wr);
+  sr::note_kernel("weight_refresh_kernel");
+  return sr::check_launch("sr_weight_refresh_bf16");
+}
+
 extern "C" int sr_transpose_f32(sr_stream_t stream, int out_dtype, const float* src, int64_t lds, int rows, int cols,
                                 const float* rowscale, void* dst, int64_t ldd) {
   SR_CHECK(src && dst && rows > 0 && cols > 0 && lds >= cols && ldd >= rows, SR_EINVAL, "sr_transpose_f32: bad args");

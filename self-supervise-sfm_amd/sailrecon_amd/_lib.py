@@ -74,6 +74,24 @@ class AttnDesc(ctypes.Structure):
     ]
 
 
+class WeightItem(ctypes.Structure):
+    """sr_weight_item (include/sfm_amd.h)."""
+    _fields_ = [
+        ("src", _vp),
+        ("lds", _i64),
+        ("rows", _i32),
+        ("cols", _i32),
+        ("rowscale", _vp),
+        ("cast", _vp),
+        ("ldc", _i64),
+        ("trans", _vp),
+        ("ldt", _i64),
+    ]
+
+
+SR_WEIGHT_REFRESH_MAX = 4
+
+
 class AttnBwdDesc(ctypes.Structure):
     _fields_ = [
         ("f", AttnDesc),
@@ -154,6 +172,7 @@ _PROTOS = {
     "sr_attention_key_box_scratch": (_i32, [_i32, _i32, _i32]),
     "sr_qk_bwd_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
     "sr_cast_bf16": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _f32]),
+    "sr_weight_refresh_bf16": (_i32, [_vp, _i32, _vp]),
     "sr_nonfinite_check": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "sr_adam_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
     "sr_transpose_f32": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i64]),

@@ -1101,6 +1101,27 @@ def adam(p: Tensor, g: Tensor, m: Tensor, v: Tensor, *, lr: float, beta1: float,
                                   weight_decay, step, _p(scale), _p(found_inf)), "sr_adam_f32")
 
 
+def weight_refresh(items) -> None:
+    """Up to 4 fp32 weights in one launch (sr_weight_refresh_bf16): ``items`` = (src fp32 [R, C],
+    cast bf16 [R, C] or None, trans bf16 [C, R] or None, rowscale fp32 [R] or None) -- the bf16
+    forward operand and the rowscaled transposed dgrad operand from one read of each weight."""
+    if not 0 < len(items) <= _lib.SR_WEIGHT_REFRESH_MAX:
+        raise ValueError("weight_refresh: 1..4 items")
+    arr = (_lib.WeightItem * len(items))()
+    for it, (src, cast, trans, rowscale) in zip(arr, items):
+        R, C = src.shape
+        if src.dtype != torch.float32 or (cast is None and trans is None):
+            raise ValueError("weight_refresh: fp32 src and a cast and / or trans output")
+        for t, shape in ((cast, (R, C)), (trans, (C, R))):
+            if t is not None and (t.dtype != torch.bfloat16 or tuple(t.shape) != shape):
+                raise ValueError(f"weight_refresh: bf16 outputs {(R, C)} / {(C, R)}")
+        it.src, it.lds, it.rows, it.cols = src.data_ptr(), _rowmajor(src, "src"), R, C
+        it.rowscale = None if rowscale is None else rowscale.data_ptr()
+        it.cast, it.ldc = (None, 0) if cast is None else (cast.data_ptr(), _rowmajor(cast, "cast"))
+        it.trans, it.ldt = (None, 0) if trans is None else (trans.data_ptr(), _rowmajor(trans, "trans"))
+    check(_lib.load().sr_weight_refresh_bf16(_stream(items[0][0]), len(items), arr), "sr_weight_refresh_bf16")
+
+
 def transpose(src: Tensor, dst: Tensor, rowscale: Optional[Tensor] = None) -> None:
     """dst[c, r] = dst.dtype(rowscale[r] * src[r, c]) (fp32 src)."""
     R, C = src.shape

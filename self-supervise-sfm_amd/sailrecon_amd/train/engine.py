@@ -161,6 +161,18 @@ def pack_bwd(blk, pb: runtime.PackedBlock, dtype: torch.dtype, into: Optional[Bw
     return into
 
 
+def refresh_block_bf16(blk, pb: runtime.PackedBlock, into: BwdPack) -> None:
+    """After an optimizer step, one launch per block (sr_weight_refresh_bf16): the four bf16
+    forward weights of the packed block (casts in place) and the four transposed dgrad packs of
+    pack_bwd (LayerScale gammas folded into proj / fc2), each fp32 weight read once."""
+    a = blk.attn
+    f = lambda t: t.detach()  # noqa: E731
+    ops.weight_refresh([(f(a.qkv.weight), pb.w_qkv, into.wt_qkv, None),
+                        (f(a.proj.weight), pb.w_proj, into.wt_proj, pb.g1),
+                        (f(blk.mlp.fc1.weight), pb.w_fc1, into.wt_fc1, None),
+                        (f(blk.mlp.fc2.weight), pb.w_fc2, into.wt_fc2, pb.g2)])
+
+
 class BwdScratch:
     """Grow-only backward scratch shared by every block of one stream."""
 

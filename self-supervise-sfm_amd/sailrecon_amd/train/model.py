@@ -75,9 +75,17 @@ class TrainGraph:
     def refresh_packs(self) -> None:
         """After an optimizer step: recast the bf16 forward weights in place (fp32 biases, gammas
         and norms alias the flat parameter buffer) and rebuild the transposed backward packs."""
+        # bf16 blocks with a backward pack: casts and transposed packs in one launch per block
+        fused = set()
+        for key in list(self._bwd):
+            blk, dt = self._bwd_src[key]
+            pb = blk._packed.get(BF16)
+            if dt == BF16 and pb is not None:
+                engine.refresh_block_bf16(blk, pb, self._bwd[key])
+                fused.add(id(blk))
         for blk in self._agg_blocks():
             pb = blk._packed.get(BF16)
-            if pb is not None:
+            if pb is not None and id(blk) not in fused:
                 a = blk.attn
                 for src, dst in ((a.qkv.weight, pb.w_qkv), (a.proj.weight, pb.w_proj),
                                  (blk.mlp.fc1.weight, pb.w_fc1), (blk.mlp.fc2.weight, pb.w_fc2)):
@@ -88,8 +96,8 @@ class TrainGraph:
             pe._pos_cache = {}
         for key in list(self._bwd):
             blk, dt = self._bwd_src[key]
-            pb = blk.packed(dt)
-            engine.pack_bwd(blk, pb, dt, into=self._bwd[key])
+            if id(blk) not in fused:
+                engine.pack_bwd(blk, blk.packed(dt), dt, into=self._bwd[key])
 
     def _agg_blocks(self):
         a = self.agg

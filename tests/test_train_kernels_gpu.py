@@ -335,3 +335,28 @@ def test_fp32_backward_gemms(ops):
     sw = torch.empty(K, N, device=DEV)
     ops.transpose(w, sw, rowscale=gam)
     assert torch.allclose(sw, (w * gam[:, None]).t())
+
+
+def test_weight_refresh(ops):
+    """sr_weight_refresh_bf16 (train/model.py refresh_packs): one launch over a block's four
+    weights (ragged 64-row tiles included) gives exactly sr_cast_bf16's forward operand and
+    sr_transpose_f32's row-scaled transposed dgrad operand."""
+    torch.manual_seed(11)
+    shapes = [(3072, 1024), (1024, 1024), (4096, 1000), (1000, 4096)]
+    srcs = [torch.randn(r, c, device=DEV) for r, c in shapes]
+    scales = [None, torch.randn(1024, device=DEV), None, torch.randn(1000, device=DEV)]
+    casts = [torch.empty(r, c, device=DEV, dtype=torch.bfloat16) for r, c in shapes]
+    trans = [torch.empty(c, r, device=DEV, dtype=torch.bfloat16) for r, c in shapes]
+    ops.weight_refresh(list(zip(srcs, casts, trans, scales)))
+    for src, cast, tr, sc in zip(srcs, casts, trans, scales):
+        c0 = torch.empty_like(cast)
+        t0 = torch.empty_like(tr)
+        ops.cast_bf16(src, c0)
+        ops.transpose(src, t0, rowscale=sc)
+        torch.cuda.synchronize()
+        assert torch.equal(cast, c0) and torch.equal(tr, t0)
+    # cast-only and transpose-only items
+    c1, t1 = torch.empty_like(casts[0]), torch.empty_like(trans[1])
+    ops.weight_refresh([(srcs[0], c1, None, None), (srcs[1], None, t1, scales[1])])
+    torch.cuda.synchronize()
+    assert torch.equal(c1, casts[0]) and torch.equal(t1, trans[1])
