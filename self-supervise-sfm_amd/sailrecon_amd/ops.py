@@ -499,6 +499,34 @@ def _attach_key_box(d: AttnDesc, device, query_norm_max: float, name: str) -> No
     d.key_box, d.value_box, d.key_bound = _p(ws), _p(ws[vb:]), _p(ws[nb:])
 
 
+def _attach_scan_boxes(d: AttnDesc, device) -> None:
+    """Key-scan launches (no static key bound: the training forward, whose weights move every
+    step) of one long query set -- the hand-scheduled sweep's launches: the key and value boxes as
+    well (sr_attn_desc.key_box / value_box; the launch scans max |k| itself).  There is no static
+    |q| |k| to decide by, and the two passes cost ~1 % of such a launch, so they always run
+    (SR_ATTN_KEY_BOX=0: never)."""
+    if _KEY_BOX == "0" or d.head_dim != 64 or d.heads > 32 or not (d.batch == 1 or d.q_bstride == 0) or \
+            d.lq < 4096 or d.mask_mode != _lib.SR_MASK_NONE:
+        return
+    n0 = 1 if d.k0_bstride == 0 else d.batch
+    n1 = (1 if d.k1_bstride == 0 else d.batch) if d.l1 > 0 else 0
+    per = d.heads * 128
+    ws = _train_ws(device, "attn_scan_box", 2 * (n0 + n1) * per)
+    lib = _lib.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    segs = [(d.k0, d.ldk0, d.v0, d.ldv0, d.l0, d.k0_bstride, n0, 0)]
+    if n1:
+        segs.append((d.k1, d.ldk1, d.v1, d.ldv1, d.l1, d.k1_bstride, n1, n0 * per))
+    vb = (n0 + n1) * per
+    sc = _train_ws(device, "attn_box_scratch", max(lib.sr_attention_key_box_scratch(g[4], g[6], d.heads) for g in segs))
+    for k, ldk, v, ldv, rows, bstride, n, off in segs:
+        check(lib.sr_attention_key_box(stream, k, ldk, rows, bstride, n, d.heads, _p(ws[off:]), None, _p(sc)),
+              "sr_attention_key_box")
+        check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:]), None, _p(sc)),
+              "sr_attention_key_box(values)")
+    d.key_box, d.value_box = _p(ws), _p(ws[vb:])
+
+
 def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: float, flops: float,
                       nbytes: float, query_norm_max: float = 0.0) -> None:
     if q.dtype == torch.bfloat16 and _ATTN_BOUND and key_norm_max > 0.0:
@@ -508,6 +536,7 @@ def _launch_attention(d: AttnDesc, q: Tensor, tag: Optional[str], key_norm_max: 
         nb = _lib.load().sr_attention_bound_floats(ctypes.byref(d))
         if nb > 0:
             d.key_bound = _p(_train_ws(q.device, "attn_key_bound", nb))
+            _attach_scan_boxes(d, q.device)
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
     rc = _lib.load().sr_attention(_stream(q), dtype_code(q.dtype), ctypes.byref(d))

@@ -799,3 +799,33 @@ def test_reloc_attention_two_segment_boxes(ops, tail):
         for o in outs:
             assert _rel(o[fr][rows].float(), ref) < 1e-2, j
     assert _rel(outs[1].float(), outs[0].float()) < 1e-2
+
+
+def test_global_attention_scan_boxes(ops):
+    """Key-scan launches (no static key bound: the training forward) of one long query set attach
+    the key and value boxes themselves (ops._attach_scan_boxes): at qk-gain 4.5 on LayerNorm'd random
+    q / k every wave then runs the hand-scheduled sweep, where the scanned 2-norm window alone sends
+    every wave to the compiled loop.  Both against fp64."""
+    g, L = 4.5, 32 * P
+    gen = torch.Generator(device=DEV).manual_seed(450)
+    q, _ = _qk_gain(L, g, gen)
+    k, _ = _qk_gain(L, g, gen)
+    v = torch.randn(L, C, device=DEV, generator=gen).bfloat16()
+    rows = _sample_rows(L, 128, 450).to(DEV)
+    ref = _ref_rows(q[rows], k, v, D ** -0.5)
+    waves = (L + 63) // 64 * H
+    saved = ops._KEY_BOX
+    try:
+        for mode, want in (("0", [0, waves]), ("auto", [waves, 0])):
+            ops._KEY_BOX = mode
+            st = torch.zeros(2, dtype=torch.int32, device=DEV)
+            o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+            ops.attention(q, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                          sweep_stats=st)
+            torch.cuda.synchronize()
+            err = _rel(o[rows].float(), ref)
+            print(f"scan mode, SR_ATTN_KEY_BOX={mode}: waves {st.tolist()}, rel {err:.2e}")
+            assert st.tolist() == want
+            assert err < 1.5e-2
+    finally:
+        ops._KEY_BOX = saved

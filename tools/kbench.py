@@ -561,7 +561,8 @@ def train():
     """BASELINE config 4 (train_imc.py step, 16-view batches): full-size SailRecon aggregator +
     camera head (DPT heads off: no loss reaches them), seeded synthetic weights, a synthetic
     16-view IMC-shaped batch (15 chained pairs x 1024 correspondences, per-frame CDF nodes), bf16
-    aggregator / fp32 heads, fwd + loss + bwd + Adam per step."""
+    aggregator / fp32 heads, fwd + loss + bwd + Adam per step.  SR_TRAIN_QK_GAIN=g scales every
+    q_norm / k_norm weight by g first (trained-like gains)."""
     from sailrecon_amd.models.sail_recon import SailRecon
     from sailrecon_amd.train.data import synthetic_batch
     from sailrecon_amd.train.loss import CDFLossIndexPytorch
@@ -572,8 +573,16 @@ def train():
     t0 = time.perf_counter()
     m = SailRecon(enable_point=False, enable_depth=False)
     m.load_state_dict(synth_state_dict_like(m), strict=False)
+    gain = float(os.environ.get("SR_TRAIN_QK_GAIN", "1"))
+    if gain != 1.0:  # trained-like q_norm / k_norm weights (bench.py --qk-gain)
+        with torch.no_grad():
+            for mod in m.modules():
+                for nm in ("q_norm", "k_norm"):
+                    ln = getattr(mod, nm, None)
+                    if ln is not None and getattr(ln, "weight", None) is not None:
+                        ln.weight.mul_(gain)
     m = m.to(DEV)
-    print(f"train: model built in {time.perf_counter() - t0:.1f} s", flush=True)
+    print(f"train: model built in {time.perf_counter() - t0:.1f} s (qk-norm gain {gain:g})", flush=True)
     b = synthetic_batch(n, n_points=1024, size=518, seed=0)
     cdf = CDFLossIndexPytorch(0.0, 15.0, 250, b["src_idx"], b["dst_idx"], gradient_smooth=0.05, num_nodes=n)
     tr = Trainer(m, max_lr=2e-4, warmup_steps=2000, max_steps=100_000, cdf=cdf)
