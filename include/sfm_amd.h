@@ -142,8 +142,20 @@ typedef struct sr_gemm_epi {
      qk-norm / RoPE) to aux (dtype, row stride ld_aux) for the backward; GELU_BWD reads it */
   void* aux;
   int64_t ld_aux;
+  /* BIAS / QKV (bf16 outputs): output columns [0, q_cols) -- the Q block -- are multiplied by
+     q_scale in fp32 before the one rounding to the output type (0 = off).  With q_scale =
+     scale * log2(e) the attention reads c*q rounded once (sr_attn_desc.q_scaled) instead of
+     re-rounding c * bf16(q) (ABI 1.0).  q_cols a multiple of 64. */
+  float q_scale;
+  int q_cols;
 } sr_gemm_epi;
 
+/* bf16 kernels: 256x256 tiles (one workgroup per CU) for >= 512 such tiles, else 128x128; with
+ * SR_TUNE_GEMM_TAIL the rows past the 256x256 kernel's last whole workgroup round run on the 128x128
+ * kernel in a second launch.  Both run the same MFMA over the same k order per output element, so
+ * the accumulators agree and only the epilogue's fp32 contraction may differ (rel <= 1e-6,
+ * test_kernels_gpu.py::test_gemm_tail_split over every epilogue, aux and row-map form); the
+ * split-K path (sr_gemm_splitk) sums in another order. */
 int sr_gemm(sr_stream_t stream, int dtype, int epilogue, const void* A, int64_t lda, const void* W,
             int64_t ldw, void* out, int64_t ldo, int M, int N, int K, const sr_gemm_epi* ep);
 
@@ -218,17 +230,15 @@ typedef struct sr_attn_desc {
   float* lse;  /* optional: [batch][heads][lq] row log-sum-exp of scale*log2(e)*q.k (log2
                   domain), saved for sr_attention_bwd and for sr_attn_merge */
   float* key_bound; /* optional scratch (bf16 path, >= sr_attention_bound_floats(d) floats, 4-B
-                  aligned): per key-segment instance and head, max |k| over the keys.  With it a
-                  query row whose Cauchy-Schwarz bound c|q| max|k| lies within 2^174 of its first
-                  tile's max runs the sweep with a FIXED softmax offset m = max(tile max, bound - 64)
-                  (m = 0 for a bound <= 64): no per-tile row max, no rescale; every P <= 2^64 and the
-                  row's largest P >= 2^-110, so no overflow and the same precision.  The
-                  hand-scheduled sweep (bf16, 256-row workgroups) fixes m = max(0, bound - 64) for
-                  every row whose bound is within 2^174 of its max over the first three key tiles;
-                  other waves run the compiled loop; NULL (and no key_norm_max) = per-tile max.
-                  (The per-head value is max |k|^2.)  With key_norm_max > 0 a non-NULL key_bound is
-                  NOT scratch but caller-filled (sr_attention_key_box's norm2_out) and the bound uses
-                  the smaller of the two: the keys' actual max norm is often well below the static one */
+                  aligned): per key-segment instance and head, max |k|^2 over the keys, scanned by the
+                  launch itself.  With it a query row whose Cauchy-Schwarz bound c|q| max|k| lies
+                  within 2^174 of its first tile's max runs the sweep with a FIXED softmax offset
+                  m = max(tile max, bound - 64) (m = 0 for a bound <= 64): no per-tile row max, no
+                  rescale; every P <= 2^64 and the row's largest P >= 2^-110, so no overflow and the
+                  same precision.  The hand-scheduled sweep (bf16, 256-row workgroups) fixes
+                  m = max(0, bound - 64) for every row whose bound is within 2^174 of its max over the
+                  first three key tiles; other waves run the compiled loop; NULL (and no key_norm_max,
+                  no key_norm2) = per-tile max.  IGNORED when key_norm_max > 0 (no scan). */
   float key_norm_max; /* optional (bf16 path): > 0 = a static upper bound of |k| (2-norm per head)
                   for every key, used INSTEAD of key_bound (no key scan).  For keys that come out of
                   the qk LayerNorm (attention.py:49-50,78) and RoPE (a rotation), |k| <=
@@ -275,6 +285,16 @@ typedef struct sr_attn_desc {
                   to what the launch's fp32 sums allow, 125 - ceil(log2(l0 + l1)) -
                   ceil(log2 max|v|) (at most 100), so rows with a larger gap between their bound and
                   their true score max stay on the hand-scheduled sweep.  NULL = the 2^64 side */
+  /* ABI 1.0 */
+  const float* key_norm2; /* optional (bf16 path), CALLER-FILLED: per key-segment instance and head
+                  (layout as key_bound), max |k|^2 over the keys (sr_attention_key_box's norm2_out).
+                  The bound uses sqrt of it, or the smaller of it and key_norm_max when both are set.
+                  NULL = unset.  (Before ABI 1.0 this was key_bound's meaning when key_norm_max > 0.) */
+  int32_t q_scaled; /* bf16 path: 1 = q already holds c*q, c = scale*log2(e), rounded once to bf16
+                  (sr_gemm_epi.q_scale in the QKV / bias epilogue that wrote it), so the kernel uses
+                  it as is; 0 = q is plain and the kernel forms c*q itself (a second rounding of
+                  q).  sr_attention_qk8 / qkv8 take their q from sr_quant_fp8 and ignore it; the f32
+                  kernel and sr_attention_bwd reject 1. */
 } sr_attn_desc;
 
 /* floats of key_bound scratch sr_attention needs for d (0 if d does not use it) */
@@ -284,8 +304,8 @@ int sr_attention_bound_floats(const sr_attn_desc* d);
  * [h*64 + d] (bf16 keys, head_dim 64; out fp32, n_inst*heads*128 floats): the key box of
  * sr_attn_desc.key_box for one key segment (inst_stride 0 with n_inst 1: keys shared by every item);
  * on the values, sr_attn_desc.value_box.  norm2_out (optional, n_inst*heads floats): max over the rows
- * of |k|^2 per instance and head (fp32 sums of the bf16 squares), sr_attn_desc.key_bound's caller-
- * filled form.  Two launches (per-workgroup partial boxes in scratch, then their reduction), no atomics.
+ * of |k|^2 per instance and head (fp32 sums of the bf16 squares): sr_attn_desc.key_norm2.  out and
+ * norm2_out 16-B aligned (the attention reads the boxes as 16-B vectors).  Two launches (per-workgroup partial boxes in scratch, then their reduction), no atomics.
  * Replaces nothing in the reference: a bound the fixed-offset softmax of attention.py:103-109's
  * replacement uses. */
 int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t ldk, int rows, int64_t inst_stride, int n_inst,
@@ -402,10 +422,13 @@ int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B,
 
 /* Column sums (bias / token / positional-embedding grads):
  *   out[c] = (accumulate ? out[c] : 0) + scale * sum_{r<M} X[r*ldx + c],  c < N (N % 4 == 0).
- * X is `dtype`; two deterministic passes through `workspace` (>= 1024 * N floats, or
- * ceil(M / 16) * N if smaller). */
+ * X is `dtype`; two deterministic passes through `workspace` (16-B aligned, workspace_floats >=
+ * sr_colsum_workspace_floats(M, N), checked: at most ceil(M / 16) * N and 1024 * N; ABI 1.0 adds the
+ * size argument so that a caller sized to an older contract fails with SR_EINVAL, not an
+ * out-of-bounds write). */
+int64_t sr_colsum_workspace_floats(int M, int N);
 int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
-              float scale, float* workspace);
+              float scale, float* workspace, int64_t workspace_floats);
 
 /* LayerNorm backward (block.py:50,70 norm1 / norm2; vision_transformer.py:300 norm):
  * for row r (x row / dx row = rowmap ? rowmap[r] : r):

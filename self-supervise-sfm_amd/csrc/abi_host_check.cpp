@@ -54,7 +54,8 @@ void layout() {
                        FIELD(sr_gemm_epi, pos_row_base), FIELD(sr_gemm_epi, tokens_per_frame),
                        FIELD(sr_gemm_epi, patch_start), FIELD(sr_gemm_epi, grid_w), FIELD(sr_gemm_epi, seg_rows),
                        FIELD(sr_gemm_epi, seg_stride), FIELD(sr_gemm_epi, seg_offset), FIELD(sr_gemm_epi, row_add),
-                       FIELD(sr_gemm_epi, aux), FIELD(sr_gemm_epi, ld_aux)));
+                       FIELD(sr_gemm_epi, aux), FIELD(sr_gemm_epi, ld_aux), FIELD(sr_gemm_epi, q_scale),
+                       FIELD(sr_gemm_epi, q_cols)));
   STRUCT(sr_gemm_problem, (FIELD(sr_gemm_problem, A), FIELD(sr_gemm_problem, lda), FIELD(sr_gemm_problem, W),
                            FIELD(sr_gemm_problem, ldw), FIELD(sr_gemm_problem, out), FIELD(sr_gemm_problem, ldo),
                            FIELD(sr_gemm_problem, M), FIELD(sr_gemm_problem, N), FIELD(sr_gemm_problem, K),
@@ -72,7 +73,8 @@ void layout() {
           FIELD(sr_attn_desc, mask_hstride), FIELD(sr_attn_desc, mask_ld), FIELD(sr_attn_desc, tail_rows_readable),
           FIELD(sr_attn_desc, merge_o), FIELD(sr_attn_desc, ld_merge_o), FIELD(sr_attn_desc, merge_lse),
           FIELD(sr_attn_desc, merge_rows), FIELD(sr_attn_desc, sweep_stats),
-          FIELD(sr_attn_desc, key_box), FIELD(sr_attn_desc, value_box)));
+          FIELD(sr_attn_desc, key_box), FIELD(sr_attn_desc, value_box), FIELD(sr_attn_desc, key_norm2),
+          FIELD(sr_attn_desc, q_scaled)));
   STRUCT(sr_attn_bwd_desc,
          (FIELD(sr_attn_bwd_desc, f), FIELD(sr_attn_bwd_desc, dout), FIELD(sr_attn_bwd_desc, lddo),
           FIELD(sr_attn_bwd_desc, delta), FIELD(sr_attn_bwd_desc, dq), FIELD(sr_attn_bwd_desc, lddq),
@@ -123,7 +125,7 @@ sr_attn_desc attn(int batch, int heads, int lq, int l0, int l1) {
 
 void check() {
   // ---- tuning table and strings
-  if (sr_version() < 3) ++g_fail;
+  if (sr_version() < (1 << 16)) ++g_fail;
   for (int k = 0; k < SR_TUNE_COUNT; ++k) {
     const char* n = sr_tuning_name(k);
     const int v = sr_get_tuning(k);
@@ -153,6 +155,14 @@ void check() {
         std::snprintf(what, sizeof(what), "sr_gemm f32 epi %d M %d N %d", epi, M, N);
         expect(what, sr_gemm(nullptr, SR_F32, epi, fake(0), 1024, fake(1), 1024, fake(2), N, M, N, 1024, &ep), true);
       }
+  ep.q_scale = 0.18f;  // ABI 1.0: the Q block of a BIAS / QKV output leaves scaled
+  ep.q_cols = 1024;
+  expect("sr_gemm BIAS q_scale", sr_gemm(nullptr, SR_BF16, SR_EPI_BIAS, fake(0), 1024, fake(1), 1024, fake(2), 3072, 87936, 3072, 1024, &ep), true);
+  expect("sr_gemm RESID q_scale", sr_gemm(nullptr, SR_BF16, SR_EPI_BIAS_RESID, fake(0), 1024, fake(1), 1024, fake(2), 3072, 87936, 3072, 1024, &ep), false);
+  ep.q_cols = 100;
+  expect("sr_gemm q_cols not a multiple of 64", sr_gemm(nullptr, SR_BF16, SR_EPI_BIAS, fake(0), 1024, fake(1), 1024, fake(2), 3072, 87936, 3072, 1024, &ep), false);
+  ep.q_scale = 0.f;
+  ep.q_cols = 0;
   expect("sr_gemm_splitk 3 slices of 16 tiles", sr_gemm_splitk(nullptr, SR_BF16, SR_EPI_BIAS, fake(0), 1024, fake(1), 1024, fake(2), 1024, 64, 1024, 1024, 3, fake<float>(3), &ep), false);
   expect("sr_gemm_splitk 4 slices", sr_gemm_splitk(nullptr, SR_BF16, SR_EPI_BIAS, fake(0), 1024, fake(1), 1024, fake(2), 1024, 64, 1024, 1024, 4, fake<float>(3), &ep), true);
   std::vector<sr_gemm_problem> pr(5);
@@ -188,6 +198,25 @@ void check() {
   d.key_norm_max = 0.f;
   d.key_bound = fake<float>(7);
   expect("sr_attention global, key scan", sr_attention(nullptr, SR_BF16, &d), true);
+  // ABI 1.0: the caller-filled norms have their own field; boxes need a bound and 16-B alignment
+  d = attn(1, 16, 43968, 43968, 0);
+  d.key_norm_max = 40.f;
+  d.key_norm2 = fake<float>(10);
+  d.key_box = fake<float>(11);
+  d.value_box = fake<float>(12);
+  d.q_scaled = 1;
+  expect("sr_attention global, key_norm2 + boxes + q_scaled", sr_attention(nullptr, SR_BF16, &d), true);
+  d.key_box = (const float*)((const char*)fake<float>(11) + 4);
+  expect("sr_attention misaligned key_box", sr_attention(nullptr, SR_BF16, &d), false);
+  d.key_box = fake<float>(11);
+  d.key_norm_max = 0.f;
+  d.key_norm2 = nullptr;
+  expect("sr_attention boxes without a bound", sr_attention(nullptr, SR_BF16, &d), false);
+  d = attn(4, 16, 300, 300, 0);
+  d.q_scaled = 1;
+  expect("sr_attention f32 q_scaled", sr_attention(nullptr, SR_F32, &d), false);
+  d.q_scaled = 2;
+  expect("sr_attention bf16 q_scaled 2", sr_attention(nullptr, SR_BF16, &d), false);
   d = attn(64, 16, 1374, 1374, 0);
   d.k0_bstride = 1374;
   expect("sr_attention frame", sr_attention(nullptr, SR_BF16, &d), true);
@@ -250,7 +279,15 @@ void check() {
   expect("sr_quant_fp8_vt null", sr_quant_fp8_vt(nullptr, nullptr, 8, 8, 1, nullptr, nullptr, nullptr), false);
   expect("sr_attention_bwd null", sr_attention_bwd(nullptr, nullptr), false);
   expect("sr_gemm_wgrad null", sr_gemm_wgrad(nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, 0, 0, 0, nullptr, nullptr, 0, nullptr, 0, nullptr), false);
-  expect("sr_colsum null", sr_colsum(nullptr, SR_F32, nullptr, 0, 0, 0, nullptr, 0, 1.f, nullptr), false);
+  expect("sr_colsum null", sr_colsum(nullptr, SR_F32, nullptr, 0, 0, 0, nullptr, 0, 1.f, nullptr, 0), false);
+  {  // ABI 1.0: the workspace size is checked against sr_colsum_workspace_floats
+    const int64_t need = sr_colsum_workspace_floats(87936, 1024);
+    if (need <= 0 || need > 1024LL * 1024) ++g_fail;
+    expect("sr_colsum workspace one float short",
+           sr_colsum(nullptr, SR_F32, fake(1), 1024, 87936, 1024, fake<float>(2), 0, 1.f, fake<float>(3), need - 1), false);
+    expect("sr_colsum sized workspace",
+           sr_colsum(nullptr, SR_F32, fake(1), 1024, 87936, 1024, fake<float>(2), 0, 1.f, fake<float>(3), need), true);
+  }
   expect("sr_imc_loss null", sr_imc_loss(nullptr, nullptr), false);
   std::printf("imc workspace floats: %lld\n", (long long)sr_imc_loss_workspace(4, 3, 1024, 1, 100));
   expect("sr_pose_decode_f32 null", sr_pose_decode_f32(nullptr, nullptr, 9, 0, 518, 518, nullptr, nullptr), false);

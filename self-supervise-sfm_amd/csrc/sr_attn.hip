@@ -196,12 +196,14 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // scoreboard carries the Q loads into the loop and places vmcnt waits before the first
   // MFMAs of every tile, which (counting the asm-issued DMAs too) drain the K/V ring.
   __builtin_amdgcn_s_waitcnt(0);
+  if (!d.q_scaled) {  // q plain: form c*q here (a second rounding; q_scaled: rounded once upstream)
 #pragma unroll
-  for (int b = 0; b < QB; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qf[b][s][j] = (bf16)((float)qf[b][s][j] * c);
+        for (int j = 0; j < 8; ++j) qf[b][s][j] = (bf16)((float)qf[b][s][j] * c);
+  }
 
   // Fixed-offset sweep (d.key_bound set): qb = |cq| max|k| bounds every score of the row
   // (Cauchy-Schwarz).  After tile 0 a wave whose rows all satisfy qb - max_tile0 <= FIX_HI + FIX_LO
@@ -214,15 +216,18 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   // sum_d max(cq_d kmax_d, cq_d kmin_d) where d.key_box is set (min of the two)
   float qb[QB], qs[QB];
   float fix_hi = FIX_HI;  // the window's upper side (wider with d.value_box: value_window_hi)
-  const bool use_bound = d.key_bound != nullptr || d.key_norm_max > 0.f;
+  // the per-head max |k|^2 the bound reads: the launch's own scan (key_bound scratch, only without
+  // a static bound) or the caller's (key_norm2)
+  const float* kn2p = d.key_norm2 ? d.key_norm2 : (d.key_norm_max > 0.f ? nullptr : d.key_bound);
+  const bool use_bound = kn2p != nullptr || d.key_norm_max > 0.f;
   if (use_bound) {
-    // static bound, scanned bound (scratch filled above), or the smaller of a static and a
+    // static bound, scanned bound, caller-filled bound, or the smaller of a static and a
     // caller-filled one (sr_attention_key_box's norm2_out)
     float kn = d.key_norm_max > 0.f ? d.key_norm_max : INFINITY;
-    if (d.key_bound) {
-      float kn2 = d.key_bound[(d.k0_bstride == 0 ? 0 : item) * d.heads + head];
+    if (kn2p) {
+      float kn2 = kn2p[(d.k0_bstride == 0 ? 0 : item) * d.heads + head];
       if (args.ntile1 > 0)
-        kn2 = fmaxf(kn2, d.key_bound[(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head]);
+        kn2 = fmaxf(kn2, kn2p[(args.kb_n0 + (d.k1_bstride == 0 ? 0 : item)) * d.heads + head]);
       kn = fminf(kn, sqrtf(kn2) * 1.0001f);  // (+ the fp32 sums of the squares)
     }
 #pragma unroll
@@ -1648,10 +1653,10 @@ extern "C" int sr_attention_key_box(sr_stream_t stream, const void* k, int64_t l
   SR_CHECK(k && out && scratch, SR_EINVAL, "sr_attention_key_box: null k / out / scratch");
   SR_CHECK(rows > 0 && n_inst > 0 && heads > 0 && heads <= 32, SR_EINVAL,
            "sr_attention_key_box: rows, instances > 0 and 1..32 heads (rows=%d n_inst=%d heads=%d)", rows, n_inst, heads);
-  SR_CHECK(ldk % 8 == 0 && ldk >= 64 * heads && ((uintptr_t)k & 15) == 0 && ((uintptr_t)out & 3) == 0 &&
+  SR_CHECK(ldk % 8 == 0 && ldk >= 64 * heads && ((uintptr_t)k & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
                ((uintptr_t)norm2_out & 3) == 0 && ((uintptr_t)scratch & 3) == 0 && (n_inst == 1 || inst_stride >= rows),
-           SR_EINVAL, "sr_attention_key_box: ldk a multiple of 8 covering the heads, 16-B aligned k, 4-B aligned "
-                      "out / norm2_out / scratch, inst_stride >= rows");
+           SR_EINVAL, "sr_attention_key_box: ldk a multiple of 8 covering the heads, 16-B aligned k and out, 4-B "
+                      "aligned norm2_out / scratch, inst_stride >= rows");
   SR_CHECK(n_inst <= 65535, SR_EINVAL, "sr_attention_key_box: at most 65535 instances");
   hipStream_t s = (hipStream_t)stream;
   const int gx = key_box_parts(rows, n_inst, heads);
@@ -1669,6 +1674,19 @@ extern "C" int sr_attention_bound_floats(const sr_attn_desc* desc) {
   return bound_instances(*desc, n0) * desc->heads;
 }
 
+// The optional bound inputs of a bf16 launch: the key / value boxes are read as 16-B
+// vectors and exist only beside a key bound; key_norm2 is read per (instance, head).
+static int check_bound_fields(const sr_attn_desc& d, const char* who) {
+  SR_CHECK((((uintptr_t)d.key_box | (uintptr_t)d.value_box) & 15) == 0 && ((uintptr_t)d.key_norm2 & 3) == 0, SR_EINVAL,
+           "%s: key_box / value_box must be 16-B aligned and key_norm2 4-B aligned", who);
+  SR_CHECK(!(d.key_box || d.value_box) || d.key_bound || d.key_norm2 || d.key_norm_max > 0.f, SR_EINVAL,
+           "%s: key_box / value_box need a key bound (key_bound scratch, key_norm2 or key_norm_max)", who);
+  SR_CHECK(!(d.key_box || d.value_box || d.key_norm2) || (d.head_dim == 64 && d.heads <= 32), SR_EINVAL,
+           "%s: key_box / value_box / key_norm2 need head_dim 64 and at most 32 heads", who);
+  SR_CHECK(d.q_scaled == 0 || d.q_scaled == 1, SR_EINVAL, "%s: q_scaled must be 0 or 1", who);
+  return SR_OK;
+}
+
 // The hand-scheduled sweep's launch conditions for one problem of sr_attention_pair (bf16, one
 // long query set against one segment of whole key tiles, a static key bound).
 static int pair_args(const sr_attn_desc& d, AttnArgs& a, const char* which) {
@@ -1679,6 +1697,8 @@ static int pair_args(const sr_attn_desc& d, AttnArgs& a, const char* which) {
            "sr_attention_pair(%s): whole key tiles (>= 4) and a static key bound", which);
   SR_CHECK(d.ldq % 8 == 0 && d.ldk0 % 8 == 0 && d.ldv0 % 8 == 0 && d.ldo % 4 == 0, SR_EINVAL,
            "sr_attention_pair(%s): leading dims must be multiples of 8", which);
+  int rc = check_bound_fields(d, "sr_attention_pair");
+  if (rc != SR_OK) return rc;
   a.d = d;
   a.ntile0 = d.l0 / KT;
   a.ntile1 = 0;
@@ -1733,7 +1753,9 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     a.ntile1 = (d.l1 + KT - 1) / KT;
     const int n_inst = bound_instances(d, a.kb_n0);
     a.allow_mzero = sr::tune(SR_TUNE_ATTN_MZERO);
-    if (d.key_bound && !(d.key_norm_max > 0.f)) {
+    const int brc = check_bound_fields(d, "sr_attention(bf16)");
+    if (brc != SR_OK) return brc;
+    if (d.key_bound && !(d.key_norm_max > 0.f) && !d.key_norm2) {
       SR_CHECK(d.heads <= 32 && ((uintptr_t)d.key_bound & 3) == 0, SR_EINVAL, "sr_attention: key_bound needs heads <= 32");
       SR_CHECK(hipMemsetAsync(d.key_bound, 0, sizeof(float) * n_inst * d.heads, s) == hipSuccess, SR_ELAUNCH,
                "sr_attention: key_bound memset");
@@ -1781,7 +1803,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     // the _SEG variant by default only for ONE long query set (one ragged q-tile per item): the
     // reloc block's shared-subsample pass (aggregator.py split reloc), ragged global segments and
     // the key-split items of one query set (q_bstride 0) whose chunk tails are readable
-    else if (pipe && (d.key_bound || d.key_norm_max > 0.f) &&
+    else if (pipe && (d.key_bound || d.key_norm2 || d.key_norm_max > 0.f) &&
              ((d.l1 == 0 && d.l0 % KT == 0) ||
               ((pipe_seg || ((d.batch == 1 || d.q_bstride == 0) && d.lq >= 4096)) && d.tail_rows_readable >= KT)))
       SR_ATTN_LAUNCH(4, 2, true);  // the asm sweep: one segment of full tiles, or (_SEG) two / ragged
@@ -1790,6 +1812,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
     return sr::check_launch("sr_attention(bf16)");
   }
   SR_CHECK(dtype == SR_F32, SR_EINVAL, "sr_attention: bad dtype %d", dtype);
+  SR_CHECK(!d.q_scaled, SR_EUNSUPPORTED, "sr_attention(f32): q_scaled is a bf16-path convention");
   a.ntile0 = a.ntile1 = 0;
   const bool no_short = sr::tune(SR_TUNE_ATTN_NO_SHORT) != 0;
   const bool al16 = (((uintptr_t)d.q | (uintptr_t)d.k0 | (uintptr_t)(d.l1 ? d.k1 : d.k0)) & 15) == 0;

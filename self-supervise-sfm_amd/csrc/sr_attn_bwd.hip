@@ -464,6 +464,7 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   SR_CHECK(f.head_dim == 64 && f.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED,
            "sr_attention_bwd: head_dim 64 without mask only");
   SR_CHECK(f.batch > 0 && f.heads > 0 && f.lq > 0 && f.l0 > 0 && f.l1 >= 0, SR_EINVAL, "sr_attention_bwd: bad sizes");
+  SR_CHECK(!f.q_scaled, SR_EUNSUPPORTED, "sr_attention_bwd: q_scaled (a forward-only convention) is not supported");
   SR_CHECK(f.l1 == 0 || (f.k1 && f.v1 && b.dk1 && b.dv1), SR_EINVAL, "sr_attention_bwd: segment 1 needs k1/v1/dk1/dv1");
   SR_CHECK(f.ldq % 8 == 0 && f.ldk0 % 8 == 0 && f.ldv0 % 8 == 0 && f.ldo % 8 == 0 && b.lddo % 8 == 0 &&
                b.lddq % 4 == 0 && b.lddk0 % 4 == 0 && b.lddv0 % 4 == 0 &&

@@ -76,6 +76,13 @@ template <> struct Mma<float> {
   }
 };
 
+// Element types the epilogues store: RESID / F32 / PATCH write fp32 whatever the operand type,
+// the others the operand type; the saved pre-activation (sr_gemm_epi.aux) has the operand type.
+template <typename T, int EPI>
+using OutT = std::conditional_t<EPI == SR_EPI_BIAS_RESID || EPI == SR_EPI_F32 || EPI == SR_EPI_PATCH, float, T>;
+template <typename T>
+using AuxT = T;
+
 // Fused epilogue on C^T accumulator tiles: acc[mi][ni] covers output rows
 // rowbase + mi*16 + lr and the 4 consecutive columns colw + ni*16 + 4*lg + r.
 // Final per-lane values of every epilogue but PATCH, handed to emit(row, col, v[4]):
@@ -134,6 +141,9 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
       }
     }
   } else if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU || EPI == SR_EPI_F32) {
+    // the Q block of a plain-bias QKV projection (DINO) leaves scaled by q_scale (wave-uniform:
+    // the wave's 64 columns start at colw, q_cols is a multiple of 64)
+    const float qs = EPI == SR_EPI_BIAS && ep.q_scale != 0.f && colw < ep.q_cols ? ep.q_scale : 1.f;
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int row = rowbase + mi * 16 + lr;
@@ -142,6 +152,10 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
         for (int ni = 0; ni < 4; ++ni) {
           float v[4];
           biased(mi, ni, v);
+          if (qs != 1.f) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] *= qs;
+          }
           if constexpr (EPI == SR_EPI_BIAS_GELU) {
             if (ep.aux) save_aux(row, colw + ni * 16 + 4 * lg, v);
 #pragma unroll
@@ -183,6 +197,7 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
     const float* nb = region == 0 ? ep.qn_b : ep.kn_b;
     const bool do_norm = qk && nw != nullptr;
     const bool do_rope = qk && ep.rope_cos != nullptr;
+    const float q_scale = ep.q_scale != 0.f && colw < ep.q_cols ? ep.q_scale : 1.f;  // wave-uniform
     float4 w4[4], b4[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
@@ -244,6 +259,12 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
           v[3][r] = x1;
         }
       }
+      if (q_scale != 1.f) {  // c*q for the attention, rounded once (sr_attn_desc.q_scaled)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[ni][r] *= q_scale;
+      }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) emit(row, colw + ni * 16 + 4 * lg, v[ni]);
     }
@@ -288,6 +309,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
   } else {
     produce<T, EPI, MT>(g, acc, rowbase, colw, lr, lg, [&](int row, int col, const float (&v)[4]) {
       if (row >= g.M || col >= g.N) return;
+      static_assert(sizeof(OutT<T, EPI>) == (EPI == SR_EPI_BIAS_RESID || EPI == SR_EPI_F32 ? 4 : sizeof(T)),
+                    "row_slice's element sizes must match these stores");
       if constexpr (EPI == SR_EPI_BIAS_RESID) {
         float4* p = (float4*)((float*)g.out + (int64_t)row * g.ldo + col);
         float4 xv = *p;
@@ -362,11 +385,14 @@ __device__ __forceinline__ void bias_full(const GemmArgs& g, f32x4 (&acc)[8][4],
   for (int ni = 0; ni < 4; ++ni)
     bs[ni] = ep.bias ? *(const f32x4*)(ep.bias + colw + ni * 16 + 4 * lg) : f32x4{0.f, 0.f, 0.f, 0.f};
   bf16* ob = (bf16*)g.out + (int64_t)(rowbase + lr) * g.ldo + colw + 4 * lg;
+  // the Q block of a plain-bias QKV projection, scaled (see produce)
+  const float qs = EPI == SR_EPI_BIAS && ep.q_scale != 0.f && colw < ep.q_cols ? ep.q_scale : 1.f;
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       f32x4 v = acc[mi][ni] + bs[ni];
+      if (qs != 1.f) v *= qs;
       if constexpr (EPI == SR_EPI_BIAS_GELU) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = sr::gelu_erf_fast(v[r]);
@@ -595,6 +621,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
   f32x4 v = *(const f32x4*)(g.partial + (int64_t)row * g.N + col);
   for (int z = 1; z < slices; ++z) v += *(const f32x4*)(g.partial + ((int64_t)z * g.M + row) * g.N + col);
   if (g.ep.bias) v += *(const f32x4*)(g.ep.bias + col);
+  if (EPI == SR_EPI_BIAS && g.ep.q_scale != 0.f && col < g.ep.q_cols) v *= g.ep.q_scale;
   if constexpr (EPI == SR_EPI_BIAS_GELU) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = sr::is_bf16<T>::value ? sr::gelu_erf_fast(v[r]) : sr::gelu_erf(v[r]);
@@ -895,14 +922,16 @@ int launch(const GemmArgs& a, hipStream_t s) {
   return sr::check_launch("sr_gemm");
 }
 
-// Rows [r0, r0 + rows) of a GEMM as a GEMM of its own: A / out / aux and the QKV epilogue's row
-// positions advanced by r0 (every epilogue but PATCH, whose row remap is absolute).
-static GemmArgs row_slice(const GemmArgs& a, int epi, int r0, int rows) {
+// Rows [r0, r0 + rows) of a bf16 GEMM as a GEMM of its own: A / out / aux and the QKV epilogue's row
+// positions advanced by r0 (every epilogue but PATCH, whose row remap is absolute).  Element sizes
+// come from OutT / AuxT, the types the epilogues store (no hand-kept table).
+template <int EPI>
+static GemmArgs row_slice(const GemmArgs& a, int r0, int rows) {
+  static_assert(EPI != SR_EPI_PATCH, "PATCH rows map to absolute output rows");
   GemmArgs b = a;
   b.A += (int64_t)r0 * a.lda_b;
-  const int oes = (epi == SR_EPI_BIAS_RESID || epi == SR_EPI_F32) ? 4 : 2;  // bf16 GEMMs only
-  b.out = (char*)a.out + (int64_t)r0 * a.ldo * oes;
-  if (a.ep.aux) b.ep.aux = (char*)a.ep.aux + (int64_t)r0 * a.ep.ld_aux * 2;
+  b.out = (char*)a.out + (int64_t)r0 * a.ldo * (int64_t)sizeof(OutT<bf16, EPI>);
+  if (a.ep.aux) b.ep.aux = (char*)a.ep.aux + (int64_t)r0 * a.ep.ld_aux * (int64_t)sizeof(AuxT<bf16>);
   if (a.ep.pos_yx) b.ep.pos_yx += 2 * (int64_t)r0;
   else if (a.ep.pos_rowmap) b.ep.pos_rowmap += r0;
   else b.ep.pos_row_base += r0;
@@ -929,7 +958,7 @@ int launch256_tail(GemmArgs a, hipStream_t s) {
       head.M = main_rows;
       int rc = launch256<EPI>(head, s);
       if (rc != SR_OK) return rc;
-      rc = launch<bf16, EPI>(row_slice(a, EPI, main_rows, rest), s);
+      rc = launch<bf16, EPI>(row_slice<EPI>(a, main_rows, rest), s);
       // the launch the time goes to
       sr::note_kernel(use_persist(EPI, whole) ? "gemm256_persist_kernel<%d>" : "gemm256_kernel<%d>", EPI);
       return rc;
@@ -1099,6 +1128,10 @@ static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda
     SR_CHECK(ldo % 4 == 0 && ((uintptr_t)out % 16) == 0, SR_EINVAL, "sr_gemm: F32 output must be 16-B aligned");
   if (epi == SR_EPI_PATCH)
     SR_CHECK(ep->row_add && ep->seg_rows > 0 && ep->seg_stride >= ep->seg_rows, SR_EINVAL, "sr_gemm: PATCH params");
+  if (ep->q_scale != 0.f)
+    SR_CHECK((epi == SR_EPI_BIAS || epi == SR_EPI_QKV) && ep->q_cols >= 0 && ep->q_cols % 64 == 0 && ep->q_cols <= N &&
+                 ep->q_scale == ep->q_scale,
+             SR_EINVAL, "sr_gemm: q_scale needs the BIAS or QKV epilogue and q_cols a multiple of 64 within N");
   if (epi == SR_EPI_QKV) {
     SR_CHECK(ep->head_dim == 64 && ep->embed_dim % 64 == 0 && ep->embed_dim > 0, SR_EUNSUPPORTED,
              "sr_gemm: QKV epilogue needs head_dim 64 (got %d)", ep->head_dim);

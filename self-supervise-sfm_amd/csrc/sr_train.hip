@@ -330,13 +330,21 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
   }
 }
 
+// row chunks of the partial pass (~1024 partial workgroups of >= 16 rows): the workspace holds
+// chunks x N floats (sr_colsum_workspace_floats)
+static int colsum_chunks(int M, int N, int& rpc) {
+  const int64_t gx = (N / 4 + 255) / 256;
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 15) / 16));
+  rpc = (M + chunks - 1) / chunks;
+  return (M + rpc - 1) / rpc;
+}
+
 int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
                   float scale, float* ws) {
   // ~1024 partial workgroups of >= 16 rows, then the parallel final reduction
   const int64_t gx = (N / 4 + 255) / 256;
-  int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 15) / 16));
-  const int rpc = (M + chunks - 1) / chunks;
-  chunks = (M + rpc - 1) / rpc;
+  int rpc;
+  const int chunks = colsum_chunks(M, N, rpc);
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(colsum_partial_kernel<bf16>, dim3((unsigned)gx, chunks), dim3(256), 0, s, (const bf16*)X, ldx,
                        M, N, rpc, ws);
@@ -947,12 +955,21 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   return sr::check_launch("sr_gemm_wgrad");
 }
 
+extern "C" int64_t sr_colsum_workspace_floats(int M, int N) {
+  if (M <= 0 || N <= 0 || N % 4) return 0;
+  int rpc;
+  return (int64_t)colsum_chunks(M, N, rpc) * N;
+}
+
 extern "C" int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out,
-                         int accumulate, float scale, float* workspace) {
+                         int accumulate, float scale, float* workspace, int64_t workspace_floats) {
   SR_CHECK(X && out && workspace, SR_EINVAL, "sr_colsum: null pointer");
   SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_colsum: bad dtype");
   SR_CHECK(M > 0 && N > 0 && N % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)out % 16) == 0, SR_EINVAL,
            "sr_colsum: bad shape M=%d N=%d ldx=%lld", M, N, (long long)ldx);
+  SR_CHECK(workspace_floats >= sr_colsum_workspace_floats(M, N) && ((uintptr_t)workspace % 16) == 0, SR_EINVAL,
+           "sr_colsum: workspace of %lld floats, needs %lld (sr_colsum_workspace_floats), 16-B aligned",
+           (long long)workspace_floats, (long long)sr_colsum_workspace_floats(M, N));
   return colsum_launch((hipStream_t)stream, dtype, X, ldx, M, N, out, accumulate, scale, workspace);
 }
 

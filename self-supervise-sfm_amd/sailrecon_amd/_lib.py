@@ -39,6 +39,7 @@ class GemmEpi(ctypes.Structure):
         ("tokens_per_frame", _i32), ("patch_start", _i32), ("grid_w", _i32),
         ("seg_rows", _i32), ("seg_stride", _i32), ("seg_offset", _i32), ("row_add", _vp),
         ("aux", _vp), ("ld_aux", _i64),
+        ("q_scale", _f32), ("q_cols", _i32),
     ]
 
 
@@ -71,6 +72,8 @@ class AttnDesc(ctypes.Structure):
         ("sweep_stats", _vp),
         ("key_box", _vp),
         ("value_box", _vp),
+        ("key_norm2", _vp),
+        ("q_scaled", _i32),
     ]
 
 
@@ -164,7 +167,8 @@ _PROTOS = {
     # training step
     "sr_gemm_wgrad": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp,
                              _i32, _vp]),
-    "sr_colsum": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i32, _f32, _vp]),
+    "sr_colsum": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i32, _f32, _vp, _i64]),
+    "sr_colsum_workspace_floats": (_i64, [_i32, _i32]),
     "sr_layernorm_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _f32, _vp, _i64, _vp, _i64, _vp, _vp,
                                 _i32, _i32, _vp, _vp]),
     "sr_qk_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),

@@ -95,16 +95,14 @@ class Attention(nn.Module):
         if self.rope is not None and pos is not None:
             rope = self.rope.tables(self.head_dim, int(pos.max()) + 1, x.device)
             pos_yx = pos.reshape(B * N, 2).to(device=x.device, dtype=torch.int32).contiguous()
-            epi = runtime.qkv_params(pa, rope, pos_yx=pos_yx)
+            epi = runtime.qkv_params(pa, rope, prescale=True, pos_yx=pos_yx)
         else:
-            epi = runtime.qkv_params(pa, None)
-        if epi is None:
-            ops.gemm(xa, pa.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pa.b_qkv)
-        else:
-            ops.gemm(xa, pa.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pa.b_qkv, qkv=epi)
+            epi = runtime.qkv_params(pa, None, prescale=True)
+        qs = runtime.q_prescale(pa)  # bf16: c*q rounded once by the GEMM (0 in fp32 mode)
+        runtime.qkv_gemm(pa, xa, pa.w_qkv, qkv, pa.b_qkv, epi, qs)
         o = torch.empty(B * N, C, device=x.device, dtype=dtype)
         if attn_mask is None:
-            runtime.frame_attend(pa, B, N)(qkv, o)
+            runtime.frame_attend(pa, B, N, q_scaled=qs > 0)(qkv, o)
         else:
             mode, m = sdpa_mask(attn_mask, B, self.num_heads, N, N, x.device)
             ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=self.num_heads,

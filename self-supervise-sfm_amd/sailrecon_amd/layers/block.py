@@ -67,18 +67,19 @@ class Block(nn.Module):
         if self.attn.rope is not None and pos is not None:
             rope = self.attn.rope.tables(pb.head_dim, int(pos.max()) + 1, x.device)
             pos_yx = pos.reshape(B * N, 2).to(device=x.device, dtype=torch.int32).contiguous()
-            qkv_epi = runtime.qkv_params(pb, rope, pos_yx=pos_yx)
+            qkv_epi = runtime.qkv_params(pb, rope, prescale=True, pos_yx=pos_yx)
         else:
-            qkv_epi = runtime.qkv_params(pb, None)
+            qkv_epi = runtime.qkv_params(pb, None, prescale=True)
+        qs = runtime.q_prescale(pb)  # bf16: the QKV GEMM writes c*q, rounded once (0 in fp32 mode)
         if attn_mask is None:
-            attend = runtime.frame_attend(pb, B, N)
+            attend = runtime.frame_attend(pb, B, N, q_scaled=qs > 0)
         else:
             mode, m = sdpa_mask(attn_mask, B, pb.heads, N, N, x.device)
 
             def attend(qkv, o):
                 ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=pb.heads, head_dim=pb.head_dim,
                               batch=B, lq=N, q_bstride=N, l0=N, k0_bstride=N, mask_mode=mode, mask=m)
-        runtime.run_block(pb, xf, 0, B * N, sc, attend, qkv_epi)
+        runtime.run_block(pb, xf, 0, B * N, sc, attend, qkv_epi, q_scale=qs)
         return xf.view(B, N, C).to(x.dtype)
 
 

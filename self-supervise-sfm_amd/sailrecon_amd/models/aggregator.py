@@ -251,8 +251,11 @@ class Aggregator(nn.Module):
             nblk = len(dino.blocks)
             for i, blk in enumerate(dino.blocks):
                 pb = blk.packed(dtype)
-                p = runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True), None,
-                                      pending=pending, defer=i < nblk - 1)
+                qs = runtime.q_prescale(pb)  # c*q rounded once by the QKV GEMM (runtime.q_prescale)
+                p = runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True,
+                                                                            q_scaled=qs > 0),
+                                      runtime.qkv_params(pb, None, prescale=True), pending=pending,
+                                      defer=i < nblk - 1, q_scale=qs)
                 if p is not None:
                     pending.append(p)
             assert not pending
@@ -359,8 +362,9 @@ class Aggregator(nn.Module):
         pending = []  # the global / reloc blocks' fc2 residuals, folded into the next frame block's LN1
         for l in range(self.depth):
             pb = self.frame_blocks[l].packed(dtype)
-            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True),
-                              runtime.qkv_params(pb, rope, pos_row_base=0, **posctx), pending=pending)
+            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True, q_scaled=_qs(pb)),
+                              runtime.qkv_params(pb, rope, prescale=True, pos_row_base=0, **posctx), pending=pending,
+                              q_scale=runtime.q_prescale(pb))
             if l in out_maps and Nq_l > 0:  # frame half of the intermediate, :403-413
                 for b in range(B):
                     ops.copy_rows(out_maps[l][b].view(Nq_l * P, 2 * C)[:, :C],
@@ -454,8 +458,9 @@ class Aggregator(nn.Module):
         out_maps = {l: torch.empty(1, S, P, 2 * C, device=dev, dtype=torch.float32) for l in self.intermediate_layer_idx}
         for l in range(self.depth):
             pb = self.frame_blocks[l].packed(dtype)
-            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True),
-                              runtime.qkv_params(pb, rope, pos_row_base=0, **posctx))
+            runtime.run_block(pb, x, 0, R, sc, runtime.frame_attend(pb, F_, P, tail_readable=True, q_scaled=_qs(pb)),
+                              runtime.qkv_params(pb, rope, prescale=True, pos_row_base=0, **posctx),
+                              q_scale=runtime.q_prescale(pb))
             if l in out_maps:
                 ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, :C], x, R)
             pr = self.global_reloc_blocks[l].packed(dtype)
@@ -466,8 +471,10 @@ class Aggregator(nn.Module):
                               batch=F_, lq=P, q_bstride=P, l0=n_sub, k0_bstride=0, k1=qkv[:, C:2 * C],
                               v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
                               key_norm_max=runtime.key_norm_bound(pr),
-                              query_norm_max=runtime.query_norm_bound(pr))
-            runtime.run_block(pr, x, 0, R, sc, attend_cached, runtime.qkv_params(pr, rope, pos_row_base=0, **posctx))
+                              query_norm_max=runtime.query_norm_bound(pr), q_scaled=_qs(pr))
+            runtime.run_block(pr, x, 0, R, sc, attend_cached,
+                              runtime.qkv_params(pr, rope, prescale=True, pos_row_base=0, **posctx),
+                              q_scale=runtime.q_prescale(pr))
             if l in out_maps:
                 ops.copy_rows(out_maps[l][0].view(R, 2 * C)[:, C:], x, R)
         assert self.depth - 1 in out_maps, \
@@ -524,12 +531,8 @@ class Aggregator(nn.Module):
             kv_all = ws.get("kv_all", La, 2 * C, dtype, dev)
             kv_loc = ws.get("kv_loc", La_l, 2 * C, dtype, dev)
             ops.layernorm(xs, pg.ln1_w, pg.ln1_b, pg.eps, xn)
-            epi = runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx)
-            if epi is None:
-                ops.gemm(xn, pg.w_qkv[:C], qkv[:, :C], _lib.SR_EPI_BIAS, bias=_sl(pg.b_qkv, 0, C), tag="gemm")
-            else:
-                ops.gemm(xn, pg.w_qkv[:C], qkv[:, :C], _lib.SR_EPI_QKV, bias=_sl(pg.b_qkv, 0, C), qkv=epi,
-                         tag="gemm")
+            epi = runtime.qkv_params(pg, rope, prescale=True, pos_row_base=a0, **posctx)
+            runtime.qkv_gemm(pg, xn, pg.w_qkv[:C], qkv[:, :C], _sl(pg.b_qkv, 0, C), epi, runtime.q_prescale(pg))
             self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
             work_kv = gather_rows(kv_all, kv_loc, [c * P for c in a_counts], group, r)
         if paired:
@@ -541,8 +544,8 @@ class Aggregator(nn.Module):
             # reloc own-frame pass folds the subsample pass in, and both blocks' tails follow
             rows, La = Nq_l * P, q0 - a0
             n_full = n_sub_all // 64 * 64
-            epi_r = runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx)
-            epi_g = runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx)
+            epi_r = runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx)
+            epi_g = runtime.qkv_params(pg, rope, prescale=True, pos_row_base=a0, **posctx)
             epi_s = runtime.qkv_params(pr, rope, pos_rowmap=rowmap, **posctx) if defer_kv else None
             if epi_s is not None:
                 epi_s["col_offset"] = C
@@ -555,8 +558,8 @@ class Aggregator(nn.Module):
                 ops.layernorm(x[a0:q0], pg.ln1_w, pg.ln1_b, pg.eps, sc.xn[a0:q0])
                 ops.gemm_group(probs, _lib.SR_EPI_QKV, tag="gemm")
             else:
-                runtime.run_block_head(pr, x, q0, q1, sc, epi_r)
-                runtime.run_block_head(pg, x, a0, q0, sc, epi_g)
+                runtime.run_block_head(pr, x, q0, q1, sc, epi_r, runtime.q_prescale(pr))
+                runtime.run_block_head(pg, x, a0, q0, sc, epi_g, runtime.q_prescale(pg))
                 if defer_kv:
                     self._kv_gemm(pr, xn_sub, kv_sub_all, rope, dict(pos_rowmap=rowmap, **posctx))
             qkv_r, qkv_g = sc.qkv[q0:q1], sc.qkv[a0:q0]
@@ -564,10 +567,11 @@ class Aggregator(nn.Module):
             lse_a = lse_a[0]
             ops.attention_pair(
                 dict(q=qkv_g[:, 0:C], k0=qkv_g[:, C:2 * C], v0=qkv_g[:, 2 * C:3 * C], o=sc.o[a0:q0], lq=La, l0=La,
-                     key_norm_max=runtime.key_norm_bound(pg), query_norm_max=runtime.query_norm_bound(pg)),
+                     key_norm_max=runtime.key_norm_bound(pg), query_norm_max=runtime.query_norm_bound(pg),
+                     q_scaled=_qs(pg)),
                 dict(q=qkv_r[:, 0:C], k0=kv_sub_all[:n_full, 0:C], v0=kv_sub_all[:n_full, C:2 * C], o=o_a, lq=rows,
                      l0=n_full, key_norm_max=runtime.key_norm_bound(pr), query_norm_max=runtime.query_norm_bound(pr),
-                     lse=lse_a.view(-1)),
+                     lse=lse_a.view(-1), q_scaled=_qs(pr)),
                 heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
             self._reloc_own_pass(pr, qkv_r, kv_sub_all, sc.o[q0:q1], o_a, lse_a, Nq_l, P, n_sub_all, n_full)
             keep(runtime.run_block_tail(pr, x, q0, q1, sc, defer=defer))
@@ -600,21 +604,23 @@ class Aggregator(nn.Module):
                                   o_a, heads=pr.heads, head_dim=pr.head_dim, batch=1, lq=rows,
                                   q_bstride=0, l0=n_full, k0_bstride=0, tag="attn_reloc", key_norm_max=kb,
                                   query_norm_max=qb,
-                                  lse=lse_a.view(-1), tail_readable=True)
+                                  lse=lse_a.view(-1), tail_readable=True, q_scaled=_qs(pr))
                     self._reloc_own_pass(pr, qkv, kv_sub_all, o, o_a, lse_a, Nq_l, P, n_sub_all, n_full)
                     return
                 ops.attention(qkv[:, 0:C], kv_sub_all[:, 0:C], kv_sub_all[:, C:2 * C], o, heads=pr.heads,
                               head_dim=pr.head_dim, batch=Nq_l, lq=P, q_bstride=P, l0=n_sub_all, k0_bstride=0,
                               k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                              key_norm_max=kb, query_norm_max=qb, tail_readable=True)
+                              key_norm_max=kb, query_norm_max=qb, tail_readable=True, q_scaled=_qs(pr))
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream(dev))  # frame block + subsample K/V are done
                 with torch.cuda.stream(side):
                     runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
-                                      runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
+                                      runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
+                                      q_scale=runtime.q_prescale(pr))
             else:
                 keep(runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
-                                       runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx), defer=defer))
+                                       runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
+                                       defer=defer, q_scale=runtime.q_prescale(pr)))
         _wait(work_sub)  # a rank without query frames still fed the others (send buffer reuse)
         if G > 1:
             o, q = sc.o[a0:q0], sc.qkv[a0:q0, 0:C]
@@ -629,7 +635,8 @@ class Aggregator(nn.Module):
             def attend_global(qkv, o):
                 self._global_attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, pg, La, La)
             keep(runtime.run_block(pg, x, a0, q0, sc, attend_global,
-                                   runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx), defer=defer))
+                                   runtime.qkv_params(pg, rope, prescale=True, pos_row_base=a0, **posctx),
+                                   defer=defer, q_scale=runtime.q_prescale(pg)))
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)  # join before the next frame block
         return out
@@ -663,7 +670,7 @@ class Aggregator(nn.Module):
                 ops.attention_partials(q, kv[:, 0:C], kv[:, C:2 * C], o_parts[p0 * lq:(p0 + p) * lq],
                                        lse_parts[p0:p0 + p], heads=H, head_dim=D, lq=lq, l0=kv.shape[0], parts=p,
                                        tag="attn_global", key_norm_max=kb, query_norm_max=qb,
-                                       tail_readable=_SHARD_TAIL)
+                                       tail_readable=_SHARD_TAIL, q_scaled=_qs(pg))
                 p0 += p
             ops.attn_merge_n(o_parts, lse_parts, o, parts=total, rows=lq, heads=H, head_dim=D)
             return
@@ -672,13 +679,14 @@ class Aggregator(nn.Module):
         lse_rem = ws.get("lse_rem", H, lq, torch.float32, q.device)
         o_rem = ws.get("o_rem", lq, C, o.dtype, q.device)
         ops.attention(q, kv_loc[:, 0:C], kv_loc[:, C:2 * C], o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0,
-                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc, key_norm_max=kb, query_norm_max=qb)
+                      l0=lq, k0_bstride=0, tag="attn_global", lse=lse_loc, key_norm_max=kb, query_norm_max=qb,
+                      q_scaled=_qs(pg))
         _wait(work_kv)
         (s0, n0), (s1, n1) = segs[0], (segs[1] if len(segs) > 1 else (0, 0))
         ops.attention(q, kv_all[s0:s0 + n0, 0:C], kv_all[s0:s0 + n0, C:2 * C], o_rem, heads=H, head_dim=D, batch=1,
                       lq=lq, q_bstride=0, l0=n0, k0_bstride=0, k1=kv_all[s1:s1 + n1, 0:C] if n1 else None,
                       v1=kv_all[s1:s1 + n1, C:2 * C] if n1 else None, l1=n1, k1_bstride=0, tag="attn_global",
-                      lse=lse_rem, key_norm_max=kb, query_norm_max=qb)
+                      lse=lse_rem, key_norm_max=kb, query_norm_max=qb, q_scaled=_qs(pg))
         ops.attn_merge(o, lse_loc, o_rem, lse_rem, o, heads=H, head_dim=D, tag="attn_merge")
 
     def _global_attention(self, q, k, v, o, pg, lq, lk):
@@ -687,11 +695,11 @@ class Aggregator(nn.Module):
                 self._fp8_ws = ops.Fp8Workspace()
             ops.attention_qk8(q, k, v, o, heads=pg.heads, batch=1, lq=lq, q_bstride=0, l0=lk, k0_bstride=0,
                               tag="attn_global", ws=self._fp8_ws, fp8_v=self.fp8_v,
-                              key_norm_max=runtime.key_norm_bound(pg))
+                              key_norm_max=runtime.key_norm_bound(pg), q_scaled=_qs(pg))
         else:
             ops.attention(q, k, v, o, heads=pg.heads, head_dim=pg.head_dim, batch=1, lq=lq, q_bstride=0, l0=lk,
                           k0_bstride=0, tag="attn_global", key_norm_max=runtime.key_norm_bound(pg),
-                          query_norm_max=runtime.query_norm_bound(pg))
+                          query_norm_max=runtime.query_norm_bound(pg), q_scaled=_qs(pg))
 
     @staticmethod
     def _reloc_own_pass(pr, qkv, kv_sub_all, o, o_a, lse_a, nq: int, P: int, n_sub_all: int, n_full: int) -> None:
@@ -703,12 +711,13 @@ class Aggregator(nn.Module):
             ops.attention(qkv[:, 0:C], kv_sub_all[n_full:, 0:C], kv_sub_all[n_full:, C:2 * C], o, heads=pr.heads,
                           head_dim=pr.head_dim, batch=nq, lq=P, q_bstride=P, l0=n_sub_all - n_full, k0_bstride=0,
                           k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:3 * C], l1=P, k1_bstride=P, tag="attn_reloc",
-                          key_norm_max=kb, query_norm_max=qb, tail_readable=True, merge_o=o_a, merge_lse=lse_a)
+                          key_norm_max=kb, query_norm_max=qb, tail_readable=True, merge_o=o_a, merge_lse=lse_a,
+                          q_scaled=_qs(pr))
         else:
             ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pr.heads, head_dim=pr.head_dim,
                           batch=nq, lq=P, q_bstride=P, l0=P, k0_bstride=P, tag="attn_reloc", key_norm_max=kb,
                           query_norm_max=qb,
-                          tail_readable=True, merge_o=o_a, merge_lse=lse_a)
+                          tail_readable=True, merge_o=o_a, merge_lse=lse_a, q_scaled=_qs(pr))
 
     def _paired_attention(self, pr, pg, dtype, rows: int, La: int, n_sub: int) -> bool:
         """Single GPU, bf16, split reloc, a global query set that fills the chip without key
@@ -766,6 +775,11 @@ _RELOC_SPLIT_MIN_WG = int(os.environ.get("SR_RELOC_SPLIT_MIN_WG", "2048"))
 
 def _sl(t, a, b):
     return None if t is None else t[a:b]
+
+
+def _qs(pb) -> bool:
+    """Whether pb's QKV GEMMs here write c*q (runtime.q_prescale): the attention takes q_scaled."""
+    return runtime.q_prescale(pb) > 0
 
 
 def _wait(works):

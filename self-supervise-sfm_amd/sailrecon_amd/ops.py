@@ -206,15 +206,20 @@ def _fill_qkv_epi(ep: GemmEpi, qkv: dict) -> None:
     ep.tokens_per_frame = qkv.get("tokens_per_frame", 1)
     ep.patch_start = qkv.get("patch_start", 0)
     ep.grid_w = qkv.get("grid_w", 1)
+    # the Q block of a full q|k|v output leaves as c*q, rounded once (runtime.q_prescale)
+    if qkv.get("q_scale") and ep.col_offset == 0:
+        ep.q_scale, ep.q_cols = float(qkv["q_scale"]), ep.embed_dim
 
 
 def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] = None,
          gamma: Optional[Tensor] = None, rows: Optional[int] = None, qkv: Optional[dict] = None,
          patch: Optional[dict] = None, tag: Optional[str] = None, splits: Optional[int] = None,
-         aux: Optional[Tensor] = None) -> None:
+         aux: Optional[Tensor] = None, q_scale: float = 0.0, q_cols: int = 0) -> None:
     """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows).
     ``splits`` K slices (sr_gemm_splitk); default: automatic for few rows.  ``aux`` (a's dtype,
-    [M, N] view): BIAS_GELU / QKV store the pre-activation there; GELU_BWD reads it."""
+    [M, N] view): BIAS_GELU / QKV store the pre-activation there; GELU_BWD reads it.
+    ``q_scale`` / ``q_cols`` (BIAS / QKV): output columns [0, q_cols) leave multiplied by q_scale
+    before their one rounding (sr_gemm_epi.q_scale; a QKV dict's "q_scale" key sets both)."""
     lda = _rowmajor(a, "a")
     ldw = _rowmajor(w, "w")
     ldo = _rowmajor(out, "out")
@@ -229,6 +234,8 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
     ep.gamma = _p(gamma)
     if qkv is not None:
         _fill_qkv_epi(ep, qkv)
+    if q_scale:
+        ep.q_scale, ep.q_cols = float(q_scale), int(q_cols)
     if aux is not None:
         if aux.dtype != a.dtype:
             raise TypeError("gemm: aux must have the operand dtype")
@@ -292,6 +299,8 @@ def gemm_group(problems, epi: int, tag: Optional[str] = None) -> None:
         q.ep.bias, q.ep.gamma = _p(p.get("bias")), _p(p.get("gamma"))
         if p.get("qkv") is not None:
             _fill_qkv_epi(q.ep, p["qkv"])
+        if p.get("q_scale"):
+            q.ep.q_scale, q.ep.q_cols = float(p["q_scale"]), int(p["q_cols"])
         flops += 2.0 * a.shape[0] * N * K
         nbytes += (a.shape[0] * K + N * K) * a.element_size() + a.shape[0] * N * out.element_size()
     if tag == "gemm":
@@ -348,7 +357,7 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
               scale: Optional[float] = None, tag: Optional[str] = None, lse: Optional[Tensor] = None,
               key_norm_max: float = 0.0, mask: Optional[Tensor] = None, tail_readable: bool = False,
               merge_o: Optional[Tensor] = None, merge_lse: Optional[Tensor] = None,
-              sweep_stats: Optional[Tensor] = None, query_norm_max: float = 0.0) -> None:
+              sweep_stats: Optional[Tensor] = None, query_norm_max: float = 0.0, q_scaled: bool = False) -> None:
     """softmax(scale q k^T) v over segment 0 (+ segment 1) keys; see sr_attn_desc.  ``mask``
     (mask_mode SR_MASK_DENSE: bool / uint8, nonzero = attend; SR_MASK_ADD: fp32 added to the
     scores) is a [batch, heads, lq, l0 + l1] view (broadcast dims may have stride 0, the last dim
@@ -367,7 +376,9 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
     DISJOINT key set ([R, >= heads*head_dim] bf16, row item*q_bstride + i) and its log2-domain LSE
     (fp32 [heads, R]); o then receives the softmax over the union (sr_attn_desc.merge_o).
     ``sweep_stats`` (int32 [2], caller-zeroed, bf16): the launch adds its waves on the
-    hand-scheduled sweep / on the compiled loop (sr_attn_desc.sweep_stats); it forces one launch."""
+    hand-scheduled sweep / on the compiled loop (sr_attn_desc.sweep_stats); it forces one launch.
+    ``q_scaled`` (bf16): q holds c*q, c = scale*log2(e), rounded once by the QKV GEMM's epilogue
+    (runtime.q_prescale, sr_attn_desc.q_scaled); False: the kernel forms c*q itself."""
     parts = key_split_parts(dtype=q.dtype, batch=batch, lq=lq, heads=heads, l0=l0, l1=l1, mask_mode=mask_mode)
     if sweep_stats is not None:
         parts = 1
@@ -385,12 +396,12 @@ def attention(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, head_
         o_parts, lse_parts = key_split_workspace(q.device, parts, lq, heads * head_dim, heads)
         attention_partials(q, k0, v0, o_parts, lse_parts, heads=heads, head_dim=head_dim, lq=lq, l0=l0, parts=parts,
                            scale=scale, tag=tag, key_norm_max=key_norm_max, tail_readable=tail_readable,
-                           query_norm_max=query_norm_max)
+                           query_norm_max=query_norm_max, q_scaled=q_scaled)
         attn_merge_n(o_parts, lse_parts, o, parts=parts, rows=lq, heads=heads, head_dim=head_dim, lse_out=lse)
         return
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, mask_mode=mask_mode,
-                   n_anchor=n_anchor, scale=scale, lse=lse)
+                   n_anchor=n_anchor, scale=scale, lse=lse, q_scaled=q_scaled)
     if tail_readable:
         d.tail_rows_readable = 64
     _set_sweep_stats(d, sweep_stats)
@@ -436,8 +447,8 @@ _ATTN_PAIR = os.environ.get("SR_ATTN_PAIR", "1") != "0"
 
 def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional[str] = None) -> None:
     """Two single-query-set bf16 attentions in ONE launch (sr_attention_pair): ``a`` / ``b`` are
-    dicts with q, k0, v0, o, lq, l0, key_norm_max and optionally lse, query_norm_max (keys as
-    attention()'s, batch 1, one segment).
+    dicts with q, k0, v0, o, lq, l0, key_norm_max and optionally lse, query_norm_max, q_scaled (keys
+    as attention()'s, batch 1, one segment).
     a's workgroups run first and b's fill the CUs a's last round leaves idle.  Both must pass
     pair_eligible (checked)."""
     descs = []
@@ -446,7 +457,7 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
         if not pair_eligible(p["q"].dtype, p["l0"], head_dim, p["key_norm_max"]):
             raise ValueError("attention_pair: a problem does not qualify (see pair_eligible)")
         d = _attn_desc(p["q"], p["k0"], p["v0"], p["o"], heads=heads, head_dim=head_dim, batch=1, lq=p["lq"],
-                       q_bstride=0, l0=p["l0"], k0_bstride=0, lse=p.get("lse"))
+                       q_bstride=0, l0=p["l0"], k0_bstride=0, lse=p.get("lse"), q_scaled=p.get("q_scaled", False))
         d.key_norm_max = float(p["key_norm_max"])
         _set_sweep_stats(d, p.get("sweep_stats"))
         _attach_key_box(d, p["k0"].device, p.get("query_norm_max", 0.0), "attn_key_box" + str(len(descs)))
@@ -470,7 +481,7 @@ _BOX_MIN_BOUND = (64.0 + 110.0) / 2
 
 
 def _attach_key_box(d: AttnDesc, device, query_norm_max: float, name: str) -> None:
-    """Set d.key_box, d.value_box and d.key_bound (the keys' actual max |k|^2, which tightens the
+    """Set d.key_box, d.value_box and d.key_norm2 (the keys' actual max |k|^2, which tightens the
     static key_norm_max) when the 2-norm score bound scale*log2(e)*|q|*|k| exceeds 87, above which the
     default window can miss: sr_attention_key_box over each key and value segment into a
     per-stream workspace, instances as sr_attention_bound_floats' (k0's, then k1's)."""
@@ -496,7 +507,7 @@ def _attach_key_box(d: AttnDesc, device, query_norm_max: float, name: str) -> No
                                        _p(ws[nb + off // 128:]), _p(sc)), "sr_attention_key_box")
         check(lib.sr_attention_key_box(stream, v, ldv, rows, bstride, n, d.heads, _p(ws[vb + off:]), None, _p(sc)),
               "sr_attention_key_box(values)")
-    d.key_box, d.value_box, d.key_bound = _p(ws), _p(ws[vb:]), _p(ws[nb:])
+    d.key_box, d.value_box, d.key_norm2 = _p(ws), _p(ws[vb:]), _p(ws[nb:])
 
 
 def _attach_scan_boxes(d: AttnDesc, device) -> None:
@@ -557,7 +568,7 @@ def key_split_workspace(device, parts: int, rows: int, cols: int, heads: int, na
 def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_parts: Tensor, *, heads: int,
                        head_dim: int, lq: int, l0: int, parts: int, scale: Optional[float] = None,
                        tag: Optional[str] = None, key_norm_max: float = 0.0, tail_readable: bool = False,
-                       query_norm_max: float = 0.0) -> None:
+                       query_norm_max: float = 0.0, q_scaled: bool = False) -> None:
     """One bf16 launch of ``parts`` items over equal key chunks of k0/v0 (item s: keys
     [s*l0/parts, (s+1)*l0/parts)) against the same lq queries: item s writes its normalised
     partial output at rows s*lq of o_parts and its LSE to lse_parts[s] ([heads, lq]).  The parts
@@ -569,7 +580,7 @@ def attention_partials(q: Tensor, k0: Tensor, v0: Tensor, o_parts: Tensor, lse_p
         raise ValueError("attention_partials: o_parts [parts*lq, C] / lse_parts fp32 [parts, heads, lq]")
     chunk = l0 // parts
     d = _attn_desc(q, k0, v0, o_parts, heads=heads, head_dim=head_dim, batch=parts, lq=lq, q_bstride=0, l0=chunk,
-                   k0_bstride=chunk, scale=scale, lse=lse_parts)
+                   k0_bstride=chunk, scale=scale, lse=lse_parts, q_scaled=q_scaled)
     d.o_bstride = lq
     if tail_readable:  # rows past k0/v0's end readable: each chunk's ragged tile may go to the asm sweep
         d.tail_rows_readable = 64
@@ -674,11 +685,11 @@ def quant_fp8_vt(v: Tensor, heads: int, dst: Tensor, exp_out: Tensor) -> None:
 def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, batch: int, lq: int, q_bstride: int,
                   l0: int, k0_bstride: int, scale: Optional[float] = None, tag: Optional[str] = None,
                   lse: Optional[Tensor] = None, ws: Optional[Fp8Workspace] = None, fp8_v: bool = False,
-                  key_norm_max: float = 0.0) -> None:
+                  key_norm_max: float = 0.0, q_scaled: bool = False) -> None:
     """attention() with q.k^T in block-scaled fp8 (BASELINE C5): q and k (bf16, head_dim 64) are
     quantised to e4m3 with one power-of-two scale each (q with scale*log2(e) folded in); V / P.V
     stay bf16 unless ``fp8_v`` (then V is quantised too and P enters the MFMA as e4m3).  One key
-    segment, no mask."""
+    segment, no mask.  ``q_scaled``: q already holds c*q (see attention), so it is quantised as is."""
     head_dim = 64
     d = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                    k0_bstride=k0_bstride, scale=scale, lse=lse)
@@ -689,7 +700,7 @@ def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, b
     q8, k8, ex = ws.get(q.shape[0], k0.shape[0], C, q.device)
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    quant_fp8(q[:, :C], d.scale * 1.4426950408889634, q8, ex[0:1])
+    quant_fp8(q[:, :C], 1.0 if q_scaled else d.scale * 1.4426950408889634, q8, ex[0:1])
     quant_fp8(k0[:, :C], 1.0, k8, ex[1:2])
     if fp8_v:
         if batch != 1:
@@ -708,7 +719,8 @@ def attention_qk8(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, *, heads: int, b
 
 
 def _attn_desc(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
-               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, lse=None) -> AttnDesc:
+               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, lse=None,
+               q_scaled=False) -> AttnDesc:
     d = AttnDesc()
     d.q, d.ldq = _p(q), _rowmajor(q, "q")
     d.k0, d.ldk0 = _p(k0), _rowmajor(k0, "k0")
@@ -723,6 +735,10 @@ def _attn_desc(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bs
     d.l1, d.k1_bstride = l1, k1_bstride
     d.mask_mode, d.n_anchor = mask_mode, n_anchor
     d.scale = head_dim ** -0.5 if scale is None else scale
+    if q_scaled:
+        if q.dtype != torch.bfloat16:
+            raise ValueError("attention: q_scaled is a bf16-path convention")
+        d.q_scaled = 1
     if lse is not None:
         if lse.dtype != torch.float32 or not lse.is_contiguous() or lse.numel() != batch * heads * lq:
             raise ValueError("attention: lse must be contiguous fp32 [batch, heads, lq]")
@@ -1068,9 +1084,11 @@ def colsum(x: Tensor, out: Tensor, *, rows: Optional[int] = None, cols: Optional
     N = x.shape[1] if cols is None else cols
     if out.dtype != torch.float32 or out.numel() < N:
         raise ValueError("colsum: out must be fp32 with >= cols elements")
-    ws = _train_ws(x.device, "colsum", min(2048, max(1, -(-M // 16))) * N)
-    rc = _lib.load().sr_colsum(_stream(x), dtype_code(x.dtype), _p(x), ldx, M, N, _p(out), int(accumulate),
-                               float(scale), _p(ws))
+    lib = _lib.load()
+    nws = lib.sr_colsum_workspace_floats(M, N)
+    ws = _train_ws(x.device, "colsum", max(1, nws))
+    rc = lib.sr_colsum(_stream(x), dtype_code(x.dtype), _p(x), ldx, M, N, _p(out), int(accumulate),
+                       float(scale), _p(ws), ws.numel())
     check(rc, "sr_colsum")
 
 

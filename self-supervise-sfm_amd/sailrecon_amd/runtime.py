@@ -188,16 +188,48 @@ def scratch(ws: Workspace, rows: int, dim: int, hidden: int, dtype: torch.dtype,
                         h=ws.get("h" + tag, rows, hidden, dtype, device))
 
 
-def qkv_params(pb: PackedBlock, rope: Optional[Tuple[Tensor, Tensor]], **pos) -> Optional[dict]:
-    """Epilogue parameters for the fused qkv GEMM; None if plain bias suffices."""
+# The attention's c*q (c = scale * log2(e): scores in the exp2 domain) is formed by the QKV GEMM's
+# epilogue from its fp32 value and rounded to bf16 ONCE (sr_gemm_epi.q_scale), and the attention
+# takes it as is (sr_attn_desc.q_scaled).  The reference rounds q once (autocast SDPA input,
+# attention.py:103-109) and scales inside SDPA; forming c * bf16(q) in the kernel instead rounded q
+# twice.  Forward-only (inference) convention: the training tape keeps plain q
+# for sr_attention_bwd.  SR_Q_PRESCALE=0 restores the in-kernel product (A/B).
+_Q_PRESCALE = os.environ.get("SR_Q_PRESCALE", "1") != "0"
+_LOG2E = 1.4426950408889634
+
+
+def q_prescale(pb: PackedBlock) -> float:
+    """c = head_dim^-0.5 * log2(e) for a bf16 pack (0.0: fp32 parity mode keeps plain q)."""
+    if not _Q_PRESCALE or pb.w_qkv.dtype != torch.bfloat16 or pb.head_dim != 64:
+        return 0.0
+    return pb.head_dim ** -0.5 * _LOG2E
+
+
+def qkv_params(pb: PackedBlock, rope: Optional[Tuple[Tensor, Tensor]], prescale: bool = False,
+               **pos) -> Optional[dict]:
+    """Epilogue parameters for the fused qkv GEMM; None if plain bias suffices.  ``prescale``: the
+    Q block leaves as c*q (q_prescale; the attention then takes q_scaled=True)."""
     if not pb.qk_norm and rope is None:
         return None
     d = dict(embed_dim=pb.dim, head_dim=pb.head_dim, qk_eps=pb.qk_eps,
              qn_w=pb.qn_w, qn_b=pb.qn_b, kn_w=pb.kn_w, kn_b=pb.kn_b)
+    if prescale and q_prescale(pb):
+        d["q_scale"] = q_prescale(pb)
     if rope is not None:
         d["rope_cos"], d["rope_sin"] = rope
         d.update(pos)
     return d
+
+
+def qkv_gemm(pb: PackedBlock, xn: Tensor, w: Tensor, out: Tensor, bias, qkv_epi: Optional[dict],
+             q_scale: float = 0.0) -> None:
+    """The QKV projection: the fused qk-norm / RoPE epilogue when ``qkv_epi`` is set, else plain bias
+    (DINO), whose Q block (the first pb.dim output columns) leaves scaled by ``q_scale`` if nonzero."""
+    if qkv_epi is None:
+        ops.gemm(xn, w, out, _lib.SR_EPI_BIAS, bias=bias, tag="gemm", q_scale=q_scale,
+                 q_cols=pb.dim if q_scale else 0)
+    else:
+        ops.gemm(xn, w, out, _lib.SR_EPI_QKV, bias=bias, qkv=qkv_epi, tag="gemm")
 
 
 # Residual updates folded into the next LayerNorm (VERDICT r3 item 3).  The reference's autocast
@@ -280,32 +312,29 @@ def mlp_residual(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
 
 def run_block(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
               attend: Callable[[Tensor, Tensor], None], qkv_epi: Optional[dict], tag: str = "blk",
-              pending: Optional[list] = None, defer: bool = False) -> Optional[Pending]:
+              pending: Optional[list] = None, defer: bool = False, q_scale: float = 0.0) -> Optional[Pending]:
     """x[r0:r1] <- Block(x[r0:r1]); ``attend(qkv_rows, o_rows)`` launches the attention.
     ``pending``: deferred residual updates of earlier blocks, applied by this block's LN1 (the list
-    is consumed).  ``defer``: leave this block's fc2 residual pending (returned; see mlp_residual)."""
+    is consumed).  ``defer``: leave this block's fc2 residual pending (returned; see mlp_residual).
+    ``q_scale``: the plain-bias QKV projection's Q block leaves scaled (qkv_gemm; a fused epilogue
+    carries its own in ``qkv_epi``)."""
     xs = x[r0:r1]
     xn, qkv, o = sc.xn[r0:r1], sc.qkv[r0:r1], sc.o[r0:r1]
     layernorm_pending(x, r0, r1, pb.ln1_w, pb.ln1_b, pb.eps, xn, pending)
-    if qkv_epi is None:
-        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
-    else:
-        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
+    qkv_gemm(pb, xn, pb.w_qkv, qkv, pb.b_qkv, qkv_epi, q_scale)
     attend(qkv, o)
     proj_residual_ln2(pb, xs, o, qkv, xn)
     return mlp_residual(pb, x, r0, r1, sc, defer)
 
 
-def run_block_head(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch, qkv_epi: Optional[dict]) -> None:
+def run_block_head(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch, qkv_epi: Optional[dict],
+                   q_scale: float = 0.0) -> None:
     """First half of run_block (LN1 + the QKV GEMM) when the attention is launched separately
     (the global and reloc blocks' attentions paired in one launch)."""
     xs = x[r0:r1]
     xn, qkv = sc.xn[r0:r1], sc.qkv[r0:r1]
     ops.layernorm(xs, pb.ln1_w, pb.ln1_b, pb.eps, xn)
-    if qkv_epi is None:
-        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_BIAS, bias=pb.b_qkv, tag="gemm")
-    else:
-        ops.gemm(xn, pb.w_qkv, qkv, _lib.SR_EPI_QKV, bias=pb.b_qkv, qkv=qkv_epi, tag="gemm")
+    qkv_gemm(pb, xn, pb.w_qkv, qkv, pb.b_qkv, qkv_epi, q_scale)
 
 
 def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch,
@@ -318,14 +347,16 @@ def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
     return mlp_residual(pb, x, r0, r1, sc, defer)
 
 
-def frame_attend(pb: PackedBlock, frames: int, tokens: int, tail_readable: bool = False) -> Callable[[Tensor, Tensor], None]:
+def frame_attend(pb: PackedBlock, frames: int, tokens: int, tail_readable: bool = False,
+                 q_scaled: bool = False) -> Callable[[Tensor, Tensor], None]:
     """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C]).
-    ``tail_readable``: the qkv buffers come from a Workspace (rows past the last frame readable)."""
+    ``tail_readable``: the qkv buffers come from a Workspace (rows past the last frame readable).
+    ``q_scaled``: the QKV GEMM wrote c*q (q_prescale)."""
     C, D = pb.dim, pb.head_dim
     kb, qb = key_norm_bound(pb), query_norm_bound(pb)
 
     def attend(qkv: Tensor, o: Tensor) -> None:
         ops.attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, heads=pb.heads, head_dim=D,
                       batch=frames, lq=tokens, q_bstride=tokens, l0=tokens, k0_bstride=tokens, tag="attn_frame",
-                      key_norm_max=kb, query_norm_max=qb, tail_readable=tail_readable)
+                      key_norm_max=kb, query_norm_max=qb, tail_readable=tail_readable, q_scaled=q_scaled)
     return attend

@@ -18,12 +18,17 @@ import torch.nn.functional as F
 from sailrecon_amd import _lib, ops as real_ops, runtime
 
 
-def gemm(a, w, out, epi, *, bias=None, gamma=None, rows=None, qkv=None, patch=None, tag=None):
+def gemm(a, w, out, epi, *, bias=None, gamma=None, rows=None, qkv=None, patch=None, tag=None, q_scale=0.0,
+         q_cols=0):
     M = a.shape[0] if rows is None else rows
     y = a[:M].float() @ w.float().t()
     if bias is not None:
         y = y + bias
+    if qkv is not None and qkv.get("q_scale") and qkv.get("col_offset", 0) == 0:  # sr_gemm_epi.q_scale
+        q_scale, q_cols = qkv["q_scale"], qkv["embed_dim"]
     if epi == _lib.SR_EPI_BIAS:
+        if q_scale:
+            y[:, :q_cols] *= q_scale
         out[:M] = y.to(out.dtype)
     elif epi == _lib.SR_EPI_BIAS_GELU:
         out[:M] = F.gelu(y).to(out.dtype)
@@ -59,6 +64,8 @@ def gemm(a, w, out, epi, *, bias=None, gamma=None, rows=None, qkv=None, patch=No
                     return torch.cat([v1 * c - v2 * s, v2 * c + v1 * s], 1)
                 seg = torch.cat([rot(seg[:, :2 * q], py), rot(seg[:, 2 * q:], px)], 1)
             y[:, h0:h0 + D] = seg
+        if q_scale:
+            y[:, :q_cols] *= q_scale
         out[:M] = y.to(out.dtype)
     else:
         raise ValueError(epi)
@@ -82,17 +89,19 @@ def _positions(qkv, M):
 def attention(q, k0, v0, o, *, heads, head_dim, batch, lq, q_bstride, l0, k0_bstride, k1=None, v1=None, l1=0,
               k1_bstride=0, mask_mode=_lib.SR_MASK_NONE, n_anchor=0, scale=None, tag=None, lse=None,
               key_norm_max=0.0, mask=None, tail_readable=False, merge_o=None, merge_lse=None, sweep_stats=None,
-              query_norm_max=0.0):
+              query_norm_max=0.0, q_scaled=False):
     """sr_attention's semantics (include/sfm_amd.h sr_attn_desc): the camera mask, SR_MASK_DENSE
     (nonzero = attend) / SR_MASK_ADD masks with zeros for a row without attended keys, and the
     merge-in of a disjoint key set's (merge_o, merge_lse).  sweep_stats (device diagnostics) is
-    rejected: there is no sweep here."""
+    rejected: there is no sweep here.  ``q_scaled``: q holds c*q, c = scale*log2(e)."""
     if sweep_stats is not None:
         raise NotImplementedError("cpu_ops.attention: sweep_stats counts GPU waves")
     if mask_mode in (_lib.SR_MASK_DENSE, _lib.SR_MASK_ADD) and mask is None:
         raise ValueError("cpu_ops.attention: dense / additive mask_mode without a mask")
     D = head_dim
     scale = D ** -0.5 if scale is None else scale
+    if q_scaled:  # (c q).k / log2(e) = scale q.k
+        scale = 1.0 / math.log2(math.e)
     for b in range(batch):
         qs = q[b * q_bstride:b * q_bstride + lq].float()
         ks = [k0[b * k0_bstride:b * k0_bstride + l0].float()]
@@ -142,14 +151,14 @@ def attn_merge(o_a, lse_a, o_b, lse_b, out, *, heads, head_dim, lse_out=None, ta
 
 
 def attention_partials(q, k0, v0, o_parts, lse_parts, *, heads, head_dim, lq, l0, parts, scale=None, tag=None,
-                       key_norm_max=0.0, tail_readable=False, query_norm_max=0.0):
+                       key_norm_max=0.0, tail_readable=False, query_norm_max=0.0, q_scaled=False):
     del tail_readable  # a memory-layout promise for the HIP sweep; no effect on the result
     assert l0 % parts == 0
     ch = l0 // parts
     for s in range(parts):
         attention(q, k0[s * ch:(s + 1) * ch], v0[s * ch:(s + 1) * ch], o_parts[s * lq:(s + 1) * lq], heads=heads,
                   head_dim=head_dim, batch=1, lq=lq, q_bstride=0, l0=ch, k0_bstride=0, scale=scale,
-                  lse=lse_parts[s])
+                  lse=lse_parts[s], q_scaled=q_scaled)
 
 
 def attn_merge_n(o_parts, lse_parts, out, *, parts, rows, heads, head_dim, lse_out=None, seg_rows=None):

@@ -139,3 +139,18 @@ def pil_load_reference(images, mode=None, square_target=None):
             t = torch.nn.functional.pad(t, (wp // 2, wp - wp // 2, hp // 2, hp - hp // 2), value=1.0)
         padded.append(t)
     return torch.stack(padded)
+
+
+# Full-model parity bounds, rel-L2 against the reference's fp32 goldens, per quantity class.  fp32
+# parity mode: 1e-4 everywhere (north star: pose within 1e-4 rel).  bf16 (autocast) mode: about 2x
+# the largest error measured on MI355X over every golden and sharded run (each test prints what it
+# measured, "PARITY ..." lines in the GPU logs), never above SURVEY §8(c)'s 2e-2.
+PARITY_TOL = {"fp32": {"feat": 1e-4, "pose": 1e-4},
+              "bf16": {"feat": 2e-2, "pose": 2e-2}}
+
+
+def parity_tol(key: str, mode: str) -> float:
+    """Bound for one checked quantity: pose encodings / extrinsics / intrinsics are the "pose"
+    class, feature maps and camera tokens the "feat" class."""
+    cls = "pose" if any(t in key for t in ("pose", "extrinsic", "intrinsic")) else "feat"
+    return PARITY_TOL[mode][cls]

@@ -238,15 +238,26 @@ def test_attn_merge_fp32_exact(ops, alias):
     assert float((lse.double() - ref_lse).abs().max()) < 1e-4
 
 
+LOG2E = 1.0 / math.log(2.0)
+
+
+def _prescale(q):
+    """What the QKV GEMM hands the attention (runtime.q_prescale, sr_attn_desc.q_scaled): c*q with
+    c = scale*log2(e), rounded to bf16 ONCE from the fp32 value (here q's own values)."""
+    return (q.float() * (D ** -0.5 * LOG2E)).bfloat16()
+
+
 @pytest.mark.parametrize("G", [3, 8], ids=["C3-3rk", "C3-8rk"])
 def test_global_attention_key_split(ops, G):
     """Key-split attention (ops.key_split_parts): one rank's query slice of the frame-sharded C3
     global block against all 43,968 keys runs as S key chunks whose bf16 partials and LSEs merge
-    with sr_attn_merge_n.  Equal to the unsplit kernel (output and LSE) and to fp64 attention."""
+    with sr_attn_merge_n.  Equal to the unsplit kernel (output and LSE) and to fp64 attention.
+    q arrives as the production path hands it over: c*q rounded once (q_scaled), so the fp64
+    reference reads the same operand, (c q).k / log2(e) = scale q.k."""
     L = 32 * P
     lq = (32 // G) * P
     q, k, v = _make(L, 17, spikes=(L - 37, 5 * P + 3))
-    qs = q[L - lq:]
+    qs = _prescale(q[L - lq:])
     parts = ops.key_split_parts(dtype=torch.bfloat16, batch=1, lq=lq, heads=H, l0=L, l1=0, mask_mode=0)
     assert parts > 1
     outs, lses = [], []
@@ -257,7 +268,8 @@ def test_global_attention_key_split(ops, G):
             o = torch.empty(lq, C, device=DEV, dtype=torch.bfloat16)
             lse = torch.empty(H, lq, device=DEV)
             ops.attention(qs, k, v, o, heads=H, head_dim=D, batch=1, lq=lq, q_bstride=0, l0=L, k0_bstride=0,
-                          lse=lse, key_norm_max=float(k.float().view(-1, H, D).norm(dim=-1).max()) * 1.01)
+                          lse=lse, key_norm_max=float(k.float().view(-1, H, D).norm(dim=-1).max()) * 1.01,
+                          q_scaled=True)
             outs.append(o)
             lses.append(lse)
     finally:
@@ -265,13 +277,12 @@ def test_global_attention_key_split(ops, G):
     torch.cuda.synchronize()
     assert _rel(outs[1].float(), outs[0].float()) < 1e-2
     rows = _sample_rows(lq, 256, G).to(DEV)
-    ref = _ref_rows(qs[rows], k, v, D ** -0.5)
-    # fp64 log2-domain LSE of the sampled rows.  Both launches fold c = scale*log2(e) into q and
-    # round c*q to bf16 (the MFMA operand), an error of the spike rows' scores that the fp64
-    # reference does not have: measured 5.0e-2 / 3.8e-2 (G = 3 / 8) for split AND unsplit alike,
-    # 1.0e-2 / 8.8e-3 between them, outputs 2.8e-3 rel -- so the LSE bounds are 6e-2 vs fp64 and
-    # 2e-2 between the two
-    s_ref = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double()) * D ** -0.5
+    ref = _ref_rows(qs[rows], k, v, LOG2E)
+    # fp64 log2-domain LSE of the sampled rows over the same operands.  Round 4 re-rounded c*q inside
+    # the kernel (c * bf16(q) to bf16 again), which put 5.0e-2 / 3.8e-2 of score error on the spike
+    # rows and needed a 6e-2 bound; with q rounded once what is left is the row sums over the
+    # bf16-rounded P of the P.V product (2^-9 per dominant term)
+    s_ref = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double()) * LOG2E
     ref_lse = torch.logsumexp(s_ref, -1) / math.log(2.0)
     e_split = float((lses[1][:, rows].double() - ref_lse).abs().max())
     e_one = float((lses[0][:, rows].double() - ref_lse).abs().max())
@@ -280,7 +291,35 @@ def test_global_attention_key_split(ops, G):
           f"{_rel(outs[0][rows].float(), ref):.2e}); LSE vs fp64 {e_split:.2e} (unsplit {e_one:.2e}), "
           f"split vs unsplit {e_pair:.2e}")
     assert _rel(outs[1][rows].float(), ref) < 1e-2
-    assert e_split < 6e-2 and e_one < 6e-2 and e_pair < 2e-2
+    assert e_split < 2e-2 and e_one < 2e-2 and e_pair < 2e-2
+
+
+@pytest.mark.parametrize("L", [43_968, 175_872], ids=["C3", "C5"])
+def test_global_attention_q_scaled(ops, L):
+    """sr_attn_desc.q_scaled (the production convention since round 5): q holds c*q rounded once,
+    the kernel uses it as is.  Against fp64 over the same operand at C3 / C5, the pair launch with
+    q_scaled bit-identical to its two launches apart, and the plain-q launch (the kernel forms
+    bf16(c * bf16(q)), a second rounding) within its own larger error."""
+    q, k, v = _make(L, 23, spikes=(L - 37, L // 2 + 5))
+    qs = _prescale(q)
+    kb = _kbound(k)
+    o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+    o_plain = torch.empty_like(o)
+    ops.attention(qs, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, key_norm_max=kb,
+                  q_scaled=True)
+    ops.attention(q, k, v, o_plain, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
+                  key_norm_max=kb)
+    rows = _sample_rows(L, 256, L + 1).to(DEV)
+    e_scaled = _rel(o[rows].float(), _ref_rows(qs[rows], k, v, LOG2E))
+    e_plain = _rel(o_plain[rows].float(), _ref_rows(q[rows], k, v, D ** -0.5))
+    print(f"q_scaled L={L}: rel vs fp64 {e_scaled:.2e} (plain q, re-rounded in the kernel: {e_plain:.2e})")
+    assert e_scaled < 1e-2 and e_plain < 1e-2
+    if L == 43_968:
+        o1, o2 = torch.empty_like(o), torch.empty_like(o)
+        ops.attention_pair(dict(q=qs, k0=k, v0=v, o=o1, lq=L, l0=L, key_norm_max=kb, q_scaled=True),
+                           dict(q=q, k0=k, v0=v, o=o2, lq=L, l0=L, key_norm_max=kb), heads=H, head_dim=D)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o) and torch.equal(o2, o_plain)
 
 
 def test_attn_merge_n_seg_rows_fp32(ops):
@@ -831,3 +870,47 @@ def test_global_attention_scan_boxes(ops):
             assert err < 1.5e-2
     finally:
         ops._KEY_BOX = saved
+
+
+@pytest.mark.parametrize("vexp", [0, -14], ids=["v1", "v2e-14"])
+def test_attention_window_low_edge(ops, vexp):
+    """ADVICE r4 (FIX_LO = 110): rows whose fixed offset m = max(0, qb - 64) sits 76-106 (log2) above
+    their true score max, so the row's largest P is down to ~2^-106 (the window allows 2^-110), with
+    V of order 1 and of order 2^-14 (every P.V product of the top keys >= 2^-121 stays a normal fp32).
+    Construction (CPU generator, checked here): every query of a head points along one direction u
+    with c|q||k| = 400; the first tile's keys make cosines 0.5-0.6 with u (the row max, inside the
+    first three tiles the window is checked on); the rest are random (>= 33 below).  Every wave
+    stays on the hand-scheduled sweep, and the result matches fp64 on sampled rows.  (Below
+    |v| ~ 2^-16 at the window's very edge the P.V products would reach fp32 denormals.)"""
+    L = 8192
+    c = D ** -0.5 * LOG2E
+    g = torch.Generator().manual_seed(101)
+    u = torch.randn(H, D, generator=g)
+    u = u / u.norm(dim=-1, keepdim=True)
+    k = torch.randn(L, H, D, generator=g)
+    w = torch.randn(64, H, D, generator=g)
+    w = w - (w * u[None]).sum(-1, keepdim=True) * u[None]
+    w = w / w.norm(dim=-1, keepdim=True)
+    cs = torch.linspace(0.5, 0.6, 64)[:, None, None]
+    k[:64] = cs * u[None] + torch.sqrt(1 - cs ** 2) * w
+    k = (k * (8.0 / k.norm(dim=-1, keepdim=True))).reshape(L, C).bfloat16().to(DEV)
+    q = u[None] + 0.02 * torch.randn(L, H, D, generator=g)
+    q = q * (400.0 / (c * 8.0) / q.norm(dim=-1, keepdim=True))
+    qs = (q * c).reshape(L, C).bfloat16().to(DEV)
+    v = (torch.randn(L, C, generator=g) * 2.0 ** vexp).bfloat16().to(DEV)
+    kb = _kbound(k)
+    st = torch.zeros(2, dtype=torch.int32, device=DEV)
+    o = torch.empty(L, C, device=DEV, dtype=torch.bfloat16)
+    ops.attention(qs, k, v, o, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0, key_norm_max=kb,
+                  sweep_stats=st, q_scaled=True)
+    torch.cuda.synchronize()
+    rows = _sample_rows(L, 128, 5).to(DEV)
+    s = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double())  # log2 domain
+    m = (qs[rows].view(-1, H, D).double().norm(dim=-1).T * kb - 64.0).clamp_min(0)
+    gap = m - s.amax(-1)
+    e = _rel(o[rows].float(), _ref_rows(qs[rows], k, v, LOG2E))
+    print(f"|v| ~ 2^{vexp}: offset above the true max {float(gap.min()):.1f} .. {float(gap.max()):.1f} (log2), "
+          f"asm / compiled waves {st.tolist()}, rel vs fp64 {e:.2e}")
+    assert float(gap.max()) > 95.0  # rows really sit near the window's low edge
+    assert st.tolist()[1] == 0 and st.tolist()[0] == L // 64 * H
+    assert e < 1e-2

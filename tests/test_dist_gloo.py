@@ -132,7 +132,8 @@ def test_sharded_global_partials_plan(G, r, force):
     kv_all = torch.randn(La, 2 * C, generator=g).bfloat16()
     kv_loc = kv_all[off:off + lq].clone()
     o = torch.empty(lq, C, dtype=torch.bfloat16)
-    pg = SimpleNamespace(dim=C, heads=H, head_dim=D, k_bound=0.0, q_bound=0.0)
+    # (fp32 w_qkv: plain q, runtime.q_prescale = 0, so the reference below reads q as it is)
+    pg = SimpleNamespace(dim=C, heads=H, head_dim=D, k_bound=0.0, q_bound=0.0, w_qkv=torch.empty(0))
     calls = []
     saved = ops._KSPLIT_ENV
     with cpu_ops.installed():

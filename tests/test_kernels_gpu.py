@@ -520,7 +520,8 @@ def test_attention_key_box(ops, rows, n_inst, heads, ld):
     assert torch.allclose(n2[fin].double(), ref[fin], rtol=1e-6, atol=0)
 
 
-@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])
+@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD",
+                                      "BIAS_GELU_AUX", "QKV_ROWMAP_AUX", "QKV_QSCALE", "BIAS_QSCALE"])
 @pytest.mark.parametrize("M,N", [(43 * 256 - 100, 3072), (87936, 1024), (2 * 5496, 4096)])
 def test_gemm_tail_split(ops, epi_name, M, N):
     """SR_GEMM_TAIL: the rows past the 256x256 kernel's last whole workgroup round run on the
@@ -530,13 +531,16 @@ def test_gemm_tail_split(ops, epi_name, M, N):
     the time-dominant kernel is still reported."""
     from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
     L = _lib()
-    epi = getattr(L, "SR_EPI_" + epi_name)
+    base = {"BIAS_GELU_AUX": "BIAS_GELU", "QKV_ROWMAP_AUX": "QKV", "QKV_QSCALE": "QKV",
+            "BIAS_QSCALE": "BIAS"}.get(epi_name, epi_name)
+    epi = getattr(L, "SR_EPI_" + base)
     K, C = 1024, 1024
     g = torch.Generator(device=DEV).manual_seed(M + N)
     a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
     w = (torch.randn(N, K, device=DEV, generator=g) / 32).bfloat16()
     kw = dict(bias=torch.randn(N, device=DEV, generator=g))
-    if epi_name == "QKV":
+    aux1 = aux0 = None
+    if base == "QKV":
         if N % C:
             pytest.skip("QKV needs whole q|k|v blocks")
         rope = RotaryPositionEmbedding2D(100).tables(64, 40, DEV)
@@ -544,6 +548,17 @@ def test_gemm_tail_split(ops, epi_name, M, N):
         kw["qkv"] = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
                          rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37,
                          pos_row_base=11, col_offset=3 * C - N)
+        if epi_name == "QKV_ROWMAP_AUX":  # the anchor-subsample form: positions through a row map
+            kw["qkv"].pop("pos_row_base")
+            kw["qkv"]["pos_rowmap"] = torch.randint(0, 64 * 1374, (M,), device=DEV, dtype=torch.int32,
+                                                    generator=g)
+    if epi_name in ("QKV_QSCALE", "BIAS_QSCALE"):
+        if base == "QKV" and N != 3 * C:
+            pytest.skip("the Q block needs a full q|k|v output")
+        kw["q_scale"], kw["q_cols"] = 0.125 * 1.4426950408889634, C
+    if epi_name in ("BIAS_GELU_AUX", "QKV_ROWMAP_AUX"):
+        aux1 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        aux0 = torch.zeros_like(aux1)
     if epi_name == "BIAS_RESID":
         kw["gamma"] = torch.randn(N, device=DEV, generator=g)
     if epi_name == "GELU_BWD":
@@ -555,16 +570,26 @@ def test_gemm_tail_split(ops, epi_name, M, N):
         out1 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
         out0 = torch.zeros_like(out1)
     with ops.tuning(SR_GEMM_TAIL=1):
-        ops.gemm(a, w, out1, epi, splits=1, **kw)
+        ops.gemm(a, w, out1, epi, splits=1, aux=aux1, **kw)
         k1 = ops.last_kernel()
     with ops.tuning(SR_GEMM_TAIL=0):
-        ops.gemm(a, w, out0, epi, splits=1, **kw)
+        ops.gemm(a, w, out0, epi, splits=1, aux=aux0, **kw)
         k0 = ops.last_kernel()
     torch.cuda.synchronize()
     assert k1 == k0 and k0.startswith("gemm256_kernel"), (k1, k0)
     same = torch.equal(out1, out0)
     print(f"{epi_name} M={M} N={N}: bit-identical={same} rel={rel(out1.float(), out0.float()):.2e}")
     assert rel(out1.float(), out0.float()) < 1e-6
+    if aux1 is not None:  # the saved pre-activation rows of the tail launch land in the right rows
+        assert rel(aux1.float(), aux0.float()) < 1e-6 and aux1.abs().sum() > 0
+    if "QSCALE" in epi_name:  # only the Q block is scaled, before the one rounding
+        kw.pop("q_scale"), kw.pop("q_cols")
+        plain = torch.zeros_like(out1)
+        ops.gemm(a, w, plain, epi, splits=1, **kw)
+        torch.cuda.synchronize()
+        c = 0.125 * 1.4426950408889634
+        assert torch.equal(out1[:, C:], plain[:, C:])
+        assert rel(out1[:, :C].float(), plain[:, :C].float() * c) < 4e-3
 
 
 @pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])

@@ -12,12 +12,11 @@ import pytest
 import torch
 import torch.nn as nn
 
-from goldens import load_npz, rel_l2, rule_state_dict
+from goldens import load_npz, parity_tol, rel_l2, rule_state_dict
 
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-TOL = {"fp32": 1e-4, "bf16": 3e-2}
 
 
 class Hot(nn.Module):
@@ -64,15 +63,13 @@ def test_small_end_to_end(small_model, tag, mode):
     feats, psi, cam_last, poses, ext, intr = run(small_model, images, n, int(g["fix_rank"]), mode)
     assert psi == 5
     assert np.array_equal(small_model.aggregator.last_subsample_indices[:, 0].numpy(), g["sub_idx"])
-    tol = TOL[mode]
-    for layer in (0, 1):
-        assert rel_l2(feats[layer].cpu().numpy(), g[f"feat_{layer}"]) < tol, layer
     assert feats[-1] is feats[1]
-    assert rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"]) < tol
-    pe = np.stack([p.cpu().numpy() for p in poses])
-    assert rel_l2(pe, g["pose_enc"]) < tol
-    assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
-    assert rel_l2(intr.cpu().numpy(), g["intrinsic"]) < tol
+    err = {f"feat_{layer}": rel_l2(feats[layer].cpu().numpy(), g[f"feat_{layer}"]) for layer in (0, 1)}
+    err["cam_token_last_layer"] = rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"])
+    err["pose_enc"] = rel_l2(np.stack([p.cpu().numpy() for p in poses]), g["pose_enc"])
+    err["extrinsic"] = rel_l2(ext.cpu().numpy(), g["extrinsic"])
+    err["intrinsic"] = rel_l2(intr.cpu().numpy(), g["intrinsic"])
+    _assert_tol(err, mode, f"g1_small_{tag}")
 
 
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
@@ -86,13 +83,11 @@ def test_small_interleaved_lists(small_model, mode):
     feats, psi, cam_last, poses, ext, intr = run(small_model, images, len(no_reloc), int(g["fix_rank"]), mode,
                                                  lists=(no_reloc, reloc))
     assert np.array_equal(small_model.aggregator.last_subsample_indices[:, 0].numpy(), g["sub_idx"])
-    tol = TOL[mode]
-    for layer in (0, 1):
-        assert rel_l2(feats[layer].cpu().numpy(), g[f"feat_{layer}"]) < tol, layer
-    assert rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"]) < tol
-    pe = np.stack([p.cpu().numpy() for p in poses])
-    assert rel_l2(pe, g["pose_enc"]) < tol
-    assert rel_l2(ext.cpu().numpy(), g["extrinsic"]) < tol
+    err = {f"feat_{layer}": rel_l2(feats[layer].cpu().numpy(), g[f"feat_{layer}"]) for layer in (0, 1)}
+    err["cam_token_last_layer"] = rel_l2(cam_last.cpu().numpy(), g["cam_token_last_layer"])
+    err["pose_enc"] = rel_l2(np.stack([p.cpu().numpy() for p in poses]), g["pose_enc"])
+    err["extrinsic"] = rel_l2(ext.cpu().numpy(), g["extrinsic"])
+    _assert_tol(err, mode, "g11_small_interleaved")
 
 
 @pytest.mark.parametrize("fused", [False, True], ids=["resid-epilogue", "fused-resid-ln"])
@@ -158,10 +153,15 @@ def _full_errors(model, fname, mode):
     return err
 
 
-def _check_full(model, fname, mode):
-    err = _full_errors(model, fname, mode)
-    bad = {k: v for k, v in err.items() if not v < TOL[mode]}
+def _assert_tol(err, mode, what):
+    """Print every measured error (GPUTEST logs show drift) and check each against its bound."""
+    print(f"PARITY {what} {mode}:", {k: float(f"{v:.3e}") for k, v in err.items()})
+    bad = {k: (v, parity_tol(k, mode)) for k, v in err.items() if not v < parity_tol(k, mode)}
     assert not bad, bad
+
+
+def _check_full(model, fname, mode, what=""):
+    _assert_tol(_full_errors(model, fname, mode), mode, fname + what)
 
 
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
@@ -196,7 +196,7 @@ def test_full_deferred_residuals(full_model, fname, mode, monkeypatch):
     from sailrecon_amd import runtime
     monkeypatch.setattr(runtime, "_FUSED_RESID_LN", True)
     monkeypatch.setattr(runtime, "_DEFER_RESID", True)
-    _check_full(full_model, fname, mode)
+    _check_full(full_model, fname, mode, " deferred residuals")
 
 
 # fp8 global attention (BASELINE C5's precision, opt-in: Aggregator.set_fp8_global) at the C3
