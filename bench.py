@@ -402,13 +402,16 @@ def main():
     ap.add_argument("--fp8-global", choices=["off", "qk", "qkv"], default="off",
                     help="BASELINE C5: the global blocks' q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 "
                          "e4m3; everything else bf16")
-    ap.add_argument("--extras", default="n64,c5,g4",
+    ap.add_argument("--extras", default="n64,c5,c5qk,g4",
                     help="comma list of extra workloads timed after the headline on the same model and reported "
                          "inside its line as extra_configs (not the metric): n64 = N=64 @518 bf16 (the north "
-                         "star's 64-view scaling workload, sharded like the headline), c5 = BASELINE C5 (N=128 "
-                         "@518, global attention in fp8; one GPU only); '' or 'none' to skip")
-    ap.add_argument("--c5-fp8", choices=["qk", "qkv"], default="qk",
-                    help="C5 extra: q.k^T (qk) or q.k^T and P.V (qkv) in block-scaled fp8 e4m3")
+                         "star's 64-view scaling workload, sharded like the headline), c5 = BASELINE C5 as BASELINE "
+                         "states it (N=128 @518, the global blocks' fp8 QKV path: q.k^T and P.V in block-scaled "
+                         "e4m3), c5qk = the same with only q.k^T in fp8 (one GPU only, both); g4 = the headline at "
+                         "qk-norm gain 4; '' or 'none' to skip")
+    ap.add_argument("--c5-fp8", choices=["qk", "qkv"], default="qkv",
+                    help="the c5 extra's fp8 mode: q.k^T and P.V (qkv, BASELINE C5's fp8 QKV path) or q.k^T "
+                         "only (qk)")
     ap.add_argument("--qk-gain", type=float, default=1.0,
                     help="scale every q_norm / k_norm weight of the aggregator by this factor (trained models carry "
                          "gains of ~2-3; the synthetic weights ~1): the attention softmax's peakedness, for A/B of "
@@ -544,9 +547,9 @@ def main():
     extras = []
     if use_bf16 and not fp8:
         for name in [e for e in args.extras.split(",") if e and e != "none"]:
-            if name == "c5" and world > 1:
+            if name in ("c5", "c5qk") and world > 1:
                 continue
-            if name not in ("n64", "c5", "g4"):
+            if name not in ("n64", "c5", "c5qk", "g4"):
                 raise SystemExit(f"bench.py: unknown extra workload {name!r}")
             if name == "g4" and args.qk_gain != 1.0:
                 continue  # the headline already runs at a scaled gain
@@ -594,20 +597,23 @@ def extra_config(model, device, args, world, name):
     line's ``extra_configs``, never as its value): ``n64`` = N=64 @518 bf16, the north star's
     64-view scaling workload (frame-sharded like the headline when world > 1); ``c5`` = BASELINE
     config 5 (N=128 @518, 256 frames, L_g = 175,872) with the global blocks' attention in fp8
-    (Aggregator.set_fp8_global), one GPU; ``g4`` = the headline workload with every q_norm / k_norm
+    (Aggregator.set_fp8_global; --c5-fp8, default q.k^T and P.V: BASELINE's "fp8 MFMA QKV path"),
+    ``c5qk`` the same with q.k^T alone in fp8, one GPU; ``g4`` = the headline workload with every q_norm / k_norm
 weight x 4 (scale_qk_gain, undone after).  One untimed warmup, then a few steps between barriers +
     synchronize, max over ranks.  A Python error is reported in the object, not raised."""
     from sailrecon_amd import ops
-    n = {"n64": 64, "c5": 128}.get(name, args.views)
-    fp8 = name == "c5"
+    n = {"n64": 64, "c5": 128, "c5qk": 128}.get(name, args.views)
+    fp8 = name in ("c5", "c5qk")
+    fp8_mode = "qk" if name == "c5qk" else args.c5_fp8
     gain = 4.0 if name == "g4" else None
-    steps = 2 if name == "c5" else 3
+    steps = 2 if fp8 else 3
     g = torch.Generator().manual_seed(n)
     x = torch.rand(n, 3, args.img, args.img, generator=g)
     images = torch.cat([x, x])[None].to(device)
     no_reloc, reloc = list(range(n)), list(range(n, 2 * n))
-    dtype = (f"bf16, global {'q.k^T' if args.c5_fp8 == 'qk' else 'q.k^T + P.V'} fp8-e4m3" if fp8 else "bf16")
-    what = {"n64": " (north-star 64-view workload)", "c5": " (BASELINE C5, fp8 global attention)",
+    dtype = (f"bf16, global {'q.k^T' if fp8_mode == 'qk' else 'q.k^T + P.V'} fp8-e4m3" if fp8 else "bf16")
+    what = {"n64": " (north-star 64-view workload)", "c5": f" (BASELINE C5, fp8 global attention: {fp8_mode})",
+            "c5qk": " (BASELINE C5, fp8 global attention: q.k^T only)",
             "g4": " at qk-norm gain 4 (trained-like q_norm / k_norm weights: every one x 4)"}.get(name, "")
     out = {"name": name, "metric": f"aggregator fwd views/sec, N={n} @ {args.img}px" + what,
            "unit": "views/s", "dtype": dtype, "views": n, "frames": 2 * n, "steps": steps, "warmup": 1}
@@ -626,7 +632,7 @@ weight x 4 (scale_qk_gain, undone after).  One untimed warmup, then a few steps 
     timer = None
     try:
         if fp8:
-            model.aggregator.set_fp8_global(True, fp8_v=args.c5_fp8 == "qkv")
+            model.aggregator.set_fp8_global(True, fp8_v=fp8_mode == "qkv")
         if gain is not None:
             scale_qk_gain(model, gain)
         step()
@@ -660,6 +666,17 @@ weight x 4 (scale_qk_gain, undone after).  One untimed warmup, then a few steps 
                 "attn_global": None if att is None else {"avg_launch_ms": round(att["avg_ms"], 4),
                                                          "tflops": round(att["tflops"], 1),
                                                          "kernels": att.get("kernels")}})
+    if fp8 and att is not None and gpu_peak()[0]:
+        # the global attention against the MFMA peak of its operand mix: qkv runs both products on the
+        # block-scaled fp8 MFMA (2x the bf16 rate); qk runs half the flops there and half at the bf16
+        # rate, i.e. 4/3 of the bf16 peak (MI355X_MICROARCH.md, "Matrix cores")
+        bf16_peak, _ = gpu_peak()
+        peak = bf16_peak * (2.0 if fp8_mode == "qkv" else 4.0 / 3.0)
+        out["roofline"] = {"bound": "mfma", "kernel": next(iter(att.get("kernels") or {}), None),
+                           "achieved": round(att["tflops"], 1), "peak": round(peak, 1), "unit": "TFLOP/s",
+                           "frac": round(att["tflops"] / peak, 4),
+                           "peak_source": f"{'2' if fp8_mode == 'qkv' else '4/3'} x the bf16 peak {bf16_peak:.1f} "
+                                          "(block-scaled e4m3 MFMA at 2x the bf16 rate)"}
     del images
     return out
 

@@ -721,6 +721,14 @@ int sr_pil_resample_v_f32(sr_stream_t stream, int mode, const void* tmp, int n, 
                           const int* bounds, const void* coeffs, int ksize, int th, float divisor, float* out,
                           int64_t frame_stride, int64_t chan_stride, int64_t ldo);
 
+/* ImagePreprocessor.reverse_transform_tensor (train/utils/io.py:197-259): a processed (C, h, w) fp32
+ * tensor resized back to (hs, ws) with F.interpolate(mode = bicubic (1) | bilinear (0),
+ * align_corners=False) and the padding cropped away, fused: out[ch][oy][ox] = resized[ch][oy + y0]
+ * [ox + x0] for the (ho, wo) crop (the resized max_side^2 image is never materialised).  torch's
+ * index / weight rules (scale in / out, cubic A = -0.75, border-clamped taps). */
+int sr_resize_crop_chw_f32(sr_stream_t stream, const float* x, int c, int h, int w, int hs, int ws, int y0, int x0,
+                           int ho, int wo, int mode, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -593,6 +593,25 @@ def preprocess_image(img, target: int = 518, is_depth: bool = False):
     return t[None], k2kp, kp2k
 
 
+def reverse_transform_tensor(processed: Tensor, kp2k: Tensor, target: int, is_depth: bool = False) -> Tensor:
+    """ImagePreprocessor.reverse_transform_tensor (train/utils/io.py:197-259) restated line by line
+    with the same torch calls (the reference module itself does not import here: cv2 / torchvision
+    are absent): scale and padding read back from K_prime_to_K, F.interpolate to max_side
+    (bicubic for RGB, bilinear for depth, align_corners=False), crop of the padding."""
+    import torch.nn.functional as F
+    scale_x = 1.0 / kp2k[0, 0].item()
+    scale_y = 1.0 / kp2k[1, 1].item()
+    offset_x = -kp2k[0, 2].item() * scale_x
+    offset_y = -kp2k[1, 2].item() * scale_y
+    max_side = int(target / scale_x)
+    pad_left = int(offset_x / scale_x)
+    pad_top = int(offset_y / scale_y)
+    r = F.interpolate(processed.unsqueeze(0), size=(max_side, max_side),
+                      mode="bicubic" if not is_depth else "bilinear", align_corners=False).squeeze(0)
+    w, h = max_side - 2 * pad_left, max_side - 2 * pad_top
+    return r[:, pad_top:pad_top + h, pad_left:pad_left + w]
+
+
 # --------------------------------------------------------------------------
 # Self-supervised training loss (SURVEY §8(f) rank 4): compute_loss (train/train_imc.py:141-246)
 # with CDFLossIndexPytorch (train/losses/cdf_loss.py:19-242) and the projective geometry of

@@ -255,7 +255,94 @@ __global__ __launch_bounds__(TPB) void pil_v_kernel(const uint8_t* __restrict__ 
 
 unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>((n + TPB - 1) / TPB, 1 << 20); }
 
+// ------------------------------------------------------------ reverse transform (io.py:197-259)
+// torch's upsample index / weight rules with align_corners=False (ATen UpSample.h):
+//   src = scale * (dst + 0.5) - 0.5, scale = in / out (float);  linear clamps src at 0, cubic does not;
+//   cubic: i = floor(src) and t = src - i (clamped to [0, 1]), the 4 taps i-1..i+2 read clamped to
+//   the image, Keys' convolution with A = -0.75 (get_cubic_upsample_coefficients).
+__device__ __forceinline__ float cubic1(float x, float A) { return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f; }
+__device__ __forceinline__ float cubic2(float x, float A) { return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A; }
+
+struct Taps {
+  int i[4];
+  float w[4];
+};
+
+template <bool CUBIC>
+__device__ __forceinline__ Taps taps(int dst, float scale, int in) {
+  Taps t;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if constexpr (CUBIC) {
+    const float fl = floorf(src);
+    const int i0 = (int)fl;
+    const float x = fminf(fmaxf(src - fl, 0.f), 1.f);
+    constexpr float A = -0.75f;
+    t.w[0] = cubic2(x + 1.f, A);
+    t.w[1] = cubic1(x, A);
+    t.w[2] = cubic1(1.f - x, A);
+    t.w[3] = cubic2(2.f - x, A);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t.i[k] = min(max(i0 - 1 + k, 0), in - 1);
+  } else {
+    src = fmaxf(src, 0.f);
+    const int i0 = (int)src;
+    const float l1 = src - (float)i0;
+    t.i[0] = i0;
+    t.i[1] = i0 + (i0 < in - 1 ? 1 : 0);
+    t.w[0] = 1.f - l1;
+    t.w[1] = l1;
+  }
+  return t;
+}
+
+// out[ch][oy][ox] = resize(x[ch], (h, w) -> (hs, ws))[oy + y0][ox + x0]: one thread per output
+// element, consecutive threads along a row (coalesced stores; the taps' reads hit L2)
+template <bool CUBIC>
+__global__ __launch_bounds__(TPB) void resize_crop_chw_kernel(const float* __restrict__ x, int c, int h, int w,
+                                                              float sh, float sw, int y0, int x0, int ho, int wo,
+                                                              float* __restrict__ out) {
+  constexpr int NT = CUBIC ? 4 : 2;
+  const int64_t total = (int64_t)c * ho * wo;
+  for (int64_t e = blockIdx.x * (int64_t)TPB + threadIdx.x; e < total; e += (int64_t)gridDim.x * TPB) {
+    const int ox = (int)(e % wo);
+    const int64_t r = e / wo;
+    const int oy = (int)(r % ho), ch = (int)(r / ho);
+    const Taps ty = taps<CUBIC>(oy + y0, sh, h), tx = taps<CUBIC>(ox + x0, sw, w);
+    const float* plane = x + (int64_t)ch * h * w;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float* row = plane + (int64_t)ty.i[j] * w;
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) v += row[tx.i[i]] * tx.w[i];
+      acc += v * ty.w[j];
+    }
+    out[e] = acc;
+  }
+}
+
 }  // namespace
+
+extern "C" int sr_resize_crop_chw_f32(sr_stream_t stream, const float* x, int c, int h, int w, int hs, int ws,
+                                      int y0, int x0, int ho, int wo, int mode, float* out) {
+  SR_CHECK(x && out && x != out && c > 0 && h > 0 && w > 0 && hs > 0 && ws > 0 && ho > 0 && wo > 0, SR_EINVAL,
+           "sr_resize_crop_chw_f32: bad args");
+  SR_CHECK(y0 >= 0 && x0 >= 0 && y0 + ho <= hs && x0 + wo <= ws, SR_EINVAL,
+           "sr_resize_crop_chw_f32: crop [%d, %d) x [%d, %d) outside the %d x %d resized image", y0, y0 + ho, x0,
+           x0 + wo, hs, ws);
+  SR_CHECK(mode == 0 || mode == 1, SR_EINVAL, "sr_resize_crop_chw_f32: mode 0 (bilinear) or 1 (bicubic)");
+  const int64_t total = (int64_t)c * ho * wo;
+  const float sh = (float)h / (float)hs, sw = (float)w / (float)ws;  // area_pixel_compute_scale
+  if (mode == 1)
+    hipLaunchKernelGGL(resize_crop_chw_kernel<true>, dim3(grid_for(total)), dim3(TPB), 0, (hipStream_t)stream, x, c,
+                       h, w, sh, sw, y0, x0, ho, wo, out);
+  else
+    hipLaunchKernelGGL(resize_crop_chw_kernel<false>, dim3(grid_for(total)), dim3(TPB), 0, (hipStream_t)stream, x,
+                       c, h, w, sh, sw, y0, x0, ho, wo, out);
+  sr::note_kernel("resize_crop_chw_kernel<%s>", mode == 1 ? "true" : "false");
+  return sr::check_launch("sr_resize_crop_chw_f32");
+}
 
 extern "C" int sr_pil_resample_h(sr_stream_t stream, int mode, const void* img, int n, int h, int w, int c,
                                  const int* bounds, const void* coeffs, int ksize, int tw, void* tmp) {

@@ -192,6 +192,7 @@ _PROTOS = {
     "sr_imc_loss_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32]),
     "sr_imc_loss": (_i32, [_vp, ctypes.POINTER(ImcLossDesc)]),
     "sr_pose_act_bwd_f32": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32]),
+    "sr_resize_crop_chw_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
 }
 EXPORTED = tuple(_PROTOS)
 

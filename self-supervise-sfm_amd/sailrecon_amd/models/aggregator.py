@@ -243,9 +243,17 @@ class Aggregator(nn.Module):
             nreg_d = dino.num_register_tokens
             if 1 + nreg_d != psi:
                 raise NotImplementedError("DINO register count must equal the aggregator's")
-            dtab = torch.cat([(dino.cls_token[0, 0] + pos_tab[0])[None], dino.register_tokens[0]], 0)
-            dtab = dtab.detach().float().contiguous()[None]
-            zero_t = ws.get("frame_type0", F_, 1, torch.int32, dev).zero_()
+            # DINO's cls (+ its pos-embed row) and register rows, and an all-zero frame-type table:
+            # parameter preprocessing, built once per resolution (no torch kernels per forward)
+            key = ("dino_tokens", H, W, F_, str(dev), dino.cls_token._version, dino.register_tokens._version,
+                   dino.pos_embed._version)
+            if key not in self._packed:
+                dtab = torch.cat([(dino.cls_token[0, 0] + pos_tab[0])[None], dino.register_tokens[0]], 0)
+                self._packed = {k: v for k, v in self._packed.items() if not (isinstance(k, tuple) and
+                                                                             k[0] == "dino_tokens")}
+                self._packed[key] = (dtab.detach().float().contiguous()[None],
+                                     torch.zeros(F_, 1, dtype=torch.int32, device=dev))
+            dtab, zero_t = self._packed[key]
             ops.set_special_tokens(x, F_, P, dtab, zero_t)
             pending = []  # fc2 residual of block i folded into block i+1's LN1 (runtime.Pending)
             nblk = len(dino.blocks)
@@ -316,35 +324,46 @@ class Aggregator(nn.Module):
         imgs = images if order == list(range(S)) else images[:, order]
         imgs = imgs.reshape(F_, 3, H, W).float().contiguous()
 
-        x, sc = self._embed(imgs, F_, H, W, ftype_t_fn=lambda: runtime.to_device(
-            torch.tensor(sum(([0 if a == 0 else 1 for a in my_anchors] + [2] * Nq_l for _ in range(B)), []),
-                         dtype=torch.int32), dev), dtype=dtype)
-
-        # ---- subsample draws (host, overlaps the GPU work above), aggregator.py:277-285, 580-626
-        if fix_rank is not None:
-            self.rank = min(fix_rank, n_patch)
-        else:
-            lo, hi = min(self.min_rank, n_patch // 2), max(self.min_rank, n_patch // 2)
-            self.rank = int(torch.randint(lo, hi, (1,), generator=self.generator).item())
-        rank_ = self.rank
-        Pp = min(rank_ + psi, P)
-        rowmap_t = None
-        # the reference draws at every layer even without queries (select_scene_repe_for_reloc,
-        # aggregator.py:351-357), so the generator advances identically
-        idx = self.draw_subsample(self.depth, B, Na, n_patch, rank_)  # every rank draws all anchors
-        self.last_subsample_indices = torch.from_numpy(idx)
         need_sub = Nq > 0 or fill_cache
+        if fill_cache and B != 1:
+            raise NotImplementedError("kv_cache needs B == 1 (aggregator.py:452)")
+        host = {}
+
+        def host_tables():
+            """Every per-forward host table in ONE pinned H2D copy, built once _embed has queued its GPU
+            work (so the subsample draws overlap DINO): the frame types (aggregator.py:287-299, by
+            ORIGINAL frame index), the anchors' camera-token rows and the per-layer subsample row maps
+            (aggregator.py:277-285, 580-626).  Returns the frame-type view."""
+            if fix_rank is not None:
+                self.rank = min(fix_rank, n_patch)
+            else:
+                lo, hi = min(self.min_rank, n_patch // 2), max(self.min_rank, n_patch // 2)
+                self.rank = int(torch.randint(lo, hi, (1,), generator=self.generator).item())
+            Pp = min(self.rank + psi, P)
+            # the reference draws at every layer even without queries (select_scene_repe_for_reloc,
+            # aggregator.py:351-357), so the generator advances identically
+            idx = self.draw_subsample(self.depth, B, Na, n_patch, self.rank)  # every rank draws all anchors
+            self.last_subsample_indices = torch.from_numpy(idx)
+            ftype = np.array(sum(([0 if a == 0 else 1 for a in my_anchors] + [2] * Nq_l for _ in range(B)), []),
+                             dtype=np.int32)
+            anchors = np.array([b * S_l * P + a * P for b in range(B) for a in range(Na_l)], dtype=np.int32)
+            parts = [ftype, anchors]
+            if need_sub:
+                idx = idx[:, :, a_start:a_start + Na_l]                       # this rank's anchors
+                base = (np.arange(B) * S_l * P)[None, :, None, None] + (np.arange(Na_l) * P)[None, None, :, None]
+                sel = base + psi + idx                                        # [depth, B, Na_l, rank]
+                spec = np.broadcast_to(base + np.arange(psi)[None, None, None, :], (self.depth, B, Na_l, psi))
+                parts.append(np.concatenate([spec, sel], axis=-1).astype(np.int32).reshape(-1))
+            buf = runtime.to_device(torch.from_numpy(np.concatenate(parts)), dev)
+            n0, n1 = len(ftype), len(ftype) + len(anchors)
+            host.update(Pp=Pp, anchor_rows0=buf[n0:n1],
+                        rowmap_t=buf[n1:].view(self.depth, B, Na_l * Pp) if need_sub else None)
+            return buf[:n0]
+
+        x, sc = self._embed(imgs, F_, H, W, ftype_t_fn=host_tables, dtype=dtype)
+        Pp, rowmap_t, anchor_rows0 = host["Pp"], host["rowmap_t"], host["anchor_rows0"]
         if fill_cache:
-            if B != 1:
-                raise NotImplementedError("kv_cache needs B == 1 (aggregator.py:452)")
             self._kv_cache_layers = [None] * self.depth
-        if need_sub:
-            idx = idx[:, :, a_start:a_start + Na_l]                       # this rank's anchors
-            base = (np.arange(B) * S_l * P)[None, :, None, None] + (np.arange(Na_l) * P)[None, None, :, None]
-            sel = base + psi + idx                                        # [depth, B, Na_l, rank]
-            spec = np.broadcast_to(base + np.arange(psi)[None, None, None, :], (self.depth, B, Na_l, psi))
-            rowmap = np.concatenate([spec, sel], axis=-1).reshape(self.depth, B, Na_l * Pp).astype(np.int32)
-            rowmap_t = runtime.to_device(torch.from_numpy(rowmap), dev)
         rope = self.rope.tables(C // nh, max(gh, gw) + 1, dev) if self.rope is not None else None
         posctx = dict(tokens_per_frame=P, patch_start=psi, grid_w=gw)
 
@@ -354,8 +373,6 @@ class Aggregator(nn.Module):
             for l in self.intermediate_layer_idx:
                 out_maps[l] = torch.empty(B, Nq_l, P, 2 * C, device=dev, dtype=torch.float32)
         cam_loc = torch.empty(B, Na_l, 2 * C, device=dev, dtype=torch.float32)
-        anchor_rows0 = runtime.to_device(
-            torch.tensor([b * S_l * P + a * P for b in range(B) for a in range(Na_l)], dtype=torch.int32), dev)
         cam_flat = cam_loc.view(B * Na_l, 2 * C)
 
         # ---- alternating layers, aggregator.py:339-423

@@ -1025,6 +1025,20 @@ def pil_tmp(n: int, c: int, rows: int, tw: int, dtype: torch.dtype, device) -> T
     return torch.empty(n, c, rows, (tw + 3) // 4 * 4, dtype=dtype, device=device)
 
 
+def resize_crop_chw(x: Tensor, size: int, top: int, left: int, out: Tensor, bicubic: bool) -> None:
+    """out[c, i, j] = F.interpolate(x[None], (size, size), bicubic | bilinear, align_corners=False)[0, c,
+    top + i, left + j] for x fp32 [C, h, w] and out fp32 [C, ho, wo] (contiguous, on device), in one
+    launch (sr_resize_crop_chw_f32): ImagePreprocessor.reverse_transform_tensor's resize + crop."""
+    if x.dtype != torch.float32 or out.dtype != torch.float32 or x.dim() != 3 or out.dim() != 3 or \
+            not x.is_contiguous() or not out.is_contiguous() or x.shape[0] != out.shape[0]:
+        raise ValueError("resize_crop_chw: x [C, h, w] and out [C, ho, wo] contiguous fp32")
+    C, h, w = x.shape
+    ho, wo = out.shape[1], out.shape[2]
+    rc = _lib.load().sr_resize_crop_chw_f32(_stream(x), _p(x), C, h, w, size, size, top, left, ho, wo,
+                                            1 if bicubic else 0, _p(out))
+    check(rc, "sr_resize_crop_chw_f32")
+
+
 # ---------------------------------------------------------------- training step (SURVEY §8(f) rank 4)
 _TRAIN_WS = {}  # ((device, stream), name) -> fp32 workspace
 

@@ -8,8 +8,9 @@ passes, the padding and the ToTensor scaling run in sr_pil_resample_h / sr_pil_r
 bit-exact with Pillow (tests/test_io_gpu.py).  Differences from the reference: tensors come back
 on ``device`` (the K matrices stay on the host, float32, as in the reference), and
 ``process_views`` forms a whole scene at once (imc2021.py:260-301 stacking) with same-size views
-in one launch pair.  ``reverse_transform_tensor`` (io.py:197-259, an evaluation helper outside the
-hot path) is not mirrored.
+in one launch pair.  ``reverse_transform_tensor`` (io.py:197-259, the evaluation helper that maps a
+processed tensor back to the original image size) is one fused HIP launch (sr_resize_crop_chw_f32:
+torch's align_corners=False bicubic / bilinear upsample with the padding crop folded in).
 """
 
 from __future__ import annotations
@@ -233,6 +234,27 @@ class ImagePreprocessor:
             for i in idx:
                 mats[i] = k
         return out, torch.stack([k[0] for k in mats]), torch.stack([k[1] for k in mats])
+
+    def reverse_transform_tensor(self, processed_tensor: Tensor, K_prime_to_K: Tensor, target_size: int,
+                                 is_depth: bool = False) -> Tensor:
+        """io.py:197-259: (C, target, target) back to the original (C, H, W).  The resize scale and
+        padding come from K_prime_to_K exactly as the reference reads them (float32 .item() values,
+        the same int() truncations); the bicubic (RGB) / bilinear (depth) upsample to max_side and the
+        crop of the padding run as one launch on the tensor's device (no max_side^2 intermediate)."""
+        runtime.require_device(processed_tensor, "ImagePreprocessor.reverse_transform_tensor")
+        K = K_prime_to_K.detach().float().cpu()
+        scale_x = 1.0 / K[0, 0].item()
+        scale_y = 1.0 / K[1, 1].item()
+        offset_x = -K[0, 2].item() * scale_x
+        offset_y = -K[1, 2].item() * scale_y
+        max_side = int(target_size / scale_x)
+        pad_left = int(offset_x / scale_x)
+        pad_top = int(offset_y / scale_y)
+        width, height = max_side - 2 * pad_left, max_side - 2 * pad_top
+        x = processed_tensor.float().contiguous()
+        out = torch.empty(x.shape[0], height, width, device=x.device, dtype=torch.float32)
+        ops.resize_crop_chw(x, max_side, pad_top, pad_left, out, bicubic=not is_depth)
+        return out
 
     def _create_transformation_matrices(self, transform_param: Dict[str, Any]) -> Tuple[Tensor, Tensor]:
         """io.py:155-195 (host, float32)."""

@@ -123,3 +123,25 @@ def test_wide_rows_and_steep_downscale_bit_exact():
         dep = _depth(hw, 42)
         d, _, _ = pre(Image.fromarray(dep), is_depth=True)
         assert torch.equal(d.cpu(), pil_process_reference(dep, 518, True)), hw
+
+
+@pytest.mark.parametrize("hw", [(300, 400), (640, 480), (518, 518), (97, 61), (1536, 2048), (700, 1000)])
+@pytest.mark.parametrize("is_depth", [False, True], ids=["rgb", "depth"])
+def test_reverse_transform_tensor(hw, is_depth):
+    """ImagePreprocessor.reverse_transform_tensor (io.py:197-259): the processed tensor back to the
+    original size through the fused HIP resize + crop, against the oracle's restatement with the
+    reference's own torch calls (F.interpolate bicubic / bilinear, align_corners=False, then the
+    crop) on the host.  fp32 interpolation with a different summation order: 2e-6 rel-L2, 1e-4 max."""
+    from oracle import sfm_oracle as O
+    from sailrecon_amd.utils.io import ImagePreprocessor
+    arr = _depth(hw, 11) if is_depth else _rgb(hw, 7)
+    pre = ImagePreprocessor(518, device=DEV)
+    t, _, kp2k = pre(arr, is_depth=is_depth)
+    got = pre.reverse_transform_tensor(t[0], kp2k, 518, is_depth=is_depth)
+    ref = O.reverse_transform_tensor(t[0].cpu(), kp2k, 518, is_depth=is_depth)
+    torch.cuda.synchronize()
+    assert tuple(got.shape) == tuple(ref.shape)
+    rel = float((got.cpu().double() - ref.double()).norm() / ref.double().norm().clamp_min(1e-30))
+    mx = float((got.cpu() - ref).abs().max())
+    print(f"reverse_transform {hw} depth={is_depth}: out {tuple(got.shape)} rel {rel:.2e} max {mx:.2e}")
+    assert rel < 2e-6 and mx < 1e-4 * max(1.0, float(ref.abs().max()))
