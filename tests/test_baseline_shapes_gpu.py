@@ -239,6 +239,7 @@ def test_attn_merge_fp32_exact(ops, alias):
 
 
 LOG2E = 1.0 / math.log(2.0)
+LN2 = math.log(2.0)  # (c q).k * ln 2 = scale q.k: the natural-log scores of a q_scaled operand
 
 
 def _prescale(q):
@@ -253,7 +254,7 @@ def test_global_attention_key_split(ops, G):
     global block against all 43,968 keys runs as S key chunks whose bf16 partials and LSEs merge
     with sr_attn_merge_n.  Equal to the unsplit kernel (output and LSE) and to fp64 attention.
     q arrives as the production path hands it over: c*q rounded once (q_scaled), so the fp64
-    reference reads the same operand, (c q).k / log2(e) = scale q.k."""
+    reference reads the same operand, (c q).k ln 2 = scale q.k."""
     L = 32 * P
     lq = (32 // G) * P
     q, k, v = _make(L, 17, spikes=(L - 37, 5 * P + 3))
@@ -277,12 +278,12 @@ def test_global_attention_key_split(ops, G):
     torch.cuda.synchronize()
     assert _rel(outs[1].float(), outs[0].float()) < 1e-2
     rows = _sample_rows(lq, 256, G).to(DEV)
-    ref = _ref_rows(qs[rows], k, v, LOG2E)
+    ref = _ref_rows(qs[rows], k, v, LN2)
     # fp64 log2-domain LSE of the sampled rows over the same operands.  Round 4 re-rounded c*q inside
     # the kernel (c * bf16(q) to bf16 again), which put 5.0e-2 / 3.8e-2 of score error on the spike
     # rows and needed a 6e-2 bound; with q rounded once what is left is the row sums over the
     # bf16-rounded P of the P.V product (2^-9 per dominant term)
-    s_ref = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double()) * LOG2E
+    s_ref = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double()) * LN2
     ref_lse = torch.logsumexp(s_ref, -1) / math.log(2.0)
     e_split = float((lses[1][:, rows].double() - ref_lse).abs().max())
     e_one = float((lses[0][:, rows].double() - ref_lse).abs().max())
@@ -310,7 +311,7 @@ def test_global_attention_q_scaled(ops, L):
     ops.attention(q, k, v, o_plain, heads=H, head_dim=D, batch=1, lq=L, q_bstride=0, l0=L, k0_bstride=0,
                   key_norm_max=kb)
     rows = _sample_rows(L, 256, L + 1).to(DEV)
-    e_scaled = _rel(o[rows].float(), _ref_rows(qs[rows], k, v, LOG2E))
+    e_scaled = _rel(o[rows].float(), _ref_rows(qs[rows], k, v, LN2))
     e_plain = _rel(o_plain[rows].float(), _ref_rows(q[rows], k, v, D ** -0.5))
     print(f"q_scaled L={L}: rel vs fp64 {e_scaled:.2e} (plain q, re-rounded in the kernel: {e_plain:.2e})")
     assert e_scaled < 1e-2 and e_plain < 1e-2
@@ -908,7 +909,7 @@ def test_attention_window_low_edge(ops, vexp):
     s = torch.einsum("qhd,khd->hqk", qs[rows].view(-1, H, D).double(), k.view(-1, H, D).double())  # log2 domain
     m = (qs[rows].view(-1, H, D).double().norm(dim=-1).T * kb - 64.0).clamp_min(0)
     gap = m - s.amax(-1)
-    e = _rel(o[rows].float(), _ref_rows(qs[rows], k, v, LOG2E))
+    e = _rel(o[rows].float(), _ref_rows(qs[rows], k, v, LN2))
     print(f"|v| ~ 2^{vexp}: offset above the true max {float(gap.min()):.1f} .. {float(gap.max()):.1f} (log2), "
           f"asm / compiled waves {st.tolist()}, rel vs fp64 {e:.2e}")
     assert float(gap.max()) > 95.0  # rows really sit near the window's low edge

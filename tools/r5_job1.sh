@@ -12,7 +12,7 @@ run() {  # name, seconds, command...
   grep -E "passed|failed|Error|views/s" "gpurun_out/$name.log" | cut -c1-300 | tail -n 6
   if [ $rc -ne 0 ]; then echo "== $name failed rc=$rc"; tail -n 40 "gpurun_out/$name.log"; exit $rc; fi
 }
-run j1_tests 1100 python -u -m pytest tests -x -q -s -m gpu --timeout 600 --timeout-method thread
+run j1_tests 1100 python -u -m pytest tests --maxfail=15 -q -s -m gpu --timeout 600 --timeout-method thread
 run j1_bench_qs1 300 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --extras ''
 SR_Q_PRESCALE=0 run j1_bench_qs0 300 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --extras ''
 run j1_bench_qs1b 300 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --extras ''
