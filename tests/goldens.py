@@ -141,12 +141,15 @@ def pil_load_reference(images, mode=None, square_target=None):
     return torch.stack(padded)
 
 
-# Full-model parity bounds, rel-L2 against the reference's fp32 goldens, per quantity class.  fp32
-# parity mode: 1e-4 everywhere (north star: pose within 1e-4 rel).  bf16 (autocast) mode: about 2x
-# the largest error measured on MI355X over every golden and sharded run (each test prints what it
-# measured, "PARITY ..." lines in the GPU logs), never above SURVEY §8(c)'s 2e-2.
-PARITY_TOL = {"fp32": {"feat": 1e-4, "pose": 1e-4},
-              "bf16": {"feat": 2e-2, "pose": 2e-2}}
+# Full-model parity bounds, rel-L2 against the reference's fp32 goldens, per quantity class: about
+# 2-4x the largest error measured on MI355X over every golden, sharded run and residual mode (each
+# test prints what it measured: "PARITY ..." lines in the GPU logs, profiles/r05_*gputests*.log),
+# never above SURVEY §8(c)'s 2e-2 (bf16) or the north star's 1e-4 (pose, fp32).  Measured round 5
+# (c*q rounded once, round-4 kernels otherwise):
+#   fp32  feat 2.7e-6 (C3 camera tokens)   pose 3.2e-7 (C3 sharded extrinsic)
+#   bf16  feat 4.7e-3 (C3 deferred-residual camera columns of layer 23)   pose 8.1e-4 (N=1 @518 extrinsic)
+PARITY_TOL = {"fp32": {"feat": 1e-5, "pose": 1e-5},
+              "bf16": {"feat": 1e-2, "pose": 2e-3}}
 
 
 def parity_tol(key: str, mode: str) -> float:

@@ -3,7 +3,8 @@ collectives on device tensors — the GPU box has one GPU; the driver's 8-GPU ru
 RCCL).  Covers even and uneven anchor / query splits, the overlapped local-then-remote
 global attention with its LSE merge (sr_attn_merge; a two-segment remote pass on the middle
 rank of 3), and BASELINE config 2 (N=8 views @518) on 2 ranks.  The concatenated per-rank
-results must reproduce the reference golden vectors (fp32 1e-4, bf16 3e-2 rel-L2)."""
+results must reproduce the reference golden vectors at the full-model bounds (goldens.PARITY_TOL:
+fp32 1e-5; bf16 1e-2 features / 2e-3 poses rel-L2), every measured error printed."""
 
 import os
 import socket
@@ -170,7 +171,7 @@ def test_frame_sharded_c3_518_n32(tmp_path, world, mode):
     """BASELINE config 3 (the headline scene, N=32 views @518) frame-sharded
     over 2 ranks (16 / 16 anchors + queries) and 3 ranks (the uneven 11 / 11 / 10 split; the
     middle rank's remote global-attention pass has two key segments), every rank's features,
-    camera tokens and poses against the reference golden g10 (fp32 1e-4, bf16 3e-2)."""
+    camera tokens and poses against the reference golden g10 (goldens.PARITY_TOL)."""
     _run(tmp_path, world, "g10_518_n32.npz", mode)
 
 
@@ -197,6 +198,9 @@ def test_frame_sharded_n64_matches_one_rank(tmp_path, world):
         for k in ("cam_last", "pose", "ext"):
             errs[f"rank{i}_{k}"] = rel_l2(r[k], one[k])
     print(f"N=64 sharded over {world} vs one rank (bf16, rel-L2):", {k: float(f"{v:.2e}") for k, v in errs.items()})
-    bad = {k: v for k, v in errs.items() if not v < 2e-2}
+    # about 2x the round-4 / round-5 measurements (features <= 2.2e-3, camera tokens 3e-3, pose
+    # encodings 2.0e-4, extrinsics 5.2e-4)
+    bound = lambda k: 2e-3 if ("pose" in k or "ext" in k) else 6e-3  # noqa: E731
+    bad = {k: (v, bound(k)) for k, v in errs.items() if not v < bound(k)}
     assert not bad, bad
 

@@ -569,11 +569,14 @@ def test_gemm_tail_split(ops, epi_name, M, N):
     else:
         out1 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
         out0 = torch.zeros_like(out1)
+    kw1, kw0 = dict(kw), dict(kw)
+    if aux1 is not None:
+        kw1["aux"], kw0["aux"] = aux1, aux0
     with ops.tuning(SR_GEMM_TAIL=1):
-        ops.gemm(a, w, out1, epi, splits=1, aux=aux1, **kw)
+        ops.gemm(a, w, out1, epi, splits=1, **kw1)
         k1 = ops.last_kernel()
     with ops.tuning(SR_GEMM_TAIL=0):
-        ops.gemm(a, w, out0, epi, splits=1, aux=aux0, **kw)
+        ops.gemm(a, w, out0, epi, splits=1, **kw0)
         k0 = ops.last_kernel()
     torch.cuda.synchronize()
     assert k1 == k0 and k0.startswith("gemm256_kernel"), (k1, k0)

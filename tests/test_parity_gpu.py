@@ -1,10 +1,13 @@
 """End-to-end parity of the HIP path against the reference's golden vectors.
 
-fp32 parity mode (no autocast): exact-fp32 MFMA GEMMs + fp32 attention; tolerance
-1e-4 relative L2 (north star: pose within 1e-4 rel).
+fp32 parity mode (no autocast): exact-fp32 MFMA GEMMs + fp32 attention.
 bf16 mode (under torch.autocast, the demo_imc_forward.py:93 convention): bf16 MFMA
-GEMMs / attention with fp32 residual and fp32 camera head; tolerance 3e-2 relative L2
-(the reference's own bf16-vs-fp32 gap is 0.7-0.9 %).
+GEMMs / attention with fp32 residual and fp32 camera head (the reference's own bf16-vs-fp32 gap
+is 0.7-0.9 %).
+Bounds per quantity class (goldens.PARITY_TOL, rel-L2): fp32 1e-5 on features and poses (north
+star: pose within 1e-4); bf16 1e-2 on feature maps / camera tokens and 2e-3 on pose encodings /
+extrinsics / intrinsics -- about 2x the worst errors measured on MI355X (4.7e-3 / 8.1e-4), under
+SURVEY §8(c)'s 2e-2.  Every test prints its measured errors ("PARITY ..." lines).
 """
 
 import numpy as np
@@ -202,7 +205,7 @@ def test_full_deferred_residuals(full_model, fname, mode, monkeypatch):
 # fp8 global attention (BASELINE C5's precision, opt-in: Aggregator.set_fp8_global) at the C3
 # headline scene against the reference's fp32 golden.  No reference output pins an fp8 contract
 # (the reference runs bf16 SDPA); the tolerances below are the measured errors with ~2-4x headroom,
-# next to bf16's 3e-2.  Measured on MI355X (round 3, printed by the test): qk feature maps / camera
+# next to bf16's 1e-2 / 2e-3.  Measured on MI355X (round 3, printed by the test): qk feature maps / camera
 # tokens <= 4.4e-3, pose encoding / extrinsic / intrinsic <= 6.3e-4; qkv 4.6e-3 / 6.9e-4 -- the fp8
 # global attention adds little to the bf16 path's own gap at this scene.
 FP8_TOL = {"qk": {"feat": 1e-2, "pose": 3e-3}, "qkv": {"feat": 1e-2, "pose": 3e-3}}

@@ -391,6 +391,28 @@ def gemm_f32():
         print(f"gemm_f32 {name:24s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:7.1f} TF/s  {fl / ms / 1e9 / 157.3:6.1%}")
 
 
+def gemm_cam():
+    """The camera trunk's fp32 weight-streaming GEMMs (camera_head.py:163-168 trunk blocks at dim 2048,
+    M = 64 camera tokens at C3): time per launch and the weight-stream rate for each split-K count
+    (the automatic plan marked *)."""
+    M = 64
+    shapes = {"qkv  ": (6144, 2048, _lib.SR_EPI_BIAS), "proj ": (2048, 2048, _lib.SR_EPI_BIAS_RESID),
+              "fc1  ": (8192, 2048, _lib.SR_EPI_BIAS_GELU), "fc2  ": (2048, 8192, _lib.SR_EPI_BIAS_RESID)}
+    for name, (N, K, epi) in shapes.items():
+        a = torch.randn(M, K, device=DEV)
+        w = torch.randn(N, K, device=DEV) / 32
+        b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
+        out = torch.zeros(M, N, device=DEV)
+        auto = ops._splitk_plan(M, N, K, epi, torch.float32)
+        kt = K // 32
+        for s in sorted({1, 2, 4, 8, 16, 32, 64, auto}):
+            if kt % s or kt // s < 2:
+                continue
+            ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam, splits=s), reps=20)
+            print(f"gemm_cam {name} N={N} K={K} splits={s:2d}{'*' if s == auto else ' '} {ms * 1e3:8.1f} us  "
+                  f"{N * K * 4 / ms / 1e9:6.2f} TB/s weights")
+
+
 def torch_mm():
     """Yardstick only (not a product path): the library GEMM (torch.matmul -> hipBLASLt) at the
     block shapes, plain bf16 output, no epilogue."""
