@@ -79,7 +79,9 @@ enum sr_tuning_key {
                                the rows past its last whole round on the 128x128 kernel (second launch)  (1) */
   SR_TUNE_GEMM_PERSIST = 14,/* 1: the 256x256 GEMM as one persistent workgroup per CU walking its tiles,
                                the next tile's first K stage staged under the current epilogue   default 0 */
-  SR_TUNE_COUNT = 15
+  SR_TUNE_ATTN_QTAIL = 15,  /* 1: a bf16 attention whose query sets end in a q-tile of <= 128 rows runs
+                               those rows as a second launch of 128-row workgroups      default 1 */
+  SR_TUNE_COUNT = 16
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -92,6 +92,18 @@ __device__ __forceinline__ void rope_pos(const sr_gemm_epi& ep, int row, int& py
   }
 }
 
+// v[l] + v[l ^ 16] and v[l] + v[l ^ 32] through the gfx950 row-swap permutes (one VALU op each, no
+// LDS round trip as __shfl_xor's ds_bpermute has); the even row's value is always the left operand,
+// so both lanes of a pair get the same bits
+__device__ __forceinline__ float sum_x16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

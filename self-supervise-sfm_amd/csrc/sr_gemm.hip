@@ -91,9 +91,14 @@ using AuxT = T;
 // acc[mi][ni] holds the C^T 16x16 tile (W rows as the MFMA A operand): lane owns output
 // row  rowbase + mi*16 + lr  and the 4 CONSECUTIVE columns  colw + ni*16 + 4*lg + r.
 // Rows >= M are emitted too; the sink drops them.
+// RoPE tables of the QKV epilogue staged into LDS by the 256x256 kernels (stage_rope): cos rows at
+// offset 0, sin rows at ROPE_LDS / 2, 64 B per position (16 floats), up to ROPE_LDS_POS positions
+constexpr int ROPE_LDS = 8192;
+constexpr int ROPE_LDS_POS = ROPE_LDS / 2 / 64;
+
 template <typename T, int EPI, int MT, typename Emit>
 __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
-                                        int lg, Emit&& emit) {
+                                        int lg, Emit&& emit, const char* rope_lds = nullptr) {
   const sr_gemm_epi& ep = g.ep;
   float4 bias[4];
 #pragma unroll
@@ -218,8 +223,7 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
         float sum = 0.f;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) sum += (v[ni][0] + v[ni][1]) + (v[ni][2] + v[ni][3]);
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
+        sum = sr::sum_x32(sr::sum_x16(sum));
         const float mean = sum * (1.f / 64.f);
         float d2 = 0.f;
 #pragma unroll
@@ -229,8 +233,7 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
             v[ni][r] -= mean;
             d2 += v[ni][r] * v[ni][r];
           }
-        d2 += __shfl_xor(d2, 16, 64);
-        d2 += __shfl_xor(d2, 32, 64);
+        d2 = sr::sum_x32(sr::sum_x16(d2));
         const float rstd = rsqrtf(d2 * (1.f / 64.f) + ep.qk_eps);
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
@@ -243,10 +246,18 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
       if (do_rope) {  // pairs (d, d+16): y half ni 0|1, x half ni 2|3; same lane, same r
         int py, px;
         sr::rope_pos(ep, min(row, g.M - 1), py, px);
-        const float4 cy = *(const float4*)(ep.rope_cos + py * 16 + 4 * lg);
-        const float4 sy = *(const float4*)(ep.rope_sin + py * 16 + 4 * lg);
-        const float4 cx = *(const float4*)(ep.rope_cos + px * 16 + 4 * lg);
-        const float4 sx = *(const float4*)(ep.rope_sin + px * 16 + 4 * lg);
+        float4 cy, sy, cx, sx;
+        if (rope_lds) {  // the tables in LDS (no global-load latency per row)
+          cy = *(const float4*)(rope_lds + py * 64 + 16 * lg);
+          sy = *(const float4*)(rope_lds + ROPE_LDS / 2 + py * 64 + 16 * lg);
+          cx = *(const float4*)(rope_lds + px * 64 + 16 * lg);
+          sx = *(const float4*)(rope_lds + ROPE_LDS / 2 + px * 64 + 16 * lg);
+        } else {
+          cy = *(const float4*)(ep.rope_cos + py * 16 + 4 * lg);
+          sy = *(const float4*)(ep.rope_sin + py * 16 + 4 * lg);
+          cx = *(const float4*)(ep.rope_cos + px * 16 + 4 * lg);
+          sx = *(const float4*)(ep.rope_sin + px * 16 + 4 * lg);
+        }
         const float cyv[4] = {cy.x, cy.y, cy.z, cy.w}, syv[4] = {sy.x, sy.y, sy.z, sy.w};
         const float cxv[4] = {cx.x, cx.y, cx.z, cx.w}, sxv[4] = {sx.x, sx.y, sx.z, sx.w};
 #pragma unroll
@@ -274,7 +285,7 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
 // Register epilogue: every lane stores its own 4-column vectors (8 B bf16 / 16 B fp32).
 template <typename T, int EPI, int MT>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
-                                         int lg) {
+                                         int lg, const char* rope_lds = nullptr) {
   const sr_gemm_epi& ep = g.ep;
   if constexpr (EPI == SR_EPI_PATCH) {
     float4 bias[4];
@@ -325,7 +336,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x4 (&acc)[MT][4],
         const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         *(bf16x4*)((T*)g.out + (int64_t)row * g.ldo + col) = o;
       }
-    });
+    }, rope_lds);
   }
 }
 
@@ -410,7 +421,8 @@ __device__ __forceinline__ void bias_full(const GemmArgs& g, f32x4 (&acc)[8][4],
 // and the copy-out's row reads are both bank-conflict free.
 template <int EPI>
 __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4], char* smem, int m0, int n0,
-                                            int wr, int wc, int lr, int lg, int lane, int wave) {
+                                            int wr, int wc, int lr, int lg, int lane, int wave,
+                                            const char* rope_lds = nullptr) {
   if constexpr (EPI == SR_EPI_PATCH) {
     epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
   } else if constexpr (EPI == SR_EPI_BIAS_RESID) {
@@ -452,7 +464,7 @@ __device__ __forceinline__ void epilogue256(const GemmArgs& g, f32x4 (&acc)[8][4
       const int rl = row - m0, cl = col - n0;
       const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       *(bf16x4*)(smem + rl * 512 + (((cl >> 3) ^ (rl & 15)) << 4) + ((cl & 7) << 1)) = o;
-    });
+    }, rope_lds);
     sr::barrier_raw();
     bf16* out = (bf16*)g.out;
     if (m0 + 256 <= g.M) {
@@ -669,13 +681,37 @@ __device__ __forceinline__ void tile_origin(const GemmArgs& g, int tile, int& m0
   n0 = tn * BIG;
 }
 
+// QKV: the RoPE cos / sin tables into LDS (ROPE_LDS bytes past the two K stages) by LDS-DMA, one
+// 1-KiB piece per wave (8 waves: pieces 0-3 of cos, 0-3 of sin); lanes past a table's end re-read its
+// last 16 B (no read past the allocation).  Issued before the first K stage, so the first k-tile's
+// vmcnt(0) + barrier covers it.  Returns the tables' LDS base, or nullptr when they do not fit (the
+// epilogue then reads them from global memory).
+template <int EPI>
+__device__ __forceinline__ const char* stage_rope(const GemmArgs& g, char* smem) {
+  if constexpr (EPI != SR_EPI_QKV) {
+    return nullptr;
+  } else {
+    const sr_gemm_epi& ep = g.ep;
+    if (!ep.rope_cos || ep.rope_npos > ROPE_LDS_POS) return nullptr;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bytes = ep.rope_npos * 64, piece = wave & 3;
+    if (piece * 1024 < bytes) {
+      const char* tab = (const char*)(wave < 4 ? ep.rope_cos : ep.rope_sin);
+      const int off = min(piece * 1024 + lane * 16, bytes - 16);
+      sr::dma16(tab + off, __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + 2 * STAGE_BIG +
+                                                          (wave < 4 ? 0 : ROPE_LDS / 2) + piece * 1024));
+    }
+    return smem + 2 * STAGE_BIG;
+  }
+}
+
 // One output tile over k-tiles [kb, ke).  ``staged``: stage kb already issued (by the previous
 // tile of a persistent workgroup).  ``next_tile`` >= 0 (persistent walk, kb = 0): this tile's
 // epilogue first issues the next tile's stage 0 into LDS buffer 0 (free once every wave is past
 // the k-loop), so that its DMA overlaps the epilogue; returns whether it did.
 template <int EPI>
 __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke, bool staged = false,
-                                             int next_tile = -1) {
+                                             int next_tile = -1, const char* rope_lds = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int m0, n0;
   tile_origin(g, tile, m0, n0);
@@ -812,19 +848,24 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
   if (g.lds_epi) {
     // the LDS-staged epilogue uses both buffers: the next tile's stage goes out after it (every
     // wave's copy-out reads are complete once it stores their data)
-    epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave);
+    epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave, rope_lds);
     return prefetch_next();
   }
   const bool pf = prefetch_next();
-  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
+  epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg, rope_lds);
   return pf;
 }
 
+// LDS of the 256x256 kernels: two K stages, plus the RoPE tables for QKV (one array: a second
+// __shared__ object can make hipcc drain the LDS-DMA ring, cdna_hip_programming.md §5 item 4(a))
+template <int EPI> constexpr int smem256() { return 2 * STAGE_BIG + (EPI == SR_EPI_QKV ? ROPE_LDS : 0); }
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
-  gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles);
+  const char* rope = stage_rope<EPI>(g, smem);
+  gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, false, -1, rope);
 }
 
 // Persistent form (SR_TUNE_GEMM_PERSIST): one workgroup per CU walks tiles t = blockIdx.x + i *
@@ -833,12 +874,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 // next tile's first K stage, and no workgroup is relaunched between tiles.
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_persist_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
+  const char* rope = stage_rope<EPI>(g, smem);
   bool staged = false;
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
     const int nxt = t + (int)gridDim.x < nt ? sr::xcd_remap(t + gridDim.x, nt) : -1;
-    staged = gemm256_tile<EPI>(g, smem, sr::xcd_remap(t, nt), 0, g.ktiles, staged, nxt);
+    staged = gemm256_tile<EPI>(g, smem, sr::xcd_remap(t, nt), 0, g.ktiles, staged, nxt, rope);
   }
 }
 
@@ -856,7 +898,7 @@ struct GemmGroup {
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BIG];
+  __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
   int p = 0;
 #pragma unroll
   for (int i = 1; i < GROUP_MAX; ++i) p += (i < gg.n && (int)blockIdx.x >= gg.start[i]) ? 1 : 0;
@@ -864,7 +906,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
   const int lin = blockIdx.x - gg.start[p];
   if (lin >= nt) return;  // padding
-  gemm256_tile<EPI>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles);
+  const char* rope = stage_rope<EPI>(g, smem);
+  gemm256_tile<EPI>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, false, -1, rope);
 }
 
 

@@ -591,8 +591,11 @@ class Aggregator(nn.Module):
                      lse=lse_a.view(-1), q_scaled=_qs(pr)),
                 heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
             self._reloc_own_pass(pr, qkv_r, kv_sub_all, sc.o[q0:q1], o_a, lse_a, Nq_l, P, n_sub_all, n_full)
-            keep(runtime.run_block_tail(pr, x, q0, q1, sc, defer=defer))
-            keep(runtime.run_block_tail(pg, x, a0, q0, sc, defer=defer))
+            if runtime.group_tails_wanted(max(q1 - q0, q0 - a0)):
+                out.extend(runtime.run_block_tails([(pr, q0, q1), (pg, a0, q0)], x, sc, defer=defer))
+            else:
+                keep(runtime.run_block_tail(pr, x, q0, q1, sc, defer=defer))
+                keep(runtime.run_block_tail(pg, x, a0, q0, sc, defer=defer))
             return out
         # G == 1: the reloc block (query rows) and the global block (anchor rows) are independent.
         # SR_CONCURRENT_STACKS=1 runs the reloc block on a side stream so that each could fill the
@@ -603,6 +606,9 @@ class Aggregator(nn.Module):
         # more -- the roofline of the dominant kernel reads 0.40 instead of 0.50.  Off by default,
         # so that the bench's roofline stays a measurement of the kernel.
         side = self._side_stream(dev) if (G == 1 and Nq_l > 0 and a0 < q0) else None
+        # frame-sharded: the reloc block's tail waits for the global attention and runs grouped with
+        # the global block's (runtime.run_block_tails: one launch per GEMM stage over both row ranges)
+        group_tails = G > 1 and Nq_l > 0 and runtime.group_tails_wanted(max(q1 - q0, q0 - a0))
         if Nq_l > 0:
             def attend_reloc(qkv, o):
                 _wait(work_sub)
@@ -634,6 +640,11 @@ class Aggregator(nn.Module):
                     runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
                                       runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
                                       q_scale=runtime.q_prescale(pr))
+            elif group_tails:  # the tail joins the global block's in run_block_tails below
+                runtime.run_block_head(pr, x, q0, q1, sc,
+                                       runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
+                                       runtime.q_prescale(pr))
+                attend_reloc(sc.qkv[q0:q1], sc.o[q0:q1])
             else:
                 keep(runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
                                        runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
@@ -647,7 +658,10 @@ class Aggregator(nn.Module):
             else:
                 _wait(work_kv)
                 self._global_attention(q, kv_all[:, 0:C], kv_all[:, C:2 * C], o, pg, La_l, La)
-            keep(runtime.run_block_tail(pg, x, a0, q0, sc, defer=defer))
+            if group_tails:
+                out.extend(runtime.run_block_tails([(pr, q0, q1), (pg, a0, q0)], x, sc, defer=defer))
+            else:
+                keep(runtime.run_block_tail(pg, x, a0, q0, sc, defer=defer))
         else:
             def attend_global(qkv, o):
                 self._global_attention(qkv[:, 0:C], qkv[:, C:2 * C], qkv[:, 2 * C:3 * C], o, pg, La, La)

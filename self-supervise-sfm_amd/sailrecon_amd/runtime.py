@@ -347,6 +347,46 @@ def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
     return mlp_residual(pb, x, r0, r1, sc, defer)
 
 
+# SR_GROUP_TAILS: 0 = never group, 1 = only blocks under GROUP_TAILS_MAX_ROWS rows (a frame-sharded
+# rank's 5,496-row global / reloc blocks), 2 = always
+_GROUP_TAILS = int(os.environ.get("SR_GROUP_TAILS", "1"))
+GROUP_TAILS_MAX_ROWS = 16384
+
+
+def group_tails_wanted(rows: int) -> bool:
+    return _GROUP_TAILS >= 2 or (_GROUP_TAILS == 1 and rows <= GROUP_TAILS_MAX_ROWS)
+
+
+def run_block_tails(items, x: Tensor, sc: BlockScratch, defer: bool = False) -> list:
+    """run_block_tail of several blocks over disjoint row ranges (``items`` = [(pb, r0, r1)]),
+    each GEMM stage as ONE sr_gemm_group launch: proj (+LayerScale residual) of every block, the
+    LayerNorms, fc1 (+GELU), fc2 (+residual).  The per-rank global (anchors) and reloc (queries)
+    blocks of a frame-sharded layer are 5,496 rows each at C3 / G = 8: one launch per stage fills
+    the CUs that two under-filled ones leave idle.  Per output tile the k order and epilogue are
+    those of sr_gemm, so the result does not depend on the grouping.  Returns the Pending updates
+    (only without grouping: grouped tails keep the fused residual epilogues)."""
+    items = [(pb, r0, r1) for pb, r0, r1 in items if r1 > r0]
+    grouped = (len(items) > 1 and not _FUSED_RESID_LN and not (defer and any(defer_enabled(pb) for pb, _, _ in items))
+               and all(pb.w_proj is not None and pb.w_fc1 is not None for pb, _, _ in items))
+    if grouped:
+        hid = [pb.w_fc1.shape[0] for pb, _, _ in items]
+        proj = [dict(a=sc.o[r0:r1], w=pb.w_proj, out=x[r0:r1], bias=pb.b_proj, gamma=pb.g1) for pb, r0, r1 in items]
+        fc1 = [dict(a=sc.xn[r0:r1], w=pb.w_fc1, out=sc.h[r0:r1, :n], bias=pb.b_fc1)
+               for (pb, r0, r1), n in zip(items, hid)]
+        fc2 = [dict(a=sc.h[r0:r1, :n], w=pb.w_fc2, out=x[r0:r1], bias=pb.b_fc2, gamma=pb.g2)
+               for (pb, r0, r1), n in zip(items, hid)]
+        grouped = all(ops.gemm_group_eligible(p) for p in (proj, fc1, fc2))
+    if not grouped:
+        out = [run_block_tail(pb, x, r0, r1, sc, defer) for pb, r0, r1 in items]
+        return [p for p in out if p is not None]
+    ops.gemm_group(proj, _lib.SR_EPI_BIAS_RESID, tag="gemm")
+    for pb, r0, r1 in items:
+        ops.layernorm(x[r0:r1], pb.ln2_w, pb.ln2_b, pb.eps, sc.xn[r0:r1])
+    ops.gemm_group(fc1, _lib.SR_EPI_BIAS_GELU, tag="gemm")
+    ops.gemm_group(fc2, _lib.SR_EPI_BIAS_RESID, tag="gemm")
+    return []
+
+
 def frame_attend(pb: PackedBlock, frames: int, tokens: int, tail_readable: bool = False,
                  q_scaled: bool = False) -> Callable[[Tensor, Tensor], None]:
     """Attention within each frame of ``tokens`` rows (attention.py:103 over [B*S, P, C]).

@@ -71,6 +71,12 @@ def gemm(a, w, out, epi, *, bias=None, gamma=None, rows=None, qkv=None, patch=No
         raise ValueError(epi)
 
 
+def gemm_group(problems, epi, tag=None):
+    for p in problems:
+        gemm(p["a"], p["w"], p["out"], epi, bias=p.get("bias"), gamma=p.get("gamma"), qkv=p.get("qkv"),
+             q_scale=p.get("q_scale", 0.0), q_cols=p.get("q_cols", 0))
+
+
 def _positions(qkv, M):
     if qkv.get("pos_yx") is not None:
         p = qkv["pos_yx"].long()
@@ -239,7 +245,7 @@ def pose_decode(enc, hw, ext, intr):
     intr.copy_(i[0])
 
 
-_NAMES = ["gemm", "attention", "attn_merge", "attention_partials", "attn_merge_n", "layernorm", "residual_layernorm",
+_NAMES = ["gemm", "gemm_group", "attention", "attn_merge", "attention_partials", "attn_merge_n", "layernorm", "residual_layernorm",
           "im2col_normalize", "set_special_tokens", "copy_rows", "linear_small",
           "silu", "adaln_modulate", "pose_update", "pose_decode"]
 

@@ -54,11 +54,19 @@ def _worker(rank, world, port, out_dir, golden, overlap):
     no_reloc, reloc = _lists(g)
     m = small_model()
     m.aggregator.set_frame_sharding(dist.group.WORLD)
-    m.aggregator.shard_overlap = overlap
+    m.aggregator.shard_overlap = overlap != "no-overlap"
     m.aggregator.generator.manual_seed(0)  # identical draws on every rank
+    groups = []
     with cpu_ops.installed(), torch.no_grad():
+        if overlap == "group-tails":  # every stage eligible: the grouped global + reloc tails run
+            from sailrecon_amd import ops as real_ops
+            real_ops.gemm_group_eligible = lambda probs: True
+            gg = real_ops.gemm_group
+            real_ops.gemm_group = lambda probs, epi, tag=None: (groups.append(len(probs)), gg(probs, epi, tag))
         feats, psi, cam_last = m.aggregator(images, no_reloc, reloc, fix_rank=int(g["fix_rank"]))
         poses = m.camera_head([m.aggregator.last_query_cam_tokens[:, :, None]], cam_last)
+    if overlap == "group-tails":  # 3 grouped stages per layer, each over both blocks
+        assert groups == [2] * 3 * m.aggregator.depth, groups
     res = {f"feat_{layer}": feats[layer].numpy() for layer in (0, 1)}
     res["cam_last"] = cam_last.numpy()
     res["pose"] = np.stack([p.numpy() for p in poses])
@@ -68,13 +76,14 @@ def _worker(rank, world, port, out_dir, golden, overlap):
 
 
 CASES = [  # (world, golden, overlap): anchors / queries per rank
-    (2, "g1_small_56.npz", True),       # 1,1
-    (2, "g1_small_70.npz", True),       # 2,1  uneven
-    (2, "g1_small_70.npz", False),      # 2,1  uneven, one pass after the gather
-    (3, "g1_small_70.npz", True),       # 1,1,1
-    (3, "g1_small_56_n5.npz", True),    # 2,2,1  uneven
-    (3, "g1_small_56_n5.npz", False),
-    (3, "g11_small_interleaved.npz", True),  # 1,1,1, permuted + interleaved frame lists
+    (2, "g1_small_56.npz", "overlap"),       # 1,1
+    (2, "g1_small_70.npz", "overlap"),       # 2,1  uneven
+    (2, "g1_small_70.npz", "no-overlap"),    # 2,1  uneven, one pass after the gather
+    (3, "g1_small_70.npz", "overlap"),       # 1,1,1
+    (3, "g1_small_56_n5.npz", "overlap"),    # 2,2,1  uneven
+    (3, "g1_small_56_n5.npz", "no-overlap"),
+    (3, "g1_small_56_n5.npz", "group-tails"),  # the global + reloc tails as grouped GEMM stages
+    (3, "g11_small_interleaved.npz", "overlap"),  # 1,1,1, permuted + interleaved frame lists
 ]
 
 

@@ -218,6 +218,35 @@ def attn_frame_cfg():
         print(f"attn frame cfg {cfg} ({kern}): {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s", flush=True)
 
 
+def attn_qtail():
+    """SR_ATTN_QTAIL A/B, interleaved: the frame / DINO attention (64 frames x 1374 tokens) and the
+    C3 reloc own-frame pass (32 query frames against the subsample's last partial tile + their own
+    1374 keys, merging the subsample pass in) with the 94 rows past each frame's whole 256-row
+    q-tiles in a second launch of 128-row workgroups (1) or in a padded 4 x 2 tile (0)."""
+    C, H, D, P, S = 1024, 16, 64, 1374, 64
+    qkv = torch.randn(S * P + 64, 3 * C, device=DEV, dtype=torch.bfloat16)[:S * P]
+    o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
+    kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())
+    nq, ntail = 32, 32 * 305 % 64
+    sub = torch.randn(ntail + 64, 2 * C, device=DEV, dtype=torch.bfloat16)
+    mo = torch.randn(nq * P, C, device=DEV, dtype=torch.bfloat16)
+    ml = torch.randn(H, nq * P, device=DEV)
+    fl_f = 4.0 * S * H * P * P * D
+    fl_r = 4.0 * nq * H * P * (P + ntail) * D
+    for qt in (0, 1, 0, 1):
+        with ops.tuning(SR_ATTN_QTAIL=qt):
+            ms = timeit(lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
+                                              batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P, key_norm_max=kb,
+                                              tail_readable=True), reps=20)
+            print(f"attn frame qtail={qt} ({ops.last_kernel()}): {ms:.3f} ms  {fl_f / ms / 1e9:.1f} TF/s", flush=True)
+            ms = timeit(lambda: ops.attention(qkv[:nq * P, :C], sub[:ntail, :C], sub[:ntail, C:], o[:nq * P], heads=H,
+                                              head_dim=D, batch=nq, lq=P, q_bstride=P, l0=ntail, k0_bstride=0,
+                                              k1=qkv[:nq * P, C:2 * C], v1=qkv[:nq * P, 2 * C:], l1=P, k1_bstride=P,
+                                              key_norm_max=kb, tail_readable=True, merge_o=mo, merge_lse=ml), reps=20)
+            print(f"attn reloc-own qtail={qt} ({ops.last_kernel()}): {ms:.3f} ms  {fl_r / ms / 1e9:.1f} TF/s",
+                  flush=True)
+
+
 def attn_frame_diag():
     """Where the frame attention loses against the long sweep: the same launch with no ragged
     q-tile (lq = 1280 = 5 x 256), with full key tiles (l0 = 1408), and with 4x longer key sweeps
@@ -357,6 +386,40 @@ def gemm(M=2 * 32 * 1374):
         ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=g))
         fl = 2.0 * M * N * K
         print(f"gemm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+
+
+def gemm_qkv(M=2 * 32 * 1374):
+    """The QKV projection at C3 rows: plain bias (DINO) against the fused qk-LayerNorm + 2-D RoPE +
+    c*q epilogue (the aggregator blocks, runtime.qkv_params(prescale=True)), and the layer's grouped
+    launch (queries' and anchors' QKV + the anchor-subsample K/V, sr_gemm_group)."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    N, K, C = 3072, 1024, 1024
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / 32
+    b = torch.randn(N, device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    rope = RotaryPositionEmbedding2D(100).tables(64, 38, DEV)
+    nw = [torch.rand(64, device=DEV) + 0.5 for _ in range(4)]
+    epi = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=nw[0], qn_b=nw[1] - 1, kn_w=nw[2], kn_b=nw[3] - 1,
+               rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37, pos_row_base=0,
+               q_scale=0.125 * 1.4426950408889634)
+    fl = 2.0 * M * N * K
+    for name, fn in (("bias", lambda: ops.gemm(a, w, out, _lib.SR_EPI_BIAS, bias=b)),
+                     ("qkv-norm-rope", lambda: ops.gemm(a, w, out, _lib.SR_EPI_QKV, bias=b, qkv=epi))):
+        ms = timeit(fn)
+        print(f"gemm_qkv {name:14s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+    half = M // 2
+    sub = torch.randint(0, half, (32 * 305,), device=DEV, dtype=torch.int32)
+    kv = torch.empty(sub.numel(), 2 * C, device=DEV, dtype=torch.bfloat16)
+    e_s = dict(epi, col_offset=C, pos_rowmap=sub)
+    e_s.pop("pos_row_base")
+    e_s.pop("q_scale")
+    probs = [dict(a=a[:half], w=w, out=out[:half], bias=b, qkv=epi),
+             dict(a=a[half:], w=w, out=out[half:], bias=b, qkv=dict(epi, pos_row_base=half)),
+             dict(a=a[:sub.numel()], w=w[C:], out=kv, bias=b[C:], qkv=e_s)]
+    ms = timeit(lambda: ops.gemm_group(probs, _lib.SR_EPI_QKV))
+    flg = fl + 2.0 * sub.numel() * 2 * C * K
+    print(f"gemm_qkv group (layer)    {ms:8.3f} ms  {flg / ms / 1e9:8.1f} TF/s  {flg / ms / 1e9 / PEAK:6.1%}")
 
 
 def gemm_k():
