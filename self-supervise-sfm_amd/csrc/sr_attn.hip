@@ -1817,7 +1817,8 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
       // Each wave's rows see the same code and key order as in the one-launch form.
       a.row_base = d.lq / 256 * 256;
       grid.x = (d.lq - a.row_base + 127) / 128;
-      SR_ATTN_LAUNCH(2, 2, false);
+      if (sr::tune(SR_TUNE_ATTN_QTAIL) == 2) SR_ATTN_LAUNCH(4, 1, false);  // 4 waves x 1 q-block
+      else SR_ATTN_LAUNCH(2, 2, false);
       a.row_base = 0;
       grid.x = d.lq / 256;
       SR_ATTN_LAUNCH(4, 2, false);

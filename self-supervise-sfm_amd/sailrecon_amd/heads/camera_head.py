@@ -87,8 +87,9 @@ class CameraHead(nn.Module):
         # pose tokens = cat(anchor cam tokens, query cam tokens) -> token_norm   :103-110
         raw = ws.get("cam_raw", M, C, f32, dev)
         rv = raw.view(B, Sc, C)
-        rv[:, :Na].copy_(cam_token_last_layer)  # [B, Na, 2C] device copy (plumbing)
-        rv[:, Na:].copy_(tokens[:, :, 0])
+        for b in range(B):  # the anchors' and the queries' camera tokens (row-strided) into one block
+            ops.copy_rows(rv[b, :Na], cam_token_last_layer[b], Na)
+            ops.copy_rows(rv[b, Na:], tokens[b, :, 0], Nq)
         tok = ws.get("cam_tok", M, C, f32, dev)
         ops.layernorm(raw, self.token_norm.weight, self.token_norm.bias, self.token_norm.eps, tok)
 

@@ -10,7 +10,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
-from typing import Optional
+from typing import Dict, Optional
 
 import torch
 
@@ -173,6 +173,33 @@ def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
     return splits
 
 
+_SKINNY_EPIS = (_lib.SR_EPI_BIAS, _lib.SR_EPI_BIAS_GELU, _lib.SR_EPI_BIAS_RESID, _lib.SR_EPI_F32)
+_SKINNY_COUNTERS: Dict[tuple, Tensor] = {}
+
+
+def _skinny_eligible(a: Tensor, M: int, N: int, K: int, epi: int, aux, out: Tensor) -> bool:
+    """fp32 GEMMs of <= 64 rows (the camera trunk) take sr_gemm_skinny_f32 (SR_GEMM_SKINNY=0: the
+    128x128 / 64x256 tiles with split-K and a reduction launch)."""
+    return (a.dtype == torch.float32 and out.dtype == torch.float32 and M <= 64 and N % 32 == 0 and K % 32 == 0
+            and epi in _SKINNY_EPIS and aux is None and get_tuning("SR_GEMM_SKINNY") != 0)
+
+
+def _gemm_skinny(a, lda, w, ldw, out, ldo, M, N, K, epi, ep) -> None:
+    lib = _lib.load()
+    splits = lib.sr_gemm_skinny_splits(M, N, K)
+    ws = cnt = None
+    if splits > 1:
+        ws = _splitk_workspace(a.device, splits * M * N)
+        key = _ws_stream_key(a.device)
+        cnt = _SKINNY_COUNTERS.get(key)
+        if cnt is None or cnt.numel() < N // 32:  # zeroed once; every launch leaves them zero
+            cnt = torch.zeros(max(N // 32, 1024), dtype=torch.int32, device=a.device)
+            _SKINNY_COUNTERS[key] = cnt
+    rc = lib.sr_gemm_skinny_f32(_stream(a), epi, _p(a), lda, _p(w), ldw, _p(out), ldo, M, N, K, splits, _p(ws),
+                                _p(cnt), ctypes.byref(ep))
+    check(rc, "sr_gemm_skinny_f32")
+
+
 def _ws_stream_key(device):
     """Scratch buffers are keyed by (device, current stream): launches on different streams (the
     opt-in concurrent reloc stack, SR_CONCURRENT_STACKS) never share one."""
@@ -249,6 +276,12 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         tag = f"gemm_{_EPI_NAME.get(epi, epi)}" + ("" if a.dtype == torch.bfloat16 else "_f32")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
+    if splits is None and _skinny_eligible(a, M, N, K, epi, aux, out):
+        _gemm_skinny(a, lda, w, ldw, out, ldo, M, N, K, epi, ep)
+        if timed:
+            TIMER.stop(tag, ev0, 2.0 * M * N * K, (M * K + N * K) * 4 + M * N * 4 * (2 if epi == _lib.SR_EPI_BIAS_RESID
+                                                                                     else 1), kernel=last_kernel())
+        return
     if splits is None:  # the split-K reduction has no aux output: saved pre-activations need one pass
         splits = 1 if aux is not None else _splitk_plan(M, N, K, epi, a.dtype)
     elif splits > 1 and aux is not None:
@@ -849,6 +882,8 @@ def mul_cols(x: Tensor, gamma: Tensor, out: Tensor) -> None:
 
 
 def copy_rows(dst: Tensor, src: Tensor, rows: int, rowmap: Optional[Tensor] = None) -> None:
+    if dst.dtype != torch.float32 or src.dtype != torch.float32 or src.shape[-1] < dst.shape[1]:
+        raise ValueError("copy_rows: fp32 rows, src at least as wide as dst")
     rc = _lib.load().sr_copy_rows_f32(_stream(dst), _p(dst), _rowmajor(dst, "dst"), _p(src), _rowmajor(src, "src"),
                                       _p(rowmap), rows, dst.shape[1])
     check(rc, "sr_copy_rows_f32")

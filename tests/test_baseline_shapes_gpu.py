@@ -538,7 +538,7 @@ def test_attention_q_tail_launch(ops, kind):
         ml = torch.randn(H, S * P, device=DEV, generator=torch.Generator(DEV).manual_seed(10)) * 4
         kw.update(k=ks, v=vs, l0=8 * PP, k0_bstride=0, k1=k, v1=v, l1=P, k1_bstride=P, merge_o=mo, merge_lse=ml)
     outs = []
-    for qt in (0, 1):
+    for qt in (0, 1, 2):  # one padded tile | 2 x 2 tail workgroups | 4 x 1
         o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
         lse = torch.empty(S, H, P, device=DEV)
         a = dict(kw)
@@ -548,9 +548,10 @@ def test_attention_q_tail_launch(ops, kind):
             assert ops.last_kernel() == f"attn_bf16_kernel<4, 2, {0 if kind == 'frame' else 1}, false>"
         outs.append((o, lse))
     torch.cuda.synchronize()
-    print(f"q-tail {kind}: max |o diff| {float((outs[0][0].float() - outs[1][0].float()).abs().max()):.3g}, "
-          f"max |lse diff| {float((outs[0][1] - outs[1][1]).abs().max()):.3g}")
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for i in (1, 2):
+        print(f"q-tail {kind} {i}: max |o diff| {float((outs[0][0].float() - outs[i][0].float()).abs().max()):.3g}, "
+              f"max |lse diff| {float((outs[0][1] - outs[i][1]).abs().max()):.3g}")
+        assert torch.equal(outs[0][0], outs[i][0]) and torch.equal(outs[0][1], outs[i][1])
     if kind == "frame":
         scale = D ** -0.5
         o = outs[1][0]

@@ -233,7 +233,7 @@ def attn_qtail():
     ml = torch.randn(H, nq * P, device=DEV)
     fl_f = 4.0 * S * H * P * P * D
     fl_r = 4.0 * nq * H * P * (P + ntail) * D
-    for qt in (0, 1, 0, 1):
+    for qt in (0, 1, 2, 0, 1, 2):
         with ops.tuning(SR_ATTN_QTAIL=qt):
             ms = timeit(lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
                                               batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P, key_norm_max=kb,
@@ -422,6 +422,23 @@ def gemm_qkv(M=2 * 32 * 1374):
     print(f"gemm_qkv group (layer)    {ms:8.3f} ms  {flg / ms / 1e9:8.1f} TF/s  {flg / ms / 1e9 / PEAK:6.1%}")
 
 
+def gemm_xpf():
+    """SR_GEMM_XPF A/B, interleaved: the residual GEMMs (proj K=1024, fc2 K=4096) over the C3 frame
+    rows with the x tile prefetched into L2 / MALL under the k-loop (1 or 2 rows per k-tile and wave)
+    or not (0)."""
+    M, N = 2 * 32 * 1374, 1024
+    x = torch.randn(M, N, device=DEV)
+    b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV) * 1e-3
+    for name, K in (("proj", 1024), ("fc2 ", 4096)):
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+        fl = 2.0 * M * N * K
+        for xpf in (0, 1, 2, 0, 1, 2):
+            with ops.tuning(SR_GEMM_XPF=xpf):
+                ms = timeit(lambda: ops.gemm(a, w, x, _lib.SR_EPI_BIAS_RESID, bias=b, gamma=gam), reps=10)
+            print(f"gemm_xpf {name} xpf={xpf} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
+
+
 def gemm_k():
     """Per-tile fixed cost of the 256x256 GEMM: exactly 5 rounds of 256 tiles (M = 81,920, N = 1024)
     at K = 256 ... 4096; time = fixed + K * per-k, the intercept is the prologue / epilogue / tile
@@ -474,6 +491,11 @@ def gemm_cam():
             ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam, splits=s), reps=20)
             print(f"gemm_cam {name} N={N} K={K} splits={s:2d}{'*' if s == auto else ' '} {ms * 1e3:8.1f} us  "
                   f"{N * K * 4 / ms / 1e9:6.2f} TB/s weights")
+        ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam), reps=20)  # sr_gemm_skinny_f32
+        fl = 2.0 * M * N * K
+        print(f"gemm_cam {name} N={N} K={K} skinny ({ops.last_kernel()}, "
+              f"{_lib.load().sr_gemm_skinny_splits(M, N, K)} slices) {ms * 1e3:8.1f} us  "
+              f"{N * K * 4 / ms / 1e9:6.2f} TB/s weights  {fl / ms / 1e9:6.1f} TF/s (f32 MFMA peak 157.3)")
 
 
 def torch_mm():
