@@ -81,11 +81,14 @@ enum sr_tuning_key {
                                the next tile's first K stage staged under the current epilogue   default 0 */
   SR_TUNE_ATTN_QTAIL = 15,  /* 1 | 2: a bf16 attention whose query sets end in a q-tile of <= 128 rows runs
                                those rows as a second launch of 128-row workgroups (1: 2 waves x 2
-                               q-blocks, 2: 4 x 1; 0: a padded 256-row tile)           default 1 */
+                               q-blocks, 2: 4 x 1; 0: a padded 256-row tile).  Bit-identical, and
+                               measured no faster at the frame shape        default 0 */
   SR_TUNE_GEMM_SKINNY = 16, /* 1: fp32 GEMMs of <= 64 rows take sr_gemm_skinny_f32 (ops.gemm's choice) (1) */
   SR_TUNE_GEMM_XPF = 17,    /* 256x256 RESID GEMMs: x rows prefetched into L2 / MALL per k-tile and wave
                                under the k-loop (0 off, 1 | 2, -1 auto)                 default 0 */
-  SR_TUNE_COUNT = 18
+  SR_TUNE_GEMM_ROPE_LDS = 18,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
+                               under the first k-tile; 0: from global memory)           default 1 */
+  SR_TUNE_COUNT = 19
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

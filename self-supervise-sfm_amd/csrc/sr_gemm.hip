@@ -46,6 +46,7 @@ struct GemmArgs {
   float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
   int group_m;       // 256x256 kernels: tile order in groups of group_m row tiles (<= 1: row-major)
   int xpf;           // 256x256 RESID: x rows prefetched per k-tile into L2 / MALL (SR_TUNE_GEMM_XPF)
+  int rope_lds;      // 256x256 QKV: RoPE tables staged in LDS (SR_TUNE_GEMM_ROPE_LDS)
   sr_gemm_epi ep;
   // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
   // (n, yo, xo) of the NHWC fp32 input x [n][H][W][C], A column k = (ky, kx, ci) — exactly
@@ -828,7 +829,7 @@ __device__ __forceinline__ const char* stage_rope(const GemmArgs& g, char* smem)
     return nullptr;
   } else {
     const sr_gemm_epi& ep = g.ep;
-    if (!ep.rope_cos || ep.rope_npos > ROPE_LDS_POS) return nullptr;
+    if (!ep.rope_cos || ep.rope_npos > ROPE_LDS_POS || !g.rope_lds) return nullptr;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int bytes = ep.rope_npos * 64, piece = wave & 3;
     if (piece * 1024 < bytes) {
@@ -1357,6 +1358,7 @@ static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda
   a.kt_per_split = a.ktiles;
   const int xpf = sr::tune(SR_TUNE_GEMM_XPF);
   a.xpf = epi != SR_EPI_BIAS_RESID || dtype != SR_BF16 ? 0 : xpf < 0 ? (a.ktiles >= 32 ? 1 : 2) : min(xpf, 2);
+  a.rope_lds = sr::tune(SR_TUNE_GEMM_ROPE_LDS) != 0;
   return SR_OK;
 }
 

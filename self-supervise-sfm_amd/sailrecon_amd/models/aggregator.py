@@ -549,8 +549,19 @@ class Aggregator(nn.Module):
             kv_loc = ws.get("kv_loc", La_l, 2 * C, dtype, dev)
             ops.layernorm(xs, pg.ln1_w, pg.ln1_b, pg.eps, xn)
             epi = runtime.qkv_params(pg, rope, prescale=True, pos_row_base=a0, **posctx)
-            runtime.qkv_gemm(pg, xn, pg.w_qkv[:C], qkv[:, :C], _sl(pg.b_qkv, 0, C), epi, runtime.q_prescale(pg))
-            self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
+            epi_kv = runtime.qkv_params(pg, rope, pos_row_base=a0, **posctx)
+            probs = []
+            if epi is not None and epi_kv is not None:
+                epi_kv["col_offset"] = C
+                probs = [dict(a=xn, w=pg.w_qkv[:C], out=qkv[:, :C], bias=_sl(pg.b_qkv, 0, C), qkv=epi),
+                         dict(a=xn, w=pg.w_qkv[C:], out=kv_loc, bias=_sl(pg.b_qkv, C, 3 * C), qkv=epi_kv)]
+            if probs and ops.gemm_group_eligible(probs):
+                # Q and K/V as ONE grouped launch: at G = 8 a rank's 5,496 anchor rows are 88 + 176
+                # tiles of 256^2, each under one workgroup round on its own
+                ops.gemm_group(probs, _lib.SR_EPI_QKV, tag="gemm")
+            else:
+                runtime.qkv_gemm(pg, xn, pg.w_qkv[:C], qkv[:, :C], _sl(pg.b_qkv, 0, C), epi, runtime.q_prescale(pg))
+                self._kv_gemm(pg, xn, kv_loc, rope, dict(pos_row_base=a0, **posctx))
             work_kv = gather_rows(kv_all, kv_loc, [c * P for c in a_counts], group, r)
         if paired:
             # G == 1, bf16: the queries' and anchors' QKV projections (and the anchor-subsample K/V

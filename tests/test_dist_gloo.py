@@ -65,8 +65,8 @@ def _worker(rank, world, port, out_dir, golden, overlap):
             real_ops.gemm_group = lambda probs, epi, tag=None: (groups.append(len(probs)), gg(probs, epi, tag))
         feats, psi, cam_last = m.aggregator(images, no_reloc, reloc, fix_rank=int(g["fix_rank"]))
         poses = m.camera_head([m.aggregator.last_query_cam_tokens[:, :, None]], cam_last)
-    if overlap == "group-tails":  # 3 grouped stages per layer, each over both blocks
-        assert groups == [2] * 3 * m.aggregator.depth, groups
+    if overlap == "group-tails":  # per layer: the global Q + K/V GEMMs, then the 3 tail stages of both blocks
+        assert groups == [2] * 4 * m.aggregator.depth, groups
     res = {f"feat_{layer}": feats[layer].numpy() for layer in (0, 1)}
     res["cam_last"] = cam_last.numpy()
     res["pose"] = np.stack([p.numpy() for p in poses])

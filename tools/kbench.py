@@ -404,10 +404,12 @@ def gemm_qkv(M=2 * 32 * 1374):
                rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37, pos_row_base=0,
                q_scale=0.125 * 1.4426950408889634)
     fl = 2.0 * M * N * K
-    for name, fn in (("bias", lambda: ops.gemm(a, w, out, _lib.SR_EPI_BIAS, bias=b)),
-                     ("qkv-norm-rope", lambda: ops.gemm(a, w, out, _lib.SR_EPI_QKV, bias=b, qkv=epi))):
-        ms = timeit(fn)
-        print(f"gemm_qkv {name:14s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+    ms = timeit(lambda: ops.gemm(a, w, out, _lib.SR_EPI_BIAS, bias=b))
+    print(f"gemm_qkv bias              M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
+    for lds in (0, 1, 0, 1):  # RoPE tables from global memory (0) or staged in LDS (1)
+        with ops.tuning(SR_GEMM_ROPE_LDS=lds):
+            ms = timeit(lambda: ops.gemm(a, w, out, _lib.SR_EPI_QKV, bias=b, qkv=epi))
+        print(f"gemm_qkv qkv-norm-rope lds={lds} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
     half = M // 2
     sub = torch.randint(0, half, (32 * 305,), device=DEV, dtype=torch.int32)
     kv = torch.empty(sub.numel(), 2 * C, device=DEV, dtype=torch.bfloat16)
@@ -417,9 +419,11 @@ def gemm_qkv(M=2 * 32 * 1374):
     probs = [dict(a=a[:half], w=w, out=out[:half], bias=b, qkv=epi),
              dict(a=a[half:], w=w, out=out[half:], bias=b, qkv=dict(epi, pos_row_base=half)),
              dict(a=a[:sub.numel()], w=w[C:], out=kv, bias=b[C:], qkv=e_s)]
-    ms = timeit(lambda: ops.gemm_group(probs, _lib.SR_EPI_QKV))
     flg = fl + 2.0 * sub.numel() * 2 * C * K
-    print(f"gemm_qkv group (layer)    {ms:8.3f} ms  {flg / ms / 1e9:8.1f} TF/s  {flg / ms / 1e9 / PEAK:6.1%}")
+    for lds in (0, 1, 0, 1):
+        with ops.tuning(SR_GEMM_ROPE_LDS=lds):
+            ms = timeit(lambda: ops.gemm_group(probs, _lib.SR_EPI_QKV))
+        print(f"gemm_qkv group (layer) lds={lds} {ms:8.3f} ms  {flg / ms / 1e9:8.1f} TF/s  {flg / ms / 1e9 / PEAK:6.1%}")
 
 
 def gemm_xpf():
