@@ -83,12 +83,11 @@ enum sr_tuning_key {
                                those rows as a second launch of 128-row workgroups (1: 2 waves x 2
                                q-blocks, 2: 4 x 1; 0: a padded 256-row tile).  Bit-identical, and
                                measured no faster at the frame shape        default 0 */
-  SR_TUNE_GEMM_SKINNY = 16, /* 1: fp32 GEMMs of <= 64 rows take sr_gemm_skinny_f32 (ops.gemm's choice) (1) */
-  SR_TUNE_GEMM_XPF = 17,    /* 256x256 RESID GEMMs: x rows prefetched into L2 / MALL per k-tile and wave
+  SR_TUNE_GEMM_XPF = 16,    /* 256x256 RESID GEMMs: x rows prefetched into L2 / MALL per k-tile and wave
                                under the k-loop (0 off, 1 | 2, -1 auto)                 default 0 */
-  SR_TUNE_GEMM_ROPE_LDS = 18,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
+  SR_TUNE_GEMM_ROPE_LDS = 17,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
                                under the first k-tile; 0: from global memory)           default 1 */
-  SR_TUNE_COUNT = 19
+  SR_TUNE_COUNT = 18
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);
@@ -199,20 +198,6 @@ int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, const sr_gemm_p
 int sr_gemm_splitk(sr_stream_t stream, int dtype, int epilogue, const void* A, int64_t lda, const void* W,
                    int64_t ldw, void* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,
                    const sr_gemm_epi* ep);
-
-/* Few-row fp32 GEMM (M <= 64; N % 32 == 0; K % 32 == 0): out = epilogue(A[M,K] . W[N,K]^T) with
- * epilogue BIAS, BIAS_GELU (exact erf), BIAS_RESID or F32.  Replaces the camera trunk's fp32
- * nn.Linear calls (camera_head.py:163-168 trunk Blocks: attention.py:73,120, mlp.py:34-40 at dim
- * 2048, M = the 2N camera tokens), which are bound by the f32 MFMA rate and the weight stream:
- * 64 x 32 output tiles x `splits` K slices spread evenly over the CUs.  sr_gemm_skinny_splits
- * gives the slice count for a shape (any count dividing K / 32 is accepted).  splits > 1 needs
- * `workspace` (splits * M * N floats, 16-B aligned) and `counters` (N / 32 uint32, all zero before
- * the first call; every call leaves them zero): the last slice of each output tile to finish sums
- * the slices in slice order (deterministic) and runs the epilogue, in the same launch. */
-int sr_gemm_skinny_splits(int M, int N, int K);
-int sr_gemm_skinny_f32(sr_stream_t stream, int epilogue, const float* A, int64_t lda, const float* W, int64_t ldw,
-                       float* out, int64_t ldo, int M, int N, int K, int splits, float* workspace,
-                       uint32_t* counters, const sr_gemm_epi* ep);
 
 /* ------------------------------------------------------------------------
  * Fused multi-head attention  O = softmax(scale * Q K^T + mask) V

@@ -165,27 +165,6 @@ void check() {
   ep.q_cols = 0;
   expect("sr_gemm_splitk 3 slices of 16 tiles", sr_gemm_splitk(nullptr, SR_BF16, SR_EPI_BIAS, fake(0), 1024, fake(1), 1024, fake(2), 1024, 64, 1024, 1024, 3, fake<float>(3), &ep), false);
   expect("sr_gemm_splitk 4 slices", sr_gemm_splitk(nullptr, SR_BF16, SR_EPI_BIAS, fake(0), 1024, fake(1), 1024, fake(2), 1024, 64, 1024, 1024, 4, fake<float>(3), &ep), true);
-  // few-row fp32 GEMMs (the camera trunk)
-  if (sr_gemm_skinny_splits(64, 6144, 2048) != 4 || sr_gemm_skinny_splits(64, 8192, 2048) != 1 ||
-      sr_gemm_skinny_splits(64, 2048, 8192) != 4 || sr_gemm_skinny_splits(65, 2048, 2048) != 1) {
-    std::printf("sr_gemm_skinny_splits plan  UNEXPECTED\n");
-    ++g_fail;
-  }
-  auto skinny = [&](int epi, int M, int N, int K, int splits, float* ws, uint32_t* cnt) {
-    return sr_gemm_skinny_f32(nullptr, epi, fake<float>(0), K, fake<float>(1), K, fake<float>(2), N, M, N, K, splits, ws,
-                              cnt, &ep);
-  };
-  expect("sr_gemm_skinny_f32 4 slices", skinny(SR_EPI_BIAS, 64, 6144, 2048, 4, fake<float>(3), fake<uint32_t>(4)), true);
-  expect("sr_gemm_skinny_f32 one slice, no workspace", skinny(SR_EPI_BIAS_GELU, 64, 8192, 2048, 1, nullptr, nullptr), true);
-  expect("sr_gemm_skinny_f32 M 65", skinny(SR_EPI_BIAS, 65, 6144, 2048, 1, nullptr, nullptr), false);
-  expect("sr_gemm_skinny_f32 N % 32", skinny(SR_EPI_BIAS, 64, 6160, 2048, 1, nullptr, nullptr), false);
-  expect("sr_gemm_skinny_f32 3 slices of 64 steps", skinny(SR_EPI_BIAS, 64, 6144, 2048, 3, fake<float>(3), fake<uint32_t>(4)), false);
-  expect("sr_gemm_skinny_f32 slices without counters", skinny(SR_EPI_BIAS, 64, 6144, 2048, 4, fake<float>(3), nullptr), false);
-  expect("sr_gemm_skinny_f32 QKV epilogue", skinny(SR_EPI_QKV, 64, 6144, 2048, 1, nullptr, nullptr), false);
-  const float* gamma0 = ep.gamma;
-  ep.gamma = nullptr;
-  expect("sr_gemm_skinny_f32 RESID without gamma", skinny(SR_EPI_BIAS_RESID, 64, 2048, 2048, 1, nullptr, nullptr), false);
-  ep.gamma = gamma0;
   std::vector<sr_gemm_problem> pr(5);
   for (auto& p : pr) {
     std::memset(&p, 0, sizeof(p));

@@ -18,7 +18,6 @@
 //   * epilogues fused in registers: bias, erf-GELU, LayerScale+residual, patch remap +
 //     positional add, and qk-LayerNorm + 2-D RoPE (each wave owns one 64-wide head).
 #include <algorithm>
-#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
@@ -30,7 +29,6 @@ namespace {
 
 constexpr int BM = 128, BN = 128;
 constexpr int ROWB = 128;                     // bytes per tile row per k-tile
-constexpr int STAGE_BYTES = (BM + BN) * ROWB; // 32 KiB
 constexpr int NTHREADS = 256;
 
 struct GemmArgs {
@@ -654,137 +652,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
     *(bf16x4*)((T*)g.out + (int64_t)row * g.ldo + col) = o;
   } else {
     *(f32x4*)((T*)g.out + (int64_t)row * g.ldo + col) = v;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Few-row fp32 GEMMs (sr_gemm_skinny_f32): the camera trunk's projections (camera_head.py:163-168
-// trunk Blocks at dim 2048: attention.py:73,120 and mlp.py:34-40 in fp32), M = the 2N camera
-// tokens (<= 64) against 2048 x 2048..8192 fp32 weights.  At 64 rows they are bound by the f32
-// MFMA rate (64 FLOP/clk/SIMD, 157 TF/s) and the weight stream, so what matters is that every CU
-// gets the same share: one workgroup per 64 x 32 output tile and K slice (sr_gemm_skinny_splits
-// spreads the tiles x slices evenly over 256 CUs).  The 4 waves interleave the slice's 32-wide
-// k-steps (wave w takes k 8w..8w+7, lane half h k 8w+4h..+3 as one float4, so the 4 waves of a
-// step read 128 B of every W row); operands come straight from global memory (A, 256 KB per 1024
-// of K, is shared by all workgroups through L2; W is streamed once), batches of SK_DEPTH steps in
-// flight under the previous batch's MFMAs.  The waves' partial tiles are summed in LDS in wave
-// order; with K slices, each slice writes its partial and the LAST workgroup of a tile (per-tile
-// counter) sums the slices in slice order and runs the epilogue -- deterministic, no second launch.
-constexpr int SK_TN = 32;    // output columns per workgroup
-constexpr int SK_KS = 32;    // k per step (4 waves x 8)
-constexpr int SK_DEPTH = 8;  // steps per load batch
-
-template <int EPI>
-__device__ __forceinline__ void skinny_store(const GemmArgs& g, int row, int col, f32x4 v) {
-  const sr_gemm_epi& ep = g.ep;
-  if (ep.bias) v += *(const f32x4*)(ep.bias + col);
-  if (EPI == SR_EPI_BIAS && ep.q_scale != 0.f && col < ep.q_cols) v *= ep.q_scale;
-  if constexpr (EPI == SR_EPI_BIAS_GELU) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = sr::gelu_erf(v[r]);
-  }
-  f32x4* op = (f32x4*)((float*)g.out + (int64_t)row * g.ldo + col);
-  if constexpr (EPI == SR_EPI_BIAS_RESID) *op += v * *(const f32x4*)(ep.gamma + col);
-  else *op = v;
-}
-
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_skinny_f32_kernel(GemmArgs g, int splits, unsigned* counters) {
-  __shared__ __attribute__((aligned(16))) float red[4][64][SK_TN + 4];
-  __shared__ int last;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = g.N / SK_TN;
-  const int tn = blockIdx.x % ntn, sl = blockIdx.x / ntn;
-  const int n0 = tn * SK_TN;
-  const int r = lane & 31, h = lane >> 5;
-  const int steps = g.K / SK_KS, per = steps / splits;
-  const int s0 = sl * per, s1 = s0 + per;
-  const int koff = 8 * wave + 4 * h;
-  const float* pa0 = (const float*)(g.A + (int64_t)min(r, g.M - 1) * g.lda_b) + koff;
-  const float* pa1 = (const float*)(g.A + (int64_t)min(r + 32, g.M - 1) * g.lda_b) + koff;
-  const float* pw = (const float*)(g.W + (int64_t)(n0 + r) * g.ldw_b) + koff;
-  f32x16 acc0 = {}, acc1 = {};
-  f32x4 xa[SK_DEPTH], xb[SK_DEPTH], xw[SK_DEPTH], ya[SK_DEPTH], yb[SK_DEPTH], yw[SK_DEPTH];
-  auto load = [&](f32x4 (&a0)[SK_DEPTH], f32x4 (&a1)[SK_DEPTH], f32x4 (&w)[SK_DEPTH], int st) {
-#pragma unroll
-    for (int j = 0; j < SK_DEPTH; ++j) {
-      const int k = min(st + j, s1 - 1) * SK_KS;  // past the slice: re-read its last step (unused)
-      w[j] = *(const f32x4*)(pw + k);
-      a0[j] = *(const f32x4*)(pa0 + k);
-      a1[j] = *(const f32x4*)(pa1 + k);
-    }
-  };
-  auto mma = [&](const f32x4 (&a0)[SK_DEPTH], const f32x4 (&a1)[SK_DEPTH], const f32x4 (&w)[SK_DEPTH], int st) {
-#pragma unroll
-    for (int j = 0; j < SK_DEPTH; ++j) {
-      if (st + j >= s1) break;  // wave-uniform
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j][e], w[j][e], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j][e], w[j][e], acc1, 0, 0, 0);
-      }
-    }
-  };
-  // the next batch's loads are unconditional (clamped to the slice), so that the compiler's counted
-  // vmcnt before each batch's MFMAs leaves the next batch in flight (a conditional load makes it
-  // wait for everything at the join)
-  load(xa, xb, xw, s0);
-  for (int st = s0; st < s1; st += 2 * SK_DEPTH) {
-    load(ya, yb, yw, st + SK_DEPTH);
-    mma(xa, xb, xw, st);
-    if (st + SK_DEPTH >= s1) break;
-    load(xa, xb, xw, st + 2 * SK_DEPTH);
-    mma(ya, yb, yw, st + SK_DEPTH);
-  }
-  // D[m][n]: n = lane & 31, m = (v & 3) + 8 (v >> 2) + 4 h (+ 32 for acc1)
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const int m = (v & 3) + 8 * (v >> 2) + 4 * h;
-    red[wave][m][r] = acc0[v];
-    red[wave][m + 32][r] = acc1[v];
-  }
-  __syncthreads();
-  // thread: row m = tid / 4, columns 8 (tid & 3) .. +7; the 4 waves summed in order
-  const int m = tid >> 2, c = (tid & 3) * 8;
-  f32x4 v0 = *(const f32x4*)&red[0][m][c], v1 = *(const f32x4*)&red[0][m][c + 4];
-#pragma unroll
-  for (int w = 1; w < 4; ++w) {
-    v0 += *(const f32x4*)&red[w][m][c];
-    v1 += *(const f32x4*)&red[w][m][c + 4];
-  }
-  const int col = n0 + c;
-  if (splits == 1) {
-    if (m < g.M) {
-      skinny_store<EPI>(g, m, col, v0);
-      skinny_store<EPI>(g, m, col + 4, v1);
-    }
-    return;
-  }
-  if (m < g.M) {
-    float* pp = g.partial + ((int64_t)sl * g.M + m) * g.N + col;
-    *(f32x4*)pp = v0;
-    *(f32x4*)(pp + 4) = v1;
-  }
-  __threadfence();  // this slice's partial is visible device-wide (every XCD's L2) ...
-  __syncthreads();
-  if (tid == 0) {   // ... before it is counted; the tile's last slice sums them all
-    const unsigned prev = __hip_atomic_fetch_add(counters + tn, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned)(splits - 1);
-    if (last) __hip_atomic_store(counters + tn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (m < g.M) {
-    const float* pp = g.partial + (int64_t)m * g.N + col;
-    const int64_t ss = (int64_t)g.M * g.N;
-    f32x4 u0 = *(const f32x4*)pp, u1 = *(const f32x4*)(pp + 4);
-    for (int z = 1; z < splits; ++z) {
-      u0 += *(const f32x4*)(pp + z * ss);
-      u1 += *(const f32x4*)(pp + z * ss + 4);
-    }
-    skinny_store<EPI>(g, m, col, u0);
-    skinny_store<EPI>(g, m, col + 4, u1);
   }
 }
 
@@ -1433,60 +1300,6 @@ extern "C" int sr_gemm_splitk(sr_stream_t stream, int dtype, int epi, const void
                               const sr_gemm_epi* ep) {
   SR_CHECK(splits >= 1, SR_EINVAL, "sr_gemm_splitk: splits=%d", splits);
   return gemm_common(stream, dtype, epi, A, lda, W, ldw, out, ldo, M, N, K, splits, workspace, ep);
-}
-
-extern "C" int sr_gemm_skinny_splits(int M, int N, int K) {
-  if (M < 1 || M > 64 || N % SK_TN || K % SK_KS) return 1;
-  // per-CU work in k-steps (workgroups spread evenly over 256 CUs) + the slices' partial round trip
-  const int ntn = N / SK_TN, steps = K / SK_KS;
-  int best = 1;
-  double bt = 1e30;
-  for (int s = 1; s <= 16; s *= 2) {
-    if (steps % s || steps / s < SK_DEPTH) continue;  // whole load batches per slice
-    const double t = std::ceil(ntn * s / 256.0) * (steps / s) + (s > 1 ? 2.0 * s : 0.0);
-    if (t < bt - 1e-9) {
-      bt = t;
-      best = s;
-    }
-  }
-  return best;
-}
-
-extern "C" int sr_gemm_skinny_f32(sr_stream_t stream, int epi, const float* A, int64_t lda, const float* W,
-                                  int64_t ldw, float* out, int64_t ldo, int M, int N, int K, int splits,
-                                  float* workspace, uint32_t* counters, const sr_gemm_epi* ep) {
-  GemmArgs a;
-  const int rc = gemm_args(a, SR_F32, epi, A, lda, W, ldw, out, ldo, M, N, K, ep);
-  if (rc != SR_OK) return rc;
-  SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID || epi == SR_EPI_F32,
-           SR_EUNSUPPORTED, "sr_gemm_skinny_f32: epilogue %d not supported", epi);
-  SR_CHECK(M <= 64 && N % SK_TN == 0 && K % SK_KS == 0, SR_EUNSUPPORTED,
-           "sr_gemm_skinny_f32: needs M <= 64, N %% 32 == 0, K %% 32 == 0 (M=%d N=%d K=%d)", M, N, K);
-  SR_CHECK(!ep->aux, SR_EUNSUPPORTED, "sr_gemm_skinny_f32: no aux output");
-  SR_CHECK(((uintptr_t)out % 16) == 0 && ldo % 4 == 0 && ldo >= N, SR_EINVAL,
-           "sr_gemm_skinny_f32: out must be 16-B aligned rows");
-  SR_CHECK((!ep->bias || ((uintptr_t)ep->bias % 16) == 0) && (!ep->gamma || ((uintptr_t)ep->gamma % 16) == 0),
-           SR_EINVAL, "sr_gemm_skinny_f32: bias / gamma must be 16-B aligned");
-  const int steps = K / SK_KS;
-  SR_CHECK(splits >= 1 && steps % splits == 0, SR_EINVAL, "sr_gemm_skinny_f32: %d k-steps not divisible into %d slices",
-           steps, splits);
-  if (splits > 1)
-    SR_CHECK(workspace && ((uintptr_t)workspace % 16) == 0 && counters && ((uintptr_t)counters % 4) == 0, SR_EINVAL,
-             "sr_gemm_skinny_f32: slices need a 16-B aligned workspace (splits*M*N floats) and N/32 counters");
-  a.partial = workspace;
-  const dim3 grid((unsigned)(N / SK_TN * splits));
-  hipStream_t s = (hipStream_t)stream;
-  unsigned* cnt = (unsigned*)counters;
-  switch (epi) {
-    case SR_EPI_BIAS: hipLaunchKernelGGL(gemm_skinny_f32_kernel<SR_EPI_BIAS>, grid, dim3(256), 0, s, a, splits, cnt); break;
-    case SR_EPI_BIAS_GELU:
-      hipLaunchKernelGGL(gemm_skinny_f32_kernel<SR_EPI_BIAS_GELU>, grid, dim3(256), 0, s, a, splits, cnt);
-      break;
-    case SR_EPI_F32: hipLaunchKernelGGL(gemm_skinny_f32_kernel<SR_EPI_F32>, grid, dim3(256), 0, s, a, splits, cnt); break;
-    default: hipLaunchKernelGGL(gemm_skinny_f32_kernel<SR_EPI_BIAS_RESID>, grid, dim3(256), 0, s, a, splits, cnt);
-  }
-  sr::note_kernel("gemm_skinny_f32_kernel<%d>", epi);
-  return sr::check_launch("sr_gemm_skinny_f32");
 }
 
 extern "C" int sr_conv3x3_f32(sr_stream_t stream, const float* x, int n, int h, int w, int c, int stride, int relu_in,

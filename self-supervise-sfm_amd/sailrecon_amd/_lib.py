@@ -127,9 +127,6 @@ _PROTOS = {
     "sr_gemm": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, ctypes.POINTER(GemmEpi)]),
     "sr_gemm_splitk": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                               ctypes.POINTER(GemmEpi)]),
-    "sr_gemm_skinny_splits": (_i32, [_i32, _i32, _i32]),
-    "sr_gemm_skinny_f32": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp,
-                                  ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_attention_pair": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnDesc)]),
     "sr_gemm_group": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(GemmProblem)]),

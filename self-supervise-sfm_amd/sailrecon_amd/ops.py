@@ -10,7 +10,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
-from typing import Dict, Optional
+from typing import Optional
 
 import torch
 
@@ -165,39 +165,15 @@ def _splitk_plan(M: int, N: int, K: int, epi: int, dtype: torch.dtype) -> int:
     ktiles = K // (64 if dtype == torch.bfloat16 else 32)
     # sr_gemm's tiles: 64 x 256 for M <= 64 (SR_GEMM_SMALLM), else 128 x 128
     wgs = -(-N // 256) if (M <= 64 and N > 128 and get_tuning("SR_GEMM_SMALLM")) else -(-M // 128) * (N // 128)
-    cap = max(1, K // (4 * M))  # partial-tile traffic (2 * splits * M * N) <= half the weight stream (N * K)
+    # partial-tile traffic (2 * splits * M * N) <= the weight stream (N * K), at most one workgroup per
+    # CU: measured best at the camera trunk's shapes (tools/kbench.py gemm_cam, M = 64, fp32: qkv 8,
+    # proj 16, fc1 8, fc2 32 slices; profiles/r05_j2_kbench_gemm_cam.log)
+    cap = max(1, K // (2 * M))
     splits = 1
-    while (wgs * splits * 2 <= 1024 and splits * 2 <= cap and ktiles % (splits * 2) == 0
+    while (wgs * splits * 2 <= 256 and splits * 2 <= cap and ktiles % (splits * 2) == 0
            and ktiles // (splits * 2) >= 4):
         splits *= 2
     return splits
-
-
-_SKINNY_EPIS = (_lib.SR_EPI_BIAS, _lib.SR_EPI_BIAS_GELU, _lib.SR_EPI_BIAS_RESID, _lib.SR_EPI_F32)
-_SKINNY_COUNTERS: Dict[tuple, Tensor] = {}
-
-
-def _skinny_eligible(a: Tensor, M: int, N: int, K: int, epi: int, aux, out: Tensor) -> bool:
-    """fp32 GEMMs of <= 64 rows (the camera trunk) take sr_gemm_skinny_f32 (SR_GEMM_SKINNY=0: the
-    128x128 / 64x256 tiles with split-K and a reduction launch)."""
-    return (a.dtype == torch.float32 and out.dtype == torch.float32 and M <= 64 and N % 32 == 0 and K % 32 == 0
-            and epi in _SKINNY_EPIS and aux is None and get_tuning("SR_GEMM_SKINNY") != 0)
-
-
-def _gemm_skinny(a, lda, w, ldw, out, ldo, M, N, K, epi, ep) -> None:
-    lib = _lib.load()
-    splits = lib.sr_gemm_skinny_splits(M, N, K)
-    ws = cnt = None
-    if splits > 1:
-        ws = _splitk_workspace(a.device, splits * M * N)
-        key = _ws_stream_key(a.device)
-        cnt = _SKINNY_COUNTERS.get(key)
-        if cnt is None or cnt.numel() < N // 32:  # zeroed once; every launch leaves them zero
-            cnt = torch.zeros(max(N // 32, 1024), dtype=torch.int32, device=a.device)
-            _SKINNY_COUNTERS[key] = cnt
-    rc = lib.sr_gemm_skinny_f32(_stream(a), epi, _p(a), lda, _p(w), ldw, _p(out), ldo, M, N, K, splits, _p(ws),
-                                _p(cnt), ctypes.byref(ep))
-    check(rc, "sr_gemm_skinny_f32")
 
 
 def _ws_stream_key(device):
@@ -276,12 +252,6 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         tag = f"gemm_{_EPI_NAME.get(epi, epi)}" + ("" if a.dtype == torch.bfloat16 else "_f32")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    if splits is None and _skinny_eligible(a, M, N, K, epi, aux, out):
-        _gemm_skinny(a, lda, w, ldw, out, ldo, M, N, K, epi, ep)
-        if timed:
-            TIMER.stop(tag, ev0, 2.0 * M * N * K, (M * K + N * K) * 4 + M * N * 4 * (2 if epi == _lib.SR_EPI_BIAS_RESID
-                                                                                     else 1), kernel=last_kernel())
-        return
     if splits is None:  # the split-K reduction has no aux output: saved pre-activations need one pass
         splits = 1 if aux is not None else _splitk_plan(M, N, K, epi, a.dtype)
     elif splits > 1 and aux is not None:

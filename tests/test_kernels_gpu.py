@@ -103,48 +103,6 @@ def test_gemm_splitk(ops, dtype, tol, M, N, K, splits):
     assert rel(o32, ref) < max(tol, 1e-5)
 
 
-@pytest.mark.parametrize("M", [64, 33, 2])
-@pytest.mark.parametrize("N,K", [(6144, 2048), (2048, 2048), (8192, 2048), (2048, 8192), (96, 256)])
-def test_gemm_skinny_f32(ops, M, N, K):
-    """sr_gemm_skinny_f32 (the camera trunk's fp32 GEMMs: qkv / proj / fc1 / fc2 at dim 2048, M = the
-    camera tokens): every epilogue against fp64, bitwise repeatable (the last K slice of each tile
-    sums the slices in slice order, whichever finishes last), the per-tile counters left at zero,
-    and against the split-K path it replaces (SR_GEMM_SKINNY=0)."""
-    L = _lib()
-    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
-    a = torch.randn(M, K, generator=g).to(DEV)
-    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
-    b, gam = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
-    ref = a.double() @ w.double().t() + b.double()
-    splits = L.load().sr_gemm_skinny_splits(M, N, K)
-    print(f"skinny M={M} N={N} K={K}: {splits} K slices")
-    out = torch.empty(M, N, device=DEV)
-    ops.gemm(a, w, out, L.SR_EPI_BIAS, bias=b)
-    assert ops.last_kernel() == "gemm_skinny_f32_kernel<0>"
-    assert rel(out, ref) < 1e-6
-    again = torch.empty_like(out)
-    for _ in range(3):
-        ops.gemm(a, w, again, L.SR_EPI_BIAS, bias=b)
-        assert torch.equal(again, out)
-    ops.gemm(a, w, out, L.SR_EPI_BIAS_GELU, bias=b)
-    assert rel(out, F.gelu(ref)) < 1e-6
-    x = torch.randn(M, N + 8, device=DEV)[:, :N]
-    x0 = x.clone()
-    ops.gemm(a, w, x, L.SR_EPI_BIAS_RESID, bias=b, gamma=gam)
-    assert rel(x.double() - x0.double(), ref * gam.double()) < 1e-6
-    o32 = torch.empty(M, N + 4, device=DEV)[:, :N]
-    ops.gemm(a, w, o32, L.SR_EPI_F32, bias=b)
-    assert rel(o32, ref) < 1e-6
-    with ops.tuning(SR_GEMM_SKINNY=0):
-        old = torch.empty(M, N, device=DEV)
-        ops.gemm(a, w, old, L.SR_EPI_BIAS, bias=b)
-        assert ops.last_kernel() != "gemm_skinny_f32_kernel<0>"
-    assert rel(old, again) < 2e-6  # the BIAS outputs of both paths
-    torch.cuda.synchronize()
-    cnt = [t for t in ops._SKINNY_COUNTERS.values()]
-    assert all(int(t.abs().sum()) == 0 for t in cnt)
-
-
 @pytest.mark.parametrize("M,K", [(33000, 1024), (43968, 4096), (8300, 256)])
 def test_gemm_resid_x_prefetch(ops, M, K):
     """SR_GEMM_XPF: the 256x256 residual GEMM fetching its x tile into L2 / MALL under the k-loop

@@ -495,11 +495,6 @@ def gemm_cam():
             ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam, splits=s), reps=20)
             print(f"gemm_cam {name} N={N} K={K} splits={s:2d}{'*' if s == auto else ' '} {ms * 1e3:8.1f} us  "
                   f"{N * K * 4 / ms / 1e9:6.2f} TB/s weights")
-        ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam), reps=20)  # sr_gemm_skinny_f32
-        fl = 2.0 * M * N * K
-        print(f"gemm_cam {name} N={N} K={K} skinny ({ops.last_kernel()}, "
-              f"{_lib.load().sr_gemm_skinny_splits(M, N, K)} slices) {ms * 1e3:8.1f} us  "
-              f"{N * K * 4 / ms / 1e9:6.2f} TB/s weights  {fl / ms / 1e9:6.1f} TF/s (f32 MFMA peak 157.3)")
 
 
 def torch_mm():
