@@ -1182,8 +1182,7 @@ __global__ __launch_bounds__(256) void key_norm_max_kernel(const bf16* __restric
   if (t < heads) red[t] = 0u;
   __syncthreads();
   float m = 0.f;
-  for (int r = blockIdx.x * rpi + row_in; r < rows; r += gridDim.x * rpi) {
-    const bf16x8 v = *(const bf16x8*)(k + (inst * inst_stride + r) * ldk + c * 8);
+  auto take = [&](const bf16x8 v) {
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ss = fmaf((float)v[j], (float)v[j], ss);
@@ -1191,7 +1190,19 @@ __global__ __launch_bounds__(256) void key_norm_max_kernel(const bf16* __restric
     ss += __shfl_xor(ss, 2, 64);
     ss += __shfl_xor(ss, 4, 64);
     m = fmaxf(m, ss);
+  };
+  // 4 rows' loads in flight per thread (one dependent load per iteration left the pass latency-bound)
+  const int step = gridDim.x * rpi;
+  const bf16* kb = k + inst * inst_stride * ldk + c * 8;
+  int r = blockIdx.x * rpi + row_in;
+  for (; r + 3 * step < rows; r += 4 * step) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(kb + (int64_t)(r + u * step) * ldk);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) take(v[u]);
   }
+  for (; r < rows; r += step) take(*(const bf16x8*)(kb + (int64_t)r * ldk));
   if ((c & 7) == 0) atomicMax(&red[head], __float_as_uint(m));
   __syncthreads();
   if (t < heads) atomicMax(&out[inst * heads + t], red[t]);

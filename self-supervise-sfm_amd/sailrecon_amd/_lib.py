@@ -214,8 +214,16 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             f"libsfm_amd.so not found at {path}: build it with `make -C self-supervise-sfm_amd/csrc` "
             "(there is no CPU fallback)")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    # an SFM_AMD_LIB override (an older build for a same-box A/B) may lack newer entry points: they
+    # stay unbound and fail if called; the in-tree library must export every one
+    override = bool(os.environ.get("SFM_AMD_LIB"))
     for name, (res, args) in _PROTOS.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if override:
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -955,3 +955,23 @@ def test_attention_window_low_edge(ops, vexp):
     assert float(gap.max()) > 95.0  # rows really sit near the window's low edge
     assert st.tolist()[1] == 0 and st.tolist()[0] == L // 64 * H
     assert e < 1e-2
+
+
+@pytest.mark.parametrize("batch,L,heads", [(64, 1374, 16), (3, 261, 6), (1, 4099, 16), (5, 7, 2)])
+def test_attention_key_scan(ops, batch, L, heads):
+    """The launch's own key scan (no static bound: DINO's blocks, key_norm_max = 0): sr_attention
+    fills key_bound with each (instance, head)'s max |k|^2 before the sweep (key_norm_max_kernel,
+    4 rows' loads in flight per thread, a plain loop for the rest) -- against torch on the same
+    bf16 keys, for row counts that leave every remainder of the unrolled loop."""
+    g = torch.Generator(device="cpu").manual_seed(batch * 1000 + L)
+    Cw = heads * D
+    qkv = (torch.randn(batch * L, 3 * Cw, generator=g) * torch.linspace(0.5, 2.0, 3 * Cw)).bfloat16().to(DEV)
+    o = torch.empty(batch * L, Cw, device=DEV, dtype=torch.bfloat16)
+    ops.attention(qkv[:, :Cw], qkv[:, Cw:2 * Cw], qkv[:, 2 * Cw:], o, heads=heads, head_dim=D, batch=batch, lq=L,
+                  q_bstride=L, l0=L, k0_bstride=L)
+    torch.cuda.synchronize()
+    kb = ops._train_ws(DEV, "attn_key_bound", batch * heads)[:batch * heads].view(batch, heads)
+    ref = (qkv[:, Cw:2 * Cw].float().view(batch, L, heads, D) ** 2).sum(-1).amax(1)
+    err = float(((kb - ref).abs() / ref).max())
+    print(f"key scan batch={batch} L={L} heads={heads}: max rel {err:.2e}")
+    assert err < 1e-6
