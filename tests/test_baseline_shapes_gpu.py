@@ -970,7 +970,7 @@ def test_attention_key_scan(ops, batch, L, heads):
     ops.attention(qkv[:, :Cw], qkv[:, Cw:2 * Cw], qkv[:, 2 * Cw:], o, heads=heads, head_dim=D, batch=batch, lq=L,
                   q_bstride=L, l0=L, k0_bstride=L)
     torch.cuda.synchronize()
-    kb = ops._train_ws(DEV, "attn_key_bound", batch * heads)[:batch * heads].view(batch, heads)
+    kb = ops._train_ws(qkv.device, "attn_key_bound", batch * heads)[:batch * heads].view(batch, heads)
     ref = (qkv[:, Cw:2 * Cw].float().view(batch, L, heads, D) ** 2).sum(-1).amax(1)
     err = float(((kb - ref).abs() / ref).max())
     print(f"key scan batch={batch} L={L} heads={heads}: max rel {err:.2e}")
