@@ -555,6 +555,8 @@ def main():
                 continue  # the headline already runs at a scaled gain
             extras.append(extra_config(model, device, args, world, name))
 
+    calib = box_calibration(device) if use_bf16 else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline({k: v for k, v in sd.items()}, args.img, n, args.cpu_views)
@@ -584,12 +586,39 @@ def main():
                        "algorithmic_tflop_per_step": round(tflop, 2),
                        "achieved_tflops_whole_step": round(tflop * args.steps / dt, 1)},
             "roofline": roofline,
+            "box_calibration": calib,
             "cpu_baseline": cpu,
             "extra_configs": extras,
         }
         print(json.dumps(line))
     if use_pg:
         dist.destroy_process_group()
+
+
+def box_calibration(device):
+    """One fixed kernel timed after the measured region, so that lines from different MI355X boxes
+    can be compared: MFMA-bound loops run 1-12 % apart across devices at the clock each holds under
+    load (MI355X_MICROARCH.md 'DVFS give-back' item 5).  The library's 256x256 bf16 GEMM on seeded
+    random 8192^3 operands (bias epilogue), 10 launches after 3 warm-up ones, HIP events."""
+    from sailrecon_amd import _lib, ops
+    n = 8192
+    g = torch.Generator(device=device).manual_seed(7)
+    a = torch.rand(n, n, device=device, generator=g, dtype=torch.float32).sub_(0.5).bfloat16()
+    w = torch.rand(n, n, device=device, generator=g, dtype=torch.float32).sub_(0.5).bfloat16()
+    out = torch.empty(n, n, device=device, dtype=torch.bfloat16)
+    for _ in range(3):
+        ops.gemm(a, w, out, _lib.SR_EPI_BIAS)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        ops.gemm(a, w, out, _lib.SR_EPI_BIAS)
+    e1.record()
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / 10
+    kern = ops.last_kernel()
+    del a, w, out
+    return {"kernel": kern, "shape": "8192^3 bf16, seeded U[-0.5, 0.5)", "avg_launch_ms": round(ms, 4),
+            "tflops": round(2.0 * n ** 3 / ms / 1e9, 1)}
 
 
 def extra_config(model, device, args, world, name):
