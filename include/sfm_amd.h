@@ -87,7 +87,9 @@ enum sr_tuning_key {
                                under the k-loop (0 off, 1 | 2, -1 auto)                 default 0 */
   SR_TUNE_GEMM_ROPE_LDS = 17,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
                                under the first k-tile; 0: from global memory)           default 1 */
-  SR_TUNE_COUNT = 18
+  SR_TUNE_GEMM_PP = 18,     /* 1: the 256x256 GEMM's ping-pong k-loop (each SIMD's two waves alternate
+                               MFMA and LDS phases; bit-identical)                     default 0 */
+  SR_TUNE_COUNT = 19
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -713,7 +713,7 @@ __device__ __forceinline__ const char* stage_rope(const GemmArgs& g, char* smem)
 // tile of a persistent workgroup).  ``next_tile`` >= 0 (persistent walk, kb = 0): this tile's
 // epilogue first issues the next tile's stage 0 into LDS buffer 0 (free once every wave is past
 // the k-loop), so that its DMA overlaps the epilogue; returns whether it did.
-template <int EPI, bool PERSIST = false>
+template <int EPI, bool PERSIST = false, bool PP = false>
 __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke, bool staged = false,
                                              int next_tile = -1, const char* rope_lds = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -780,14 +780,111 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
   // k-loop (wave w: rows m0 + 32w .. +31, 1 KiB each, xpf rows per k-tile, LDS-DMA into a sink), so
   // that the epilogue's reads do not wait on HBM.  The prefetch goes out after the next stage's DMA,
   // and the next k-tile's wait leaves exactly those xpf loads in flight.
-  const int xpf = (EPI == SR_EPI_BIAS_RESID && !PERSIST && m0 + BIG <= g.M && !g.lds_epi) ? g.xpf : 0;
+  const int xpf = (EPI == SR_EPI_BIAS_RESID && !PERSIST && !PP && m0 + BIG <= g.M && !g.lds_epi) ? g.xpf : 0;
   const char* xrow = (const char*)g.out + ((int64_t)(m0 + wave_u * 32) * g.ldo + n0) * 4;
   const uint32_t xsink = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + 2 * STAGE_BIG + wave_u * 1024);
   auto x_prefetch = [&](int kt) {
     for (int j = 0; j < xpf; ++j)
       sr::dma16_s(xrow + (int64_t)((((kt - kb) * xpf + j) & 31) * g.ldo) * 4, (uint32_t)lane * 16, xsink);
   };
-  {
+  if constexpr (PP) {
+    // Ping-pong k-loop (SR_TUNE_GEMM_PP): the two waves of each SIMD (wave s of group 0 = rows 0-127,
+    // wave s + 4 of group 1 = rows 128-255) alternate, so that one issues its k-step's 64 MFMAs
+    // back to back while the other reads its whole k-step of fragments from LDS (24 ds_read_b128)
+    // and, in group 0's load phase, issues the LDS-DMA of the stage two phases ahead (16 pieces per
+    // wave: its 64 A rows and 64 W rows).  Per k-step kt:
+    //   phase 1: group 0 MFMA(kt) | group 1 reads fragments of stage kt
+    //   phase 2: group 1 MFMA(kt) | group 0 waits for stage kt+1 (issued two phases ago), reads its
+    //            fragments, DMAs stage kt+2 into the buffer of stage kt (both groups are done with it)
+    // Each accumulator sees the same k order as in the loop below, so results are bit-identical.
+    const int grp = wave_u >> 2, wg = wave_u & 3;
+    const uint32_t voAa = (uint32_t)((lane >> 3) * g.lda_b + (((lane & 7) ^ (lane >> 4)) << 4));
+    const uint32_t voAb = (uint32_t)((lane >> 3) * g.lda_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
+    const uint32_t voWa = (uint32_t)((lane >> 3) * g.ldw_b + (((lane & 7) ^ (lane >> 4)) << 4));
+    const uint32_t voWb = (uint32_t)((lane >> 3) * g.ldw_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
+    const uint32_t dstA = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wg * 8 * 1024);
+    const uint32_t dstW = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + (wg + 4) * 8 * 1024);
+    const bool ragged = m0 + BIG > g.M;
+    auto dma_pp = [&](int kt) {  // group 0 only: stage rows of A waves wg and W waves wg + 4
+      const int arow0 = min(m0 + wg * 64, g.M - 1);
+      const char* spa = g.A + (int64_t)arow0 * g.lda_b + (int64_t)kt * ROWB;
+      const char* spw = g.W + (int64_t)(n0 + wg * 64) * g.ldw_b + (int64_t)kt * ROWB;
+      const uint32_t off = (kt & 1) * STAGE_BIG;
+      if (!ragged) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sr::dma16_s(spa + (int64_t)i * 8 * g.lda_b, (i & 1) ? voAb : voAa, dstA + off + i * 1024);
+      } else {
+        const int rlim = g.M - 1 - arow0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = min(i * 8 + (lane >> 3), rlim);
+          const int chunk = (lane & 7) ^ (4 * (i & 1) + (lane >> 4));
+          sr::dma16_s(spa, (uint32_t)(r * g.lda_b + chunk * 16), dstA + off + i * 1024);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sr::dma16_s(spw + (int64_t)i * 8 * g.ldw_b, (i & 1) ? voWb : voWa, dstW + off + i * 1024);
+    };
+    uint4 fa[8][2], fb[4][2];
+    auto read_frags = [&](int kt) {
+      const char* sb = smem + (kt & 1) * STAGE_BIG;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const char* p = sb + arow + mi * 16 * ROWB;
+        fa[mi][0] = *(const uint4*)(p + coff0);
+        fa[mi][1] = *(const uint4*)(p + coff1);
+      }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const char* p = sb + brow + ni * 16 * ROWB;
+        fb[ni][0] = *(const uint4*)(p + coff0);
+        fb[ni][1] = *(const uint4*)(p + coff1);
+      }
+    };
+    auto mma_all = [&]() {
+      sr::wait_lgkm0();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) Mma<bf16>::run(fb[ni][ks], fa[mi][ks], acc[mi][ni]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // one straight loop per group (the same barrier sequence in both)
+    if (grp == 0) {
+      dma_pp(kb);
+      if (kb + 1 < ke) {
+        dma_pp(kb + 1);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // stage kb landed; kb+1 in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      sr::barrier_raw();
+      read_frags(kb);
+      for (int kt = kb; kt < ke; ++kt) {
+        mma_all();                 // phase 1
+        sr::barrier_raw();
+        if (kt + 1 < ke) {         // phase 2
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 (issued two phases ago) landed
+          read_frags(kt + 1);
+          if (kt + 2 < ke) dma_pp(kt + 2);
+          sr::wait_lgkm0();
+        }
+        sr::barrier_raw();
+      }
+    } else {
+      sr::barrier_raw();
+      for (int kt = kb; kt < ke; ++kt) {
+        read_frags(kt);            // phase 1
+        sr::wait_lgkm0();
+        sr::barrier_raw();
+        mma_all();                 // phase 2
+        sr::barrier_raw();
+      }
+    }
+  } else {
     if (!staged) stage(kb);
     for (int kt = kb; kt < ke; ++kt) {
       // this wave's part of stage kt landed (with the x prefetch: all but the xpf loads issued after it)
@@ -889,6 +986,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, false, -1, rope);
 }
 
+// The same tile with the ping-pong k-loop (SR_TUNE_GEMM_PP, gemm256_tile<EPI, false, true>).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256pp_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
+  const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
+  const char* rope = stage_rope<EPI>(g, smem);
+  gemm256_tile<EPI, false, true>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, false, -1, rope);
+}
+
 // Persistent form (SR_TUNE_GEMM_PERSIST): one workgroup per CU walks tiles t = blockIdx.x + i *
 // gridDim.x (gridDim.x a multiple of 8, so every tile of a workgroup sits on its XCD's contiguous
 // xcd_remap range, as in the one-tile-per-workgroup launch); each tile's epilogue overlaps the
@@ -957,6 +1063,11 @@ int launch256(GemmArgs a, hipStream_t s) {
     sr::note_kernel("gemm256_persist_kernel<%d>", EPI);
     return sr::check_launch("sr_gemm(256, persistent)");
   }
+  if (sr::tune(SR_TUNE_GEMM_PP)) {
+    hipLaunchKernelGGL((gemm256pp_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
+    sr::note_kernel("gemm256pp_kernel<%d>", EPI);
+    return sr::check_launch("sr_gemm(256, ping-pong)");
+  }
   hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
   sr::note_kernel("gemm256_kernel<%d>", EPI);
   return sr::check_launch("sr_gemm(256)");
@@ -1024,7 +1135,10 @@ int launch256_tail(GemmArgs a, hipStream_t s) {
       if (rc != SR_OK) return rc;
       rc = launch<bf16, EPI>(row_slice<EPI>(a, main_rows, rest), s);
       // the launch the time goes to
-      sr::note_kernel(use_persist(EPI, whole) ? "gemm256_persist_kernel<%d>" : "gemm256_kernel<%d>", EPI);
+      sr::note_kernel(use_persist(EPI, whole)         ? "gemm256_persist_kernel<%d>"
+                      : sr::tune(SR_TUNE_GEMM_PP) ? "gemm256pp_kernel<%d>"
+                                                  : "gemm256_kernel<%d>",
+                      EPI);
       return rc;
     }
   }

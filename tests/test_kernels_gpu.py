@@ -103,6 +103,46 @@ def test_gemm_splitk(ops, dtype, tol, M, N, K, splits):
     assert rel(o32, ref) < max(tol, 1e-5)
 
 
+@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32"])
+@pytest.mark.parametrize("M,N,K", [(33000, 1024, 1024), (12000, 3072, 256), (20000, 4096, 1024), (33000, 1024, 4096)])
+def test_gemm_ping_pong(ops, epi_name, M, N, K):
+    """SR_GEMM_PP: the 256x256 GEMM's ping-pong k-loop (each SIMD's two waves alternate a k-step of
+    MFMAs with the other's LDS reads / DMA) gives bit-identical outputs to the default loop, ragged
+    last row tile and tail split included."""
+    L = _lib()
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV, torch.bfloat16)
+    b, gam = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+    epi = getattr(L, "SR_EPI_" + epi_name)
+    kw = dict(bias=b)
+    if epi_name == "BIAS_RESID":
+        kw["gamma"] = gam
+    if epi_name == "QKV":
+        C = N // 3 if N % 3 == 0 else None
+        if C is None or C % 64:
+            pytest.skip("QKV needs whole q|k|v blocks")
+        rope = RotaryPositionEmbedding2D(100).tables(64, 40, DEV)
+        qn = [torch.randn(64, device=DEV, generator=torch.Generator(DEV).manual_seed(i)) for i in range(4)]
+        kw["qkv"] = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
+                         rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37,
+                         pos_row_base=3, q_scale=0.18)
+    outs = []
+    for pp in (0, 1):
+        if epi_name in ("BIAS_RESID", "F32"):
+            out = torch.randn(M, N, generator=torch.Generator().manual_seed(5)).to(DEV)
+        else:
+            out = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        with ops.tuning(SR_GEMM_PP=pp):
+            ops.gemm(a, w, out, epi, splits=1, **kw)
+            if pp:
+                assert ops.last_kernel() == f"gemm256pp_kernel<{epi}>"
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("M,K", [(33000, 1024), (43968, 4096), (8300, 256)])
 def test_gemm_resid_x_prefetch(ops, M, K):
     """SR_GEMM_XPF: the 256x256 residual GEMM fetching its x tile into L2 / MALL under the k-loop

@@ -426,6 +426,26 @@ def gemm_qkv(M=2 * 32 * 1374):
         print(f"gemm_qkv group (layer) lds={lds} {ms:8.3f} ms  {flg / ms / 1e9:8.1f} TF/s  {flg / ms / 1e9 / PEAK:6.1%}")
 
 
+def gemm_pp():
+    """SR_GEMM_PP A/B, interleaved: the aggregator GEMMs at C3 frame rows (qkv / proj / fc1 / fc2 with
+    their epilogues) with the default k-loop (0) and the ping-pong k-loop (1), plus 8192^3 BIAS."""
+    M = 2 * 32 * 1374
+    x = torch.randn(M, 1024, device=DEV)
+    for name, (m, N, K, epi) in {"qkv ": (M, 3072, 1024, _lib.SR_EPI_BIAS), "proj": (M, 1024, 1024, _lib.SR_EPI_BIAS_RESID),
+                                 "fc1 ": (M, 4096, 1024, _lib.SR_EPI_BIAS_GELU),
+                                 "fc2 ": (M, 1024, 4096, _lib.SR_EPI_BIAS_RESID),
+                                 "8k^3": (8192, 8192, 8192, _lib.SR_EPI_BIAS)}.items():
+        a = torch.rand(m, K, device=DEV).sub_(0.5).to(torch.bfloat16)
+        w = (torch.rand(N, K, device=DEV).sub_(0.5) / K ** 0.5).to(torch.bfloat16)
+        b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV) * 1e-3
+        out = x[:m, :N] if epi == _lib.SR_EPI_BIAS_RESID else torch.empty(m, N, device=DEV, dtype=torch.bfloat16)
+        fl = 2.0 * m * N * K
+        for pp in (0, 1, 0, 1):
+            with ops.tuning(SR_GEMM_PP=pp):
+                ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam), reps=10)
+            print(f"gemm_pp {name} pp={pp} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
+
+
 def gemm_xpf():
     """SR_GEMM_XPF A/B, interleaved: the residual GEMMs (proj K=1024, fc2 K=4096) over the C3 frame
     rows with the x tile prefetched into L2 / MALL under the k-loop (1 or 2 rows per k-tile and wave)
