@@ -794,8 +794,10 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
     // and, in group 0's load phase, issues the LDS-DMA of the stage two phases ahead (16 pieces per
     // wave: its 64 A rows and 64 W rows).  Per k-step kt:
     //   phase 1: group 0 MFMA(kt) | group 1 reads fragments of stage kt
-    //   phase 2: group 1 MFMA(kt) | group 0 waits for stage kt+1 (issued two phases ago), reads its
-    //            fragments, DMAs stage kt+2 into the buffer of stage kt (both groups are done with it)
+    //   phase 2: group 1 MFMA(kt) | group 0 DMAs stage kt+2 into the buffer of stage kt (both groups
+    //            are done with it) and reads its fragments of stage kt+1
+    // Each group-0 wave waits for its own DMA pieces of stage kt+1 at the end of phase 1, before the
+    // barrier: the other waves' pieces are only known landed after it.
     // Each accumulator sees the same k order as in the loop below, so results are bit-identical.
     const int grp = wave_u >> 2, wg = wave_u & 3;
     const uint32_t voAa = (uint32_t)((lane >> 3) * g.lda_b + (((lane & 7) ^ (lane >> 4)) << 4));
@@ -865,11 +867,13 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
       read_frags(kb);
       for (int kt = kb; kt < ke; ++kt) {
         mma_all();                 // phase 1
+        // this wave's pieces of stage kt+1 (issued a phase ago) landed; after the barrier every
+        // group-0 wave's have, so group 0 reads it in phase 2 and group 1 in the next phase 1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         sr::barrier_raw();
         if (kt + 1 < ke) {         // phase 2
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 (issued two phases ago) landed
+          if (kt + 2 < ke) dma_pp(kt + 2);  // into stage kt's buffer: both groups are done with it
           read_frags(kt + 1);
-          if (kt + 2 < ke) dma_pp(kt + 2);
           sr::wait_lgkm0();
         }
         sr::barrier_raw();
