@@ -1027,7 +1027,7 @@ struct GemmGroup {
   int n;
 };
 
-template <int EPI>
+template <int EPI, bool PP = false>
 __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
   int p = 0;
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   const int lin = blockIdx.x - gg.start[p];
   if (lin >= nt) return;  // padding
   const char* rope = stage_rope<EPI>(g, smem);
-  gemm256_tile<EPI>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, false, -1, rope);
+  gemm256_tile<EPI, false, PP>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, false, -1, rope);
 }
 
 
@@ -1395,16 +1395,21 @@ extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, cons
   }
   for (int i = n + 1; i <= GROUP_MAX; ++i) gg.start[i] = gg.start[n];
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(gg.start[n]);
+  const bool pp = sr::tune(SR_TUNE_GEMM_PP) != 0;
+#define SR_GROUP_LAUNCH(E)                                                                              \
+  do {                                                                                                  \
+    if (pp) hipLaunchKernelGGL((gemm256_group_kernel<E, true>), grid, dim3(512), 0, s, gg);            \
+    else hipLaunchKernelGGL((gemm256_group_kernel<E, false>), grid, dim3(512), 0, s, gg);              \
+  } while (0)
   switch (epi) {
-    case SR_EPI_BIAS: hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS>), dim3(gg.start[n]), dim3(512), 0, s, gg); break;
-    case SR_EPI_QKV: hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_QKV>), dim3(gg.start[n]), dim3(512), 0, s, gg); break;
-    case SR_EPI_BIAS_GELU:
-      hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS_GELU>), dim3(gg.start[n]), dim3(512), 0, s, gg);
-      break;
-    default:
-      hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS_RESID>), dim3(gg.start[n]), dim3(512), 0, s, gg);
+    case SR_EPI_BIAS: SR_GROUP_LAUNCH(SR_EPI_BIAS); break;
+    case SR_EPI_QKV: SR_GROUP_LAUNCH(SR_EPI_QKV); break;
+    case SR_EPI_BIAS_GELU: SR_GROUP_LAUNCH(SR_EPI_BIAS_GELU); break;
+    default: SR_GROUP_LAUNCH(SR_EPI_BIAS_RESID);
   }
-  sr::note_kernel("gemm256_group_kernel<%d>", epi);
+#undef SR_GROUP_LAUNCH
+  sr::note_kernel("gemm256_group_kernel<%d, %s>", epi, pp ? "true" : "false");  // as rocprofv3 names it
   return sr::check_launch("sr_gemm_group");
 }
 
