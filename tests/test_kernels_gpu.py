@@ -650,7 +650,7 @@ def test_gemm_tail_split(ops, epi_name, M, N):
         ops.gemm(a, w, out0, epi, splits=1, **kw0)
         k0 = ops.last_kernel()
     torch.cuda.synchronize()
-    assert k1 == k0 and k0.startswith("gemm256_kernel"), (k1, k0)
+    assert k1 == k0 and k0.startswith(("gemm256_kernel", "gemm256pp_kernel")), (k1, k0)
     same = torch.equal(out1, out0)
     print(f"{epi_name} M={M} N={N}: bit-identical={same} rel={rel(out1.float(), out0.float()):.2e}")
     assert rel(out1.float(), out0.float()) < 1e-6
