@@ -295,26 +295,12 @@ def proj_residual_ln2(pb: PackedBlock, xs: Tensor, o: Tensor, qkv: Tensor, xn: T
         ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, xn)
 
 
-# SR_MLP_CHUNK=R (A/B switch, 0 = off): fc1 -> fc2 in row chunks of R rows, so that a chunk's hidden
-# activations (R x 4C bf16; 134 MB at R = 16,384, C = 1024) can stay in the 256 MB MALL between the
-# two GEMMs instead of a round trip through HBM.  R = 16,384 is whole workgroup rounds of both
-# GEMMs at C = 1024 (fc1 4 rounds, fc2 1).
-_MLP_CHUNK = int(os.environ.get("SR_MLP_CHUNK", "0"))
-
-
 def mlp_residual(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratch, defer: bool) -> Optional[Pending]:
     """fc1 (+GELU) and fc2 with the LayerScale residual: x[r0:r1] += g2 * fc2(gelu(fc1(xn))).
     ``defer``: fc2 ends in the bias epilogue into the block's dead attention-output rows sc.o and
     the update is returned as a Pending for the next LayerNorm over these rows."""
     xs, xn, h, o = x[r0:r1], sc.xn[r0:r1], sc.h[r0:r1], sc.o[r0:r1]
     hid = pb.w_fc1.shape[0]
-    if _MLP_CHUNK > 0 and not defer and r1 - r0 > _MLP_CHUNK:
-        for c0 in range(r0, r1, _MLP_CHUNK):
-            c1 = min(c0 + _MLP_CHUNK, r1)
-            hc = sc.h[r0:r0 + (c1 - c0), :hid]  # one chunk buffer, reused
-            ops.gemm(sc.xn[c0:c1], pb.w_fc1, hc, _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
-            ops.gemm(hc, pb.w_fc2, x[c0:c1], _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2, tag="gemm")
-        return None
     ops.gemm(xn, pb.w_fc1, h[:, :hid], _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, tag="gemm")
     if defer and defer_enabled(pb) and o.shape[1] >= pb.w_fc2.shape[0]:
         y = o[:, :pb.w_fc2.shape[0]]

@@ -157,21 +157,3 @@ def test_save_checkpoint_writes_flat_trained_weights(tmp_path):
     for n, p in m.named_parameters():
         assert torch.equal(sd[n], flat.view(flat.data, n)), n
 
-
-def test_mlp_row_chunks_equal_one_pass(monkeypatch):
-    """SR_MLP_CHUNK: fc1 -> fc2 over row chunks (the hidden activations of a chunk stay cache-sized)
-    computes every row exactly as the one-pass MLP (row-wise GEMMs): the host bookkeeping of the
-    chunk rows and the shared chunk buffer."""
-    from sailrecon_amd import runtime
-    g = load_npz("g1_small_56.npz")
-    images = torch.from_numpy(g["images"])
-    outs = []
-    m = small_model()
-    for chunk in (0, 7):
-        monkeypatch.setattr(runtime, "_MLP_CHUNK", chunk)
-        m.aggregator.generator.manual_seed(0)
-        with cpu_ops.installed(), torch.no_grad():
-            feats, _, cam_last = m.aggregator(images, [0, 1], [2, 3], fix_rank=int(g["fix_rank"]))
-        outs.append((feats[1].clone(), cam_last.clone()))
-    for a, b in zip(*outs):  # the CPU matmul's blocking depends on the row count: fp32 rounding only
-        assert rel_l2(b.numpy(), a.numpy()) < 1e-6
