@@ -620,6 +620,9 @@ class Aggregator(nn.Module):
         # frame-sharded: the reloc block's tail waits for the global attention and runs grouped with
         # the global block's (runtime.run_block_tails: one launch per GEMM stage over both row ranges)
         group_tails = G > 1 and Nq_l > 0 and runtime.group_tails_wanted(max(q1 - q0, q0 - a0))
+        # ... and with SR_SHARD_CONCURRENT=1 its attention runs on a second stream beside the global
+        # attention's key-split passes: at G = 8 both under-fill the chip on their own
+        shard_side = self._stream2(dev) if (group_tails and _SHARD_CONCURRENT) else None
         if Nq_l > 0:
             def attend_reloc(qkv, o):
                 _wait(work_sub)
@@ -655,7 +658,12 @@ class Aggregator(nn.Module):
                 runtime.run_block_head(pr, x, q0, q1, sc,
                                        runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
                                        runtime.q_prescale(pr))
-                attend_reloc(sc.qkv[q0:q1], sc.o[q0:q1])
+                if shard_side is not None:
+                    shard_side.wait_stream(torch.cuda.current_stream(dev))  # the reloc QKV is done
+                    with torch.cuda.stream(shard_side):  # (its wait on the subsample gather too)
+                        attend_reloc(sc.qkv[q0:q1], sc.o[q0:q1])
+                else:
+                    attend_reloc(sc.qkv[q0:q1], sc.o[q0:q1])
             else:
                 keep(runtime.run_block(pr, x, q0, q1, sc, attend_reloc,
                                        runtime.qkv_params(pr, rope, prescale=True, pos_row_base=q0, **posctx),
@@ -669,6 +677,8 @@ class Aggregator(nn.Module):
             else:
                 _wait(work_kv)
                 self._global_attention(q, kv_all[:, 0:C], kv_all[:, C:2 * C], o, pg, La_l, La)
+            if shard_side is not None:
+                torch.cuda.current_stream(dev).wait_stream(shard_side)  # join before the grouped tails
             if group_tails:
                 out.extend(runtime.run_block_tails([(pr, q0, q1), (pg, a0, q0)], x, sc, defer=defer))
             else:
@@ -785,6 +795,14 @@ class Aggregator(nn.Module):
         return (os.environ.get("SR_RELOC_SPLIT", "1") == "1" and dtype == torch.bfloat16 and
                 (rows + 255) // 256 * 16 >= _RELOC_SPLIT_MIN_WG and n_sub >= 64)
 
+    def _stream2(self, dev):
+        """Second HIP stream of the frame-sharded reloc attention (SR_SHARD_CONCURRENT=1)."""
+        s = getattr(self, "_shard_side", None)
+        if s is None or s.device != torch.device(dev):
+            s = torch.cuda.Stream(device=dev)
+            self._shard_side = s
+        return s
+
     def _side_stream(self, dev):
         """Second HIP stream for the concurrent reloc block (opt-in: SR_CONCURRENT_STACKS=1)."""
         if os.environ.get("SR_CONCURRENT_STACKS", "0") != "1":
@@ -811,6 +829,9 @@ class Aggregator(nn.Module):
 # hand-scheduled sweep's ragged variant (round 3 measured it level with the compiled sweep per rank:
 # DESIGN.md section 5)
 _SHARD_TAIL = os.environ.get("SR_SHARD_TAIL", "0") == "1"
+# SR_SHARD_CONCURRENT=1 (A/B): under frame sharding with grouped tails, the reloc attention on a
+# second stream beside the global attention
+_SHARD_CONCURRENT = os.environ.get("SR_SHARD_CONCURRENT", "0") == "1"
 # smallest query set (in 256-row x head workgroups) whose reloc attention runs split (A/B switch)
 _RELOC_SPLIT_MIN_WG = int(os.environ.get("SR_RELOC_SPLIT_MIN_WG", "2048"))
 
