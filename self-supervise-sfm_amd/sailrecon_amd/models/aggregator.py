@@ -622,7 +622,8 @@ class Aggregator(nn.Module):
         group_tails = G > 1 and Nq_l > 0 and runtime.group_tails_wanted(max(q1 - q0, q0 - a0))
         # ... and with SR_SHARD_CONCURRENT=1 its attention runs on a second stream beside the global
         # attention's key-split passes: at G = 8 both under-fill the chip on their own
-        shard_side = self._stream2(dev) if (group_tails and _SHARD_CONCURRENT) else None
+        shard_side = (self._stream2(dev) if group_tails and _SHARD_CONCURRENT and torch.device(dev).type == "cuda"
+                      else None)
         if Nq_l > 0:
             def attend_reloc(qkv, o):
                 _wait(work_sub)
@@ -829,9 +830,11 @@ class Aggregator(nn.Module):
 # hand-scheduled sweep's ragged variant (round 3 measured it level with the compiled sweep per rank:
 # DESIGN.md section 5)
 _SHARD_TAIL = os.environ.get("SR_SHARD_TAIL", "0") == "1"
-# SR_SHARD_CONCURRENT=1 (A/B): under frame sharding with grouped tails, the reloc attention on a
-# second stream beside the global attention
-_SHARD_CONCURRENT = os.environ.get("SR_SHARD_CONCURRENT", "0") == "1"
+# SR_SHARD_CONCURRENT (default 1; 0 for the A/B): under frame sharding with grouped tails, the reloc
+# attention on a second stream beside the global attention.  Rank-0 rehearsal, one box, 2 runs each
+# (profiles/r05_j10_rs_*.log): G = 8 69.03 / 69.15 -> 66.87 / 66.98 ms, G = 4 121.8 / 121.0 -> 120.9 /
+# 120.7 ms; the sharded GPU tests pass with it
+_SHARD_CONCURRENT = os.environ.get("SR_SHARD_CONCURRENT", "1") != "0"
 # smallest query set (in 256-row x head workgroups) whose reloc attention runs split (A/B switch)
 _RELOC_SPLIT_MIN_WG = int(os.environ.get("SR_RELOC_SPLIT_MIN_WG", "2048"))
 
