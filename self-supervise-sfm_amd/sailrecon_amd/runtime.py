@@ -348,8 +348,10 @@ def run_block_tail(pb: PackedBlock, x: Tensor, r0: int, r1: int, sc: BlockScratc
 
 
 # SR_GROUP_TAILS: 0 = never group, 1 = only blocks under GROUP_TAILS_MAX_ROWS rows (a frame-sharded
-# rank's 5,496-row global / reloc blocks), 2 = always
-_GROUP_TAILS = int(os.environ.get("SR_GROUP_TAILS", "1"))
+# rank's 5,496-row global / reloc blocks), 2 = always (default).  Measured, one box each, interleaved:
+# G = 2 rank step 213.98 / 213.02 -> 210.87 / 209.69 ms with 2 against 1 (profiles/r05_j12_rs_*.log);
+# one GPU level, 79.16 / 79.24 / 79.04 vs 79.20 / 79.09 / 79.20 views/s (r05_j13_bench_g*.log)
+_GROUP_TAILS = int(os.environ.get("SR_GROUP_TAILS", "2"))
 GROUP_TAILS_MAX_ROWS = 16384
 
 
