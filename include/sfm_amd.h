@@ -89,7 +89,9 @@ enum sr_tuning_key {
                                under the first k-tile; 0: from global memory)           default 1 */
   SR_TUNE_GEMM_PP = 18,     /* 1: the 256x256 GEMM's ping-pong k-loop (each SIMD's two waves alternate
                                MFMA and LDS phases; bit-identical)                     default 0 */
-  SR_TUNE_COUNT = 19
+  SR_TUNE_ATTN_BWD_KB = 19, /* 1 | 2: key blocks of 32 per wave in the attention backward's dK/dV sweep
+                               (2: one wave per SIMD, 64 keys; bit-identical)           default 1 */
+  SR_TUNE_COUNT = 20
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -127,8 +127,11 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 // -(c q.k - lse) and P = exp2(-S') (the sign is a source modifier of v_exp); the dP chain is seeded
 // with the stored -delta (attn_bwd_delta_kernel) and returns dO.v - delta, so dS = P dP' with no
 // sign flips (a negated V turned into 24 v_xor per tile before the packed multiplies).
-template <int SEG>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
+// KB key blocks of 32 per wave (SR_TUNE_ATTN_BWD_KB): KB = 2 runs one wave per SIMD with 64 keys,
+// so every Q / dO fragment read from LDS (row reads for S / dP, transposed reads for dV / dK) feeds
+// two key blocks' MFMAs, and the wave has two independent chain sets to interleave.
+template <int SEG, int KB = 1>
+__global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
   const sr_attn_desc& f = b.f;
@@ -142,8 +145,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
   const bf16* kp = (const bf16*)(SEG == 0 ? f.k0 : f.k1);
   const bf16* vp = (const bf16*)(SEG == 0 ? f.v0 : f.v1);
   const int64_t ldk = SEG == 0 ? f.ldk0 : f.ldk1, ldv = SEG == 0 ? f.ldv0 : f.ldv1;
-  const int key = blockIdx.x * 128 + wave * 32 + l32;
-  const int keyc = min(key, len - 1);
+  const int key_base = blockIdx.x * (128 * KB) + wave * (32 * KB) + l32;  // key of block kb: + 32 kb
   const float c = f.scale * 1.4426950408889634f;
 
   // staging: wave w issues row groups g = 4 (w & 1) .. + 3 of the Q (waves 0, 1) or dO (2, 3)
@@ -180,29 +182,37 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
     if (++s_q == ntq) s_q = 0, ++s_item;
   }
 
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[KB][4], vf[KB][4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = *(const bf16x8*)(kp + (kb0 + keyc) * ldk + hcol + 16 * s + 8 * hi);
-    vf[s] = *(const bf16x8*)(vp + (kb0 + keyc) * ldv + hcol + 16 * s + 8 * hi);
+  for (int kb = 0; kb < KB; ++kb) {
+    const int keyc = min(key_base + 32 * kb, len - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[kb][s] = *(const bf16x8*)(kp + (kb0 + keyc) * ldk + hcol + 16 * s + 8 * hi);
+      vf[kb][s] = *(const bf16x8*)(vp + (kb0 + keyc) * ldv + hcol + 16 * s + 8 * hi);
+    }
   }
   // retire these loads (and the prologue stages) with a wait the compiler sees: its scoreboard
   // would otherwise carry them into the loop, and a vmcnt wait there drains the ring
   __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      kf[s][j] = (bf16)(-(float)kf[s][j] * c);
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        kf[kb][s][j] = (bf16)(-(float)kf[kb][s][j] * c);
+      }
+      // keep the negated fragment in registers: otherwise the compiler re-derives it inside the
+      // tile loop (16 v_xor + 8 v_perm per tile and fragment set)
+      asm volatile("" : "+v"(kf[kb][s]));
     }
-    // keep the negated fragment in registers: otherwise the compiler re-derives it inside the
-    // tile loop (16 v_xor + 8 v_perm per tile and fragment set)
-    asm volatile("" : "+v"(kf[s]));
-  }
   const TrOff tro = tr_offsets(lane);
-  f32x16 dk[2], dv[2];
+  f32x16 dk[KB][2], dv[KB][2];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f;
+  for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[kb][0][i] = dk[kb][1][i] = dv[kb][0][i] = dv[kb][1][i] = 0.f;
 
   // One tile of the sweep.  MASKED (the last, ragged query tile of an item) is a separate
   // instantiation, so the full-tile body is one basic block: the compiler interleaves one q-block's
@@ -230,23 +240,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
     const float* lse_s = (const float*)(qt + 2 * TB);
     const float* dl_s = lse_s + 64;
     // seeds in accumulator order: rows qb2*32 + acc_row(r), four consecutive per float4
-    f32x16 sc[2], dp[2];
+    f32x16 sc[KB][2], dp[KB][2];
 #pragma unroll
     for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 l4 = *(const float4*)(lse_s + qb2 * 32 + 8 * g + 4 * hi);
         const float4 d4 = *(const float4*)(dl_s + qb2 * 32 + 8 * g + 4 * hi);
-        sc[qb2][4 * g] = l4.x; sc[qb2][4 * g + 1] = l4.y; sc[qb2][4 * g + 2] = l4.z; sc[qb2][4 * g + 3] = l4.w;
-        dp[qb2][4 * g] = d4.x; dp[qb2][4 * g + 1] = d4.y; dp[qb2][4 * g + 2] = d4.z; dp[qb2][4 * g + 3] = d4.w;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          sc[kb][qb2][4 * g] = l4.x; sc[kb][qb2][4 * g + 1] = l4.y;
+          sc[kb][qb2][4 * g + 2] = l4.z; sc[kb][qb2][4 * g + 3] = l4.w;
+          dp[kb][qb2][4 * g] = d4.x; dp[kb][qb2][4 * g + 1] = d4.y;
+          dp[kb][qb2][4 * g + 2] = d4.z; dp[kb][qb2][4 * g + 3] = d4.w;
+        }
       }
     // clamped duplicate rows of the ragged tile get P = 0
-    auto mask_rows = [&](int qb2) __attribute__((always_inline)) {
+    auto mask_rows = [&](int kb, int qb2) __attribute__((always_inline)) {
       if constexpr (decltype(masked)::value) {
         const int qv = f.lq - cq * 64;  // valid query rows of this tile
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (qb2 * 32 + acc_row(r, hi) >= qv) sc[qb2][r] = INFINITY;
+          if (qb2 * 32 + acc_row(r, hi) >= qv) sc[kb][qb2][r] = INFINITY;
       }
     };
     bf16x8 fq[4][2], fo[4][2];
@@ -258,32 +273,47 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
         fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
       }
 #pragma unroll
-    for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
+    for (int s = 0; s < 4; ++s)  // 4 KB independent accumulation chains in flight
 #pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2) {
-        sc[qb2] = mfma32(fq[s][qb2], kf[s], sc[qb2]);
-        dp[qb2] = mfma32(fo[s][qb2], vf[s], dp[qb2]);
-      }
-    mask_rows(0);
-    mask_rows(1);
-    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int qb2 = 0; qb2 < 2; ++qb2) {
+          sc[kb][qb2] = mfma32(fq[s][qb2], kf[kb][s], sc[kb][qb2]);
+          dp[kb][qb2] = mfma32(fo[s][qb2], vf[kb][s], dp[kb][qb2]);
+        }
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      mask_rows(kb, 0);
+      mask_rows(kb, 1);
+    }
+    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS;
+    // each transposed dO / Q fragment feeds every key block
 #pragma unroll
     for (int qb2 = 0; qb2 < 2; ++qb2)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        f32x8 pv, dv8;
+        bf16x8 pf[KB], df[KB];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = 8 * s2 + j;
-          pv[j] = __builtin_amdgcn_exp2f(-sc[qb2][r]);
-          dv8[j] = pv[j] * dp[qb2][r];
+        for (int kb = 0; kb < KB; ++kb) {
+          f32x8 pv, dv8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int r = 8 * s2 + j;
+            pv[j] = __builtin_amdgcn_exp2f(-sc[kb][qb2][r]);
+            dv8[j] = pv[j] * dp[kb][qb2][r];
+          }
+          pf[kb] = __builtin_convertvector(pv, bf16x8);
+          df[kb] = __builtin_convertvector(dv8, bf16x8);
         }
-        const bf16x8 pf = __builtin_convertvector(pv, bf16x8), df = __builtin_convertvector(dv8, bf16x8);
         const int row0 = qb2 * 32 + 16 * s2;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
-          dv[db] = mfma32(tr_frag(ot, row0, tro.off[db]), pf, dv[db]);
-          dk[db] = mfma32(tr_frag(qt, row0, tro.off[db]), df, dk[db]);
+          const bf16x8 to = tr_frag(ot, row0, tro.off[db]), tq = tr_frag(qt, row0, tro.off[db]);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            dv[kb][db] = mfma32(to, pf[kb], dv[kb][db]);
+            dk[kb][db] = mfma32(tq, df[kb], dk[kb][db]);
+          }
         }
       }
   };
@@ -298,18 +328,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc 
     }
   }
   // dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key l32, d = 32 db + acc_row(r))
-  if (key < len) {
-    float* dkp = (SEG == 0 ? b.dk0 : b.dk1) + (kb0 + key) * (SEG == 0 ? b.lddk0 : b.lddk1) + hcol;
-    float* dvp = (SEG == 0 ? b.dv0 : b.dv1) + (kb0 + key) * (SEG == 0 ? b.lddv0 : b.lddv1) + hcol;
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+  for (int kb = 0; kb < KB; ++kb) {
+    const int key = key_base + 32 * kb;
+    if (key < len) {
+      float* dkp = (SEG == 0 ? b.dk0 : b.dk1) + (kb0 + key) * (SEG == 0 ? b.lddk0 : b.lddk1) + hcol;
+      float* dvp = (SEG == 0 ? b.dv0 : b.dv1) + (kb0 + key) * (SEG == 0 ? b.lddv0 : b.lddv1) + hcol;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d0 = db * 32 + 8 * g + 4 * hi;
-        *(float4*)(dkp + d0) = make_float4(dk[db][4 * g] * f.scale, dk[db][4 * g + 1] * f.scale,
-                                           dk[db][4 * g + 2] * f.scale, dk[db][4 * g + 3] * f.scale);
-        *(float4*)(dvp + d0) = make_float4(dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]);
-      }
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = db * 32 + 8 * g + 4 * hi;
+          *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * f.scale, dk[kb][db][4 * g + 1] * f.scale,
+                                             dk[kb][db][4 * g + 2] * f.scale, dk[kb][db][4 * g + 3] * f.scale);
+          *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
+                                             dv[kb][db][4 * g + 3]);
+        }
+    }
   }
 }
 
@@ -475,11 +510,16 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<0>, dim3((f.l0 + 127) / 128, f.heads, f.k0_bstride == 0 ? 1 : f.batch),
-                     dim3(256), 0, s, b);
-  if (f.l1 > 0)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, dim3((f.l1 + 127) / 128, f.heads, f.k1_bstride == 0 ? 1 : f.batch),
-                       dim3(256), 0, s, b);
-  sr::note_kernel("attn_bwd_dkdv_kernel<0>");
+  const bool kb2 = sr::tune(SR_TUNE_ATTN_BWD_KB) == 2;
+  const int kr = kb2 ? 256 : 128;  // keys per workgroup
+  const dim3 g0((f.l0 + kr - 1) / kr, f.heads, f.k0_bstride == 0 ? 1 : f.batch);
+  if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g0, dim3(256), 0, s, b);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g0, dim3(256), 0, s, b);
+  if (f.l1 > 0) {
+    const dim3 g1((f.l1 + kr - 1) / kr, f.heads, f.k1_bstride == 0 ? 1 : f.batch);
+    if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 2>), g1, dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1>), g1, dim3(256), 0, s, b);
+  }
+  sr::note_kernel("attn_bwd_dkdv_kernel<0, %d>", kb2 ? 2 : 1);
   return sr::check_launch("sr_attention_bwd");
 }

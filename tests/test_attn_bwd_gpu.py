@@ -102,3 +102,49 @@ def test_attention_bwd_matches_autograd(case):
     assert _rel(dk0, dk0_r) < TOL and _rel(dv0, dv0_r) < TOL
     if case == "reloc":
         assert _rel(dk1, dk1_r) < TOL and _rel(dv1, dv1_r) < TOL
+
+
+@pytest.mark.parametrize("case", ["frame", "global", "reloc"])
+def test_attention_bwd_two_key_blocks_per_wave(case):
+    """SR_ATTN_BWD_KB=2: the dK/dV sweep with 64 keys per wave (one wave per SIMD, every Q / dO
+    fragment feeding two key blocks) gives bit-identical dK / dV (and dQ) to the 32-key form,
+    ragged key counts included."""
+    from sailrecon_amd import ops
+    torch.manual_seed(1)
+    H, D = 4, 64
+    C = H * D
+    if case == "frame":
+        B, P, A = 3, 150, 0
+        kw = dict(batch=B, lq=P, q_bstride=P, l0=P, k0_bstride=P)
+    elif case == "global":
+        B, P, A = 1, 1100, 0
+        kw = dict(batch=1, lq=P, q_bstride=P, l0=P, k0_bstride=P)
+    else:
+        B, P, A = 3, 150, 301
+        kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, l1=P, k1_bstride=P)
+    x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
+    q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+    if case == "reloc":
+        ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
+        k0, v0 = ka[:, :C], ka[:, C:]
+        kw.update(k1=k, v1=v)
+    else:
+        k0, v0 = k, v
+    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, P, device=DEV)
+    ops.attention(q, k0, v0, o, heads=H, head_dim=D, lse=lse, **kw)
+    g = torch.randn(B * P, C, device=DEV).bfloat16()
+    outs = []
+    for kbn in (1, 2):
+        dq = torch.empty(B * P, C, device=DEV)
+        dk0, dv0 = torch.empty(k0.shape[0], C, device=DEV), torch.empty(k0.shape[0], C, device=DEV)
+        dk1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
+        dv1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
+        delta = torch.empty(B, H, P, device=DEV)
+        with ops.tuning(SR_ATTN_BWD_KB=kbn):
+            ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
+            assert ops.last_kernel() == f"attn_bwd_dkdv_kernel<0, {kbn}>"
+        outs.append([t for t in (dq, dk0, dv0, dk1, dv1) if t is not None])
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
