@@ -91,7 +91,10 @@ enum sr_tuning_key {
                                MFMA and LDS phases; bit-identical)                     default 0 */
   SR_TUNE_ATTN_BWD_KB = 19, /* 1 | 2: key blocks of 32 per wave in the attention backward's dK/dV sweep
                                (2: one wave per SIMD, 64 keys; bit-identical)           default 1 */
-  SR_TUNE_COUNT = 20
+  SR_TUNE_ATTN_BWD_PIPE = 20,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
+                               64 keys; one item per workgroup, >= 4 full query tiles;
+                               bit-identical)                                           default 0 */
+  SR_TUNE_COUNT = 21
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

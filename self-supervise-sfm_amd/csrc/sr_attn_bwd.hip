@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "sr_common.h"
+#include "sr_attn_bwd_pipe.inc"
 
 namespace {
 
@@ -121,6 +122,115 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b)
 }
 
 // ---------------------------------------------------------------- dK, dV
+// One 64-query tile of the dK/dV sweep for KB key blocks of 32 per wave (lane: key l32 of block
+// kb): qt = the tile's LDS stage (Q tile | dO tile | 64 lse | 64 stored -delta), qv = its valid
+// rows (MASKED only: clamped duplicate rows get P = 0).  S'^T = lse - c q.k (K resident negated
+// and scaled), dP'^T = dO.v - delta; P = exp2(-S'), dS = P dP'; dV^T += dO^T P, dK^T += Q^T dS.
+template <int KB, bool MASKED>
+__device__ __forceinline__ void dkdv_tile(const char* qt, int qv, const bf16x8 (&kf)[KB][4], const bf16x8 (&vf)[KB][4],
+                                          f32x16 (&dk)[KB][2], f32x16 (&dv)[KB][2], const TrOff& tro, int l32, int hi) {
+  const char* ot = qt + TB;
+  const float* lse_s = (const float*)(qt + 2 * TB);
+  const float* dl_s = lse_s + 64;
+  // seeds in accumulator order: rows qb2*32 + acc_row(r), four consecutive per float4
+  f32x16 sc[KB][2], dp[KB][2];
+#pragma unroll
+  for (int qb2 = 0; qb2 < 2; ++qb2)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *(const float4*)(lse_s + qb2 * 32 + 8 * g + 4 * hi);
+      const float4 d4 = *(const float4*)(dl_s + qb2 * 32 + 8 * g + 4 * hi);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        sc[kb][qb2][4 * g] = l4.x; sc[kb][qb2][4 * g + 1] = l4.y;
+        sc[kb][qb2][4 * g + 2] = l4.z; sc[kb][qb2][4 * g + 3] = l4.w;
+        dp[kb][qb2][4 * g] = d4.x; dp[kb][qb2][4 * g + 1] = d4.y;
+        dp[kb][qb2][4 * g + 2] = d4.z; dp[kb][qb2][4 * g + 3] = d4.w;
+      }
+    }
+  bf16x8 fq[4][2], fo[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int qb2 = 0; qb2 < 2; ++qb2) {
+      fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
+      fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
+    }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)  // 4 KB independent accumulation chains in flight
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int qb2 = 0; qb2 < 2; ++qb2) {
+        sc[kb][qb2] = mfma32(fq[s][qb2], kf[kb][s], sc[kb][qb2]);
+        dp[kb][qb2] = mfma32(fo[s][qb2], vf[kb][s], dp[kb][qb2]);
+      }
+  if constexpr (MASKED) {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int qb2 = 0; qb2 < 2; ++qb2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (qb2 * 32 + acc_row(r, hi) >= qv) sc[kb][qb2][r] = INFINITY;
+  }
+  // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS;
+  // each transposed dO / Q fragment feeds every key block
+#pragma unroll
+  for (int qb2 = 0; qb2 < 2; ++qb2)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 pf[KB], df[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        f32x8 pv, dv8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * s2 + j;
+          pv[j] = __builtin_amdgcn_exp2f(-sc[kb][qb2][r]);
+          dv8[j] = pv[j] * dp[kb][qb2][r];
+        }
+        pf[kb] = __builtin_convertvector(pv, bf16x8);
+        df[kb] = __builtin_convertvector(dv8, bf16x8);
+      }
+      const int row0 = qb2 * 32 + 16 * s2;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const bf16x8 to = tr_frag(ot, row0, tro.off[db]), tq = tr_frag(qt, row0, tro.off[db]);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          dv[kb][db] = mfma32(to, pf[kb], dv[kb][db]);
+          dk[kb][db] = mfma32(tq, df[kb], dk[kb][db]);
+        }
+      }
+    }
+}
+
+// dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key key_base + 32 kb, d = 32 db + acc_row(r))
+template <int SEG, int KB>
+__device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb0, int key_base, int len, int hcol,
+                                           int hi, const f32x16 (&dk)[KB][2], const f32x16 (&dv)[KB][2]) {
+  const float scale = b.f.scale;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int key = key_base + 32 * kb;
+    if (key < len) {
+      float* dkp = (SEG == 0 ? b.dk0 : b.dk1) + (kb0 + key) * (SEG == 0 ? b.lddk0 : b.lddk1) + hcol;
+      float* dvp = (SEG == 0 ? b.dv0 : b.dv1) + (kb0 + key) * (SEG == 0 ? b.lddv0 : b.lddv1) + hcol;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = db * 32 + 8 * g + 4 * hi;
+          *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * scale, dk[kb][db][4 * g + 1] * scale,
+                                             dk[kb][db][4 * g + 2] * scale, dk[kb][db][4 * g + 3] * scale);
+          *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
+                                             dv[kb][db][4 * g + 3]);
+        }
+    }
+  }
+}
+
 // grid (key tiles of 128, heads, SHARED ? 1 : batch); wave w owns keys tile*128 + 32 w + l32.
 // Q / dO tiles and their lse / delta stream through the LDS-DMA ring.  The resident K fragment is
 // negated and scaled by c and the S chain is seeded with +lse straight from LDS, so it returns
@@ -214,10 +324,9 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[kb][0][i] = dk[kb][1][i] = dv[kb][0][i] = dv[kb][1][i] = 0.f;
 
-  // One tile of the sweep.  MASKED (the last, ragged query tile of an item) is a separate
-  // instantiation, so the full-tile body is one basic block: the compiler interleaves one q-block's
-  // S / dP chains with the other's exp2 / pack / dV / dK work (a uniform branch between the chains
-  // and the softmax split them apart).
+  // One tile of the sweep: wait for it, restage the ring, then dkdv_tile.  MASKED (the last,
+  // ragged query tile of an item) is a separate instantiation, so the full-tile body is one basic
+  // block the compiler can interleave.
   auto tile_body = [&](int t, int cq, auto masked) __attribute__((always_inline)) {
     // tile t has landed (later stages stay in flight: 5 DMA wave-instructions per stage on
     // waves 0-1, 4 on waves 2-3); every wave is done with tile t-1, whose buffer stage t+3 reuses
@@ -235,87 +344,7 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
       stage(t + NBUF - 1, s_item, s_q * 64);
       if (++s_q == ntq) s_q = 0, ++s_item;
     }
-    const char* qt = smem + (t & (NBUF - 1)) * STG;
-    const char* ot = qt + TB;
-    const float* lse_s = (const float*)(qt + 2 * TB);
-    const float* dl_s = lse_s + 64;
-    // seeds in accumulator order: rows qb2*32 + acc_row(r), four consecutive per float4
-    f32x16 sc[KB][2], dp[KB][2];
-#pragma unroll
-    for (int qb2 = 0; qb2 < 2; ++qb2)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 l4 = *(const float4*)(lse_s + qb2 * 32 + 8 * g + 4 * hi);
-        const float4 d4 = *(const float4*)(dl_s + qb2 * 32 + 8 * g + 4 * hi);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          sc[kb][qb2][4 * g] = l4.x; sc[kb][qb2][4 * g + 1] = l4.y;
-          sc[kb][qb2][4 * g + 2] = l4.z; sc[kb][qb2][4 * g + 3] = l4.w;
-          dp[kb][qb2][4 * g] = d4.x; dp[kb][qb2][4 * g + 1] = d4.y;
-          dp[kb][qb2][4 * g + 2] = d4.z; dp[kb][qb2][4 * g + 3] = d4.w;
-        }
-      }
-    // clamped duplicate rows of the ragged tile get P = 0
-    auto mask_rows = [&](int kb, int qb2) __attribute__((always_inline)) {
-      if constexpr (decltype(masked)::value) {
-        const int qv = f.lq - cq * 64;  // valid query rows of this tile
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (qb2 * 32 + acc_row(r, hi) >= qv) sc[kb][qb2][r] = INFINITY;
-      }
-    };
-    bf16x8 fq[4][2], fo[4][2];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int qb2 = 0; qb2 < 2; ++qb2) {
-        fq[s][qb2] = row_frag(qt, qb2 * 32 + l32, s, hi);
-        fo[s][qb2] = row_frag(ot, qb2 * 32 + l32, s, hi);
-      }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)  // 4 KB independent accumulation chains in flight
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-        for (int qb2 = 0; qb2 < 2; ++qb2) {
-          sc[kb][qb2] = mfma32(fq[s][qb2], kf[kb][s], sc[kb][qb2]);
-          dp[kb][qb2] = mfma32(fo[s][qb2], vf[kb][s], dp[kb][qb2]);
-        }
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      mask_rows(kb, 0);
-      mask_rows(kb, 1);
-    }
-    // P, dS (lane: key column l32, query rows qb2*32 + acc_row(r)); dV^T += dO^T P, dK^T += Q^T dS;
-    // each transposed dO / Q fragment feeds every key block
-#pragma unroll
-    for (int qb2 = 0; qb2 < 2; ++qb2)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf[KB], df[KB];
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          f32x8 pv, dv8;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int r = 8 * s2 + j;
-            pv[j] = __builtin_amdgcn_exp2f(-sc[kb][qb2][r]);
-            dv8[j] = pv[j] * dp[kb][qb2][r];
-          }
-          pf[kb] = __builtin_convertvector(pv, bf16x8);
-          df[kb] = __builtin_convertvector(dv8, bf16x8);
-        }
-        const int row0 = qb2 * 32 + 16 * s2;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const bf16x8 to = tr_frag(ot, row0, tro.off[db]), tq = tr_frag(qt, row0, tro.off[db]);
-#pragma unroll
-          for (int kb = 0; kb < KB; ++kb) {
-            dv[kb][db] = mfma32(to, pf[kb], dv[kb][db]);
-            dk[kb][db] = mfma32(tq, df[kb], dk[kb][db]);
-          }
-        }
-      }
+    dkdv_tile<KB, decltype(masked)::value>(smem + (t & (NBUF - 1)) * STG, f.lq - cq * 64, kf, vf, dk, dv, tro, l32, hi);
   };
   // tiles item by item; the last query tile of an item is the only one that can be ragged
   const bool ragged = f.lq % 64 != 0;
@@ -327,25 +356,123 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
       ++t;
     }
   }
-  // dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key l32, d = 32 db + acc_row(r))
+  store_dkdv<SEG, KB>(b, kb0, key_base, len, hcol, hi, dk, dv);
+}
+
+// ---------------------------------------------------------------- dK, dV: hand-scheduled sweep
+// attn_bwd_dkdv_kernel's work for one item's full query tiles as ONE inline-asm statement
+// (tools/gen_attn_bwd_pipe.py, sr_attn_bwd_pipe.inc): one wave per SIMD, 64 keys per wave (two key
+// blocks), 256 per workgroup; the two 32-query halves of a tile are pipelined half a tile apart so
+// that one half's exp2 / dS / bf16 packing runs in the MFMA gaps of the other's chains.  A ragged
+// last query tile (lq % 64) is staged up front into a fifth LDS stage and run afterwards with the
+// compiled dkdv_tile, so every dK / dV accumulation happens in the compiled kernel's order (the
+// outputs are bit-identical to attn_bwd_dkdv_kernel's).  The host picks this kernel for one item
+// per workgroup (keys not shared across the batch) and at least 4 full query tiles.
+//   LDS: ring of 4 x (Q tile | dO tile) at 0 .. 64 KB, the ring's lse | -delta at 64 KB + 512 s,
+//        the ragged stage (Q | dO | lse | -delta) after them.
+template <int SEG>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_kernel(sr_attn_bwd_desc b) {
+  constexpr int SLOT = 2 * TB, LSE0 = 4 * SLOT, RAG = LSE0 + 4 * 512;
+  __shared__ __attribute__((aligned(16))) char smem[RAG + 2 * TB + 512];
+  const sr_attn_desc& f = b.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int head = blockIdx.y, hcol = head * 64, item = blockIdx.z;
+  const int len = SEG == 0 ? f.l0 : f.l1;
+  const int64_t kb0 = (int64_t)item * (SEG == 0 ? f.k0_bstride : f.k1_bstride);
+  const bf16* kp = (const bf16*)(SEG == 0 ? f.k0 : f.k1);
+  const bf16* vp = (const bf16*)(SEG == 0 ? f.v0 : f.v1);
+  const int64_t ldk = SEG == 0 ? f.ldk0 : f.ldk1, ldv = SEG == 0 ? f.ldv0 : f.ldv1;
+  const int key_base = blockIdx.x * 256 + wave * 64 + l32;  // key of block kb: + 32 kb
+  const float c = f.scale * 1.4426950408889634f;
+  const int nfull = f.lq / 64, qv = f.lq % 64;  // nfull >= 4 (host)
+
+  // staging: wave w copies row groups 4 (w & 1) .. + 3 of the Q (waves 0, 1) or dO (2, 3) tile and
+  // the tile's 64 lse (waves 0, 2) or -delta (1, 3) values: five DMA wave-instructions per tile and
+  // wave (waves 2, 3 duplicate 0, 1's dword copy, so the asm's vmcnt counts are uniform)
+  const uint32_t lds0 = sr::lds_addr(smem);
+  const bool stage_o = wave_u >= 2;
+  const int64_t sld = stage_o ? b.lddo : f.ldq;
+  const bf16* const tbase = (const bf16*)(stage_o ? b.dout : f.q) + (int64_t)item * f.q_bstride * sld + hcol;
+  const float* const lbase = ((wave_u & 1) ? b.delta : f.lse) + ((int64_t)item * f.heads + head) * f.lq;
+  const int g0 = 4 * (wave_u & 1);
+  const uint32_t offA = piece_off(sld, 0, lane), offB = piece_off(sld, 1, lane);
+  const uint32_t ldsv = __builtin_amdgcn_readfirstlane(lds0 + (stage_o ? TB : 0) + g0 * 1024);
+  const uint32_t ldsl = __builtin_amdgcn_readfirstlane(lds0 + LSE0 + (wave_u & 1) * 256);
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const int key = key_base + 32 * kb;
-    if (key < len) {
-      float* dkp = (SEG == 0 ? b.dk0 : b.dk1) + (kb0 + key) * (SEG == 0 ? b.lddk0 : b.lddk1) + hcol;
-      float* dvp = (SEG == 0 ? b.dv0 : b.dv1) + (kb0 + key) * (SEG == 0 ? b.lddv0 : b.lddv1) + hcol;
+  for (int t = 0; t < 3; ++t) {
+    const char* p = (const char*)(tbase + (int64_t)(t * 64 + 8 * g0) * sld);
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+    for (int i = 0; i < 4; ++i) sr::dma16_s(p + (int64_t)8 * i * sld * 2, (i & 1) ? offB : offA, ldsv + t * SLOT + i * 1024);
+    sr::dma4_s(lbase + t * 64, (uint32_t)lane * 4, ldsl + t * 512);
+  }
+  if (qv) {  // the ragged last tile: rows clamped to lq - 1 (P = 0 for them: dkdv_tile<.., true>)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d0 = db * 32 + 8 * g + 4 * hi;
-          *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * f.scale, dk[kb][db][4 * g + 1] * f.scale,
-                                             dk[kb][db][4 * g + 2] * f.scale, dk[kb][db][4 * g + 3] * f.scale);
-          *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
-                                             dv[kb][db][4 * g + 3]);
-        }
+    for (int i = 0; i < 4; ++i) dma_rows(tbase, sld, nfull * 64, f.lq, g0 + i, lane, lds0 + RAG + (stage_o ? TB : 0));
+    sr::dma4(lbase + min(nfull * 64 + lane, f.lq - 1), lds0 + RAG + 2 * TB + (wave_u & 1) * 256);
+  }
+
+  bf16x8 kf[2][4], vf[2][4];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int keyc = min(key_base + 32 * kb, len - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[kb][s] = *(const bf16x8*)(kp + (kb0 + keyc) * ldk + hcol + 16 * s + 8 * hi);
+      vf[kb][s] = *(const bf16x8*)(vp + (kb0 + keyc) * ldv + hcol + 16 * s + 8 * hi);
     }
   }
+  __builtin_amdgcn_s_waitcnt(0);  // the fragments and the prologue stages
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[kb][s][j] = (bf16)(-(float)kf[kb][s][j] * c);
+  const TrOff tro = tr_offsets(lane);
+  f32x16 dk[2][2], dv[2][2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[kb][0][i] = dk[kb][1][i] = dv[kb][0][i] = dv[kb][1][i] = 0.f;
+
+  // the asm's operands: fragment lane addresses (slot, block and row offsets ride in the
+  // instructions' offset field), the DMA walk from tile 3 on (scalar bases, per-lane offsets that
+  // step one tile per stage)
+  uint32_t ra[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ra[s] = lds0 + l32 * 128 + swz(l32, 2 * s + hi) * 16;
+  const uint32_t ta00 = lds0 + tro.off[0][0], ta01 = lds0 + tro.off[0][1];
+  const uint32_t ta10 = lds0 + tro.off[1][0], ta11 = lds0 + tro.off[1][1];
+  const uint32_t sa = lds0 + LSE0 + 16 * hi;
+  const uint64_t spu = (uint64_t)(uintptr_t)(tbase + (int64_t)(3 * 64 + 8 * g0) * sld);
+  const uint32_t sp_lo = __builtin_amdgcn_readfirstlane((uint32_t)spu);
+  const uint32_t sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(spu >> 32));
+  const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
+  const char* spb2 = spb + 16 * sld * 2;
+  const uint64_t lpu = (uint64_t)(uintptr_t)(lbase + 3 * 64);
+  const uint32_t lp_lo = __builtin_amdgcn_readfirstlane((uint32_t)lpu);
+  const uint32_t lp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lpu >> 32));
+  const char* lpb = (const char*)(uintptr_t)(((uint64_t)lp_hi << 32) | lp_lo);
+  uint32_t dma0 = offA, dma1 = offB + (uint32_t)(8 * sld * 2), lofs = (uint32_t)lane * 4;
+  const uint32_t sstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * sld * 2));
+  int nn = __builtin_amdgcn_readfirstlane((nfull - 4) >> 2);
+  const int rem = __builtin_amdgcn_readfirstlane((nfull - 4) & 3);
+  asm volatile(SR_ATTN_BWD_PIPE_ASM
+               : [dk00] "+&a"(dk[0][0]), [dk01] "+&a"(dk[0][1]), [dk10] "+&a"(dk[1][0]), [dk11] "+&a"(dk[1][1]),
+                 [dv00] "+&a"(dv[0][0]), [dv01] "+&a"(dv[0][1]), [dv10] "+&a"(dv[1][0]), [dv11] "+&a"(dv[1][1]),
+                 [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [lofs] "+&v"(lofs), [n] "+&s"(nn)
+               : [k00] "v"(kf[0][0]), [k01] "v"(kf[0][1]), [k02] "v"(kf[0][2]), [k03] "v"(kf[0][3]),
+                 [k10] "v"(kf[1][0]), [k11] "v"(kf[1][1]), [k12] "v"(kf[1][2]), [k13] "v"(kf[1][3]),
+                 [v00] "v"(vf[0][0]), [v01] "v"(vf[0][1]), [v02] "v"(vf[0][2]), [v03] "v"(vf[0][3]),
+                 [v10] "v"(vf[1][0]), [v11] "v"(vf[1][1]), [v12] "v"(vf[1][2]), [v13] "v"(vf[1][3]),
+                 [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
+                 [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11), [sa] "v"(sa),
+                 [ldsv] "s"(ldsv), [ldsl] "s"(ldsl), [sp] "s"(spb), [sp2] "s"(spb2), [lp] "s"(lpb),
+                 [sstep] "s"(sstep), [rem] "s"(rem)
+               : SR_ATTN_BWD_PIPE_CLOBBERS, "memory", "m0", "scc");
+  if (qv) dkdv_tile<2, true>(smem + RAG, qv, kf, vf, dk, dv, tro, l32, hi);
+  store_dkdv<SEG, 2>(b, kb0, key_base, len, hcol, hi, dk, dv);
 }
 
 // ---------------------------------------------------------------- dQ
@@ -510,16 +637,36 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
+  // dK / dV: the hand-scheduled sweep (SR_ATTN_BWD_PIPE) where a workgroup sweeps one item's
+  // queries, at least 4 full query tiles, with 32-bit per-lane DMA offsets; else the compiled sweep
+  // with KB key blocks of 32 per wave (SR_ATTN_BWD_KB)
+  const int64_t ldmax = std::max<int64_t>(f.ldq, b.lddo);
+  const bool pipe_ok = sr::tune(SR_TUNE_ATTN_BWD_PIPE) != 0 && f.lq >= 256 &&
+                       (int64_t)(f.lq + 64) * ldmax * 2 < ((int64_t)1 << 31);
   const bool kb2 = sr::tune(SR_TUNE_ATTN_BWD_KB) == 2;
-  const int kr = kb2 ? 256 : 128;  // keys per workgroup
-  const dim3 g0((f.l0 + kr - 1) / kr, f.heads, f.k0_bstride == 0 ? 1 : f.batch);
-  if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g0, dim3(256), 0, s, b);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g0, dim3(256), 0, s, b);
-  if (f.l1 > 0) {
-    const dim3 g1((f.l1 + kr - 1) / kr, f.heads, f.k1_bstride == 0 ? 1 : f.batch);
-    if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 2>), g1, dim3(256), 0, s, b);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1>), g1, dim3(256), 0, s, b);
+  const int kr = kb2 ? 256 : 128;  // keys per workgroup of the compiled sweep
+  const char* name = nullptr;
+  for (int seg = 0; seg < (f.l1 > 0 ? 2 : 1); ++seg) {
+    const int len = seg == 0 ? f.l0 : f.l1;
+    const bool shared = (seg == 0 ? f.k0_bstride : f.k1_bstride) == 0;
+    const int nz = shared ? 1 : f.batch;
+    if (pipe_ok && (!shared || f.batch == 1)) {
+      const dim3 g((len + 255) / 256, f.heads, nz);
+      if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<0>), g, dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<1>), g, dim3(256), 0, s, b);
+      if (seg == 0) name = "attn_bwd_dkdv_pipe_kernel<0>";
+      continue;
+    }
+    const dim3 g((len + kr - 1) / kr, f.heads, nz);
+    if (seg == 0) {
+      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g, dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g, dim3(256), 0, s, b);
+      name = kb2 ? "attn_bwd_dkdv_kernel<0, 2>" : "attn_bwd_dkdv_kernel<0, 1>";
+    } else {
+      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 2>), g, dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1>), g, dim3(256), 0, s, b);
+    }
   }
-  sr::note_kernel("attn_bwd_dkdv_kernel<0, %d>", kb2 ? 2 : 1);
+  sr::note_kernel("%s", name);
   return sr::check_launch("sr_attention_bwd");
 }

@@ -679,10 +679,15 @@ def attn_bwd():
             ops.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, lse, g, d[:, :C], d[:, C:2 * C],
                               d[:, 2 * C:], delta, heads=H, batch=batch, lq=lq, q_bstride=lq, l0=lq, k0_bstride=kb)
         fl = 10.0 * batch * H * lq * lq * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
-        for kbn in (1, 2, 1, 2):  # SR_ATTN_BWD_KB: 32 or 64 keys per wave in the dK/dV sweep
-            with ops.tuning(SR_ATTN_BWD_KB=kbn):
+        # dK/dV sweep: compiled with 32 keys per wave (kb1), or the hand-scheduled asm sweep (pipe);
+        # SR_BWD_AB=kb adds the compiled 64-keys-per-wave form
+        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0)), ("pipe", dict(SR_ATTN_BWD_PIPE=1))]
+        if os.environ.get("SR_BWD_AB") == "kb":
+            arms.append(("kb2", dict(SR_ATTN_BWD_KB=2, SR_ATTN_BWD_PIPE=0)))
+        for arm, sw in arms * 2:
+            with ops.tuning(**sw):
                 ms = timeit(f, reps=3 if batch == 1 else 5, warm=1)
-            print(f"attn_bwd {name:16s} kb={kbn} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}",
+            print(f"attn_bwd {name:16s} {arm:5s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}",
                   flush=True)
 
 
