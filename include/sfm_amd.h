@@ -93,7 +93,7 @@ enum sr_tuning_key {
                                (2: one wave per SIMD, 64 keys; bit-identical)           default 1 */
   SR_TUNE_ATTN_BWD_PIPE = 20,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
                                64 keys; one item per workgroup, >= 4 full query tiles;
-                               bit-identical)                                           default 0 */
+                               bit-identical)                                           default 1 */
   SR_TUNE_COUNT = 21
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */

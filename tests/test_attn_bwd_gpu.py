@@ -141,7 +141,7 @@ def test_attention_bwd_two_key_blocks_per_wave(case):
         dk1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
         dv1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
         delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_KB=kbn):
+        with ops.tuning(SR_ATTN_BWD_KB=kbn, SR_ATTN_BWD_PIPE=0):
             ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
             assert ops.last_kernel() == f"attn_bwd_dkdv_kernel<0, {kbn}>"
         outs.append([t for t in (dq, dk0, dv0, dk1, dv1) if t is not None])

@@ -63,6 +63,10 @@ VALU_LEAD = int(os.environ.get("SR_BWD_PIPE_VALU_LEAD", "2"))
 LEAD_NOP = int(os.environ.get("SR_BWD_PIPE_LEAD_NOP", "4"))
 X_READS = float(os.environ.get("SR_BWD_PIPE_X_READS", "0.7"))
 Y_READS = float(os.environ.get("SR_BWD_PIPE_Y_READS", "0.8"))
+# timing-only ablations (WRONG results; for locating the loop's cost): comma list of nobar (no per-tile
+# barrier), nodma (no LDS-DMA staging), novalu (no exp / mul / pack), noread (no LDS reads), nowait
+# (no lgkmcnt waits)
+EXP = set(filter(None, os.environ.get("SR_BWD_PIPE_EXP", "").split(",")))
 
 
 def S(q, kb):
@@ -119,14 +123,21 @@ class Emit:
             self.n += 1
 
     def op(self, s):
+        if "nowait" in EXP and s.startswith("s_waitcnt lgkm"):
+            return
+        if "nobar" in EXP and s == "s_barrier":
+            return
         self.lines.append(s)
 
     def read(self, key, text):
-        self.op(text)
+        if "noread" not in EXP:
+            self.op(text)
         self.seq[key] = self.n
         self.n += 1
 
     def wait(self, keys):
+        if "noread" in EXP:
+            return
         s = max((self.seq[k] for k in keys if k in self.seq), default=-1)
         if s <= self.waited:
             return
@@ -135,7 +146,7 @@ class Emit:
         self.waited = self.n - 1 - cnt
 
     def wait_all(self):
-        if self.waited < self.n - 1:
+        if "noread" not in EXP and self.waited < self.n - 1:
             self.op("s_waitcnt lgkmcnt(0)")
             self.waited = self.n - 1
 
@@ -181,6 +192,8 @@ class Phase:
 
     # ---- VALU
     def val(self, q):
+        if "novalu" in EXP:
+            return
         for kb, s2 in ORDER:
             src, dsp = S(q, kb) + 8 * s2, P(q, kb) + 8 * s2
             for j in range(8):  # P = exp2(-S'), in place
@@ -227,6 +240,8 @@ class Phase:
     @staticmethod
     def dma_units(slot):
         out = []
+        if "nodma" in EXP:
+            return out
         for i in range(4):
             out.append([f"s_add_u32 m0, %[ldsv], {slot * SLOT_B + i * 1024}", "s_nop 0",
                         f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"])

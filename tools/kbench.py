@@ -684,6 +684,8 @@ def attn_bwd():
         arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0)), ("pipe", dict(SR_ATTN_BWD_PIPE=1))]
         if os.environ.get("SR_BWD_AB") == "kb":
             arms.append(("kb2", dict(SR_ATTN_BWD_KB=2, SR_ATTN_BWD_PIPE=0)))
+        if os.environ.get("SR_BWD_AB") == "pipe":  # the asm sweep only (A/B of library builds)
+            arms = arms[1:]
         for arm, sw in arms * 2:
             with ops.tuning(**sw):
                 ms = timeit(f, reps=3 if batch == 1 else 5, warm=1)

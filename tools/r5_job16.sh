@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/j16_prof -o run -- python3 tools/kbench.py attn_bwd > gpurun_out/j16_kbwd.log 2>&1 || { echo "failed"; tail -30 gpurun_out/j16_kbwd.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/j16_prof -o run --output-format csv -- python3 tools/kbench.py attn_bwd > gpurun_out/j16_kbwd.log 2>&1 || { echo "failed"; tail -30 gpurun_out/j16_kbwd.log; exit 1; }
 grep attn_bwd gpurun_out/j16_kbwd.log
 f=$(find gpurun_out/j16_prof -name "*kernel_stats.csv" | head -1)
 cp "$f" gpurun_out/j16_stats.csv
