@@ -94,7 +94,13 @@ enum sr_tuning_key {
   SR_TUNE_ATTN_BWD_PIPE = 20,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
                                64 keys; one item per workgroup, >= 4 full query tiles;
                                bit-identical)                                           default 1 */
-  SR_TUNE_COUNT = 21
+  SR_TUNE_ATTN_BWD_DQ_PIPE = 21,/* 1: the attention backward's dQ sweep as the hand-scheduled asm pipeline
+                               (one wave per SIMD, 64 queries; one key segment of >= 4 full
+                               tiles, query padding within 2 % of the compiled sweep's; 2: any
+                               padding; bit-identical)                                  default 1 */
+  SR_TUNE_ATTN_BWD_CONC = 22,/* 1: the attention backward's dK/dV sweep on a second (library-owned) stream
+                               beside dQ, forked from and joined back to the caller's stream default 0 */
+  SR_TUNE_COUNT = 23
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

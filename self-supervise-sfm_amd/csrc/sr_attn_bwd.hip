@@ -18,6 +18,7 @@
 // (r & 3) + 8 (r >> 2) + 4 hi, r = 0..15, which is the k order the tr-reads produce.
 // Tiles are 64 rows x 128 B (swizzle: see swz below).
 #include <cfloat>
+#include <mutex>
 #include <type_traits>
 
 #include "sr_common.h"
@@ -476,6 +477,57 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_kernel(sr_attn_bwd_
 }
 
 // ---------------------------------------------------------------- dQ
+// One 64-key tile of the dQ sweep for one 32-query block (lane: query l32): kt = the tile's LDS
+// stage (K tile | V tile), valid = its keys (MASKED only: keys past it get P = 0), qf = c q, nl /
+// nd = -lse / the stored -delta of the lane's query broadcast.  S'^T = K (cQ)^T - lse,
+// dP'^T = V dO^T - delta, dS = exp2(S') dP'; dQ^T += K^T dS^T.
+template <bool MASKED>
+__device__ __forceinline__ void dq_tile(const char* kt, int valid, const bf16x8 (&qf)[4], const bf16x8 (&of)[4],
+                                        const f32x16& nl, const f32x16& nd, f32x16 (&dq)[2], const TrOff& tro,
+                                        int l32, int hi) {
+  const char* vt = kt + TB;
+  f32x16 sc[2], dp[2];
+  bf16x8 fk[4][2], fv[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      fk[s][kb] = row_frag(kt, kb * 32 + l32, s, hi);
+      fv[s][kb] = row_frag(vt, kb * 32 + l32, s, hi);
+    }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      sc[kb] = mfma32(fk[s][kb], qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
+      dp[kb] = mfma32(fv[s][kb], of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
+    }
+  if constexpr (MASKED) {  // partial key tile: keys >= valid get S' = -inf, P = 0
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kb * 32 + acc_row(r, hi) >= valid) sc[kb][r] = -INFINITY;
+  }
+  // one code path for every tile: a masked copy of the dS / dQ block made the compiler join
+  // two register assignments of dq with 64 v_mov per tile
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f32x8 d8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * s2 + j;
+        d8[j] = __builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r];
+      }
+      const bf16x8 df = __builtin_convertvector(d8, bf16x8);
+      const int row0 = kb * 32 + 16 * s2;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
+    }
+}
+
 // grid (query tiles of 128, heads, batch); wave w owns query rows tile*128 + 32 w + l32.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b) {
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TB];  // ring of K tile | V tile stages
@@ -553,50 +605,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
     else wait_vm<0>();
     sr::barrier_raw();  // every wave is done with tile t-1, whose buffer stage t+3 reuses
     if (t + NBUF - 1 < ntiles) stage(t + NBUF - 1);
-    const char* kt = smem + (t & (NBUF - 1)) * 2 * TB;
-    const char* vt = kt + TB;
-    f32x16 sc[2], dp[2];
-    bf16x8 fk[4][2], fv[4][2];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        fk[s][kb] = row_frag(kt, kb * 32 + l32, s, hi);
-        fv[s][kb] = row_frag(vt, kb * 32 + l32, s, hi);
-      }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)  // four independent accumulation chains in flight
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        sc[kb] = mfma32(fk[s][kb], qf[s], s == 0 ? nl : sc[kb]);  // S^T = K (cQ)^T - lse
-        dp[kb] = mfma32(fv[s][kb], of[s], s == 0 ? nd : dp[kb]);  // dP^T = V dO^T - delta
-      }
-    if constexpr (decltype(masked)::value) {  // partial key tile: keys >= valid get S' = -inf, P = 0
+    int valid = 64;
+    if constexpr (decltype(masked)::value) {
       const int seg = t >= nt0;
-      const int valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kb * 32 + acc_row(r, hi) >= valid) sc[kb][r] = -INFINITY;
+      valid = (seg ? f.l1 : f.l0) - (seg ? t - nt0 : t) * 64;
     }
-    // one code path for every tile: a masked copy of the dS / dQ block made the compiler join
-    // two register assignments of dq with 64 v_mov per tile
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        f32x8 d8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = 8 * s2 + j;
-          d8[j] = __builtin_amdgcn_exp2f(sc[kb][r]) * dp[kb][r];
-        }
-        const bf16x8 df = __builtin_convertvector(d8, bf16x8);
-        const int row0 = kb * 32 + 16 * s2;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) dq[db] = mfma32(tr_frag(kt, row0, tro.off[db]), df, dq[db]);  // dQ^T += K^T dS^T
-      }
+    dq_tile<decltype(masked)::value>(smem + (t & (NBUF - 1)) * 2 * TB, valid, qf, of, nl, nd, dq, tro, l32, hi);
   };
   const int rag0 = f.l0 % 64 ? nt0 - 1 : -1, rag1 = nt1 > 0 && f.l1 % 64 ? ntiles - 1 : -1;
   for (int t = 0; t < ntiles; ++t) {
@@ -613,6 +627,148 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
             make_float4(dq[db][4 * g] * f.scale, dq[db][4 * g + 1] * f.scale, dq[db][4 * g + 2] * f.scale,
                         dq[db][4 * g + 3] * f.scale);
   }
+}
+
+// ---------------------------------------------------------------- dQ: hand-scheduled sweep
+// attn_bwd_dq_kernel's work for one key segment's full key tiles as ONE inline-asm statement
+// (tools/gen_attn_bwd_pipe.py, SR_ATTN_BWD_DQ_ASM): one wave per SIMD, 64 queries per wave (two
+// query blocks sharing every K / V fragment read), 256 per workgroup, the two blocks pipelined
+// half a tile apart like the dK/dV sweep.  A ragged last key tile (l0 % 64) is staged up front
+// into a fifth LDS stage and run afterwards with the compiled dq_tile, so every dQ accumulation
+// happens in the compiled kernel's order (bit-identical outputs).  The host picks this kernel for
+// one key segment (l1 == 0) of at least 4 full key tiles.
+//   LDS: ring of 4 x (K tile | V tile) at 0 .. 64 KB, the ragged stage after it.
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_desc b) {
+  constexpr int SLOT = 2 * TB, RAG = 4 * SLOT;
+  __shared__ __attribute__((aligned(16))) char smem[RAG + 2 * TB];
+  const sr_attn_desc& f = b.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int head = blockIdx.y, hcol = head * 64, item = blockIdx.z;
+  const int q0 = blockIdx.x * 256 + wave * 64;  // queries of block qb: q0 + 32 qb + l32
+  const float c = f.scale * 1.4426950408889634f;
+  const int nfull = f.l0 / 64, kv = f.l0 % 64;  // nfull >= 4 (host)
+
+  // staging: wave w copies row groups 4 (w & 1) .. + 3 of the K (waves 0, 1) or V (2, 3) tile
+  const uint32_t lds0 = sr::lds_addr(smem);
+  const bool stage_v = wave_u >= 2;
+  const int64_t sld = stage_v ? f.ldv0 : f.ldk0;
+  const bf16* const sb0 = (const bf16*)(stage_v ? f.v0 : f.k0) + (int64_t)item * f.k0_bstride * sld + hcol;
+  const int g0 = 4 * (wave_u & 1);
+  const uint32_t offA = piece_off(sld, 0, lane), offB = piece_off(sld, 1, lane);
+  const uint32_t ldsv = __builtin_amdgcn_readfirstlane(lds0 + (stage_v ? TB : 0) + g0 * 1024);
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const char* p = (const char*)(sb0 + (int64_t)(t * 64 + 8 * g0) * sld);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sr::dma16_s(p + (int64_t)8 * i * sld * 2, (i & 1) ? offB : offA, ldsv + t * SLOT + i * 1024);
+  }
+  if (kv) {  // the ragged last key tile: rows clamped to l0 - 1 (P = 0 for them: dq_tile<true>)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma_rows(sb0, sld, nfull * 64, f.l0, g0 + i, lane, lds0 + RAG + (stage_v ? TB : 0));
+  }
+
+  bf16x8 qf[2][4], of[2][4];
+  float lse[2], dlt[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrc = min(q0 + 32 * qb + l32, f.lq - 1);
+    const int64_t qr = (int64_t)item * f.q_bstride + qrc;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[qb][s] = *(const bf16x8*)((const bf16*)f.q + qr * f.ldq + hcol + 16 * s + 8 * hi);
+      of[qb][s] = *(const bf16x8*)((const bf16*)b.dout + qr * b.lddo + hcol + 16 * s + 8 * hi);
+    }
+    const int64_t lrow = ((int64_t)item * f.heads + head) * f.lq + qrc;
+    lse[qb] = f.lse[lrow];
+    dlt[qb] = b.delta[lrow];
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the fragments and the prologue stages
+  f32x16 nl[2], nd[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qb][s][j] = (bf16)((float)qf[qb][s][j] * c);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      nl[qb][i] = -lse[qb];
+      nd[qb][i] = dlt[qb];  // the stored -delta
+    }
+  }
+  const TrOff tro = tr_offsets(lane);
+  f32x16 dq[2][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dq[0][0][i] = dq[0][1][i] = dq[1][0][i] = dq[1][1][i] = 0.f;
+
+  uint32_t ra[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ra[s] = lds0 + l32 * 128 + swz(l32, 2 * s + hi) * 16;
+  const uint32_t ta00 = lds0 + tro.off[0][0], ta01 = lds0 + tro.off[0][1];
+  const uint32_t ta10 = lds0 + tro.off[1][0], ta11 = lds0 + tro.off[1][1];
+  const uint64_t spu = (uint64_t)(uintptr_t)(sb0 + (int64_t)(3 * 64 + 8 * g0) * sld);
+  const uint32_t sp_lo = __builtin_amdgcn_readfirstlane((uint32_t)spu);
+  const uint32_t sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(spu >> 32));
+  const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
+  const char* spb2 = spb + 16 * sld * 2;
+  uint32_t dma0 = offA, dma1 = offB + (uint32_t)(8 * sld * 2);
+  const uint32_t sstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * sld * 2));
+  int nn = __builtin_amdgcn_readfirstlane((nfull - 4) >> 2);
+  const int rem = __builtin_amdgcn_readfirstlane((nfull - 4) & 3);
+  asm volatile(SR_ATTN_BWD_DQ_ASM
+               : [dq00] "+&a"(dq[0][0]), [dq01] "+&a"(dq[0][1]), [dq10] "+&a"(dq[1][0]), [dq11] "+&a"(dq[1][1]),
+                 [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [n] "+&s"(nn)
+               : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
+                 [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
+                 [o00] "a"(of[0][0]), [o01] "a"(of[0][1]), [o02] "a"(of[0][2]), [o03] "a"(of[0][3]),
+                 [o10] "a"(of[1][0]), [o11] "a"(of[1][1]), [o12] "a"(of[1][2]), [o13] "a"(of[1][3]),
+                 [nl0] "v"(nl[0]), [nl1] "v"(nl[1]), [nd0] "v"(nd[0]), [nd1] "v"(nd[1]),
+                 [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
+                 [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11),
+                 [ldsv] "s"(ldsv), [sp] "s"(spb), [sp2] "s"(spb2), [sstep] "s"(sstep), [rem] "s"(rem)
+               : SR_ATTN_BWD_DQ_CLOBBERS, "memory", "m0", "scc");
+  if (kv) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) dq_tile<true>(smem + RAG, kv, qf[qb], of[qb], nl[qb], nd[qb], dq[qb], tro, l32, hi);
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = q0 + 32 * qb + l32;
+    if (qrow < f.lq) {
+      float* dqp = b.dq + ((int64_t)item * f.q_bstride + qrow) * b.lddq + hcol;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(float4*)(dqp + db * 32 + 8 * g + 4 * hi) =
+              make_float4(dq[qb][db][4 * g] * f.scale, dq[qb][db][4 * g + 1] * f.scale, dq[qb][db][4 * g + 2] * f.scale,
+                          dq[qb][db][4 * g + 3] * f.scale);
+    }
+  }
+}
+
+// Second stream of sr_attention_bwd (SR_TUNE_ATTN_BWD_CONC): dK/dV run beside dQ, so that one
+// sweep's last partial round of workgroups overlaps the other's (both hold one workgroup per CU
+// for most shapes).  Created once per device; fork / join by events on the caller's stream.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+SideStream* side_stream() {
+  static SideStream ss[64];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return x.s = nullptr, nullptr;
+    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+  }
+  return &x;
 }
 
 }  // namespace
@@ -636,7 +792,23 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   const int64_t nrows = (int64_t)f.batch * f.heads * f.lq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
+  // dQ: the hand-scheduled sweep (SR_ATTN_BWD_DQ_PIPE) over one key segment of at least 4 full
+  // tiles with 32-bit per-lane DMA offsets, where its 256-query workgroups pad the query count by
+  // at most 2 % more than the compiled sweep's 128 (frames of 1,374 tokens: 1,536 against 1,408
+  // rows, measured 1-3 % slower); else the compiled sweep
+  const int64_t qpad256 = (f.lq + 255) / 256 * 256, qpad128 = (f.lq + 127) / 128 * 128;
+  const bool dq_pipe = sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) != 0 && f.l1 == 0 && f.l0 >= 256 &&
+                       (int64_t)(f.l0 + 64) * std::max<int64_t>(f.ldk0, f.ldv0) * 2 < ((int64_t)1 << 31) &&
+                       (sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) == 2 || qpad256 * 100 <= qpad128 * 102);
+  if (dq_pipe)
+    hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
+  // dK / dV on the side stream when SR_ATTN_BWD_CONC (joined back below)
+  SideStream* side = sr::tune(SR_TUNE_ATTN_BWD_CONC) ? side_stream() : nullptr;
+  hipStream_t ks = s;
+  if (side && hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess)
+    ks = side->s;
   // dK / dV: the hand-scheduled sweep (SR_ATTN_BWD_PIPE) where a workgroup sweeps one item's
   // queries, at least 4 full query tiles, with 32-bit per-lane DMA offsets; else the compiled sweep
   // with KB key blocks of 32 per wave (SR_ATTN_BWD_KB)
@@ -652,20 +824,24 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
     const int nz = shared ? 1 : f.batch;
     if (pipe_ok && (!shared || f.batch == 1)) {
       const dim3 g((len + 255) / 256, f.heads, nz);
-      if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<0>), g, dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<1>), g, dim3(256), 0, s, b);
+      if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<0>), g, dim3(256), 0, ks, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<1>), g, dim3(256), 0, ks, b);
       if (seg == 0) name = "attn_bwd_dkdv_pipe_kernel<0>";
       continue;
     }
     const dim3 g((len + kr - 1) / kr, f.heads, nz);
     if (seg == 0) {
-      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g, dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g, dim3(256), 0, s, b);
+      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g, dim3(256), 0, ks, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g, dim3(256), 0, ks, b);
       name = kb2 ? "attn_bwd_dkdv_kernel<0, 2>" : "attn_bwd_dkdv_kernel<0, 1>";
     } else {
-      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 2>), g, dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1>), g, dim3(256), 0, s, b);
+      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 2>), g, dim3(256), 0, ks, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1>), g, dim3(256), 0, ks, b);
     }
+  }
+  if (ks != s) {
+    SR_CHECK(hipEventRecord(side->join, ks) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
+             SR_ELAUNCH, "sr_attention_bwd: joining the side stream failed");
   }
   sr::note_kernel("%s", name);
   return sr::check_launch("sr_attention_bwd");

@@ -151,13 +151,15 @@ def test_attention_bwd_two_key_blocks_per_wave(case):
 
 
 @pytest.mark.parametrize("case,P", [("frame", 1374), ("frame", 256), ("frame", 337), ("frame", 384), ("frame", 511),
-                                    ("frame", 512), ("frame", 200), ("global", 1100), ("reloc", 300)])
+                                    ("frame", 512), ("frame", 200), ("global", 1100), ("reloc", 300),
+                                    ("anchor", 150)])
 def test_attention_bwd_pipe(case, P):
-    """SR_ATTN_BWD_PIPE=1: the hand-scheduled dK/dV sweep (tools/gen_attn_bwd_pipe.py) gives
-    bit-identical dK / dV (and dQ) to the compiled sweep: full query-tile counts 4..21 (every
-    remainder of the asm's 4-tile loop), ragged last tiles (17, 30, 63 rows) and none, fewer than
-    4 full tiles (P = 200: the compiled sweep runs), anchors shared across the batch (reloc:
-    segment 0 compiled, segment 1 per item in the asm)."""
+    """SR_ATTN_BWD_PIPE / SR_ATTN_BWD_DQ_PIPE: the hand-scheduled dK/dV and dQ sweeps
+    (tools/gen_attn_bwd_pipe.py) give bit-identical dQ / dK / dV to the compiled sweeps: full tile
+    counts 4..21 (every remainder of the asm's 4-tile loop), ragged last tiles (17, 30, 44, 60, 63
+    rows) and none, fewer than 4 full tiles (P = 200: the compiled sweeps run), keys shared across
+    the batch (reloc: two key segments, dQ compiled, dK/dV segment 1 per item in the asm; anchor:
+    one shared segment of 700 keys, dQ in the asm for 150 queries per item, dK/dV compiled)."""
     from sailrecon_amd import ops
     torch.manual_seed(2)
     H, D = 4, 64
@@ -168,15 +170,19 @@ def test_attention_bwd_pipe(case, P):
     elif case == "global":
         B, A = 1, 0
         kw = dict(batch=1, lq=P, q_bstride=P, l0=P, k0_bstride=P)
+    elif case == "anchor":
+        B, A = 3, 700
+        kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0)
     else:
         B, A = 3, 301
         kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, l1=P, k1_bstride=P)
     x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
     q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
-    if case == "reloc":
+    if case in ("reloc", "anchor"):
         ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
         k0, v0 = ka[:, :C], ka[:, C:]
-        kw.update(k1=k, v1=v)
+        if case == "reloc":
+            kw.update(k1=k, v1=v)
     else:
         k0, v0 = k, v
     o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
@@ -191,9 +197,11 @@ def test_attention_bwd_pipe(case, P):
         dk1 = torch.full((B * P, C), float("nan"), device=DEV) if case == "reloc" else None
         dv1 = torch.full((B * P, C), float("nan"), device=DEV) if case == "reloc" else None
         delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_PIPE=pipe, SR_ATTN_BWD_KB=1):
+        with ops.tuning(SR_ATTN_BWD_PIPE=pipe, SR_ATTN_BWD_DQ_PIPE=2 * pipe, SR_ATTN_BWD_KB=1,
+                        SR_ATTN_BWD_CONC=pipe):
             ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
-            want = "attn_bwd_dkdv_pipe_kernel<0>" if pipe and P >= 256 and case != "reloc" else "attn_bwd_dkdv_kernel<0, 1>"
+            asm_dkdv = pipe and P >= 256 and case not in ("reloc", "anchor")
+            want = "attn_bwd_dkdv_pipe_kernel<0>" if asm_dkdv else "attn_bwd_dkdv_kernel<0, 1>"
             assert ops.last_kernel() == want
         outs.append([t for t in (dq, dk0, dv0, dk1, dv1) if t is not None])
     torch.cuda.synchronize()

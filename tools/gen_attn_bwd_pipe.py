@@ -397,7 +397,200 @@ def sweep():
     return lines, loop
 
 
+# ======================================================================== dQ sweep
+# attn_bwd_dq_pipe_kernel: each wave owns 64 queries (blocks A, B of 32; lane = the block's query
+# l32), the workgroup 256; key tiles of 64 stream through the ring (K tile | V tile).  Per tile
+# and block:  SD: S'^T = K (cQ)^T - lse and dP'^T = V dO^T - delta, two key blocks kb each (16
+# MFMAs; the K / V row fragments are read once for both query blocks);  VAL: dS = exp2(S') dP',
+# packed to bf16 in place (32 exp, 32 mul, 16 cvt);  GR: dQ^T += K^T dS^T (8 MFMAs, in the
+# compiled kernel's (kb, s2) order).  The same half-tile pipeline as the dK/dV sweep:
+#   X(t): MFMA GR(B, t-1) | SD(B, t)   VALU VAL(A, t)   LDS K rows(t+1) after SD(B, t)'s S chains | V rows(t+1)
+#   Y(t): MFMA GR(A, t)   | SD(A, t+1) VALU VAL(B, t)   LDS K^T(t+1) (the other parity set)
+# The row fragments are single-buffered (64 AGPRs), K^T double-buffered by tile parity (64 AGPRs);
+# dQ^T (64 AGPRs), c q and dO (64 AGPRs) and the -lse / -delta seeds (64 VGPRs) are operands.
+
+
+def FK(kb, s):
+    return 4 * (4 * kb + s)
+
+
+def FV(kb, s):
+    return 32 + 4 * (4 * kb + s)
+
+
+def KT(par, kb, s2, db):
+    return 64 + 32 * par + 4 * (4 * kb + 2 * s2 + db)
+
+
+class DqPhase(Phase):
+    def sd(self, q):
+        for which in "SP":
+            for kb in range(2):
+                acc = S(q, kb) if which == "S" else P(q, kb)
+                for s in range(4):
+                    a = FK(kb, s) if which == "S" else FV(kb, s)
+                    b = f"%[q{q}{s}]" if which == "S" else f"%[o{q}{s}]"
+                    c = (f"%[nl{q}]" if which == "S" else f"%[nd{q}]") if s == 0 else vr(acc, 16)
+                    key = ("krow", kb, s) if which == "S" else ("vrow", kb, s)
+                    self.mfma.append((f"v_mfma_f32_32x32x16_bf16 {vr(acc, 16)}, {ar(a, 4)}, {b}, {c}", [key]))
+
+    def gr(self, q, par):
+        for kb in range(2):
+            for s2 in range(2):
+                for db in range(2):
+                    self.mfma.append((f"v_mfma_f32_32x32x16_bf16 %[dq{q}{db}], {ar(KT(par, kb, s2, db), 4)}, "
+                                      f"{vr(PD(q, kb, s2), 4)}, %[dq{q}{db}]", [("kt", par, kb, s2, db)]))
+
+    def val(self, q):
+        if "novalu" in EXP:
+            return
+        for kb, s2 in ORDER:
+            src, dsp = S(q, kb) + 8 * s2, P(q, kb) + 8 * s2
+            for j in range(8):  # P = exp2(S'), in place
+                self.valu.append((COST["exp"], [f"v_exp_f32_e32 {vr(src + j)}, {vr(src + j)}"]))
+            for j in range(8):  # dS = P dP', in place
+                self.valu.append((COST["mul"], [f"v_mul_f32_e32 {vr(dsp + j)}, {vr(src + j)}, {vr(dsp + j)}"]))
+            pd = PD(q, kb, s2)
+            for jj in range(4):
+                self.valu.append((COST["cvt"], [f"v_cvt_pk_bf16_f32 {vr(pd + jj)}, {vr(dsp + 2 * jj)}, {vr(dsp + 2 * jj + 1)}"]))
+
+    @staticmethod
+    def row_units(which, slot):
+        out = []
+        for kb in range(2):
+            for s in range(4):
+                if which == "K":
+                    out.append([("read", ("krow", kb, s),
+                                 f"ds_read_b128 {ar(FK(kb, s), 4)}, %[ra{s}] offset:{slot * SLOT_B + kb * 4096}")])
+                else:
+                    out.append([("read", ("vrow", kb, s),
+                                 f"ds_read_b128 {ar(FV(kb, s), 4)}, %[ra{s}] offset:{slot * SLOT_B + TILE_B + kb * 4096}")])
+        return out
+
+    @staticmethod
+    def kt_units(slot, par):
+        out = []
+        for kb in range(2):
+            for s2 in range(2):
+                for db in range(2):
+                    off = slot * SLOT_B + (kb * 32 + 16 * s2) * 128
+                    base = KT(par, kb, s2, db)
+                    out.append([("read", ("kt0", par, kb, s2, db), f"ds_read_b64_tr_b16 {ar(base, 2)}, %[ta{db}0] offset:{off}"),
+                                ("read", ("kt", par, kb, s2, db), f"ds_read_b64_tr_b16 {ar(base + 2, 2)}, %[ta{db}1] offset:{off}")])
+        return out
+
+    @staticmethod
+    def dq_dma_units(slot, pieces):
+        out = []
+        if "nodma" in EXP:
+            return out
+        for i in pieces:
+            u = [f"s_add_u32 m0, %[ldsv], {slot * SLOT_B + i * 1024}", "s_nop 0",
+                 f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"]
+            if i == 3:
+                u += ["v_add_u32 %[dma0], %[sstep], %[dma0]", "v_add_u32 %[dma1], %[sstep], %[dma1]"]
+            out.append(u)
+        return out
+
+
+def dq_body(t4, first=False, stage=True, vm=4, last=False):
+    e = Emit()
+    cur, nxt, stg = t4, (t4 + 1) & 3, (t4 + 3) & 3
+    par = t4 & 1
+    e.op(f"; ---- dQ tile body slot {t4} first={int(first)} stage={int(stage)} vmcnt={vm} last={int(last)}")
+    e.op(f"s_waitcnt vmcnt({vm})")  # tile t+1 landed (tile t+2's four pieces may stay in flight)
+    e.op("s_barrier")
+    if first:
+        p = DqPhase(e)
+        for u in DqPhase.row_units("K", cur) + DqPhase.row_units("V", cur) + DqPhase.kt_units(cur, par):
+            p.other.append((0, u, 0))
+        p.sd(0)
+        p.emit(all_other_first=True)
+    # X(t)
+    p = DqPhase(e)
+    if not first:
+        p.gr(1, par ^ 1)
+    n_gr = len(p.mfma)
+    p.sd(1)
+    p.val(0)
+    if not last:
+        p.add_other(DqPhase.row_units("K", nxt), COST["read"], n_gr + 8)  # after SD(B, t)'s S chains
+        p.tail = DqPhase.row_units("V", nxt)
+    if stage:
+        for u in DqPhase.dq_dma_units(stg, (0, 1)):
+            p.other.append((COST["dma"], u, 2))
+    p.emit(other_frac=1.0)
+    # Y(t)
+    p = DqPhase(e)
+    p.gr(0, par)
+    if not last:
+        p.sd(0)
+        p.add_other(DqPhase.kt_units(nxt, par ^ 1), COST["read"], 0)
+    p.val(1)
+    if stage:
+        for u in DqPhase.dq_dma_units(stg, (2, 3)):
+            p.other.append((COST["dma"], u, 2))
+    p.emit(other_frac=Y_READS)
+    if last:
+        e.op("s_nop 4")
+        p = DqPhase(e)
+        p.gr(1, par)
+        p.emit()
+    e.wait_all()
+    return e.lines
+
+
+def dq_sweep():
+    L = lambda n: f"{n}_%="  # noqa: E731
+    lines = ["s_nop 4", "s_waitcnt lgkmcnt(0)"]
+    lines += dq_body(0, first=True)
+    lines += [f"{L('Lgrp')}:", "s_cmp_eq_u32 %[n], 0", f"s_cbranch_scc1 {L('Lrem')}"]
+    loop = []
+    for t4 in (1, 2, 3, 0):
+        loop += dq_body(t4)
+    lines += loop
+    lines += ["s_sub_u32 %[n], %[n], 1", f"s_branch {L('Lgrp')}", f"{L('Lrem')}:"]
+    for r in range(4):
+        lines += [f"s_cmp_eq_u32 %[rem], {r}", f"s_cbranch_scc1 {L(f'Lr{r}')}"]
+    for r in range(4):
+        lines += [f"{L(f'Lr{r}')}:"]
+        for k in range(r):
+            lines += dq_body(1 + k)
+        t0 = 1 + r
+        lines += dq_body(t0 & 3, stage=False, vm=4) + dq_body((t0 + 1) & 3, stage=False, vm=0)
+        lines += dq_body((t0 + 2) & 3, stage=False, vm=0, last=True)
+        lines += [f"s_branch {L('Ldone')}"]
+    lines += [f"{L('Ldone')}:", "s_nop 15", "s_nop 15"]
+    return lines, loop
+
+
+def stats(name, lines, loop):
+    n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
+    n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_mul", "v_cvt"))) // 4
+    n_ds = sum(1 for l in loop if l.startswith("ds_")) // 4
+    n_wait = sum(1 for l in loop if l.startswith("s_waitcnt lgkm")) // 4
+    n_all = sum(1 for l in loop if not l.startswith(";") and not l.endswith(":")) // 4
+    return (f"{name}: per tile {n_mfma} MFMA, {n_valu} exp/mul/pack VALU, {n_ds} LDS reads, {n_wait} lgkmcnt "
+            f"waits, {n_all} instructions; {len(lines)} asm lines")
+
+
 def main():
+    out = ["// GENERATED by tools/gen_attn_bwd_pipe.py — do not edit by hand."]
+    for name, (lines, loop) in (("SR_ATTN_BWD_PIPE_ASM", sweep()), ("SR_ATTN_BWD_DQ_ASM", dq_sweep())):
+        st = stats(name, lines, loop)
+        print(st)
+        out.append("// " + st)
+        out.append(f"#define {name} \\")
+        out.append(" \\\n".join("  \"" + l + "\\n\\t\"" for l in lines))
+    clob = ", ".join([f'"v{r}"' for r in NAMED_V] + [f'"a{r}"' for r in NAMED_A])
+    out.append("#define SR_ATTN_BWD_PIPE_CLOBBERS " + clob)
+    clob = ", ".join([f'"v{r}"' for r in range(128, 256)] + [f'"a{r}"' for r in range(0, 128)])
+    out.append("#define SR_ATTN_BWD_DQ_CLOBBERS " + clob)
+    with open(OUT, "w") as f:
+        f.write("\n".join(out) + "\n")
+
+
+def main_old():
     lines, loop = sweep()
     n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
     n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_mul", "v_cvt"))) // 4

@@ -681,11 +681,14 @@ def attn_bwd():
         fl = 10.0 * batch * H * lq * lq * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
         # dK/dV sweep: compiled with 32 keys per wave (kb1), or the hand-scheduled asm sweep (pipe);
         # SR_BWD_AB=kb adds the compiled 64-keys-per-wave form
-        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0)), ("pipe", dict(SR_ATTN_BWD_PIPE=1))]
+        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0)),
+                ("pipe", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=0)),
+                ("pipe2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CONC=0)),
+                ("conc", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CONC=1))]
         if os.environ.get("SR_BWD_AB") == "kb":
             arms.append(("kb2", dict(SR_ATTN_BWD_KB=2, SR_ATTN_BWD_PIPE=0)))
-        if os.environ.get("SR_BWD_AB") == "pipe":  # the asm sweep only (A/B of library builds)
-            arms = arms[1:]
+        if os.environ.get("SR_BWD_AB") == "pipe":  # the asm sweeps only (A/B of library builds)
+            arms = arms[2:]
         for arm, sw in arms * 2:
             with ops.tuning(**sw):
                 ms = timeit(f, reps=3 if batch == 1 else 5, warm=1)
