@@ -100,7 +100,11 @@ enum sr_tuning_key {
                                padding; bit-identical)                                  default 1 */
   SR_TUNE_ATTN_BWD_CONC = 22,/* 1: the attention backward's dK/dV sweep on a second (library-owned) stream
                                beside dQ, forked from and joined back to the caller's stream default 0 */
-  SR_TUNE_COUNT = 23
+  SR_TUNE_ATTN_BWD_QSPLIT = 23,/* 1: where keys are shared by a batch > 1, the compiled dK/dV sweep splits
+                               the items in two halves whose partials add atomically into
+                               zero-filled dK / dV (deterministic), when that fills the last
+                               round of workgroups better (2: always)                  default 0 */
+  SR_TUNE_COUNT = 24
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -208,7 +208,10 @@ __device__ __forceinline__ void dkdv_tile(const char* qt, int qv, const bf16x8 (
 }
 
 // dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key key_base + 32 kb, d = 32 db + acc_row(r))
-template <int SEG, int KB>
+// ATOMIC: the sweep covered half of the shared keys' queries (SPLIT2) and adds its partial into
+// zero-filled dK / dV; with exactly two addends into +0 the result is the same whichever lands
+// first (a + b = b + a in fp32), so the outputs stay deterministic.
+template <int SEG, int KB, bool ATOMIC = false>
 __device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb0, int key_base, int len, int hcol,
                                            int hi, const f32x16 (&dk)[KB][2], const f32x16 (&dv)[KB][2]) {
   const float scale = b.f.scale;
@@ -223,10 +226,18 @@ __device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int d0 = db * 32 + 8 * g + 4 * hi;
-          *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * scale, dk[kb][db][4 * g + 1] * scale,
-                                             dk[kb][db][4 * g + 2] * scale, dk[kb][db][4 * g + 3] * scale);
-          *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
-                                             dv[kb][db][4 * g + 3]);
+          if constexpr (ATOMIC) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              unsafeAtomicAdd(dkp + d0 + j, dk[kb][db][4 * g + j] * scale);
+              unsafeAtomicAdd(dvp + d0 + j, dv[kb][db][4 * g + j]);
+            }
+          } else {
+            *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * scale, dk[kb][db][4 * g + 1] * scale,
+                                               dk[kb][db][4 * g + 2] * scale, dk[kb][db][4 * g + 3] * scale);
+            *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
+                                               dv[kb][db][4 * g + 3]);
+          }
         }
     }
   }
@@ -241,7 +252,9 @@ __device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb
 // KB key blocks of 32 per wave (SR_TUNE_ATTN_BWD_KB): KB = 2 runs one wave per SIMD with 64 keys,
 // so every Q / dO fragment read from LDS (row reads for S / dP, transposed reads for dV / dK) feeds
 // two key blocks' MFMAs, and the wave has two independent chain sets to interleave.
-template <int SEG, int KB = 1>
+// SPLIT2 (keys shared across the batch only): blockIdx.z = 0 / 1 sweeps the first / second half of
+// the items and adds its partial dK / dV atomically (store_dkdv<.., true>; the host zero-fills them).
+template <int SEG, int KB = 1, bool SPLIT2 = false>
 __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
@@ -250,7 +263,9 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int head = blockIdx.y, hcol = head * 64;
   const bool shared = (SEG == 0 ? f.k0_bstride : f.k1_bstride) == 0;
-  const int it0 = shared ? 0 : blockIdx.z, it1 = shared ? f.batch : blockIdx.z + 1;
+  const int hb = (f.batch + 1) / 2;
+  const int it0 = shared ? (SPLIT2 ? (int)blockIdx.z * hb : 0) : blockIdx.z;
+  const int it1 = shared ? (SPLIT2 ? min(f.batch, ((int)blockIdx.z + 1) * hb) : f.batch) : blockIdx.z + 1;
   const int len = SEG == 0 ? f.l0 : f.l1;
   const int64_t kb0 = (int64_t)(shared ? 0 : blockIdx.z) * (SEG == 0 ? f.k0_bstride : f.k1_bstride);
   const bf16* kp = (const bf16*)(SEG == 0 ? f.k0 : f.k1);
@@ -357,7 +372,7 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
       ++t;
     }
   }
-  store_dkdv<SEG, KB>(b, kb0, key_base, len, hcol, hi, dk, dv);
+  store_dkdv<SEG, KB, SPLIT2>(b, kb0, key_base, len, hcol, hi, dk, dv);
 }
 
 // ---------------------------------------------------------------- dK, dV: hand-scheduled sweep
@@ -630,13 +645,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
 }
 
 // ---------------------------------------------------------------- dQ: hand-scheduled sweep
-// attn_bwd_dq_kernel's work for one key segment's full key tiles as ONE inline-asm statement
-// (tools/gen_attn_bwd_pipe.py, SR_ATTN_BWD_DQ_ASM): one wave per SIMD, 64 queries per wave (two
-// query blocks sharing every K / V fragment read), 256 per workgroup, the two blocks pipelined
-// half a tile apart like the dK/dV sweep.  A ragged last key tile (l0 % 64) is staged up front
-// into a fifth LDS stage and run afterwards with the compiled dq_tile, so every dQ accumulation
-// happens in the compiled kernel's order (bit-identical outputs).  The host picks this kernel for
-// one key segment (l1 == 0) of at least 4 full key tiles.
+// attn_bwd_dq_kernel's work as ONE inline-asm statement per key segment (tools/gen_attn_bwd_pipe.py,
+// SR_ATTN_BWD_DQ_ASM): one wave per SIMD, 64 queries per wave (two query blocks sharing every K / V
+// fragment read), 256 per workgroup, the two blocks pipelined half a tile apart like the dK/dV
+// sweep.  Per segment: its first three tiles and its ragged last tile (l % 64 rows, into a fifth LDS
+// stage) are staged, the asm sweeps the full tiles, then the compiled dq_tile runs the ragged one.
+// Segment 1 follows segment 0 after a barrier.  Every dQ accumulation therefore happens in the
+// compiled kernel's order (segment 0's tiles, its ragged tile, segment 1's ...): bit-identical
+// outputs.  The host picks this kernel when every segment has at least 4 full key tiles.
 //   LDS: ring of 4 x (K tile | V tile) at 0 .. 64 KB, the ragged stage after it.
 __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_desc b) {
   constexpr int SLOT = 2 * TB, RAG = 4 * SLOT;
@@ -647,26 +663,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_de
   const int head = blockIdx.y, hcol = head * 64, item = blockIdx.z;
   const int q0 = blockIdx.x * 256 + wave * 64;  // queries of block qb: q0 + 32 qb + l32
   const float c = f.scale * 1.4426950408889634f;
-  const int nfull = f.l0 / 64, kv = f.l0 % 64;  // nfull >= 4 (host)
-
-  // staging: wave w copies row groups 4 (w & 1) .. + 3 of the K (waves 0, 1) or V (2, 3) tile
   const uint32_t lds0 = sr::lds_addr(smem);
-  const bool stage_v = wave_u >= 2;
-  const int64_t sld = stage_v ? f.ldv0 : f.ldk0;
-  const bf16* const sb0 = (const bf16*)(stage_v ? f.v0 : f.k0) + (int64_t)item * f.k0_bstride * sld + hcol;
+  const bool stage_v = wave_u >= 2;  // wave w copies row groups 4 (w & 1) .. + 3 of the K (waves 0, 1) or V (2, 3) tile
   const int g0 = 4 * (wave_u & 1);
-  const uint32_t offA = piece_off(sld, 0, lane), offB = piece_off(sld, 1, lane);
   const uint32_t ldsv = __builtin_amdgcn_readfirstlane(lds0 + (stage_v ? TB : 0) + g0 * 1024);
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const char* p = (const char*)(sb0 + (int64_t)(t * 64 + 8 * g0) * sld);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sr::dma16_s(p + (int64_t)8 * i * sld * 2, (i & 1) ? offB : offA, ldsv + t * SLOT + i * 1024);
-  }
-  if (kv) {  // the ragged last key tile: rows clamped to l0 - 1 (P = 0 for them: dq_tile<true>)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dma_rows(sb0, sld, nfull * 64, f.l0, g0 + i, lane, lds0 + RAG + (stage_v ? TB : 0));
-  }
 
   bf16x8 qf[2][4], of[2][4];
   float lse[2], dlt[2];
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_de
     lse[qb] = f.lse[lrow];
     dlt[qb] = b.delta[lrow];
   }
-  __builtin_amdgcn_s_waitcnt(0);  // the fragments and the prologue stages
+  __builtin_amdgcn_s_waitcnt(0);
   f32x16 nl[2], nd[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -701,36 +701,57 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_de
   f32x16 dq[2][2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) dq[0][0][i] = dq[0][1][i] = dq[1][0][i] = dq[1][1][i] = 0.f;
-
   uint32_t ra[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) ra[s] = lds0 + l32 * 128 + swz(l32, 2 * s + hi) * 16;
   const uint32_t ta00 = lds0 + tro.off[0][0], ta01 = lds0 + tro.off[0][1];
   const uint32_t ta10 = lds0 + tro.off[1][0], ta11 = lds0 + tro.off[1][1];
-  const uint64_t spu = (uint64_t)(uintptr_t)(sb0 + (int64_t)(3 * 64 + 8 * g0) * sld);
-  const uint32_t sp_lo = __builtin_amdgcn_readfirstlane((uint32_t)spu);
-  const uint32_t sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(spu >> 32));
-  const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
-  const char* spb2 = spb + 16 * sld * 2;
-  uint32_t dma0 = offA, dma1 = offB + (uint32_t)(8 * sld * 2);
-  const uint32_t sstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * sld * 2));
-  int nn = __builtin_amdgcn_readfirstlane((nfull - 4) >> 2);
-  const int rem = __builtin_amdgcn_readfirstlane((nfull - 4) & 3);
-  asm volatile(SR_ATTN_BWD_DQ_ASM
-               : [dq00] "+&a"(dq[0][0]), [dq01] "+&a"(dq[0][1]), [dq10] "+&a"(dq[1][0]), [dq11] "+&a"(dq[1][1]),
-                 [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [n] "+&s"(nn)
-               : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
-                 [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
-                 [o00] "a"(of[0][0]), [o01] "a"(of[0][1]), [o02] "a"(of[0][2]), [o03] "a"(of[0][3]),
-                 [o10] "a"(of[1][0]), [o11] "a"(of[1][1]), [o12] "a"(of[1][2]), [o13] "a"(of[1][3]),
-                 [nl0] "v"(nl[0]), [nl1] "v"(nl[1]), [nd0] "v"(nd[0]), [nd1] "v"(nd[1]),
-                 [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
-                 [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11),
-                 [ldsv] "s"(ldsv), [sp] "s"(spb), [sp2] "s"(spb2), [sstep] "s"(sstep), [rem] "s"(rem)
-               : SR_ATTN_BWD_DQ_CLOBBERS, "memory", "m0", "scc");
-  if (kv) {
+
+  const int nseg = f.l1 > 0 ? 2 : 1;
+  for (int seg = 0; seg < nseg; ++seg) {
+    if (seg) __syncthreads();  // every wave is done with segment 0's ring and ragged stage
+    const int len = seg ? f.l1 : f.l0;
+    const int nfull = len / 64, kv = len % 64;  // nfull >= 4 (host)
+    const int64_t sld = stage_v ? (seg ? f.ldv1 : f.ldv0) : (seg ? f.ldk1 : f.ldk0);
+    const void* kvp = stage_v ? (seg ? f.v1 : f.v0) : (seg ? f.k1 : f.k0);
+    const bf16* const sb = (const bf16*)kvp + (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride) * sld + hcol;
+    const uint32_t offA = piece_off(sld, 0, lane), offB = piece_off(sld, 1, lane);
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) dq_tile<true>(smem + RAG, kv, qf[qb], of[qb], nl[qb], nd[qb], dq[qb], tro, l32, hi);
+    for (int t = 0; t < 3; ++t) {
+      const char* p = (const char*)(sb + (int64_t)(t * 64 + 8 * g0) * sld);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sr::dma16_s(p + (int64_t)8 * i * sld * 2, (i & 1) ? offB : offA, ldsv + t * SLOT + i * 1024);
+    }
+    if (kv) {  // the ragged last key tile: rows clamped to len - 1 (P = 0 for them: dq_tile<true>)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma_rows(sb, sld, nfull * 64, len, g0 + i, lane, lds0 + RAG + (stage_v ? TB : 0));
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the prologue stages
+    const uint64_t spu = (uint64_t)(uintptr_t)(sb + (int64_t)(3 * 64 + 8 * g0) * sld);
+    const uint32_t sp_lo = __builtin_amdgcn_readfirstlane((uint32_t)spu);
+    const uint32_t sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(spu >> 32));
+    const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
+    const char* spb2 = spb + 16 * sld * 2;
+    uint32_t dma0 = offA, dma1 = offB + (uint32_t)(8 * sld * 2);
+    const uint32_t sstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * sld * 2));
+    int nn = __builtin_amdgcn_readfirstlane((nfull - 4) >> 2);
+    const int rem = __builtin_amdgcn_readfirstlane((nfull - 4) & 3);
+    asm volatile(SR_ATTN_BWD_DQ_ASM
+                 : [dq00] "+&a"(dq[0][0]), [dq01] "+&a"(dq[0][1]), [dq10] "+&a"(dq[1][0]), [dq11] "+&a"(dq[1][1]),
+                   [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [n] "+&s"(nn)
+                 : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
+                   [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
+                   [o00] "a"(of[0][0]), [o01] "a"(of[0][1]), [o02] "a"(of[0][2]), [o03] "a"(of[0][3]),
+                   [o10] "a"(of[1][0]), [o11] "a"(of[1][1]), [o12] "a"(of[1][2]), [o13] "a"(of[1][3]),
+                   [nl0] "v"(nl[0]), [nl1] "v"(nl[1]), [nd0] "v"(nd[0]), [nd1] "v"(nd[1]),
+                   [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
+                   [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11),
+                   [ldsv] "s"(ldsv), [sp] "s"(spb), [sp2] "s"(spb2), [sstep] "s"(sstep), [rem] "s"(rem)
+                 : SR_ATTN_BWD_DQ_CLOBBERS, "memory", "m0", "scc");
+    if (kv) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) dq_tile<true>(smem + RAG, kv, qf[qb], of[qb], nl[qb], nd[qb], dq[qb], tro, l32, hi);
+    }
   }
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -792,13 +813,14 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   const int64_t nrows = (int64_t)f.batch * f.heads * f.lq;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
-  // dQ: the hand-scheduled sweep (SR_ATTN_BWD_DQ_PIPE) over one key segment of at least 4 full
-  // tiles with 32-bit per-lane DMA offsets, where its 256-query workgroups pad the query count by
+  // dQ: the hand-scheduled sweep (SR_ATTN_BWD_DQ_PIPE) where every key segment has at least 4 full
+  // tiles and 32-bit per-lane DMA offsets, and where its 256-query workgroups pad the query count by
   // at most 2 % more than the compiled sweep's 128 (frames of 1,374 tokens: 1,536 against 1,408
   // rows, measured 1-3 % slower); else the compiled sweep
   const int64_t qpad256 = (f.lq + 255) / 256 * 256, qpad128 = (f.lq + 127) / 128 * 128;
-  const bool dq_pipe = sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) != 0 && f.l1 == 0 && f.l0 >= 256 &&
+  const bool dq_pipe = sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) != 0 && f.l0 >= 256 && (f.l1 == 0 || f.l1 >= 256) &&
                        (int64_t)(f.l0 + 64) * std::max<int64_t>(f.ldk0, f.ldv0) * 2 < ((int64_t)1 << 31) &&
+                       (f.l1 == 0 || (int64_t)(f.l1 + 64) * std::max<int64_t>(f.ldk1, f.ldv1) * 2 < ((int64_t)1 << 31)) &&
                        (sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) == 2 || qpad256 * 100 <= qpad128 * 102);
   if (dq_pipe)
     hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
@@ -829,7 +851,27 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
       if (seg == 0) name = "attn_bwd_dkdv_pipe_kernel<0>";
       continue;
     }
-    const dim3 g((len + kr - 1) / kr, f.heads, nz);
+    // keys shared by a batch > 1: one workgroup sweeps every item's queries, so the launch is only
+    // len/128 x heads workgroups; with SR_ATTN_BWD_QSPLIT the items split in two halves whose
+    // partials add atomically (deterministic: two addends into zeros) where that raises the
+    // filled fraction of the last round of workgroups
+    const int wg = (len + kr - 1) / kr * f.heads, slots = 2 * 256 / (kb2 ? 2 : 1);
+    auto fill = [&](int n) { const int r = (n + slots - 1) / slots; return (double)n / (r * slots); };
+    const int qsplit = sr::tune(SR_TUNE_ATTN_BWD_QSPLIT);
+    const bool split2 = shared && f.batch > 1 && !kb2 && qsplit != 0 && (qsplit == 2 || fill(2 * wg) > fill(wg) + 0.05);
+    const dim3 g((len + kr - 1) / kr, f.heads, split2 ? 2 : nz);
+    if (split2) {
+      float* dkz = seg == 0 ? b.dk0 : b.dk1;
+      float* dvz = seg == 0 ? b.dv0 : b.dv1;
+      const int64_t lddk = seg == 0 ? b.lddk0 : b.lddk1, lddv = seg == 0 ? b.lddv0 : b.lddv1;
+      SR_CHECK(hipMemset2DAsync(dkz, lddk * 4, 0, (size_t)f.heads * 64 * 4, len, ks) == hipSuccess &&
+                   hipMemset2DAsync(dvz, lddv * 4, 0, (size_t)f.heads * 64 * 4, len, ks) == hipSuccess,
+               SR_ELAUNCH, "sr_attention_bwd: zero-filling dK / dV failed");
+      if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1, true>), g, dim3(256), 0, ks, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1, true>), g, dim3(256), 0, ks, b);
+      if (seg == 0) name = "attn_bwd_dkdv_kernel<0, 1, split2>";
+      continue;
+    }
     if (seg == 0) {
       if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g, dim3(256), 0, ks, b);
       else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g, dim3(256), 0, ks, b);

@@ -208,3 +208,39 @@ def test_attention_bwd_pipe(case, P):
     for a, b in zip(*outs):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+
+
+def test_attention_bwd_shared_key_split():
+    """SR_ATTN_BWD_QSPLIT: anchors shared by a batch of 3 (the reloc block's segment 0): the dK/dV
+    sweep over the items in two halves adding atomically into zero-filled outputs equals the one-pass
+    sweep to fp32 summation order, and is deterministic (two addends into zeros)."""
+    from sailrecon_amd import ops
+    torch.manual_seed(3)
+    H, D, B, P, A = 4, 64, 3, 300, 301
+    C = H * D
+    kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, l1=P, k1_bstride=P)
+    x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
+    q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+    ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
+    k0, v0 = ka[:, :C], ka[:, C:]
+    kw.update(k1=k, v1=v)
+    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, P, device=DEV)
+    ops.attention(q, k0, v0, o, heads=H, head_dim=D, lse=lse, **kw)
+    g = torch.randn(B * P, C, device=DEV).bfloat16()
+    outs = []
+    for split in (0, 2, 2):
+        dq = torch.empty(B * P, C, device=DEV)
+        dk0 = torch.full((A, C), float("nan"), device=DEV)
+        dv0 = torch.full((A, C), float("nan"), device=DEV)
+        dk1, dv1 = torch.empty(B * P, C, device=DEV), torch.empty(B * P, C, device=DEV)
+        delta = torch.empty(B, H, P, device=DEV)
+        with ops.tuning(SR_ATTN_BWD_QSPLIT=split):
+            ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
+            assert ops.last_kernel() == ("attn_bwd_dkdv_kernel<0, 1, split2>" if split else "attn_bwd_dkdv_kernel<0, 1>")
+        outs.append((dq, dk0, dv0, dk1, dv1))
+    torch.cuda.synchronize()
+    for a, b, c in zip(*outs):
+        assert torch.isfinite(b).all()
+        assert torch.equal(b, c)  # deterministic
+        assert (a - b).abs().max() <= 1e-5 * a.abs().max()  # summation order only

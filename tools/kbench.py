@@ -662,29 +662,49 @@ def attn_fp8():
 
 
 def attn_bwd():
-    """Attention backward at the training shapes (C4: 16 anchors -> global L = 21984; frames)."""
+    """Attention backward at the training shapes (C4: 16 anchors -> global L = 21984; frames; the
+    reloc block: 16 query frames against SR_BWD_RELOC_ANCHORS shared anchor keys + their own frame)."""
     C, H, D, P = 1024, 16, 64, 1374
-    for name, rows, batch, lq in (("global L=21984", 16 * P, 1, 16 * P), ("frame 32x1374", 32 * P, 32, P)):
+    na = int(os.environ.get("SR_BWD_RELOC_ANCHORS", "9984"))
+    shapes = [("global L=21984", 16 * P, 1, 16 * P, 0), ("frame 32x1374", 32 * P, 32, P, 0)]
+    if os.environ.get("SR_BWD_RELOC", "1") != "0":
+        shapes.append((f"reloc 16x{P}+{na}", 16 * P, 16, P, na))
+    for name, rows, batch, lq, anchors in shapes:
         qkv = torch.randn(rows, 3 * C, device=DEV, dtype=torch.bfloat16)
         o = torch.empty(rows, C, device=DEV, dtype=torch.bfloat16)
         lse = torch.empty(batch, H, lq, device=DEV)
         kb = 0 if batch == 1 else lq
-        ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D, batch=batch, lq=lq,
-                      q_bstride=lq, l0=lq, k0_bstride=kb, lse=lse)
+        if anchors:  # segment 0: anchor keys shared by every item; segment 1: the item's own frame
+            akv = torch.randn(anchors, 2 * C, device=DEV, dtype=torch.bfloat16)
+            seg = dict(k0=akv[:, :C], v0=akv[:, C:], l0=anchors, k0_bstride=0, l1=lq, k1_bstride=lq)
+            dka = torch.empty(anchors, 2 * C, device=DEV)
+        else:
+            seg = dict(k0=qkv[:, C:2 * C], v0=qkv[:, 2 * C:], l0=lq, k0_bstride=kb)
+        fwd_kw = dict(seg)
+        k0, v0 = fwd_kw.pop("k0"), fwd_kw.pop("v0")
+        if anchors:
+            fwd_kw.update(k1=qkv[:, C:2 * C], v1=qkv[:, 2 * C:])
+        ops.attention(qkv[:, :C], k0, v0, o, heads=H, head_dim=D, batch=batch, lq=lq, q_bstride=lq, lse=lse,
+                      **fwd_kw)
         g = torch.randn(rows, C, device=DEV, dtype=torch.bfloat16)
         d = torch.empty(rows, 3 * C, device=DEV)
         delta = torch.empty(batch * H * lq, device=DEV)
 
         def f():
-            ops.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, lse, g, d[:, :C], d[:, C:2 * C],
-                              d[:, 2 * C:], delta, heads=H, batch=batch, lq=lq, q_bstride=lq, l0=lq, k0_bstride=kb)
-        fl = 10.0 * batch * H * lq * lq * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
+            if anchors:
+                ops.attention_bwd(qkv[:, :C], k0, v0, o, lse, g, d[:, :C], dka[:, :C], dka[:, C:], delta, heads=H,
+                                  batch=batch, lq=lq, q_bstride=lq, dk1=d[:, C:2 * C], dv1=d[:, 2 * C:], **fwd_kw)
+            else:
+                ops.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, lse, g, d[:, :C], d[:, C:2 * C],
+                                  d[:, 2 * C:], delta, heads=H, batch=batch, lq=lq, q_bstride=lq, l0=lq, k0_bstride=kb)
+        fl = 10.0 * batch * H * lq * (lq + anchors) * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
         # dK/dV sweep: compiled with 32 keys per wave (kb1), or the hand-scheduled asm sweep (pipe);
         # SR_BWD_AB=kb adds the compiled 64-keys-per-wave form
-        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0)),
+        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0, SR_ATTN_BWD_QSPLIT=0)),
                 ("pipe", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=0)),
                 ("pipe2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CONC=0)),
-                ("conc", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CONC=1))]
+                ("dq2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=2, SR_ATTN_BWD_CONC=0)),
+                ("split", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_QSPLIT=1))]
         if os.environ.get("SR_BWD_AB") == "kb":
             arms.append(("kb2", dict(SR_ATTN_BWD_KB=2, SR_ATTN_BWD_PIPE=0)))
         if os.environ.get("SR_BWD_AB") == "pipe":  # the asm sweeps only (A/B of library builds)
