@@ -96,8 +96,8 @@ enum sr_tuning_key {
                                bit-identical)                                           default 1 */
   SR_TUNE_ATTN_BWD_DQ_PIPE = 21,/* 1: the attention backward's dQ sweep as the hand-scheduled asm pipeline
                                (one wave per SIMD, 64 queries; one key segment of >= 4 full
-                               tiles, query padding within 2 % of the compiled sweep's; 2: any
-                               padding; bit-identical)                                  default 1 */
+                               tiles, query padding within 2 % of the compiled sweep's or
+                               >= 4,096 keys; 2: always; bit-identical)                default 1 */
   SR_TUNE_ATTN_BWD_CONC = 22,/* 1: the attention backward's dK/dV sweep on a second (library-owned) stream
                                beside dQ, forked from and joined back to the caller's stream default 0 */
   SR_TUNE_ATTN_BWD_QSPLIT = 23,/* 1: where keys are shared by a batch > 1, the compiled dK/dV sweep splits

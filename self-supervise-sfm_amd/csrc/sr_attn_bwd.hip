@@ -815,13 +815,16 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
                      dim3(256), 0, s, b);
   // dQ: the hand-scheduled sweep (SR_ATTN_BWD_DQ_PIPE) where every key segment has at least 4 full
   // tiles and 32-bit per-lane DMA offsets, and where its 256-query workgroups pad the query count by
-  // at most 2 % more than the compiled sweep's 128 (frames of 1,374 tokens: 1,536 against 1,408
-  // rows, measured 1-3 % slower); else the compiled sweep
+  // at most 2 % more than the compiled sweep's 128 or the key sweep is long enough to carry the
+  // padding (frames of 1,374 tokens: 1,536 against 1,408 rows over 1,374 keys, measured 1-3 %
+  // slower, forced 16 % slower; the reloc block's 1,374-row items over 9,984 + 1,374 keys: 3 %
+  // faster, profiles/r05_j22_kbwd.log); else the compiled sweep
   const int64_t qpad256 = (f.lq + 255) / 256 * 256, qpad128 = (f.lq + 127) / 128 * 128;
   const bool dq_pipe = sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) != 0 && f.l0 >= 256 && (f.l1 == 0 || f.l1 >= 256) &&
                        (int64_t)(f.l0 + 64) * std::max<int64_t>(f.ldk0, f.ldv0) * 2 < ((int64_t)1 << 31) &&
                        (f.l1 == 0 || (int64_t)(f.l1 + 64) * std::max<int64_t>(f.ldk1, f.ldv1) * 2 < ((int64_t)1 << 31)) &&
-                       (sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) == 2 || qpad256 * 100 <= qpad128 * 102);
+                       (sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) == 2 || qpad256 * 100 <= qpad128 * 102 ||
+                        (int64_t)f.l0 + f.l1 >= 4096);
   if (dq_pipe)
     hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
   else

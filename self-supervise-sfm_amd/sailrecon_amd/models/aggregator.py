@@ -720,11 +720,20 @@ class Aggregator(nn.Module):
             for i, (kv, p) in enumerate(plan):
                 if i == 1:
                     _wait(work_kv)  # the remote anchors' K/V
-                ops.attention_partials(q, kv[:, 0:C], kv[:, C:2 * C], o_parts[p0 * lq:(p0 + p) * lq],
-                                       lse_parts[p0:p0 + p], heads=H, head_dim=D, lq=lq, l0=kv.shape[0], parts=p,
-                                       tag="attn_global", key_norm_max=kb, query_norm_max=qb,
-                                       tail_readable=_SHARD_TAIL, q_scaled=_qs(pg))
-                p0 += p
+                n = kv.shape[0]
+                # SR_SHARD_ALIGN: the first p-1 chunks hold whole 64-key tiles (the hand-scheduled
+                # sweep takes them), the last one the rest (1,374-row frames never split into
+                # 64-multiples evenly); two launches into the same stacked partials
+                c = (n + p * 64 - 1) // (p * 64) * 64
+                pieces = [(0, n, p)]
+                if _SHARD_ALIGN and p > 1 and n % (p * 64) and n - (p - 1) * c > 0:
+                    pieces = [(0, (p - 1) * c, p - 1), ((p - 1) * c, n - (p - 1) * c, 1)]
+                for a, m, pp in pieces:
+                    ops.attention_partials(q, kv[a:a + m, 0:C], kv[a:a + m, C:2 * C],
+                                           o_parts[p0 * lq:(p0 + pp) * lq], lse_parts[p0:p0 + pp], heads=H,
+                                           head_dim=D, lq=lq, l0=m, parts=pp, tag="attn_global", key_norm_max=kb,
+                                           query_norm_max=qb, tail_readable=_SHARD_TAIL, q_scaled=_qs(pg))
+                    p0 += pp
             ops.attn_merge_n(o_parts, lse_parts, o, parts=total, rows=lq, heads=H, head_dim=D)
             return
         ws = self._ws
@@ -830,6 +839,10 @@ class Aggregator(nn.Module):
 # hand-scheduled sweep's ragged variant (round 3 measured it level with the compiled sweep per rank:
 # DESIGN.md section 5)
 _SHARD_TAIL = os.environ.get("SR_SHARD_TAIL", "0") == "1"
+# SR_SHARD_ALIGN (A/B switch): the frame-sharded global block's key-split passes cut their keys into
+# p-1 chunks of whole 64-key tiles plus one remainder chunk instead of p equal chunks, so that p-1
+# of them run on the hand-scheduled sweep (an equal split of 1,374-row frames is never tile-aligned)
+_SHARD_ALIGN = os.environ.get("SR_SHARD_ALIGN", "0") == "1"
 # SR_SHARD_CONCURRENT (default 1; 0 for the A/B): under frame sharding with grouped tails, the reloc
 # attention on a second stream beside the global attention.  Rank-0 rehearsal, one box, 2 runs each
 # (profiles/r05_j10_rs_*.log): G = 8 69.03 / 69.15 -> 66.87 / 66.98 ms, G = 4 121.8 / 121.0 -> 120.9 /
