@@ -104,7 +104,10 @@ enum sr_tuning_key {
                                the items in two halves whose partials add atomically into
                                zero-filled dK / dV (deterministic), when that fills the last
                                round of workgroups better (2: always)                  default 0 */
-  SR_TUNE_COUNT = 24
+  SR_TUNE_ATTN_BWD_CAT = 24,/* 1: keys shared by a batch > 1 whose items' queries are consecutive rows:
+                               the dK/dV asm sweep over the concatenated queries (one sequence of
+                               batch * lq rows; same sum, other tile grouping)          default 0 */
+  SR_TUNE_COUNT = 25
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

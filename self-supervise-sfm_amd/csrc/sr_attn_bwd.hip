@@ -386,14 +386,18 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
 // per workgroup (keys not shared across the batch) and at least 4 full query tiles.
 //   LDS: ring of 4 x (Q tile | dO tile) at 0 .. 64 KB, the ring's lse | -delta at 64 KB + 512 s,
 //        the ragged stage (Q | dO | lse | -delta) after them.
-template <int SEG>
+// CAT: keys shared by a batch > 1 whose items' queries are consecutive rows (q_bstride == lq): the
+// items run as ONE query sequence of batch * lq rows (64-row tiles straddle items; a row's lse /
+// -delta sit at (b H + h) lq + i, formed per tile in the asm, SR_ATTN_BWD_PIPE_ASM_CAT).  The sum
+// over queries is the same, grouped into other tiles than the compiled kernel's per-item sweep.
+template <int SEG, bool CAT = false>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_kernel(sr_attn_bwd_desc b) {
   constexpr int SLOT = 2 * TB, LSE0 = 4 * SLOT, RAG = LSE0 + 4 * 512;
   __shared__ __attribute__((aligned(16))) char smem[RAG + 2 * TB + 512];
   const sr_attn_desc& f = b.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int head = blockIdx.y, hcol = head * 64, item = blockIdx.z;
+  const int head = blockIdx.y, hcol = head * 64, item = CAT ? 0 : blockIdx.z;
   const int len = SEG == 0 ? f.l0 : f.l1;
   const int64_t kb0 = (int64_t)item * (SEG == 0 ? f.k0_bstride : f.k1_bstride);
   const bf16* kp = (const bf16*)(SEG == 0 ? f.k0 : f.k1);
@@ -401,7 +405,24 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_kernel(sr_attn_bwd_
   const int64_t ldk = SEG == 0 ? f.ldk0 : f.ldk1, ldv = SEG == 0 ? f.ldv0 : f.ldv1;
   const int key_base = blockIdx.x * 256 + wave * 64 + l32;  // key of block kb: + 32 kb
   const float c = f.scale * 1.4426950408889634f;
-  const int nfull = f.lq / 64, qv = f.lq % 64;  // nfull >= 4 (host)
+  const int lqt = CAT ? f.batch * f.lq : f.lq;  // the swept query rows
+  const int nfull = lqt / 64, qv = lqt % 64;  // nfull >= 4 (host)
+  // CAT: row r's lse / -delta float offset from the head's item-0 base, r + (r / lq) (H-1) lq, with
+  // r / lq = mulhi(r, msh_m) >> msh (exact for r < 2^24: M lq - 2^(32+s) < lq < 2^(s+1))
+  int msh = 0;
+  uint32_t mgc = 0;
+  if constexpr (CAT) {
+    msh = 31 - __builtin_clz((uint32_t)f.lq);
+    if ((1 << msh) == f.lq) --msh;
+    mgc = (uint32_t)(((1ull << (32 + msh)) + (uint64_t)f.lq - 1) / (uint64_t)f.lq);
+    msh = __builtin_amdgcn_readfirstlane(msh);
+    mgc = __builtin_amdgcn_readfirstlane(mgc);
+  }
+  const uint32_t istr = __builtin_amdgcn_readfirstlane((uint32_t)((f.heads - 1) * f.lq * 4));
+  auto loff = [&](int r) -> uint32_t {  // CAT: bytes from the head's base to row r's lse
+    const uint32_t bi = __umulhi((uint32_t)r, mgc) >> msh;
+    return (uint32_t)r * 4 + bi * istr;
+  };
 
   // staging: wave w copies row groups 4 (w & 1) .. + 3 of the Q (waves 0, 1) or dO (2, 3) tile and
   // the tile's 64 lse (waves 0, 2) or -delta (1, 3) values: five DMA wave-instructions per tile and
@@ -420,12 +441,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_kernel(sr_attn_bwd_
     const char* p = (const char*)(tbase + (int64_t)(t * 64 + 8 * g0) * sld);
 #pragma unroll
     for (int i = 0; i < 4; ++i) sr::dma16_s(p + (int64_t)8 * i * sld * 2, (i & 1) ? offB : offA, ldsv + t * SLOT + i * 1024);
-    sr::dma4_s(lbase + t * 64, (uint32_t)lane * 4, ldsl + t * 512);
+    if constexpr (CAT) sr::dma4((const char*)lbase + loff(t * 64 + lane), ldsl + t * 512);
+    else sr::dma4_s(lbase + t * 64, (uint32_t)lane * 4, ldsl + t * 512);
   }
-  if (qv) {  // the ragged last tile: rows clamped to lq - 1 (P = 0 for them: dkdv_tile<.., true>)
+  if (qv) {  // the ragged last tile: rows clamped to the last row (P = 0 for them: dkdv_tile<.., true>)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma_rows(tbase, sld, nfull * 64, f.lq, g0 + i, lane, lds0 + RAG + (stage_o ? TB : 0));
-    sr::dma4(lbase + min(nfull * 64 + lane, f.lq - 1), lds0 + RAG + 2 * TB + (wave_u & 1) * 256);
+    for (int i = 0; i < 4; ++i) dma_rows(tbase, sld, nfull * 64, lqt, g0 + i, lane, lds0 + RAG + (stage_o ? TB : 0));
+    const int rl = min(nfull * 64 + lane, lqt - 1);
+    if constexpr (CAT) sr::dma4((const char*)lbase + loff(rl), lds0 + RAG + 2 * TB + (wave_u & 1) * 256);
+    else sr::dma4(lbase + rl, lds0 + RAG + 2 * TB + (wave_u & 1) * 256);
   }
 
   bf16x8 kf[2][4], vf[2][4];
@@ -466,27 +490,45 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_kernel(sr_attn_bwd_
   const uint32_t sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(spu >> 32));
   const char* spb = (const char*)(uintptr_t)(((uint64_t)sp_hi << 32) | sp_lo);
   const char* spb2 = spb + 16 * sld * 2;
-  const uint64_t lpu = (uint64_t)(uintptr_t)(lbase + 3 * 64);
+  const uint64_t lpu = (uint64_t)(uintptr_t)(lbase + (CAT ? 0 : 3 * 64));
   const uint32_t lp_lo = __builtin_amdgcn_readfirstlane((uint32_t)lpu);
   const uint32_t lp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lpu >> 32));
   const char* lpb = (const char*)(uintptr_t)(((uint64_t)lp_hi << 32) | lp_lo);
-  uint32_t dma0 = offA, dma1 = offB + (uint32_t)(8 * sld * 2), lofs = (uint32_t)lane * 4;
+  uint32_t dma0 = offA, dma1 = offB + (uint32_t)(8 * sld * 2), lofs = CAT ? loff(3 * 64 + lane) : (uint32_t)lane * 4;
   const uint32_t sstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * sld * 2));
   int nn = __builtin_amdgcn_readfirstlane((nfull - 4) >> 2);
   const int rem = __builtin_amdgcn_readfirstlane((nfull - 4) & 3);
-  asm volatile(SR_ATTN_BWD_PIPE_ASM
-               : [dk00] "+&a"(dk[0][0]), [dk01] "+&a"(dk[0][1]), [dk10] "+&a"(dk[1][0]), [dk11] "+&a"(dk[1][1]),
-                 [dv00] "+&a"(dv[0][0]), [dv01] "+&a"(dv[0][1]), [dv10] "+&a"(dv[1][0]), [dv11] "+&a"(dv[1][1]),
-                 [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [lofs] "+&v"(lofs), [n] "+&s"(nn)
-               : [k00] "v"(kf[0][0]), [k01] "v"(kf[0][1]), [k02] "v"(kf[0][2]), [k03] "v"(kf[0][3]),
-                 [k10] "v"(kf[1][0]), [k11] "v"(kf[1][1]), [k12] "v"(kf[1][2]), [k13] "v"(kf[1][3]),
-                 [v00] "v"(vf[0][0]), [v01] "v"(vf[0][1]), [v02] "v"(vf[0][2]), [v03] "v"(vf[0][3]),
-                 [v10] "v"(vf[1][0]), [v11] "v"(vf[1][1]), [v12] "v"(vf[1][2]), [v13] "v"(vf[1][3]),
-                 [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
-                 [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11), [sa] "v"(sa),
-                 [ldsv] "s"(ldsv), [ldsl] "s"(ldsl), [sp] "s"(spb), [sp2] "s"(spb2), [lp] "s"(lpb),
-                 [sstep] "s"(sstep), [rem] "s"(rem)
-               : SR_ATTN_BWD_PIPE_CLOBBERS, "memory", "m0", "scc");
+  if constexpr (CAT) {
+    uint32_t rrow = 3 * 64 + lane, tmp;
+    asm volatile(SR_ATTN_BWD_PIPE_ASM_CAT
+                 : [dk00] "+&a"(dk[0][0]), [dk01] "+&a"(dk[0][1]), [dk10] "+&a"(dk[1][0]), [dk11] "+&a"(dk[1][1]),
+                   [dv00] "+&a"(dv[0][0]), [dv01] "+&a"(dv[0][1]), [dv10] "+&a"(dv[1][0]), [dv11] "+&a"(dv[1][1]),
+                   [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [lofs] "+&v"(lofs), [n] "+&s"(nn),
+                     [rrow] "+&v"(rrow), [tmp] "=&v"(tmp)
+                 : [k00] "v"(kf[0][0]), [k01] "v"(kf[0][1]), [k02] "v"(kf[0][2]), [k03] "v"(kf[0][3]),
+                   [k10] "v"(kf[1][0]), [k11] "v"(kf[1][1]), [k12] "v"(kf[1][2]), [k13] "v"(kf[1][3]),
+                   [v00] "v"(vf[0][0]), [v01] "v"(vf[0][1]), [v02] "v"(vf[0][2]), [v03] "v"(vf[0][3]),
+                   [v10] "v"(vf[1][0]), [v11] "v"(vf[1][1]), [v12] "v"(vf[1][2]), [v13] "v"(vf[1][3]),
+                   [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
+                   [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11), [sa] "v"(sa),
+                   [ldsv] "s"(ldsv), [ldsl] "s"(ldsl), [sp] "s"(spb), [sp2] "s"(spb2), [lp] "s"(lpb),
+                   [sstep] "s"(sstep), [rem] "s"(rem), [mgc] "s"(mgc), [msh] "s"(msh), [istr] "s"(istr)
+                 : SR_ATTN_BWD_PIPE_CLOBBERS, "memory", "m0", "scc");
+  } else {
+    asm volatile(SR_ATTN_BWD_PIPE_ASM
+                 : [dk00] "+&a"(dk[0][0]), [dk01] "+&a"(dk[0][1]), [dk10] "+&a"(dk[1][0]), [dk11] "+&a"(dk[1][1]),
+                   [dv00] "+&a"(dv[0][0]), [dv01] "+&a"(dv[0][1]), [dv10] "+&a"(dv[1][0]), [dv11] "+&a"(dv[1][1]),
+                   [dma0] "+&v"(dma0), [dma1] "+&v"(dma1), [lofs] "+&v"(lofs), [n] "+&s"(nn)
+                 : [k00] "v"(kf[0][0]), [k01] "v"(kf[0][1]), [k02] "v"(kf[0][2]), [k03] "v"(kf[0][3]),
+                   [k10] "v"(kf[1][0]), [k11] "v"(kf[1][1]), [k12] "v"(kf[1][2]), [k13] "v"(kf[1][3]),
+                   [v00] "v"(vf[0][0]), [v01] "v"(vf[0][1]), [v02] "v"(vf[0][2]), [v03] "v"(vf[0][3]),
+                   [v10] "v"(vf[1][0]), [v11] "v"(vf[1][1]), [v12] "v"(vf[1][2]), [v13] "v"(vf[1][3]),
+                   [ra0] "v"(ra[0]), [ra1] "v"(ra[1]), [ra2] "v"(ra[2]), [ra3] "v"(ra[3]),
+                   [ta00] "v"(ta00), [ta01] "v"(ta01), [ta10] "v"(ta10), [ta11] "v"(ta11), [sa] "v"(sa),
+                   [ldsv] "s"(ldsv), [ldsl] "s"(ldsl), [sp] "s"(spb), [sp2] "s"(spb2), [lp] "s"(lpb),
+                   [sstep] "s"(sstep), [rem] "s"(rem)
+                 : SR_ATTN_BWD_PIPE_CLOBBERS, "memory", "m0", "scc");
+  }
   if (qv) dkdv_tile<2, true>(smem + RAG, qv, kf, vf, dk, dv, tro, l32, hi);
   store_dkdv<SEG, 2>(b, kb0, key_base, len, hcol, hi, dk, dv);
 }
@@ -852,6 +894,18 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
       if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<0>), g, dim3(256), 0, ks, b);
       else hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<1>), g, dim3(256), 0, ks, b);
       if (seg == 0) name = "attn_bwd_dkdv_pipe_kernel<0>";
+      continue;
+    }
+    // keys shared by a batch > 1 with the items' queries in consecutive rows: one asm sweep over the
+    // concatenated queries (SR_ATTN_BWD_CAT)
+    const int64_t lqt = (int64_t)f.batch * f.lq;
+    if (shared && f.batch > 1 && sr::tune(SR_TUNE_ATTN_BWD_PIPE) != 0 && sr::tune(SR_TUNE_ATTN_BWD_CAT) != 0 &&
+        f.q_bstride == f.lq && f.lq >= 2 && lqt >= 256 && lqt < (1 << 24) &&
+        (lqt + 64) * ldmax * 2 < ((int64_t)1 << 31) && (int64_t)(f.heads - 1) * f.lq * 4 < (1 << 24)) {
+      const dim3 g((len + 255) / 256, f.heads, 1);
+      if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<0, true>), g, dim3(256), 0, ks, b);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_pipe_kernel<1, true>), g, dim3(256), 0, ks, b);
+      if (seg == 0) name = "attn_bwd_dkdv_pipe_kernel<0, cat>";
       continue;
     }
     // keys shared by a batch > 1: one workgroup sweeps every item's queries, so the launch is only

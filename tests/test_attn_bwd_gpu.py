@@ -198,7 +198,7 @@ def test_attention_bwd_pipe(case, P):
         dv1 = torch.full((B * P, C), float("nan"), device=DEV) if case == "reloc" else None
         delta = torch.empty(B, H, P, device=DEV)
         with ops.tuning(SR_ATTN_BWD_PIPE=pipe, SR_ATTN_BWD_DQ_PIPE=2 * pipe, SR_ATTN_BWD_KB=1,
-                        SR_ATTN_BWD_CONC=pipe):
+                        SR_ATTN_BWD_CONC=pipe, SR_ATTN_BWD_CAT=0):
             ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
             asm_dkdv = pipe and P >= 256 and case not in ("reloc", "anchor")
             want = "attn_bwd_dkdv_pipe_kernel<0>" if asm_dkdv else "attn_bwd_dkdv_kernel<0, 1>"
@@ -235,7 +235,7 @@ def test_attention_bwd_shared_key_split():
         dv0 = torch.full((A, C), float("nan"), device=DEV)
         dk1, dv1 = torch.empty(B * P, C, device=DEV), torch.empty(B * P, C, device=DEV)
         delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_QSPLIT=split):
+        with ops.tuning(SR_ATTN_BWD_QSPLIT=split, SR_ATTN_BWD_CAT=0):
             ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
             assert ops.last_kernel() == ("attn_bwd_dkdv_kernel<0, 1, split2>" if split else "attn_bwd_dkdv_kernel<0, 1>")
         outs.append((dq, dk0, dv0, dk1, dv1))
@@ -244,3 +244,47 @@ def test_attention_bwd_shared_key_split():
         assert torch.isfinite(b).all()
         assert torch.equal(b, c)  # deterministic
         assert (a - b).abs().max() <= 1e-5 * a.abs().max()  # summation order only
+
+
+@pytest.mark.parametrize("B,P", [(3, 300), (2, 1374), (5, 64)])
+def test_attention_bwd_concatenated_items(B, P):
+    """SR_ATTN_BWD_CAT: anchors shared by a batch whose queries are consecutive rows run as ONE
+    asm dK/dV sweep over the concatenated queries (tiles straddling items; each row's lse / -delta
+    found per tile).  Equal to the compiled per-item sweep up to fp32 summation grouping, and
+    deterministic; dQ and the per-item segment are unchanged."""
+    from sailrecon_amd import ops
+    torch.manual_seed(4)
+    H, D, A = 4, 64, 301
+    C = H * D
+    kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, l1=P, k1_bstride=P)
+    x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
+    q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
+    ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
+    k0, v0 = ka[:, :C], ka[:, C:]
+    kw.update(k1=k, v1=v)
+    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, P, device=DEV)
+    ops.attention(q, k0, v0, o, heads=H, head_dim=D, lse=lse, **kw)
+    g = torch.randn(B * P, C, device=DEV).bfloat16()
+    outs = []
+    for cat in (0, 1, 1):
+        dq = torch.empty(B * P, C, device=DEV)
+        dk0 = torch.full((A, C), float("nan"), device=DEV)
+        dv0 = torch.full((A, C), float("nan"), device=DEV)
+        dk1, dv1 = torch.empty(B * P, C, device=DEV), torch.empty(B * P, C, device=DEV)
+        delta = torch.empty(B, H, P, device=DEV)
+        with ops.tuning(SR_ATTN_BWD_CAT=cat, SR_ATTN_BWD_QSPLIT=0):
+            ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
+            want = "attn_bwd_dkdv_pipe_kernel<0, cat>" if cat and B * P >= 256 else "attn_bwd_dkdv_kernel<0, 1>"
+            assert ops.last_kernel() == want
+        outs.append((dq, dk0, dv0, dk1, dv1))
+    torch.cuda.synchronize()
+    for i, (a, b, c) in enumerate(zip(*outs)):
+        assert torch.isfinite(b).all()
+        assert torch.equal(b, c)  # deterministic
+        if i in (1, 2):  # dK / dV of the shared anchors: summation grouping only
+            err = float((a - b).abs().max() / a.abs().max())
+            print(f"B={B} P={P} {'dk0' if i == 1 else 'dv0'} concatenated vs per-item: {err:.2e}")
+            assert err <= 1e-5
+        else:
+            assert torch.equal(a, b)

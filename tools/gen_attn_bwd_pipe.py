@@ -67,6 +67,8 @@ Y_READS = float(os.environ.get("SR_BWD_PIPE_Y_READS", "0.8"))
 # barrier), nodma (no LDS-DMA staging), novalu (no exp / mul / pack), noread (no LDS reads), nowait
 # (no lgkmcnt waits)
 EXP = set(filter(None, os.environ.get("SR_BWD_PIPE_EXP", "").split(",")))
+# the dK/dV sweep's concatenated-items variant (SR_ATTN_BWD_PIPE_ASM_CAT): set while it is generated
+CAT = False
 
 
 def S(q, kb):
@@ -245,9 +247,19 @@ class Phase:
         for i in range(4):
             out.append([f"s_add_u32 m0, %[ldsv], {slot * SLOT_B + i * 1024}", "s_nop 0",
                         f"global_load_lds_dwordx4 %[dma{i & 1}], %[{'sp' if i < 2 else 'sp2'}]"])
-        out.append([f"s_add_u32 m0, %[ldsl], {slot * LSE_SLOT}", "s_nop 0", "global_load_lds_dword %[lofs], %[lp]",
-                    "v_add_u32 %[dma0], %[sstep], %[dma0]", "v_add_u32 %[dma1], %[sstep], %[dma1]",
-                    "v_add_u32 %[lofs], 0x100, %[lofs]"])
+        u = [f"s_add_u32 m0, %[ldsl], {slot * LSE_SLOT}", "s_nop 0", "global_load_lds_dword %[lofs], %[lp]",
+             "v_add_u32 %[dma0], %[sstep], %[dma0]", "v_add_u32 %[dma1], %[sstep], %[dma1]"]
+        if CAT:
+            # items concatenated (one sweep over every item's queries): the lse / -delta of query
+            # row r = b lq + i sits at float (b H + h) lq + i, i.e. r + b (H-1) lq past the head's
+            # base; b = mulhi(r, M) >> s (exact for r < 2^24, the host's M and s); the next tile's
+            # offset is formed right after this tile's copy
+            u += ["v_add_u32 %[rrow], 64, %[rrow]", "v_mul_hi_u32 %[tmp], %[rrow], %[mgc]",
+                  "v_lshrrev_b32 %[tmp], %[msh], %[tmp]", "v_mul_u32_u24 %[tmp], %[istr], %[tmp]",
+                  "v_lshl_add_u32 %[lofs], %[rrow], 2, %[tmp]"]
+        else:
+            u += ["v_add_u32 %[lofs], 0x100, %[lofs]"]
+        out.append(u)
         return out
 
     def add_other(self, units, cost, min_gap=0):
@@ -574,9 +586,19 @@ def stats(name, lines, loop):
             f"waits, {n_all} instructions; {len(lines)} asm lines")
 
 
+def cat_sweep():
+    global CAT
+    CAT = True
+    try:
+        return sweep()
+    finally:
+        CAT = False
+
+
 def main():
     out = ["// GENERATED by tools/gen_attn_bwd_pipe.py — do not edit by hand."]
-    for name, (lines, loop) in (("SR_ATTN_BWD_PIPE_ASM", sweep()), ("SR_ATTN_BWD_DQ_ASM", dq_sweep())):
+    for name, (lines, loop) in (("SR_ATTN_BWD_PIPE_ASM", sweep()), ("SR_ATTN_BWD_PIPE_ASM_CAT", cat_sweep()),
+                                ("SR_ATTN_BWD_DQ_ASM", dq_sweep())):
         st = stats(name, lines, loop)
         print(st)
         out.append("// " + st)

@@ -698,17 +698,15 @@ def attn_bwd():
                 ops.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, lse, g, d[:, :C], d[:, C:2 * C],
                                   d[:, 2 * C:], delta, heads=H, batch=batch, lq=lq, q_bstride=lq, l0=lq, k0_bstride=kb)
         fl = 10.0 * batch * H * lq * (lq + anchors) * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
-        # dK/dV sweep: compiled with 32 keys per wave (kb1), or the hand-scheduled asm sweep (pipe);
+        # compiled sweeps (kb1), the asm sweeps (pipe2), + the concatenated-items dK/dV sweep (cat);
         # SR_BWD_AB=kb adds the compiled 64-keys-per-wave form
-        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0, SR_ATTN_BWD_QSPLIT=0)),
-                ("pipe", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=0)),
-                ("pipe2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CONC=0)),
-                ("dq2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=2, SR_ATTN_BWD_CONC=0)),
-                ("split", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_QSPLIT=1))]
+        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0, SR_ATTN_BWD_CAT=0)),
+                ("pipe2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CAT=0)),
+                ("cat", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CAT=1))]
         if os.environ.get("SR_BWD_AB") == "kb":
             arms.append(("kb2", dict(SR_ATTN_BWD_KB=2, SR_ATTN_BWD_PIPE=0)))
         if os.environ.get("SR_BWD_AB") == "pipe":  # the asm sweeps only (A/B of library builds)
-            arms = arms[2:]
+            arms = arms[1:2]
         for arm, sw in arms * 2:
             with ops.tuning(**sw):
                 ms = timeit(f, reps=3 if batch == 1 else 5, warm=1)
