@@ -696,6 +696,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(sr_attn_bwd_desc b)
 // compiled kernel's order (segment 0's tiles, its ragged tile, segment 1's ...): bit-identical
 // outputs.  The host picks this kernel when every segment has at least 4 full key tiles.
 //   LDS: ring of 4 x (K tile | V tile) at 0 .. 64 KB, the ragged stage after it.
+template <int NSEG>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_desc b) {
   constexpr int SLOT = 2 * TB, RAG = 4 * SLOT;
   __shared__ __attribute__((aligned(16))) char smem[RAG + 2 * TB];
@@ -749,8 +750,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_de
   const uint32_t ta00 = lds0 + tro.off[0][0], ta01 = lds0 + tro.off[0][1];
   const uint32_t ta10 = lds0 + tro.off[1][0], ta11 = lds0 + tro.off[1][1];
 
-  const int nseg = f.l1 > 0 ? 2 : 1;
-  for (int seg = 0; seg < nseg; ++seg) {
+#pragma unroll
+  for (int seg = 0; seg < NSEG; ++seg) {  // NSEG = 1 + (l1 > 0), a template so that one segment compiles alone
     if (seg) __syncthreads();  // every wave is done with segment 0's ring and ragged stage
     const int len = seg ? f.l1 : f.l0;
     const int nfull = len / 64, kv = len % 64;  // nfull >= 4 (host)
@@ -867,8 +868,10 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
                        (f.l1 == 0 || (int64_t)(f.l1 + 64) * std::max<int64_t>(f.ldk1, f.ldv1) * 2 < ((int64_t)1 << 31)) &&
                        (sr::tune(SR_TUNE_ATTN_BWD_DQ_PIPE) == 2 || qpad256 * 100 <= qpad128 * 102 ||
                         (int64_t)f.l0 + f.l1 >= 4096);
-  if (dq_pipe)
-    hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
+  if (dq_pipe && f.l1 > 0)
+    hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel<2>, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
+  else if (dq_pipe)
+    hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel<1>, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
   else
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
   // dK / dV on the side stream when SR_ATTN_BWD_CONC (joined back below)
