@@ -106,7 +106,7 @@ enum sr_tuning_key {
                                round of workgroups better (2: always)                  default 0 */
   SR_TUNE_ATTN_BWD_CAT = 24,/* 1: keys shared by a batch > 1 whose items' queries are consecutive rows:
                                the dK/dV asm sweep over the concatenated queries (one sequence of
-                               batch * lq rows; same sum, other tile grouping)          default 0 */
+                               batch * lq rows; same sum, other tile grouping)          default 1 */
   SR_TUNE_COUNT = 25
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
