@@ -199,7 +199,8 @@ typedef struct sr_gemm_problem {
   sr_gemm_epi ep;
 } sr_gemm_problem;
 
-/* 1..4 independent bf16 GEMMs of one epilogue kind (BIAS, QKV, BIAS_GELU, BIAS_RESID; N % 256 == 0)
+/* 1..4 independent bf16 GEMMs of one epilogue kind (BIAS, QKV, BIAS_GELU, BIAS_RESID, and the training
+ * dgrads' F32 / GELU_BWD; N % 256 == 0)
  * in ONE launch of the 256x256 kernel, so that their last partial workgroup rounds merge (the
  * layer's query, anchor and anchor-subsample QKV projections after a frame block).  Every problem
  * runs on the 256x256 kernel with sr_gemm's tile order, so it is bit-identical to sr_gemm only

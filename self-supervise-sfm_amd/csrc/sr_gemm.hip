@@ -1378,7 +1378,8 @@ static int gemm_common(sr_stream_t stream, int dtype, int epi, const void* A, in
 extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, const sr_gemm_problem* pr) {
   SR_CHECK(pr && n >= 1 && n <= GROUP_MAX, SR_EINVAL, "sr_gemm_group: 1..%d problems (got %d)", GROUP_MAX, n);
   SR_CHECK(dtype == SR_BF16, SR_EUNSUPPORTED, "sr_gemm_group: bf16 only");
-  SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_QKV || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID,
+  SR_CHECK(epi == SR_EPI_BIAS || epi == SR_EPI_QKV || epi == SR_EPI_BIAS_GELU || epi == SR_EPI_BIAS_RESID ||
+               epi == SR_EPI_F32 || epi == SR_EPI_GELU_BWD,
            SR_EUNSUPPORTED, "sr_gemm_group: epilogue %d not supported", epi);
   GemmGroup gg{};
   gg.n = n;
@@ -1406,6 +1407,8 @@ extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, cons
     case SR_EPI_BIAS: SR_GROUP_LAUNCH(SR_EPI_BIAS); break;
     case SR_EPI_QKV: SR_GROUP_LAUNCH(SR_EPI_QKV); break;
     case SR_EPI_BIAS_GELU: SR_GROUP_LAUNCH(SR_EPI_BIAS_GELU); break;
+    case SR_EPI_F32: SR_GROUP_LAUNCH(SR_EPI_F32); break;
+    case SR_EPI_GELU_BWD: SR_GROUP_LAUNCH(SR_EPI_GELU_BWD); break;
     default: SR_GROUP_LAUNCH(SR_EPI_BIAS_RESID);
   }
 #undef SR_GROUP_LAUNCH

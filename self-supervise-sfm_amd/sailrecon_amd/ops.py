@@ -284,7 +284,7 @@ def gemm_group_eligible(problems) -> bool:
 
 def gemm_group(problems, epi: int, tag: Optional[str] = None) -> None:
     """Several independent gemm() calls of one epilogue kind in ONE launch of the 256x256 kernel
-    (sr_gemm_group): each problem a dict with a, w, out and gemm()'s bias / gamma / qkv keywords;
+    (sr_gemm_group): each problem a dict with a, w, out and gemm()'s bias / gamma / qkv / aux keywords;
     their last partial workgroup rounds merge."""
     if not gemm_group_eligible(problems):
         raise ValueError("gemm_group: bf16 problems with N % 256 == 0, at most 4")
@@ -304,6 +304,11 @@ def gemm_group(problems, epi: int, tag: Optional[str] = None) -> None:
             _fill_qkv_epi(q.ep, p["qkv"])
         if p.get("q_scale"):
             q.ep.q_scale, q.ep.q_cols = float(p["q_scale"]), int(p["q_cols"])
+        if p.get("aux") is not None:  # GELU_BWD's saved pre-activation / the forward's aux output
+            aux = p["aux"]
+            if aux.dtype != a.dtype:
+                raise TypeError("gemm_group: aux must have the operand dtype")
+            q.ep.aux, q.ep.ld_aux = _p(aux), _rowmajor(aux, "aux")
         flops += 2.0 * a.shape[0] * N * K
         nbytes += (a.shape[0] * K + N * K) * a.element_size() + a.shape[0] * N * out.element_size()
     if tag == "gemm":

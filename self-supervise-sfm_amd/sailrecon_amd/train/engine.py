@@ -263,6 +263,82 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
     ops.layernorm_bwd(tape.x0, dxn, pb.ln1_w, pb.eps, dx, dxb=dxb, dw=g.ln1_w, db=g.ln1_b)
 
 
+def block_bwd_multi(items, tag: str = "pair") -> None:
+    """block_bwd for several independent block applications of equal width at once (the layer's
+    reloc and global blocks: different weights, disjoint rows): stage by stage in block_bwd's
+    order, each stage's dgrad GEMMs of all items as ONE grouped launch (sr_gemm_group), whose
+    last partial round of workgroups the items share (at C4 each item's N = 1,024 dgrads are
+    344 tiles of 256^2, 1.3 rounds alone).  ``items``: dicts of block_bwd's arguments (pb, bp, g,
+    tape, dx, dxb, attend_bwd, qkv_epi, sc, tag); their attention backwards run in list order.
+    A grouped product runs on the 256^2 kernel with sr_gemm's per-tile order; where sr_gemm
+    alone would have picked the 128^2 kernel the results differ by fp32 accumulation order."""
+    if len(items) == 1 or not all(it["tape"].xn1.dtype == torch.bfloat16 for it in items) or \
+            len({(it["dx"].shape[1], it["tape"].u.shape[1]) for it in items}) != 1:
+        for it in items:
+            block_bwd(it["pb"], it["bp"], it["g"], it["tape"], it["dx"], it["dxb"], it["attend_bwd"], it["qkv_epi"],
+                      it["sc"], tag=it["tag"])
+        return
+    C = items[0]["dx"].shape[1]
+    Hd = items[0]["tape"].u.shape[1]
+    dev = items[0]["dx"].device
+    dt = torch.bfloat16
+
+    def dgrad(epi, probs):
+        if ops.gemm_group_eligible(probs):
+            ops.gemm_group(probs, epi, tag=tag + ".dgrad")
+        else:
+            for q in probs:
+                ops.gemm(q["a"], q["w"], q["out"], epi, aux=q.get("aux"), tag=tag + ".dgrad")
+
+    def wgrad(it, dy, x, dw, db=None, rowscale=None, wdot=None, rowdot=None):
+        ops.gemm_wgrad(dy, x, dw, accumulate=True, rowscale=rowscale, wdot=wdot, rowdot=rowdot,
+                       tag=it["tag"] + ".wgrad")
+        if db is not None:
+            ops.colsum(dy, db, accumulate=True)
+
+    for it in items:
+        R = it["dx"].shape[0]
+        it["_tmp"] = it["sc"].get("colsum_tmp", 1, max(C, Hd, 3 * C), torch.float32, dev)[0]
+        it["_dU"] = it["sc"].get("dU", R, Hd, dt, dev)
+        it["_dxn"] = it["sc"].get("dxn", R, C, torch.float32, dev)
+        it["_dO"] = it["sc"].get("dO", R, C, dt, dev)
+    # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
+    dgrad(_lib.SR_EPI_GELU_BWD, [dict(a=it["dxb"], w=it["bp"].wt_fc2, out=it["_dU"], aux=it["tape"].u) for it in items])
+    for it in items:
+        pb, bp, g = it["pb"], it["bp"], it["g"]
+        wgrad(it, it["dxb"], it["tape"].h, g.w_fc2, rowscale=pb.g2, wdot=bp.w_fc2 if g.g2 is not None else None,
+              rowdot=g.g2 if g.g2 is not None else None)
+        _resid_param_grads(it["dx"], bp.b_fc2, pb.g2, g.b_fc2, g.g2, it["_tmp"][:C])
+    dgrad(_lib.SR_EPI_F32, [dict(a=it["_dU"], w=it["bp"].wt_fc1, out=it["_dxn"]) for it in items])
+    for it in items:
+        pb, bp, g = it["pb"], it["bp"], it["g"]
+        wgrad(it, it["_dU"], it["tape"].xn2, g.w_fc1, db=g.b_fc1)
+        it["_fused"] = g.ln2_w is not None and C <= 2048 and _resid_wants_sum(bp.b_proj, g.b_proj, g.g1)
+        ops.layernorm_bwd(it["tape"].x1, it["_dxn"], pb.ln2_w, pb.eps, it["dx"], dxb=it["dxb"], dw=g.ln2_w,
+                          db=g.ln2_b, dx_sum=it["_tmp"][:C] if it["_fused"] else None)
+    # ---- attention: x1 = x0 + g1 * proj(attn(qk(qkv(LN1(x0)))))
+    dgrad(_lib.SR_EPI_BIAS, [dict(a=it["dxb"], w=it["bp"].wt_proj, out=it["_dO"]) for it in items])
+    for it in items:
+        pb, bp, g = it["pb"], it["bp"], it["g"]
+        wgrad(it, it["dxb"], it["tape"].o, g.w_proj, rowscale=pb.g1, wdot=bp.w_proj if g.g1 is not None else None,
+              rowdot=g.g1 if g.g1 is not None else None)
+        _resid_param_grads(it["dx"], bp.b_proj, pb.g1, g.b_proj, g.g1, it["_tmp"][:C], summed=it["_fused"])
+    for it in items:
+        R = it["dx"].shape[0]
+        dqkv = it["sc"].get("dqkv", R, 3 * C, torch.float32, dev)
+        it["attend_bwd"](it["tape"], it["_dO"], dqkv)
+        it["_draw"] = it["sc"].get("draw", R, 3 * C, dt, dev)
+        qkv_epi = it["qkv_epi"]
+        ops.qk_bwd(it["tape"].raw if qkv_epi is not None else None, dqkv, it["_draw"],
+                   qkv_epi or dict(embed_dim=C, head_dim=64), grads=it["g"].qkn)
+    dgrad(_lib.SR_EPI_F32, [dict(a=it["_draw"], w=it["bp"].wt_qkv, out=it["_dxn"]) for it in items])
+    for it in items:
+        pb, g = it["pb"], it["g"]
+        wgrad(it, it["_draw"], it["tape"].xn1, g.w_qkv, db=g.b_qkv)
+        ops.layernorm_bwd(it["tape"].x0, it["_dxn"], pb.ln1_w, pb.eps, it["dx"], dxb=it["dxb"], dw=g.ln1_w,
+                          db=g.ln1_b)
+
+
 def frame_attend_train(pb: runtime.PackedBlock, frames: int, tokens: int):
     """Forward / backward attention callbacks within each frame (frame and DINO blocks)."""
     C = pb.dim

@@ -20,6 +20,7 @@ Residual stream layout as in inference (models/aggregator.py): rows [0, Na*P) an
 
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -32,6 +33,9 @@ from .params import FlatParams
 Tensor = torch.Tensor
 BF16 = torch.bfloat16
 F32 = torch.float32
+# SR_TRAIN_PAIR_DGRAD (default 1; 0 for the A/B): the layer's reloc and global blocks run their
+# backward stage by stage with each stage's dgrad GEMMs grouped into one launch
+_PAIR_DGRAD = os.environ.get("SR_TRAIN_PAIR_DGRAD", "1") != "0"
 
 
 def _i32(rows, dev) -> Tensor:
@@ -51,6 +55,7 @@ class TrainGraph:
         self.invalidate()
         self._tapes = {}
         self._sc = engine.BwdScratch()
+        self._sc2 = engine.BwdScratch()  # the global block's scratch beside the reloc block's (block_bwd_multi)
         self.state: Optional[dict] = None
         # grad_ready_hook(module): called once a module's parameter grads are final within the
         # backward (data-parallel training starts that module's all-reduce right away)
@@ -450,13 +455,22 @@ class TrainGraph:
             # reloc block (query rows); its shared segment's dK|dV land in dkv_sub
             _, rbwd = self._reloc_attn(pr, kv_sub, dkv_sub, Nq, P, n_sub)
             gr = engine.block_grads(br)
-            engine.block_bwd(pr, self._bwd_pack(br, BF16), gr, self._tapes[("reloc", l)], dx[q0:], dxb[q0:], rbwd,
-                             runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx), self._sc, tag="reloc")
             # global block (anchor rows)
             _, gbwd = self._global_attn(pg, q0)
             tg = self._tapes[("global", l)]
-            engine.block_bwd(pg, self._bwd_pack(bg, BF16), engine.block_grads(bg), tg, dx[:q0], dxb[:q0], gbwd,
-                             runtime.qkv_params(pg, rope, pos_row_base=0, **posctx), self._sc, tag="global")
+            rel = dict(pb=pr, bp=self._bwd_pack(br, BF16), g=gr, tape=self._tapes[("reloc", l)], dx=dx[q0:],
+                       dxb=dxb[q0:], attend_bwd=rbwd, qkv_epi=runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx),
+                       sc=self._sc, tag="reloc")
+            glo = dict(pb=pg, bp=self._bwd_pack(bg, BF16), g=engine.block_grads(bg), tape=tg, dx=dx[:q0],
+                       dxb=dxb[:q0], attend_bwd=gbwd, qkv_epi=runtime.qkv_params(pg, rope, pos_row_base=0, **posctx),
+                       sc=self._sc2, tag="global")
+            if _PAIR_DGRAD and Nq > 0:
+                # the two blocks' dgrad GEMMs stage by stage as grouped launches (engine.block_bwd_multi)
+                engine.block_bwd_multi([rel, glo], tag="pair")
+            else:
+                for it in (rel, glo):
+                    engine.block_bwd(it["pb"], it["bp"], it["g"], it["tape"], it["dx"], it["dxb"], it["attend_bwd"],
+                                     it["qkv_epi"], self._sc, tag=it["tag"])
             # anchor subsample: k-norm + RoPE backward -> K|V dgrad / wgrad -> LN1 (row map) backward
             epi = runtime.qkv_params(pr, rope, pos_rowmap=rowmap[l], **posctx)
             if epi is not None:

@@ -538,6 +538,38 @@ def test_gemm_group(ops, epi_name):
         assert torch.equal(p["out"], ref_out)
 
 
+@pytest.mark.parametrize("epi_name", ["F32", "GELU_BWD"])
+def test_gemm_group_dgrad(ops, epi_name):
+    """sr_gemm_group with the training dgrads' epilogues (F32: fp32 out; GELU_BWD: dU = GELU'(u) *
+    (a . w) with the saved pre-activation u as aux), as train.engine.block_bwd_multi groups the
+    layer's reloc and global blocks: bit-identical to the problems launched apart on the 256x256
+    kernel (>= 512 tiles each)."""
+    L = _lib()
+    epi = getattr(L, "SR_EPI_" + epi_name)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    probs, plain = [], []
+    for M, N, K in ((43 * 256 - 100, 4096, 1024), (86 * 256 - 32, 2048, 4096)) if epi_name == "F32" else \
+            ((43 * 256 - 100, 4096, 1024), (40 * 256, 4096, 1024)):
+        a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+        w = (torch.randn(N, K, device=DEV, generator=g) / 32).bfloat16()
+        p = dict(a=a, w=w)
+        if epi_name == "GELU_BWD":
+            p["aux"] = torch.randn(M, N, device=DEV, generator=g).bfloat16()
+            p["out"] = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        else:
+            p["out"] = torch.empty(M, N, device=DEV)
+        probs.append(p)
+        plain.append(torch.empty_like(p["out"]))
+    ops.gemm_group(probs, epi)
+    with ops.tuning(SR_GEMM_TAIL=0):
+        for p, ref_out in zip(probs, plain):
+            ops.gemm(p["a"], p["w"], ref_out, epi, aux=p.get("aux"), splits=1)
+    torch.cuda.synchronize()
+    for p, ref_out in zip(probs, plain):
+        assert torch.isfinite(p["out"].float()).all()
+        assert torch.equal(p["out"], ref_out)
+
+
 @pytest.mark.parametrize("var", range(8))
 def test_residual_layernorm_variants(ops, var):
     """Every sr_residual_layernorm variant of the SR_RLN_WIDE switch (16-B lanes, two rows per
