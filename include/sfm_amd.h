@@ -107,7 +107,9 @@ enum sr_tuning_key {
   SR_TUNE_ATTN_BWD_CAT = 24,/* 1: keys shared by a batch > 1 whose items' queries are consecutive rows:
                                the dK/dV asm sweep over the concatenated queries (one sequence of
                                batch * lq rows; same sum, other tile grouping)          default 1 */
-  SR_TUNE_COUNT = 25
+  SR_TUNE_WGRAD_STAGES = 25,/* 2: the 256x256 wgrad stages one 64-row m-tile ahead; 3: two 48-row m-tiles
+                               ahead (144 KiB of LDS; other fp32 slice boundaries)     default 2 */
+  SR_TUNE_COUNT = 26
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

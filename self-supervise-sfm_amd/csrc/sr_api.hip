@@ -25,7 +25,7 @@ constexpr TuneDef kTune[SR_TUNE_COUNT] = {
     {"SR_ATTN_QTAIL", 0},   {"SR_GEMM_XPF", 0},       {"SR_GEMM_ROPE_LDS", 1},  {"SR_GEMM_PP", 0},
     {"SR_ATTN_BWD_KB", 1},   {"SR_ATTN_BWD_PIPE", 1},  {"SR_ATTN_BWD_DQ_PIPE", 1},
     {"SR_ATTN_BWD_CONC", 0},     {"SR_ATTN_BWD_QSPLIT", 0},
-    {"SR_ATTN_BWD_CAT", 1},
+    {"SR_ATTN_BWD_CAT", 1},      {"SR_WGRAD_STAGES", 2},
 };
 std::atomic<int> g_tune[SR_TUNE_COUNT];
 std::once_flag g_tune_once;

@@ -153,28 +153,34 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs g) {
 // staged bytes per FLOP of the 128 x 128 tile; the reduction over M splits into gridDim.y slices
 // whose fp32 partials wgrad_reduce_kernel sums.
 constexpr int WT2 = 256;
-constexpr int WSTAGE2 = 8 * SUB;  // 64 KiB
 
+// MT rows per m-tile, NST LDS stages (MT/8 DMA pieces per wave and stage): <64, 2> stages the next
+// 64-row tile while computing the current one; <48, 3> (SR_TUNE_WGRAD_STAGES=3) keeps two 48-row tiles
+// in flight (144 KiB), for operands that come from beyond L2.
+template <int MT, int NST>
 __global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * WSTAGE2];
+  constexpr int SUBT = MT * 128;  // one sub-tile: MT rows x 64 bf16 columns
+  constexpr int STG = 8 * SUBT;
+  constexpr int PCS = MT / 8;     // DMA wave-instructions per wave and stage
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hi = lane >> 5;
   const int ntk = g.K / WT2, ntiles = (g.N / WT2) * ntk;
   const int tile = sr::xcd_remap(blockIdx.x, ntiles);
   const int tn = tile / ntk, tk = tile - tn * ntk;
   const int n0 = tn * WT2, k0 = tk * WT2;
 
-  // wave w fills sub-tile w (0-3: A columns n0 + 64w; 4-7: B columns k0 + 64(w-4)), 8 DMAs of 8 rows
+  // wave w fills sub-tile w (0-3: A columns n0 + 64w; 4-7: B columns k0 + 64(w-4)), PCS DMAs of 8 rows
   const char* base = wave < 4 ? g.A + (int64_t)(n0 + 64 * wave) * 2 : g.B + (int64_t)(k0 + 64 * (wave - 4)) * 2;
   const int64_t ld = wave < 4 ? g.lda_b : g.ldb_b;
   const int rsub = lane >> 3, slot = lane & 7;
-  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * SUB);
+  const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * SUBT);
   auto stage = [&](int mt, int buf) {
-    const uint32_t db = dst0 + buf * WSTAGE2;
+    const uint32_t db = dst0 + buf * STG;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < PCS; ++i) {
       const int r = 8 * i + rsub;
       const int chunk = slot ^ (((r >> 1) & 1) << 2);
-      const int row = min(mt * 64 + r, g.M - 1);
+      const int row = min(mt * MT + r, g.M - 1);
       sr::dma16(base + (int64_t)row * ld + chunk * 16, db + i * 1024);
     }
   };
@@ -191,27 +197,35 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
 
   const int mt0 = blockIdx.y * g.mt_per_split;
   const int mt1 = min(mt0 + g.mt_per_split, g.mtiles);
-  if (mt0 < mt1) stage(mt0, 0);
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (mt0 + j < mt1) stage(mt0 + j, j);
+  int buf = 0;
   for (int mt = mt0; mt < mt1; ++mt) {
-    const int buf = (mt - mt0) & 1;
-    sr::wait_vmcnt0();   // this wave's part of stage mt landed
-    sr::barrier_raw();   // ... every wave's; every wave is done reading the other buffer
-    if (mt + 1 < mt1) stage(mt + 1, buf ^ 1);
-    char* sb = smem + buf * WSTAGE2;
-    const int valid = g.M - mt * 64;
-    if (valid < 64) {  // ragged last m-tile: zero the clamped rows (uniform branch)
-      for (int e = tid; e < 8 * 64 * 8; e += 512) {
-        const int st = e >> 9, r = (e >> 3) & 63, c = e & 7;
-        if (r >= valid) *(uint4*)(sb + st * SUB + r * 128 + c * 16) = uint4{0u, 0u, 0u, 0u};
+    // this wave's part of stage mt landed (the NST-2 later stages may stay in flight) ...
+    if constexpr (NST == 3) {
+      if (mt + 1 < mt1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS) : "memory");
+      else sr::wait_vmcnt0();
+    } else {
+      sr::wait_vmcnt0();
+    }
+    sr::barrier_raw();   // ... every wave's; every wave is done reading the buffer restaged next
+    if (mt + NST - 1 < mt1) stage(mt + NST - 1, buf == 0 ? NST - 1 : buf - 1);
+    char* sb = smem + buf * STG;
+    const int valid = g.M - mt * MT;
+    if (valid < MT) {  // ragged last m-tile: zero the clamped rows (uniform branch)
+      for (int e = tid; e < 8 * MT * 8; e += 512) {
+        const int st = e / (MT * 8), r = (e >> 3) % MT, c = e & 7;
+        if (r >= valid) *(uint4*)(sb + st * SUBT + r * 128 + c * 16) = uint4{0u, 0u, 0u, 0u};
       }
       __syncthreads();
     }
-    const char* tb = sb + (4 + wc) * SUB;
+    const char* tb = sb + (4 + wc) * SUBT;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < MT / 16; ++s) {
       bf16x8 a[4], b[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = tr_frag(sb + (2 * wr + (i >> 1)) * SUB, 16 * s, tro.off[i & 1]);
+      for (int i = 0; i < 4; ++i) a[i] = tr_frag(sb + (2 * wr + (i >> 1)) * SUBT, 16 * s, tro.off[i & 1]);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = tr_frag(tb, 16 * s, tro.off[j]);
       __builtin_amdgcn_s_setprio(1);
@@ -221,6 +235,7 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
+    buf = buf == NST - 1 ? 0 : buf + 1;
   }
   // lane: column k = k0 + 64 wc + 32 j + l32, rows n = n0 + 128 wr + 32 i + acc_row(e, hi)
   float* part = g.part + (int64_t)blockIdx.y * g.N * g.K;
@@ -936,15 +951,20 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   g.M = M;
   g.N = N;
   g.K = K;
-  g.mtiles = (M + 63) / 64;
+  // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
+  const bool big = sr::tune(SR_TUNE_WGRAD256) != 0 && N % WT2 == 0 && K % WT2 == 0;
+  const bool st3 = big && sr::tune(SR_TUNE_WGRAD_STAGES) == 3;
+  const int mt = st3 ? 48 : 64;  // rows per m-tile
+  g.mtiles = (M + mt - 1) / mt;
   splits = std::min(splits, g.mtiles);
   g.mt_per_split = (g.mtiles + splits - 1) / splits;
   splits = (g.mtiles + g.mt_per_split - 1) / g.mt_per_split;
   hipStream_t s = (hipStream_t)stream;
-  // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
-  const bool big = sr::tune(SR_TUNE_WGRAD256) != 0;
-  if (big && N % WT2 == 0 && K % WT2 == 0) {
-    hipLaunchKernelGGL(wgrad256_kernel, dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
+  if (st3) {
+    hipLaunchKernelGGL((wgrad256_kernel<48, 3>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
+    sr::note_kernel("wgrad256_kernel<48, 3>");
+  } else if (big) {
+    hipLaunchKernelGGL((wgrad256_kernel<64, 2>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
     sr::note_kernel("wgrad256_kernel");
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3((N / WT) * (K / WT), splits), dim3(256), 0, s, g);
