@@ -451,6 +451,30 @@ int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B,
                   int64_t lddw, int M, int N, int K, int accumulate, const float* rowscale, const float* wdot,
                   int64_t ldwd, float* rowdot, int splits, float* workspace);
 
+/* One problem of sr_gemm_wgrad_pair: the arguments of sr_gemm_wgrad. */
+typedef struct sr_wgrad_problem {
+  const void* A;
+  int64_t lda;
+  const void* B;
+  int64_t ldb;
+  float* dW;
+  int64_t lddw;
+  int M, N, K, accumulate;
+  const float* rowscale;
+  const float* wdot;
+  int64_t ldwd;
+  float* rowdot;
+  int splits;
+  float* workspace; /* its own: splits * N * K floats */
+} sr_wgrad_problem;
+
+/* Two sr_gemm_wgrad problems of equal N and K (multiples of 256; different rows and weights: the
+ * layer's reloc and global blocks) with their M slices in ONE launch of the 256x256 kernel, so each
+ * problem can take half the slices and the slices stay long; per problem the same m-tiles, k order
+ * and reduction as sr_gemm_wgrad with the same `splits` (bit-identical to it).  Replaces the weight
+ * grads of the two blocks' nn.Linear layers in loss.backward() (train_imc.py:404). */
+int sr_gemm_wgrad_pair(sr_stream_t stream, const sr_wgrad_problem* problems);
+
 /* Column sums (bias / token / positional-embedding grads):
  *   out[c] = (accumulate ? out[c] : 0) + scale * sum_{r<M} X[r*ldx + c],  c < N (N % 4 == 0).
  * X is `dtype`; two deterministic passes through `workspace` (16-B aligned, workspace_floats >=

@@ -60,6 +60,13 @@ void layout() {
                            FIELD(sr_gemm_problem, ldw), FIELD(sr_gemm_problem, out), FIELD(sr_gemm_problem, ldo),
                            FIELD(sr_gemm_problem, M), FIELD(sr_gemm_problem, N), FIELD(sr_gemm_problem, K),
                            FIELD(sr_gemm_problem, ep)));
+  STRUCT(sr_wgrad_problem,
+         (FIELD(sr_wgrad_problem, A), FIELD(sr_wgrad_problem, lda), FIELD(sr_wgrad_problem, B),
+          FIELD(sr_wgrad_problem, ldb), FIELD(sr_wgrad_problem, dW), FIELD(sr_wgrad_problem, lddw),
+          FIELD(sr_wgrad_problem, M), FIELD(sr_wgrad_problem, N), FIELD(sr_wgrad_problem, K),
+          FIELD(sr_wgrad_problem, accumulate), FIELD(sr_wgrad_problem, rowscale), FIELD(sr_wgrad_problem, wdot),
+          FIELD(sr_wgrad_problem, ldwd), FIELD(sr_wgrad_problem, rowdot), FIELD(sr_wgrad_problem, splits),
+          FIELD(sr_wgrad_problem, workspace)));
   STRUCT(sr_attn_desc,
          (FIELD(sr_attn_desc, q), FIELD(sr_attn_desc, ldq), FIELD(sr_attn_desc, k0), FIELD(sr_attn_desc, v0),
           FIELD(sr_attn_desc, ldk0), FIELD(sr_attn_desc, ldv0), FIELD(sr_attn_desc, k1), FIELD(sr_attn_desc, v1),

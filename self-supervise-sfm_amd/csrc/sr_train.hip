@@ -157,8 +157,13 @@ constexpr int WT2 = 256;
 // MT rows per m-tile, NST LDS stages (MT/8 DMA pieces per wave and stage): <64, 2> stages the next
 // 64-row tile while computing the current one; <48, 3> (SR_TUNE_WGRAD_STAGES=3) keeps two 48-row tiles
 // in flight (144 KiB), for operands that come from beyond L2.
+// Two problems of equal N and K in one launch (sr_gemm_wgrad_pair): slices blockIdx.y < y0 belong to
+// g0, the rest to g1 (a single problem passes g1 = g0, y0 = its slice count).
 template <int MT, int NST>
-__global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
+__global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g0, WgradArgs g1, int y0) {
+  const bool second = (int)blockIdx.y >= y0;
+  const WgradArgs g = second ? g1 : g0;
+  const int ys = second ? (int)blockIdx.y - y0 : (int)blockIdx.y;
   constexpr int SUBT = MT * 128;  // one sub-tile: MT rows x 64 bf16 columns
   constexpr int STG = 8 * SUBT;
   constexpr int PCS = MT / 8;     // DMA wave-instructions per wave and stage
@@ -195,7 +200,7 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int mt0 = blockIdx.y * g.mt_per_split;
+  const int mt0 = ys * g.mt_per_split;
   const int mt1 = min(mt0 + g.mt_per_split, g.mtiles);
 #pragma unroll
   for (int j = 0; j < NST - 1; ++j)
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(WgradArgs g) {
     buf = buf == NST - 1 ? 0 : buf + 1;
   }
   // lane: column k = k0 + 64 wc + 32 j + l32, rows n = n0 + 128 wr + 32 i + acc_row(e, hi)
-  float* part = g.part + (int64_t)blockIdx.y * g.N * g.K;
+  float* part = g.part + (int64_t)ys * g.N * g.K;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -369,6 +374,42 @@ int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, i
   hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N / 4 + 15) / 16)), dim3(256), 0, s, ws, chunks, N, out,
                      accumulate, scale);
   return sr::check_launch("sr_colsum");
+}
+
+// dw | db (| dx_colsum) from layernorm_bwd_kernel's partial rows [nrows][np * cols] in ONE launch
+// (was a partial + final colsum pair per output): workgroup = 4 column quads x 64 row groups, each
+// thread sums rows g, g + 64, ... (four in flight), then a fixed LDS tree over the 64 groups
+// (deterministic).  dw / db accumulate, dx_colsum is assigned.
+__global__ __launch_bounds__(256) void lnb_final_kernel(const float* __restrict__ part, int nrows, int cols, int np,
+                                                        float* dw, float* db, float* dxs) {
+  __shared__ f32x4 red[64][4];
+  const int qi = threadIdx.x & 3, g = threadIdx.x >> 2;
+  const int N = np * cols;
+  const int c = (blockIdx.x * 4 + qi) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    f32x4 s1 = s, s2 = s, s3 = s;
+    int z = g;
+    for (; z + 192 < nrows; z += 256) {
+      s += *(const f32x4*)(part + (int64_t)z * N + c);
+      s1 += *(const f32x4*)(part + (int64_t)(z + 64) * N + c);
+      s2 += *(const f32x4*)(part + (int64_t)(z + 128) * N + c);
+      s3 += *(const f32x4*)(part + (int64_t)(z + 192) * N + c);
+    }
+    for (; z < nrows; z += 64) s += *(const f32x4*)(part + (int64_t)z * N + c);
+    s = (s + s1) + (s2 + s3);
+  }
+  red[g][qi] = s;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (g < w) red[g][qi] += red[g + w][qi];
+    __syncthreads();
+  }
+  if (g == 0 && c < N) {  // cols % 4 == 0: a quad never straddles two outputs
+    const int seg = c / cols, cc = c - seg * cols;
+    f32x4* o = (f32x4*)((seg == 0 ? dw : seg == 1 ? db : dxs) + cc);
+    *o = seg < 2 ? *o + red[0][qi] : red[0][qi];
+  }
 }
 
 // ================================================================ LayerNorm backward
@@ -931,9 +972,9 @@ unsigned grid_for(int64_t n, int64_t cap = 4096) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B, int64_t ldb, float* dW,
-                             int64_t lddw, int M, int N, int K, int accumulate, const float* rowscale,
-                             const float* wdot, int64_t ldwd, float* rowdot, int splits, float* workspace) {
+namespace {
+int wgrad_check(const void* A, int64_t lda, const void* B, int64_t ldb, float* dW, int64_t lddw, int M, int N, int K,
+                const float* wdot, int64_t ldwd, float* rowdot, int splits, float* workspace) {
   SR_CHECK(A && B && dW && workspace, SR_EINVAL, "sr_gemm_wgrad: null pointer");
   SR_CHECK(M > 0 && N > 0 && K > 0 && N % WT == 0 && K % WT == 0, SR_EUNSUPPORTED,
            "sr_gemm_wgrad: N=%d, K=%d must be multiples of 128 (M=%d)", N, K, M);
@@ -942,6 +983,12 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
            SR_EINVAL, "sr_gemm_wgrad: bad leading dims / alignment");
   SR_CHECK(!wdot || (rowdot && ldwd >= K && ldwd % 4 == 0), SR_EINVAL, "sr_gemm_wgrad: wdot needs rowdot");
   SR_CHECK(splits >= 1, SR_EINVAL, "sr_gemm_wgrad: splits=%d", splits);
+  return SR_OK;
+}
+
+// kernel arguments of one problem; `splits` is clamped to the slices that get m-tiles
+WgradArgs wgrad_args(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, int mt, int& splits,
+                     float* workspace) {
   WgradArgs g;
   g.A = (const char*)A;
   g.lda_b = lda * 2;
@@ -951,20 +998,29 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   g.M = M;
   g.N = N;
   g.K = K;
-  // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
-  const bool big = sr::tune(SR_TUNE_WGRAD256) != 0 && N % WT2 == 0 && K % WT2 == 0;
-  const bool st3 = big && sr::tune(SR_TUNE_WGRAD_STAGES) == 3;
-  const int mt = st3 ? 48 : 64;  // rows per m-tile
   g.mtiles = (M + mt - 1) / mt;
   splits = std::min(splits, g.mtiles);
   g.mt_per_split = (g.mtiles + splits - 1) / splits;
   splits = (g.mtiles + g.mt_per_split - 1) / g.mt_per_split;
+  return g;
+}
+}  // namespace
+
+extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, const void* B, int64_t ldb, float* dW,
+                             int64_t lddw, int M, int N, int K, int accumulate, const float* rowscale,
+                             const float* wdot, int64_t ldwd, float* rowdot, int splits, float* workspace) {
+  const int rc = wgrad_check(A, lda, B, ldb, dW, lddw, M, N, K, wdot, ldwd, rowdot, splits, workspace);
+  if (rc != SR_OK) return rc;
+  // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
+  const bool big = sr::tune(SR_TUNE_WGRAD256) != 0 && N % WT2 == 0 && K % WT2 == 0;
+  const bool st3 = big && sr::tune(SR_TUNE_WGRAD_STAGES) == 3;
+  const WgradArgs g = wgrad_args(A, lda, B, ldb, M, N, K, st3 ? 48 : 64, splits, workspace);
   hipStream_t s = (hipStream_t)stream;
   if (st3) {
-    hipLaunchKernelGGL((wgrad256_kernel<48, 3>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
+    hipLaunchKernelGGL((wgrad256_kernel<48, 3>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g, g, splits);
     sr::note_kernel("wgrad256_kernel<48, 3>");
   } else if (big) {
-    hipLaunchKernelGGL((wgrad256_kernel<64, 2>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g);
+    hipLaunchKernelGGL((wgrad256_kernel<64, 2>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g, g, splits);
     sr::note_kernel("wgrad256_kernel");
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3((N / WT) * (K / WT), splits), dim3(256), 0, s, g);
@@ -973,6 +1029,34 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, workspace, splits, N, K, dW, lddw, accumulate,
                      rowscale, wdot, ldwd, rowdot);
   return sr::check_launch("sr_gemm_wgrad");
+}
+
+extern "C" int sr_gemm_wgrad_pair(sr_stream_t stream, const sr_wgrad_problem* p) {
+  SR_CHECK(p, SR_EINVAL, "sr_gemm_wgrad_pair: null problems");
+  for (int i = 0; i < 2; ++i) {
+    const int rc = wgrad_check(p[i].A, p[i].lda, p[i].B, p[i].ldb, p[i].dW, p[i].lddw, p[i].M, p[i].N, p[i].K,
+                               p[i].wdot, p[i].ldwd, p[i].rowdot, p[i].splits, p[i].workspace);
+    if (rc != SR_OK) return rc;
+  }
+  const int N = p[0].N, K = p[0].K;
+  SR_CHECK(p[1].N == N && p[1].K == K && N % WT2 == 0 && K % WT2 == 0, SR_EUNSUPPORTED,
+           "sr_gemm_wgrad_pair: both problems need the same N, K, multiples of %d (%dx%d, %dx%d)", WT2, N, K, p[1].N,
+           p[1].K);
+  SR_CHECK(sr::tune(SR_TUNE_WGRAD256) != 0, SR_EUNSUPPORTED, "sr_gemm_wgrad_pair: needs the 256x256 kernel");
+  const bool st3 = sr::tune(SR_TUNE_WGRAD_STAGES) == 3;
+  int sp[2] = {p[0].splits, p[1].splits};
+  WgradArgs g[2];
+  for (int i = 0; i < 2; ++i)
+    g[i] = wgrad_args(p[i].A, p[i].lda, p[i].B, p[i].ldb, p[i].M, N, K, st3 ? 48 : 64, sp[i], p[i].workspace);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((N / WT2) * (K / WT2), sp[0] + sp[1]);
+  if (st3) hipLaunchKernelGGL((wgrad256_kernel<48, 3>), grid, dim3(512), 0, s, g[0], g[1], sp[0]);
+  else hipLaunchKernelGGL((wgrad256_kernel<64, 2>), grid, dim3(512), 0, s, g[0], g[1], sp[0]);
+  sr::note_kernel(st3 ? "wgrad256_kernel<48, 3>" : "wgrad256_kernel");
+  for (int i = 0; i < 2; ++i)
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, p[i].workspace, sp[i], N, K, p[i].dW, p[i].lddw,
+                       p[i].accumulate, p[i].rowscale, p[i].wdot, p[i].ldwd, p[i].rowdot);
+  return sr::check_launch("sr_gemm_wgrad_pair");
 }
 
 extern "C" int64_t sr_colsum_workspace_floats(int M, int N) {
@@ -1033,17 +1117,9 @@ extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, i
       return SR_EUNSUPPORTED;
   }
 #undef LNB_CASE
-  if (want) {  // partial rows [wgs*4][np*cols] -> dw | db (| dx_colsum, assigned)
-    float* tail = workspace + (int64_t)wgs * 4 * np * cols;
-    int rc = colsum_launch(s, SR_F32, workspace, np * cols, wgs * 4, cols, dw, 1, 1.f, tail);
-    if (rc) return rc;
-    rc = colsum_launch(s, SR_F32, workspace + cols, np * cols, wgs * 4, cols, db, 1, 1.f, tail);
-    if (rc) return rc;
-    if (want_sum) {
-      rc = colsum_launch(s, SR_F32, workspace + 2 * cols, np * cols, wgs * 4, cols, dx_colsum, 0, 1.f, tail);
-      if (rc) return rc;
-    }
-  }
+  if (want)  // partial rows [wgs*4][np*cols] -> dw | db (| dx_colsum, assigned), one launch
+    hipLaunchKernelGGL(lnb_final_kernel, dim3((unsigned)((np * cols / 4 + 3) / 4)), dim3(256), 0, s, workspace,
+                       wgs * 4, cols, np, dw, db, dx_colsum);
   return sr::check_launch("sr_layernorm_bwd");
 }
 

@@ -50,6 +50,14 @@ class GemmProblem(ctypes.Structure):
     ]
 
 
+class WgradProblem(ctypes.Structure):
+    _fields_ = [
+        ("A", _vp), ("lda", _i64), ("B", _vp), ("ldb", _i64), ("dW", _vp), ("lddw", _i64),
+        ("M", _i32), ("N", _i32), ("K", _i32), ("accumulate", _i32),
+        ("rowscale", _vp), ("wdot", _vp), ("ldwd", _i64), ("rowdot", _vp), ("splits", _i32), ("workspace", _vp),
+    ]
+
+
 class AttnDesc(ctypes.Structure):
     _fields_ = [
         ("q", _vp), ("ldq", _i64),
@@ -165,6 +173,7 @@ _PROTOS = {
     "sr_pose_update_f32": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _i32]),
     "sr_pose_decode_f32": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     # training step
+    "sr_gemm_wgrad_pair": (_i32, [_vp, ctypes.POINTER(WgradProblem)]),
     "sr_gemm_wgrad": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp,
                              _i32, _vp]),
     "sr_colsum": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i32, _f32, _vp, _i64]),

@@ -10,7 +10,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -1098,6 +1098,53 @@ def gemm_wgrad(dy: Tensor, x: Tensor, dw: Tensor, *, accumulate: bool = False, r
     check(rc, "sr_gemm_wgrad")
     if timed:
         TIMER.stop(tag, ev0, 2.0 * M * N * K, 2 * M * (N + K) + 4 * N * K * (3 if accumulate else 2))
+
+
+def wgrad_pair_splits(M0: int, M1: int, N: int, K: int) -> Optional[Tuple[int, int]]:
+    """Slices per problem when two gemm_wgrad problems of equal N, K share one launch
+    (gemm_wgrad_pair), or None where that does not pay: both problems' slices must fill one round
+    of 256 workgroups exactly as one problem alone would (256 / tiles even: proj / fc1 / fc2 at
+    C = 1,024, not qkv's 48 tiles), so each slice walks twice the m-tiles and the two launches'
+    fixed costs and half the fp32 partials go."""
+    if not get_tuning("SR_WGRAD256") or N % 256 or K % 256:
+        return None
+    tiles = (N // 256) * (K // 256)
+    per = 256 // tiles
+    if per < 2 or per % 2:
+        return None
+    s = min(per // 2, 16)
+    return max(1, min(s, -(-M0 // 64) // 8)), max(1, min(s, -(-M1 // 64) // 8))
+
+
+def gemm_wgrad_pair(probs, splits: Tuple[int, int], tag: Optional[str] = None) -> None:
+    """Two gemm_wgrad problems (dicts: dy, x, dw and gemm_wgrad's accumulate / rowscale / wdot /
+    rowdot keywords) of equal N, K in one launch (sr_gemm_wgrad_pair), ``splits`` slices each."""
+    if len(probs) != 2:
+        raise ValueError("gemm_wgrad_pair: exactly two problems")
+    arr = (_lib.WgradProblem * 2)()
+    flops = nbytes = 0.0
+    for i, p in enumerate(probs):
+        dy, x, dw = p["dy"], p["x"], p["dw"]
+        M, N = dy.shape
+        K = x.shape[1]
+        if x.shape[0] != M or dw.shape != (N, K) or dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 \
+                or dw.dtype != torch.float32:
+            raise ValueError(f"gemm_wgrad_pair: dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)} mismatch")
+        q = arr[i]
+        q.A, q.lda, q.B, q.ldb = _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x")
+        q.dW, q.lddw = _p(dw), _rowmajor(dw, "dw")
+        q.M, q.N, q.K, q.accumulate = M, N, K, int(p.get("accumulate", False))
+        q.rowscale, q.wdot, q.rowdot = _p(p.get("rowscale")), _p(p.get("wdot")), _p(p.get("rowdot"))
+        q.ldwd = 0 if p.get("wdot") is None else _rowmajor(p["wdot"], "wdot")
+        q.splits = int(splits[i])
+        q.workspace = _p(_train_ws(dy.device, f"wgrad{i}", splits[i] * N * K))
+        flops += 2.0 * M * N * K
+        nbytes += 2 * M * (N + K) + 4 * N * K * (3 if q.accumulate else 2)
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    check(_lib.load().sr_gemm_wgrad_pair(_stream(probs[0]["dy"]), arr), "sr_gemm_wgrad_pair")
+    if timed:
+        TIMER.stop(tag, ev0, flops, nbytes)
 
 
 def colsum(x: Tensor, out: Tensor, *, rows: Optional[int] = None, cols: Optional[int] = None,

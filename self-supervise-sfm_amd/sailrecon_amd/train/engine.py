@@ -25,6 +25,7 @@ weight-gradient kernel and the masked fp32 attention backward.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -50,6 +51,9 @@ class BlockTape:
 
 
 TAIL_ROWS = 64
+# SR_TRAIN_PAIR_WGRAD (default 1; 0 for the A/B): block_bwd_multi's two items share weight-grad
+# launches (ops.gemm_wgrad_pair) where ops.wgrad_pair_splits says it pays
+_PAIR_WGRAD = os.environ.get("SR_TRAIN_PAIR_WGRAD", "1") != "0"
 
 
 def alloc_tape(rows: int, dim: int, hidden: int, dtype: torch.dtype, device, lse_numel: int,
@@ -79,6 +83,55 @@ def run_block_train(pb: runtime.PackedBlock, x: Tensor, r0: int, r1: int, tape: 
     ops.layernorm(xs, pb.ln2_w, pb.ln2_b, pb.eps, tape.xn2, x_copy=tape.x1)  # x1 = x likewise
     ops.gemm(tape.xn2, pb.w_fc1, tape.h, _lib.SR_EPI_BIAS_GELU, bias=pb.b_fc1, aux=tape.u, tag="gemm")
     ops.gemm(tape.h, pb.w_fc2, xs, _lib.SR_EPI_BIAS_RESID, bias=pb.b_fc2, gamma=pb.g2, tag="gemm")
+
+
+def run_block_train_multi(items) -> None:
+    """run_block_train for several independent block applications of equal width at once (the
+    layer's reloc and global blocks: different weights, disjoint rows of x, the reloc block's
+    anchor K|V already projected): stage by stage in run_block_train's order, each GEMM of all
+    items as ONE grouped launch (sr_gemm_group) whose last partial round the items share.  At C4
+    each item's N = 1,024 GEMMs (proj, fc2) are 344 tiles of 256^2, which sr_gemm alone runs on
+    the 128^2 kernel; grouped they run on the 256^2 kernel, whose results differ from it by fp32
+    accumulation order only (gemm_resid 41.7 -> 38.9 ms per C4 step, profiles/r05_j29_*).  fc1
+    stays one launch per item.  ``items``: dicts of run_block_train's arguments (pb, x, r0, r1,
+    tape, attend, qkv_epi); their attentions run in list order."""
+    if len(items) == 1 or not all(it["tape"].xn1.dtype == torch.bfloat16 for it in items) or \
+            len({(it["pb"].dim, it["tape"].u.shape[1]) for it in items}) != 1 or \
+            len({it["qkv_epi"] is None for it in items}) != 1:
+        for it in items:
+            run_block_train(it["pb"], it["x"], it["r0"], it["r1"], it["tape"], it["attend"], it["qkv_epi"])
+        return
+
+    def group(epi, probs):
+        if ops.gemm_group_eligible(probs):
+            ops.gemm_group(probs, epi, tag="gemm")
+        else:
+            for q in probs:
+                ops.gemm(q["a"], q["w"], q["out"], epi, bias=q.get("bias"), gamma=q.get("gamma"), qkv=q.get("qkv"),
+                         aux=q.get("aux"), tag="gemm")
+
+    for it in items:
+        it["_xs"] = it["x"][it["r0"]:it["r1"]]
+        ops.layernorm(it["_xs"], it["pb"].ln1_w, it["pb"].ln1_b, it["pb"].eps, it["tape"].xn1, x_copy=it["tape"].x0)
+    if items[0]["qkv_epi"] is None:
+        group(_lib.SR_EPI_BIAS, [dict(a=it["tape"].xn1, w=it["pb"].w_qkv, out=it["tape"].qkv, bias=it["pb"].b_qkv)
+                                 for it in items])
+    else:
+        group(_lib.SR_EPI_QKV, [dict(a=it["tape"].xn1, w=it["pb"].w_qkv, out=it["tape"].qkv, bias=it["pb"].b_qkv,
+                                     qkv=it["qkv_epi"], aux=it["tape"].raw) for it in items])
+    for it in items:
+        it["attend"](it["tape"].qkv, it["tape"].o, it["tape"].lse)
+    group(_lib.SR_EPI_BIAS_RESID, [dict(a=it["tape"].o, w=it["pb"].w_proj, out=it["_xs"], bias=it["pb"].b_proj,
+                                        gamma=it["pb"].g1) for it in items])
+    for it in items:
+        ops.layernorm(it["_xs"], it["pb"].ln2_w, it["pb"].ln2_b, it["pb"].eps, it["tape"].xn2, x_copy=it["tape"].x1)
+    for it in items:  # fc1 apart: sr_gemm's tail split beats the group here (35.5 vs 34.9 ms/step, j29)
+        ops.gemm(it["tape"].xn2, it["pb"].w_fc1, it["tape"].h, _lib.SR_EPI_BIAS_GELU, bias=it["pb"].b_fc1,
+                 aux=it["tape"].u, tag="gemm")
+    group(_lib.SR_EPI_BIAS_RESID, [dict(a=it["tape"].h, w=it["pb"].w_fc2, out=it["_xs"], bias=it["pb"].b_fc2,
+                                        gamma=it["pb"].g2) for it in items])
+    for it in items:
+        it.pop("_xs")
 
 
 # ----------------------------------------------------------------------------- parameters
@@ -296,6 +349,22 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         if db is not None:
             ops.colsum(dy, db, accumulate=True)
 
+    def wgrads(args):
+        """One stage's weight grads of every item: (it, dy, x, dw, db, rowscale, wdot, rowdot) each;
+        two items of one weight shape share one launch where ops.wgrad_pair_splits says it pays."""
+        sp = None
+        if _PAIR_WGRAD and len(args) == 2 and args[0][3].shape == args[1][3].shape:
+            sp = ops.wgrad_pair_splits(args[0][1].shape[0], args[1][1].shape[0], *args[0][3].shape)
+        if sp is None:
+            for a in args:
+                wgrad(*a)
+            return
+        ops.gemm_wgrad_pair([dict(dy=a[1], x=a[2], dw=a[3], accumulate=True, rowscale=a[5], wdot=a[6], rowdot=a[7])
+                             for a in args], sp, tag=tag + ".wgrad")
+        for a in args:
+            if a[4] is not None:
+                ops.colsum(a[1], a[4], accumulate=True)
+
     for it in items:
         R = it["dx"].shape[0]
         it["_tmp"] = it["sc"].get("colsum_tmp", 1, max(C, Hd, 3 * C), torch.float32, dev)[0]
@@ -304,24 +373,24 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         it["_dO"] = it["sc"].get("dO", R, C, dt, dev)
     # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
     dgrad(_lib.SR_EPI_GELU_BWD, [dict(a=it["dxb"], w=it["bp"].wt_fc2, out=it["_dU"], aux=it["tape"].u) for it in items])
+    wgrads([(it, it["dxb"], it["tape"].h, it["g"].w_fc2, None, it["pb"].g2,
+             it["bp"].w_fc2 if it["g"].g2 is not None else None, it["g"].g2) for it in items])
     for it in items:
         pb, bp, g = it["pb"], it["bp"], it["g"]
-        wgrad(it, it["dxb"], it["tape"].h, g.w_fc2, rowscale=pb.g2, wdot=bp.w_fc2 if g.g2 is not None else None,
-              rowdot=g.g2 if g.g2 is not None else None)
         _resid_param_grads(it["dx"], bp.b_fc2, pb.g2, g.b_fc2, g.g2, it["_tmp"][:C])
     dgrad(_lib.SR_EPI_F32, [dict(a=it["_dU"], w=it["bp"].wt_fc1, out=it["_dxn"]) for it in items])
+    wgrads([(it, it["_dU"], it["tape"].xn2, it["g"].w_fc1, it["g"].b_fc1, None, None, None) for it in items])
     for it in items:
         pb, bp, g = it["pb"], it["bp"], it["g"]
-        wgrad(it, it["_dU"], it["tape"].xn2, g.w_fc1, db=g.b_fc1)
         it["_fused"] = g.ln2_w is not None and C <= 2048 and _resid_wants_sum(bp.b_proj, g.b_proj, g.g1)
         ops.layernorm_bwd(it["tape"].x1, it["_dxn"], pb.ln2_w, pb.eps, it["dx"], dxb=it["dxb"], dw=g.ln2_w,
                           db=g.ln2_b, dx_sum=it["_tmp"][:C] if it["_fused"] else None)
     # ---- attention: x1 = x0 + g1 * proj(attn(qk(qkv(LN1(x0)))))
     dgrad(_lib.SR_EPI_BIAS, [dict(a=it["dxb"], w=it["bp"].wt_proj, out=it["_dO"]) for it in items])
+    wgrads([(it, it["dxb"], it["tape"].o, it["g"].w_proj, None, it["pb"].g1,
+             it["bp"].w_proj if it["g"].g1 is not None else None, it["g"].g1) for it in items])
     for it in items:
         pb, bp, g = it["pb"], it["bp"], it["g"]
-        wgrad(it, it["dxb"], it["tape"].o, g.w_proj, rowscale=pb.g1, wdot=bp.w_proj if g.g1 is not None else None,
-              rowdot=g.g1 if g.g1 is not None else None)
         _resid_param_grads(it["dx"], bp.b_proj, pb.g1, g.b_proj, g.g1, it["_tmp"][:C], summed=it["_fused"])
     for it in items:
         R = it["dx"].shape[0]
@@ -332,9 +401,9 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         ops.qk_bwd(it["tape"].raw if qkv_epi is not None else None, dqkv, it["_draw"],
                    qkv_epi or dict(embed_dim=C, head_dim=64), grads=it["g"].qkn)
     dgrad(_lib.SR_EPI_F32, [dict(a=it["_draw"], w=it["bp"].wt_qkv, out=it["_dxn"]) for it in items])
+    wgrads([(it, it["_draw"], it["tape"].xn1, it["g"].w_qkv, it["g"].b_qkv, None, None, None) for it in items])
     for it in items:
         pb, g = it["pb"], it["g"]
-        wgrad(it, it["_draw"], it["tape"].xn1, g.w_qkv, db=g.b_qkv)
         ops.layernorm_bwd(it["tape"].x0, it["_dxn"], pb.ln1_w, pb.eps, it["dx"], dxb=it["dxb"], dw=g.ln1_w,
                           db=g.ln1_b)
 

@@ -36,6 +36,9 @@ F32 = torch.float32
 # SR_TRAIN_PAIR_DGRAD (default 1; 0 for the A/B): the layer's reloc and global blocks run their
 # backward stage by stage with each stage's dgrad GEMMs grouped into one launch
 _PAIR_DGRAD = os.environ.get("SR_TRAIN_PAIR_DGRAD", "1") != "0"
+# SR_TRAIN_PAIR_FWD (default 1; 0 for the A/B): their forward likewise, each GEMM of the two
+# blocks as one grouped launch (engine.run_block_train_multi)
+_PAIR_FWD = os.environ.get("SR_TRAIN_PAIR_FWD", "1") != "0"
 
 
 def _i32(rows, dev) -> Tensor:
@@ -246,12 +249,18 @@ class TrainGraph:
                 ops.gemm(xn_sub, pr.w_qkv[C:], kv_sub, _lib.SR_EPI_QKV, bias=_sl(pr.b_qkv, C, 3 * C), qkv=epi,
                          aux=kv_raw, tag="gemm")
             rfwd, _ = self._reloc_attn(pr, kv_sub, None, Nq, P, n_sub)
-            engine.run_block_train(pr, x, q0, R, self._tape(("reloc", l), R - q0, C, hidden, BF16,
-                                                            Nq * pr.heads * P, True),
-                                   rfwd, runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
+            rel = dict(pb=pr, x=x, r0=q0, r1=R, tape=self._tape(("reloc", l), R - q0, C, hidden, BF16,
+                                                                Nq * pr.heads * P, True),
+                       attend=rfwd, qkv_epi=runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
             gfwd, _ = self._global_attn(pg, q0)
-            engine.run_block_train(pg, x, 0, q0, self._tape(("global", l), q0, C, hidden, BF16, pg.heads * q0, True),
-                                   gfwd, runtime.qkv_params(pg, rope, pos_row_base=0, **posctx))
+            glo = dict(pb=pg, x=x, r0=0, r1=q0, tape=self._tape(("global", l), q0, C, hidden, BF16, pg.heads * q0, True),
+                       attend=gfwd, qkv_epi=runtime.qkv_params(pg, rope, pos_row_base=0, **posctx))
+            if _PAIR_FWD:  # disjoint rows; the reloc block's anchor K|V was projected above
+                engine.run_block_train_multi([rel, glo])
+            else:
+                for it in (rel, glo):
+                    engine.run_block_train(it["pb"], it["x"], it["r0"], it["r1"], it["tape"], it["attend"],
+                                           it["qkv_epi"])
             if l == agg.depth - 1:
                 ops.copy_rows(cam_in[:, C:], x, S, rowmap=cam_rows)
         self.state = st

@@ -43,7 +43,8 @@ def test_ctypes_struct_layout_matches_c(debug_build):
     r = _run(debug_build, "layout")
     assert r.returncode == 0, r.stderr
     lay = json.loads(r.stdout)
-    mirror = {"sr_gemm_epi": _lib.GemmEpi, "sr_gemm_problem": _lib.GemmProblem, "sr_attn_desc": _lib.AttnDesc,
+    mirror = {"sr_gemm_epi": _lib.GemmEpi, "sr_gemm_problem": _lib.GemmProblem, "sr_wgrad_problem": _lib.WgradProblem,
+              "sr_attn_desc": _lib.AttnDesc,
               "sr_attn_bwd_desc": _lib.AttnBwdDesc, "sr_imc_loss_desc": _lib.ImcLossDesc,
               "sr_weight_item": _lib.WeightItem}
     assert set(lay) == set(mirror)

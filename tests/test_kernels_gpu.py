@@ -493,14 +493,18 @@ def test_small_fp32_ops(ops):
     assert rel(ext.cpu(), re[0]) < 1e-6 and rel(intr.cpu(), ri[0]) < 1e-6
 
 
-@pytest.mark.parametrize("epi_name", ["QKV", "BIAS", "BIAS_RESID"])
+@pytest.mark.parametrize("epi_name", ["QKV", "BIAS", "BIAS_RESID", "BIAS_GELU_AUX", "QKV_AUX"])
 def test_gemm_group(ops, epi_name):
     """sr_gemm_group: 3 independent bf16 GEMMs of one epilogue in ONE 256x256 launch (different M
     and N, one problem's workgroup count not a multiple of 8) are bit-identical to the same
     problems launched apart on the 256x256 kernel (>= 512 tiles each) -- and, QKV, the layer's
-    query / anchor / subsample-K|V projections with the qk-LayerNorm + RoPE epilogue."""
+    query / anchor / subsample-K|V projections with the qk-LayerNorm + RoPE epilogue.  *_AUX: with
+    the training forward's saved pre-activation / pre-norm q|k|v output (aux), as
+    train.engine.run_block_train_multi groups the layer's reloc and global blocks."""
     from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
     L = _lib()
+    with_aux = epi_name.endswith("_AUX")
+    epi_name = epi_name[:-4] if with_aux else epi_name
     epi = getattr(L, "SR_EPI_" + epi_name)
     C, H, D, P, gw = 1024, 16, 64, 21, 4
     g = torch.Generator(device=DEV).manual_seed(3)
@@ -526,16 +530,21 @@ def test_gemm_group(ops, epi_name):
         else:
             p["out"] = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
             ref_out = torch.empty_like(p["out"])
+        if with_aux:
+            p["aux"] = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            p["ref_aux"] = torch.empty_like(p["aux"])
         probs.append(p)
         plain.append(ref_out)
     ops.gemm_group(probs, epi)
     with ops.tuning(SR_GEMM_TAIL=0):  # sr_gemm on the 256x256 kernel alone (no 128x128 tail launch)
         for p, ref_out in zip(probs, plain):
             ops.gemm(p["a"], p["w"], ref_out, epi, bias=p["bias"], gamma=p.get("gamma"), qkv=p.get("qkv"),
-                     splits=1)
+                     aux=p.get("ref_aux"), splits=1)
     torch.cuda.synchronize()
     for p, ref_out in zip(probs, plain):
         assert torch.equal(p["out"], ref_out)
+        if with_aux:
+            assert torch.equal(p["aux"], p["ref_aux"])
 
 
 @pytest.mark.parametrize("epi_name", ["F32", "GELU_BWD"])

@@ -73,6 +73,43 @@ def test_gemm_wgrad_strided_accumulate_rowscale_rowdot(ops, K):
     assert rel(rowdot - rd0, (wdot * G).sum(1)) < 1e-5
 
 
+@pytest.mark.parametrize("stages", [2, 3])
+@pytest.mark.parametrize("M0, M1, N, K", [(21984, 21984, 1024, 4096), (21984, 4397, 1024, 1024),
+                                          (777, 1300, 256, 512)])
+def test_gemm_wgrad_pair(ops, M0, M1, N, K, stages):
+    """sr_gemm_wgrad_pair (the layer's reloc and global blocks' weight grads in one launch, as
+    train.engine.block_bwd_multi runs them): per problem bit-identical to sr_gemm_wgrad with the
+    same slices, with accumulate / rowscale / rowdot on one problem and not the other; and within
+    fp32 rounding of dy^T x."""
+    torch.manual_seed(4)
+    probs, refs = [], []
+    for i, M in enumerate((M0, M1)):
+        dy = torch.randn(M, N, device=DEV).bfloat16()
+        x = torch.randn(M, K, device=DEV).bfloat16()
+        dw0 = torch.randn(N, K, device=DEV)
+        p = dict(dy=dy, x=x, dw=dw0.clone())
+        if i == 0:
+            p.update(accumulate=True, rowscale=torch.randn(N, device=DEV), wdot=torch.randn(N, K, device=DEV),
+                     rowdot=torch.zeros(N, device=DEV))
+        probs.append(p)
+        refs.append(dict(p, dw=dw0.clone(), rowdot=None if i else torch.zeros(N, device=DEV)))
+    sp = ops.wgrad_pair_splits(M0, M1, N, K) or (3, 5)
+    with ops.tuning(SR_WGRAD_STAGES=stages):
+        ops.gemm_wgrad_pair(probs, sp)
+        for r, s in zip(refs, sp):
+            ops.gemm_wgrad(r["dy"], r["x"], r["dw"], accumulate=r.get("accumulate", False), rowscale=r.get("rowscale"),
+                           wdot=r.get("wdot"), rowdot=r.get("rowdot"), splits=s)
+    torch.cuda.synchronize()
+    for i, (p, r) in enumerate(zip(probs, refs)):
+        assert torch.equal(p["dw"], r["dw"])
+        G = p["dy"].float().t() @ p["x"].float()
+        if i == 0:
+            assert torch.equal(p["rowdot"], r["rowdot"])
+            assert rel(p["rowdot"], (p["wdot"] * G).sum(1)) < 1e-5
+        else:
+            assert rel(p["dw"], G) < 1e-5
+
+
 def test_gemm_f32_and_gelu_bwd_epilogues(ops):
     torch.manual_seed(2)
     lib = L()
