@@ -101,24 +101,28 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int row0, const int 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 
 // ---------------------------------------------------------------- delta = rowsum(dO * O)
+// Eight lanes per (row, head), one 16-B chunk of the head's 64 columns each, heads fastest: a wave
+// reads 8 heads x 128 B of one row contiguously.  Each lane's 8 products, then a fixed xor tree
+// over the 8 lanes (deterministic).
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(sr_attn_bwd_desc b) {
   const sr_attn_desc& f = b.f;
-  const int64_t n = (int64_t)f.batch * f.heads * f.lq;
+  const int64_t n = (int64_t)f.batch * f.heads * f.lq * 8;
+  const int c = threadIdx.x & 7;
   for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
-    const int row = (int)(e % f.lq);
-    const int64_t ih = e / f.lq;
-    const int head = (int)(ih % f.heads), item = (int)(ih / f.heads);
+    const int64_t gi = e >> 3;  // (item, row, head), head fastest
+    const int head = (int)(gi % f.heads);
+    const int64_t ir = gi / f.heads;
+    const int row = (int)(ir % f.lq), item = (int)(ir / f.lq);
     const int64_t r = (int64_t)item * f.q_bstride + row;
-    const bf16* o = (const bf16*)f.o + r * f.ldo + head * 64;
-    const bf16* g = (const bf16*)b.dout + r * b.lddo + head * 64;
+    const bf16x8 ov = *(const bf16x8*)((const bf16*)f.o + r * f.ldo + head * 64 + 8 * c);
+    const bf16x8 gv = *(const bf16x8*)((const bf16*)b.dout + r * b.lddo + head * 64 + 8 * c);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const bf16x8 ov = *(const bf16x8*)(o + 8 * c), gv = *(const bf16x8*)(g + 8 * c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s = fmaf((float)ov[j], (float)gv[j], s);
-    }
-    b.delta[e] = -s;  // stored negated: it seeds the dP chains as is
+    for (int j = 0; j < 8; ++j) s = fmaf((float)ov[j], (float)gv[j], s);
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    if (c == 0) b.delta[((int64_t)item * f.heads + head) * f.lq + row] = -s;  // negated: seeds the dP chains
   }
 }
 
@@ -854,7 +858,7 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
            SR_EINVAL, "sr_attention_bwd: leading dims (bf16 multiples of 8, fp32 multiples of 4)");
   hipStream_t s = (hipStream_t)stream;
   const int64_t nrows = (int64_t)f.batch * f.heads * f.lq;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 20)),
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)std::min<int64_t>((nrows * 8 + 255) / 256, 1 << 20)),
                      dim3(256), 0, s, b);
   // dQ: the hand-scheduled sweep (SR_ATTN_BWD_DQ_PIPE) where every key segment has at least 4 full
   // tiles and 32-bit per-lane DMA offsets, and where its 256-query workgroups pad the query count by
