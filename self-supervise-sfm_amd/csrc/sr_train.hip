@@ -1204,6 +1204,34 @@ __global__ __launch_bounds__(256) void weight_refresh_kernel(WeightRefresh wr) {
   const sr_weight_item& w = wr.it[p];
   const int t = blockIdx.x - wr.start[p], ntc = (w.cols + 63) / 64;
   const int r0 = (t / ntc) * 64, c0 = (t % ntc) * 64;
+  // whole tile with 16-B source rows and 8-B bf16 destination rows (the aggregator's weights):
+  // float4 loads, bf16x4 stores of the cast and of the transpose (same values as the scalar path)
+  const bool vec = r0 + 64 <= w.rows && c0 + 64 <= w.cols && (w.lds & 3) == 0 && ((uintptr_t)w.src & 15) == 0 &&
+                   (!w.cast || ((w.ldc & 3) == 0 && ((uintptr_t)w.cast & 7) == 0)) &&
+                   (!w.trans || ((w.ldt & 3) == 0 && ((uintptr_t)w.trans & 7) == 0));
+  if (vec) {
+    const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // column quad, row (+16 i)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rr + 16 * i;
+      f32x4 v = *(const f32x4*)(w.src + (int64_t)(r0 + r) * w.lds + c0 + 4 * q);
+      if (w.cast)
+        *(bf16x4*)((bf16*)w.cast + (int64_t)(r0 + r) * w.ldc + c0 + 4 * q) =
+            bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      if (w.rowscale) v *= w.rowscale[r0 + r];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tile[r][4 * q + j] = v[j];
+    }
+    if (!w.trans) return;  // workgroup-uniform
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // transposed row c0 + c, rows r0 + 4q .. + 3
+      const int c = rr + 16 * i;
+      *(bf16x4*)((bf16*)w.trans + (int64_t)(c0 + c) * w.ldt + r0 + 4 * q) =
+          bf16x4{(bf16)tile[4 * q][c], (bf16)tile[4 * q + 1][c], (bf16)tile[4 * q + 2][c], (bf16)tile[4 * q + 3][c]};
+    }
+    return;
+  }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int r = r0 + i, c = c0 + tx;
