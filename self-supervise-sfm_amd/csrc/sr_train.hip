@@ -718,6 +718,21 @@ __global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict_
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found, 1);
 }
 
+// One element of the Adam update.  Contraction is off and the two FMAs are explicit, so the float4
+// path and the scalar tail round identically (one function, one rounding sequence).
+__device__ __forceinline__ void adam_elem(float g, float& p, float& m, float& v, float inv, float beta1, float beta2,
+                                          float eps, float wd, float bc2_sqrt, float step_size) {
+#pragma clang fp contract(off)
+  float gr = g * inv;
+  if (wd != 0.f) gr = gr + wd * p;
+  const float mn = fmaf(1.f - beta1, gr - m, m);  // lerp(m, g, 1 - beta1), weight < 0.5
+  const float vn = fmaf(1.f - beta2, gr * gr, beta2 * v);
+  const float denom = sqrtf(vn) / bc2_sqrt + eps;
+  p = p - step_size * (mn / denom);
+  m = mn;
+  v = vn;
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* p, const float* __restrict__ g, float* m, float* v,
                                                    int64_t n, float lr, float beta1, float beta2, float eps, float wd,
                                                    float bc1, float bc2_sqrt, const float* __restrict__ scale,
@@ -725,17 +740,34 @@ __global__ __launch_bounds__(256) void adam_kernel(float* p, const float* __rest
   if (found && *found) return;  // GradScaler.step skips the update on inf / nan
   const float inv = scale ? 1.f / *scale : 1.f;
   const float step_size = lr / bc1;
-  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
-    float gr = g[e] * inv;
-    const float pv = p[e];
-    if (wd != 0.f) gr += wd * pv;
-    const float mo = m[e];
-    const float mn = mo + (1.f - beta1) * (gr - mo);  // lerp(m, g, 1 - beta1), weight < 0.5
-    const float vn = beta2 * v[e] + (1.f - beta2) * gr * gr;
-    m[e] = mn;
-    v[e] = vn;
-    const float denom = sqrtf(vn) / bc2_sqrt + eps;
-    p[e] = pv - step_size * (mn / denom);
+  int64_t e0 = 0;
+  if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) {
+    // 16-B aligned (the flat parameter buffers): four elements per thread and iteration; the scalar
+    // loop below then takes the n % 4 tail
+    const int64_t n4 = n >> 2;
+    for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256) {
+      const f32x4 g4 = ((const f32x4*)g)[q];
+      f32x4 p4 = ((const f32x4*)p)[q], m4 = ((const f32x4*)m)[q], v4 = ((const f32x4*)v)[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pj = p4[j], mj = m4[j], vj = v4[j];
+        adam_elem(g4[j], pj, mj, vj, inv, beta1, beta2, eps, wd, bc2_sqrt, step_size);
+        p4[j] = pj;
+        m4[j] = mj;
+        v4[j] = vj;
+      }
+      ((f32x4*)m)[q] = m4;
+      ((f32x4*)v)[q] = v4;
+      ((f32x4*)p)[q] = p4;
+    }
+    e0 = n4 << 2;
+  }
+  for (int64_t e = e0 + blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    float pe = p[e], me = m[e], ve = v[e];
+    adam_elem(g[e], pe, me, ve, inv, beta1, beta2, eps, wd, bc2_sqrt, step_size);
+    m[e] = me;
+    v[e] = ve;
+    p[e] = pe;
   }
 }
 

@@ -314,6 +314,19 @@ def test_cast_nonfinite_adam(ops):
     ops.adam(p, g, m, v, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step=4, scale=scale,
              found_inf=found)
     assert torch.equal(p, p0)
+    # the 16-B aligned float4 path (with its n % 4 tail) equals the scalar path of misaligned views
+    vals = [torch.randn(n, device=DEV) for _ in range(4)]
+    vals[3] = vals[3].abs()  # second moments
+    al = [t.clone() for t in vals]
+    bufs = [torch.empty(n + 1, device=DEV) for _ in range(4)]
+    for b, t in zip(bufs, vals):
+        b[1:] = t
+    mis = [b[1:] for b in bufs]  # 4-B offset: the scalar loop
+    for a in (al, mis):
+        ops.adam(a[0], a[1], a[2], a[3], lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, step=5)
+    torch.cuda.synchronize()
+    for a, b in zip(al, mis):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("mask", [False, True])
