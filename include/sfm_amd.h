@@ -434,6 +434,12 @@ typedef struct sr_attn_bwd_desc {
 
 int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* d);
 
+/* The same gradient for fp32 operands (q / k / v / o / dout fp32; head_dim 64 | 128, no mask),
+ * exact fp32 on the VALU with the softmax recomputed from the forward's LSE (sr_attention with
+ * dtype SR_F32 and lse set): TrainGraph's fp32 mode (ABI 1.2), whose whole-graph gradients are
+ * checked against fp32 autograd.  Same outputs and batch-stride-0 summation as sr_attention_bwd. */
+int sr_attention_bwd_f32(sr_stream_t stream, const sr_attn_bwd_desc* d);
+
 /* ------------------------------------------------------------------------
  * Training step (train_imc.py:320-429, the backward of every
  * nn.Linear / LayerNorm / LayerScale / qk-norm + RoPE of the Blocks, and the Adam step).

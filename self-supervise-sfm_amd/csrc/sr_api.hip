@@ -96,7 +96,7 @@ int check_launch(const char* what) {
 
 extern "C" const char* sr_last_error(void) { return g_err; }
 extern "C" const char* sr_last_kernel(void) { return g_kernel; }
-extern "C" int sr_version(void) { return (1 << 16) | 1; }  // 1.1: sr_gemm_wgrad_pair
+extern "C" int sr_version(void) { return (1 << 16) | 2; }  // 1.1: sr_gemm_wgrad_pair; 1.2: sr_attention_bwd_f32
 
 extern "C" int sr_set_tuning(int key, int value) {
   SR_CHECK(key >= 0 && key < SR_TUNE_COUNT, SR_EINVAL, "sr_set_tuning: unknown key %d", key);

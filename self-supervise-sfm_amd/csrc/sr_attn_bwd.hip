@@ -952,3 +952,199 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
   sr::note_kernel("%s", name);
   return sr::check_launch("sr_attention_bwd");
 }
+
+// ---------------------------------------------------------------------------------------------
+// Exact fp32 attention backward (sr_attention_bwd_f32): the same gradient as above for fp32
+// operands, head_dim 64 | 128, any segment / batch layout of the forward, on the VALU in fp32
+// with the softmax recomputed from the forward's LSE.  It serves TrainGraph's fp32 mode, whose
+// gradients are checked against the oracle's fp32 autograd at 1e-4 (the bf16 graph can only be
+// held to the reference's own bf16 noise).  No MFMA, no atomics: a thread owns one query row
+// (dQ) or one key row (dK, dV; a key shared by every item sums over all of them in item order).
+namespace {
+
+constexpr int F32B_T = 128;  // rows (threads) per workgroup
+constexpr int F32B_KT = 16;  // rows per LDS tile
+
+__global__ __launch_bounds__(256) void attn_bwd_delta_f32_kernel(sr_attn_bwd_desc b) {
+  const sr_attn_desc& f = b.f;
+  const int64_t n = (int64_t)f.batch * f.heads * f.lq;
+  const int64_t ob = f.o_bstride ? f.o_bstride : f.q_bstride;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int row = (int)(e % f.lq);
+    const int64_t ih = e / f.lq;
+    const int head = (int)(ih % f.heads), item = (int)(ih / f.heads);
+    const int64_t r = (int64_t)item * ob + row;
+    const float* o = (const float*)f.o + r * f.ldo + (int64_t)head * f.head_dim;
+    const float* g = (const float*)b.dout + r * b.lddo + (int64_t)head * f.head_dim;
+    float s = 0.f;
+    for (int d = 0; d < f.head_dim; ++d) s = fmaf(g[d], o[d], s);
+    b.delta[e] = s;  // [item][head][row]
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(F32B_T) void attn_bwd_dq_f32_kernel(sr_attn_bwd_desc b) {
+  __shared__ float ks[F32B_KT][D];
+  __shared__ float vs[F32B_KT][D];
+  const sr_attn_desc& f = b.f;
+  const int tid = threadIdx.x, head = blockIdx.y, item = blockIdx.z;
+  const int hcol = head * D;
+  const int qrow = blockIdx.x * F32B_T + tid, qc = min(qrow, f.lq - 1);
+  const int64_t qr = (int64_t)item * f.q_bstride + qc;
+  const int64_t orow = (int64_t)item * (f.o_bstride ? f.o_bstride : f.q_bstride) + qc;
+  const float c = f.scale * 1.4426950408889634f;
+  float q[D], g[D], dq[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    q[i] = ((const float*)f.q)[qr * f.ldq + hcol + i];
+    g[i] = ((const float*)b.dout)[orow * b.lddo + hcol + i];
+    dq[i] = 0.f;
+  }
+  const int64_t st = ((int64_t)item * f.heads + head) * f.lq + qc;
+  const float lse = f.lse[st], dl = b.delta[st];
+  for (int seg = 0; seg < 2; ++seg) {
+    const int len = seg ? f.l1 : f.l0;
+    if (len <= 0) continue;
+    const float* kb = (const float*)(seg ? f.k1 : f.k0);
+    const float* vb = (const float*)(seg ? f.v1 : f.v0);
+    const int64_t ldk = seg ? f.ldk1 : f.ldk0, ldv = seg ? f.ldv1 : f.ldv0;
+    const int64_t rb = (int64_t)item * (seg ? f.k1_bstride : f.k0_bstride);
+    for (int t0 = 0; t0 < len; t0 += F32B_KT) {
+      const int n = min(F32B_KT, len - t0);
+      __syncthreads();
+      for (int e = tid; e < F32B_KT * D; e += F32B_T) {
+        const int r = e / D, cc = e - r * D, key = min(t0 + r, len - 1);
+        ks[r][cc] = kb[(rb + key) * ldk + hcol + cc];
+        vs[r][cc] = vb[(rb + key) * ldv + hcol + cc];
+      }
+      __syncthreads();
+      for (int j = 0; j < n; ++j) {
+        float s = 0.f, dp = 0.f;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          s = fmaf(q[i], ks[j][i], s);
+          dp = fmaf(g[i], vs[j][i], dp);
+        }
+        const float p = exp2f(s * c - lse);
+        const float ds = p * (dp - dl);
+#pragma unroll
+        for (int i = 0; i < D; ++i) dq[i] = fmaf(ds, ks[j][i], dq[i]);
+      }
+    }
+  }
+  if (qrow < f.lq) {
+    float* out = b.dq + qr * b.lddq + hcol;
+#pragma unroll
+    for (int i = 0; i < D; ++i) out[i] = dq[i] * f.scale;
+  }
+}
+
+// key rows of segment SEG: blockIdx.z = the item owning them (bstride > 0) or 0 (shared keys: every
+// item's queries, summed in item order)
+template <int D, int SEG>
+__global__ __launch_bounds__(F32B_T) void attn_bwd_dkdv_f32_kernel(sr_attn_bwd_desc b) {
+  __shared__ float qs[F32B_KT][D];
+  __shared__ float gs[F32B_KT][D];
+  __shared__ float ls[F32B_KT], dls[F32B_KT];
+  const sr_attn_desc& f = b.f;
+  const int tid = threadIdx.x, head = blockIdx.y;
+  const int hcol = head * D;
+  const int len = SEG ? f.l1 : f.l0;
+  const int64_t bstride = SEG ? f.k1_bstride : f.k0_bstride;
+  const bool shared = bstride == 0;
+  const int key = blockIdx.x * F32B_T + tid, kc = min(key, len - 1);
+  const int64_t kr = (shared ? 0 : (int64_t)blockIdx.z * bstride) + kc;
+  const float* kb = (const float*)(SEG ? f.k1 : f.k0);
+  const float* vb = (const float*)(SEG ? f.v1 : f.v0);
+  const int64_t ldk = SEG ? f.ldk1 : f.ldk0, ldv = SEG ? f.ldv1 : f.ldv0;
+  const int64_t ob = f.o_bstride ? f.o_bstride : f.q_bstride;
+  const float c = f.scale * 1.4426950408889634f;
+  float k[D], v[D], dk[D], dv[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    k[i] = kb[kr * ldk + hcol + i];
+    v[i] = vb[kr * ldv + hcol + i];
+    dk[i] = 0.f;
+    dv[i] = 0.f;
+  }
+  const int i0 = shared ? 0 : blockIdx.z, i1 = shared ? f.batch : blockIdx.z + 1;
+  for (int item = i0; item < i1; ++item) {
+    for (int t0 = 0; t0 < f.lq; t0 += F32B_KT) {
+      const int n = min(F32B_KT, f.lq - t0);
+      __syncthreads();
+      for (int e = tid; e < F32B_KT * D; e += F32B_T) {
+        const int r = e / D, cc = e - r * D, row = min(t0 + r, f.lq - 1);
+        qs[r][cc] = ((const float*)f.q)[((int64_t)item * f.q_bstride + row) * f.ldq + hcol + cc];
+        gs[r][cc] = ((const float*)b.dout)[((int64_t)item * ob + row) * b.lddo + hcol + cc];
+      }
+      if (tid < F32B_KT) {
+        const int64_t stt = ((int64_t)item * f.heads + head) * f.lq + min(t0 + tid, f.lq - 1);
+        ls[tid] = f.lse[stt];
+        dls[tid] = b.delta[stt];
+      }
+      __syncthreads();
+      for (int j = 0; j < n; ++j) {
+        float s = 0.f, dp = 0.f;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          s = fmaf(qs[j][i], k[i], s);
+          dp = fmaf(gs[j][i], v[i], dp);
+        }
+        const float p = exp2f(s * c - ls[j]);
+        const float ds = p * (dp - dls[j]);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          dv[i] = fmaf(p, gs[j][i], dv[i]);
+          dk[i] = fmaf(ds, qs[j][i], dk[i]);
+        }
+      }
+    }
+  }
+  if (key < len) {
+    float* odk = (SEG ? b.dk1 : b.dk0) + kr * (SEG ? b.lddk1 : b.lddk0) + hcol;
+    float* odv = (SEG ? b.dv1 : b.dv0) + kr * (SEG ? b.lddv1 : b.lddv0) + hcol;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      odk[i] = dk[i] * f.scale;
+      odv[i] = dv[i];
+    }
+  }
+}
+
+template <int D>
+void launch_bwd_f32(const sr_attn_bwd_desc& b, hipStream_t s) {
+  const sr_attn_desc& f = b.f;
+  hipLaunchKernelGGL(attn_bwd_dq_f32_kernel<D>, dim3((f.lq + F32B_T - 1) / F32B_T, f.heads, f.batch), dim3(F32B_T),
+                     0, s, b);
+  const dim3 g0((f.l0 + F32B_T - 1) / F32B_T, f.heads, f.k0_bstride == 0 ? 1 : f.batch);
+  hipLaunchKernelGGL((attn_bwd_dkdv_f32_kernel<D, 0>), g0, dim3(F32B_T), 0, s, b);
+  if (f.l1 > 0) {
+    const dim3 g1((f.l1 + F32B_T - 1) / F32B_T, f.heads, f.k1_bstride == 0 ? 1 : f.batch);
+    hipLaunchKernelGGL((attn_bwd_dkdv_f32_kernel<D, 1>), g1, dim3(F32B_T), 0, s, b);
+  }
+}
+
+}  // namespace
+
+extern "C" int sr_attention_bwd_f32(sr_stream_t stream, const sr_attn_bwd_desc* desc) {
+  SR_CHECK(desc, SR_EINVAL, "sr_attention_bwd_f32: null desc");
+  const sr_attn_bwd_desc& b = *desc;
+  const sr_attn_desc& f = b.f;
+  SR_CHECK(f.q && f.k0 && f.v0 && f.o && f.lse && b.dout && b.delta && b.dq && b.dk0 && b.dv0, SR_EINVAL,
+           "sr_attention_bwd_f32: null pointer");
+  SR_CHECK((f.head_dim == 64 || f.head_dim == 128) && f.mask_mode == SR_MASK_NONE, SR_EUNSUPPORTED,
+           "sr_attention_bwd_f32: head_dim 64 | 128 without mask only");
+  SR_CHECK(f.batch > 0 && f.heads > 0 && f.lq > 0 && f.l0 > 0 && f.l1 >= 0, SR_EINVAL,
+           "sr_attention_bwd_f32: bad sizes");
+  SR_CHECK(!f.q_scaled, SR_EUNSUPPORTED, "sr_attention_bwd_f32: q_scaled is a bf16 forward convention");
+  SR_CHECK(f.l1 == 0 || (f.k1 && f.v1 && b.dk1 && b.dv1), SR_EINVAL,
+           "sr_attention_bwd_f32: segment 1 needs k1/v1/dk1/dv1");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nrows = (int64_t)f.batch * f.heads * f.lq;
+  hipLaunchKernelGGL(attn_bwd_delta_f32_kernel, dim3((unsigned)std::min<int64_t>((nrows + 255) / 256, 1 << 16)),
+                     dim3(256), 0, s, b);
+  if (f.head_dim == 64) launch_bwd_f32<64>(b, s);
+  else launch_bwd_f32<128>(b, s);
+  sr::note_kernel("attn_bwd_dq_f32_kernel<%d>", f.head_dim);
+  return sr::check_launch("sr_attention_bwd_f32");
+}

@@ -718,17 +718,23 @@ __global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict_
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found, 1);
 }
 
-// One element of the Adam update.  Contraction is off and the two FMAs are explicit, so the float4
-// path and the scalar tail round identically (one function, one rounding sequence).
+// One element of the Adam update, in the operation order of torch.optim.Adam's single-tensor step
+// (the reference's optimizer, train_imc.py:475) with its pointwise kernels' contractions:
+//   grad.add(p, alpha=wd)            -> fma(wd, p, g)
+//   m.lerp_(g, 1 - b1)  (weight < .5) -> fma(1 - b1, g - m, m)
+//   v.mul_(b2).addcmul_(g, g, 1 - b2) -> fma((1 - b2) g, g, b2 v)
+//   p.addcdiv_(m, denom, -step_size)  -> fma(-step_size, m / denom, p)
+// Contraction is off and every FMA is explicit, so the float4 path and the scalar tail round
+// identically (one function, one rounding sequence).
 __device__ __forceinline__ void adam_elem(float g, float& p, float& m, float& v, float inv, float beta1, float beta2,
                                           float eps, float wd, float bc2_sqrt, float step_size) {
 #pragma clang fp contract(off)
   float gr = g * inv;
-  if (wd != 0.f) gr = gr + wd * p;
-  const float mn = fmaf(1.f - beta1, gr - m, m);  // lerp(m, g, 1 - beta1), weight < 0.5
-  const float vn = fmaf(1.f - beta2, gr * gr, beta2 * v);
+  if (wd != 0.f) gr = fmaf(wd, p, gr);
+  const float mn = fmaf(1.f - beta1, gr - m, m);
+  const float vn = fmaf((1.f - beta2) * gr, gr, beta2 * v);
   const float denom = sqrtf(vn) / bc2_sqrt + eps;
-  p = p - step_size * (mn / denom);
+  p = fmaf(-step_size, mn / denom, p);
   m = mn;
   v = vn;
 }

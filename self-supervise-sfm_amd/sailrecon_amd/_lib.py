@@ -146,6 +146,7 @@ _PROTOS = {
     "sr_quant_fp8_vt": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     "sr_attention_qkv8": (_i32, [_vp, ctypes.POINTER(AttnDesc), _vp, _i64, _vp, _i64, _vp, _vp]),
     "sr_attention_bwd": (_i32, [_vp, ctypes.POINTER(AttnBwdDesc)]),
+    "sr_attention_bwd_f32": (_i32, [_vp, ctypes.POINTER(AttnBwdDesc)]),
     "sr_im2col3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "sr_conv3x3_f32": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _i32,
                               ctypes.POINTER(GemmEpi), _vp, _i64, _vp]),
@@ -206,6 +207,10 @@ _PROTOS = {
 EXPORTED = tuple(_PROTOS)
 
 
+# oldest library ABI (sr_version, major << 16 | minor) whose entry points these bindings call correctly
+ABI_MIN = 1 << 16
+
+
 class SfmAmdError(RuntimeError):
     pass
 
@@ -224,8 +229,17 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "(there is no CPU fallback)")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     # an SFM_AMD_LIB override (an older build for a same-box A/B) may lack newer entry points: they
-    # stay unbound and fail if called; the in-tree library must export every one
+    # stay unbound and fail if called; the in-tree library must export every one.  A build older
+    # than ABI_MIN is refused: its existing entry points take structs / arguments that changed
+    # meaning in 1.0 (GemmEpi.q_scale / q_cols, AttnDesc.q_scaled, sr_colsum's workspace), which an
+    # older library would silently ignore
     override = bool(os.environ.get("SFM_AMD_LIB"))
+    lib.sr_version.restype = ctypes.c_int32
+    lib.sr_version.argtypes = []
+    ver = lib.sr_version()
+    if ver < ABI_MIN:
+        raise SfmAmdError(f"{path}: ABI {ver >> 16}.{ver & 0xFFFF} is older than the {ABI_MIN >> 16}."
+                          f"{ABI_MIN & 0xFFFF} these bindings need")
     for name, (res, args) in _PROTOS.items():
         try:
             fn = getattr(lib, name)

@@ -759,10 +759,16 @@ def attention_bwd(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, lse: Tensor, dou
                   k0_bstride: int, k1: Optional[Tensor] = None, v1: Optional[Tensor] = None,
                   dk1: Optional[Tensor] = None, dv1: Optional[Tensor] = None, l1: int = 0, k1_bstride: int = 0,
                   scale: Optional[float] = None, tag: Optional[str] = None) -> None:
-    """Gradient of attention() (bf16, head_dim 64): dq / dk* / dv* fp32 in q's / k's / v's layouts;
-    ``delta`` fp32 [batch, heads, lq] workspace.  See sr_attention_bwd."""
+    """Gradient of attention(): dq / dk* / dv* fp32 in q's / k's / v's layouts; ``delta`` fp32
+    [batch, heads, lq] workspace.  bf16 operands (head_dim 64): sr_attention_bwd; fp32 operands
+    (TrainGraph's fp32 mode, head_dim 64 | 128): the exact sr_attention_bwd_f32."""
+    f32 = q.dtype == torch.float32
+    for t, name in ((k0, "k0"), (v0, "v0"), (o, "o"), (dout, "dout")) + (((k1, "k1"), (v1, "v1")) if l1 > 0 else ()):
+        if t.dtype != q.dtype:
+            raise TypeError(f"attention_bwd: {name} must have q's dtype {q.dtype}")
+    head_dim = q.shape[1] // heads if f32 else 64
     b = _lib.AttnBwdDesc()
-    b.f = _attn_desc(q, k0, v0, o, heads=heads, head_dim=64, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
+    b.f = _attn_desc(q, k0, v0, o, heads=heads, head_dim=head_dim, batch=batch, lq=lq, q_bstride=q_bstride, l0=l0,
                      k0_bstride=k0_bstride, k1=k1, v1=v1, l1=l1, k1_bstride=k1_bstride, scale=scale, lse=lse)
     for t, name in ((dq, "dq"), (dk0, "dk0"), (dv0, "dv0"), (delta, "delta")) + \
             (((dk1, "dk1"), (dv1, "dv1")) if l1 > 0 else ()):
@@ -780,7 +786,8 @@ def attention_bwd(q: Tensor, k0: Tensor, v0: Tensor, o: Tensor, lse: Tensor, dou
         b.dv1, b.lddv1 = _p(dv1), _rowmajor(dv1, "dv1")
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    check(_lib.load().sr_attention_bwd(_stream(q), ctypes.byref(b)), "sr_attention_bwd")
+    fn = "sr_attention_bwd_f32" if f32 else "sr_attention_bwd"
+    check(getattr(_lib.load(), fn)(_stream(q), ctypes.byref(b)), fn)
     if timed:
         kv = (l0 if k0_bstride == 0 else batch * l0) + batch * l1
         TIMER.stop(tag, ev0, 10.0 * batch * heads * lq * (l0 + l1) * 64, 2 * heads * 64 * (4 * batch * lq + 4 * kv))

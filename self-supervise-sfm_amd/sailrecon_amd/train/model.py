@@ -49,7 +49,14 @@ class TrainGraph:
     """Training forward/backward for a SailRecon-style module with ``aggregator`` and
     ``camera_head`` (the DPT heads are not run: they do not feed the loss)."""
 
-    def __init__(self, model, flat: Optional[FlatParams] = None):
+    def __init__(self, model, flat: Optional[FlatParams] = None, compute_dtype: torch.dtype = BF16):
+        """``compute_dtype``: the aggregator's operand dtype.  bf16 (default) is train_imc.py's
+        autocast; fp32 runs every aggregator GEMM and attention (forward and backward) in exact
+        fp32, which pins the graph's wiring against fp32 autograd far below bf16 noise
+        (tests/test_train_graph_gpu.py)."""
+        if compute_dtype not in (BF16, F32):
+            raise ValueError(f"TrainGraph: compute_dtype bf16 or fp32 (got {compute_dtype})")
+        self.cdt = compute_dtype
         self.model = model
         self.agg = model.aggregator
         self.cam = model.camera_head
@@ -168,8 +175,9 @@ class TrainGraph:
         # ---- patch embed (+ DINO), vision_transformer.py:242-307 / aggregator.py:267-274
         x = self._buf("x", R, C, F32)
         kpad = -(-3 * ps * ps // 64) * 64
-        misc = agg._pack_misc(BF16, kpad)
-        cols = self._buf("im2col", S * n_patch, kpad, BF16)
+        cdt = self.cdt
+        misc = agg._pack_misc(cdt, kpad)
+        cols = self._buf("im2col", S * n_patch, kpad, cdt)
         ops.im2col_normalize(imgs, ps, cols, kpad)
         is_dino = hasattr(agg.patch_embed, "blocks")
         if is_dino:
@@ -193,9 +201,9 @@ class TrainGraph:
             ops.set_special_tokens(x, S, P, dtab.detach().float().contiguous()[None],
                                    torch.zeros(S, device=dev, dtype=torch.int32))
             for i, blk in enumerate(dino.blocks):
-                pb = blk.packed(BF16)
+                pb = blk.packed(cdt)
                 fwd, _ = engine.frame_attend_train(pb, S, P)
-                engine.run_block_train(pb, x, 0, R, self._tape(("dino", i), R, C, hidden, BF16, S * pb.heads * P,
+                engine.run_block_train(pb, x, 0, R, self._tape(("dino", i), R, C, hidden, cdt, S * pb.heads * P,
                                                                 False), fwd, None)
             x_prenorm = self._buf("dino_prenorm", R, C, F32)
             ops.copy_rows(x_prenorm, x, R)
@@ -228,18 +236,18 @@ class TrainGraph:
         cam_rows = _i32([f * P for f in range(S)], dev)
         st["cam_rows"] = cam_rows
         for l in range(agg.depth):
-            pf = agg.frame_blocks[l].packed(BF16)
+            pf = agg.frame_blocks[l].packed(cdt)
             fwd, _ = engine.frame_attend_train(pf, S, P)
-            engine.run_block_train(pf, x, 0, R, self._tape(("frame", l), R, C, hidden, BF16, S * pf.heads * P, True),
+            engine.run_block_train(pf, x, 0, R, self._tape(("frame", l), R, C, hidden, cdt, S * pf.heads * P, True),
                                    fwd, runtime.qkv_params(pf, rope, pos_row_base=0, **posctx))
             if l == agg.depth - 1:
                 ops.copy_rows(cam_in[:, :C], x, S, rowmap=cam_rows)
-            pr = agg.global_reloc_blocks[l].packed(BF16)
-            pg = agg.global_blocks[l].packed(BF16)
+            pr = agg.global_reloc_blocks[l].packed(cdt)
+            pg = agg.global_blocks[l].packed(cdt)
             # anchor-subsample K|V of the reloc block (reads the anchors before the global block)
-            xn_sub = self._buf(f"xn_sub{l}", n_sub, C, BF16)
-            kv_sub = self._buf(f"kv_sub{l}", n_sub, 2 * C, BF16)
-            kv_raw = self._buf(f"kv_raw{l}", n_sub, 2 * C, BF16)
+            xn_sub = self._buf(f"xn_sub{l}", n_sub, C, cdt)
+            kv_sub = self._buf(f"kv_sub{l}", n_sub, 2 * C, cdt)
+            kv_raw = self._buf(f"kv_raw{l}", n_sub, 2 * C, cdt)
             ops.layernorm(x, pr.ln1_w, pr.ln1_b, pr.eps, xn_sub, rowmap=rowmap_t[l], rows=n_sub)
             epi = runtime.qkv_params(pr, rope, pos_rowmap=rowmap_t[l], **posctx)
             if epi is None:
@@ -249,11 +257,11 @@ class TrainGraph:
                 ops.gemm(xn_sub, pr.w_qkv[C:], kv_sub, _lib.SR_EPI_QKV, bias=_sl(pr.b_qkv, C, 3 * C), qkv=epi,
                          aux=kv_raw, tag="gemm")
             rfwd, _ = self._reloc_attn(pr, kv_sub, None, Nq, P, n_sub)
-            rel = dict(pb=pr, x=x, r0=q0, r1=R, tape=self._tape(("reloc", l), R - q0, C, hidden, BF16,
+            rel = dict(pb=pr, x=x, r0=q0, r1=R, tape=self._tape(("reloc", l), R - q0, C, hidden, cdt,
                                                                 Nq * pr.heads * P, True),
                        attend=rfwd, qkv_epi=runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx))
             gfwd, _ = self._global_attn(pg, q0)
-            glo = dict(pb=pg, x=x, r0=0, r1=q0, tape=self._tape(("global", l), q0, C, hidden, BF16, pg.heads * q0, True),
+            glo = dict(pb=pg, x=x, r0=0, r1=q0, tape=self._tape(("global", l), q0, C, hidden, cdt, pg.heads * q0, True),
                        attend=gfwd, qkv_epi=runtime.qkv_params(pg, rope, pos_row_base=0, **posctx))
             if _PAIR_FWD:  # disjoint rows; the reloc block's anchor K|V was projected above
                 engine.run_block_train_multi([rel, glo])
@@ -449,29 +457,32 @@ class TrainGraph:
         n_sub, rowmap, rope, posctx = st["n_sub"], st["rowmap"], st["rope"], st["posctx"]
         cam_rows = st["cam_rows"]
         g = lambda p: p.grad  # noqa: E731
+        cdt = self.cdt
+        bf = cdt == BF16
         dx = self._buf("dx", R, C, F32).zero_()
-        dxb = self._buf("dxb", R, C, BF16)
+        dxb = self._buf("dxb", R, C, BF16) if bf else None  # fp32 mode: dx itself is the GEMM operand
         # camera tokens of the last layer: second half = after the global / reloc blocks
         ops.scatter_rows(dx, cam_rows, d_raw[:, C:], accumulate=True)
         dkv_sub = self._buf("dkv_sub", n_sub, 2 * C, F32)
-        dkv_raw = self._buf("dkv_raw", n_sub, 2 * C, BF16)
+        dkv_raw = self._buf("dkv_raw", n_sub, 2 * C, BF16) if bf else dkv_sub
         dxn_sub = self._buf("dxn_sub", n_sub, C, F32)
         for l in reversed(range(agg.depth)):
-            ops.cast_bf16(dx, dxb)
+            if bf:
+                ops.cast_bf16(dx, dxb)
             br, bg = agg.global_reloc_blocks[l], agg.global_blocks[l]
-            pr, pg = br.packed(BF16), bg.packed(BF16)
-            kv_sub = self._buf(f"kv_sub{l}", n_sub, 2 * C, BF16)
+            pr, pg = br.packed(cdt), bg.packed(cdt)
+            kv_sub = self._buf(f"kv_sub{l}", n_sub, 2 * C, cdt)
             # reloc block (query rows); its shared segment's dK|dV land in dkv_sub
             _, rbwd = self._reloc_attn(pr, kv_sub, dkv_sub, Nq, P, n_sub)
             gr = engine.block_grads(br)
             # global block (anchor rows)
             _, gbwd = self._global_attn(pg, q0)
             tg = self._tapes[("global", l)]
-            rel = dict(pb=pr, bp=self._bwd_pack(br, BF16), g=gr, tape=self._tapes[("reloc", l)], dx=dx[q0:],
-                       dxb=dxb[q0:], attend_bwd=rbwd, qkv_epi=runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx),
+            rel = dict(pb=pr, bp=self._bwd_pack(br, cdt), g=gr, tape=self._tapes[("reloc", l)], dx=dx[q0:],
+                       dxb=dxb[q0:] if bf else None, attend_bwd=rbwd, qkv_epi=runtime.qkv_params(pr, rope, pos_row_base=q0, **posctx),
                        sc=self._sc, tag="reloc")
-            glo = dict(pb=pg, bp=self._bwd_pack(bg, BF16), g=engine.block_grads(bg), tape=tg, dx=dx[:q0],
-                       dxb=dxb[:q0], attend_bwd=gbwd, qkv_epi=runtime.qkv_params(pg, rope, pos_row_base=0, **posctx),
+            glo = dict(pb=pg, bp=self._bwd_pack(bg, cdt), g=engine.block_grads(bg), tape=tg, dx=dx[:q0],
+                       dxb=dxb[:q0] if bf else None, attend_bwd=gbwd, qkv_epi=runtime.qkv_params(pg, rope, pos_row_base=0, **posctx),
                        sc=self._sc2, tag="global")
             if _PAIR_DGRAD and Nq > 0:
                 # the two blocks' dgrad GEMMs stage by stage as grouped launches (engine.block_bwd_multi)
@@ -484,25 +495,30 @@ class TrainGraph:
             epi = runtime.qkv_params(pr, rope, pos_rowmap=rowmap[l], **posctx)
             if epi is not None:
                 epi["col_offset"] = C
-            ops.qk_bwd(self._buf(f"kv_raw{l}", n_sub, 2 * C, BF16) if epi is not None else None, dkv_sub, dkv_raw,
-                       epi or dict(embed_dim=C, head_dim=64, col_offset=C), grads=gr.qkn)
-            bp = self._bwd_pack(br, BF16)
+            kv_raw = self._buf(f"kv_raw{l}", n_sub, 2 * C, cdt) if epi is not None else None
+            if bf or epi is not None:  # fp32 without qk-norm / RoPE: dkv_raw is dkv_sub
+                ops.qk_bwd(kv_raw, dkv_sub, dkv_raw, epi or dict(embed_dim=C, head_dim=64, col_offset=C), grads=gr.qkn)
+            bp = self._bwd_pack(br, cdt)
             ops.gemm(dkv_raw, bp.wt_qkv[:, C:], dxn_sub, _lib.SR_EPI_F32, tag="reloc.dgrad")
-            ops.gemm_wgrad(dkv_raw, self._buf(f"xn_sub{l}", n_sub, C, BF16), gr.w_qkv[C:], accumulate=True,
-                           tag="reloc.wgrad")
-            if gr.b_qkv is not None:
-                ops.colsum(dkv_raw, gr.b_qkv[C:], accumulate=True)
+            xn_sub = self._buf(f"xn_sub{l}", n_sub, C, cdt)
+            if bf:
+                ops.gemm_wgrad(dkv_raw, xn_sub, gr.w_qkv[C:], accumulate=True, tag="reloc.wgrad")
+                if gr.b_qkv is not None:
+                    ops.colsum(dkv_raw, gr.b_qkv[C:], accumulate=True)
+            else:
+                ops.wgrad_small(dkv_raw, xn_sub, gr.w_qkv[C:], db=_sl(gr.b_qkv, C, 3 * C), accumulate=True)
             ops.layernorm_bwd(tg.x0, dxn_sub, pr.ln1_w, pr.eps, dx, rowmap=rowmap[l], rows=n_sub,
                               dw=gr.ln1_w, db=gr.ln1_b)
             self._ready(br)
             self._ready(bg)
             if l == agg.depth - 1:  # first half of the camera tokens = the frame block's output
                 ops.scatter_rows(dx, cam_rows, d_raw[:, :C], accumulate=True)
-            ops.cast_bf16(dx, dxb)
+            if bf:
+                ops.cast_bf16(dx, dxb)
             bf_ = agg.frame_blocks[l]
-            pf = bf_.packed(BF16)
+            pf = bf_.packed(cdt)
             _, fbwd = engine.frame_attend_train(pf, S, P)
-            engine.block_bwd(pf, self._bwd_pack(bf_, BF16), engine.block_grads(bf_), self._tapes[("frame", l)], dx,
+            engine.block_bwd(pf, self._bwd_pack(bf_, cdt), engine.block_grads(bf_), self._tapes[("frame", l)], dx,
                              dxb, fbwd, runtime.qkv_params(pf, rope, pos_row_base=0, **posctx), self._sc, tag="frame")
             self._ready(bf_)
         self._embed_backward(dx, dxb)
@@ -541,9 +557,9 @@ class TrainGraph:
             dx = dx2
             for i in reversed(range(len(dino.blocks))):
                 blk = dino.blocks[i]
-                pb = blk.packed(BF16)
+                pb = blk.packed(self.cdt)
                 _, bwd = engine.frame_attend_train(pb, S, P)
-                engine.block_bwd(pb, self._bwd_pack(blk, BF16), engine.block_grads(blk), self._tapes[("dino", i)],
+                engine.block_bwd(pb, self._bwd_pack(blk, self.cdt), engine.block_grads(blk), self._tapes[("dino", i)],
                                  dx, dxb, bwd, None, self._sc, tag="dino")
                 self._ready(blk)
             # cls + pos[0] (row 0), registers (rows 1..4), patches + pos[1:] (vision_transformer.py:242-259)
@@ -570,15 +586,18 @@ class TrainGraph:
         prow = _i32([f * P + psi + p for f in range(S) for p in range(n_patch)], self.dev)
         dpatch = self._buf("dpatch", S * n_patch, C, F32)
         ops.copy_rows(dpatch, dx, S * n_patch, rowmap=prow)
-        dpb = self._buf("dpatch_b", S * n_patch, C, BF16)
-        ops.cast_bf16(dpatch, dpb)
         kk = 3 * agg.patch_size ** 2
         kpad = -(-kk // 64) * 64
-        cols = self._buf("im2col", S * n_patch, kpad, BF16)
-        if kpad % 128:
-            raise NotImplementedError("patch wgrad needs the im2col width to be a multiple of 128")
+        cols = self._buf("im2col", S * n_patch, kpad, self.cdt)
         wtmp = self._buf("dw_patch", C, kpad, F32)
-        ops.gemm_wgrad(dpb, cols, wtmp, tag="patch.wgrad")
+        if self.cdt == BF16:
+            dpb = self._buf("dpatch_b", S * n_patch, C, BF16)
+            ops.cast_bf16(dpatch, dpb)
+            if kpad % 128:
+                raise NotImplementedError("patch wgrad needs the im2col width to be a multiple of 128")
+            ops.gemm_wgrad(dpb, cols, wtmp, tag="patch.wgrad")
+        else:
+            ops.wgrad_small(dpatch, cols, wtmp)
         ops.copy2d(conv.weight.grad.reshape(C, kk), wtmp[:, :kk], accumulate=True)
         if conv.bias is not None:
             ops.colsum(dpatch, conv.bias.grad, accumulate=True)

@@ -240,7 +240,9 @@ class ImagePreprocessor:
         """io.py:197-259: (C, target, target) back to the original (C, H, W).  The resize scale and
         padding come from K_prime_to_K exactly as the reference reads them (float32 .item() values,
         the same int() truncations); the bicubic (RGB) / bilinear (depth) upsample to max_side and the
-        crop of the padding run as one launch on the tensor's device (no max_side^2 intermediate)."""
+        crop of the padding run as one launch on the tensor's device (no max_side^2 intermediate).
+        The result has the input's dtype, as F.interpolate and the slice give it (a bf16 / fp16
+        input is resampled in fp32 and rounded once at the end)."""
         runtime.require_device(processed_tensor, "ImagePreprocessor.reverse_transform_tensor")
         K = K_prime_to_K.detach().float().cpu()
         scale_x = 1.0 / K[0, 0].item()
@@ -254,6 +256,8 @@ class ImagePreprocessor:
         x = processed_tensor.float().contiguous()
         out = torch.empty(x.shape[0], height, width, device=x.device, dtype=torch.float32)
         ops.resize_crop_chw(x, max_side, pad_top, pad_left, out, bicubic=not is_depth)
+        if processed_tensor.dtype != torch.float32:
+            out = out.to(processed_tensor.dtype)
         return out
 
     def _create_transformation_matrices(self, transform_param: Dict[str, Any]) -> Tuple[Tensor, Tensor]:

@@ -102,3 +102,17 @@ def test_generated_asm_sweep_matches_generator(tmp_path):
                    capture_output=True)
     shipped = open(os.path.join(REPO, "self-supervise-sfm_amd", "csrc", "sr_attn_pipe.inc")).read()
     assert out.read_text() == shipped
+
+
+def test_generated_bwd_asm_sweeps_match_generator(tmp_path):
+    """csrc/sr_attn_bwd_pipe.inc (the dK/dV, concatenated-items dK/dV and dQ asm sweeps)
+    is what tools/gen_attn_bwd_pipe.py emits with its default knobs."""
+    import subprocess
+    import sys
+    out = tmp_path / "bwd_pipe.inc"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("SR_BWD_PIPE_")}
+    env["SR_BWD_PIPE_OUT"] = str(out)
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "gen_attn_bwd_pipe.py")], env=env, check=True,
+                   capture_output=True)
+    shipped = open(os.path.join(REPO, "self-supervise-sfm_amd", "csrc", "sr_attn_bwd_pipe.inc")).read()
+    assert out.read_text() == shipped

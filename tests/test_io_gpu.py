@@ -145,3 +145,23 @@ def test_reverse_transform_tensor(hw, is_depth):
     mx = float((got.cpu() - ref).abs().max())
     print(f"reverse_transform {hw} depth={is_depth}: out {tuple(got.shape)} rel {rel:.2e} max {mx:.2e}")
     assert rel < 2e-6 and mx < 1e-4 * max(1.0, float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_reverse_transform_tensor_dtype(dtype):
+    """reverse_transform_tensor keeps a reduced-precision input's dtype, as the reference's
+    F.interpolate + slice do: the result equals the fp32 path rounded once, and matches
+    the oracle's torch restatement on the same reduced-precision input within that rounding."""
+    from oracle import sfm_oracle as O
+    from sailrecon_amd.utils.io import ImagePreprocessor
+    pre = ImagePreprocessor(518, device=DEV)
+    t, _, kp2k = pre(_rgb((300, 400), 7))
+    x = t[0].to(dtype)
+    got = pre.reverse_transform_tensor(x, kp2k, 518)
+    f32 = pre.reverse_transform_tensor(x.float(), kp2k, 518)
+    torch.cuda.synchronize()
+    assert got.dtype == dtype
+    assert torch.equal(got, f32.to(dtype))
+    ref = O.reverse_transform_tensor(x.float().cpu(), kp2k, 518)
+    rel = float((got.cpu().double() - ref.double()).norm() / ref.double().norm())
+    assert rel < (4e-3 if dtype == torch.bfloat16 else 6e-4), rel

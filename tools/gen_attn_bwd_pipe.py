@@ -612,25 +612,5 @@ def main():
         f.write("\n".join(out) + "\n")
 
 
-def main_old():
-    lines, loop = sweep()
-    n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
-    n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_mul", "v_cvt"))) // 4
-    n_ds = sum(1 for l in loop if l.startswith("ds_")) // 4
-    n_wait = sum(1 for l in loop if l.startswith("s_waitcnt lgkm")) // 4
-    n_all = sum(1 for l in loop if not l.startswith(";") and not l.endswith(":")) // 4
-    out = ["// GENERATED by tools/gen_attn_bwd_pipe.py — do not edit by hand.",
-           f"// SR_ATTN_BWD_PIPE_ASM: per tile {n_mfma} MFMA, {n_valu} exp/mul/pack VALU, {n_ds} LDS reads, "
-           f"{n_wait} lgkmcnt waits, {n_all} instructions; {len(lines)} asm lines",
-           "#define SR_ATTN_BWD_PIPE_ASM \\"]
-    out.append(" \\\n".join("  \"" + l + "\\n\\t\"" for l in lines))
-    clob = ", ".join([f'"v{r}"' for r in NAMED_V] + [f'"a{r}"' for r in NAMED_A])
-    out.append("#define SR_ATTN_BWD_PIPE_CLOBBERS " + clob)
-    with open(OUT, "w") as f:
-        f.write("\n".join(out) + "\n")
-    print(f"per tile {n_mfma} MFMA / {n_valu} VALU / {n_ds} ds reads / {n_wait} waits / {n_all} instructions, "
-          f"{len(lines)} asm lines")
-
-
 if __name__ == "__main__":
     main()

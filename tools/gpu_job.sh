@@ -126,6 +126,20 @@ for step in "$@"; do
                python3 tools/kbench.py train ;;
     pmc_bwd1) run pmc_bwd1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_bwd1 -o run --output-format csv -- python3 tools/kbench.py attn_bwd ;;
     pmc_bwd2) run pmc_bwd2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_bwd2 -o run --output-format csv -- python3 tools/kbench.py attn_bwd ;;
+    tests_a) run tests_a 1100 python -u -m pytest tests -q -m gpu --timeout 600 --timeout-method thread \
+               --ignore tests/test_dist_gpu.py --ignore tests/test_train_step_gpu.py --ignore tests/test_c4_golden_gpu.py ;;
+    tests_b) run tests_b 1000 python -u -m pytest tests/test_dist_gpu.py tests/test_train_step_gpu.py \
+               tests/test_c4_golden_gpu.py -q -m gpu --timeout 600 --timeout-method thread ;;
+    # 256x256 GEMM tile order A/B (SR_GEMM_GROUP_M = g row tiles per group; 1 = row-major): kbench
+    # timings, then per-launch fetch / clock from one FETCH_SIZE + GRBM_GUI_ACTIVE pass per order
+    raster) for g in ${RASTER_GROUPS:-1 4 8 16}; do
+              run kgemm_g${g} 300 env SR_GEMM_GROUP_M=$g python tools/kbench.py gemm gemm_qkv || exit 1
+            done
+            for g in ${RASTER_GROUPS:-1 4 8 16}; do
+              run pmc_raster_g${g} 300 env SR_GEMM_GROUP_M=$g rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE \
+                -d gpurun_out/pmc_raster_g${g} -o run --output-format csv -- python3 tools/kbench.py gemm || exit 1
+              python tools/pmc_dispatch.py gpurun_out/pmc_raster_g${g} gemm > gpurun_out/pmc_raster_g${g}.txt
+            done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
