@@ -55,7 +55,7 @@ const char* sr_last_kernel(void);
  * are read at every launch, so sr_set_tuning takes effect for the next call on any thread.
  * Not synchronised with launches in flight on other threads.
  * ---------------------------------------------------------------------- */
-enum sr_tuning_key {
+enum sr_tuning_key {  /* renumbered in ABI 1.3: switches that measured level or slower were removed */
   SR_TUNE_ATTN_MZERO = 0,   /* 1: a fixed softmax offset of 0 drops the -m fold MFMAs, and the
                                hand-scheduled sweep may run (0: neither)               default 1 */
   SR_TUNE_ATTN_CFG = 1,     /* -1 auto; 0 | 1 | 2: force the bf16 attention workgroup shape
@@ -77,39 +77,21 @@ enum sr_tuning_key {
   SR_TUNE_RLN_WIDE = 12,    /* sr_residual_layernorm variant bits: 1 16-B lanes, 2 two rows per wave, 4 nt x stores (0) */
   SR_TUNE_GEMM_TAIL = 13,   /* 1: a 256x256 GEMM whose last workgroup round would run few tiles computes
                                the rows past its last whole round on the 128x128 kernel (second launch)  (1) */
-  SR_TUNE_GEMM_PERSIST = 14,/* 1: the 256x256 GEMM as one persistent workgroup per CU walking its tiles,
-                               the next tile's first K stage staged under the current epilogue   default 0 */
-  SR_TUNE_ATTN_QTAIL = 15,  /* 1 | 2: a bf16 attention whose query sets end in a q-tile of <= 128 rows runs
-                               those rows as a second launch of 128-row workgroups (1: 2 waves x 2
-                               q-blocks, 2: 4 x 1; 0: a padded 256-row tile).  Bit-identical, and
-                               measured no faster at the frame shape        default 0 */
-  SR_TUNE_GEMM_XPF = 16,    /* 256x256 RESID GEMMs: x rows prefetched into L2 / MALL per k-tile and wave
-                               under the k-loop (0 off, 1 | 2, -1 auto)                 default 0 */
-  SR_TUNE_GEMM_ROPE_LDS = 17,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
+  SR_TUNE_GEMM_RESID_LDS = 14,/* 1: the 256x256 RESID GEMM's epilogue stages the x tile through LDS by
+                               LDS-DMA (64-row quarters, two in flight; whole-row stores)  default 1 */
+  SR_TUNE_GEMM_ROPE_LDS = 15,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
                                under the first k-tile; 0: from global memory)           default 1 */
-  SR_TUNE_GEMM_PP = 18,     /* 1: the 256x256 GEMM's ping-pong k-loop (each SIMD's two waves alternate
-                               MFMA and LDS phases; bit-identical)                     default 0 */
-  SR_TUNE_ATTN_BWD_KB = 19, /* 1 | 2: key blocks of 32 per wave in the attention backward's dK/dV sweep
-                               (2: one wave per SIMD, 64 keys; bit-identical)           default 1 */
-  SR_TUNE_ATTN_BWD_PIPE = 20,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
+  SR_TUNE_ATTN_BWD_PIPE = 16,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
                                64 keys; one item per workgroup, >= 4 full query tiles;
                                bit-identical)                                           default 1 */
-  SR_TUNE_ATTN_BWD_DQ_PIPE = 21,/* 1: the attention backward's dQ sweep as the hand-scheduled asm pipeline
+  SR_TUNE_ATTN_BWD_DQ_PIPE = 17,/* 1: the attention backward's dQ sweep as the hand-scheduled asm pipeline
                                (one wave per SIMD, 64 queries; one key segment of >= 4 full
                                tiles, query padding within 2 % of the compiled sweep's or
                                >= 4,096 keys; 2: always; bit-identical)                default 1 */
-  SR_TUNE_ATTN_BWD_CONC = 22,/* 1: the attention backward's dK/dV sweep on a second (library-owned) stream
-                               beside dQ, forked from and joined back to the caller's stream default 0 */
-  SR_TUNE_ATTN_BWD_QSPLIT = 23,/* 1: where keys are shared by a batch > 1, the compiled dK/dV sweep splits
-                               the items in two halves whose partials add atomically into
-                               zero-filled dK / dV (deterministic), when that fills the last
-                               round of workgroups better (2: always)                  default 0 */
-  SR_TUNE_ATTN_BWD_CAT = 24,/* 1: keys shared by a batch > 1 whose items' queries are consecutive rows:
+  SR_TUNE_ATTN_BWD_CAT = 18,/* 1: keys shared by a batch > 1 whose items' queries are consecutive rows:
                                the dK/dV asm sweep over the concatenated queries (one sequence of
                                batch * lq rows; same sum, other tile grouping)          default 1 */
-  SR_TUNE_WGRAD_STAGES = 25,/* 2: the 256x256 wgrad stages one 64-row m-tile ahead; 3: two 48-row m-tiles
-                               ahead (144 KiB of LDS; other fp32 slice boundaries)     default 2 */
-  SR_TUNE_COUNT = 26
+  SR_TUNE_COUNT = 19
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -18,14 +18,11 @@ struct TuneDef {
 };
 // index = sr_tuning_key
 constexpr TuneDef kTune[SR_TUNE_COUNT] = {
-    {"SR_ATTN_MZERO", 1},   {"SR_ATTN_CFG", -1},      {"SR_ATTN_PIPE", 1},       {"SR_ATTN_PIPE_SEG", 0},
-    {"SR_ATTN_NO_SHORT", 0}, {"SR_GEMM_GROUP_M", -1}, {"SR_GEMM_SMALLM", 1},     {"SR_GEMM_NO256", 0},
-    {"SR_GEMM_REG_EPI", 0},  {"SR_CONV_NO_NARROW", 0}, {"SR_WGRAD256", 1},       {"SR_SYNC_CHECK", 0},
-    {"SR_RLN_WIDE", 0},      {"SR_GEMM_TAIL", 1},      {"SR_GEMM_PERSIST", 0},
-    {"SR_ATTN_QTAIL", 0},   {"SR_GEMM_XPF", 0},       {"SR_GEMM_ROPE_LDS", 1},  {"SR_GEMM_PP", 0},
-    {"SR_ATTN_BWD_KB", 1},   {"SR_ATTN_BWD_PIPE", 1},  {"SR_ATTN_BWD_DQ_PIPE", 1},
-    {"SR_ATTN_BWD_CONC", 0},     {"SR_ATTN_BWD_QSPLIT", 0},
-    {"SR_ATTN_BWD_CAT", 1},      {"SR_WGRAD_STAGES", 2},
+    {"SR_ATTN_MZERO", 1}, {"SR_ATTN_CFG", -1}, {"SR_ATTN_PIPE", 1}, {"SR_ATTN_PIPE_SEG", 0},
+    {"SR_ATTN_NO_SHORT", 0}, {"SR_GEMM_GROUP_M", -1}, {"SR_GEMM_SMALLM", 1}, {"SR_GEMM_NO256", 0},
+    {"SR_GEMM_REG_EPI", 0}, {"SR_CONV_NO_NARROW", 0}, {"SR_WGRAD256", 1}, {"SR_SYNC_CHECK", 0},
+    {"SR_RLN_WIDE", 0}, {"SR_GEMM_TAIL", 1}, {"SR_GEMM_RESID_LDS", 1}, {"SR_GEMM_ROPE_LDS", 1},
+    {"SR_ATTN_BWD_PIPE", 1}, {"SR_ATTN_BWD_DQ_PIPE", 1}, {"SR_ATTN_BWD_CAT", 1},
 };
 std::atomic<int> g_tune[SR_TUNE_COUNT];
 std::once_flag g_tune_once;
@@ -96,7 +93,7 @@ int check_launch(const char* what) {
 
 extern "C" const char* sr_last_error(void) { return g_err; }
 extern "C" const char* sr_last_kernel(void) { return g_kernel; }
-extern "C" int sr_version(void) { return (1 << 16) | 2; }  // 1.1: sr_gemm_wgrad_pair; 1.2: sr_attention_bwd_f32
+extern "C" int sr_version(void) { return (1 << 16) | 3; }  // 1.1: sr_gemm_wgrad_pair; 1.2: sr_attention_bwd_f32; 1.3: tuning keys renumbered
 
 extern "C" int sr_set_tuning(int key, int value) {
   SR_CHECK(key >= 0 && key < SR_TUNE_COUNT, SR_EINVAL, "sr_set_tuning: unknown key %d", key);

@@ -35,7 +35,6 @@ struct AttnArgs {
   int ntile0, ntile1;  // key tiles per segment
   int kb_n0;           // segment-0 instances in d.key_bound (1 if shared, else batch)
   int allow_mzero;     // fixed offset m == 0 drops the -m fold MFMAs (SR_ATTN_MZERO=0: keep them)
-  int row_base;        // first query row of the launch's q-tile 0 (the q-tail launch: past the whole tiles)
 };
 
 // ------------------------------------------------------------------ bf16 / MFMA
@@ -731,7 +730,7 @@ __global__ __launch_bounds__(NW * 64, PIPE ? 1 : (NW >= 8 ? 4 : 2)) void attn_bf
     head = (tile / nq) % nh;
     item = tile / (nq * nh);
   }
-  attn_bf16_body<NW, QB, KIND, PIPE>(args, args.row_base + qt * QROWS, head, item, smem);
+  attn_bf16_body<NW, QB, KIND, PIPE>(args, qt * QROWS, head, item, smem);
 }
 
 // Two single-query-set problems of the hand-scheduled sweep in ONE launch (sr_attention_pair):
@@ -1716,7 +1715,6 @@ static int pair_args(const sr_attn_desc& d, AttnArgs& a, const char* which) {
   a.ntile1 = 0;
   a.kb_n0 = 1;
   a.allow_mzero = sr::tune(SR_TUNE_ATTN_MZERO);
-  a.row_base = 0;
   return SR_OK;
 }
 
@@ -1820,20 +1818,7 @@ extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d
              ((d.l1 == 0 && d.l0 % KT == 0) ||
               ((pipe_seg || ((d.batch == 1 || d.q_bstride == 0) && d.lq >= 4096)) && d.tail_rows_readable >= KT)))
       SR_ATTN_LAUNCH(4, 2, true);  // the asm sweep: one segment of full tiles, or (_SEG) two / ragged
-    else if (force_cfg < 0 && sr::tune(SR_TUNE_ATTN_QTAIL) && d.lq > 256 && d.lq % 256 != 0 && d.lq % 256 <= 128) {
-      // q-tail split: a 1,374-row frame is 5 whole 256-row tiles + 94 rows, and a sixth 4 x 2 tile
-      // would run 162 padding rows (10 % of the frame / DINO launch's waves).  The rows past the
-      // whole tiles run as their own launch of 128-row (2 x 2) workgroups -- first, so that the
-      // main launch stays the call's last kernel -- and the main launch covers the whole tiles.
-      // Each wave's rows see the same code and key order as in the one-launch form.
-      a.row_base = d.lq / 256 * 256;
-      grid.x = (d.lq - a.row_base + 127) / 128;
-      if (sr::tune(SR_TUNE_ATTN_QTAIL) == 2) SR_ATTN_LAUNCH(4, 1, false);  // 4 waves x 1 q-block
-      else SR_ATTN_LAUNCH(2, 2, false);
-      a.row_base = 0;
-      grid.x = d.lq / 256;
-      SR_ATTN_LAUNCH(4, 2, false);
-    } else SR_ATTN_LAUNCH(4, 2, false);
+    else SR_ATTN_LAUNCH(4, 2, false);
 #undef SR_ATTN_LAUNCH
     return sr::check_launch("sr_attention(bf16)");
   }

@@ -18,7 +18,6 @@
 // (r & 3) + 8 (r >> 2) + 4 hi, r = 0..15, which is the k order the tr-reads produce.
 // Tiles are 64 rows x 128 B (swizzle: see swz below).
 #include <cfloat>
-#include <mutex>
 #include <type_traits>
 
 #include "sr_common.h"
@@ -212,10 +211,7 @@ __device__ __forceinline__ void dkdv_tile(const char* qt, int qv, const bf16x8 (
 }
 
 // dK[key][d] = scale * dK^T[d][key], dV likewise (lane: key key_base + 32 kb, d = 32 db + acc_row(r))
-// ATOMIC: the sweep covered half of the shared keys' queries (SPLIT2) and adds its partial into
-// zero-filled dK / dV; with exactly two addends into +0 the result is the same whichever lands
-// first (a + b = b + a in fp32), so the outputs stay deterministic.
-template <int SEG, int KB, bool ATOMIC = false>
+template <int SEG, int KB>
 __device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb0, int key_base, int len, int hcol,
                                            int hi, const f32x16 (&dk)[KB][2], const f32x16 (&dv)[KB][2]) {
   const float scale = b.f.scale;
@@ -230,18 +226,10 @@ __device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int d0 = db * 32 + 8 * g + 4 * hi;
-          if constexpr (ATOMIC) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              unsafeAtomicAdd(dkp + d0 + j, dk[kb][db][4 * g + j] * scale);
-              unsafeAtomicAdd(dvp + d0 + j, dv[kb][db][4 * g + j]);
-            }
-          } else {
-            *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * scale, dk[kb][db][4 * g + 1] * scale,
-                                               dk[kb][db][4 * g + 2] * scale, dk[kb][db][4 * g + 3] * scale);
-            *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
-                                               dv[kb][db][4 * g + 3]);
-          }
+          *(float4*)(dkp + d0) = make_float4(dk[kb][db][4 * g] * scale, dk[kb][db][4 * g + 1] * scale,
+                                             dk[kb][db][4 * g + 2] * scale, dk[kb][db][4 * g + 3] * scale);
+          *(float4*)(dvp + d0) = make_float4(dv[kb][db][4 * g], dv[kb][db][4 * g + 1], dv[kb][db][4 * g + 2],
+                                             dv[kb][db][4 * g + 3]);
         }
     }
   }
@@ -253,13 +241,11 @@ __device__ __forceinline__ void store_dkdv(const sr_attn_bwd_desc& b, int64_t kb
 // -(c q.k - lse) and P = exp2(-S') (the sign is a source modifier of v_exp); the dP chain is seeded
 // with the stored -delta (attn_bwd_delta_kernel) and returns dO.v - delta, so dS = P dP' with no
 // sign flips (a negated V turned into 24 v_xor per tile before the packed multiplies).
-// KB key blocks of 32 per wave (SR_TUNE_ATTN_BWD_KB): KB = 2 runs one wave per SIMD with 64 keys,
-// so every Q / dO fragment read from LDS (row reads for S / dP, transposed reads for dV / dK) feeds
-// two key blocks' MFMAs, and the wave has two independent chain sets to interleave.
-// SPLIT2 (keys shared across the batch only): blockIdx.z = 0 / 1 sweeps the first / second half of
-// the items and adds its partial dK / dV atomically (store_dkdv<.., true>; the host zero-fills them).
-template <int SEG, int KB = 1, bool SPLIT2 = false>
-__global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
+// One key block of 32 per wave, two workgroups per CU (64 keys per wave with one wave per SIMD is
+// the asm sweep's form; the compiled 64-key variant measured no faster and was removed in round 6).
+template <int SEG>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(sr_attn_bwd_desc b) {
+  constexpr int KB = 1;
   constexpr int STG = 2 * TB + 2 * 64 * 4;  // one stage: Q tile | dO tile | lse | delta
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
   const sr_attn_desc& f = b.f;
@@ -267,9 +253,8 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int head = blockIdx.y, hcol = head * 64;
   const bool shared = (SEG == 0 ? f.k0_bstride : f.k1_bstride) == 0;
-  const int hb = (f.batch + 1) / 2;
-  const int it0 = shared ? (SPLIT2 ? (int)blockIdx.z * hb : 0) : blockIdx.z;
-  const int it1 = shared ? (SPLIT2 ? min(f.batch, ((int)blockIdx.z + 1) * hb) : f.batch) : blockIdx.z + 1;
+  const int it0 = shared ? 0 : blockIdx.z;
+  const int it1 = shared ? f.batch : blockIdx.z + 1;
   const int len = SEG == 0 ? f.l0 : f.l1;
   const int64_t kb0 = (int64_t)(shared ? 0 : blockIdx.z) * (SEG == 0 ? f.k0_bstride : f.k1_bstride);
   const bf16* kp = (const bf16*)(SEG == 0 ? f.k0 : f.k1);
@@ -376,7 +361,7 @@ __global__ __launch_bounds__(256, KB == 1 ? 2 : 1) void attn_bwd_dkdv_kernel(sr_
       ++t;
     }
   }
-  store_dkdv<SEG, KB, SPLIT2>(b, kb0, key_base, len, hcol, hi, dk, dv);
+  store_dkdv<SEG, KB>(b, kb0, key_base, len, hcol, hi, dk, dv);
 }
 
 // ---------------------------------------------------------------- dK, dV: hand-scheduled sweep
@@ -816,29 +801,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_pipe_kernel(sr_attn_bwd_de
   }
 }
 
-// Second stream of sr_attention_bwd (SR_TUNE_ATTN_BWD_CONC): dK/dV run beside dQ, so that one
-// sweep's last partial round of workgroups overlaps the other's (both hold one workgroup per CU
-// for most shapes).  Created once per device; fork / join by events on the caller's stream.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream* side_stream() {
-  static SideStream ss[64];
-  static std::mutex mu;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  SideStream& x = ss[dev];
-  if (!x.s) {
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return x.s = nullptr, nullptr;
-    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess)
-      return nullptr;
-  }
-  return &x;
-}
-
 }  // namespace
 
 extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc) {
@@ -878,19 +840,13 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
     hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel<1>, dim3((f.lq + 255) / 256, f.heads, f.batch), dim3(256), 0, s, b);
   else
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((f.lq + 127) / 128, f.heads, f.batch), dim3(256), 0, s, b);
-  // dK / dV on the side stream when SR_ATTN_BWD_CONC (joined back below)
-  SideStream* side = sr::tune(SR_TUNE_ATTN_BWD_CONC) ? side_stream() : nullptr;
-  hipStream_t ks = s;
-  if (side && hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess)
-    ks = side->s;
   // dK / dV: the hand-scheduled sweep (SR_ATTN_BWD_PIPE) where a workgroup sweeps one item's
   // queries, at least 4 full query tiles, with 32-bit per-lane DMA offsets; else the compiled sweep
-  // with KB key blocks of 32 per wave (SR_ATTN_BWD_KB)
+  hipStream_t ks = s;
   const int64_t ldmax = std::max<int64_t>(f.ldq, b.lddo);
   const bool pipe_ok = sr::tune(SR_TUNE_ATTN_BWD_PIPE) != 0 && f.lq >= 256 &&
                        (int64_t)(f.lq + 64) * ldmax * 2 < ((int64_t)1 << 31);
-  const bool kb2 = sr::tune(SR_TUNE_ATTN_BWD_KB) == 2;
-  const int kr = kb2 ? 256 : 128;  // keys per workgroup of the compiled sweep
+  constexpr int kr = 128;  // keys per workgroup of the compiled sweep
   const char* name = nullptr;
   for (int seg = 0; seg < (f.l1 > 0 ? 2 : 1); ++seg) {
     const int len = seg == 0 ? f.l0 : f.l1;
@@ -915,39 +871,14 @@ extern "C" int sr_attention_bwd(sr_stream_t stream, const sr_attn_bwd_desc* desc
       if (seg == 0) name = "attn_bwd_dkdv_pipe_kernel<0, cat>";
       continue;
     }
-    // keys shared by a batch > 1: one workgroup sweeps every item's queries, so the launch is only
-    // len/128 x heads workgroups; with SR_ATTN_BWD_QSPLIT the items split in two halves whose
-    // partials add atomically (deterministic: two addends into zeros) where that raises the
-    // filled fraction of the last round of workgroups
-    const int wg = (len + kr - 1) / kr * f.heads, slots = 2 * 256 / (kb2 ? 2 : 1);
-    auto fill = [&](int n) { const int r = (n + slots - 1) / slots; return (double)n / (r * slots); };
-    const int qsplit = sr::tune(SR_TUNE_ATTN_BWD_QSPLIT);
-    const bool split2 = shared && f.batch > 1 && !kb2 && qsplit != 0 && (qsplit == 2 || fill(2 * wg) > fill(wg) + 0.05);
-    const dim3 g((len + kr - 1) / kr, f.heads, split2 ? 2 : nz);
-    if (split2) {
-      float* dkz = seg == 0 ? b.dk0 : b.dk1;
-      float* dvz = seg == 0 ? b.dv0 : b.dv1;
-      const int64_t lddk = seg == 0 ? b.lddk0 : b.lddk1, lddv = seg == 0 ? b.lddv0 : b.lddv1;
-      SR_CHECK(hipMemset2DAsync(dkz, lddk * 4, 0, (size_t)f.heads * 64 * 4, len, ks) == hipSuccess &&
-                   hipMemset2DAsync(dvz, lddv * 4, 0, (size_t)f.heads * 64 * 4, len, ks) == hipSuccess,
-               SR_ELAUNCH, "sr_attention_bwd: zero-filling dK / dV failed");
-      if (seg == 0) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1, true>), g, dim3(256), 0, ks, b);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1, true>), g, dim3(256), 0, ks, b);
-      if (seg == 0) name = "attn_bwd_dkdv_kernel<0, 1, split2>";
-      continue;
-    }
+    // keys shared by a batch > 1 otherwise: one workgroup sweeps every item's queries
+    const dim3 g((len + kr - 1) / kr, f.heads, nz);
     if (seg == 0) {
-      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 2>), g, dim3(256), 0, ks, b);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 1>), g, dim3(256), 0, ks, b);
-      name = kb2 ? "attn_bwd_dkdv_kernel<0, 2>" : "attn_bwd_dkdv_kernel<0, 1>";
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0>), g, dim3(256), 0, ks, b);
+      name = "attn_bwd_dkdv_kernel<0>";
     } else {
-      if (kb2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 2>), g, dim3(256), 0, ks, b);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 1>), g, dim3(256), 0, ks, b);
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1>), g, dim3(256), 0, ks, b);
     }
-  }
-  if (ks != s) {
-    SR_CHECK(hipEventRecord(side->join, ks) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
-             SR_ELAUNCH, "sr_attention_bwd: joining the side stream failed");
   }
   sr::note_kernel("%s", name);
   return sr::check_launch("sr_attention_bwd");

@@ -30,6 +30,8 @@ namespace {
 constexpr int BM = 128, BN = 128;
 constexpr int ROWB = 128;                     // bytes per tile row per k-tile
 constexpr int NTHREADS = 256;
+constexpr int BIG = 256;                      // the 256x256 kernels' tile
+constexpr int STAGE_BIG = 2 * BIG * ROWB;     // their K stage: 64 KiB
 
 struct GemmArgs {
   const char* A;
@@ -43,7 +45,7 @@ struct GemmArgs {
   int kt_per_split;  // split-K (gemm_kernel, gridDim.y slices): k-tiles per slice
   float* partial;    // split-K: [slices][M][N] fp32 partial tiles (epilogue runs in the reduction)
   int group_m;       // 256x256 kernels: tile order in groups of group_m row tiles (<= 1: row-major)
-  int xpf;           // 256x256 RESID: x rows prefetched per k-tile into L2 / MALL (SR_TUNE_GEMM_XPF)
+  int resid_lds;     // 256x256 RESID: the x tile staged through LDS by LDS-DMA (SR_TUNE_GEMM_RESID_LDS)
   int rope_lds;      // 256x256 QKV: RoPE tables staged in LDS (SR_TUNE_GEMM_ROPE_LDS)
   sr_gemm_epi ep;
   // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
@@ -95,9 +97,6 @@ using AuxT = T;
 // RoPE tables of the QKV epilogue staged into LDS by the 256x256 kernels (stage_rope): cos rows at
 // offset 0, sin rows at ROPE_LDS / 2, 64 B per position (16 floats), up to ROPE_LDS_POS positions
 constexpr int ROPE_LDS = 8192;
-// RESID x prefetch (GemmArgs.xpf): the LDS-DMA of one 1-KiB x row segment per wave lands in a sink
-// past the two K stages that nothing reads
-constexpr int XPF_SINK = 8192;
 constexpr int ROPE_LDS_POS = ROPE_LDS / 2 / 64;
 
 template <typename T, int EPI, int MT, typename Emit>
@@ -388,6 +387,128 @@ __device__ __forceinline__ void resid_full(const GemmArgs& g, f32x4 (&acc)[8][4]
   }
 }
 
+// ---- RESID epilogue staged through LDS (GemmArgs.resid_lds), 256x256 tiles (a partial last row tile
+// reads row M - 1 for the rows past M and stores only rows < M).
+// The register form above keeps 8 KiB of x loads in flight per wave (64 KiB per CU) in 4 dependent
+// rounds, each wave instruction touching 16 rows x 64 B; the epilogue then costs about as much as
+// the K = 1024 k-loop (0.15 of proj's 0.30 ms) and is bound by that latency, not by HBM.
+// Here the x tile moves as 1-KiB rows by LDS-DMA, in 64-row quarters through the two 64-KiB stage
+// buffers: quarter 0 goes out under the last k-tile's MFMAs (into the stage buffer that k-tile does
+// not read), quarter 1 right after it, and quarter k+2 as soon as quarter k's copy-out has read its
+// buffer, so two quarters (128 KiB) are in flight while the owner waves add gamma * (acc + bias)
+// in LDS and all eight waves store whole rows.  16-B chunk c of quarter row r sits at c ^ (r & 15):
+// the DMA's per-lane source chunk, the owners' accumulator-layout read-modify-write (16 rows x one
+// chunk column per 16 lanes) and the copy-out's row reads are all bank-conflict free.
+// Per element the same fp32 operations as resid_full: x + (acc + bias) * gamma.  The tile's gamma and
+// bias columns ride along with quarter 0 (1 KiB each, waves 0 / 1, past the stage buffers): the
+// epilogue issues no compiler-visible load, so the compiler's wait counting never waits on the
+// LDS-DMA it cannot see.
+constexpr int RESID_GB = 2048;  // LDS past the two stages: gamma | bias of the tile's 256 columns
+__device__ __forceinline__ void resid_dma_quarter(const GemmArgs& g, char* smem, int m0, int n0, int q, int buf,
+                                                  int lane, int wave_u) {
+  if (q == 0 && wave_u < 2 && (wave_u == 0 || g.ep.bias))
+    sr::dma16_s(wave_u == 0 ? g.ep.gamma + n0 : g.ep.bias + n0, (uint32_t)lane * 16,
+                __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + 2 * STAGE_BIG + wave_u * 1024));
+  const uint32_t base = sr::lds_addr(smem) + buf * STAGE_BIG + wave_u * 8 * 1024;
+  const int r0 = m0 + q * 64 + wave_u * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int swz = ((wave_u & 1) << 3) | i;  // (quarter row 8 wave + i) & 15
+    const int r = min(r0 + i, g.M - 1);       // rows past M (a partial last row tile): any valid row
+    sr::dma16_s((const char*)g.out + ((int64_t)r * g.ldo + n0) * 4, (uint32_t)((lane ^ swz) << 4),
+                __builtin_amdgcn_readfirstlane(base + i * 1024));
+  }
+}
+
+__device__ __forceinline__ void resid_add_quarter(f32x4 (&acc)[8][4], char* smem, int buf, int q, int wc, int lr,
+                                                  int lg, const f32x4 (&gm)[4], const f32x4 (&bs)[4]) {
+  // one 16-row block at a time (16 x VGPRs live: the accumulators already fill the AGPRs and the
+  // epilogue must not spill -- a scratch reload's vmcnt(0) would also wait out the LDS-DMA in flight)
+  char* sb = smem + buf * STAGE_BIG + lr * 1024;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    f32x4 xv[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) xv[ni] = *(const f32x4*)(sb + m * 16 * 1024 + (((wc * 16 + ni * 4 + lg) ^ lr) << 4));
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      xv[ni] += (acc[(q & 1) * 4 + m][ni] + bs[ni]) * gm[ni];
+      *(f32x4*)(sb + m * 16 * 1024 + (((wc * 16 + ni * 4 + lg) ^ lr) << 4)) = xv[ni];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void resid_store_quarter(const GemmArgs& g, const char* smem, int buf, int m0, int n0,
+                                                    int q, int lane, int wave_u) {
+  const char* sb = smem + buf * STAGE_BIG + wave_u * 8 * 1024;
+  f32x4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = *(const f32x4*)(sb + i * 1024 + lane * 16);
+  const int r0 = m0 + q * 64 + wave_u * 8;
+  float* xr = (float*)g.out + (int64_t)r0 * g.ldo + n0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int swz = ((wave_u & 1) << 3) | i;
+    if (r0 + i < g.M) *(f32x4*)(xr + (int64_t)i * g.ldo + ((lane ^ swz) << 2)) = v[i];  // wave-uniform
+  }
+}
+
+// After the k-loop: quarter 0 is in flight into buffer fb (issued under the last k-tile), the last
+// k-tile read buffer fb ^ 1.  vmcnt counts this wave's LDS-DMA pieces (8 per quarter) and its row
+// stores (8 per quarter) in issue order.
+__device__ __forceinline__ void resid_lds_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], char* smem, int m0, int n0,
+                                                   int fb, int wr, int wc, int lr, int lg, int lane, int wave_u) {
+  const int kb = fb ^ 1;
+  // a partial last row tile skips the stores of rows >= M, so the store counts below do not hold:
+  // it waits for everything instead (one tile per launch at most)
+  const bool partial = m0 + BIG > g.M;
+  auto wait_q = [&]() {  // the quarter two DMA issues back landed: 16 younger ops (its successor's
+    if (partial) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // 8 pieces, 8 row stores)
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  };
+  sr::barrier_raw();                                          // every wave is done reading buffer kb
+  resid_dma_quarter(g, smem, m0, n0, 1, kb, lane, wave_u);   // in flight: Q0 Q1
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           // Q0 (+ gamma / bias) landed: this wave's
+  sr::barrier_raw();                                          // ... every wave's
+  f32x4 gm[4], bs[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int off = (wc * 64 + ni * 16 + 4 * lg) * 4;
+    gm[ni] = *(const f32x4*)(smem + 2 * STAGE_BIG + off);
+    bs[ni] = g.ep.bias ? *(const f32x4*)(smem + 2 * STAGE_BIG + 1024 + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (wr == 0) resid_add_quarter(acc, smem, fb, 0, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, fb, m0, n0, 0, lane, wave_u);  // Q1 S0
+  sr::wait_lgkm0();
+  sr::barrier_raw();                                          // buffer fb read out
+  resid_dma_quarter(g, smem, m0, n0, 2, fb, lane, wave_u);   // Q1 S0 Q2
+  wait_q();                                                  // Q1 landed
+  sr::barrier_raw();
+  if (wr == 0) resid_add_quarter(acc, smem, kb, 1, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, kb, m0, n0, 1, lane, wave_u);  // S0 Q2 S1
+  sr::wait_lgkm0();
+  sr::barrier_raw();                                          // buffer kb read out
+  resid_dma_quarter(g, smem, m0, n0, 3, kb, lane, wave_u);   // S0 Q2 S1 Q3
+  wait_q();                                                  // Q2 landed
+  sr::barrier_raw();
+  if (wr == 1) resid_add_quarter(acc, smem, fb, 2, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, fb, m0, n0, 2, lane, wave_u);  // S1 Q3 S2
+  if (partial) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q3 landed (8 younger: S2)
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  sr::barrier_raw();
+  if (wr == 1) resid_add_quarter(acc, smem, kb, 3, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, kb, m0, n0, 3, lane, wave_u);
+}
+
 // bias (+ erf-GELU) -> bf16 for a full 256x256 tile (every row < M; N % 256 == 0 here; no aux):
 // the guarded produce/emit form compiles to an exec branch around every one of the 32 stores
 // per lane; here they are plain stores with the math of the next vectors in between.
@@ -665,8 +786,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g, int slic
 //   * the tile is computed as 4 quadrant phases (64 rows x 32 cols, 16 MFMAs each) ordered so
 //     consecutive quadrants share A or B fragments (28 ds_read_b128 per 64 MFMAs);
 //   * s_setprio 1 around each MFMA cluster keeps the cluster intact (cdna_hip_programming.md T5).
-constexpr int BIG = 256;
-constexpr int STAGE_BIG = 2 * BIG * ROWB;  // 64 KiB
 
 // Output tile -> (m0, n0): column-major inside groups of group_m row tiles, else row-major.
 __device__ __forceinline__ void tile_origin(const GemmArgs& g, int tile, int& m0, int& n0) {
@@ -709,13 +828,14 @@ __device__ __forceinline__ const char* stage_rope(const GemmArgs& g, char* smem)
   }
 }
 
-// One output tile over k-tiles [kb, ke).  ``staged``: stage kb already issued (by the previous
-// tile of a persistent workgroup).  ``next_tile`` >= 0 (persistent walk, kb = 0): this tile's
-// epilogue first issues the next tile's stage 0 into LDS buffer 0 (free once every wave is past
-// the k-loop), so that its DMA overlaps the epilogue; returns whether it did.
-template <int EPI, bool PERSIST = false, bool PP = false>
-__device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke, bool staged = false,
-                                             int next_tile = -1, const char* rope_lds = nullptr) {
+// One output tile over k-tiles [kb, ke) (the one-tile-per-workgroup 256x256 kernels).  RLDS: the RESID
+// epilogue through LDS (resid_lds_epilogue, full and partial row tiles) -- a template parameter, not
+// a run-time branch, so that no other epilogue's compiler-counted loads and stores share its control
+// flow (a merged path made the compiler wait vmcnt(0) on the epilogue's LDS-DMA).
+template <int EPI, bool RLDS = false>
+__device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int tile, int kb, int ke,
+                                             const char* rope_lds = nullptr) {
+  static_assert(!RLDS || EPI == SR_EPI_BIAS_RESID, "the LDS-staged epilogue is RESID's");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int m0, n0;
   tile_origin(g, tile, m0, n0);
@@ -731,13 +851,13 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
   const uint32_t voA = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (lane >> 4)) << 4));
   const uint32_t voB = (uint32_t)((lane >> 3) * ld_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
   const uint32_t dst0 = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wave * 8 * 1024);
-  // pieces [i0, i1) of stage kt of the tile at (m0_, n0_) (one wave-uniform branch per call):
-  // this wave's first staged row (A rows clamped to M - 1 for a ragged last row tile)
-  auto dma_tile = [&](int m0_, int n0_, int kt, int i0, int i1) {
-    const int brow0 = a_wave ? min(m0_ + wave_u * 64, g.M - 1) : n0_ + (wave_u - 4) * 64;
+  // pieces [i0, i1) of stage kt (one wave-uniform branch per call): this wave's first staged row
+  // (A rows clamped to M - 1 for a ragged last row tile)
+  auto dma_pieces = [&](int kt, int i0, int i1) {
+    const int brow0 = a_wave ? min(m0 + wave_u * 64, g.M - 1) : n0 + (wave_u - 4) * 64;
     const char* sp = (a_wave ? g.A : g.W) + (int64_t)brow0 * ld_b + (int64_t)kt * ROWB;
     const uint32_t base = dst0 + (kt & 1) * STAGE_BIG;
-    if (!(a_wave && m0_ + BIG > g.M)) {
+    if (!(a_wave && m0 + BIG > g.M)) {
 #pragma unroll
       for (int i = i0; i < i1; ++i) sr::dma16_s(sp + (int64_t)i * 8 * ld_b, (i & 1) ? voB : voA, base + i * 1024);
     } else {
@@ -750,17 +870,7 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
       }
     }
   };
-  auto dma_pieces = [&](int kt, int i0, int i1) { dma_tile(m0, n0, kt, i0, i1); };
   auto stage = [&](int kt) { dma_pieces(kt, 0, 8); };
-  // the next tile's stage 0 into buffer 0 once every wave is done with this tile's LDS
-  auto prefetch_next = [&]() -> bool {
-    if (next_tile < 0) return false;
-    int nm0, nn0;
-    tile_origin(g, next_tile, nm0, nn0);
-    sr::barrier_raw();
-    dma_tile(nm0, nn0, 0, 0, 8);
-    return true;
-  };
 
   const int wr = wave >> 2, wc = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
@@ -776,243 +886,102 @@ __device__ __forceinline__ bool gemm256_tile(const GemmArgs& g, char* smem, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // RESID with g.xpf: the x tile this epilogue read-modify-writes is fetched into L2 / MALL under the
-  // k-loop (wave w: rows m0 + 32w .. +31, 1 KiB each, xpf rows per k-tile, LDS-DMA into a sink), so
-  // that the epilogue's reads do not wait on HBM.  The prefetch goes out after the next stage's DMA,
-  // and the next k-tile's wait leaves exactly those xpf loads in flight.
-  const int xpf = (EPI == SR_EPI_BIAS_RESID && !PERSIST && !PP && m0 + BIG <= g.M && !g.lds_epi) ? g.xpf : 0;
-  const char* xrow = (const char*)g.out + ((int64_t)(m0 + wave_u * 32) * g.ldo + n0) * 4;
-  const uint32_t xsink = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + 2 * STAGE_BIG + wave_u * 1024);
-  auto x_prefetch = [&](int kt) {
-    for (int j = 0; j < xpf; ++j)
-      sr::dma16_s(xrow + (int64_t)((((kt - kb) * xpf + j) & 31) * g.ldo) * 4, (uint32_t)lane * 16, xsink);
-  };
-  if constexpr (PP) {
-    // Ping-pong k-loop (SR_TUNE_GEMM_PP): the two waves of each SIMD (wave s of group 0 = rows 0-127,
-    // wave s + 4 of group 1 = rows 128-255) alternate, so that one issues its k-step's 64 MFMAs
-    // back to back while the other reads its whole k-step of fragments from LDS (24 ds_read_b128)
-    // and, in group 0's load phase, issues the LDS-DMA of the stage two phases ahead (16 pieces per
-    // wave: its 64 A rows and 64 W rows).  Per k-step kt:
-    //   phase 1: group 0 MFMA(kt) | group 1 reads fragments of stage kt
-    //   phase 2: group 1 MFMA(kt) | group 0 DMAs stage kt+2 into the buffer of stage kt (both groups
-    //            are done with it) and reads its fragments of stage kt+1
-    // Each group-0 wave waits for its own DMA pieces of stage kt+1 at the end of phase 1, before the
-    // barrier: the other waves' pieces are only known landed after it.
-    // Each accumulator sees the same k order as in the loop below, so results are bit-identical.
-    const int grp = wave_u >> 2, wg = wave_u & 3;
-    const uint32_t voAa = (uint32_t)((lane >> 3) * g.lda_b + (((lane & 7) ^ (lane >> 4)) << 4));
-    const uint32_t voAb = (uint32_t)((lane >> 3) * g.lda_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
-    const uint32_t voWa = (uint32_t)((lane >> 3) * g.ldw_b + (((lane & 7) ^ (lane >> 4)) << 4));
-    const uint32_t voWb = (uint32_t)((lane >> 3) * g.ldw_b + (((lane & 7) ^ (4 + (lane >> 4))) << 4));
-    const uint32_t dstA = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + wg * 8 * 1024);
-    const uint32_t dstW = __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + (wg + 4) * 8 * 1024);
-    const bool ragged = m0 + BIG > g.M;
-    auto dma_pp = [&](int kt) {  // group 0 only: stage rows of A waves wg and W waves wg + 4
-      const int arow0 = min(m0 + wg * 64, g.M - 1);
-      const char* spa = g.A + (int64_t)arow0 * g.lda_b + (int64_t)kt * ROWB;
-      const char* spw = g.W + (int64_t)(n0 + wg * 64) * g.ldw_b + (int64_t)kt * ROWB;
-      const uint32_t off = (kt & 1) * STAGE_BIG;
-      if (!ragged) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) sr::dma16_s(spa + (int64_t)i * 8 * g.lda_b, (i & 1) ? voAb : voAa, dstA + off + i * 1024);
-      } else {
-        const int rlim = g.M - 1 - arow0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = min(i * 8 + (lane >> 3), rlim);
-          const int chunk = (lane & 7) ^ (4 * (i & 1) + (lane >> 4));
-          sr::dma16_s(spa, (uint32_t)(r * g.lda_b + chunk * 16), dstA + off + i * 1024);
-        }
+  stage(kb);
+  for (int kt = kb; kt < ke; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of stage kt landed
+    sr::barrier_raw();                                  // ... every wave's; all done with kt-1
+    const bool more = kt + 1 < ke;
+    // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
+    // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
+    // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
+    // measured no better)
+    auto dma_phase = [&](int ph) {
+      if (!more) {  // last k-tile: the RESID x tile's first quarter into the stage buffer it does not read
+        if (RLDS && ph == 0) resid_dma_quarter(g, smem, m0, n0, 0, (kt + 1) & 1, lane, wave_u);
+        return;
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sr::dma16_s(spw + (int64_t)i * 8 * g.ldw_b, (i & 1) ? voWb : voWa, dstW + off + i * 1024);
+      if (ph < 2) dma_pieces(kt + 1, 4 * ph, 4 * ph + 4);
     };
-    uint4 fa[8][2], fb[4][2];
-    auto read_frags = [&](int kt) {
-      const char* sb = smem + (kt & 1) * STAGE_BIG;
+    const char* sb = smem + (kt & 1) * STAGE_BIG;
+    // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
+    // the current quadrant's MFMA cluster so their LDS latency hides under it
+    uint4 aX[4][2], aY[4][2], bX[2][2], bY[2][2];
+    auto load_a = [&](uint4 (&a)[4][2], int qm) {
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const char* p = sb + arow + mi * 16 * ROWB;
-        fa[mi][0] = *(const uint4*)(p + coff0);
-        fa[mi][1] = *(const uint4*)(p + coff1);
-      }
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const char* p = sb + brow + ni * 16 * ROWB;
-        fb[ni][0] = *(const uint4*)(p + coff0);
-        fb[ni][1] = *(const uint4*)(p + coff1);
+      for (int mi = 0; mi < 4; ++mi) {
+        const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
+        a[mi][0] = *(const uint4*)(p + coff0);
+        a[mi][1] = *(const uint4*)(p + coff1);
       }
     };
-    auto mma_all = [&]() {
-      sr::wait_lgkm0();
+    auto load_b = [&](uint4 (&b)[2][2], int qn) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
+        b[ni][0] = *(const uint4*)(p + coff0);
+        b[ni][1] = *(const uint4*)(p + coff1);
+      }
+    };
+    auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
+        for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) Mma<bf16>::run(fb[ni][ks], fa[mi][ks], acc[mi][ni]);
+          for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
       __builtin_amdgcn_s_setprio(0);
     };
-    // one straight loop per group (the same barrier sequence in both)
-    if (grp == 0) {
-      dma_pp(kb);
-      if (kb + 1 < ke) {
-        dma_pp(kb + 1);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // stage kb landed; kb+1 in flight
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      sr::barrier_raw();
-      read_frags(kb);
-      for (int kt = kb; kt < ke; ++kt) {
-        mma_all();                 // phase 1
-        // this wave's pieces of stage kt+1 (issued a phase ago) landed; after the barrier every
-        // group-0 wave's have, so group 0 reads it in phase 2 and group 1 in the next phase 1
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sr::barrier_raw();
-        if (kt + 1 < ke) {         // phase 2
-          if (kt + 2 < ke) dma_pp(kt + 2);  // into stage kt's buffer: both groups are done with it
-          read_frags(kt + 1);
-          sr::wait_lgkm0();
-        }
-        sr::barrier_raw();
-      }
-    } else {
-      sr::barrier_raw();
-      for (int kt = kb; kt < ke; ++kt) {
-        read_frags(kt);            // phase 1
-        sr::wait_lgkm0();
-        sr::barrier_raw();
-        mma_all();                 // phase 2
-        sr::barrier_raw();
-      }
-    }
-  } else {
-    if (!staged) stage(kb);
-    for (int kt = kb; kt < ke; ++kt) {
-      // this wave's part of stage kt landed (with the x prefetch: all but the xpf loads issued after it)
-      if (xpf == 0 || kt == kb) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (xpf == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      sr::barrier_raw();                                  // ... every wave's; all done with kt-1
-      const bool more = kt + 1 < ke;
-      // the 8 DMA pieces of stage kt+1 (overwriting the buffer of kt-1) go out 4 before each of the
-      // first two MFMA phases rather than as one burst after the barrier (same-box A/B: qkv +4 %,
-      // fc1 +2 %, proj / fc2 even; 2 per phase over all four phases, or waves 0-3 / 4-7 in turn,
-      // measured no better)
-      auto dma_phase = [&](int ph) {
-        if (!more) return;
-        if (ph < 2) dma_pieces(kt + 1, 4 * ph, 4 * ph + 4);
-        else if (ph == 3 && xpf) x_prefetch(kt);
-      };
-      const char* sb = smem + (kt & 1) * STAGE_BIG;
-      // fragments double-buffered by quadrant: the next quadrant's ds_reads are issued before
-      // the current quadrant's MFMA cluster so their LDS latency hides under it
-      uint4 aX[4][2], aY[4][2], bX[2][2], bY[2][2];
-      auto load_a = [&](uint4 (&a)[4][2], int qm) {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const char* p = sb + arow + (qm * 64 + mi * 16) * ROWB;
-          a[mi][0] = *(const uint4*)(p + coff0);
-          a[mi][1] = *(const uint4*)(p + coff1);
-        }
-      };
-      auto load_b = [&](uint4 (&b)[2][2], int qn) {
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const char* p = sb + brow + (qn * 32 + ni * 16) * ROWB;
-          b[ni][0] = *(const uint4*)(p + coff0);
-          b[ni][1] = *(const uint4*)(p + coff1);
-        }
-      };
-      auto mma = [&](const uint4 (&a)[4][2], const uint4 (&b)[2][2], int qm, int qn) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni) Mma<bf16>::run(b[ni][ks], a[mi][ks], acc[qm * 4 + mi][qn * 2 + ni]);
-        __builtin_amdgcn_s_setprio(0);
-      };
-      load_a(aX, 0);
-      load_b(bX, 0);
-      load_b(bY, 1);
-      dma_phase(0);
-      mma(aX, bX, 0, 0);
-      load_a(aY, 1);
-      dma_phase(1);
-      mma(aX, bY, 0, 1);
-      load_b(bX, 0);
-      dma_phase(2);
-      mma(aY, bY, 1, 1);
-      dma_phase(3);
-      mma(aY, bX, 1, 0);
-    }
+    load_a(aX, 0);
+    load_b(bX, 0);
+    load_b(bY, 1);
+    dma_phase(0);
+    mma(aX, bX, 0, 0);
+    load_a(aY, 1);
+    dma_phase(1);
+    mma(aX, bY, 0, 1);
+    load_b(bX, 0);
+    dma_phase(2);
+    mma(aY, bY, 1, 1);
+    dma_phase(3);
+    mma(aY, bX, 1, 0);
+  }
+  if constexpr (RLDS) {
+    resid_lds_epilogue(g, acc, smem, m0, n0, ke & 1, wr, wc, lr, lg, lane, wave_u);
+    return;
   }
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
     if (m0 + BIG <= g.M && !g.lds_epi) {
-      const bool pf = prefetch_next();
       resid_full(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-      return pf;
+      return;
     }
   }
   if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU) {
     if (m0 + BIG <= g.M && !g.lds_epi && !g.ep.aux) {
-      const bool pf = prefetch_next();
       bias_full<EPI>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg);
-      return pf;
+      return;
     }
   }
   if (g.lds_epi) {
-    // the LDS-staged epilogue uses both buffers: the next tile's stage goes out after it (every
-    // wave's copy-out reads are complete once it stores their data)
     epilogue256<EPI>(g, acc, smem, m0, n0, wr, wc, lr, lg, lane, wave, rope_lds);
-    return prefetch_next();
+    return;
   }
-  const bool pf = prefetch_next();
   epilogue<bf16, EPI, 8>(g, acc, m0 + wr * 128, n0 + wc * 64, lr, lg, rope_lds);
-  return pf;
 }
 
-// LDS of the 256x256 kernels: two K stages, plus the RoPE tables for QKV (one array: a second
-// __shared__ object can make hipcc drain the LDS-DMA ring, cdna_hip_programming.md §5 item 4(a))
+// LDS of the 256x256 kernels: two K stages, plus the RoPE tables for QKV / the gamma | bias columns
+// for RESID (one array: a second __shared__ object can make hipcc drain the LDS-DMA ring,
+// cdna_hip_programming.md §5 item 4(a))
 template <int EPI> constexpr int smem256() {
-  return 2 * STAGE_BIG + (EPI == SR_EPI_QKV ? ROPE_LDS : EPI == SR_EPI_BIAS_RESID ? XPF_SINK : 0);
+  return 2 * STAGE_BIG + (EPI == SR_EPI_QKV ? ROPE_LDS : EPI == SR_EPI_BIAS_RESID ? RESID_GB : 0);
 }
 
-template <int EPI>
+template <int EPI, bool RLDS>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
   const char* rope = stage_rope<EPI>(g, smem);
-  gemm256_tile<EPI>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, false, -1, rope);
-}
-
-// The same tile with the ping-pong k-loop (SR_TUNE_GEMM_PP, gemm256_tile<EPI, false, true>).
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256pp_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
-  const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
-  const char* rope = stage_rope<EPI>(g, smem);
-  gemm256_tile<EPI, false, true>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, false, -1, rope);
-}
-
-// Persistent form (SR_TUNE_GEMM_PERSIST): one workgroup per CU walks tiles t = blockIdx.x + i *
-// gridDim.x (gridDim.x a multiple of 8, so every tile of a workgroup sits on its XCD's contiguous
-// xcd_remap range, as in the one-tile-per-workgroup launch); each tile's epilogue overlaps the
-// next tile's first K stage, and no workgroup is relaunched between tiles.
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256_persist_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
-  const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
-  const char* rope = stage_rope<EPI>(g, smem);
-  bool staged = false;
-  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    const int nxt = t + (int)gridDim.x < nt ? sr::xcd_remap(t + gridDim.x, nt) : -1;
-    staged = gemm256_tile<EPI, true>(g, smem, sr::xcd_remap(t, nt), 0, g.ktiles, staged, nxt, rope);
-  }
+  gemm256_tile<EPI, RLDS>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, rope);
 }
 
 // Up to 4 independent 256x256 GEMMs of one epilogue kind in ONE launch (sr_gemm_group): problem
@@ -1027,7 +996,7 @@ struct GemmGroup {
   int n;
 };
 
-template <int EPI, bool PP = false>
+template <int EPI, bool RLDS>
 __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
   int p = 0;
@@ -1038,7 +1007,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   const int lin = blockIdx.x - gg.start[p];
   if (lin >= nt) return;  // padding
   const char* rope = stage_rope<EPI>(g, smem);
-  gemm256_tile<EPI, false, PP>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, false, -1, rope);
+  gemm256_tile<EPI, RLDS>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, rope);
 }
 
 
@@ -1051,29 +1020,19 @@ static int tile_group_m(int N) {
   return g >= 0 ? g : (N >= 3072 ? 4 : 0);
 }
 
-// the persistent form applies (SR_TUNE_GEMM_PERSIST, more tiles than one round)
-static bool use_persist(int epi, long nwg) {
-  const int cus = sr::cu_count() / 8 * 8;
-  return sr::tune(SR_TUNE_GEMM_PERSIST) && epi != SR_EPI_PATCH && cus >= 8 && nwg > cus;
-}
-
 template <int EPI>
 int launch256(GemmArgs a, hipStream_t s) {
   const int nwg = (a.N / BIG) * ((a.M + BIG - 1) / BIG);
   a.group_m = tile_group_m(a.N);
-  const int cus = sr::cu_count() / 8 * 8;
-  if (use_persist(EPI, nwg)) {
-    hipLaunchKernelGGL((gemm256_persist_kernel<EPI>), dim3(cus), dim3(512), 0, s, a);
-    sr::note_kernel("gemm256_persist_kernel<%d>", EPI);
-    return sr::check_launch("sr_gemm(256, persistent)");
+  if constexpr (EPI == SR_EPI_BIAS_RESID) {
+    if (a.resid_lds) {
+      hipLaunchKernelGGL((gemm256_kernel<EPI, true>), dim3(nwg), dim3(512), 0, s, a);
+      sr::note_kernel("gemm256_kernel<%d, true>", EPI);
+      return sr::check_launch("sr_gemm(256)");
+    }
   }
-  if (sr::tune(SR_TUNE_GEMM_PP)) {
-    hipLaunchKernelGGL((gemm256pp_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
-    sr::note_kernel("gemm256pp_kernel<%d>", EPI);
-    return sr::check_launch("sr_gemm(256, ping-pong)");
-  }
-  hipLaunchKernelGGL((gemm256_kernel<EPI>), dim3(nwg), dim3(512), 0, s, a);
-  sr::note_kernel("gemm256_kernel<%d>", EPI);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, false>), dim3(nwg), dim3(512), 0, s, a);
+  sr::note_kernel("gemm256_kernel<%d, false>", EPI);
   return sr::check_launch("sr_gemm(256)");
 }
 
@@ -1139,10 +1098,7 @@ int launch256_tail(GemmArgs a, hipStream_t s) {
       if (rc != SR_OK) return rc;
       rc = launch<bf16, EPI>(row_slice<EPI>(a, main_rows, rest), s);
       // the launch the time goes to
-      sr::note_kernel(use_persist(EPI, whole)         ? "gemm256_persist_kernel<%d>"
-                      : sr::tune(SR_TUNE_GEMM_PP) ? "gemm256pp_kernel<%d>"
-                                                  : "gemm256_kernel<%d>",
-                      EPI);
+      sr::note_kernel("gemm256_kernel<%d, %s>", EPI, EPI == SR_EPI_BIAS_RESID && a.resid_lds ? "true" : "false");
       return rc;
     }
   }
@@ -1341,8 +1297,9 @@ static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda
   a.ep = *ep;
   a.partial = nullptr;
   a.kt_per_split = a.ktiles;
-  const int xpf = sr::tune(SR_TUNE_GEMM_XPF);
-  a.xpf = epi != SR_EPI_BIAS_RESID || dtype != SR_BF16 ? 0 : xpf < 0 ? (a.ktiles >= 32 ? 1 : 2) : min(xpf, 2);
+  a.resid_lds = epi == SR_EPI_BIAS_RESID && dtype == SR_BF16 && sr::tune(SR_TUNE_GEMM_RESID_LDS) != 0 &&
+                ((uintptr_t)out % 16) == 0 && ldo % 4 == 0 && ((uintptr_t)ep->gamma % 16) == 0 &&
+                ((uintptr_t)ep->bias % 16) == 0;
   a.rope_lds = sr::tune(SR_TUNE_GEMM_ROPE_LDS) != 0;
   return SR_OK;
 }
@@ -1397,22 +1354,22 @@ extern "C" int sr_gemm_group(sr_stream_t stream, int dtype, int epi, int n, cons
   for (int i = n + 1; i <= GROUP_MAX; ++i) gg.start[i] = gg.start[n];
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(gg.start[n]);
-  const bool pp = sr::tune(SR_TUNE_GEMM_PP) != 0;
-#define SR_GROUP_LAUNCH(E)                                                                              \
-  do {                                                                                                  \
-    if (pp) hipLaunchKernelGGL((gemm256_group_kernel<E, true>), grid, dim3(512), 0, s, gg);            \
-    else hipLaunchKernelGGL((gemm256_group_kernel<E, false>), grid, dim3(512), 0, s, gg);              \
-  } while (0)
+  // the LDS-staged RESID epilogue when every problem qualifies (gemm_args: alignment, the switch)
+  bool rlds = epi == SR_EPI_BIAS_RESID;
+  for (int i = 0; i < n; ++i) rlds = rlds && gg.g[i].resid_lds;
+#define SR_GROUP_LAUNCH(E) hipLaunchKernelGGL((gemm256_group_kernel<E, false>), grid, dim3(512), 0, s, gg)
   switch (epi) {
     case SR_EPI_BIAS: SR_GROUP_LAUNCH(SR_EPI_BIAS); break;
     case SR_EPI_QKV: SR_GROUP_LAUNCH(SR_EPI_QKV); break;
     case SR_EPI_BIAS_GELU: SR_GROUP_LAUNCH(SR_EPI_BIAS_GELU); break;
     case SR_EPI_F32: SR_GROUP_LAUNCH(SR_EPI_F32); break;
     case SR_EPI_GELU_BWD: SR_GROUP_LAUNCH(SR_EPI_GELU_BWD); break;
-    default: SR_GROUP_LAUNCH(SR_EPI_BIAS_RESID);
+    default:
+      if (rlds) hipLaunchKernelGGL((gemm256_group_kernel<SR_EPI_BIAS_RESID, true>), grid, dim3(512), 0, s, gg);
+      else SR_GROUP_LAUNCH(SR_EPI_BIAS_RESID);
   }
 #undef SR_GROUP_LAUNCH
-  sr::note_kernel("gemm256_group_kernel<%d, %s>", epi, pp ? "true" : "false");  // as rocprofv3 names it
+  sr::note_kernel("gemm256_group_kernel<%d, %s>", epi, rlds ? "true" : "false");  // as rocprofv3 names it
   return sr::check_launch("sr_gemm_group");
 }
 

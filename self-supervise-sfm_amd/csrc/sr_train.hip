@@ -155,8 +155,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs g) {
 constexpr int WT2 = 256;
 
 // MT rows per m-tile, NST LDS stages (MT/8 DMA pieces per wave and stage): <64, 2> stages the next
-// 64-row tile while computing the current one; <48, 3> (SR_TUNE_WGRAD_STAGES=3) keeps two 48-row tiles
-// in flight (144 KiB), for operands that come from beyond L2.
+// 64-row tile while computing the current one (a <48, 3> form with two 48-row tiles in flight measured
+// no faster and was removed in round 6).
 // Two problems of equal N and K in one launch (sr_gemm_wgrad_pair): slices blockIdx.y < y0 belong to
 // g0, the rest to g1 (a single problem passes g1 = g0, y0 = its slice count).
 template <int MT, int NST>
@@ -1051,13 +1051,9 @@ extern "C" int sr_gemm_wgrad(sr_stream_t stream, const void* A, int64_t lda, con
   if (rc != SR_OK) return rc;
   // 256 x 256 tiles (one workgroup per CU) for the aggregator shapes; SR_WGRAD256=0: 128 x 128
   const bool big = sr::tune(SR_TUNE_WGRAD256) != 0 && N % WT2 == 0 && K % WT2 == 0;
-  const bool st3 = big && sr::tune(SR_TUNE_WGRAD_STAGES) == 3;
-  const WgradArgs g = wgrad_args(A, lda, B, ldb, M, N, K, st3 ? 48 : 64, splits, workspace);
+  const WgradArgs g = wgrad_args(A, lda, B, ldb, M, N, K, 64, splits, workspace);
   hipStream_t s = (hipStream_t)stream;
-  if (st3) {
-    hipLaunchKernelGGL((wgrad256_kernel<48, 3>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g, g, splits);
-    sr::note_kernel("wgrad256_kernel<48, 3>");
-  } else if (big) {
+  if (big) {
     hipLaunchKernelGGL((wgrad256_kernel<64, 2>), dim3((N / WT2) * (K / WT2), splits), dim3(512), 0, s, g, g, splits);
     sr::note_kernel("wgrad256_kernel");
   } else {
@@ -1081,16 +1077,14 @@ extern "C" int sr_gemm_wgrad_pair(sr_stream_t stream, const sr_wgrad_problem* p)
            "sr_gemm_wgrad_pair: both problems need the same N, K, multiples of %d (%dx%d, %dx%d)", WT2, N, K, p[1].N,
            p[1].K);
   SR_CHECK(sr::tune(SR_TUNE_WGRAD256) != 0, SR_EUNSUPPORTED, "sr_gemm_wgrad_pair: needs the 256x256 kernel");
-  const bool st3 = sr::tune(SR_TUNE_WGRAD_STAGES) == 3;
   int sp[2] = {p[0].splits, p[1].splits};
   WgradArgs g[2];
   for (int i = 0; i < 2; ++i)
-    g[i] = wgrad_args(p[i].A, p[i].lda, p[i].B, p[i].ldb, p[i].M, N, K, st3 ? 48 : 64, sp[i], p[i].workspace);
+    g[i] = wgrad_args(p[i].A, p[i].lda, p[i].B, p[i].ldb, p[i].M, N, K, 64, sp[i], p[i].workspace);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((N / WT2) * (K / WT2), sp[0] + sp[1]);
-  if (st3) hipLaunchKernelGGL((wgrad256_kernel<48, 3>), grid, dim3(512), 0, s, g[0], g[1], sp[0]);
-  else hipLaunchKernelGGL((wgrad256_kernel<64, 2>), grid, dim3(512), 0, s, g[0], g[1], sp[0]);
-  sr::note_kernel(st3 ? "wgrad256_kernel<48, 3>" : "wgrad256_kernel");
+  hipLaunchKernelGGL((wgrad256_kernel<64, 2>), grid, dim3(512), 0, s, g[0], g[1], sp[0]);
+  sr::note_kernel("wgrad256_kernel");
   for (int i = 0; i < 2; ++i)
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(N), dim3(256), 0, s, p[i].workspace, sp[i], N, K, p[i].dW, p[i].lddw,
                        p[i].accumulate, p[i].rowscale, p[i].wdot, p[i].ldwd, p[i].rowdot);

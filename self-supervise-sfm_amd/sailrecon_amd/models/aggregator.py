@@ -714,7 +714,7 @@ class Aggregator(nn.Module):
             split = lambda n: ops.key_split_parts(dtype=q.dtype, batch=1, lq=lq, heads=H, l0=n, l1=0,  # noqa: E731
                                                   mask_mode=0)
             plan = [(kv_loc, split(lq))] + [(kv_all[a:a + n], split(n)) for a, n in segs]
-            plan = [(kv, _align_pieces(kv.shape[0], p)) for kv, p in plan]
+            plan = [(kv, [(0, kv.shape[0], p)]) for kv, p in plan]  # one launch of p equal chunks per pass
             total = sum(pp for _, pieces in plan for _, _, pp in pieces)
             o_parts, lse_parts = ops.key_split_workspace(q.device, total, lq, C, H, name="attn_shard")
             p0 = 0
@@ -832,29 +832,6 @@ class Aggregator(nn.Module):
 # hand-scheduled sweep's ragged variant (round 3 measured it level with the compiled sweep per rank:
 # DESIGN.md section 5)
 _SHARD_TAIL = os.environ.get("SR_SHARD_TAIL", "0") == "1"
-# SR_SHARD_ALIGN (A/B switch): the frame-sharded global block's key-split passes cut their keys into
-# p-1 chunks of whole 64-key tiles plus one remainder chunk instead of p equal chunks, so that p-1
-# of them run on the hand-scheduled sweep (an equal split of 1,374-row frames is never tile-aligned)
-_SHARD_ALIGN = int(os.environ.get("SR_SHARD_ALIGN", "0"))
-
-
-def _align_pieces(n: int, p: int):
-    """Key chunks of one key-split pass over n keys in p parts, as launches (start, keys, parts):
-    p equal chunks (SR_SHARD_ALIGN=0); p-1 chunks of ceil(n/p/64) whole tiles + the rest (=1); p
-    chunks of floor(n/p/64) whole tiles + a short remainder chunk, p+1 parts (=2; =3: only for
-    passes of p >= 4 parts).  Whole-tile
-    chunks run on the hand-scheduled sweep; 1,374-row frames never split into them evenly."""
-    if not _SHARD_ALIGN or p < 2 or n % (p * 64) == 0 or (_SHARD_ALIGN == 3 and p < 4):
-        return [(0, n, p)]
-    if _SHARD_ALIGN == 1:
-        c = (n + p * 64 - 1) // (p * 64) * 64
-        if n - (p - 1) * c <= 0:
-            return [(0, n, p)]
-        return [(0, (p - 1) * c, p - 1), ((p - 1) * c, n - (p - 1) * c, 1)]
-    c = n // (p * 64) * 64
-    if c == 0:
-        return [(0, n, p)]
-    return [(0, p * c, p), (p * c, n - p * c, 1)]
 # SR_SHARD_CONCURRENT (default 1; 0 for the A/B): under frame sharding with grouped tails, the reloc
 # attention on a second stream beside the global attention.  Rank-0 rehearsal, one box, 2 runs each
 # (profiles/r05_j10_rs_*.log): G = 8 69.03 / 69.15 -> 66.87 / 66.98 ms, G = 4 121.8 / 121.0 -> 120.9 /

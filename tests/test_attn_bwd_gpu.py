@@ -109,52 +109,6 @@ def test_attention_bwd_matches_autograd(case, dt, D):
         assert _rel(dk1, dk1_r) < tol and _rel(dv1, dv1_r) < tol
 
 
-@pytest.mark.parametrize("case", ["frame", "global", "reloc"])
-def test_attention_bwd_two_key_blocks_per_wave(case):
-    """SR_ATTN_BWD_KB=2: the dK/dV sweep with 64 keys per wave (one wave per SIMD, every Q / dO
-    fragment feeding two key blocks) gives bit-identical dK / dV (and dQ) to the 32-key form,
-    ragged key counts included."""
-    from sailrecon_amd import ops
-    torch.manual_seed(1)
-    H, D = 4, 64
-    C = H * D
-    if case == "frame":
-        B, P, A = 3, 150, 0
-        kw = dict(batch=B, lq=P, q_bstride=P, l0=P, k0_bstride=P)
-    elif case == "global":
-        B, P, A = 1, 1100, 0
-        kw = dict(batch=1, lq=P, q_bstride=P, l0=P, k0_bstride=P)
-    else:
-        B, P, A = 3, 150, 301
-        kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, l1=P, k1_bstride=P)
-    x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
-    q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
-    if case == "reloc":
-        ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
-        k0, v0 = ka[:, :C], ka[:, C:]
-        kw.update(k1=k, v1=v)
-    else:
-        k0, v0 = k, v
-    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
-    lse = torch.empty(B, H, P, device=DEV)
-    ops.attention(q, k0, v0, o, heads=H, head_dim=D, lse=lse, **kw)
-    g = torch.randn(B * P, C, device=DEV).bfloat16()
-    outs = []
-    for kbn in (1, 2):
-        dq = torch.empty(B * P, C, device=DEV)
-        dk0, dv0 = torch.empty(k0.shape[0], C, device=DEV), torch.empty(k0.shape[0], C, device=DEV)
-        dk1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
-        dv1 = torch.empty(B * P, C, device=DEV) if case == "reloc" else None
-        delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_KB=kbn, SR_ATTN_BWD_PIPE=0):
-            ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
-            assert ops.last_kernel() == f"attn_bwd_dkdv_kernel<0, {kbn}>"
-        outs.append([t for t in (dq, dk0, dv0, dk1, dv1) if t is not None])
-    torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("case,P", [("frame", 1374), ("frame", 256), ("frame", 337), ("frame", 384), ("frame", 511),
                                     ("frame", 512), ("frame", 200), ("global", 1100), ("reloc", 300),
                                     ("anchor", 150)])
@@ -202,53 +156,16 @@ def test_attention_bwd_pipe(case, P):
         dk1 = torch.full((B * P, C), float("nan"), device=DEV) if case == "reloc" else None
         dv1 = torch.full((B * P, C), float("nan"), device=DEV) if case == "reloc" else None
         delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_PIPE=pipe, SR_ATTN_BWD_DQ_PIPE=2 * pipe, SR_ATTN_BWD_KB=1,
-                        SR_ATTN_BWD_CONC=pipe, SR_ATTN_BWD_CAT=0):
+        with ops.tuning(SR_ATTN_BWD_PIPE=pipe, SR_ATTN_BWD_DQ_PIPE=2 * pipe, SR_ATTN_BWD_CAT=0):
             ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
             asm_dkdv = pipe and P >= 256 and case not in ("reloc", "anchor")
-            want = "attn_bwd_dkdv_pipe_kernel<0>" if asm_dkdv else "attn_bwd_dkdv_kernel<0, 1>"
+            want = "attn_bwd_dkdv_pipe_kernel<0>" if asm_dkdv else "attn_bwd_dkdv_kernel<0>"
             assert ops.last_kernel() == want
         outs.append([t for t in (dq, dk0, dv0, dk1, dv1) if t is not None])
     torch.cuda.synchronize()
     for a, b in zip(*outs):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
-
-
-def test_attention_bwd_shared_key_split():
-    """SR_ATTN_BWD_QSPLIT: anchors shared by a batch of 3 (the reloc block's segment 0): the dK/dV
-    sweep over the items in two halves adding atomically into zero-filled outputs equals the one-pass
-    sweep to fp32 summation order, and is deterministic (two addends into zeros)."""
-    from sailrecon_amd import ops
-    torch.manual_seed(3)
-    H, D, B, P, A = 4, 64, 3, 300, 301
-    C = H * D
-    kw = dict(batch=B, lq=P, q_bstride=P, l0=A, k0_bstride=0, l1=P, k1_bstride=P)
-    x = torch.randn(B * P, 3 * C, device=DEV).bfloat16()
-    q, k, v = x[:, :C], x[:, C:2 * C], x[:, 2 * C:]
-    ka = torch.randn(A, 2 * C, device=DEV).bfloat16()
-    k0, v0 = ka[:, :C], ka[:, C:]
-    kw.update(k1=k, v1=v)
-    o = torch.empty(B * P, C, device=DEV, dtype=torch.bfloat16)
-    lse = torch.empty(B, H, P, device=DEV)
-    ops.attention(q, k0, v0, o, heads=H, head_dim=D, lse=lse, **kw)
-    g = torch.randn(B * P, C, device=DEV).bfloat16()
-    outs = []
-    for split in (0, 2, 2):
-        dq = torch.empty(B * P, C, device=DEV)
-        dk0 = torch.full((A, C), float("nan"), device=DEV)
-        dv0 = torch.full((A, C), float("nan"), device=DEV)
-        dk1, dv1 = torch.empty(B * P, C, device=DEV), torch.empty(B * P, C, device=DEV)
-        delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_QSPLIT=split, SR_ATTN_BWD_CAT=0):
-            ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
-            assert ops.last_kernel() == ("attn_bwd_dkdv_kernel<0, 1, split2>" if split else "attn_bwd_dkdv_kernel<0, 1>")
-        outs.append((dq, dk0, dv0, dk1, dv1))
-    torch.cuda.synchronize()
-    for a, b, c in zip(*outs):
-        assert torch.isfinite(b).all()
-        assert torch.equal(b, c)  # deterministic
-        assert (a - b).abs().max() <= 1e-5 * a.abs().max()  # summation order only
 
 
 @pytest.mark.parametrize("B,P", [(3, 300), (2, 1374), (5, 64)])
@@ -278,9 +195,9 @@ def test_attention_bwd_concatenated_items(B, P):
         dv0 = torch.full((A, C), float("nan"), device=DEV)
         dk1, dv1 = torch.empty(B * P, C, device=DEV), torch.empty(B * P, C, device=DEV)
         delta = torch.empty(B, H, P, device=DEV)
-        with ops.tuning(SR_ATTN_BWD_CAT=cat, SR_ATTN_BWD_QSPLIT=0):
+        with ops.tuning(SR_ATTN_BWD_CAT=cat):
             ops.attention_bwd(q, k0, v0, o, lse, g, dq, dk0, dv0, delta, heads=H, dk1=dk1, dv1=dv1, **kw)
-            want = "attn_bwd_dkdv_pipe_kernel<0, cat>" if cat and B * P >= 256 else "attn_bwd_dkdv_kernel<0, 1>"
+            want = "attn_bwd_dkdv_pipe_kernel<0, cat>" if cat and B * P >= 256 else "attn_bwd_dkdv_kernel<0>"
             assert ops.last_kernel() == want
         outs.append((dq, dk0, dv0, dk1, dv1))
     torch.cuda.synchronize()

@@ -521,46 +521,6 @@ def test_frame_attention_production(ops, tail):
         assert _rel(o[fr][rows].float(), ref) < 1e-2, j
 
 
-@pytest.mark.parametrize("kind", ["frame", "reloc"])
-def test_attention_q_tail_launch(ops, kind):
-    """SR_ATTN_QTAIL (default on): the 94 rows of each 1,374-row frame past its 5 whole 256-row
-    q-tiles run as a second launch of 128-row workgroups instead of a padded sixth 4 x 2 tile.
-    Each wave's rows see the same code and key order, so the output (and the reloc own-frame
-    pass's LSE and merge-in) is bit-identical to the one-launch form; the tail rows against fp64."""
-    S = 16
-    q, k, v = _make(S * P, 7, spikes=(S * P - 2, 5 * 256 + 3))
-    kw = dict(heads=H, head_dim=D, batch=S, lq=P, q_bstride=P)
-    if kind == "frame":
-        kw.update(k=k, v=v, l0=P, k0_bstride=P)
-    else:
-        ks, _, vs = _make(8 * PP, 8)
-        mo = torch.randn(S * P, C, device=DEV, generator=torch.Generator(DEV).manual_seed(9)).bfloat16()
-        ml = torch.randn(H, S * P, device=DEV, generator=torch.Generator(DEV).manual_seed(10)) * 4
-        kw.update(k=ks, v=vs, l0=8 * PP, k0_bstride=0, k1=k, v1=v, l1=P, k1_bstride=P, merge_o=mo, merge_lse=ml)
-    outs = []
-    for qt in (0, 1, 2):  # one padded tile | 2 x 2 tail workgroups | 4 x 1
-        o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
-        lse = torch.empty(S, H, P, device=DEV)
-        a = dict(kw)
-        kk, vv = a.pop("k"), a.pop("v")
-        with ops.tuning(SR_ATTN_QTAIL=qt):
-            ops.attention(q, kk, vv, o, lse=lse.view(-1), **a)
-            assert ops.last_kernel() == f"attn_bf16_kernel<4, 2, {0 if kind == 'frame' else 1}, false>"
-        outs.append((o, lse))
-    torch.cuda.synchronize()
-    for i in (1, 2):
-        print(f"q-tail {kind} {i}: max |o diff| {float((outs[0][0].float() - outs[i][0].float()).abs().max()):.3g}, "
-              f"max |lse diff| {float((outs[0][1] - outs[i][1]).abs().max()):.3g}")
-        assert torch.equal(outs[0][0], outs[i][0]) and torch.equal(outs[0][1], outs[i][1])
-    if kind == "frame":
-        scale = D ** -0.5
-        o = outs[1][0]
-        for j in (0, 9, S - 1):
-            fr = slice(j * P, (j + 1) * P)
-            rows = torch.arange(5 * 256, P, device=DEV)
-            assert _rel(o[fr][rows].float(), _ref_rows(q[fr][rows], k[fr], v[fr], scale)) < 1e-2, j
-
-
 @pytest.mark.parametrize("S,L,static", [(16, P, True), (16, P, False), (40, 300, True), (5, P, False),
                                         (24, 777, True)],
                          ids=["16x1374", "16x1374-keyscan", "40x300", "5x1374-keyscan", "24x777"])

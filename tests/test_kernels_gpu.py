@@ -103,51 +103,13 @@ def test_gemm_splitk(ops, dtype, tol, M, N, K, splits):
     assert rel(o32, ref) < max(tol, 1e-5)
 
 
-@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32"])
-@pytest.mark.parametrize("M,N,K", [(33000, 1024, 1024), (12000, 3072, 256), (20000, 4096, 1024), (33000, 1024, 4096)])
-def test_gemm_ping_pong(ops, epi_name, M, N, K):
-    """SR_GEMM_PP: the 256x256 GEMM's ping-pong k-loop (each SIMD's two waves alternate a k-step of
-    MFMAs with the other's LDS reads / DMA) gives bit-identical outputs to the default loop, ragged
-    last row tile and tail split included."""
-    L = _lib()
-    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
-    g = torch.Generator(device="cpu").manual_seed(M + N + K)
-    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV, torch.bfloat16)
-    b, gam = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
-    epi = getattr(L, "SR_EPI_" + epi_name)
-    kw = dict(bias=b)
-    if epi_name == "BIAS_RESID":
-        kw["gamma"] = gam
-    if epi_name == "QKV":
-        C = N // 3 if N % 3 == 0 else None
-        if C is None or C % 64:
-            pytest.skip("QKV needs whole q|k|v blocks")
-        rope = RotaryPositionEmbedding2D(100).tables(64, 40, DEV)
-        qn = [torch.randn(64, device=DEV, generator=torch.Generator(DEV).manual_seed(i)) for i in range(4)]
-        kw["qkv"] = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
-                         rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37,
-                         pos_row_base=3, q_scale=0.18)
-    outs = []
-    for pp in (0, 1):
-        if epi_name in ("BIAS_RESID", "F32"):
-            out = torch.randn(M, N, generator=torch.Generator().manual_seed(5)).to(DEV)
-        else:
-            out = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
-        with ops.tuning(SR_GEMM_PP=pp):
-            ops.gemm(a, w, out, epi, splits=1, **kw)
-            if pp:
-                assert ops.last_kernel() == f"gemm256pp_kernel<{epi}>"
-        outs.append(out)
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("M,K", [(33000, 1024), (43968, 4096), (8300, 256)])
-def test_gemm_resid_x_prefetch(ops, M, K):
-    """SR_GEMM_XPF: the 256x256 residual GEMM fetching its x tile into L2 / MALL under the k-loop
-    (1 or 2 rows per k-tile and wave, or auto) computes exactly what it computes without, in the
-    one-kernel launch, with the 128x128 tail split, and in a grouped launch."""
+@pytest.mark.parametrize("M,K", [(33000, 1024), (43968, 4096), (8300, 256), (4100, 64)])
+def test_gemm_resid_lds_epilogue(ops, M, K):
+    """SR_GEMM_RESID_LDS: the 256x256 residual GEMM staging its x tile through LDS by LDS-DMA
+    (quarter 0 under the last k-tile, two quarters in flight, whole-row stores) computes exactly
+    what the register epilogue computes, in the one-kernel launch, with the 128x128 tail split, and
+    in a grouped launch; K = 64 is a single k-tile (quarter 0 into the never-used stage buffer),
+    ragged M leaves a partial last row tile on the guarded path."""
     L = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + K)
     N = 1024
@@ -156,22 +118,27 @@ def test_gemm_resid_x_prefetch(ops, M, K):
     b, gam = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
     x0 = torch.randn(M, N, generator=g).to(DEV)
     outs = []
-    for xpf in (0, 1, 2, -1):
+    for rl in (0, 1):
         for tail in (0, 1):
             x = x0.clone()
-            with ops.tuning(SR_GEMM_XPF=xpf, SR_GEMM_TAIL=tail):
+            with ops.tuning(SR_GEMM_RESID_LDS=rl, SR_GEMM_TAIL=tail):
                 ops.gemm(a, w, x, L.SR_EPI_BIAS_RESID, bias=b, gamma=gam, splits=1)
             outs.append(x)
         x = x0.clone()
-        with ops.tuning(SR_GEMM_XPF=xpf):
+        with ops.tuning(SR_GEMM_RESID_LDS=rl):
             h = M // 2
             ops.gemm_group([dict(a=a[:h], w=w, out=x[:h], bias=b, gamma=gam),
                             dict(a=a[h:], w=w, out=x[h:], bias=b, gamma=gam)], L.SR_EPI_BIAS_RESID)
         outs.append(x)
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
+        x = x0.clone()
+        with ops.tuning(SR_GEMM_RESID_LDS=rl):  # no bias
+            ops.gemm(a, w, x, L.SR_EPI_BIAS_RESID, gamma=gam, splits=1)
+        outs.append(x)
+    for i in (1, 2, 4, 5, 6):
+        assert torch.equal(outs[i], outs[0 if i != 6 else 3]), i
     ref = (a.float() @ w.float().t() + b) * gam
     assert rel(outs[0] - x0, ref) < 1e-5
+    assert rel(outs[3] - x0, (a.float() @ w.float().t()) * gam) < 1e-5
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-5)])
@@ -691,7 +658,7 @@ def test_gemm_tail_split(ops, epi_name, M, N):
         ops.gemm(a, w, out0, epi, splits=1, **kw0)
         k0 = ops.last_kernel()
     torch.cuda.synchronize()
-    assert k1 == k0 and k0.startswith(("gemm256_kernel", "gemm256pp_kernel")), (k1, k0)
+    assert k1 == k0 and k0.startswith("gemm256_kernel"), (k1, k0)
     same = torch.equal(out1, out0)
     print(f"{epi_name} M={M} N={N}: bit-identical={same} rel={rel(out1.float(), out0.float()):.2e}")
     assert rel(out1.float(), out0.float()) < 1e-6
@@ -705,51 +672,6 @@ def test_gemm_tail_split(ops, epi_name, M, N):
         c = 0.125 * 1.4426950408889634
         assert torch.equal(out1[:, C:], plain[:, C:])
         assert rel(out1[:, :C].float(), plain[:, :C].float() * c) < 4e-3
-
-
-@pytest.mark.parametrize("epi_name", ["BIAS", "BIAS_GELU", "BIAS_RESID", "QKV", "F32", "GELU_BWD"])
-@pytest.mark.parametrize("M,N,K", [(43 * 256 - 100, 3072, 1024), (87936, 1024, 1024), (2 * 5496, 4096, 1024),
-                                   (43968, 1024, 4096)])
-def test_gemm_persistent(ops, epi_name, M, N, K):
-    """SR_GEMM_PERSIST: the 256x256 GEMM as one persistent workgroup per CU, each tile's epilogue
-    overlapping the next tile's first K stage (register and LDS-staged epilogues, ragged last row
-    tile, with and without the tail split).  Per output tile the same MFMA sequence as the
-    one-tile-per-workgroup kernel: bit-identical."""
-    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
-    L = _lib()
-    epi = getattr(L, "SR_EPI_" + epi_name)
-    C = 1024
-    g = torch.Generator(device=DEV).manual_seed(M + N + K)
-    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
-    w = (torch.randn(N, K, device=DEV, generator=g) / 32).bfloat16()
-    kw = dict(bias=torch.randn(N, device=DEV, generator=g))
-    if epi_name == "QKV":
-        if N % C or N > 3 * C:
-            pytest.skip("QKV needs whole q|k|v blocks")
-        rope = RotaryPositionEmbedding2D(100).tables(64, 40, DEV)
-        qn = [torch.randn(64, device=DEV, generator=g) for _ in range(4)]
-        kw["qkv"] = dict(embed_dim=C, head_dim=64, qk_eps=1e-5, qn_w=qn[0], qn_b=qn[1], kn_w=qn[2], kn_b=qn[3],
-                         rope_cos=rope[0], rope_sin=rope[1], tokens_per_frame=1374, patch_start=5, grid_w=37,
-                         pos_row_base=11, col_offset=3 * C - N)
-    if epi_name == "BIAS_RESID":
-        kw["gamma"] = torch.randn(N, device=DEV, generator=g)
-    if epi_name == "GELU_BWD":
-        kw = dict(aux=torch.randn(M, N, device=DEV, generator=g).bfloat16())
-    if epi_name in ("BIAS_RESID", "F32"):
-        x0 = torch.randn(M, N, device=DEV, generator=g)
-        outs = [x0.clone() for _ in range(4)]
-    else:
-        outs = [torch.zeros(M, N, device=DEV, dtype=torch.bfloat16) for _ in range(4)]
-    names = []
-    for i, (persist, tail) in enumerate(((0, 0), (1, 0), (0, 1), (1, 1))):
-        with ops.tuning(SR_GEMM_PERSIST=persist, SR_GEMM_TAIL=tail):
-            ops.gemm(a, w, outs[i], epi, splits=1, **kw)
-            names.append(ops.last_kernel())
-    torch.cuda.synchronize()
-    print(f"{epi_name} M={M} N={N} K={K}: {names}")
-    assert names[1].startswith("gemm256_persist_kernel") and names[0].startswith("gemm256_kernel"), names
-    assert torch.equal(outs[1], outs[0])
-    assert torch.equal(outs[3], outs[2])
 
 
 def test_merge_with_empty_partial(ops):

@@ -45,11 +45,9 @@ def test_gemm_wgrad(ops, M, N, K, splits):
     dy = torch.randn(M, N, device=DEV).bfloat16()
     x = torch.randn(M, K, device=DEV).bfloat16()
     ref = dy.float().t() @ x.float()
-    for stages in (2, 3):  # SR_WGRAD_STAGES: 64-row m-tiles one stage ahead / 48-row two ahead
-        dw = torch.empty(N, K, device=DEV)
-        with ops.tuning(SR_WGRAD_STAGES=stages):
-            ops.gemm_wgrad(dy, x, dw, splits=splits)
-        assert rel(dw, ref) < 1e-5
+    dw = torch.empty(N, K, device=DEV)
+    ops.gemm_wgrad(dy, x, dw, splits=splits)
+    assert rel(dw, ref) < 1e-5
 
 
 @pytest.mark.parametrize("K", [128, 256])
@@ -73,10 +71,9 @@ def test_gemm_wgrad_strided_accumulate_rowscale_rowdot(ops, K):
     assert rel(rowdot - rd0, (wdot * G).sum(1)) < 1e-5
 
 
-@pytest.mark.parametrize("stages", [2, 3])
 @pytest.mark.parametrize("M0, M1, N, K", [(21984, 21984, 1024, 4096), (21984, 4397, 1024, 1024),
                                           (777, 1300, 256, 512)])
-def test_gemm_wgrad_pair(ops, M0, M1, N, K, stages):
+def test_gemm_wgrad_pair(ops, M0, M1, N, K):
     """sr_gemm_wgrad_pair (the layer's reloc and global blocks' weight grads in one launch, as
     train.engine.block_bwd_multi runs them): per problem bit-identical to sr_gemm_wgrad with the
     same slices, with accumulate / rowscale / rowdot on one problem and not the other; and within
@@ -94,11 +91,10 @@ def test_gemm_wgrad_pair(ops, M0, M1, N, K, stages):
         probs.append(p)
         refs.append(dict(p, dw=dw0.clone(), rowdot=None if i else torch.zeros(N, device=DEV)))
     sp = ops.wgrad_pair_splits(M0, M1, N, K) or (3, 5)
-    with ops.tuning(SR_WGRAD_STAGES=stages):
-        ops.gemm_wgrad_pair(probs, sp)
-        for r, s in zip(refs, sp):
-            ops.gemm_wgrad(r["dy"], r["x"], r["dw"], accumulate=r.get("accumulate", False), rowscale=r.get("rowscale"),
-                           wdot=r.get("wdot"), rowdot=r.get("rowdot"), splits=s)
+    ops.gemm_wgrad_pair(probs, sp)
+    for r, s in zip(refs, sp):
+        ops.gemm_wgrad(r["dy"], r["x"], r["dw"], accumulate=r.get("accumulate", False), rowscale=r.get("rowscale"),
+                       wdot=r.get("wdot"), rowdot=r.get("rowdot"), splits=s)
     torch.cuda.synchronize()
     for i, (p, r) in enumerate(zip(probs, refs)):
         assert torch.equal(p["dw"], r["dw"])

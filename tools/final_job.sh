@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# round-5 final validation.  A = every GPU test but the multi-rank ones, B = the multi-rank tests +
+# final validation of a round (tools/final_job.sh A|B|C|D).  A = every GPU test but the multi-rank ones, B = the multi-rank tests +
 # smoke, C = default bench (cpu baseline, extras) + rocprofv3 kernel stats (1 and 3 steps: the
 # steady-state counts) + FETCH_SIZE / WRITE_SIZE PMC passes, D = training kernel stats.
 set -u

@@ -218,35 +218,6 @@ def attn_frame_cfg():
         print(f"attn frame cfg {cfg} ({kern}): {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s", flush=True)
 
 
-def attn_qtail():
-    """SR_ATTN_QTAIL A/B, interleaved: the frame / DINO attention (64 frames x 1374 tokens) and the
-    C3 reloc own-frame pass (32 query frames against the subsample's last partial tile + their own
-    1374 keys, merging the subsample pass in) with the 94 rows past each frame's whole 256-row
-    q-tiles in a second launch of 128-row workgroups (1) or in a padded 4 x 2 tile (0)."""
-    C, H, D, P, S = 1024, 16, 64, 1374, 64
-    qkv = torch.randn(S * P + 64, 3 * C, device=DEV, dtype=torch.bfloat16)[:S * P]
-    o = torch.empty(S * P, C, device=DEV, dtype=torch.bfloat16)
-    kb = float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max())
-    nq, ntail = 32, 32 * 305 % 64
-    sub = torch.randn(ntail + 64, 2 * C, device=DEV, dtype=torch.bfloat16)
-    mo = torch.randn(nq * P, C, device=DEV, dtype=torch.bfloat16)
-    ml = torch.randn(H, nq * P, device=DEV)
-    fl_f = 4.0 * S * H * P * P * D
-    fl_r = 4.0 * nq * H * P * (P + ntail) * D
-    for qt in (0, 1, 2, 0, 1, 2):
-        with ops.tuning(SR_ATTN_QTAIL=qt):
-            ms = timeit(lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, heads=H, head_dim=D,
-                                              batch=S, lq=P, q_bstride=P, l0=P, k0_bstride=P, key_norm_max=kb,
-                                              tail_readable=True), reps=20)
-            print(f"attn frame qtail={qt} ({ops.last_kernel()}): {ms:.3f} ms  {fl_f / ms / 1e9:.1f} TF/s", flush=True)
-            ms = timeit(lambda: ops.attention(qkv[:nq * P, :C], sub[:ntail, :C], sub[:ntail, C:], o[:nq * P], heads=H,
-                                              head_dim=D, batch=nq, lq=P, q_bstride=P, l0=ntail, k0_bstride=0,
-                                              k1=qkv[:nq * P, C:2 * C], v1=qkv[:nq * P, 2 * C:], l1=P, k1_bstride=P,
-                                              key_norm_max=kb, tail_readable=True, merge_o=mo, merge_lse=ml), reps=20)
-            print(f"attn reloc-own qtail={qt} ({ops.last_kernel()}): {ms:.3f} ms  {fl_r / ms / 1e9:.1f} TF/s",
-                  flush=True)
-
-
 def attn_frame_diag():
     """Where the frame attention loses against the long sweep: the same launch with no ragged
     q-tile (lq = 1280 = 5 x 256), with full key tiles (l0 = 1408), and with 4x longer key sweeps
@@ -426,30 +397,9 @@ def gemm_qkv(M=2 * 32 * 1374):
         print(f"gemm_qkv group (layer) lds={lds} {ms:8.3f} ms  {flg / ms / 1e9:8.1f} TF/s  {flg / ms / 1e9 / PEAK:6.1%}")
 
 
-def gemm_pp():
-    """SR_GEMM_PP A/B, interleaved: the aggregator GEMMs at C3 frame rows (qkv / proj / fc1 / fc2 with
-    their epilogues) with the default k-loop (0) and the ping-pong k-loop (1), plus 8192^3 BIAS."""
-    M = 2 * 32 * 1374
-    x = torch.randn(M, 1024, device=DEV)
-    for name, (m, N, K, epi) in {"qkv ": (M, 3072, 1024, _lib.SR_EPI_BIAS), "proj": (M, 1024, 1024, _lib.SR_EPI_BIAS_RESID),
-                                 "fc1 ": (M, 4096, 1024, _lib.SR_EPI_BIAS_GELU),
-                                 "fc2 ": (M, 1024, 4096, _lib.SR_EPI_BIAS_RESID),
-                                 "8k^3": (8192, 8192, 8192, _lib.SR_EPI_BIAS)}.items():
-        a = torch.rand(m, K, device=DEV).sub_(0.5).to(torch.bfloat16)
-        w = (torch.rand(N, K, device=DEV).sub_(0.5) / K ** 0.5).to(torch.bfloat16)
-        b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV) * 1e-3
-        out = x[:m, :N] if epi == _lib.SR_EPI_BIAS_RESID else torch.empty(m, N, device=DEV, dtype=torch.bfloat16)
-        fl = 2.0 * m * N * K
-        for pp in (0, 1, 0, 1):
-            with ops.tuning(SR_GEMM_PP=pp):
-                ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam), reps=10)
-            print(f"gemm_pp {name} pp={pp} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
-
-
-def gemm_xpf():
-    """SR_GEMM_XPF A/B, interleaved: the residual GEMMs (proj K=1024, fc2 K=4096) over the C3 frame
-    rows with the x tile prefetched into L2 / MALL under the k-loop (1 or 2 rows per k-tile and wave)
-    or not (0)."""
+def gemm_resid():
+    """SR_GEMM_RESID_LDS A/B, interleaved: the residual GEMMs (proj K=1024, fc2 K=4096) over the C3
+    frame rows with the x tile staged through LDS (1) or the register epilogue (0)."""
     M, N = 2 * 32 * 1374, 1024
     x = torch.randn(M, N, device=DEV)
     b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV) * 1e-3
@@ -457,10 +407,10 @@ def gemm_xpf():
         a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
         w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
         fl = 2.0 * M * N * K
-        for xpf in (0, 1, 2, 0, 1, 2):
-            with ops.tuning(SR_GEMM_XPF=xpf):
+        for rl in (0, 1, 0, 1):
+            with ops.tuning(SR_GEMM_RESID_LDS=rl):
                 ms = timeit(lambda: ops.gemm(a, w, x, _lib.SR_EPI_BIAS_RESID, bias=b, gamma=gam), reps=10)
-            print(f"gemm_xpf {name} xpf={xpf} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
+            print(f"gemm_resid {name} resid_lds={rl} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
 
 
 def gemm_k():
@@ -698,13 +648,10 @@ def attn_bwd():
                 ops.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, lse, g, d[:, :C], d[:, C:2 * C],
                                   d[:, 2 * C:], delta, heads=H, batch=batch, lq=lq, q_bstride=lq, l0=lq, k0_bstride=kb)
         fl = 10.0 * batch * H * lq * (lq + anchors) * D  # S, dP, dV, dK, dQ (flash-attention backward convention)
-        # compiled sweeps (kb1), the asm sweeps (pipe2), + the concatenated-items dK/dV sweep (cat);
-        # SR_BWD_AB=kb adds the compiled 64-keys-per-wave form
-        arms = [("kb1", dict(SR_ATTN_BWD_KB=1, SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0, SR_ATTN_BWD_CAT=0)),
+        # compiled sweeps (kb1), the asm sweeps (pipe2), + the concatenated-items dK/dV sweep (cat)
+        arms = [("kb1", dict(SR_ATTN_BWD_PIPE=0, SR_ATTN_BWD_DQ_PIPE=0, SR_ATTN_BWD_CAT=0)),
                 ("pipe2", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CAT=0)),
                 ("cat", dict(SR_ATTN_BWD_PIPE=1, SR_ATTN_BWD_DQ_PIPE=1, SR_ATTN_BWD_CAT=1))]
-        if os.environ.get("SR_BWD_AB") == "kb":
-            arms.append(("kb2", dict(SR_ATTN_BWD_KB=2, SR_ATTN_BWD_PIPE=0)))
         if os.environ.get("SR_BWD_AB") == "pipe":  # the asm sweeps only (A/B of library builds)
             arms = arms[1:2]
         for arm, sw in arms * 2:
