@@ -160,6 +160,12 @@ typedef struct sr_gemm_epi {
      re-rounding c * bf16(q) (ABI 1.0).  q_cols a multiple of 64. */
   float q_scale;
   int q_cols;
+  /* GELU_BWD (training): per-64-row-block column sums of the bf16 output dH, i.e. the fc1 bias
+     gradient's partials without re-reading dH (ABI 1.4): colsum[(r / 64) * N + c] = sum over the
+     block's rows r < M of bf16(dH[r][c]), written (not accumulated) for every block the call
+     covers; ceil(M / 64) * N floats, 16-B aligned.  NULL = off.  sr_colsum over the ceil(M / 64)
+     rows then gives the full column sum. */
+  float* colsum;
 } sr_gemm_epi;
 
 /* bf16 kernels: 256x256 tiles (one workgroup per CU) for >= 512 such tiles, else 128x128; with

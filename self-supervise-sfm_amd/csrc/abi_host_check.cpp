@@ -55,7 +55,7 @@ void layout() {
                        FIELD(sr_gemm_epi, patch_start), FIELD(sr_gemm_epi, grid_w), FIELD(sr_gemm_epi, seg_rows),
                        FIELD(sr_gemm_epi, seg_stride), FIELD(sr_gemm_epi, seg_offset), FIELD(sr_gemm_epi, row_add),
                        FIELD(sr_gemm_epi, aux), FIELD(sr_gemm_epi, ld_aux), FIELD(sr_gemm_epi, q_scale),
-                       FIELD(sr_gemm_epi, q_cols)));
+                       FIELD(sr_gemm_epi, q_cols), FIELD(sr_gemm_epi, colsum)));
   STRUCT(sr_gemm_problem, (FIELD(sr_gemm_problem, A), FIELD(sr_gemm_problem, lda), FIELD(sr_gemm_problem, W),
                            FIELD(sr_gemm_problem, ldw), FIELD(sr_gemm_problem, out), FIELD(sr_gemm_problem, ldo),
                            FIELD(sr_gemm_problem, M), FIELD(sr_gemm_problem, N), FIELD(sr_gemm_problem, K),

@@ -99,6 +99,39 @@ using AuxT = T;
 constexpr int ROPE_LDS = 8192;
 constexpr int ROPE_LDS_POS = ROPE_LDS / 2 / 64;
 
+// GELU_BWD's column sums: per lane and 64-row block (4 accumulator rows mi), the 16 columns
+// colw + 16 ni + 4 lg + r summed over its rows; the 16 lanes lr of a 16-lane DPP row share those
+// columns, so four DPP adds (quad swaps, half-row and row mirrors) leave the block's sums in every
+// lane and lane lr = 0 stores them: ep.colsum[(row block) * N + col].
+__device__ __forceinline__ float dpp_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+template <int MT>
+__device__ __forceinline__ void colsum_store(const GemmArgs& g, float (&cs)[MT / 4][4][4], int rowbase, int colw,
+                                             int lr, int lg) {
+#pragma unroll
+  for (int i = 0; i < MT / 4; ++i) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[i][ni][r] = dpp_sum16(cs[i][ni][r]);
+    const int rb = rowbase + i * 64;
+    if (lr == 0 && rb < g.M) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = colw + ni * 16 + 4 * lg;
+        if (col < g.N)
+          *(float4*)(g.ep.colsum + (int64_t)(rb >> 6) * g.N + col) =
+              make_float4(cs[i][ni][0], cs[i][ni][1], cs[i][ni][2], cs[i][ni][3]);
+      }
+    }
+  }
+}
+
 template <typename T, int EPI, int MT, typename Emit>
 __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], int rowbase, int colw, int lr,
                                         int lg, Emit&& emit, const char* rope_lds = nullptr) {
@@ -126,7 +159,15 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
   };
 
   if constexpr (EPI == SR_EPI_GELU_BWD) {
-    // dH = acc * gelu'(u), u = the saved fc1 pre-activation (aux, T) of the same element
+    // dH = acc * gelu'(u), u = the saved fc1 pre-activation (aux, T) of the same element; with
+    // ep.colsum also the column sums of the stored (T-rounded) dH per 64-row block (colsum_store)
+    float cs[MT / 4][4][4];
+#pragma unroll
+    for (int i = 0; i < MT / 4; ++i)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[i][ni][r] = 0.f;
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int row = rowbase + mi * 16 + lr;
@@ -146,8 +187,13 @@ __device__ __forceinline__ void produce(const GemmArgs& g, f32x4 (&acc)[MT][4], 
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[mi][ni][r] * sr::gelu_erf_grad<sr::is_bf16<T>::value>(u[r]);
         emit(row, colw + ni * 16 + 4 * lg, v);
+        if (ep.colsum && row < g.M) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[mi >> 2][ni][r] += sr::to_f32(sr::from_f32<T>(v[r]));
+        }
       }
     }
+    if (ep.colsum) colsum_store<MT>(g, cs, rowbase, colw, lr, lg);
   } else if constexpr (EPI == SR_EPI_BIAS || EPI == SR_EPI_BIAS_GELU || EPI == SR_EPI_F32) {
     // the Q block of a plain-bias QKV projection (DINO) leaves scaled by q_scale (wave-uniform:
     // the wave's 64 columns start at colw, q_cols is a multiple of 64)
@@ -1070,6 +1116,7 @@ static GemmArgs row_slice(const GemmArgs& a, int r0, int rows) {
   b.A += (int64_t)r0 * a.lda_b;
   b.out = (char*)a.out + (int64_t)r0 * a.ldo * (int64_t)sizeof(OutT<bf16, EPI>);
   if (a.ep.aux) b.ep.aux = (char*)a.ep.aux + (int64_t)r0 * a.ep.ld_aux * (int64_t)sizeof(AuxT<bf16>);
+  if (a.ep.colsum) b.ep.colsum = a.ep.colsum + (int64_t)(r0 / 64) * a.N;  // r0: whole 256-row tiles
   if (a.ep.pos_yx) b.ep.pos_yx += 2 * (int64_t)r0;
   else if (a.ep.pos_rowmap) b.ep.pos_rowmap += r0;
   else b.ep.pos_row_base += r0;
@@ -1259,6 +1306,8 @@ static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda
   if (epi == SR_EPI_BIAS_RESID) SR_CHECK(ep->gamma, SR_EINVAL, "sr_gemm: RESID needs gamma");
   if (epi == SR_EPI_GELU_BWD) SR_CHECK(ep->aux && ep->ld_aux >= N && (ep->ld_aux * esz) % 8 == 0, SR_EINVAL,
                                        "sr_gemm: GELU_BWD needs aux (the saved pre-activation)");
+  SR_CHECK(!ep->colsum || (epi == SR_EPI_GELU_BWD && ((uintptr_t)ep->colsum % 16) == 0), SR_EINVAL,
+           "sr_gemm: colsum needs the GELU_BWD epilogue and a 16-B aligned buffer");
   if (ep->aux && (epi == SR_EPI_BIAS_GELU || epi == SR_EPI_QKV))
     SR_CHECK(ep->ld_aux >= N && (ep->ld_aux * esz) % 8 == 0 && ((uintptr_t)ep->aux % 8) == 0, SR_EINVAL,
              "sr_gemm: bad aux buffer");

@@ -39,7 +39,7 @@ class GemmEpi(ctypes.Structure):
         ("tokens_per_frame", _i32), ("patch_start", _i32), ("grid_w", _i32),
         ("seg_rows", _i32), ("seg_stride", _i32), ("seg_offset", _i32), ("row_add", _vp),
         ("aux", _vp), ("ld_aux", _i64),
-        ("q_scale", _f32), ("q_cols", _i32),
+        ("q_scale", _f32), ("q_cols", _i32), ("colsum", _vp),
     ]
 
 

@@ -217,10 +217,13 @@ def _fill_qkv_epi(ep: GemmEpi, qkv: dict) -> None:
 def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] = None,
          gamma: Optional[Tensor] = None, rows: Optional[int] = None, qkv: Optional[dict] = None,
          patch: Optional[dict] = None, tag: Optional[str] = None, splits: Optional[int] = None,
-         aux: Optional[Tensor] = None, q_scale: float = 0.0, q_cols: int = 0) -> None:
+         aux: Optional[Tensor] = None, q_scale: float = 0.0, q_cols: int = 0,
+         colsum: Optional[Tensor] = None) -> None:
     """out = epilogue(a[M,K] . w[N,K]^T).  ``rows`` overrides M (PATCH: out has more rows).
     ``splits`` K slices (sr_gemm_splitk); default: automatic for few rows.  ``aux`` (a's dtype,
     [M, N] view): BIAS_GELU / QKV store the pre-activation there; GELU_BWD reads it.
+    ``colsum`` (GELU_BWD; fp32, contiguous, >= colsum_blocks(M) * N): the output's column sums per
+    64-row block (sr_gemm_epi.colsum), so colsum(colsum_view) gives the bias gradient.
     ``q_scale`` / ``q_cols`` (BIAS / QKV): output columns [0, q_cols) leave multiplied by q_scale
     before their one rounding (sr_gemm_epi.q_scale; a QKV dict's "q_scale" key sets both)."""
     lda = _rowmajor(a, "a")
@@ -243,6 +246,10 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         if aux.dtype != a.dtype:
             raise TypeError("gemm: aux must have the operand dtype")
         ep.aux, ep.ld_aux = _p(aux), _rowmajor(aux, "aux")
+    if colsum is not None:
+        _check_colsum(colsum, M, N)
+        ep.colsum = _p(colsum)
+        splits = 1
     if patch is not None:
         ep.seg_rows = patch["seg_rows"]
         ep.seg_stride = patch["seg_stride"]
@@ -269,6 +276,16 @@ def gemm(a: Tensor, w: Tensor, out: Tensor, epi: int, *, bias: Optional[Tensor] 
         es, eo = a.element_size(), out.element_size()
         nb = (M * K + N * K) * es + M * N * eo * (2 if epi == _lib.SR_EPI_BIAS_RESID else 1)
         TIMER.stop(tag, ev0, 2.0 * M * N * K, nb, kernel=last_kernel())
+
+
+def colsum_blocks(M: int) -> int:
+    """Rows of a GELU_BWD colsum buffer (sr_gemm_epi.colsum): one per 64 output rows."""
+    return (M + 63) // 64
+
+
+def _check_colsum(t: Tensor, M: int, N: int) -> None:
+    if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < colsum_blocks(M) * N or t.data_ptr() % 16:
+        raise ValueError(f"gemm: colsum must be a contiguous 16-B aligned fp32 buffer of >= {colsum_blocks(M) * N}")
 
 
 GEMM_GROUP_MAX = 4
@@ -309,6 +326,9 @@ def gemm_group(problems, epi: int, tag: Optional[str] = None) -> None:
             if aux.dtype != a.dtype:
                 raise TypeError("gemm_group: aux must have the operand dtype")
             q.ep.aux, q.ep.ld_aux = _p(aux), _rowmajor(aux, "aux")
+        if p.get("colsum") is not None:  # GELU_BWD's per-64-row-block column sums
+            _check_colsum(p["colsum"], a.shape[0], N)
+            q.ep.colsum = _p(p["colsum"])
         flops += 2.0 * a.shape[0] * N * K
         nbytes += (a.shape[0] * K + N * K) * a.element_size() + a.shape[0] * N * out.element_size()
     if tag == "gemm":

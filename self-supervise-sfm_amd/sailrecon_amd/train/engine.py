@@ -282,13 +282,17 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
 
     # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
     dU = sc.get("dU", R, Hd, dt, dev)
-    ops.gemm(a_op, bp.wt_fc2, dU, _lib.SR_EPI_GELU_BWD, aux=tape.u, tag=tag + ".dgrad")
+    # bf16: fc1's bias grad from the GELU_BWD epilogue's per-64-row column sums (no re-read of dU)
+    csU = sc.get("dU_colsum", ops.colsum_blocks(R), Hd, torch.float32, dev) if bf and g.b_fc1 is not None else None
+    ops.gemm(a_op, bp.wt_fc2, dU, _lib.SR_EPI_GELU_BWD, aux=tape.u, colsum=csU, tag=tag + ".dgrad")
     wgrad(a_op, tape.h, g.w_fc2, rowscale=pb.g2, wdot=bp.w_fc2 if g.g2 is not None else None,
           rowdot=g.g2 if g.g2 is not None else None)
     _resid_param_grads(dx, bp.b_fc2, pb.g2, g.b_fc2, g.g2, tmp[:C])
     dxn = sc.get("dxn", R, C, torch.float32, dev)
     ops.gemm(dU, bp.wt_fc1, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
-    wgrad(dU, tape.xn2, g.w_fc1, db=g.b_fc1)
+    wgrad(dU, tape.xn2, g.w_fc1, db=None if csU is not None else g.b_fc1)
+    if csU is not None:
+        ops.colsum(csU, g.b_fc1, accumulate=True)
     # (LN2's backward also sums the updated dx over the rows: proj's bias / gamma grads below)
     fused_sum = g.ln2_w is not None and C <= 2048 and _resid_wants_sum(bp.b_proj, g.b_proj, g.g1)
     ops.layernorm_bwd(tape.x1, dxn, pb.ln2_w, pb.eps, dx, dxb=dxb, dw=g.ln2_w, db=g.ln2_b,
@@ -341,7 +345,7 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
             ops.gemm_group(probs, epi, tag=tag + ".dgrad")
         else:
             for q in probs:
-                ops.gemm(q["a"], q["w"], q["out"], epi, aux=q.get("aux"), tag=tag + ".dgrad")
+                ops.gemm(q["a"], q["w"], q["out"], epi, aux=q.get("aux"), colsum=q.get("colsum"), tag=tag + ".dgrad")
 
     def wgrad(it, dy, x, dw, db=None, rowscale=None, wdot=None, rowdot=None):
         ops.gemm_wgrad(dy, x, dw, accumulate=True, rowscale=rowscale, wdot=wdot, rowdot=rowdot,
@@ -369,17 +373,23 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         R = it["dx"].shape[0]
         it["_tmp"] = it["sc"].get("colsum_tmp", 1, max(C, Hd, 3 * C), torch.float32, dev)[0]
         it["_dU"] = it["sc"].get("dU", R, Hd, dt, dev)
+        it["_csU"] = (it["sc"].get("dU_colsum", ops.colsum_blocks(R), Hd, torch.float32, dev)
+                      if it["g"].b_fc1 is not None else None)
         it["_dxn"] = it["sc"].get("dxn", R, C, torch.float32, dev)
         it["_dO"] = it["sc"].get("dO", R, C, dt, dev)
     # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
-    dgrad(_lib.SR_EPI_GELU_BWD, [dict(a=it["dxb"], w=it["bp"].wt_fc2, out=it["_dU"], aux=it["tape"].u) for it in items])
+    dgrad(_lib.SR_EPI_GELU_BWD, [dict(a=it["dxb"], w=it["bp"].wt_fc2, out=it["_dU"], aux=it["tape"].u,
+                                      colsum=it["_csU"]) for it in items])
     wgrads([(it, it["dxb"], it["tape"].h, it["g"].w_fc2, None, it["pb"].g2,
              it["bp"].w_fc2 if it["g"].g2 is not None else None, it["g"].g2) for it in items])
     for it in items:
         pb, bp, g = it["pb"], it["bp"], it["g"]
         _resid_param_grads(it["dx"], bp.b_fc2, pb.g2, g.b_fc2, g.g2, it["_tmp"][:C])
     dgrad(_lib.SR_EPI_F32, [dict(a=it["_dU"], w=it["bp"].wt_fc1, out=it["_dxn"]) for it in items])
-    wgrads([(it, it["_dU"], it["tape"].xn2, it["g"].w_fc1, it["g"].b_fc1, None, None, None) for it in items])
+    wgrads([(it, it["_dU"], it["tape"].xn2, it["g"].w_fc1, None, None, None, None) for it in items])
+    for it in items:  # fc1's bias grads from the GELU_BWD epilogue's column sums
+        if it["_csU"] is not None:
+            ops.colsum(it["_csU"], it["g"].b_fc1, accumulate=True)
     for it in items:
         pb, bp, g = it["pb"], it["bp"], it["g"]
         it["_fused"] = g.ln2_w is not None and C <= 2048 and _resid_wants_sum(bp.b_proj, g.b_proj, g.g1)

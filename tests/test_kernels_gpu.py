@@ -702,3 +702,41 @@ def test_merge_with_empty_partial(ops):
         assert torch.isfinite(t.float()).all()
         assert rel(t.float(), o_ref.float()) < 1e-2
     assert torch.equal(out, o_ref) and torch.equal(lse_out, lse_ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(43968, 4096, 1024), (43 * 256 - 100, 3072, 1024), (300, 256, 128)])
+def test_gemm_gelu_bwd_colsum(ops, M, N, K):
+    """sr_gemm_epi.colsum (ABI 1.4): the GELU_BWD epilogue's per-64-row-block column sums of its bf16
+    output dH -- the 256x256 kernel with and without the tail split, the 128x128 kernel and a grouped
+    launch -- equal the column sums of the stored dH to fp32 summation order, and the output itself
+    is unchanged."""
+    L = _lib()
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) / 32).bfloat16()
+    u = torch.randn(M, N, device=DEV, generator=g).bfloat16()
+    nb = ops.colsum_blocks(M)
+    ref_out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(a, w, ref_out, L.SR_EPI_GELU_BWD, aux=u)
+    torch.cuda.synchronize()
+    ref = ref_out.float().sum(0)
+    runs = []
+    for tail in (0, 1):
+        out = torch.empty_like(ref_out)
+        cs = torch.full((nb, N), float("nan"), device=DEV)
+        with ops.tuning(SR_GEMM_TAIL=tail):
+            ops.gemm(a, w, out, L.SR_EPI_GELU_BWD, aux=u, colsum=cs)
+        runs.append((out, cs))
+    if N % 256 == 0:
+        out = torch.empty_like(ref_out)
+        cs = torch.full((nb, N), float("nan"), device=DEV)
+        h = (M // 2) // 64 * 64
+        ops.gemm_group([dict(a=a[:h], w=w, out=out[:h], aux=u[:h], colsum=cs[:h // 64]),
+                        dict(a=a[h:], w=w, out=out[h:], aux=u[h:], colsum=cs[h // 64:])], L.SR_EPI_GELU_BWD)
+        runs.append((out, cs))
+    torch.cuda.synchronize()
+    for out, cs in runs:
+        assert torch.equal(out, ref_out)
+        assert torch.isfinite(cs).all()
+        assert rel(cs.sum(0), ref) < 1e-5
+        assert rel(cs[-1], ref_out[(nb - 1) * 64:].float().sum(0)) < 1e-5  # the last, ragged block
