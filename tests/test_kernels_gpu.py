@@ -134,8 +134,10 @@ def test_gemm_resid_lds_epilogue(ops, M, K):
         with ops.tuning(SR_GEMM_RESID_LDS=rl):  # no bias
             ops.gemm(a, w, x, L.SR_EPI_BIAS_RESID, gamma=gam, splits=1)
         outs.append(x)
+    # outs: [register epilogue: one kernel, tail split, grouped, no bias] then the same with RESID_LDS
     for i in (1, 2, 4, 5, 6):
-        assert torch.equal(outs[i], outs[0 if i != 6 else 3]), i
+        assert torch.equal(outs[i], outs[0]), i
+    assert torch.equal(outs[7], outs[3])
     ref = (a.float() @ w.float().t() + b) * gam
     assert rel(outs[0] - x0, ref) < 1e-5
     assert rel(outs[3] - x0, (a.float() @ w.float().t()) * gam) < 1e-5
