@@ -91,9 +91,7 @@ enum sr_tuning_key {  /* renumbered in ABI 1.3: switches that measured level or 
   SR_TUNE_ATTN_BWD_CAT = 18,/* 1: keys shared by a batch > 1 whose items' queries are consecutive rows:
                                the dK/dV asm sweep over the concatenated queries (one sequence of
                                batch * lq rows; same sum, other tile grouping)          default 1 */
-  SR_TUNE_GEMM_STAGGER = 19,/* n > 0: the 256x256 GEMMs' first-round workgroups on every other CU of an XCD
-                               start n x 8,128 cycles late (epilogues of the two halves apart) default 0 */
-  SR_TUNE_COUNT = 20
+  SR_TUNE_COUNT = 19
 };
 /* Sets a switch; returns its previous value (SR_EINVAL for an unknown key). */
 int sr_set_tuning(int key, int value);

@@ -22,7 +22,7 @@ constexpr TuneDef kTune[SR_TUNE_COUNT] = {
     {"SR_ATTN_NO_SHORT", 0}, {"SR_GEMM_GROUP_M", -1}, {"SR_GEMM_SMALLM", 1}, {"SR_GEMM_NO256", 0},
     {"SR_GEMM_REG_EPI", 0}, {"SR_CONV_NO_NARROW", 0}, {"SR_WGRAD256", 1}, {"SR_SYNC_CHECK", 0},
     {"SR_RLN_WIDE", 0}, {"SR_GEMM_TAIL", 1}, {"SR_GEMM_RESID_LDS", 1}, {"SR_GEMM_ROPE_LDS", 1},
-    {"SR_ATTN_BWD_PIPE", 1}, {"SR_ATTN_BWD_DQ_PIPE", 1}, {"SR_ATTN_BWD_CAT", 1}, {"SR_GEMM_STAGGER", 0},
+    {"SR_ATTN_BWD_PIPE", 1}, {"SR_ATTN_BWD_DQ_PIPE", 1}, {"SR_ATTN_BWD_CAT", 1},
 };
 std::atomic<int> g_tune[SR_TUNE_COUNT];
 std::once_flag g_tune_once;

@@ -47,8 +47,6 @@ struct GemmArgs {
   int group_m;       // 256x256 kernels: tile order in groups of group_m row tiles (<= 1: row-major)
   int resid_lds;     // 256x256 RESID: the x tile staged through LDS by LDS-DMA (SR_TUNE_GEMM_RESID_LDS)
   int rope_lds;      // 256x256 QKV: RoPE tables staged in LDS (SR_TUNE_GEMM_ROPE_LDS)
-  int stagger;       // 256x256: first-round workgroups of odd CUs per XCD sleep stagger x 8,128 cycles
-  int first_round;   //   (SR_TUNE_GEMM_STAGGER), so that half the CUs' epilogues overlap the others' k-loops
   sr_gemm_epi ep;
   // implicit-GEMM 3x3 / pad-1 conv (gemm_kernel<float, EPI, true>): A row m = output pixel
   // (n, yo, xo) of the NHWC fp32 input x [n][H][W][C], A column k = (ky, kx, ci) — exactly
@@ -1024,17 +1022,9 @@ template <int EPI> constexpr int smem256() {
   return 2 * STAGE_BIG + (EPI == SR_EPI_QKV ? ROPE_LDS : EPI == SR_EPI_BIAS_RESID ? RESID_GB : 0);
 }
 
-// SR_TUNE_GEMM_STAGGER: the first round's workgroups on every other CU of an XCD (blockIdx / 8 odd) start
-// late, so that later rounds keep the two halves' epilogues (the RESID read-modify-write of x) apart
-__device__ __forceinline__ void stagger_start(const GemmArgs& g, int bid) {
-  if (g.stagger > 0 && bid < g.first_round && ((bid >> 3) & 1))
-    for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-}
-
 template <int EPI, bool RLDS>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[smem256<EPI>()];
-  stagger_start(g, blockIdx.x);
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
   const char* rope = stage_rope<EPI>(g, smem);
   gemm256_tile<EPI, RLDS>(g, smem, sr::xcd_remap(blockIdx.x, nt), 0, g.ktiles, rope);
@@ -1062,7 +1052,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_group_kernel(GemmGroup gg) {
   const int nt = (g.N / BIG) * ((g.M + BIG - 1) / BIG);
   const int lin = blockIdx.x - gg.start[p];
   if (lin >= nt) return;  // padding
-  stagger_start(g, blockIdx.x);
   const char* rope = stage_rope<EPI>(g, smem);
   gemm256_tile<EPI, RLDS>(g, smem, sr::xcd_remap(lin, nt), 0, g.ktiles, rope);
 }
@@ -1361,8 +1350,6 @@ static int gemm_args(GemmArgs& a, int dtype, int epi, const void* A, int64_t lda
                 ((uintptr_t)out % 16) == 0 && ldo % 4 == 0 && ((uintptr_t)ep->gamma % 16) == 0 &&
                 ((uintptr_t)ep->bias % 16) == 0;
   a.rope_lds = sr::tune(SR_TUNE_GEMM_ROPE_LDS) != 0;
-  a.stagger = dtype == SR_BF16 ? sr::tune(SR_TUNE_GEMM_STAGGER) : 0;
-  a.first_round = sr::cu_count();
   return SR_OK;
 }
 

@@ -413,25 +413,6 @@ def gemm_resid():
             print(f"gemm_resid {name} resid_lds={rl} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
 
 
-def gemm_stagger():
-    """SR_GEMM_STAGGER A/B, interleaved: the four aggregator GEMMs at C3 frame rows with the first
-    round's odd CUs started 0 / 1 / 2 / 3 / 4 x 8,128 cycles late."""
-    M = 2 * 32 * 1374
-    x = torch.randn(M, 1024, device=DEV)
-    for name, (N, K, epi) in {"qkv ": (3072, 1024, _lib.SR_EPI_BIAS), "proj": (1024, 1024, _lib.SR_EPI_BIAS_RESID),
-                              "fc1 ": (4096, 1024, _lib.SR_EPI_BIAS_GELU),
-                              "fc2 ": (1024, 4096, _lib.SR_EPI_BIAS_RESID)}.items():
-        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-        w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
-        b, gam = torch.randn(N, device=DEV), torch.randn(N, device=DEV) * 1e-3
-        out = x if epi == _lib.SR_EPI_BIAS_RESID else torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        fl = 2.0 * M * N * K
-        for st in (0, 1, 2, 3, 4, 0, 1, 2, 3, 4):
-            with ops.tuning(SR_GEMM_STAGGER=st):
-                ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b, gamma=gam), reps=10)
-            print(f"gemm_stagger {name} stagger={st} {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s", flush=True)
-
-
 def gemm_k():
     """Per-tile fixed cost of the 256x256 GEMM: exactly 5 rounds of 256 tiles (M = 81,920, N = 1024)
     at K = 256 ... 4096; time = fixed + K * per-k, the intercept is the prologue / epilogue / tile
