@@ -142,6 +142,9 @@ for step in "$@"; do
             done ;;
     gemm_tests2) run gemm_tests2 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "gemm" --timeout 300 --timeout-method thread ;;
     kresid)  run kresid 300 python tools/kbench.py gemm_resid gemm ;;
+    train_tests) run train_tests 1100 python -u -m pytest tests/test_train_graph_gpu.py tests/test_train_kernels_gpu.py \
+               tests/test_train_block_gpu.py tests/test_attn_bwd_gpu.py tests/test_c4_golden_gpu.py tests/test_train_step_gpu.py \
+               -x -q -m gpu --timeout 900 --timeout-method thread ;;
     resid_ab) for i in 1 2; do
                 run bench_rl0_$i 400 env SR_GEMM_RESID_LDS=0 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
                 run bench_rl1_$i 400 env SR_GEMM_RESID_LDS=1 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
