@@ -508,6 +508,11 @@ int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx,
 int sr_qk_bwd(sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds, void* out,
               int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace);
 
+/* ep->colsum (ABI 1.4, optional): also colsum[c] += sum over the rows of out[r][c] (the qkv bias
+ * gradient, summed from the values as stored, in a fixed order), ncols <= 3072; the workspace then
+ * holds >= sr_qk_bwd_workspace_floats(rows, ncols) floats. */
+int64_t sr_qk_bwd_workspace_floats(int rows, int ncols);
+
 /* sr_qk_bwd for fp32 blocks (autocast off: the reference's fp32 Attention with qk_norm / RoPE):
  * raw and out fp32, otherwise identical.  out may alias dsrc (same ld). */
 int sr_qk_bwd_f32(sr_stream_t stream, const float* raw, int64_t ldr, const float* dsrc, int64_t lds, float* out,

@@ -286,6 +286,7 @@ void check() {
   expect("sr_quant_fp8_vt null", sr_quant_fp8_vt(nullptr, nullptr, 8, 8, 1, nullptr, nullptr, nullptr), false);
   expect("sr_attention_bwd null", sr_attention_bwd(nullptr, nullptr), false);
   expect("sr_attention_bwd_f32 null", sr_attention_bwd_f32(nullptr, nullptr), false);
+  if (sr_qk_bwd_workspace_floats(43968, 3072) < 1024LL * 3072 || sr_qk_bwd_workspace_floats(0, 3072) != 0) ++g_fail;
   expect("sr_gemm_wgrad null", sr_gemm_wgrad(nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, 0, 0, 0, nullptr, nullptr, 0, nullptr, 0, nullptr), false);
   expect("sr_colsum null", sr_colsum(nullptr, SR_F32, nullptr, 0, 0, 0, nullptr, 0, 1.f, nullptr, 0), false);
   {  // ABI 1.0: the workspace size is checked against sr_colsum_workspace_floats

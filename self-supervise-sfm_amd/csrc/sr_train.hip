@@ -547,10 +547,17 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // One wave per row; 4 heads per pass (16 lanes x 4 values per head: dims 4 li .. 4 li + 3).
 // RoPE pairs (d, d + 16) of each half sit in lanes li and li ^ 4.
 // T = bf16 (autocast blocks) or float (fp32 blocks): the type of raw and out.
+// ep.colsum: every wave also adds the values it stores into its own LDS row [wave][col] (a lane owns
+// its columns: plain read-add-write, no atomics), then the workgroup's 4 rows sum into one partial
+// row [blockIdx.x][ncols] of cpart; the host sums those rows into ep.colsum (a fixed order).
+constexpr int QKB_PASSES = 3;  // ncols <= 3072 with ep.colsum
+constexpr int ep_colsum_lds_floats() { return 4 * QKB_PASSES * 1024; }  // 48 KiB
 template <typename T>
 __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, int64_t ldr,
                                                      const float* __restrict__ dsrc, int64_t lds, T* out,
-                                                     int64_t ldo, int rows, int ncols, sr_gemm_epi ep, float* part) {
+                                                     int64_t ldo, int rows, int ncols, sr_gemm_epi ep, float* part,
+                                                     float* cpart) {
+  extern __shared__ float csl[];  // ep_colsum_lds_floats() when ep.colsum (dynamic: no LDS otherwise)
   constexpr bool BF = sr::is_bf16<T>::value;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
@@ -573,6 +580,10 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
   }
   (void)bq;
   (void)bk;
+  const bool want_cs = ep.colsum != nullptr;  // uniform
+  float* const csw = csl + (threadIdx.x >> 6) * (QKB_PASSES * 1024);  // this wave's LDS row
+  if (want_cs)
+    for (int c = 4 * lane; c < ncols; c += 256) *(float4*)(csw + c) = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int row = gw; row < rows; row += nw) {
     float cs[4] = {1.f, 1.f, 1.f, 1.f}, sn[4] = {0.f, 0.f, 0.f, 0.f};
     if (rope) {
@@ -673,6 +684,14 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
           *(bf16x4*)(out + (int64_t)row * ldo + col) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
         else
           *(f32x4*)(out + (int64_t)row * ldo + col) = f32x4{d[0], d[1], d[2], d[3]};
+        if (want_cs) {
+          float4 t = *(float4*)(csw + col);
+          t.x += sr::to_f32(sr::from_f32<T>(d[0]));
+          t.y += sr::to_f32(sr::from_f32<T>(d[1]));
+          t.z += sr::to_f32(sr::from_f32<T>(d[2]));
+          t.w += sr::to_f32(sr::from_f32<T>(d[3]));
+          *(float4*)(csw + col) = t;
+        }
       }
       }
       }
@@ -692,6 +711,13 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int e = 0; e < 4; ++e) pw[t * 64 + 4 * li + e] = acc[t][e];
+    }
+  }
+  if (want_cs) {  // the workgroup's 4 LDS rows -> its partial row (fixed order)
+    __syncthreads();
+    for (int c = threadIdx.x; c < ncols; c += 256) {
+      const int s = QKB_PASSES * 1024;
+      cpart[(int64_t)blockIdx.x * ncols + c] = (csl[c] + csl[s + c]) + (csl[2 * s + c] + csl[3 * s + c]);
     }
   }
 }
@@ -1155,6 +1181,16 @@ extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, i
   return sr::check_launch("sr_layernorm_bwd");
 }
 
+static int qk_bwd_wgs(int rows) { return std::min(1024, (rows + 3) / 4); }
+
+extern "C" int64_t sr_qk_bwd_workspace_floats(int rows, int ncols) {
+  if (rows <= 0 || ncols <= 0 || ncols % 4) return 0;
+  const int wgs = qk_bwd_wgs(rows);
+  int rpc;
+  const int64_t norm = (int64_t)wgs * 4 * 256 + (int64_t)colsum_chunks(wgs * 4, 256, rpc) * 256;
+  return norm + (int64_t)wgs * ncols + (int64_t)colsum_chunks(wgs, ncols, rpc) * ncols;
+}
+
 template <typename T>
 static int qk_bwd(const char* who, sr_stream_t stream, const void* raw, int64_t ldr, const float* dsrc, int64_t lds,
                   void* out, int64_t ldo, int rows, int ncols, const sr_gemm_epi* ep, float* grads, float* workspace) {
@@ -1166,14 +1202,24 @@ static int qk_bwd(const char* who, sr_stream_t stream, const void* raw, int64_t 
            "%s: qk-norm needs raw, the four norm params, grads and workspace", who);
   SR_CHECK(!ep->rope_cos || (ep->rope_sin && (ep->pos_yx || (ep->tokens_per_frame > ep->patch_start && ep->grid_w > 0))),
            SR_EINVAL, "%s: rope params", who);
+  SR_CHECK(!ep->colsum || (ncols <= QKB_PASSES * 1024 && workspace && ((uintptr_t)ep->colsum % 16) == 0),
+           SR_EINVAL, "%s: colsum needs ncols <= %d, a workspace and a 16-B aligned output", who, QKB_PASSES * 1024);
   hipStream_t s = (hipStream_t)stream;
-  const int wgs = std::min(1024, (rows + 3) / 4);
-  hipLaunchKernelGGL(qk_bwd_kernel<T>, dim3(wgs), dim3(256), 0, s, (const T*)raw, ldr, dsrc, lds, (T*)out, ldo,
-                     rows, ncols, *ep, workspace);
+  const int wgs = qk_bwd_wgs(rows);
+  int rpc;
+  // workspace: norm partials [wgs*4][256] | their colsum scratch | colsum partials [wgs][ncols] | scratch
+  float* cpart = workspace ? workspace + (int64_t)wgs * 4 * 256 + (int64_t)colsum_chunks(wgs * 4, 256, rpc) * 256
+                           : nullptr;
+  hipLaunchKernelGGL(qk_bwd_kernel<T>, dim3(wgs), dim3(256), ep->colsum ? ep_colsum_lds_floats() * 4 : 0, s,
+                     (const T*)raw, ldr, dsrc, lds, (T*)out, ldo, rows, ncols, *ep, workspace, cpart);
   sr::note_kernel("qk_bwd_kernel<%s>", sr::is_bf16<T>::value ? "__bf16" : "float");
   if (norm) {  // [wgs*4][4][64] -> grads[4][64]
     const int rc = colsum_launch(s, SR_F32, workspace, 256, wgs * 4, 256, grads, 1, 1.f,
                                  workspace + (int64_t)wgs * 4 * 256);
+    if (rc) return rc;
+  }
+  if (ep->colsum) {  // [wgs][ncols] -> colsum[ncols] (accumulated)
+    const int rc = colsum_launch(s, SR_F32, cpart, ncols, wgs, ncols, ep->colsum, 1, 1.f, cpart + (int64_t)wgs * ncols);
     if (rc) return rc;
   }
   return sr::check_launch(who);

@@ -184,6 +184,7 @@ _PROTOS = {
     "sr_qk_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
     "sr_attention_key_box": (_i32, [_vp, _vp, _i64, _i32, _i64, _i32, _i32, _vp, _vp, _vp]),
     "sr_attention_key_box_scratch": (_i32, [_i32, _i32, _i32]),
+    "sr_qk_bwd_workspace_floats": (_i64, [_i32, _i32]),
     "sr_qk_bwd_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
     "sr_cast_bf16": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _f32]),
     "sr_weight_refresh_bf16": (_i32, [_vp, _i32, _vp]),

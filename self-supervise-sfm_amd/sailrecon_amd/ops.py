@@ -1210,16 +1210,22 @@ def layernorm_bwd(x: Tensor, dy: Tensor, w: Optional[Tensor], eps: float, dx: Te
 
 
 def qk_bwd(raw: Optional[Tensor], dsrc: Tensor, out: Tensor, qkv: dict, *, grads: Optional[Tensor] = None,
-           ncols: Optional[int] = None) -> None:
+           ncols: Optional[int] = None, bias_grad: Optional[Tensor] = None) -> None:
     """d(pre-norm q|k|v) (out: bf16, or fp32 for fp32 blocks with raw fp32) from fp32 d(q|k|v)
-    through RoPE^T and the qk-norm backward; grads fp32 [4, 64] += (dqn_w, dqn_b, dkn_w, dkn_b)."""
+    through RoPE^T and the qk-norm backward; grads fp32 [4, 64] += (dqn_w, dqn_b, dkn_w, dkn_b).
+    ``bias_grad`` (fp32 [ncols]): += the column sums of out (the qkv bias gradient) from the same
+    pass (sr_gemm_epi.colsum of sr_qk_bwd), no re-read of out."""
     ep = GemmEpi()
     _fill_qkv_epi(ep, qkv)
     rows = dsrc.shape[0]
     nc = out.shape[1] if ncols is None else ncols
     if raw is not None and raw.dtype != out.dtype:
         raise TypeError("qk_bwd: raw and out must share a dtype")
-    ws = _train_ws(dsrc.device, "qkbwd", 4352 * 256)
+    if bias_grad is not None:
+        if bias_grad.dtype != torch.float32 or not bias_grad.is_contiguous() or bias_grad.numel() < nc:
+            raise ValueError("qk_bwd: bias_grad must be contiguous fp32 [ncols]")
+        ep.colsum = _p(bias_grad)
+    ws = _train_ws(dsrc.device, "qkbwd", max(4352 * 256, int(_lib.load().sr_qk_bwd_workspace_floats(rows, nc))))
     fn = "sr_qk_bwd_f32" if out.dtype == torch.float32 else "sr_qk_bwd"
     rc = getattr(_lib.load(), fn)(_stream(dsrc), _p(raw), 0 if raw is None else _rowmajor(raw, "raw"), _p(dsrc),
                                   _rowmajor(dsrc, "dsrc"), _p(out), _rowmajor(out, "out"), rows, nc, ctypes.byref(ep),

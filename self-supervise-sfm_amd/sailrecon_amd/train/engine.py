@@ -306,17 +306,17 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
     _resid_param_grads(dx, bp.b_proj, pb.g1, g.b_proj, g.g1, tmp[:C], summed=fused_sum)
     dqkv = sc.get("dqkv", R, 3 * C, torch.float32, dev)
     attend_bwd(tape, dO, dqkv)
-    if bf:
+    if bf:  # (+ the qkv bias grad from the same pass: no bf16 column sum of draw afterwards)
         draw = sc.get("draw", R, 3 * C, dt, dev)
         ops.qk_bwd(tape.raw if qkv_epi is not None else None, dqkv, draw, qkv_epi or dict(embed_dim=C, head_dim=64),
-                   grads=g.qkn)
+                   grads=g.qkn, bias_grad=g.b_qkv)
     elif qkv_epi is not None:  # fp32 block (autocast off) with qk-norm / RoPE: in place on dqkv
         ops.qk_bwd(tape.raw, dqkv, dqkv, qkv_epi, grads=g.qkn)
         draw = dqkv
     else:
         draw = dqkv
     ops.gemm(draw, bp.wt_qkv, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
-    wgrad(draw, tape.xn1, g.w_qkv, db=g.b_qkv)
+    wgrad(draw, tape.xn1, g.w_qkv, db=None if bf else g.b_qkv)
     ops.layernorm_bwd(tape.x0, dxn, pb.ln1_w, pb.eps, dx, dxb=dxb, dw=g.ln1_w, db=g.ln1_b)
 
 
@@ -409,9 +409,9 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         it["_draw"] = it["sc"].get("draw", R, 3 * C, dt, dev)
         qkv_epi = it["qkv_epi"]
         ops.qk_bwd(it["tape"].raw if qkv_epi is not None else None, dqkv, it["_draw"],
-                   qkv_epi or dict(embed_dim=C, head_dim=64), grads=it["g"].qkn)
+                   qkv_epi or dict(embed_dim=C, head_dim=64), grads=it["g"].qkn, bias_grad=it["g"].b_qkv)
     dgrad(_lib.SR_EPI_F32, [dict(a=it["_draw"], w=it["bp"].wt_qkv, out=it["_dxn"]) for it in items])
-    wgrads([(it, it["_draw"], it["tape"].xn1, it["g"].w_qkv, it["g"].b_qkv, None, None, None) for it in items])
+    wgrads([(it, it["_draw"], it["tape"].xn1, it["g"].w_qkv, None, None, None, None) for it in items])
     for it in items:
         pb, g = it["pb"], it["g"]
         ops.layernorm_bwd(it["tape"].x0, it["_dxn"], pb.ln1_w, pb.eps, it["dx"], dxb=it["dxb"], dw=g.ln1_w,

@@ -262,8 +262,11 @@ def test_qk_bwd(ops, C, frames, col_offset):
     d_d = dout[:, lo:].to(DEV).contiguous()
     out = torch.empty(M, 3 * C - lo, device=DEV, dtype=torch.bfloat16)
     grads = torch.zeros(4, D, device=DEV)
-    ops.qk_bwd(raw_d, d_d, out, epi, grads=grads)
+    bg0 = torch.randn(3 * C - lo, device=DEV)  # the qkv bias grad, accumulated into
+    bg = bg0.clone()
+    ops.qk_bwd(raw_d, d_d, out, epi, grads=grads, bias_grad=bg)
     assert rel(out.float().cpu(), raw.grad[:, lo:]) < 8e-3
+    assert rel(bg - bg0, out.float().sum(0)) < 1e-5  # column sums of the stored bf16 values
     gref = torch.stack([nrm[0].grad, nrm[1].grad, nrm[2].grad, nrm[3].grad])
     if col_offset:
         assert rel(grads[2:].cpu(), gref[2:]) < 1e-5
@@ -276,8 +279,10 @@ def test_qk_bwd_plain_cast(ops):
     M, C = 500, 384
     d = torch.randn(M, 3 * C, device=DEV)
     out = torch.empty(M, 3 * C, device=DEV, dtype=torch.bfloat16)
-    ops.qk_bwd(None, d, out, dict(embed_dim=C, head_dim=64))
+    bg = torch.zeros(3 * C, device=DEV)
+    ops.qk_bwd(None, d, out, dict(embed_dim=C, head_dim=64), bias_grad=bg)
     assert torch.equal(out, d.bfloat16())
+    assert rel(bg, out.float().sum(0)) < 1e-5
 
 
 def test_cast_nonfinite_adam(ops):
