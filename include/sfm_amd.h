@@ -77,8 +77,9 @@ enum sr_tuning_key {  /* renumbered in ABI 1.3: switches that measured level or 
   SR_TUNE_RLN_WIDE = 12,    /* sr_residual_layernorm variant bits: 1 16-B lanes, 2 two rows per wave, 4 nt x stores (0) */
   SR_TUNE_GEMM_TAIL = 13,   /* 1: a 256x256 GEMM whose last workgroup round would run few tiles computes
                                the rows past its last whole round on the 128x128 kernel (second launch)  (1) */
-  SR_TUNE_GEMM_RESID_LDS = 14,/* 1: the 256x256 RESID GEMM's epilogue stages the x tile through LDS by
-                               LDS-DMA (64-row quarters, two in flight; whole-row stores)  default 1 */
+  SR_TUNE_GEMM_RESID_LDS = 14,/* 1: the 256x256 RESID GEMM's epilogue stages rows 0-127 of the x tile
+                               through LDS by LDS-DMA (two 64-row halves in flight; whole-row
+                               stores) while waves 4-7 update rows 128-255 in registers  default 1 */
   SR_TUNE_GEMM_ROPE_LDS = 15,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
                                under the first k-tile; 0: from global memory)           default 1 */
   SR_TUNE_ATTN_BWD_PIPE = 16,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
@@ -343,6 +344,19 @@ int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* d);
  * Replaces the two F.scaled_dot_product_attention calls of one layer's global and global_reloc
  * blocks (attention.py:103-109; aggregator.py:672-769). */
 int sr_attention_pair(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1);
+
+/* sr_attention_pair with each problem's V given ALSO as pre-transposed tiles (ABI 1.5): vt0 / vt1 from
+ * sr_vt_tiles over the desc's v0 (L = l0), 16-B aligned.  The sweep then stages V^T and reads each
+ * P.V operand fragment with one ds_read_b128 instead of two transposing reads.  Bit-identical to
+ * sr_attention_pair (same products in the same order); v0 is still required and validated. */
+int sr_attention_pair_vt(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1,
+                         const void* vt0, const void* vt1);
+
+/* V bf16 [L][ldv] (heads * 64 columns used) -> V^T tiles [heads][ceil(L/64)][64 d][64 key slots] bf16
+ * (ABI 1.5): slot 32kb + 16s2 + 8h + j of a tile holds key 32kb + 16s2 + 8(j >> 2) + 4h + (j & 3) --
+ * the bf16 P fragment's k order -- and keys past L are zero.  dst: heads * ceil(L/64) * 8192 bytes.
+ * ldv a multiple of 8, v / dst 16-B aligned. */
+int sr_vt_tiles(sr_stream_t stream, const void* v, int64_t ldv, int L, int heads, void* dst);
 
 /* Merge two attention results of the same query rows over DISJOINT key sets, given each one's
  * log2-domain LSE ([heads][rows] fp32, as sr_attention writes for batch 1):

@@ -251,6 +251,8 @@ void check() {
   sr_attn_desc a = attn(1, 16, 43968, 43968, 0), b = attn(1, 16, 43968, 9728, 0);
   a.key_norm_max = b.key_norm_max = 40.f;
   expect("sr_attention_pair", sr_attention_pair(nullptr, SR_BF16, &a, &b), true);
+  expect("sr_attention_pair_vt null tiles", sr_attention_pair_vt(nullptr, SR_BF16, &a, &b, fake(0), nullptr), false);
+  expect("sr_vt_tiles null", sr_vt_tiles(nullptr, nullptr, 3072, 64, 16, nullptr), false);
   b.l0 = 9760;
   expect("sr_attention_pair ragged keys", sr_attention_pair(nullptr, SR_BF16, &a, &b), false);
   b = attn(1, 8, 43968, 9728, 0);

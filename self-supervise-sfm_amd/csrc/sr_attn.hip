@@ -35,6 +35,7 @@ struct AttnArgs {
   int ntile0, ntile1;  // key tiles per segment
   int kb_n0;           // segment-0 instances in d.key_bound (1 if shared, else batch)
   int allow_mzero;     // fixed offset m == 0 drops the -m fold MFMAs (SR_ATTN_MZERO=0: keep them)
+  const void* vt;      // VT bodies: segment 0's V^T tiles (sr_vt_tiles), [head][tile][64 d][64 slots]
 };
 
 // ------------------------------------------------------------------ bf16 / MFMA
@@ -102,7 +103,10 @@ __device__ __forceinline__ float value_window_hi(const sr_attn_desc& d, const At
 // the item's segments.
 template <int NW> constexpr int attn_nbuf() { return NW >= 4 ? 4 : 2; }  // K/V ring stages
 
-template <int NW, int QB, int KIND, bool PIPE>
+// VT (the pair launch with V^T tiles, one segment of whole tiles): the V waves stage V^T tile t of
+// the head (8 KiB, contiguous) with K's swizzle, and a P.V fragment is one ds_read_b128 at a K
+// fragment address (below); the LDS image and the arithmetic are otherwise those of V.
+template <int NW, int QB, int KIND, bool PIPE, bool VT = false>
 __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int row0, const int head, const int item,
                                                char* smem) {
   static_assert(!PIPE || (NW == 4 && QB == 2), "the pipelined sweep pairs the two q-blocks of a wave");
@@ -125,18 +129,21 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const bool stage_v = wave_u * DPW >= 8;  // wave-uniform: a wave stages only K or only V
   const int grow0 = ((wave_u * DPW) & 7) * 8;  // first tile row of this wave's pieces
-  const char* const sb0 = (const char*)(stage_v ? d.v0 : d.k0) + 2 * hcol;
+  const bool vt_stage = VT && stage_v;  // V^T tiles: 128-B rows (d), KT rows per tile, contiguous
+  const char* const sb0 = vt_stage ? (const char*)args.vt + (int64_t)head * args.ntile0 * TILE_B
+                                   : (const char*)(stage_v ? d.v0 : d.k0) + 2 * hcol;
   const char* const sb1 = (const char*)(stage_v ? d.v1 : d.k1) + 2 * hcol;
-  const int64_t sld0 = stage_v ? d.ldv0 : d.ldk0, sld1 = stage_v ? d.ldv1 : d.ldk1;
-  const int64_t srb0 = (int64_t)item * d.k0_bstride, srb1 = (int64_t)item * d.k1_bstride;
+  const int64_t sld0 = vt_stage ? 64 : stage_v ? d.ldv0 : d.ldk0, sld1 = stage_v ? d.ldv1 : d.ldk1;
+  const int64_t srb0 = vt_stage ? 0 : (int64_t)item * d.k0_bstride, srb1 = (int64_t)item * d.k1_bstride;
   const int nt0 = args.ntile0, len0 = d.l0, len1 = d.l1;
   // K rows: chunk ^ ((r>>1)&7) (conflict-free ds_read_b128 fragments); with r = 8(gi&7) + lane/8
   // that is chunk ^ (4(gi&1) + lane/16).  V rows: chunk ^ (((r>>1)&1)<<2) = chunk ^ (((lane/16)&1)<<2)
   // (conflict-free ds_read_b64_tr_b16: rows r, r+2 of a 4-row transposed block land in
-  // opposite 64-B halves).
+  // opposite 64-B halves).  V^T rows (VT): K's swizzle.
   const int lrow = lane >> 3;
-  const int chA = stage_v ? ((lane & 7) ^ (((lane >> 4) & 1) << 2)) : ((lane & 7) ^ (lane >> 4));
-  const int chB = stage_v ? chA : ((lane & 7) ^ (4 + (lane >> 4)));
+  const bool vsw_rows = stage_v && !vt_stage;
+  const int chA = vsw_rows ? ((lane & 7) ^ (((lane >> 4) & 1) << 2)) : ((lane & 7) ^ (lane >> 4));
+  const int chB = vsw_rows ? chA : ((lane & 7) ^ (4 + (lane >> 4)));
   const uint32_t voA0 = (uint32_t)((lrow * sld0 + chA * 8) * 2), voB0 = (uint32_t)((lrow * sld0 + chB * 8) * 2);
   const uint32_t voA1 = (uint32_t)((lrow * sld1 + chA * 8) * 2), voB1 = (uint32_t)((lrow * sld1 + chB * 8) * 2);
   const char* sp = sb0 + (srb0 + grow0) * sld0 * 2;  // row grow0 of the next tile to stage
@@ -461,6 +468,12 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
         const int rowoff = (kb * 32 + 16 * s2) * 128;
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
+          if constexpr (VT) {  // V^T rows d = 32 db + l32, key slots 32 kb + 16 s2 + 8 hi .. + 8
+            const bf16x8 vf = *(const bf16x8*)(vt_lds + db * 4096 + koff[2 * kb + s2]);
+#pragma unroll
+            for (int b = 0; b < QB; ++b) o[b][db] = mfma32(vf, pf[b], o[b][db]);
+            continue;
+          }
           const char* pa = vt_lds + rowoff + (db ? voff1 : voff0);
           const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)pa);
           const s16x4 vb =
@@ -582,7 +595,7 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
     // fragment lane addresses (ring slot and block offsets ride in the instructions' offset field)
     const uint32_t ka0 = lds0 + koff[0], ka1 = lds0 + koff[1], ka2 = lds0 + koff[2], ka3 = lds0 + koff[3];
     const uint32_t va0 = lds0 + voff0, va1 = lds0 + voff1;
-    if (!(args.ntile1 == 0 && len0 % KT == 0)) {
+    if (!VT && !(args.ntile1 == 0 && len0 % KT == 0)) {  // (VT launches: one segment of whole tiles)
       // segment switch when tile nt0 is staged (the asm stages tile t+3 during tile t); a switch
       // inside the C++ prologue (nt0 <= 2) already left sp / sstep on segment 1
       const uint32_t nsw = nt0 >= LOOK && args.ntile1 > 0 ? (uint32_t)(nt0 - LOOK) : 0xffffffffu;
@@ -615,7 +628,18 @@ __device__ __forceinline__ void attn_bf16_body(const AttnArgs& args, const int r
                      [trag0] "s"(trag0), [trag1] "s"(trag1), [vk0] "v"(vk0), [vk1] "v"(vk1), [ninf] "v"(ninf),
                      [mn0] "v"(mneg[0]), [mn1] "v"(mneg[1])
                    : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc", "vcc");
-    } else
+    } else if constexpr (VT)
+    asm volatile(SR_ATTN_PIPE_ASM_VT
+                 : [o00] "+&a"(o[0][0]), [o01] "+&a"(o[0][1]), [o10] "+&a"(o[1][0]), [o11] "+&a"(o[1][1]),
+                   [l0] "+&a"(lacc[0]), [l1] "+&a"(lacc[1]), [dma0] "+&v"(dm[0]), [dma1] "+&v"(dm[1]),
+                   [n] "+&s"(nn)
+                 : [q00] "a"(qf[0][0]), [q01] "a"(qf[0][1]), [q02] "a"(qf[0][2]), [q03] "a"(qf[0][3]),
+                   [q10] "a"(qf[1][0]), [q11] "a"(qf[1][1]), [q12] "a"(qf[1][2]), [q13] "a"(qf[1][3]),
+                   [suma] "v"(sum_a), [ka0] "v"(ka0), [ka1] "v"(ka1), [ka2] "v"(ka2), [ka3] "v"(ka3),
+                   [sp] "s"(spb), [sp2] "s"(spb2), [sstep] "s"(sst32),
+                   [ldsv] "s"(ldsv), [rem] "s"(rem), [mn0] "v"(mneg[0]), [mn1] "v"(mneg[1])
+                 : SR_ATTN_PIPE_CLOBBERS, "memory", "m0", "scc");
+    else
     asm volatile(SR_ATTN_PIPE_ASM
                  // every output early-clobber: the asm writes them while it still reads inputs (an
                  // input of equal value may otherwise share a tied output's register)
@@ -744,7 +768,7 @@ struct AttnPair {
   int nq[2], nh;  // q-tiles per problem, heads (both)
 };
 
-template <int KIND>
+template <int KIND, bool VT = false>
 __global__ __launch_bounds__(256, 1) void attn_bf16_pair_kernel(AttnPair p) {
   int lin = blockIdx.x;
   const int sel = lin >= p.nwg0p ? 1 : 0;
@@ -753,7 +777,7 @@ __global__ __launch_bounds__(256, 1) void attn_bf16_pair_kernel(AttnPair p) {
   if (lin >= nwg) return;  // problem 0's padding
   const int tile = sr::xcd_remap(lin, nwg);
   __shared__ __attribute__((aligned(16))) char smem[attn_nbuf<4>() * STAGE_B];
-  attn_bf16_body<4, 2, KIND, true>(p.a[sel], (tile % nq) * 256, tile / nq, 0, smem);
+  attn_bf16_body<4, 2, KIND, true, VT>(p.a[sel], (tile % nq) * 256, tile / nq, 0, smem);
 }
 
 // ------------------------------------------------------------------ fp8 Q.K^T (BASELINE C5)
@@ -1165,6 +1189,36 @@ __global__ __launch_bounds__(256) void quant_fp8_vt_kernel(const bf16* __restric
     w[q] = __builtin_amdgcn_cvt_pk_fp8_f32(x4[2], x4[3], lo, true);
   }
   *(int4*)(dst + (((int64_t)head * ntiles + t) * 64 + d) * 64 + p0) = make_int4(w[0], w[1], w[2], w[3]);
+}
+
+// V -> V^T tiles for the pair launch's VT sweep (bf16, exact copy): tile t of head h = 64 rows d x
+// 64 key slots; slot 8 c + j of row d (chunk c = 4 kb + 2 s2 + hh) holds V[64 t + key][64 h + d]
+// with key = 32 kb + 16 s2 + 8 (j >> 2) + 4 hh + (j & 3) -- the P fragment's k order (a 16-key
+// group's slots 4-7 and 8-11 swapped).  Keys past L are zero.  One workgroup per (tile, head):
+// 16-B row reads of the 64 x 64 block into LDS, 16-B writes of whole V^T rows.
+__global__ __launch_bounds__(256) void vt_tiles_kernel(const bf16* __restrict__ v, int64_t ldv, int L, int ntiles,
+                                                       bf16* __restrict__ dst) {
+  __shared__ bf16 tile[KT][64 + 2];  // +2: the column reads below spread over the banks
+  const int t = blockIdx.x, head = blockIdx.y, tid = threadIdx.x;
+  for (int i = tid; i < KT * 8; i += 256) {  // 64 keys x 8 chunks of 8 bf16
+    const int key = i >> 3, c = (i & 7) * 8, gk = t * KT + key;
+    bf16x8 x = {};
+    if (gk < L) x = *(const bf16x8*)(v + (int64_t)gk * ldv + head * 64 + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[key][c + j] = x[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < 64 * 8; i += 256) {  // row d, chunk c of the V^T tile
+    const int d = i >> 3, c = i & 7;
+    bf16x8 y;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int p = 8 * c + j;  // slot: kb = p >> 5, s2 = (p >> 4) & 1, hh = (p >> 3) & 1
+      const int key = (p & 48) + 8 * (j >> 2) + 4 * ((p >> 3) & 1) + (j & 3);
+      y[j] = tile[key][d];
+    }
+    *(bf16x8*)(dst + (((int64_t)head * ntiles + t) * 64 + d) * 64 + 8 * c) = y;
+  }
 }
 
 // key_bound of sr_attention: out[inst * heads + h] = max over the instance's rows of |k[row, h]|^2
@@ -1718,24 +1772,46 @@ static int pair_args(const sr_attn_desc& d, AttnArgs& a, const char* which) {
   return SR_OK;
 }
 
-extern "C" int sr_attention_pair(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1) {
+static int attention_pair(hipStream_t s, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1, const void* vt0,
+                          const void* vt1) {
   SR_CHECK(d0 && d1, SR_EINVAL, "sr_attention_pair: null desc");
   SR_CHECK(dtype == SR_BF16, SR_EUNSUPPORTED, "sr_attention_pair: bf16 only");
+  const bool vt = vt0 != nullptr;
+  SR_CHECK((vt0 == nullptr) == (vt1 == nullptr), SR_EINVAL, "sr_attention_pair_vt: both V^T tile sets or neither");
+  SR_CHECK(!vt || ((((uintptr_t)vt0 | (uintptr_t)vt1) & 15) == 0), SR_EINVAL,
+           "sr_attention_pair_vt: V^T tiles must be 16-B aligned");
   SR_CHECK(d0->heads == d1->heads, SR_EINVAL, "sr_attention_pair: both problems need the same head count");
   AttnPair p;
   int rc = pair_args(*d0, p.a[0], "0");
   if (rc != SR_OK) return rc;
   rc = pair_args(*d1, p.a[1], "1");
   if (rc != SR_OK) return rc;
+  p.a[0].vt = vt0;
+  p.a[1].vt = vt1;
   p.nh = d0->heads;
   p.nq[0] = (d0->lq + 255) / 256;
   p.nq[1] = (d1->lq + 255) / 256;
   const int nwg0 = p.nq[0] * p.nh;
   p.nwg0p = (nwg0 + 7) / 8 * 8;
   const int grid = p.nwg0p + p.nq[1] * p.nh;
-  hipLaunchKernelGGL((attn_bf16_pair_kernel<2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
-  sr::note_kernel("attn_bf16_pair_kernel<2>");
+  if (vt) {
+    hipLaunchKernelGGL((attn_bf16_pair_kernel<2, true>), dim3(grid), dim3(256), 0, s, p);
+    sr::note_kernel("attn_bf16_pair_kernel<2, true>");
+  } else {
+    hipLaunchKernelGGL((attn_bf16_pair_kernel<2>), dim3(grid), dim3(256), 0, s, p);
+    sr::note_kernel("attn_bf16_pair_kernel<2>");
+  }
   return sr::check_launch("sr_attention_pair");
+}
+
+extern "C" int sr_attention_pair(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1) {
+  return attention_pair((hipStream_t)stream, dtype, d0, d1, nullptr, nullptr);
+}
+
+extern "C" int sr_attention_pair_vt(sr_stream_t stream, int dtype, const sr_attn_desc* d0, const sr_attn_desc* d1,
+                                    const void* vt0, const void* vt1) {
+  SR_CHECK(vt0 && vt1, SR_EINVAL, "sr_attention_pair_vt: null V^T tiles");
+  return attention_pair((hipStream_t)stream, dtype, d0, d1, vt0, vt1);
 }
 
 extern "C" int sr_attention(sr_stream_t stream, int dtype, const sr_attn_desc* desc) {
@@ -1942,6 +2018,17 @@ extern "C" int sr_attention_qk8(sr_stream_t stream, const sr_attn_desc* desc, co
     hipLaunchKernelGGL((attn_qk8_kernel<0, false>), grid, dim3(256), 0, s, a, (const uint8_t*)q8, ldq8,
                        (const uint8_t*)k8, ldk8, nov, qk_exp);
   return sr::check_launch("sr_attention_qk8");
+}
+
+extern "C" int sr_vt_tiles(sr_stream_t stream, const void* v, int64_t ldv, int L, int heads, void* dst) {
+  SR_CHECK(v && dst && L > 0 && heads > 0, SR_EINVAL, "sr_vt_tiles: bad arguments");
+  SR_CHECK(ldv % 8 == 0 && ldv >= (int64_t)heads * 64 && ((uintptr_t)v & 15) == 0 && ((uintptr_t)dst & 15) == 0,
+           SR_EINVAL, "sr_vt_tiles: ldv a multiple of 8 (>= 64 heads), v and dst 16-B aligned");
+  const int ntiles = (L + KT - 1) / KT;
+  hipLaunchKernelGGL(vt_tiles_kernel, dim3(ntiles, heads), dim3(256), 0, (hipStream_t)stream, (const bf16*)v, ldv, L,
+                     ntiles, (bf16*)dst);
+  sr::note_kernel("vt_tiles_kernel");
+  return sr::check_launch("sr_vt_tiles");
 }
 
 extern "C" int sr_quant_fp8_vt(sr_stream_t stream, const void* v, int64_t ldv, int L, int heads, void* dst,

@@ -137,6 +137,8 @@ _PROTOS = {
                               ctypes.POINTER(GemmEpi)]),
     "sr_attention": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc)]),
     "sr_attention_pair": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnDesc)]),
+    "sr_attention_pair_vt": (_i32, [_vp, _i32, ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnDesc), _vp, _vp]),
+    "sr_vt_tiles": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp]),
     "sr_gemm_group": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(GemmProblem)]),
     "sr_attention_bound_floats": (_i32, [ctypes.POINTER(AttnDesc)]),
     "sr_attn_merge_n": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),

@@ -593,14 +593,19 @@ class Aggregator(nn.Module):
             qkv_r, qkv_g = sc.qkv[q0:q1], sc.qkv[a0:q0]
             o_a, lse_a = ops.key_split_workspace(dev, 1, rows, C, pr.heads, name="reloc_split")
             lse_a = lse_a[0]
-            ops.attention_pair(
-                dict(q=qkv_g[:, 0:C], k0=qkv_g[:, C:2 * C], v0=qkv_g[:, 2 * C:3 * C], o=sc.o[a0:q0], lq=La, l0=La,
-                     key_norm_max=runtime.key_norm_bound(pg), query_norm_max=runtime.query_norm_bound(pg),
-                     q_scaled=_qs(pg)),
-                dict(q=qkv_r[:, 0:C], k0=kv_sub_all[:n_full, 0:C], v0=kv_sub_all[:n_full, C:2 * C], o=o_a, lq=rows,
-                     l0=n_full, key_norm_max=runtime.key_norm_bound(pr), query_norm_max=runtime.query_norm_bound(pr),
-                     lse=lse_a.view(-1), q_scaled=_qs(pr)),
-                heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
+            pa = dict(q=qkv_g[:, 0:C], k0=qkv_g[:, C:2 * C], v0=qkv_g[:, 2 * C:3 * C], o=sc.o[a0:q0], lq=La, l0=La,
+                      key_norm_max=runtime.key_norm_bound(pg), query_norm_max=runtime.query_norm_bound(pg),
+                      q_scaled=_qs(pg))
+            pb = dict(q=qkv_r[:, 0:C], k0=kv_sub_all[:n_full, 0:C], v0=kv_sub_all[:n_full, C:2 * C], o=o_a, lq=rows,
+                      l0=n_full, key_norm_max=runtime.key_norm_bound(pr), query_norm_max=runtime.query_norm_bound(pr),
+                      lse=lse_a.view(-1), q_scaled=_qs(pr))
+            if ops.PAIR_VT:
+                # both problems' V as pre-transposed tiles: one ds_read_b128 per P.V fragment in the sweep
+                for p_, name, blk in ((pa, "vt_g", pg), (pb, "vt_s", pr)):
+                    p_["vt"] = ops.vt_tiles(p_["v0"], p_["l0"], blk.heads,
+                                            ws.get(name, *ops.vt_tile_shape(p_["l0"], blk.heads), dtype, dev),
+                                            tag="vt_tiles")
+            ops.attention_pair(pa, pb, heads=pg.heads, head_dim=pg.head_dim, tag="attn_global")
             self._reloc_own_pass(pr, qkv_r, kv_sub_all, sc.o[q0:q1], o_a, lse_a, Nq_l, P, n_sub_all, n_full)
             if runtime.group_tails_wanted(max(q1 - q0, q0 - a0)):
                 out.extend(runtime.run_block_tails([(pr, q0, q1), (pg, a0, q0)], x, sc, defer=defer))

@@ -476,7 +476,8 @@ _ATTN_PAIR = os.environ.get("SR_ATTN_PAIR", "1") != "0"
 def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional[str] = None) -> None:
     """Two single-query-set bf16 attentions in ONE launch (sr_attention_pair): ``a`` / ``b`` are
     dicts with q, k0, v0, o, lq, l0, key_norm_max and optionally lse, query_norm_max, q_scaled (keys
-    as attention()'s, batch 1, one segment).
+    as attention()'s, batch 1, one segment) and vt (v0 as vt_tiles(); both or neither:
+    sr_attention_pair_vt, bit-identical).
     a's workgroups run first and b's fill the CUs a's last round leaves idle.  Both must pass
     pair_eligible (checked)."""
     descs = []
@@ -492,13 +493,54 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
         descs.append(d)
         flops += 4.0 * heads * p["lq"] * p["l0"] * head_dim
         nbytes += p["q"].element_size() * heads * head_dim * (2 * p["lq"] + 2 * p["l0"])
+    vts = [p.get("vt") for p in (a, b)]
+    if (vts[0] is None) != (vts[1] is None):
+        raise ValueError("attention_pair: V^T tiles for both problems or for neither")
+    for p, vt in zip((a, b), vts):
+        if vt is not None:
+            _check_vt_tiles(vt, p["l0"], heads)
     timed = TIMER is not None and TIMER.wants(tag)
     ev0 = TIMER.start() if timed else None
-    rc = _lib.load().sr_attention_pair(_stream(a["q"]), dtype_code(a["q"].dtype), ctypes.byref(descs[0]),
-                                       ctypes.byref(descs[1]))
+    lib = _lib.load()
+    if vts[0] is not None:
+        rc = lib.sr_attention_pair_vt(_stream(a["q"]), dtype_code(a["q"].dtype), ctypes.byref(descs[0]),
+                                      ctypes.byref(descs[1]), _p(vts[0]), _p(vts[1]))
+    else:
+        rc = lib.sr_attention_pair(_stream(a["q"]), dtype_code(a["q"].dtype), ctypes.byref(descs[0]),
+                                   ctypes.byref(descs[1]))
     check(rc, "sr_attention_pair")
     if timed:
         TIMER.stop(tag, ev0, flops, nbytes, kernel=last_kernel())
+
+
+# SR_ATTN_PAIR_VT=0: the pair launch reads V with transposing LDS reads instead of pre-transposed
+# V^T tiles (sr_vt_tiles + sr_attention_pair_vt)
+PAIR_VT = os.environ.get("SR_ATTN_PAIR_VT", "1") != "0"
+
+
+def vt_tile_shape(L: int, heads: int) -> tuple:
+    """(rows, 64) of the bf16 V^T tile buffer sr_vt_tiles fills for L keys."""
+    return (heads * ((L + 63) // 64) * 64, 64)
+
+
+def _check_vt_tiles(vt: torch.Tensor, L: int, heads: int) -> None:
+    if vt.dtype != torch.bfloat16 or not vt.is_contiguous() or vt.numel() < heads * ((L + 63) // 64) * 4096 \
+            or vt.data_ptr() % 16:
+        raise ValueError("V^T tiles: contiguous bf16, 16-B aligned, heads * ceil(L / 64) * 4096 elements")
+
+
+def vt_tiles(v: torch.Tensor, L: int, heads: int, out: torch.Tensor, tag: Optional[str] = None) -> torch.Tensor:
+    """V (bf16 [L][heads * 64], row stride v.stride(0)) -> V^T tiles (sr_vt_tiles) for attention_pair's
+    ``vt``: [heads][ceil(L/64)][64 d][64 key slots], the bf16 P fragment's key order."""
+    if v.dtype != torch.bfloat16 or v.stride(1) != 1 or v.shape[0] < L or v.shape[1] < heads * 64:
+        raise ValueError("vt_tiles: v must be bf16 [L][>= heads * 64] with unit column stride")
+    _check_vt_tiles(out, L, heads)
+    timed = TIMER is not None and TIMER.wants(tag)
+    ev0 = TIMER.start() if timed else None
+    check(_lib.load().sr_vt_tiles(_stream(v), _p(v), v.stride(0), L, heads, _p(out)), "sr_vt_tiles")
+    if timed:
+        TIMER.stop(tag, ev0, 0.0, 4.0 * L * heads * 64, kernel=last_kernel())
+    return out
 
 
 _KEY_BOX = os.environ.get("SR_ATTN_KEY_BOX", "auto")  # auto | 1 (always) | 0 (never)

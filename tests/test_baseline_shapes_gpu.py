@@ -622,6 +622,83 @@ def test_global_attention_qk_gain(ops, g):
         assert float(((lse[h, rws].double() - l2).abs() - 3e-3 * l2.abs()).max()) < 3e-2
 
 
+def _vt_ref(v, L, heads):
+    """sr_vt_tiles' layout in torch: [heads][ceil(L/64)][64 d][64 slots], slot 32kb + 16s2 + 8h + j
+    holding key 32kb + 16s2 + 8(j >> 2) + 4h + (j & 3) of the tile (zero past L)."""
+    nt = (L + 63) // 64
+    vp = torch.zeros(nt * 64, heads * D, dtype=v.dtype, device=v.device)
+    vp[:L] = v[:L, :heads * D]
+    p = torch.arange(64)
+    j = p & 7
+    key = (p & 48) + 8 * (j >> 2) + 4 * ((p >> 3) & 1) + (j & 3)
+    t = vp.view(nt, 64, heads, D)[:, key.to(v.device)]          # [tile][slot][head][d]
+    return t.permute(2, 0, 3, 1).contiguous()                    # [head][tile][d][slot]
+
+
+@pytest.mark.parametrize("case", ["C3", "padded", "gain8"])
+def test_attention_pair_vt(ops, case):
+    """sr_attention_pair_vt (V^T tiles from sr_vt_tiles, one ds_read_b128 per P.V fragment) is
+    bit-identical to sr_attention_pair, on the hand-scheduled sweep (C3, 'padded': 3 heads and a
+    padded first problem) and on the compiled fallback loop ('gain8': qk-norm gain 8 puts the rows
+    outside the fixed-offset window, sweep_stats counts compiled waves).  The tiles match the
+    layout built in torch (ragged L included)."""
+    if case == "C3":
+        heads, La, rows, nk = H, 32 * P, 32 * P, 32 * PP // 64 * 64
+        qg, kg, vg = _make(La, 11, spikes=(La - 5, 77))
+        qr, _, _ = _make(rows, 12)
+        _, ks, vs = _make(nk, 13, spikes=(nk - 1,))
+        kbg, kbr = _kbound(kg, heads), _kbound(ks, heads)
+    elif case == "padded":
+        heads, La, rows, nk = 3, 21 * 256 - 128, 9 * 256 + 7, 40 * 64
+        g = torch.Generator(device=DEV).manual_seed(5)
+        mk = lambda n: (torch.randn(n, heads * D, device=DEV, generator=g) * 0.5).bfloat16()  # noqa: E731
+        qg, kg, vg, qr, ks, vs = mk(La), mk(La), mk(La), mk(rows), mk(nk), mk(nk)
+        kbg, kbr = _kbound(kg, heads), _kbound(ks, heads)
+    else:
+        heads, La, nk = H, 16 * P, 16 * PP // 64 * 64
+        La = La // 64 * 64
+        rows = La
+        gen = torch.Generator(device=DEV).manual_seed(80)
+        qg, _ = _qk_gain(La, 8.0, gen)
+        kg, kbg = _qk_gain(La, 8.0, gen)
+        vg = torch.randn(La, C, device=DEV, generator=gen).bfloat16()
+        qr, _ = _qk_gain(rows, 8.0, gen)
+        ks, kbr = _qk_gain(nk, 8.0, gen)
+        vs = torch.randn(nk, C, device=DEV, generator=gen).bfloat16()
+    cols = heads * D
+    vtg = torch.empty(ops.vt_tile_shape(La, heads), dtype=torch.bfloat16, device=DEV)
+    vtr = torch.empty(ops.vt_tile_shape(nk, heads), dtype=torch.bfloat16, device=DEV)
+    ops.vt_tiles(vg, La, heads, vtg)
+    ops.vt_tiles(vs, nk, heads, vtr)
+    outs = []
+    for vt in (None, (vtg, vtr)):
+        og, orr = (torch.empty(n, cols, device=DEV, dtype=torch.bfloat16) for n in (La, rows))
+        lse = torch.empty(heads, rows, device=DEV)
+        st = torch.zeros(2, dtype=torch.int32, device=DEV)
+        a = dict(q=qg, k0=kg, v0=vg, o=og, lq=La, l0=La, key_norm_max=kbg, sweep_stats=st)
+        b = dict(q=qr, k0=ks, v0=vs, o=orr, lq=rows, l0=nk, key_norm_max=kbr, lse=lse.view(-1), sweep_stats=st)
+        if vt is not None:
+            a["vt"], b["vt"] = vt
+        ops.attention_pair(a, b, heads=heads, head_dim=D)
+        torch.cuda.synchronize()
+        outs.append((og, orr, lse, st.tolist()))
+    print(f"pair_vt {case}: asm / compiled waves {outs[1][3]}")
+    assert outs[0][3] == outs[1][3]
+    if case == "gain8":
+        assert outs[1][3][1] > 0
+    else:
+        assert outs[1][3][1] == 0
+    for x, y in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(x, y)
+    assert torch.equal(vtg.view(heads, -1, 64, 64), _vt_ref(vg, La, heads))
+    # a ragged L (keys past L zero) and a strided V (columns of a wider row)
+    Lr = 1000
+    wide = torch.randn(Lr, 3 * cols, device=DEV).bfloat16()
+    vt_r = torch.full(ops.vt_tile_shape(Lr, heads), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.vt_tiles(wide[:, cols:2 * cols], Lr, heads, vt_r)
+    assert torch.equal(vt_r.view(heads, -1, 64, 64), _vt_ref(wide[:, cols:2 * cols], Lr, heads))
+
+
 def test_attention_dma_base_bit31(ops):
     """The round-3 fault's cause (readfirstlane returns int, and the widened low
     word of the LDS-DMA base sign-extended into the high word when bit 31 was set; fixed at

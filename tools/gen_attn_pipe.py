@@ -32,6 +32,9 @@ Hazards handled here: lgkmcnt counted per fragment read (LDS returns in order), 
 compiler reads O / l.
 
     python3 tools/gen_attn_pipe.py          (writes the .inc; committed, regenerate after edits)
+
+Three statements: SR_ATTN_PIPE_ASM (one segment of whole tiles), SR_ATTN_PIPE_ASM_SEG (two segments,
+ragged tails) and SR_ATTN_PIPE_ASM_VT (as the first, V staged pre-transposed: see VT below).
 """
 
 import os
@@ -72,6 +75,11 @@ DMA_SPLIT = int(os.environ.get("SR_PIPE_DMA_SPLIT", "0"))
 # %[trag1], per-lane valid-key thresholds %[vk0] / %[vk1] = valid - 4 hi).  The staging then reads
 # up to 63 rows past a segment's end: the caller guarantees them readable and finite.
 SEG = False
+# SR_ATTN_PIPE_ASM_VT (generated with VT = True): the V half of each stage holds the V^T tile
+# (sr_vt_tiles: 64 rows d x 64 key slots in the P fragment's k order, staged with K's swizzle), so a
+# V^T fragment is ONE ds_read_b128 at a K-fragment lane address (%[ka<2 kb + s2>], +4096 for d block
+# 1) instead of two ds_read_b64_tr_b16
+VT = False
 _LABEL = [0]
 
 
@@ -180,6 +188,11 @@ class Phase:
             for db in range(2):
                 off = slot * STAGE_B + TILE_B + (kb * 32 + 16 * s2) * 128
                 f = vfrag(p, i, db)
+                if VT:
+                    lines = [("ds", f"ds_read_b128 {ar(f, 4)}, %[ka{2 * kb + s2}] "
+                                    f"offset:{slot * STAGE_B + TILE_B + db * 4096}", seqs, (p, i, db))]
+                    self.other.append((COST["read"], lines, "read"))
+                    continue
                 if EXP_VB128:
                     lines = [("ds", f"ds_read_b128 {ar(f, 4)}, %[ka{(2 * i + db) & 3}] "
                                     f"offset:{slot * STAGE_B + TILE_B + (i >> 1) * 4096}", seqs, (p, i, db))]
@@ -392,10 +405,11 @@ def sweep():
 
 
 def main():
-    global SEG
+    global SEG, VT
     out = ["// GENERATED by tools/gen_attn_pipe.py — do not edit by hand."]
-    for seg, name in ((False, "SR_ATTN_PIPE_ASM"), (True, "SR_ATTN_PIPE_ASM_SEG")):
-        SEG = seg
+    for seg, vt, name in ((False, False, "SR_ATTN_PIPE_ASM"), (True, False, "SR_ATTN_PIPE_ASM_SEG"),
+                          (False, True, "SR_ATTN_PIPE_ASM_VT")):
+        SEG, VT = seg, vt
         lines, loop = sweep()
         n_mfma = sum(1 for l in loop if l.startswith("v_mfma")) // 4
         n_valu = sum(1 for l in loop if l.startswith(("v_exp", "v_cvt"))) // 4

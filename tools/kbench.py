@@ -128,11 +128,26 @@ def attn_pair():
         ops.attention_pair(dict(q=qkv[:, :C], k0=qkv[:, C:2 * C], v0=qkv[:, 2 * C:], o=og, lq=L, l0=L, key_norm_max=kbg),
                            dict(q=qr, k0=kv[:, :C], v0=kv[:, C:], o=oa, lq=L, l0=nf, key_norm_max=kbr,
                                 lse=lse.view(-1)), heads=H, head_dim=D)
+    vtg = torch.empty(ops.vt_tile_shape(L, H), device=DEV, dtype=torch.bfloat16)
+    vtr = torch.empty(ops.vt_tile_shape(nf, H), device=DEV, dtype=torch.bfloat16)
+
+    def tiles():
+        ops.vt_tiles(qkv[:, 2 * C:], L, H, vtg)
+        ops.vt_tiles(kv[:, C:], nf, H, vtr)
+
+    def paired_vt():
+        ops.attention_pair(dict(q=qkv[:, :C], k0=qkv[:, C:2 * C], v0=qkv[:, 2 * C:], o=og, lq=L, l0=L, key_norm_max=kbg,
+                                vt=vtg),
+                           dict(q=qr, k0=kv[:, :C], v0=kv[:, C:], o=oa, lq=L, l0=nf, key_norm_max=kbr,
+                                lse=lse.view(-1), vt=vtr), heads=H, head_dim=D)
+    tiles()
     fl = 4.0 * H * L * (L + nf) * D
     for i in range(2):
-        ta, tp = timeit(apart, reps=5), timeit(paired, reps=5)
+        ta, tp, tv, tt = (timeit(apart, reps=5), timeit(paired, reps=5), timeit(paired_vt, reps=5),
+                          timeit(tiles, reps=20))
         print(f"attn pair C3 global + reloc subsample: apart {ta:.3f} ms ({fl / ta / 1e9:.1f} TF/s), "
-              f"paired {tp:.3f} ms ({fl / tp / 1e9:.1f} TF/s)", flush=True)
+              f"paired {tp:.3f} ms ({fl / tp / 1e9:.1f} TF/s), paired V^T {tv:.3f} ms ({fl / tv / 1e9:.1f} TF/s) "
+              f"+ its two sr_vt_tiles {tt * 1e3:.1f} us", flush=True)
 
 
 def qk_normed(rows, g, gen, H=16, D=64):
