@@ -149,6 +149,9 @@ for step in "$@"; do
                 run bench_rl0_$i 400 env SR_GEMM_RESID_LDS=0 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
                 run bench_rl1_$i 400 env SR_GEMM_RESID_LDS=1 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
               done ;;
+    pair_tests) run pair_tests 600 python -u -m pytest tests/test_baseline_shapes_gpu.py -x -q -m gpu -k "pair or dma_base or qk_gain" \
+               --timeout 300 --timeout-method thread ;;
+    kpair)   run kpair 300 python tools/kbench.py attn_pair ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
