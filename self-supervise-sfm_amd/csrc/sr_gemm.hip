@@ -433,47 +433,43 @@ __device__ __forceinline__ void resid_full(const GemmArgs& g, f32x4 (&acc)[8][4]
   }
 }
 
-// ---- RESID epilogue, LDS-staged half (GemmArgs.resid_lds), 256x256 tiles (a partial last row tile
+// ---- RESID epilogue staged through LDS (GemmArgs.resid_lds), 256x256 tiles (a partial last row tile
 // reads row M - 1 for the rows past M and stores only rows < M).
 // The register form above keeps 8 KiB of x loads in flight per wave (64 KiB per CU) in 4 dependent
 // rounds, each wave instruction touching 16 rows x 64 B; the epilogue then costs about as much as
-// the K = 1024 k-loop (0.15 of proj's 0.30 ms) and is bound by that latency.  Here the
-// two wave rows split the tile:
-//   * waves 0-3 (rows 0-127) move their x rows as 1-KiB rows by LDS-DMA, in two 64-row halves into
-//     the two 64-KiB stage buffers (half 0 under the last k-tile's MFMAs into the buffer that k-tile
-//     does not read, half 1 right after it, both in flight at once), add gamma * (acc + bias) in LDS
-//     and store whole rows;
-//   * waves 4-7 (rows 128-255) run resid_full's register read-modify-write over their rows meanwhile,
-//     between the same five barriers.
-// The two halves are separate uniform branches, so the compiler's wait counting in waves 4-7 (its
-// loads) never meets the LDS-DMA of waves 0-3, and waves 0-3 issue no compiler-visible load: their
-// gamma | bias columns ride along with half 0 (1 KiB each, waves 0 / 1, past the stage buffers).
-// 16-B chunk c of LDS row r sits at c ^ (r & 15): the DMA's per-lane source chunk, the owners'
-// accumulator-layout read-modify-write (16 rows x one chunk column per 16 lanes) and the copy-out's
-// row reads are bank-conflict free.  Per element the same fp32 operations as resid_full:
-// x + (acc + bias) * gamma.
+// the K = 1024 k-loop (0.15 of proj's 0.30 ms) and is bound by that latency, not by HBM.
+// Here the x tile moves as 1-KiB rows by LDS-DMA, in 64-row quarters through the two 64-KiB stage
+// buffers: quarter 0 goes out under the last k-tile's MFMAs (into the stage buffer that k-tile does
+// not read), quarter 1 right after it, and quarter k+2 as soon as quarter k's copy-out has read its
+// buffer, so two quarters (128 KiB) are in flight while the owner waves add gamma * (acc + bias)
+// in LDS and all eight waves store whole rows.  16-B chunk c of quarter row r sits at c ^ (r & 15):
+// the DMA's per-lane source chunk, the owners' accumulator-layout read-modify-write (16 rows x one
+// chunk column per 16 lanes) and the copy-out's row reads are all bank-conflict free.
+// Per element the same fp32 operations as resid_full: x + (acc + bias) * gamma.  The tile's gamma and
+// bias columns ride along with quarter 0 (1 KiB each, waves 0 / 1, past the stage buffers): the
+// epilogue issues no compiler-visible load, so the compiler's wait counting never waits on the
+// LDS-DMA it cannot see.
 constexpr int RESID_GB = 2048;  // LDS past the two stages: gamma | bias of the tile's 256 columns
-// half h (rows 64 h .. 64 h + 63) of waves 0-3's rows: wave w < 4 stages rows 64 h + 16 w .. + 15
-__device__ __forceinline__ void resid_dma_half(const GemmArgs& g, char* smem, int m0, int n0, int h, int buf,
-                                               int lane, int wave_u) {
-  if (h == 0 && wave_u < 2 && (wave_u == 0 || g.ep.bias))
+__device__ __forceinline__ void resid_dma_quarter(const GemmArgs& g, char* smem, int m0, int n0, int q, int buf,
+                                                  int lane, int wave_u) {
+  if (q == 0 && wave_u < 2 && (wave_u == 0 || g.ep.bias))
     sr::dma16_s(wave_u == 0 ? g.ep.gamma + n0 : g.ep.bias + n0, (uint32_t)lane * 16,
                 __builtin_amdgcn_readfirstlane(sr::lds_addr(smem) + 2 * STAGE_BIG + wave_u * 1024));
-  const uint32_t base = sr::lds_addr(smem) + buf * STAGE_BIG + wave_u * 16 * 1024;
-  const int r0 = m0 + h * 64 + wave_u * 16;
+  const uint32_t base = sr::lds_addr(smem) + buf * STAGE_BIG + wave_u * 8 * 1024;
+  const int r0 = m0 + q * 64 + wave_u * 8;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int r = min(r0 + i, g.M - 1);  // rows past M (a partial last row tile): any valid row
-    sr::dma16_s((const char*)g.out + ((int64_t)r * g.ldo + n0) * 4, (uint32_t)((lane ^ i) << 4),
-                __builtin_amdgcn_readfirstlane(base + i * 1024));  // LDS row 16 w + i: swizzle i
+  for (int i = 0; i < 8; ++i) {
+    const int swz = ((wave_u & 1) << 3) | i;  // (quarter row 8 wave + i) & 15
+    const int r = min(r0 + i, g.M - 1);       // rows past M (a partial last row tile): any valid row
+    sr::dma16_s((const char*)g.out + ((int64_t)r * g.ldo + n0) * 4, (uint32_t)((lane ^ swz) << 4),
+                __builtin_amdgcn_readfirstlane(base + i * 1024));
   }
 }
 
-// the owners (waves 0-3, accumulator rows mi = 4 h .. 4 h + 3) add gamma * (acc + bias) in LDS, one
-// 16-row block at a time (16 x VGPRs live: the accumulators fill the AGPRs and the epilogue must not
-// spill -- a scratch reload's vmcnt(0) would also wait out the LDS-DMA in flight)
-__device__ __forceinline__ void resid_add_half(f32x4 (&acc)[8][4], char* smem, int buf, int h, int wc, int lr,
-                                               int lg, const f32x4 (&gm)[4], const f32x4 (&bs)[4]) {
+__device__ __forceinline__ void resid_add_quarter(f32x4 (&acc)[8][4], char* smem, int buf, int q, int wc, int lr,
+                                                  int lg, const f32x4 (&gm)[4], const f32x4 (&bs)[4]) {
+  // one 16-row block at a time (16 x VGPRs live: the accumulators already fill the AGPRs and the
+  // epilogue must not spill -- a scratch reload's vmcnt(0) would also wait out the LDS-DMA in flight)
   char* sb = smem + buf * STAGE_BIG + lr * 1024;
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -482,120 +478,81 @@ __device__ __forceinline__ void resid_add_half(f32x4 (&acc)[8][4], char* smem, i
     for (int ni = 0; ni < 4; ++ni) xv[ni] = *(const f32x4*)(sb + m * 16 * 1024 + (((wc * 16 + ni * 4 + lg) ^ lr) << 4));
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-      xv[ni] += (acc[h * 4 + m][ni] + bs[ni]) * gm[ni];
+      xv[ni] += (acc[(q & 1) * 4 + m][ni] + bs[ni]) * gm[ni];
       *(f32x4*)(sb + m * 16 * 1024 + (((wc * 16 + ni * 4 + lg) ^ lr) << 4)) = xv[ni];
     }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-__device__ __forceinline__ void resid_store_half(const GemmArgs& g, const char* smem, int buf, int m0, int n0, int h,
-                                                 int lane, int wave_u) {
-  const char* sb = smem + buf * STAGE_BIG + wave_u * 16 * 1024;
-  f32x4 v[16];
+__device__ __forceinline__ void resid_store_quarter(const GemmArgs& g, const char* smem, int buf, int m0, int n0,
+                                                    int q, int lane, int wave_u) {
+  const char* sb = smem + buf * STAGE_BIG + wave_u * 8 * 1024;
+  f32x4 v[8];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(sb + i * 1024 + lane * 16);
-  const int r0 = m0 + h * 64 + wave_u * 16;
+  for (int i = 0; i < 8; ++i) v[i] = *(const f32x4*)(sb + i * 1024 + lane * 16);
+  const int r0 = m0 + q * 64 + wave_u * 8;
   float* xr = (float*)g.out + (int64_t)r0 * g.ldo + n0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (r0 + i < g.M) *(f32x4*)(xr + (int64_t)i * g.ldo + ((lane ^ i) << 2)) = v[i];  // wave-uniform
+  for (int i = 0; i < 8; ++i) {
+    const int swz = ((wave_u & 1) << 3) | i;
+    if (r0 + i < g.M) *(f32x4*)(xr + (int64_t)i * g.ldo + ((lane ^ swz) << 2)) = v[i];  // wave-uniform
+  }
 }
 
-// waves 4-7's rows 128-255 in registers: resid_full's rounds of 2 row blocks, between the five
-// barriers of waves 0-3's LDS half.  GUARD (a partial last row tile): loads read row M - 1 past M,
-// stores skip those rows -- its own instantiation, so the full tiles' wait counting stays exact.
-template <bool GUARD>
-__device__ __forceinline__ void resid_reg_half(const GemmArgs& g, f32x4 (&acc)[8][4], int m0, int n0, int wc, int lr,
-                                               int lg) {
-  const sr_gemm_epi& ep = g.ep;
+// After the k-loop: quarter 0 is in flight into buffer fb (issued under the last k-tile), the last
+// k-tile read buffer fb ^ 1.  vmcnt counts this wave's LDS-DMA pieces (8 per quarter) and its row
+// stores (8 per quarter) in issue order.
+__device__ __forceinline__ void resid_lds_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], char* smem, int m0, int n0,
+                                                   int fb, int wr, int wc, int lr, int lg, int lane, int wave_u) {
+  const int kb = fb ^ 1;
+  // a partial last row tile skips the stores of rows >= M, so the store counts below do not hold:
+  // it waits for everything instead (one tile per launch at most)
+  const bool partial = m0 + BIG > g.M;
+  auto wait_q = [&]() {  // the quarter two DMA issues back landed: 16 younger ops (its successor's
+    if (partial) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // 8 pieces, 8 row stores)
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  };
+  sr::barrier_raw();                                          // every wave is done reading buffer kb
+  resid_dma_quarter(g, smem, m0, n0, 1, kb, lane, wave_u);   // in flight: Q0 Q1
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");           // Q0 (+ gamma / bias) landed: this wave's
+  sr::barrier_raw();                                          // ... every wave's
   f32x4 gm[4], bs[4];
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {
-    const int col = n0 + wc * 64 + ni * 16 + 4 * lg;
-    gm[ni] = *(const f32x4*)(ep.gamma + col);
-    bs[ni] = ep.bias ? *(const f32x4*)(ep.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int off = (wc * 64 + ni * 16 + 4 * lg) * 4;
+    gm[ni] = *(const f32x4*)(smem + 2 * STAGE_BIG + off);
+    bs[ni] = g.ep.bias ? *(const f32x4*)(smem + 2 * STAGE_BIG + 1024 + off) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int row0 = m0 + 128 + lr;  // + 16 mi
-  float* xb = (float*)g.out + n0 + wc * 64 + 4 * lg;
-  auto rowp = [&](int mi) {
-    const int r = row0 + mi * 16;
-    return xb + (int64_t)(GUARD ? min(r, g.M - 1) : r) * g.ldo;
-  };
-  f32x4 xq[2][2][4];
-  auto load = [&](int q) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float* p = rowp(2 * q + i);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) xq[q & 1][i][ni] = *(const f32x4*)(p + ni * 16);
-    }
-  };
-  auto update = [&](int q) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      float* p = rowp(2 * q + i);
-      const bool ok = !GUARD || row0 + (2 * q + i) * 16 < g.M;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        f32x4& xv = xq[q & 1][i][ni];
-        xv += (acc[2 * q + i][ni] + bs[ni]) * gm[ni];
-        if (ok) *(f32x4*)(p + ni * 16) = xv;
-      }
-    }
-  };
-  load(0);
-  sr::barrier_raw();  // B1
-  load(1);
-  update(0);
-  sr::barrier_raw();  // B2
-  load(2);
-  update(1);
-  sr::barrier_raw();  // B3
-  load(3);
-  update(2);
-  sr::barrier_raw();  // B4
-  update(3);
-  sr::barrier_raw();  // B5
-}
-
-// After the k-loop: waves 0-3's half 0 is in flight into buffer fb (issued under the last k-tile),
-// the last k-tile read buffer fb ^ 1.  vmcnt counts a wave's LDS-DMA pieces (16 per half) and its
-// row stores (16 per half) in issue order.
-__device__ __forceinline__ void resid_lds_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], char* smem, int m0, int n0,
-                                                   int fb, int wc, int lr, int lg, int lane, int wave_u) {
-  const int kb = fb ^ 1;
-  // a partial last row tile skips the stores of rows >= M, so the store count below does not hold:
-  // it waits for everything instead (one tile per launch at most)
-  const bool partial = m0 + BIG > g.M;
-  if (wave_u < 4) {  // rows 0-127 through LDS
-    sr::barrier_raw();                                         // B1: every wave is done reading buffer kb
-    resid_dma_half(g, smem, m0, n0, 1, kb, lane, wave_u);     // in flight: H0 H1
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");         // H0 (+ gamma / bias) landed: this wave's
-    sr::barrier_raw();                                         // B2: ... every wave's
-    f32x4 gm[4], bs[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int off = (wc * 64 + ni * 16 + 4 * lg) * 4;
-      gm[ni] = *(const f32x4*)(smem + 2 * STAGE_BIG + off);
-      bs[ni] = g.ep.bias ? *(const f32x4*)(smem + 2 * STAGE_BIG + 1024 + off) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    resid_add_half(acc, smem, fb, 0, wc, lr, lg, gm, bs);
-    sr::wait_lgkm0();
-    sr::barrier_raw();                                         // B3
-    resid_store_half(g, smem, fb, m0, n0, 0, lane, wave_u);   // H1 S0
-    if (partial) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");    // H1 landed (16 younger: S0)
-    sr::barrier_raw();                                         // B4
-    resid_add_half(acc, smem, kb, 1, wc, lr, lg, gm, bs);
-    sr::wait_lgkm0();
-    sr::barrier_raw();                                         // B5
-    resid_store_half(g, smem, kb, m0, n0, 1, lane, wave_u);
-  } else if (!partial) {  // rows 128-255 in registers
-    resid_reg_half<false>(g, acc, m0, n0, wc, lr, lg);
-  } else {
-    resid_reg_half<true>(g, acc, m0, n0, wc, lr, lg);
-  }
+  if (wr == 0) resid_add_quarter(acc, smem, fb, 0, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, fb, m0, n0, 0, lane, wave_u);  // Q1 S0
+  sr::wait_lgkm0();
+  sr::barrier_raw();                                          // buffer fb read out
+  resid_dma_quarter(g, smem, m0, n0, 2, fb, lane, wave_u);   // Q1 S0 Q2
+  wait_q();                                                  // Q1 landed
+  sr::barrier_raw();
+  if (wr == 0) resid_add_quarter(acc, smem, kb, 1, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, kb, m0, n0, 1, lane, wave_u);  // S0 Q2 S1
+  sr::wait_lgkm0();
+  sr::barrier_raw();                                          // buffer kb read out
+  resid_dma_quarter(g, smem, m0, n0, 3, kb, lane, wave_u);   // S0 Q2 S1 Q3
+  wait_q();                                                  // Q2 landed
+  sr::barrier_raw();
+  if (wr == 1) resid_add_quarter(acc, smem, fb, 2, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, fb, m0, n0, 2, lane, wave_u);  // S1 Q3 S2
+  if (partial) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q3 landed (8 younger: S2)
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  sr::barrier_raw();
+  if (wr == 1) resid_add_quarter(acc, smem, kb, 3, wc, lr, lg, gm, bs);
+  sr::wait_lgkm0();
+  sr::barrier_raw();
+  resid_store_quarter(g, smem, kb, m0, n0, 3, lane, wave_u);
 }
 
 // bias (+ erf-GELU) -> bf16 for a full 256x256 tile (every row < M; N % 256 == 0 here; no aux):
@@ -986,7 +943,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
     // measured no better)
     auto dma_phase = [&](int ph) {
       if (!more) {  // last k-tile: the RESID x tile's first quarter into the stage buffer it does not read
-        if (RLDS && ph == 0 && wave_u < 4) resid_dma_half(g, smem, m0, n0, 0, (kt + 1) & 1, lane, wave_u);
+        if (RLDS && ph == 0) resid_dma_quarter(g, smem, m0, n0, 0, (kt + 1) & 1, lane, wave_u);
         return;
       }
       if (ph < 2) dma_pieces(kt + 1, 4 * ph, 4 * ph + 4);
@@ -1036,7 +993,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmArgs& g, char* smem, int 
     mma(aY, bX, 1, 0);
   }
   if constexpr (RLDS) {
-    resid_lds_epilogue(g, acc, smem, m0, n0, ke & 1, wc, lr, lg, lane, wave_u);
+    resid_lds_epilogue(g, acc, smem, m0, n0, ke & 1, wr, wc, lr, lg, lane, wave_u);
     return;
   }
   if constexpr (EPI == SR_EPI_BIAS_RESID) {
