@@ -77,9 +77,8 @@ enum sr_tuning_key {  /* renumbered in ABI 1.3: switches that measured level or 
   SR_TUNE_RLN_WIDE = 12,    /* sr_residual_layernorm variant bits: 1 16-B lanes, 2 two rows per wave, 4 nt x stores (0) */
   SR_TUNE_GEMM_TAIL = 13,   /* 1: a 256x256 GEMM whose last workgroup round would run few tiles computes
                                the rows past its last whole round on the 128x128 kernel (second launch)  (1) */
-  SR_TUNE_GEMM_RESID_LDS = 14,/* 1: the 256x256 RESID GEMM's epilogue stages rows 0-127 of the x tile
-                               through LDS by LDS-DMA (two 64-row halves in flight; whole-row
-                               stores) while waves 4-7 update rows 128-255 in registers  default 1 */
+  SR_TUNE_GEMM_RESID_LDS = 14,/* 1: the 256x256 RESID GEMM's epilogue stages the x tile through LDS by
+                               LDS-DMA (64-row quarters, two in flight; whole-row stores)  default 1 */
   SR_TUNE_GEMM_ROPE_LDS = 15,/* 1: the 256x256 QKV epilogue reads its RoPE tables from LDS (staged by DMA
                                under the first k-tile; 0: from global memory)           default 1 */
   SR_TUNE_ATTN_BWD_PIPE = 16,/* 1: the dK/dV sweep as the hand-scheduled asm pipeline (one wave per SIMD,
