@@ -547,17 +547,19 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // One wave per row; 4 heads per pass (16 lanes x 4 values per head: dims 4 li .. 4 li + 3).
 // RoPE pairs (d, d + 16) of each half sit in lanes li and li ^ 4.
 // T = bf16 (autocast blocks) or float (fp32 blocks): the type of raw and out.
-// ep.colsum: every wave also adds the values it stores into its own LDS row [wave][col] (a lane owns
-// its columns: plain read-add-write, no atomics), then the workgroup's 4 rows sum into one partial
-// row [blockIdx.x][ncols] of cpart; the host sums those rows into ep.colsum (a fixed order).
+// The column blocks of 1,024 are the OUTER loop (each wave walks its rows once per block), so that
+// with ep.colsum a lane sums the values it stores for its 16 columns of the block in registers
+// (rows in order); at the end of a block the workgroup's 4 wave rows meet in LDS and sum into one
+// partial row [blockIdx.x][ncols] of cpart; the host sums those rows into ep.colsum (a fixed order).
+// (An LDS row per wave across the whole row loop cost 48 KiB of LDS per workgroup: 3 workgroups per
+// CU, and 1.5x the kernel time.)
 constexpr int QKB_PASSES = 3;  // ncols <= 3072 with ep.colsum
-constexpr int ep_colsum_lds_floats() { return 4 * QKB_PASSES * 1024; }  // 48 KiB
 template <typename T>
 __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, int64_t ldr,
                                                      const float* __restrict__ dsrc, int64_t lds, T* out,
                                                      int64_t ldo, int rows, int ncols, sr_gemm_epi ep, float* part,
                                                      float* cpart) {
-  extern __shared__ float csl[];  // ep_colsum_lds_floats() when ep.colsum (dynamic: no LDS otherwise)
+  __shared__ float csl[4][1024];  // ep.colsum: the 4 waves' sums of one column block
   constexpr bool BF = sr::is_bf16<T>::value;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
@@ -581,9 +583,8 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
   (void)bq;
   (void)bk;
   const bool want_cs = ep.colsum != nullptr;  // uniform
-  float* const csw = csl + (threadIdx.x >> 6) * (QKB_PASSES * 1024);  // this wave's LDS row
-  if (want_cs)
-    for (int c = 4 * lane; c < ncols; c += 256) *(float4*)(csw + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int cb_ = 0; cb_ < ncols; cb_ += 1024) {
+  f32x4 csa[4] = {};  // ep.colsum: this lane's columns cb + 256 p + 4 lane .. + 4, summed over its rows
   for (int row = gw; row < rows; row += nw) {
     float cs[4] = {1.f, 1.f, 1.f, 1.f}, sn[4] = {0.f, 0.f, 0.f, 0.f};
     if (rope) {
@@ -596,8 +597,12 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
       sn[0] = s4.x; sn[1] = s4.y; sn[2] = s4.z; sn[3] = s4.w;
     }
     // passes of 4 heads (256 columns) in groups of 4: every load of a group is issued before its
-    // math (16 heads of loads in flight per wave; one pass at a time left HBM latency exposed)
-    for (int cb = 0; cb < ncols; cb += 1024) {
+    // math (16 heads of loads in flight per wave; one pass at a time left HBM latency exposed).
+    // cb re-read per row: hoisting the 4 passes' column / region / weight selections out of the
+    // row loop costs more registers than it saves instructions
+    {
+      int cb = cb_;
+      asm volatile("" : "+s"(cb));
       float4 d4s[4];
       f32x4 r4s[4] = {};
 #pragma unroll
@@ -685,17 +690,23 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
         else
           *(f32x4*)(out + (int64_t)row * ldo + col) = f32x4{d[0], d[1], d[2], d[3]};
         if (want_cs) {
-          float4 t = *(float4*)(csw + col);
-          t.x += sr::to_f32(sr::from_f32<T>(d[0]));
-          t.y += sr::to_f32(sr::from_f32<T>(d[1]));
-          t.z += sr::to_f32(sr::from_f32<T>(d[2]));
-          t.w += sr::to_f32(sr::from_f32<T>(d[3]));
-          *(float4*)(csw + col) = t;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) csa[p][e] += sr::to_f32(sr::from_f32<T>(d[e]));
         }
       }
       }
       }
     }
+  }
+  if (want_cs) {  // the workgroup's 4 wave sums of this block -> its partial row (fixed order)
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) *(f32x4*)(&csl[w][256 * p + 4 * lane]) = csa[p];
+    __syncthreads();
+    for (int c = threadIdx.x; c < 1024 && cb_ + c < ncols; c += 256)
+      cpart[(int64_t)blockIdx.x * ncols + cb_ + c] = (csl[0][c] + csl[1][c]) + (csl[2][c] + csl[3][c]);
+    __syncthreads();
+  }
   }
   if (norm) {  // lanes li, li+16, li+32, li+48 hold the same dims
 #pragma unroll
@@ -711,13 +722,6 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int e = 0; e < 4; ++e) pw[t * 64 + 4 * li + e] = acc[t][e];
-    }
-  }
-  if (want_cs) {  // the workgroup's 4 LDS rows -> its partial row (fixed order)
-    __syncthreads();
-    for (int c = threadIdx.x; c < ncols; c += 256) {
-      const int s = QKB_PASSES * 1024;
-      cpart[(int64_t)blockIdx.x * ncols + c] = (csl[c] + csl[s + c]) + (csl[2 * s + c] + csl[3 * s + c]);
     }
   }
 }
@@ -1181,7 +1185,8 @@ extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, i
   return sr::check_launch("sr_layernorm_bwd");
 }
 
-static int qk_bwd_wgs(int rows) { return std::min(1024, (rows + 3) / 4); }
+// 138 VGPRs: 3 waves per SIMD, so 3 workgroups of 4 waves per CU are resident -- one round of 768
+static int qk_bwd_wgs(int rows) { return std::min(768, (rows + 3) / 4); }
 
 extern "C" int64_t sr_qk_bwd_workspace_floats(int rows, int ncols) {
   if (rows <= 0 || ncols <= 0 || ncols % 4) return 0;
@@ -1210,7 +1215,7 @@ static int qk_bwd(const char* who, sr_stream_t stream, const void* raw, int64_t 
   // workspace: norm partials [wgs*4][256] | their colsum scratch | colsum partials [wgs][ncols] | scratch
   float* cpart = workspace ? workspace + (int64_t)wgs * 4 * 256 + (int64_t)colsum_chunks(wgs * 4, 256, rpc) * 256
                            : nullptr;
-  hipLaunchKernelGGL(qk_bwd_kernel<T>, dim3(wgs), dim3(256), ep->colsum ? ep_colsum_lds_floats() * 4 : 0, s,
+  hipLaunchKernelGGL(qk_bwd_kernel<T>, dim3(wgs), dim3(256), 0, s,
                      (const T*)raw, ldr, dsrc, lds, (T*)out, ldo, rows, ncols, *ep, workspace, cpart);
   sr::note_kernel("qk_bwd_kernel<%s>", sr::is_bf16<T>::value ? "__bf16" : "float");
   if (norm) {  // [wgs*4][4][64] -> grads[4][64]

@@ -513,9 +513,10 @@ def attention_pair(a: dict, b: dict, *, heads: int, head_dim: int, tag: Optional
         TIMER.stop(tag, ev0, flops, nbytes, kernel=last_kernel())
 
 
-# SR_ATTN_PAIR_VT=0: the pair launch reads V with transposing LDS reads instead of pre-transposed
-# V^T tiles (sr_vt_tiles + sr_attention_pair_vt)
-PAIR_VT = os.environ.get("SR_ATTN_PAIR_VT", "1") != "0"
+# SR_ATTN_PAIR_VT=1: the forward's pair launch reads pre-transposed V^T tiles (sr_vt_tiles +
+# sr_attention_pair_vt) instead of V with transposing LDS reads.  Bit-identical; measured level, off:
+# the launch gains 18-21 us of 7.88 ms, the two sr_vt_tiles cost 38 us (profiles/r06_j5_kpair_vt.log)
+PAIR_VT = os.environ.get("SR_ATTN_PAIR_VT", "0") == "1"
 
 
 def vt_tile_shape(L: int, heads: int) -> tuple:
