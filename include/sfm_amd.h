@@ -491,6 +491,12 @@ int sr_gemm_wgrad_pair(sr_stream_t stream, const sr_wgrad_problem* problems);
 int64_t sr_colsum_workspace_floats(int M, int N);
 int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
               float scale, float* workspace, int64_t workspace_floats);
+/* The LayerScale residual's parameter grads from one column sum s = sum_r X[r][c] (ABI 1.5):
+ *   out1[c] += mul1[c] * s[c],  out2[c] += mul2[c] * s[c]   (either pair may be NULL, not both)
+ * -- sr_colsum into a scratch row followed by sr_vec_fma_f32 per pair, in the same two launches the
+ * column sum alone takes (bit-identical to that sequence).  Workspace as sr_colsum. */
+int sr_colsum_fma(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out1,
+                  const float* mul1, float* out2, const float* mul2, float* workspace, int64_t workspace_floats);
 
 /* LayerNorm backward (block.py:50,70 norm1 / norm2; vision_transformer.py:300 norm):
  * for row r (x row / dx row = rowmap ? rowmap[r] : r):
@@ -608,8 +614,11 @@ int sr_copy2d_f32(sr_stream_t stream, float* dst, int64_t ldd, const float* src,
  * d_act[r - n_anchor] * (c < 7 || act[r][c] > 0); act = the forward's activated encoding. */
 int sr_pose_act_bwd_f32(sr_stream_t stream, float* dd, const float* d_act, const float* act, int rows, int n_anchor);
 
-/* out[i] += a[i] * b[i] */
+/* out[i] += a[i] * b[i]  (one fused multiply-add) */
 int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, const float* b, int n);
+/* out1[i] += a1[i] * b[i] and out2[i] += a2[i] * b[i] in one launch (ABI 1.5; each as sr_vec_fma_f32) */
+int sr_vec_fma2_f32(sr_stream_t stream, float* out1, const float* a1, float* out2, const float* a2, const float* b,
+                    int n);
 
 /* Self-supervised IMC loss (compute_loss, train/train_imc.py:141-246; CDFLossIndexPytorch,
  * train/losses/cdf_loss.py:19-242; geometry, train/utils/geometry.py:89-303): value and the

@@ -285,6 +285,9 @@ void check() {
   expect("sr_quant_fp8 null", sr_quant_fp8(nullptr, nullptr, 8, 8, 8, 1.f, nullptr, 8, nullptr, nullptr), false);
   expect("sr_attention_qk8 null", sr_attention_qk8(nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr), false);
   expect("sr_attention_qkv8 null", sr_attention_qkv8(nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr), false);
+  expect("sr_colsum_fma no pair", sr_colsum_fma(nullptr, SR_F32, fake(0), 8, 8, 8, nullptr, nullptr, nullptr, nullptr,
+                                                   fake<float>(1), 1 << 20), false);
+  expect("sr_vec_fma2_f32 null", sr_vec_fma2_f32(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 8), false);
   expect("sr_quant_fp8_vt null", sr_quant_fp8_vt(nullptr, nullptr, 8, 8, 1, nullptr, nullptr, nullptr), false);
   expect("sr_attention_bwd null", sr_attention_bwd(nullptr, nullptr), false);
   expect("sr_attention_bwd_f32 null", sr_attention_bwd_f32(nullptr, nullptr), false);

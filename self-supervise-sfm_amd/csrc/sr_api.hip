@@ -93,7 +93,7 @@ int check_launch(const char* what) {
 
 extern "C" const char* sr_last_error(void) { return g_err; }
 extern "C" const char* sr_last_kernel(void) { return g_kernel; }
-extern "C" int sr_version(void) { return (1 << 16) | 5; }  // 1.1: sr_gemm_wgrad_pair; 1.2: sr_attention_bwd_f32; 1.3: tuning keys renumbered; 1.4: sr_gemm_epi.colsum; 1.5: sr_attention_pair_vt, sr_vt_tiles
+extern "C" int sr_version(void) { return (1 << 16) | 5; }  // 1.1: sr_gemm_wgrad_pair; 1.2: sr_attention_bwd_f32; 1.3: tuning keys renumbered; 1.4: sr_gemm_epi.colsum; 1.5: sr_attention_pair_vt, sr_vt_tiles, sr_colsum_fma, sr_vec_fma2_f32
 
 extern "C" int sr_set_tuning(int key, int value) {
   SR_CHECK(key >= 0 && key < SR_TUNE_COUNT, SR_EINVAL, "sr_set_tuning: unknown key %d", key);

@@ -319,8 +319,13 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 
 // partial rows [chunks][N] -> out: workgroup = 16 column quads x 16 chunk groups; each thread sums
 // its chunks z = g, g + 16, ... in order, then a fixed LDS tree over the 16 groups (deterministic)
+// FMA form (sr_colsum_fma): out[c] += m1[c] * s[c] and o2[c] += m2[c] * s[c] for the pairs given
+// (each as sr_vec_fma_f32 on the plain colsum's result: the same sum and the same fused multiply-add)
+template <bool FMA = false>
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
-                                                           float* out, int accumulate, float scale) {
+                                                           float* out, int accumulate, float scale,
+                                                           const float* __restrict__ m1 = nullptr, float* o2 = nullptr,
+                                                           const float* __restrict__ m2 = nullptr) {
   __shared__ f32x4 red[16][16];
   const int qi = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int64_t c = ((int64_t)blockIdx.x * 16 + qi) * 4;
@@ -345,8 +350,17 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
     __syncthreads();
   }
   if (g == 0 && c < N) {
-    f32x4* o = (f32x4*)(out + c);
-    *o = accumulate ? *o + red[0][qi] * scale : red[0][qi] * scale;
+    if constexpr (FMA) {
+      const f32x4 sv = red[0][qi];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (out) out[c + e] = __builtin_fmaf(m1[c + e], sv[e], out[c + e]);
+        if (o2) o2[c + e] = __builtin_fmaf(m2[c + e], sv[e], o2[c + e]);
+      }
+    } else {
+      f32x4* o = (f32x4*)(out + c);
+      *o = accumulate ? *o + red[0][qi] * scale : red[0][qi] * scale;
+    }
   }
 }
 
@@ -360,7 +374,8 @@ static int colsum_chunks(int M, int N, int& rpc) {
 }
 
 int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, int N, float* out, int accumulate,
-                  float scale, float* ws) {
+                  float scale, float* ws, const float* m1 = nullptr, float* o2 = nullptr, const float* m2 = nullptr,
+                  bool fma = false) {
   // ~1024 partial workgroups of >= 16 rows, then the parallel final reduction
   const int64_t gx = (N / 4 + 255) / 256;
   int rpc;
@@ -371,8 +386,12 @@ int colsum_launch(hipStream_t s, int dtype, const void* X, int64_t ldx, int M, i
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((unsigned)gx, chunks), dim3(256), 0, s, (const float*)X, ldx,
                        M, N, rpc, ws);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N / 4 + 15) / 16)), dim3(256), 0, s, ws, chunks, N, out,
-                     accumulate, scale);
+  if (fma)
+    hipLaunchKernelGGL(colsum_final_kernel<true>, dim3((unsigned)((N / 4 + 15) / 16)), dim3(256), 0, s, ws, chunks, N,
+                       out, 1, 1.f, m1, o2, m2);
+  else
+    hipLaunchKernelGGL(colsum_final_kernel<false>, dim3((unsigned)((N / 4 + 15) / 16)), dim3(256), 0, s, ws, chunks, N,
+                       out, accumulate, scale, nullptr, nullptr, nullptr);
   return sr::check_launch("sr_colsum");
 }
 
@@ -1028,9 +1047,13 @@ __global__ void pose_act_bwd_kernel(float* dd, const float* __restrict__ d_act, 
 }
 
 // out[i] += a[i] * b[i]  (LayerScale gamma / bias grads from column sums)
-__global__ void vec_fma_kernel(float* out, const float* __restrict__ a, const float* __restrict__ b, int n) {
+__global__ void vec_fma_kernel(float* out, const float* __restrict__ a, const float* __restrict__ b, int n,
+                               float* out2, const float* __restrict__ a2) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] += a[i] * b[i];
+  if (i < n) {
+    out[i] = __builtin_fmaf(a[i], b[i], out[i]);
+    if (out2) out2[i] = __builtin_fmaf(a2[i], b[i], out2[i]);
+  }
 }
 
 unsigned grid_for(int64_t n, int64_t cap = 4096) {
@@ -1137,6 +1160,20 @@ extern "C" int sr_colsum(sr_stream_t stream, int dtype, const void* X, int64_t l
            "sr_colsum: workspace of %lld floats, needs %lld (sr_colsum_workspace_floats), 16-B aligned",
            (long long)workspace_floats, (long long)sr_colsum_workspace_floats(M, N));
   return colsum_launch((hipStream_t)stream, dtype, X, ldx, M, N, out, accumulate, scale, workspace);
+}
+
+extern "C" int sr_colsum_fma(sr_stream_t stream, int dtype, const void* X, int64_t ldx, int M, int N, float* out1,
+                             const float* mul1, float* out2, const float* mul2, float* workspace,
+                             int64_t workspace_floats) {
+  SR_CHECK(X && workspace && (out1 || out2) && (!out1 || mul1) && (!out2 || mul2), SR_EINVAL,
+           "sr_colsum_fma: null pointer (X, workspace, and at least one out / mul pair)");
+  SR_CHECK(dtype == SR_F32 || dtype == SR_BF16, SR_EINVAL, "sr_colsum_fma: bad dtype");
+  SR_CHECK(M > 0 && N > 0 && N % 4 == 0 && ldx % 4 == 0, SR_EINVAL, "sr_colsum_fma: bad shape M=%d N=%d ldx=%lld", M,
+           N, (long long)ldx);
+  SR_CHECK(workspace_floats >= sr_colsum_workspace_floats(M, N) && ((uintptr_t)workspace % 16) == 0, SR_EINVAL,
+           "sr_colsum_fma: workspace of %lld floats, needs %lld (sr_colsum_workspace_floats), 16-B aligned",
+           (long long)workspace_floats, (long long)sr_colsum_workspace_floats(M, N));
+  return colsum_launch((hipStream_t)stream, dtype, X, ldx, M, N, out1, 1, 1.f, workspace, mul1, out2, mul2, true);
 }
 
 extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, int64_t ldx, const int32_t* rowmap,
@@ -1425,8 +1462,16 @@ extern "C" int sr_act_bwd_f32(sr_stream_t stream, int mode, const float* x, cons
 
 extern "C" int sr_vec_fma_f32(sr_stream_t stream, float* out, const float* a, const float* b, int n) {
   SR_CHECK(out && a && b && n > 0, SR_EINVAL, "sr_vec_fma_f32: bad args");
-  hipLaunchKernelGGL(vec_fma_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, a, b, n);
+  hipLaunchKernelGGL(vec_fma_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, a, b, n, nullptr,
+                     nullptr);
   return sr::check_launch("sr_vec_fma_f32");
+}
+
+extern "C" int sr_vec_fma2_f32(sr_stream_t stream, float* out1, const float* a1, float* out2, const float* a2,
+                               const float* b, int n) {
+  SR_CHECK(out1 && a1 && out2 && a2 && b && n > 0, SR_EINVAL, "sr_vec_fma2_f32: bad args");
+  hipLaunchKernelGGL(vec_fma_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out1, a1, b, n, out2, a2);
+  return sr::check_launch("sr_vec_fma2_f32");
 }
 
 extern "C" int sr_scatter_rows_f32(sr_stream_t stream, float* dst, int64_t ldd, const int32_t* rowmap, const float* src,

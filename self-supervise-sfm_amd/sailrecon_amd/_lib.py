@@ -200,6 +200,8 @@ _PROTOS = {
     "sr_adaln_bwd_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32]),
     "sr_act_bwd_f32": (_i32, [_vp, _i32, _vp, _vp, _vp, _i64]),
     "sr_vec_fma_f32": (_i32, [_vp, _vp, _vp, _vp, _i32]),
+    "sr_vec_fma2_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i32]),
+    "sr_colsum_fma": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64]),
     "sr_scatter_rows_f32": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32]),
     "sr_copy2d_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32]),
     "sr_imc_loss_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32]),

@@ -1233,6 +1233,22 @@ def colsum(x: Tensor, out: Tensor, *, rows: Optional[int] = None, cols: Optional
     check(rc, "sr_colsum")
 
 
+def colsum_fma(x: Tensor, pairs) -> None:
+    """out[c] += mul[c] * sum_r x[r, c] for each (out, mul) of ``pairs`` (one or two; fp32 [cols]),
+    in the launches of one column sum (sr_colsum_fma; the same bits as colsum + vec_fma)."""
+    ldx = _rowmajor(x, "x")
+    M, N = x.shape
+    if not 1 <= len(pairs) <= 2 or any(o.dtype != torch.float32 or o.numel() < N or m.numel() < N for o, m in pairs):
+        raise ValueError("colsum_fma: one or two (out, mul) fp32 pairs of >= cols elements")
+    (o1, m1), (o2, m2) = pairs[0], (pairs[1] if len(pairs) == 2 else (None, None))
+    lib = _lib.load()
+    nws = lib.sr_colsum_workspace_floats(M, N)
+    ws = _train_ws(x.device, "colsum", max(1, nws))
+    rc = lib.sr_colsum_fma(_stream(x), dtype_code(x.dtype), _p(x), ldx, M, N, _p(o1), _p(m1), _p(o2), _p(m2), _p(ws),
+                           ws.numel())
+    check(rc, "sr_colsum_fma")
+
+
 def layernorm_bwd(x: Tensor, dy: Tensor, w: Optional[Tensor], eps: float, dx: Tensor, *,
                   dxb: Optional[Tensor] = None, dw: Optional[Tensor] = None, db: Optional[Tensor] = None,
                   rowmap: Optional[Tensor] = None, rows: Optional[int] = None,
@@ -1373,8 +1389,15 @@ def act_bwd(mode: int, x: Tensor, dy: Tensor, dx: Tensor) -> None:
     check(_lib.load().sr_act_bwd_f32(_stream(x), mode, _p(x), _p(dy), _p(dx), x.numel()), "sr_act_bwd_f32")
 
 
-def vec_fma(out: Tensor, a: Tensor, b: Tensor) -> None:
-    check(_lib.load().sr_vec_fma_f32(_stream(out), _p(out), _p(a), _p(b), out.numel()), "sr_vec_fma_f32")
+def vec_fma(out: Tensor, a: Tensor, b: Tensor, out2: Optional[Tensor] = None, a2: Optional[Tensor] = None) -> None:
+    """out += a * b (and out2 += a2 * b in the same launch), fp32, one fused multiply-add each."""
+    if out2 is None:
+        check(_lib.load().sr_vec_fma_f32(_stream(out), _p(out), _p(a), _p(b), out.numel()), "sr_vec_fma_f32")
+        return
+    if a2 is None or out2.numel() != out.numel():
+        raise ValueError("vec_fma: out2 needs a2 and out's length")
+    check(_lib.load().sr_vec_fma2_f32(_stream(out), _p(out), _p(a), _p(out2), _p(a2), _p(b), out.numel()),
+          "sr_vec_fma2_f32")
 
 
 def scatter_rows(dst: Tensor, rowmap: Tensor, src: Tensor, *, accumulate: bool = True, rows: Optional[int] = None) -> None:

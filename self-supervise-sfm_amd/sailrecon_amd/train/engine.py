@@ -247,14 +247,16 @@ def _resid_param_grads(dx: Tensor, bias: Optional[Tensor], gamma: Optional[Tenso
     ``summed``: tmp already holds colsum(dx) (layernorm_bwd's dx_sum)."""
     if not _resid_wants_sum(bias, g_bias, g_gamma):
         return
-    if not summed:
-        ops.colsum(dx, tmp)
-    if g_bias is not None:
-        if gamma is None:
-            raise RuntimeError("bias grad without gamma")
-        ops.vec_fma(g_bias, gamma, tmp)
-    if g_gamma is not None and bias is not None:
-        ops.vec_fma(g_gamma, bias, tmp)
+    if g_bias is not None and gamma is None:
+        raise RuntimeError("bias grad without gamma")
+    pairs = ([(g_bias, gamma)] if g_bias is not None else []) + \
+        ([(g_gamma, bias)] if g_gamma is not None and bias is not None else [])
+    if not summed:  # the column sum's final launch applies the products (no scratch row, no extra launch)
+        ops.colsum_fma(dx, pairs)
+    elif len(pairs) == 2:
+        ops.vec_fma(pairs[0][0], pairs[0][1], tmp, out2=pairs[1][0], a2=pairs[1][1])
+    else:
+        ops.vec_fma(pairs[0][0], pairs[0][1], tmp)
 
 
 def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTape, dx: Tensor,

@@ -164,6 +164,34 @@ def test_colsum(ops, dtype, M, N):
     assert rel(out - o0, 0.5 * x.float().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(31, 1024), (43968, 1024), (777, 4096)])
+def test_colsum_fma(ops, dtype, M, N):
+    """sr_colsum_fma (the LayerScale residual's bias / gamma grads in the column sum's own final
+    launch) and sr_vec_fma2_f32: bit-identical to sr_colsum into a scratch row followed by
+    sr_vec_fma_f32 per pair (one pair or two)."""
+    torch.manual_seed(5)
+    big = torch.randn(M, N + 8, device=DEV).to(dtype)
+    x = big[:, 4:N + 4]
+    m1, m2 = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
+    o1, o2 = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
+    r1, r2 = o1.clone(), o2.clone()
+    tmp = torch.empty(N, device=DEV)
+    ops.colsum(x, tmp)
+    ops.vec_fma(r1, m1, tmp)
+    ops.vec_fma(r2, m2, tmp)
+    f1, f2 = o1.clone(), o2.clone()
+    ops.colsum_fma(x, [(f1, m1), (f2, m2)])
+    g1 = o1.clone()
+    ops.colsum_fma(x, [(g1, m1)])
+    h1, h2 = o1.clone(), o2.clone()
+    ops.vec_fma(h1, m1, tmp, out2=h2, a2=m2)
+    torch.cuda.synchronize()
+    assert torch.equal(f1, r1) and torch.equal(f2, r2) and torch.equal(g1, r1)
+    assert torch.equal(h1, r1) and torch.equal(h2, r2)
+    assert rel(r1 - o1, m1 * x.float().sum(0)) < 1e-5
+
+
 def _ln_ref(x, dy, w, b, eps):
     x = x.detach().clone().requires_grad_(True)
     w = w.detach().clone().requires_grad_(True)
