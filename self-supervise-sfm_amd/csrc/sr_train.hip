@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // (An LDS row per wave across the whole row loop cost 48 KiB of LDS per workgroup: 3 workgroups per
 // CU, and 1.5x the kernel time.)
 constexpr int QKB_PASSES = 3;  // ncols <= 3072 with ep.colsum
-template <typename T>
+template <typename T, bool CS>
 __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, int64_t ldr,
                                                      const float* __restrict__ dsrc, int64_t lds, T* out,
                                                      int64_t ldo, int rows, int ncols, sr_gemm_epi ep, float* part,
@@ -601,9 +601,9 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
   }
   (void)bq;
   (void)bk;
-  const bool want_cs = ep.colsum != nullptr;  // uniform
-  for (int cb_ = 0; cb_ < ncols; cb_ += 1024) {
-  f32x4 csa[4] = {};  // ep.colsum: this lane's columns cb + 256 p + 4 lane .. + 4, summed over its rows
+  // CS (ep.colsum): the column blocks outer, one per row pass; otherwise every block of a row in turn
+  for (int cbo = 0; cbo < (CS ? ncols : 1); cbo += 1024) {
+  f32x4 csa[4] = {};  // CS: this lane's columns cbo + 256 p + 4 lane .. + 4, summed over its rows
   for (int row = gw; row < rows; row += nw) {
     float cs[4] = {1.f, 1.f, 1.f, 1.f}, sn[4] = {0.f, 0.f, 0.f, 0.f};
     if (rope) {
@@ -619,9 +619,9 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
     // math (16 heads of loads in flight per wave; one pass at a time left HBM latency exposed).
     // cb re-read per row: hoisting the 4 passes' column / region / weight selections out of the
     // row loop costs more registers than it saves instructions
-    {
+    for (int cb_ = CS ? cbo : 0; cb_ < (CS ? cbo + 1 : ncols); cb_ += 1024) {
       int cb = cb_;
-      asm volatile("" : "+s"(cb));
+      if constexpr (CS) asm volatile("" : "+s"(cb));
       float4 d4s[4];
       f32x4 r4s[4] = {};
 #pragma unroll
@@ -708,7 +708,7 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
           *(bf16x4*)(out + (int64_t)row * ldo + col) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
         else
           *(f32x4*)(out + (int64_t)row * ldo + col) = f32x4{d[0], d[1], d[2], d[3]};
-        if (want_cs) {
+        if constexpr (CS) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) csa[p][e] += sr::to_f32(sr::from_f32<T>(d[e]));
         }
@@ -717,13 +717,13 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
       }
     }
   }
-  if (want_cs) {  // the workgroup's 4 wave sums of this block -> its partial row (fixed order)
+  if constexpr (CS) {  // the workgroup's 4 wave sums of this block -> its partial row (fixed order)
     const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int p = 0; p < 4; ++p) *(f32x4*)(&csl[w][256 * p + 4 * lane]) = csa[p];
     __syncthreads();
-    for (int c = threadIdx.x; c < 1024 && cb_ + c < ncols; c += 256)
-      cpart[(int64_t)blockIdx.x * ncols + cb_ + c] = (csl[0][c] + csl[1][c]) + (csl[2][c] + csl[3][c]);
+    for (int c = threadIdx.x; c < 1024 && cbo + c < ncols; c += 256)
+      cpart[(int64_t)blockIdx.x * ncols + cbo + c] = (csl[0][c] + csl[1][c]) + (csl[2][c] + csl[3][c]);
     __syncthreads();
   }
   }
@@ -1222,12 +1222,12 @@ extern "C" int sr_layernorm_bwd(sr_stream_t stream, int dtype, const float* x, i
   return sr::check_launch("sr_layernorm_bwd");
 }
 
-// 138 VGPRs: 3 waves per SIMD, so 3 workgroups of 4 waves per CU are resident -- one round of 768
-static int qk_bwd_wgs(int rows) { return std::min(768, (rows + 3) / 4); }
+// one resident round: the column-sum form (138 VGPRs) runs 3 waves per SIMD, the plain one (110) 4
+static int qk_bwd_wgs(int rows, bool cs) { return std::min(cs ? 768 : 1024, (rows + 3) / 4); }
 
 extern "C" int64_t sr_qk_bwd_workspace_floats(int rows, int ncols) {
   if (rows <= 0 || ncols <= 0 || ncols % 4) return 0;
-  const int wgs = qk_bwd_wgs(rows);
+  const int wgs = qk_bwd_wgs(rows, false) > qk_bwd_wgs(rows, true) ? qk_bwd_wgs(rows, false) : qk_bwd_wgs(rows, true);
   int rpc;
   const int64_t norm = (int64_t)wgs * 4 * 256 + (int64_t)colsum_chunks(wgs * 4, 256, rpc) * 256;
   return norm + (int64_t)wgs * ncols + (int64_t)colsum_chunks(wgs, ncols, rpc) * ncols;
@@ -1247,14 +1247,18 @@ static int qk_bwd(const char* who, sr_stream_t stream, const void* raw, int64_t 
   SR_CHECK(!ep->colsum || (ncols <= QKB_PASSES * 1024 && workspace && ((uintptr_t)ep->colsum % 16) == 0),
            SR_EINVAL, "%s: colsum needs ncols <= %d, a workspace and a 16-B aligned output", who, QKB_PASSES * 1024);
   hipStream_t s = (hipStream_t)stream;
-  const int wgs = qk_bwd_wgs(rows);
+  const int wgs = qk_bwd_wgs(rows, ep->colsum != nullptr);
   int rpc;
   // workspace: norm partials [wgs*4][256] | their colsum scratch | colsum partials [wgs][ncols] | scratch
   float* cpart = workspace ? workspace + (int64_t)wgs * 4 * 256 + (int64_t)colsum_chunks(wgs * 4, 256, rpc) * 256
                            : nullptr;
-  hipLaunchKernelGGL(qk_bwd_kernel<T>, dim3(wgs), dim3(256), 0, s,
-                     (const T*)raw, ldr, dsrc, lds, (T*)out, ldo, rows, ncols, *ep, workspace, cpart);
-  sr::note_kernel("qk_bwd_kernel<%s>", sr::is_bf16<T>::value ? "__bf16" : "float");
+  if (ep->colsum)
+    hipLaunchKernelGGL((qk_bwd_kernel<T, true>), dim3(wgs), dim3(256), 0, s,
+                       (const T*)raw, ldr, dsrc, lds, (T*)out, ldo, rows, ncols, *ep, workspace, cpart);
+  else
+    hipLaunchKernelGGL((qk_bwd_kernel<T, false>), dim3(wgs), dim3(256), 0, s,
+                       (const T*)raw, ldr, dsrc, lds, (T*)out, ldo, rows, ncols, *ep, workspace, cpart);
+  sr::note_kernel("qk_bwd_kernel<%s, %s>", sr::is_bf16<T>::value ? "__bf16" : "float", ep->colsum ? "true" : "false");
   if (norm) {  // [wgs*4][4][64] -> grads[4][64]
     const int rc = colsum_launch(s, SR_F32, workspace, 256, wgs * 4, 256, grads, 1, 1.f,
                                  workspace + (int64_t)wgs * 4 * 256);

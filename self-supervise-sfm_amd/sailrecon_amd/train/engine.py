@@ -54,6 +54,12 @@ TAIL_ROWS = 64
 # SR_TRAIN_PAIR_WGRAD (default 1; 0 for the A/B): block_bwd_multi's two items share weight-grad
 # launches (ops.gemm_wgrad_pair) where ops.wgrad_pair_splits says it pays
 _PAIR_WGRAD = os.environ.get("SR_TRAIN_PAIR_WGRAD", "1") != "0"
+# SR_TRAIN_BIAS_COLSUM (bits, default 3; 0 for the A/B): bf16 bias grads from the producing pass
+# instead of a column sum that re-reads the gradient: 1 = fc1's from the GELU_BWD dgrad epilogue,
+# 2 = qkv's from sr_qk_bwd
+_BIAS_COLSUM = int(os.environ.get("SR_TRAIN_BIAS_COLSUM", "3"))
+GELU_COLSUM = bool(_BIAS_COLSUM & 1)
+QK_COLSUM = bool(_BIAS_COLSUM & 2)
 
 
 def alloc_tape(rows: int, dim: int, hidden: int, dtype: torch.dtype, device, lse_numel: int,
@@ -285,7 +291,8 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
     # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
     dU = sc.get("dU", R, Hd, dt, dev)
     # bf16: fc1's bias grad from the GELU_BWD epilogue's per-64-row column sums (no re-read of dU)
-    csU = sc.get("dU_colsum", ops.colsum_blocks(R), Hd, torch.float32, dev) if bf and g.b_fc1 is not None else None
+    csU = (sc.get("dU_colsum", ops.colsum_blocks(R), Hd, torch.float32, dev)
+           if bf and g.b_fc1 is not None and GELU_COLSUM else None)
     ops.gemm(a_op, bp.wt_fc2, dU, _lib.SR_EPI_GELU_BWD, aux=tape.u, colsum=csU, tag=tag + ".dgrad")
     wgrad(a_op, tape.h, g.w_fc2, rowscale=pb.g2, wdot=bp.w_fc2 if g.g2 is not None else None,
           rowdot=g.g2 if g.g2 is not None else None)
@@ -311,14 +318,14 @@ def block_bwd(pb: runtime.PackedBlock, bp: BwdPack, g: BlockGrads, tape: BlockTa
     if bf:  # (+ the qkv bias grad from the same pass: no bf16 column sum of draw afterwards)
         draw = sc.get("draw", R, 3 * C, dt, dev)
         ops.qk_bwd(tape.raw if qkv_epi is not None else None, dqkv, draw, qkv_epi or dict(embed_dim=C, head_dim=64),
-                   grads=g.qkn, bias_grad=g.b_qkv)
+                   grads=g.qkn, bias_grad=g.b_qkv if QK_COLSUM else None)
     elif qkv_epi is not None:  # fp32 block (autocast off) with qk-norm / RoPE: in place on dqkv
         ops.qk_bwd(tape.raw, dqkv, dqkv, qkv_epi, grads=g.qkn)
         draw = dqkv
     else:
         draw = dqkv
     ops.gemm(draw, bp.wt_qkv, dxn, _lib.SR_EPI_F32, tag=tag + ".dgrad")
-    wgrad(draw, tape.xn1, g.w_qkv, db=None if bf else g.b_qkv)
+    wgrad(draw, tape.xn1, g.w_qkv, db=None if bf and QK_COLSUM else g.b_qkv)
     ops.layernorm_bwd(tape.x0, dxn, pb.ln1_w, pb.eps, dx, dxb=dxb, dw=g.ln1_w, db=g.ln1_b)
 
 
@@ -376,7 +383,7 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         it["_tmp"] = it["sc"].get("colsum_tmp", 1, max(C, Hd, 3 * C), torch.float32, dev)[0]
         it["_dU"] = it["sc"].get("dU", R, Hd, dt, dev)
         it["_csU"] = (it["sc"].get("dU_colsum", ops.colsum_blocks(R), Hd, torch.float32, dev)
-                      if it["g"].b_fc1 is not None else None)
+                      if it["g"].b_fc1 is not None and GELU_COLSUM else None)
         it["_dxn"] = it["sc"].get("dxn", R, C, torch.float32, dev)
         it["_dO"] = it["sc"].get("dO", R, C, dt, dev)
     # ---- MLP: x2 = x1 + g2 * fc2(GELU(fc1(LN2(x1))))
@@ -388,7 +395,8 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         pb, bp, g = it["pb"], it["bp"], it["g"]
         _resid_param_grads(it["dx"], bp.b_fc2, pb.g2, g.b_fc2, g.g2, it["_tmp"][:C])
     dgrad(_lib.SR_EPI_F32, [dict(a=it["_dU"], w=it["bp"].wt_fc1, out=it["_dxn"]) for it in items])
-    wgrads([(it, it["_dU"], it["tape"].xn2, it["g"].w_fc1, None, None, None, None) for it in items])
+    wgrads([(it, it["_dU"], it["tape"].xn2, it["g"].w_fc1, None if it["_csU"] is not None else it["g"].b_fc1,
+             None, None, None) for it in items])
     for it in items:  # fc1's bias grads from the GELU_BWD epilogue's column sums
         if it["_csU"] is not None:
             ops.colsum(it["_csU"], it["g"].b_fc1, accumulate=True)
@@ -411,9 +419,11 @@ def block_bwd_multi(items, tag: str = "pair") -> None:
         it["_draw"] = it["sc"].get("draw", R, 3 * C, dt, dev)
         qkv_epi = it["qkv_epi"]
         ops.qk_bwd(it["tape"].raw if qkv_epi is not None else None, dqkv, it["_draw"],
-                   qkv_epi or dict(embed_dim=C, head_dim=64), grads=it["g"].qkn, bias_grad=it["g"].b_qkv)
+                   qkv_epi or dict(embed_dim=C, head_dim=64), grads=it["g"].qkn,
+                   bias_grad=it["g"].b_qkv if QK_COLSUM else None)
     dgrad(_lib.SR_EPI_F32, [dict(a=it["_draw"], w=it["bp"].wt_qkv, out=it["_dxn"]) for it in items])
-    wgrads([(it, it["_draw"], it["tape"].xn1, it["g"].w_qkv, None, None, None, None) for it in items])
+    wgrads([(it, it["_draw"], it["tape"].xn1, it["g"].w_qkv, None if QK_COLSUM else it["g"].b_qkv, None, None, None)
+            for it in items])
     for it in items:
         pb, g = it["pb"], it["g"]
         ops.layernorm_bwd(it["tape"].x0, it["_dxn"], pb.ln1_w, pb.eps, it["dx"], dxb=it["dxb"], dw=g.ln1_w,

@@ -498,12 +498,14 @@ class TrainGraph:
             kv_raw = self._buf(f"kv_raw{l}", n_sub, 2 * C, cdt) if epi is not None else None
             if bf or epi is not None:  # fp32 without qk-norm / RoPE: dkv_raw is dkv_sub
                 ops.qk_bwd(kv_raw, dkv_sub, dkv_raw, epi or dict(embed_dim=C, head_dim=64, col_offset=C), grads=gr.qkn,
-                           bias_grad=_sl(gr.b_qkv, C, 3 * C) if bf else None)
+                           bias_grad=_sl(gr.b_qkv, C, 3 * C) if bf and engine.QK_COLSUM else None)
             bp = self._bwd_pack(br, cdt)
             ops.gemm(dkv_raw, bp.wt_qkv[:, C:], dxn_sub, _lib.SR_EPI_F32, tag="reloc.dgrad")
             xn_sub = self._buf(f"xn_sub{l}", n_sub, C, cdt)
             if bf:  # (the k|v bias grad came out of qk_bwd)
                 ops.gemm_wgrad(dkv_raw, xn_sub, gr.w_qkv[C:], accumulate=True, tag="reloc.wgrad")
+                if not engine.QK_COLSUM:
+                    ops.colsum(dkv_raw, _sl(gr.b_qkv, C, 3 * C), accumulate=True)
             else:
                 ops.wgrad_small(dkv_raw, xn_sub, gr.w_qkv[C:], db=_sl(gr.b_qkv, C, 3 * C), accumulate=True)
             ops.layernorm_bwd(tg.x0, dxn_sub, pr.ln1_w, pr.eps, dx, rowmap=rowmap[l], rows=n_sub,

@@ -139,3 +139,37 @@ def test_train_graph_matches_autograd(lists, px):
     med = sorted(errs.values())[len(errs) // 2]
     assert med < 2e-2, f"median grad rel-L2 {med}"
     assert worst[0][1] < 4e-2, worst
+
+
+def test_train_graph_bias_colsum_modes(monkeypatch):
+    """SR_TRAIN_BIAS_COLSUM: the bf16 bias grads of fc1 (GELU_BWD epilogue column sums) and of qkv
+    (sr_qk_bwd's) against the separate column sums of dU / d(q|k|v) they replace -- the same
+    bf16-rounded addends summed in another order (~1e-6); every other gradient bit-identical."""
+    from sailrecon_amd.train import engine
+    from sailrecon_amd.train.model import TrainGraph
+    from sailrecon_amd.utils.synth_weights import synth_state_dict_like
+    grads = []
+    for mode in (3, 0):
+        monkeypatch.setattr(engine, "GELU_COLSUM", bool(mode & 1))
+        monkeypatch.setattr(engine, "QK_COLSUM", bool(mode & 2))
+        torch.manual_seed(0)
+        m = Hot()
+        m.load_state_dict(synth_state_dict_like(m))
+        m = m.to(DEV)
+        tg = TrainGraph(m)
+        x = torch.rand(2, 3, 56, 56, generator=torch.Generator().manual_seed(1))
+        m.aggregator.generator.manual_seed(0)
+        tg.forward(torch.cat([x, x])[None].to(DEV), [0, 1], [2, 3], fix_rank=10)
+        tg.flat.zero_grad()
+        tg.backward(torch.randn(1, 2, 9, generator=torch.Generator().manual_seed(2)).to(DEV))
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters() if p.requires_grad})
+    fused, plain = grads
+    n_bias = 0
+    for name, g in fused.items():
+        if name.endswith(("fc1.bias", "qkv.bias")) and "aggregator" in name:
+            n_bias += 1
+            assert rel(g, plain[name]) < 1e-4, name
+        else:
+            assert torch.equal(g, plain[name]), name
+    assert n_bias > 0

@@ -676,6 +676,38 @@ def attn_bwd():
                   flush=True)
 
 
+def qk_bwd():
+    """sr_qk_bwd at the C4 frame block's shape (43,968 rows, q|k|v 3,072 columns, qk-norm + RoPE):
+    plain, plain + the bf16 column sum of its output (the qkv bias grad, as before round 6), and
+    with the column sum from the same pass (bias_grad)."""
+    from sailrecon_amd.layers.rope import RotaryPositionEmbedding2D
+    R, C, D = 32 * 1374, 1024, 64
+    g = torch.Generator(device=DEV).manual_seed(3)
+    raw = torch.randn(R, 3 * C, device=DEV, generator=g).bfloat16()
+    dsrc = torch.randn(R, 3 * C, device=DEV, generator=g)
+    out = torch.empty(R, 3 * C, device=DEV, dtype=torch.bfloat16)
+    rope = RotaryPositionEmbedding2D(100).tables(D, 37, DEV)
+    epi = dict(embed_dim=C, head_dim=D, qk_eps=1e-6, qn_w=torch.randn(D, device=DEV), qn_b=torch.randn(D, device=DEV),
+               kn_w=torch.randn(D, device=DEV), kn_b=torch.randn(D, device=DEV), rope_cos=rope[0], rope_sin=rope[1],
+               tokens_per_frame=1374, patch_start=5, grid_w=37, pos_row_base=0)
+    grads = torch.zeros(4, 64, device=DEV)
+    bg = torch.zeros(3 * C, device=DEV)
+
+    def plain():
+        ops.qk_bwd(raw, dsrc, out, epi, grads=grads)
+
+    def plain_cs():
+        ops.qk_bwd(raw, dsrc, out, epi, grads=grads)
+        ops.colsum(out, bg, accumulate=True)
+
+    def fused():
+        ops.qk_bwd(raw, dsrc, out, epi, grads=grads, bias_grad=bg)
+    for i in range(2):
+        tp, tc, tf = timeit(plain, reps=20), timeit(plain_cs, reps=20), timeit(fused, reps=20)
+        print(f"qk_bwd C4 frame rows: plain {tp * 1e3:.1f} us, plain + colsum {tc * 1e3:.1f} us, "
+              f"fused colsum {tf * 1e3:.1f} us", flush=True)
+
+
 def train():
     """BASELINE config 4 (train_imc.py step, 16-view batches): full-size SailRecon aggregator +
     camera head (DPT heads off: no loss reaches them), seeded synthetic weights, a synthetic
