@@ -39,6 +39,22 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
+// Sum over the 16 lanes of a DPP row, left in every lane of the row (quad swaps, then the half-row
+// and row mirrors; every lane adds the same two values at each step, so all 16 hold the same bits).
+__device__ __forceinline__ float dpp_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+// The value of lane l ^ 4 (within a DPP row): row_half_mirror (l -> 7 - l in each half row), then
+// quad_perm 3,2,1,0 (l -> 3 - l in each quad) -- two DPP moves, no LDS permute.
+__device__ __forceinline__ float dpp_xor4(float v) {
+  const int m = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false);
+  return __int_as_float(__builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
 
 // erf-GELU for bf16 outputs: erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below

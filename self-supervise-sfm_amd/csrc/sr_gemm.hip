@@ -103,13 +103,6 @@ constexpr int ROPE_LDS_POS = ROPE_LDS / 2 / 64;
 // colw + 16 ni + 4 lg + r summed over its rows; the 16 lanes lr of a 16-lane DPP row share those
 // columns, so four DPP adds (quad swaps, half-row and row mirrors) leave the block's sums in every
 // lane and lane lr = 0 stores them: ep.colsum[(row block) * N + col].
-__device__ __forceinline__ float dpp_sum16(float v) {
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
-}
 template <int MT>
 __device__ __forceinline__ void colsum_store(const GemmArgs& g, float (&cs)[MT / 4][4][4], int rowbase, int colw,
                                              int lr, int lg) {
@@ -118,7 +111,7 @@ __device__ __forceinline__ void colsum_store(const GemmArgs& g, float (&cs)[MT /
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cs[i][ni][r] = dpp_sum16(cs[i][ni][r]);
+      for (int r = 0; r < 4; ++r) cs[i][ni][r] = sr::dpp_sum16(cs[i][ni][r]);
     const int rb = rowbase + i * 64;
     if (lr == 0 && rb < g.M) {
 #pragma unroll

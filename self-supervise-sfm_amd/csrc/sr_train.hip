@@ -651,25 +651,21 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
         if (rope) {  // inverse rotation: first a: da = c dA + s dB; second b: db = c dB - s dA
           float pd[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) pd[e] = __shfl_xor(d[e], 4, 64);
+          for (int e = 0; e < 4; ++e) pd[e] = sr::dpp_xor4(d[e]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) d[e] = first ? fmaf(cs[e], d[e], sn[e] * pd[e]) : fmaf(cs[e], d[e], -sn[e] * pd[e]);
         }
         if (norm) {
           const f32x4 r4 = r4s[p];
           float v[4] = {r4[0], r4[1], r4[2], r4[3]};
-          float s = (v[0] + v[1]) + (v[2] + v[3]);
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-          const float mean = s * (1.f / 64.f);
+          const float mean = sr::dpp_sum16((v[0] + v[1]) + (v[2] + v[3])) * (1.f / 64.f);
           float s2 = 0.f;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v[e] -= mean;
             s2 += v[e] * v[e];
           }
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+          s2 = sr::dpp_sum16(s2);
           const float rstd = rsqrtf(s2 * (1.f / 64.f) + ep.qk_eps);
           float wv[4];  // selected per element: a pointer / index select here demoted the arrays to scratch
 #pragma unroll
@@ -692,11 +688,8 @@ __global__ __launch_bounds__(256) void qk_bwd_kernel(const T* __restrict__ raw, 
             sg += g[e];
             sgx += g[e] * v[e];
           }
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            sg += __shfl_xor(sg, o, 64);
-            sgx += __shfl_xor(sgx, o, 64);
-          }
+          sg = sr::dpp_sum16(sg);
+          sgx = sr::dpp_sum16(sgx);
           sg *= 1.f / 64.f;
           sgx *= 1.f / 64.f;
 #pragma unroll

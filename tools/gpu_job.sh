@@ -154,8 +154,9 @@ for step in "$@"; do
     kpair)   run kpair 300 python tools/kbench.py attn_pair ;;
     kqk)     run kqk 300 python tools/kbench.py qk_bwd ;;
     train_ab) for i in 1 2; do
-                run ktrain_cs0_$i 600 env SR_TRAIN_BIAS_COLSUM=0 python tools/kbench.py train || exit 1
-                run ktrain_cs3_$i 600 env SR_TRAIN_BIAS_COLSUM=3 python tools/kbench.py train || exit 1
+                for m in ${TRAIN_AB_MODES:-0 3}; do
+                  run ktrain_cs${m}_$i 600 env SR_TRAIN_BIAS_COLSUM=$m python tools/kbench.py train || exit 1
+                done
               done ;;
     pmc_pair) run pmc_pair1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_pair1 -o run --output-format csv -- python3 tools/kbench.py attn_pair && \
               run pmc_pair2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_pair2 -o run --output-format csv -- python3 tools/kbench.py attn_pair && \
