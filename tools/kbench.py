@@ -760,6 +760,11 @@ def train():
               f"{r['tflops']:7.1f} TF/s")
     print(f"train: {n} views ({2 * n} frames @518) {ms:.1f} ms/step = {n / ms * 1e3:.2f} views/s "
           f"({1e3 / ms:.3f} steps/s); timed kernels {tot:.1f} ms; loss {out['loss']:.5f}", flush=True)
+    # the box's calibration GEMM (bench.py box_calibration), so that steps from different boxes compare
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import box_calibration
+    cal = box_calibration(torch.device(DEV))
+    print(f"train: box calibration {cal['tflops']} TF/s ({cal['kernel']}, {cal['shape']})", flush=True)
 
 
 if __name__ == "__main__":
