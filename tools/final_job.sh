@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # final validation of a round (tools/final_job.sh A|B|C|D).  A = every GPU test but the multi-rank ones, B = the multi-rank tests +
 # smoke, C = default bench (cpu baseline, extras) + rocprofv3 kernel stats (1 and 3 steps: the
-# steady-state counts) + FETCH_SIZE / WRITE_SIZE PMC passes, D = training kernel stats.
+# steady-state counts) + FETCH_SIZE / WRITE_SIZE PMC passes, D = training kernel stats + an unprofiled training step, E = the per-rank rehearsal (tools/rank_sim.py).
 set -u
 mkdir -p gpurun_out
 run() {  # name seconds cmd...
@@ -25,6 +25,8 @@ case ${1:-} in
      run f_prof_s3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/f_prof_s3 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 $NB
      run f_pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/f_pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 $NB
      run f_pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/f_pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 $NB ;;
-  D) run f_prof_train 500 rocprofv3 --kernel-trace --stats -d gpurun_out/f_prof_train -o run --output-format csv -- python3 tools/kbench.py train ;;
-  *) echo "usage: $0 A|B|C|D"; exit 2 ;;
+  D) run f_prof_train 500 rocprofv3 --kernel-trace --stats -d gpurun_out/f_prof_train -o run --output-format csv -- python3 tools/kbench.py train
+     run f_ktrain 500 python tools/kbench.py train ;;
+  E) run f_rank_sim 900 python tools/rank_sim.py --worlds 1,2,4,8 --steps 5 ;;
+  *) echo "usage: $0 A|B|C|D|E"; exit 2 ;;
 esac
