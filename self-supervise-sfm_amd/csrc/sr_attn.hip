@@ -1799,7 +1799,7 @@ static int attention_pair(hipStream_t s, int dtype, const sr_attn_desc* d0, cons
     sr::note_kernel("attn_bf16_pair_kernel<2, true>");
   } else {
     hipLaunchKernelGGL((attn_bf16_pair_kernel<2>), dim3(grid), dim3(256), 0, s, p);
-    sr::note_kernel("attn_bf16_pair_kernel<2>");
+    sr::note_kernel("attn_bf16_pair_kernel<2, false>");  // (rocprofv3 spells the defaulted argument)
   }
   return sr::check_launch("sr_attention_pair");
 }
