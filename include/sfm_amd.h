@@ -570,6 +570,15 @@ typedef struct sr_weight_item {
   int64_t ldt;
 } sr_weight_item;
 int sr_weight_refresh_bf16(sr_stream_t stream, int n, const sr_weight_item* items);
+/* The whole model's refresh in ONE launch (ABI 1.5): the caller keeps `n` items and their tile
+ * prefix in DEVICE memory (static across steps: the flat parameter buffer and the packs do not
+ * move).  sr_weight_refresh_plan validates a host copy of the items exactly as
+ * sr_weight_refresh_bf16 does and fills start[0..n] (n + 1 ints; start[n] = the launch's tiles);
+ * upload both, then sr_weight_refresh_list_bf16(stream, n, items_dev, start_dev, start[n]) per
+ * step.  Per item the same tiles and values as sr_weight_refresh_bf16. */
+int sr_weight_refresh_plan(int n, const sr_weight_item* items, int* start);
+int sr_weight_refresh_list_bf16(sr_stream_t stream, int n, const sr_weight_item* items_dev, const int* start_dev,
+                                int tiles);
 
 /* dst[c][r] = out_dtype(rowscale[r] * src[r][c])  (fp32 src [rows][lds]; W^T packs of the dgrad
  * GEMMs with LayerScale gamma folded into W's rows; rowscale may be NULL) */

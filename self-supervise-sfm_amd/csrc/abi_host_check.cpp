@@ -319,6 +319,19 @@ void check() {
   wi.trans = fake(2);
   wi.ldt = 3072;
   expect("sr_weight_refresh_bf16", sr_weight_refresh_bf16(nullptr, 1, &wi), true);
+  {
+    sr_weight_item two[2] = {wi, wi};
+    int start[3] = {-1, -1, -1};
+    const int rc = sr_weight_refresh_plan(2, two, start);  // host-only: SR_OK
+    const bool ok = rc == SR_OK && start[0] == 0 && start[1] == 768 && start[2] == 1536;
+    std::printf("%-44s rc=%d  %sprefix %d %d %d\n", "sr_weight_refresh_plan", rc, ok ? "" : "UNEXPECTED  ", start[0],
+                start[1], start[2]);
+    if (!ok) ++g_fail;
+    two[1].trans = nullptr;
+    two[1].cast = nullptr;
+    expect("sr_weight_refresh_plan no outputs", sr_weight_refresh_plan(2, two, start), false);
+    expect("sr_weight_refresh_list_bf16 empty", sr_weight_refresh_list_bf16(nullptr, 0, nullptr, nullptr, 0), false);
+  }
   expect("sr_im2col_normalize null", sr_im2col_normalize(nullptr, SR_BF16, nullptr, 0, 518, 518, 14, nullptr, nullptr, nullptr, 0), false);
 }
 

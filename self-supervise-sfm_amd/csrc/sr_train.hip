@@ -1313,13 +1313,10 @@ struct WeightRefresh {
   int n;
 };
 
-__global__ __launch_bounds__(256) void weight_refresh_kernel(WeightRefresh wr) {
-  __shared__ float tile[64][65];
-  int p = 0;
-#pragma unroll
-  for (int i = 1; i < SR_WEIGHT_REFRESH_MAX; ++i) p += (i < wr.n && (int)blockIdx.x >= wr.start[i]) ? 1 : 0;
-  const sr_weight_item& w = wr.it[p];
-  const int t = blockIdx.x - wr.start[p], ntc = (w.cols + 63) / 64;
+// One 64 x 64 tile t of weight w: read once, written as the bf16 cast and / or the rowscaled bf16
+// transpose.
+__device__ __forceinline__ void refresh_tile(const sr_weight_item& w, int t, float (*tile)[65]) {
+  const int ntc = (w.cols + 63) / 64;
   const int r0 = (t / ntc) * 64, c0 = (t % ntc) * 64;
   // whole tile with 16-B source rows and 8-B bf16 destination rows (the aggregator's weights):
   // float4 loads, bf16x4 stores of the cast and of the transpose (same values as the scalar path)
@@ -1368,6 +1365,30 @@ __global__ __launch_bounds__(256) void weight_refresh_kernel(WeightRefresh wr) {
   }
 }
 
+__global__ __launch_bounds__(256) void weight_refresh_kernel(WeightRefresh wr) {
+  __shared__ float tile[64][65];
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < SR_WEIGHT_REFRESH_MAX; ++i) p += (i < wr.n && (int)blockIdx.x >= wr.start[i]) ? 1 : 0;
+  refresh_tile(wr.it[p], blockIdx.x - wr.start[p], tile);
+}
+
+// sr_weight_refresh_list_bf16: every item of a device-resident table in ONE launch (the whole model's
+// per-step refresh); workgroup -> item by a binary search of the tile-count prefix start[0..n].
+__global__ __launch_bounds__(256) void weight_refresh_list_kernel(const sr_weight_item* __restrict__ items,
+                                                                  const int* __restrict__ start, int n) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;  // the last item whose start <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (start[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const sr_weight_item w = items[lo];
+  refresh_tile(w, b - start[lo], tile);
+}
+
 extern "C" int sr_weight_refresh_bf16(sr_stream_t stream, int n, const sr_weight_item* items) {
   SR_CHECK(items && n > 0 && n <= SR_WEIGHT_REFRESH_MAX, SR_EINVAL, "sr_weight_refresh_bf16: 1..%d items (got %d)",
            SR_WEIGHT_REFRESH_MAX, n);
@@ -1387,6 +1408,33 @@ extern "C" int sr_weight_refresh_bf16(sr_stream_t stream, int n, const sr_weight
   hipLaunchKernelGGL(weight_refresh_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, wr);
   sr::note_kernel("weight_refresh_kernel");
   return sr::check_launch("sr_weight_refresh_bf16");
+}
+
+extern "C" int sr_weight_refresh_plan(int n, const sr_weight_item* items, int* start) {
+  SR_CHECK(items && start && n > 0, SR_EINVAL, "sr_weight_refresh_plan: null items / start or n <= 0");
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const sr_weight_item& w = items[i];
+    SR_CHECK(w.src && w.rows > 0 && w.cols > 0 && w.lds >= w.cols && (w.cast || w.trans) &&
+                 (!w.cast || w.ldc >= w.cols) && (!w.trans || w.ldt >= w.rows),
+             SR_EINVAL, "sr_weight_refresh_plan: item %d: bad shape / pointers", i);
+    start[i] = tiles;
+    const int64_t t = (int64_t)tiles + (int64_t)((w.rows + 63) / 64) * ((w.cols + 63) / 64);
+    SR_CHECK(t < (1ll << 31), SR_EINVAL, "sr_weight_refresh_plan: too many tiles");
+    tiles = (int)t;
+  }
+  start[n] = tiles;
+  return SR_OK;
+}
+
+extern "C" int sr_weight_refresh_list_bf16(sr_stream_t stream, int n, const sr_weight_item* items_dev,
+                                           const int* start_dev, int tiles) {
+  SR_CHECK(items_dev && start_dev && n > 0 && tiles > 0, SR_EINVAL,
+           "sr_weight_refresh_list_bf16: null table or empty plan");
+  hipLaunchKernelGGL(weight_refresh_list_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, items_dev, start_dev,
+                     n);
+  sr::note_kernel("weight_refresh_list_kernel");
+  return sr::check_launch("sr_weight_refresh_list_bf16");
 }
 
 extern "C" int sr_transpose_f32(sr_stream_t stream, int out_dtype, const float* src, int64_t lds, int rows, int cols,

@@ -190,6 +190,8 @@ _PROTOS = {
     "sr_qk_bwd_f32": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, ctypes.POINTER(GemmEpi), _vp, _vp]),
     "sr_cast_bf16": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _f32]),
     "sr_weight_refresh_bf16": (_i32, [_vp, _i32, _vp]),
+    "sr_weight_refresh_plan": (_i32, [_i32, _vp, _vp]),
+    "sr_weight_refresh_list_bf16": (_i32, [_vp, _i32, _vp, _vp, _i32]),
     "sr_nonfinite_check": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "sr_adam_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _vp, _vp]),
     "sr_transpose_f32": (_i32, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i64]),

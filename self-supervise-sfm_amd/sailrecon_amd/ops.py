@@ -1311,12 +1311,7 @@ def adam(p: Tensor, g: Tensor, m: Tensor, v: Tensor, *, lr: float, beta1: float,
                                   weight_decay, step, _p(scale), _p(found_inf)), "sr_adam_f32")
 
 
-def weight_refresh(items) -> None:
-    """Up to 4 fp32 weights in one launch (sr_weight_refresh_bf16): ``items`` = (src fp32 [R, C],
-    cast bf16 [R, C] or None, trans bf16 [C, R] or None, rowscale fp32 [R] or None) -- the bf16
-    forward operand and the rowscaled transposed dgrad operand from one read of each weight."""
-    if not 0 < len(items) <= _lib.SR_WEIGHT_REFRESH_MAX:
-        raise ValueError("weight_refresh: 1..4 items")
+def _weight_items(items):
     arr = (_lib.WeightItem * len(items))()
     for it, (src, cast, trans, rowscale) in zip(arr, items):
         R, C = src.shape
@@ -1329,7 +1324,36 @@ def weight_refresh(items) -> None:
         it.rowscale = None if rowscale is None else rowscale.data_ptr()
         it.cast, it.ldc = (None, 0) if cast is None else (cast.data_ptr(), _rowmajor(cast, "cast"))
         it.trans, it.ldt = (None, 0) if trans is None else (trans.data_ptr(), _rowmajor(trans, "trans"))
+    return arr
+
+
+def weight_refresh(items) -> None:
+    """Up to 4 fp32 weights in one launch (sr_weight_refresh_bf16): ``items`` = (src fp32 [R, C],
+    cast bf16 [R, C] or None, trans bf16 [C, R] or None, rowscale fp32 [R] or None) -- the bf16
+    forward operand and the rowscaled transposed dgrad operand from one read of each weight."""
+    if not 0 < len(items) <= _lib.SR_WEIGHT_REFRESH_MAX:
+        raise ValueError("weight_refresh: 1..4 items")
+    arr = _weight_items(items)
     check(_lib.load().sr_weight_refresh_bf16(_stream(items[0][0]), len(items), arr), "sr_weight_refresh_bf16")
+
+
+def weight_refresh_table(items, device) -> dict:
+    """The device-resident table of sr_weight_refresh_list_bf16 for any number of weight_refresh
+    items (validated by sr_weight_refresh_plan); the tensors' addresses must stay put while it is used."""
+    if not items:
+        raise ValueError("weight_refresh_table: no items")
+    arr = _weight_items(items)
+    start = (ctypes.c_int * (len(items) + 1))()
+    check(_lib.load().sr_weight_refresh_plan(len(items), arr, start), "sr_weight_refresh_plan")
+    raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return dict(n=len(items), tiles=int(start[len(items)]), items=raw.to(device),
+                start=torch.tensor(list(start), dtype=torch.int32).to(device))
+
+
+def weight_refresh_list(table: dict) -> None:
+    """Every item of a weight_refresh_table in ONE launch (sr_weight_refresh_list_bf16)."""
+    check(_lib.load().sr_weight_refresh_list_bf16(_stream(table["items"]), table["n"], _p(table["items"]),
+                                                  _p(table["start"]), table["tiles"]), "sr_weight_refresh_list_bf16")
 
 
 def transpose(src: Tensor, dst: Tensor, rowscale: Optional[Tensor] = None) -> None:

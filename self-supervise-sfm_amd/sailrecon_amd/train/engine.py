@@ -220,16 +220,20 @@ def pack_bwd(blk, pb: runtime.PackedBlock, dtype: torch.dtype, into: Optional[Bw
     return into
 
 
-def refresh_block_bf16(blk, pb: runtime.PackedBlock, into: BwdPack) -> None:
-    """After an optimizer step, one launch per block (sr_weight_refresh_bf16): the four bf16
-    forward weights of the packed block (casts in place) and the four transposed dgrad packs of
-    pack_bwd (LayerScale gammas folded into proj / fc2), each fp32 weight read once."""
+def refresh_items_bf16(blk, pb: runtime.PackedBlock, into: BwdPack) -> list:
+    """The block's four weight_refresh items: the bf16 forward weights of the packed block (casts in
+    place) and the transposed dgrad packs of pack_bwd (LayerScale gammas folded into proj / fc2)."""
     a = blk.attn
     f = lambda t: t.detach()  # noqa: E731
-    ops.weight_refresh([(f(a.qkv.weight), pb.w_qkv, into.wt_qkv, None),
-                        (f(a.proj.weight), pb.w_proj, into.wt_proj, pb.g1),
-                        (f(blk.mlp.fc1.weight), pb.w_fc1, into.wt_fc1, None),
-                        (f(blk.mlp.fc2.weight), pb.w_fc2, into.wt_fc2, pb.g2)])
+    return [(f(a.qkv.weight), pb.w_qkv, into.wt_qkv, None),
+            (f(a.proj.weight), pb.w_proj, into.wt_proj, pb.g1),
+            (f(blk.mlp.fc1.weight), pb.w_fc1, into.wt_fc1, None),
+            (f(blk.mlp.fc2.weight), pb.w_fc2, into.wt_fc2, pb.g2)]
+
+
+def refresh_block_bf16(blk, pb: runtime.PackedBlock, into: BwdPack) -> None:
+    """After an optimizer step, one launch per block (sr_weight_refresh_bf16), each fp32 weight read once."""
+    ops.weight_refresh(refresh_items_bf16(blk, pb, into))
 
 
 class BwdScratch:

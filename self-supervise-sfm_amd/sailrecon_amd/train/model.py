@@ -85,19 +85,28 @@ class TrainGraph:
         if hasattr(pe, "_pos_cache"):
             pe._pos_cache = {}
         self._bwd: Dict[int, engine.BwdPack] = {}
+        self._refresh_table = None  # (block keys, ops.weight_refresh_table) of refresh_packs
         self._packs_fresh = False
 
     def refresh_packs(self) -> None:
         """After an optimizer step: recast the bf16 forward weights in place (fp32 biases, gammas
         and norms alias the flat parameter buffer) and rebuild the transposed backward packs."""
-        # bf16 blocks with a backward pack: casts and transposed packs in one launch per block
-        fused = set()
-        for key in list(self._bwd):
-            blk, dt = self._bwd_src[key]
-            pb = blk._packed.get(BF16)
-            if dt == BF16 and pb is not None:
-                engine.refresh_block_bf16(blk, pb, self._bwd[key])
-                fused.add(id(blk))
+        # bf16 blocks with a backward pack: every block's casts and transposed packs in ONE launch
+        # (sr_weight_refresh_list_bf16 over a device table built once: the packs and the flat
+        # parameter buffer do not move; one launch per block left the GPU waiting on the host)
+        # (keyed on the pack objects, which the table's item list keeps alive: a re-created pack
+        # rebuilds the table instead of refreshing a stale copy)
+        blocks = [(self._bwd_src[k][0], self._bwd[k]) for k in self._bwd
+                  if self._bwd_src[k][1] == BF16 and self._bwd_src[k][0]._packed.get(BF16) is not None]
+        keys = tuple((id(blk), id(blk._packed[BF16]), id(into)) for blk, into in blocks)
+        fused = {id(blk) for blk, _ in blocks}
+        if keys:
+            if self._refresh_table is None or self._refresh_table[0] != keys:
+                items = []
+                for blk, into in blocks:
+                    items += engine.refresh_items_bf16(blk, blk._packed[BF16], into)
+                self._refresh_table = (keys, ops.weight_refresh_table(items, self.dev), items)
+            ops.weight_refresh_list(self._refresh_table[1])
         for blk in self._agg_blocks():
             pb = blk._packed.get(BF16)
             if pb is not None and id(blk) not in fused:

@@ -441,3 +441,25 @@ def test_weight_refresh(ops):
     ops.weight_refresh([(srcs[0], c1, None, None), (srcs[1], None, t1, scales[1])])
     torch.cuda.synchronize()
     assert torch.equal(c1, casts[0]) and torch.equal(t1, trans[1])
+    # the whole-model form (sr_weight_refresh_list_bf16): 9 items over a device table, one launch,
+    # the same bits per item; re-run after the sources change (the table is reused)
+    items = [(src, torch.empty_like(c), torch.empty_like(t), sc) for src, c, t, sc in zip(srcs, casts, trans, scales)]
+    items = items + items[:2] + [(srcs[2], torch.empty_like(casts[2]), None, None)] * 2 + \
+        [(srcs[3], None, torch.empty_like(trans[3]), scales[3])]
+    table = ops.weight_refresh_table(items, DEV)
+    for rnd in range(2):
+        if rnd:
+            for src in srcs:
+                src.mul_(-0.5)
+        ops.weight_refresh_list(table)
+        for src, cast, tr, sc in items:
+            if cast is not None:
+                c0 = torch.empty_like(cast)
+                ops.cast_bf16(src, c0)
+                torch.cuda.synchronize()
+                assert torch.equal(cast, c0)
+            if tr is not None:
+                t0 = torch.empty_like(tr)
+                ops.transpose(src, t0, rowscale=sc)
+                torch.cuda.synchronize()
+                assert torch.equal(tr, t0)
