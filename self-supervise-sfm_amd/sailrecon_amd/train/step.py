@@ -134,13 +134,19 @@ class Trainer:
     # ------------------------------------------------------------------ the step
     def step(self, images: Tensor, no_reloc_list: List[int], reloc_list: List[int], batch: dict,
              fix_rank: int = 300) -> Dict[str, float]:
+        # the loss's batch tensors go to the device first, while the stream is idle: a host tensor's
+        # copy blocks the host until the stream reaches it, so in the middle of the step it stalled the
+        # launch queue behind the whole forward (imc_loss converts the same way; no-ops afterwards)
+        dev = images.device
+        lb = {k: batch[k].to(device=dev, dtype=torch.int32 if k in ("src_idx", "dst_idx") else torch.float32).contiguous()
+              for k in ("K_prime_to_K", "src_idx", "dst_idx", "src_coords", "dst_coords", "src_depth", "dst_depth")}
         self.opt.zero_grad()
         self._works, self._reduced = [], {}
         pose = self.graph.forward(images, no_reloc_list, reloc_list, fix_rank=fix_rank)
         H, W = images.shape[-2], images.shape[-1]
-        loss, d_enc = imc_loss(pose[0], (H, W), batch["K_prime_to_K"], bool(batch["shared_focal"]), batch["src_idx"],
-                               batch["dst_idx"], batch["src_coords"], batch["dst_coords"], batch["src_depth"],
-                               batch["dst_depth"], self.cdf, grad_scale=self.scaler.get_scale())
+        loss, d_enc = imc_loss(pose[0], (H, W), lb["K_prime_to_K"], bool(batch["shared_focal"]), lb["src_idx"],
+                               lb["dst_idx"], lb["src_coords"], lb["dst_coords"], lb["src_depth"],
+                               lb["dst_depth"], self.cdf, grad_scale=self.scaler.get_scale())
         self.graph.backward(d_enc[None])
         for w in self._works:
             w.wait()
