@@ -61,20 +61,27 @@ class GradScaler:
                               torch.zeros(1, device=device, dtype=torch.int32))
         return self._dev[key]
 
-    def step(self, optimizer: Adam, world_size: int = 1) -> bool:
+    def step(self, optimizer: Adam, world_size: int = 1, before_sync=None) -> bool:
         """unscale (by scale * world_size: DDP's mean), check, step unless inf; returns found_inf
-        (reads one int back: the reference reads loss.item() every step anyway)."""
+        (reads one int back: the reference reads loss.item() every step anyway).  ``before_sync``:
+        called after the update is queued and before that read, so that its launches (the weight
+        refresh) keep the GPU busy while the host waits (a skipped update leaves the weights, so
+        work derived from them comes out the same)."""
         dev = optimizer.flat.grad.device
         scale_t, found = self._buffers(dev)
         scale_t.fill_(self._scale * world_size)
         if not self.enabled:
             # a disabled torch GradScaler steps unconditionally: no inf/NaN check, no skip
             optimizer.step(scale=scale_t, found_inf=None)
+            if before_sync is not None:
+                before_sync()
             self._found = False
             return False
         found.zero_()
         ops.nonfinite_check(optimizer.flat.grad, found, scale_t)
         optimizer.step(scale=scale_t, found_inf=found)
+        if before_sync is not None:
+            before_sync()
         self._found = bool(found.item())
         if self._found:
             optimizer.step_count -= 1  # torch.optim.Adam's state step does not advance on a skipped step

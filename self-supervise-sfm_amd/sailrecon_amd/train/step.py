@@ -151,10 +151,10 @@ class Trainer:
         for w in self._works:
             w.wait()
         self._works = []
-        found = self.scaler.step(self.opt, world_size=self.world)
+        # the bf16 / transposed weight packs are refreshed from the (possibly unchanged, if the update
+        # was skipped) fp32 weights before the host reads found_inf back
+        found = self.scaler.step(self.opt, world_size=self.world, before_sync=self.graph.refresh_packs)
         self.scaler.update()
-        if not found:
-            self.graph.refresh_packs()
         lr = self.sched.step()
         self.steps_done += 1
         return {"loss": float(loss.item()), "lr": lr, "skipped": found}
