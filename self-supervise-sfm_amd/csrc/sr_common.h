@@ -120,9 +120,12 @@ __device__ __forceinline__ float sum_x32(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// wave64 reductions.  wave_sum: the 16-lane DPP row sums, then the row-swap permutes (all VALU: no
-// ds_bpermute LDS round trips on the row's critical path); every lane ends with the same bits.
-__device__ __forceinline__ float wave_sum(float v) { return sum_x32(sum_x16(dpp_sum16(v))); }
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
