@@ -153,6 +153,12 @@ for step in "$@"; do
                --timeout 300 --timeout-method thread ;;
     kpair)   run kpair 300 python tools/kbench.py attn_pair ;;
     kqk)     run kqk 300 python tools/kbench.py qk_bwd ;;
+    lib_ab)  for i in 1 2; do  # the committed build against ablib/libsfm_${AB_NAME}.so (an earlier build)
+               run kln_${AB_NAME}_$i 300 env SFM_AMD_LIB=ablib/libsfm_${AB_NAME}.so python tools/kbench.py ln || exit 1
+               run kln_new_$i 300 python tools/kbench.py ln || exit 1
+               run bench_${AB_NAME}_$i 400 env SFM_AMD_LIB=ablib/libsfm_${AB_NAME}.so python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
+               run bench_new_$i 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
+             done ;;
     train_ab) for i in 1 2; do
                 for m in ${TRAIN_AB_MODES:-0 3}; do
                   run ktrain_cs${m}_$i 600 env SR_TRAIN_BIAS_COLSUM=$m python tools/kbench.py train || exit 1
