@@ -153,6 +153,11 @@ for step in "$@"; do
                --timeout 300 --timeout-method thread ;;
     kpair)   run kpair 300 python tools/kbench.py attn_pair ;;
     kqk)     run kqk 300 python tools/kbench.py qk_bwd ;;
+    resid_modes) for i in 1 2; do  # proj -> LN2 fusion (SR_FUSED_RESID_LN) x fc2 -> next LN1 (SR_DEFER_RESID)
+                   for m in 00 10 01 11; do
+                     run bench_rm${m}_$i 400 env SR_FUSED_RESID_LN=${m:0:1} SR_DEFER_RESID=${m:1:1} python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
+                   done
+                 done ;;
     lib_ab)  for i in 1 2; do  # the committed build against ablib/libsfm_${AB_NAME}.so (an earlier build)
                run kln_${AB_NAME}_$i 300 env SFM_AMD_LIB=ablib/libsfm_${AB_NAME}.so python tools/kbench.py ln || exit 1
                run kln_new_$i 300 python tools/kbench.py ln || exit 1
