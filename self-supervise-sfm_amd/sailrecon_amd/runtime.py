@@ -243,8 +243,13 @@ def qkv_gemm(pb: PackedBlock, xn: Tensor, w: Tensor, out: Tensor, bias, qkv_epi:
 #                        other reader of x comes in between (Pending / run_block's ``pending``).
 # Measured (round 3, proj only): the GEMMs' MFMA utilisation 0.378 -> 0.391 at C3 and the step even
 # (409.9 / 409.9 vs 409.1 / 408.6 ms): the fused pass moves 12 B per element where LayerNorm moves 6.
+# Round 6, one box, interleaved, 2 runs each (profiles/r06_j13_bench_rm*.log; proj-fused, fc2-deferred):
+#   neither 80.55 / 80.67 views/s (gemm_mfma_util 0.391 / 0.392), proj 80.15 / 80.31 (0.402 / 0.404),
+#   fc2 80.63 / 80.63 (0.401 / 0.401), both 80.13 / 80.03 (0.411 / 0.411): the fc2 deferral is the
+#   default -- level on the step, and the reference's order (bf16 Linear output, then LayerScale and
+#   the fp32 residual add outside it)
 _FUSED_RESID_LN = os.environ.get("SR_FUSED_RESID_LN", "0") == "1"
-_DEFER_RESID = os.environ.get("SR_DEFER_RESID", "0") == "1"
+_DEFER_RESID = os.environ.get("SR_DEFER_RESID", "1") == "1"
 
 
 @dataclass
@@ -362,21 +367,28 @@ def group_tails_wanted(rows: int) -> bool:
 def run_block_tails(items, x: Tensor, sc: BlockScratch, defer: bool = False) -> list:
     """run_block_tail of several blocks over disjoint row ranges (``items`` = [(pb, r0, r1)]),
     each GEMM stage as ONE sr_gemm_group launch: proj (+LayerScale residual) of every block, the
-    LayerNorms, fc1 (+GELU), fc2 (+residual).  The per-rank global (anchors) and reloc (queries)
-    blocks of a frame-sharded layer are 5,496 rows each at C3 / G = 8: one launch per stage fills
-    the CUs that two under-filled ones leave idle.  Per output tile the k order and epilogue are
-    those of sr_gemm, so the result does not depend on the grouping.  Returns the Pending updates
-    (only without grouping: grouped tails keep the fused residual epilogues)."""
+    LayerNorms, fc1 (+GELU), fc2 (+residual, or deferred).  The per-rank global (anchors) and reloc
+    (queries) blocks of a frame-sharded layer are 5,496 rows each at C3 / G = 8: one launch per
+    stage fills the CUs that two under-filled ones leave idle.  Per output tile the k order and
+    epilogue are those of sr_gemm, so the result does not depend on the grouping.  Returns the
+    Pending updates of the deferred fc2 residuals (``defer``)."""
     items = [(pb, r0, r1) for pb, r0, r1 in items if r1 > r0]
-    grouped = (len(items) > 1 and not _FUSED_RESID_LN and not (defer and any(defer_enabled(pb) for pb, _, _ in items))
+    # ``defer`` with every block deferrable: fc2 ends in the bias epilogue into each block's dead
+    # attention-output rows sc.o and the updates come back as Pendings (as mlp_residual does alone)
+    n_defer = sum(1 for pb, _, _ in items if defer and defer_enabled(pb) and sc.o.shape[1] >= pb.w_fc2.shape[0])
+    grouped = (len(items) > 1 and not _FUSED_RESID_LN and n_defer in (0, len(items))
                and all(pb.w_proj is not None and pb.w_fc1 is not None for pb, _, _ in items))
     if grouped:
         hid = [pb.w_fc1.shape[0] for pb, _, _ in items]
         proj = [dict(a=sc.o[r0:r1], w=pb.w_proj, out=x[r0:r1], bias=pb.b_proj, gamma=pb.g1) for pb, r0, r1 in items]
         fc1 = [dict(a=sc.xn[r0:r1], w=pb.w_fc1, out=sc.h[r0:r1, :n], bias=pb.b_fc1)
                for (pb, r0, r1), n in zip(items, hid)]
-        fc2 = [dict(a=sc.h[r0:r1, :n], w=pb.w_fc2, out=x[r0:r1], bias=pb.b_fc2, gamma=pb.g2)
-               for (pb, r0, r1), n in zip(items, hid)]
+        if n_defer:
+            fc2 = [dict(a=sc.h[r0:r1, :n], w=pb.w_fc2, out=sc.o[r0:r1, :pb.w_fc2.shape[0]], bias=pb.b_fc2)
+                   for (pb, r0, r1), n in zip(items, hid)]
+        else:
+            fc2 = [dict(a=sc.h[r0:r1, :n], w=pb.w_fc2, out=x[r0:r1], bias=pb.b_fc2, gamma=pb.g2)
+                   for (pb, r0, r1), n in zip(items, hid)]
         grouped = all(ops.gemm_group_eligible(p) for p in (proj, fc1, fc2))
     if not grouped:
         out = [run_block_tail(pb, x, r0, r1, sc, defer) for pb, r0, r1 in items]
@@ -385,6 +397,9 @@ def run_block_tails(items, x: Tensor, sc: BlockScratch, defer: bool = False) -> 
     for pb, r0, r1 in items:
         ops.layernorm(x[r0:r1], pb.ln2_w, pb.ln2_b, pb.eps, sc.xn[r0:r1])
     ops.gemm_group(fc1, _lib.SR_EPI_BIAS_GELU, tag="gemm")
+    if n_defer:
+        ops.gemm_group(fc2, _lib.SR_EPI_BIAS, tag="gemm")
+        return [Pending(r0, r1, q["out"], pb.g2) for (pb, r0, r1), q in zip(items, fc2)]
     ops.gemm_group(fc2, _lib.SR_EPI_BIAS_RESID, tag="gemm")
     return []
 

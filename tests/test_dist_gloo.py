@@ -58,14 +58,20 @@ def _worker(rank, world, port, out_dir, golden, overlap):
     m.aggregator.generator.manual_seed(0)  # identical draws on every rank
     groups = []
     with cpu_ops.installed(), torch.no_grad():
-        if overlap == "group-tails":  # every stage eligible: the grouped global + reloc tails run
+        if overlap.startswith("group-tails"):  # every stage eligible: the grouped global + reloc tails run
             from sailrecon_amd import ops as real_ops
+            from sailrecon_amd import runtime
+            # group-tails-defer: the grouped fc2 stage ends in the bias epilogue and its residuals
+            # are applied by the next frame block's LN1 (runtime.Pending); group-tails: fused epilogues
+            runtime._DEFER_RESID = overlap == "group-tails-defer"
+            if runtime._DEFER_RESID:
+                real_ops.RESIDUAL_LN_COLS = tuple(real_ops.RESIDUAL_LN_COLS) + (384,)  # the small model's width
             real_ops.gemm_group_eligible = lambda probs: True
             gg = real_ops.gemm_group
             real_ops.gemm_group = lambda probs, epi, tag=None: (groups.append(len(probs)), gg(probs, epi, tag))
         feats, psi, cam_last = m.aggregator(images, no_reloc, reloc, fix_rank=int(g["fix_rank"]))
         poses = m.camera_head([m.aggregator.last_query_cam_tokens[:, :, None]], cam_last)
-    if overlap == "group-tails":  # per layer: the global Q + K/V GEMMs, then the 3 tail stages of both blocks
+    if overlap.startswith("group-tails"):  # per layer: the global Q + K/V GEMMs, then the 3 tail stages of both blocks
         assert groups == [2] * 4 * m.aggregator.depth, groups
     res = {f"feat_{layer}": feats[layer].numpy() for layer in (0, 1)}
     res["cam_last"] = cam_last.numpy()
@@ -83,6 +89,7 @@ CASES = [  # (world, golden, overlap): anchors / queries per rank
     (3, "g1_small_56_n5.npz", "overlap"),    # 2,2,1  uneven
     (3, "g1_small_56_n5.npz", "no-overlap"),
     (3, "g1_small_56_n5.npz", "group-tails"),  # the global + reloc tails as grouped GEMM stages
+    (3, "g1_small_56_n5.npz", "group-tails-defer"),  # ... with the fc2 residuals deferred (Pending)
     (3, "g11_small_interleaved.npz", "overlap"),  # 1,1,1, permuted + interleaved frame lists
 ]
 
