@@ -92,6 +92,14 @@ for step in "$@"; do
                 run bench_rl1_$i 400 env SR_FUSED_RESID_LN=1 python bench.py --steps 4 --warmup 1 --no-cpu-baseline || exit 1
               done ;;
     kln)     run kln 300 python tools/kbench.py ln ;;
+    kb_ab)   for i in 1 2; do  # kbench modes $AB_KB: ablib/libsfm_${AB_NAME}.so (an earlier build) against the committed one
+               run kb_${AB_NAME}_$i 300 env SFM_AMD_LIB=ablib/libsfm_${AB_NAME}.so python tools/kbench.py $AB_KB || exit 1
+               run kb_new_$i 300 python tools/kbench.py $AB_KB || exit 1
+             done ;;
+    bench_ab) for i in 1 2; do
+               run bench_${AB_NAME}_$i 400 env SFM_AMD_LIB=ablib/libsfm_${AB_NAME}.so python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
+               run bench_new_$i 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
+             done ;;
     kgemm_var) for i in 1 2; do
                  run kgemm_v0_$i 300 python tools/kbench.py gemm || exit 1
                  for v in $GEMM_VARIANTS; do
@@ -153,8 +161,8 @@ for step in "$@"; do
                --timeout 300 --timeout-method thread ;;
     kpair)   run kpair 300 python tools/kbench.py attn_pair ;;
     kqk)     run kqk 300 python tools/kbench.py qk_bwd ;;
-    resid_modes) for i in 1 2; do  # proj -> LN2 fusion (SR_FUSED_RESID_LN) x fc2 -> next LN1 (SR_DEFER_RESID)
-                   for m in 00 10 01 11; do
+    resid_modes) for i in ${RM_RUNS:-1 2}; do  # proj -> LN2 fusion (SR_FUSED_RESID_LN) x fc2 -> next LN1 (SR_DEFER_RESID)
+                   for m in ${RM_MODES:-00 10 01 11}; do
                      run bench_rm${m}_$i 400 env SR_FUSED_RESID_LN=${m:0:1} SR_DEFER_RESID=${m:1:1} python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extras none || exit 1
                    done
                  done ;;

@@ -502,6 +502,14 @@ def ln():
     ms = timeit(lambda: ops.layernorm(x, w, b, 1e-5, out))
     gb = M * C * 6 / 1e9
     print(f"layernorm M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s")
+    # the stream rate of the same bytes without the row reductions (ATen's cast copy, fp32 -> bf16):
+    # the roofline the LayerNorm's 6 B per element is held against
+    ms = timeit(lambda: out.copy_(x), reps=20)
+    print(f"aten cast copy fp32->bf16 M={M} C={C} {ms:8.3f} ms  {gb / ms * 1e3:8.1f} GB/s")
+    x2 = torch.empty_like(x)
+    ms = timeit(lambda: x2.copy_(x), reps=20)
+    print(f"aten copy fp32 M={M} C={C} {ms:8.3f} ms  {M * C * 8 / 1e9 / ms * 1e3:8.1f} GB/s", flush=True)
+    del x2
     # x += g * y; out = LN(x) (runtime.proj_residual_ln2), y strided in the qkv slot
     ybuf = torch.randn(M, 3 * C, device=DEV).bfloat16()
     g = torch.randn(C, device=DEV) * 0.01
