@@ -352,6 +352,30 @@ def attn_rank_small():
         print(f"attn rank G={G} frame {2 * nq:2d}x{P}        {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s")
 
 
+def attn_rank_cfg():
+    """attn_rank_small's per-rank reloc attention at G = 4 and 8 under each bf16 workgroup shape
+    (SR_ATTN_CFG: -1 auto, 0 = 4 waves x 2 q-blocks, 1 = 8 x 1, 2 = 2 x 2 = 128 rows), interleaved."""
+    C, H, D, P, N = 1024, 16, 64, 1374, 32
+    nsub = N * 305
+    for G in (4, 8):
+        nq = N // G
+        qkv = torch.randn(nq * P + 64, 3 * C, device=DEV, dtype=torch.bfloat16)[:nq * P]
+        kv = torch.randn(nsub + 64, 2 * C, device=DEV, dtype=torch.bfloat16)[:nsub]
+        o = torch.empty(nq * P, C, device=DEV, dtype=torch.bfloat16)
+        kb = 1.01 * max(float(qkv[:, C:2 * C].float().view(-1, H, D).norm(dim=-1).max()),
+                        float(kv[:, :C].float().view(-1, H, D).norm(dim=-1).max()))
+        fl = 4.0 * nq * H * P * (nsub + P) * D
+        for cfg in (-1, 0, 1, 2, -1, 0, 1, 2):
+            with ops.tuning(SR_ATTN_CFG=cfg):
+                ms = timeit(lambda: ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], o, heads=H, head_dim=D, batch=nq,
+                                                  lq=P, q_bstride=P, l0=nsub, k0_bstride=0, k1=qkv[:, C:2 * C],
+                                                  v1=qkv[:, 2 * C:], l1=P, k1_bstride=P, key_norm_max=kb,
+                                                  tail_readable=True))
+                kern = ops.last_kernel()
+            print(f"attn rank cfg G={G} reloc {nq}x({nsub}+{P}) cfg {cfg:2d} ({kern}) {ms:8.3f} ms  "
+                  f"{fl / ms / 1e9:8.1f} TF/s", flush=True)
+
+
 def gemm_rank():
     """The block GEMMs at the per-rank row counts of the frame-sharded C3 forward (64/G frames)."""
     for G in (1, 2, 4, 8):
