@@ -398,6 +398,22 @@ def gemm(M=2 * 32 * 1374):
         print(f"gemm {name:5s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s  {fl / ms / 1e9 / PEAK:6.1%}")
 
 
+def gemm_epi(M=2 * 32 * 1374):
+    """fc1's shape (N = 4,096, K = 1,024) under each epilogue, interleaved: what the erf-GELU costs
+    beside the plain bias epilogue, and K = 2,048 / 4,096 for the k-loop's share."""
+    N = 4096
+    for K in (1024, 2048, 4096):
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / 32
+        b = torch.randn(N, device=DEV)
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        fl = 2.0 * M * N * K
+        for name, epi in (("bias", _lib.SR_EPI_BIAS), ("gelu", _lib.SR_EPI_BIAS_GELU)) * 2:
+            ms = timeit(lambda: ops.gemm(a, w, out, epi, bias=b))
+            print(f"gemm_epi {name:4s} M={M} N={N} K={K} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s", flush=True)
+        del a, w
+
+
 def gemm_qkv(M=2 * 32 * 1374):
     """The QKV projection at C3 rows: plain bias (DINO) against the fused qk-LayerNorm + 2-D RoPE +
     c*q epilogue (the aggregator blocks, runtime.qkv_params(prescale=True)), and the layer's grouped
