@@ -222,6 +222,8 @@ if __name__ == "__main__":
         small_case("70", 70, 3, 10)
     if "small5" in which:  # 5 anchors + 5 queries: uneven frame sharding over 2 / 3 ranks
         small_case("56_n5", 56, 5, 10)
+    if "small9" in which:  # 9 anchors + 9 queries: frame sharding over 8 ranks (2,1,1,1,1,1,1,1)
+        small_case("56_n9", 56, 9, 10)
     if "blocks" in which:
         block_kats()
     if "ops" in which:

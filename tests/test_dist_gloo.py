@@ -91,6 +91,9 @@ CASES = [  # (world, golden, overlap): anchors / queries per rank
     (3, "g1_small_56_n5.npz", "group-tails"),  # the global + reloc tails as grouped GEMM stages
     (3, "g1_small_56_n5.npz", "group-tails-defer"),  # ... with the fc2 residuals deferred (Pending)
     (3, "g11_small_interleaved.npz", "overlap"),  # 1,1,1, permuted + interleaved frame lists
+    (4, "g1_small_56_n5.npz", "overlap"),    # 2,1,1,1  uneven
+    (8, "g1_small_56_n9.npz", "overlap"),    # 2,1,1,1,1,1,1,1: the driver's 8-rank world
+    (8, "g1_small_56_n9.npz", "group-tails-defer"),
 ]
 
 
@@ -110,6 +113,40 @@ def test_frame_sharded_matches_reference(tmp_path, world, golden, overlap):
     for r in rs:
         assert rel_l2(r["cam_last"], g["cam_token_last_layer"]) < 1e-5
         assert rel_l2(r["pose"], g["pose_enc"]) < 1e-5
+
+
+def _worker_too_few(rank, world, port, out_dir):
+    for p in (REPO, os.path.join(REPO, "self-supervise-sfm_amd"), HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cpu_ops
+    from goldens import load_npz
+    from test_host_cpu import small_model
+
+    g = load_npz("g1_small_56_n5.npz")
+    m = small_model()
+    m.aggregator.set_frame_sharding(dist.group.WORLD)
+    msg = ""
+    with cpu_ops.installed(), torch.no_grad():
+        try:
+            m.aggregator(torch.from_numpy(g["images"]), *_lists(g), fix_rank=int(g["fix_rank"]))
+        except ValueError as e:
+            msg = str(e)
+    with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_frame_sharding_needs_an_anchor_per_rank(tmp_path):
+    """5 anchor frames over 8 ranks: every rank refuses before any collective (no rank waits on a
+    peer that left), with the contract in the message."""
+    mp.spawn(_worker_too_few, args=(8, _free_port(), str(tmp_path)), nprocs=8, join=True)
+    for rank in range(8):
+        assert "at least one anchor frame per rank" in (tmp_path / f"rank{rank}.txt").read_text()
 
 
 def test_shard_range_partitions():

@@ -160,17 +160,26 @@ def test_frame_sharded_three_ranks_uneven(tmp_path, mode, overlap):
 
 
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_frame_sharded_eight_ranks(tmp_path, mode):
+    """9 anchors + 9 queries over 8 ranks sharing the GPU (2 / 1 / ... / 1 frames each): every
+    rank's remote anchors are one or two key segments, gathered from seven peers."""
+    _run(tmp_path, 8, "g1_small_56_n9.npz", mode)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_frame_sharded_c2_518_n8_two_ranks(tmp_path, mode):
     """BASELINE config 2 (N=8 views @518) split over 2 ranks: 4 anchors + 4 queries each; the
     global block's local pass runs on 5,496 keys, the remote pass on the other 5,496."""
     _run(tmp_path, 2, "g9_518_n8.npz", mode)
 
 
-@pytest.mark.parametrize("world,mode", [(2, "fp32"), (3, "bf16"), (3, "fp32")], ids=["2rk-fp32", "3rk-bf16", "3rk-fp32"])
+@pytest.mark.parametrize("world,mode", [(2, "fp32"), (3, "bf16"), (3, "fp32"), (8, "bf16")],
+                         ids=["2rk-fp32", "3rk-bf16", "3rk-fp32", "8rk-bf16"])
 def test_frame_sharded_c3_518_n32(tmp_path, world, mode):
     """BASELINE config 3 (the headline scene, N=32 views @518) frame-sharded
-    over 2 ranks (16 / 16 anchors + queries) and 3 ranks (the uneven 11 / 11 / 10 split; the
-    middle rank's remote global-attention pass has two key segments), every rank's features,
+    over 2 ranks (16 / 16 anchors + queries), 3 ranks (the uneven 11 / 11 / 10 split; the
+    middle rank's remote global-attention pass has two key segments) and 8 ranks (the driver's
+    8-GPU world: 4 + 4 frames per rank, key-split global passes), every rank's features,
     camera tokens and poses against the reference golden g10 (goldens.PARITY_TOL)."""
     _run(tmp_path, world, "g10_518_n32.npz", mode)
 
