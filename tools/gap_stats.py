@@ -3,13 +3,17 @@
 `bench.py` (run_kernel_trace.csv): each forward starts at the patch-embed GEMM
 (gemm256_kernel<4, ...>, one per forward); the gaps (next start - this end, one stream) of the
 forwards after the first are summed, bucketed, and the largest are listed with their neighbours.
+SR_GAP_BOUNDARY names another once-per-step kernel (adam_kernel for `tools/kbench.py train`).
 
     python3 tools/gap_stats.py gpurun_out/prof/run_kernel_trace.csv [out.json]
 """
 import csv
 import json
+import os
 import re
 import sys
+
+BOUNDARY = os.environ.get("SR_GAP_BOUNDARY", "gemm256_kernel<4")
 
 
 def short(name: str) -> str:
@@ -19,7 +23,7 @@ def short(name: str) -> str:
 
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "gemm256_kernel<4" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows) if BOUNDARY in r["Kernel_Name"]]
     if len(starts) < 3:
         raise SystemExit("need >= 3 forwards in the trace")
     gaps, fwd_ms = [], []
@@ -43,6 +47,11 @@ def main():
            "gap_count_per_forward": {k: v / nf for k, v in buckets.items()},
            "gap_ms_per_forward": {k: round(v / nf, 3) for k, v in bsum.items()},
            "largest": [{"us": g / 1e3, "after": a, "before": b} for g, a, b in sorted(gaps, reverse=True)[:25]]}
+    after = {}
+    for g, a, _ in gaps:
+        if g > 0:
+            after[a] = after.get(a, 0.0) + g / 1e6 / nf
+    out["idle_ms_after_kernel"] = dict(sorted(((k, round(v, 3)) for k, v in after.items()), key=lambda kv: -kv[1])[:25])
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 2:
         with open(sys.argv[2], "w") as f:
