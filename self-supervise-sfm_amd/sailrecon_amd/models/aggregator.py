@@ -718,7 +718,13 @@ class Aggregator(nn.Module):
             # slice alone leaves CUs idle at G >= 4), one N-way LSE merge at the end
             split = lambda n: ops.key_split_parts(dtype=q.dtype, batch=1, lq=lq, heads=H, l0=n, l1=0,  # noqa: E731
                                                   mask_mode=0)
-            plan = [(kv_loc, split(lq))] + [(kv_all[a:a + n], split(n)) for a, n in segs]
+            plan = [[kv_loc, split(lq)]] + [[kv_all[a:a + n], split(n)] for a, n in segs]
+            # one sr_attn_merge_n takes at most SR_ATTN_MERGE_MAX_PARTS partials: a middle rank's two
+            # remote segments can each want 8 (C3 at G = 8, ranks 3 and 4: 2 + 8 + 8), so the pass
+            # with the most parts gives up half of them (its chunks double) until the total fits
+            while sum(p for _, p in plan) > _lib.SR_ATTN_MERGE_MAX_PARTS:
+                big = max(plan, key=lambda e: e[1])
+                big[1] = max(1, big[1] // 2)
             plan = [(kv, [(0, kv.shape[0], p)]) for kv, p in plan]  # one launch of p equal chunks per pass
             total = sum(pp for _, pieces in plan for _, _, pp in pieces)
             o_parts, lse_parts = ops.key_split_workspace(q.device, total, lq, C, H, name="attn_shard")

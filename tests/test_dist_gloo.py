@@ -209,6 +209,43 @@ def test_sharded_global_partials_plan(G, r, force):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("G,N", [(8, 32), (8, 64), (4, 32), (3, 32), (6, 32)])
+def test_sharded_global_plan_fits_one_merge(G, N):
+    """Every rank's key-split plan of the frame-sharded global attention at the BASELINE sizes
+    (P = 1,374 tokens, 16 heads; C3 / N=64 over G ranks) ends in ONE sr_attn_merge_n of at most
+    SR_ATTN_MERGE_MAX_PARTS partials.  A middle rank of C3 at G = 8 has two remote segments of 3 and 4
+    anchors that each wanted 8 parts (2 + 8 + 8 = 18: the merge refused and the 8-GPU run stopped).
+    The plan only: the attention and merge launches are recorded, not run."""
+    from types import SimpleNamespace
+
+    from sailrecon_amd import _lib, ops
+    from sailrecon_amd.models.aggregator import Aggregator, shard_range
+
+    H, D, P = 16, 64, 1374
+    C = H * D
+    La = N * P
+    kv_all = torch.empty(La, 2 * C, dtype=torch.bfloat16)
+    pg = SimpleNamespace(dim=C, heads=H, head_dim=D, k_bound=0.0, q_bound=0.0, w_qkv=torch.empty(0))
+    saved = (ops.attention_partials, ops.attn_merge_n, ops.key_split_workspace)
+    try:
+        for r in range(G):
+            a0, na = shard_range(N, G, r)
+            lq, off = na * P, a0 * P
+            q = torch.empty(lq, C, dtype=torch.bfloat16)
+            calls, merges = [], []
+            ops.attention_partials = lambda *a, **k: calls.append((k["l0"], k["parts"]))
+            ops.attn_merge_n = lambda *a, **k: merges.append(k["parts"])
+            ops.key_split_workspace = lambda dev, parts, rows, cols, heads, name=None: (
+                torch.empty(parts * rows, 1), torch.empty(parts, 1))
+            Aggregator._global_attention_sharded(None, q, kv_all[off:off + lq], kv_all, q, pg, lq, La, off, [])
+            segs = [n for n in (off, La - off - lq) if n > 0]
+            assert [l0 for l0, _ in calls] == [lq] + segs, (r, calls)
+            assert merges == [sum(p for _, p in calls)], (r, calls, merges)
+            assert 1 <= merges[0] <= _lib.SR_ATTN_MERGE_MAX_PARTS, (G, N, r, calls)
+    finally:
+        ops.attention_partials, ops.attn_merge_n, ops.key_split_workspace = saved
+
+
 def test_rank_sim_rehearsal_matches_shard_shapes():
     """aggregator.RankSim (tools/rank_sim.py): one rank of a 3-rank frame-sharded forward run
     alone, gathers replaced by the rank's own slot -- its local frame work and outputs have the

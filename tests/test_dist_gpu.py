@@ -30,6 +30,15 @@ def _free_port():
 
 
 def _worker(rank, world, port, out_dir, golden, mode, overlap, backend="gloo", shard=True):
+    try:
+        _work(rank, world, port, out_dir, golden, mode, overlap, backend, shard)
+    except BaseException:  # name the rank that failed first (its peers then only see closed connections)
+        import traceback
+        print(f"RANK {rank}/{world} FAILED:\n{traceback.format_exc()}", flush=True)
+        raise
+
+
+def _work(rank, world, port, out_dir, golden, mode, overlap, backend, shard):
     for p in (REPO, os.path.join(REPO, "self-supervise-sfm_amd"), HERE):
         if p not in sys.path:
             sys.path.insert(0, p)
