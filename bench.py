@@ -434,12 +434,16 @@ def main():
     if not on_gpu and not args.launch_only:
         raise SystemExit("bench.py: no ROCm GPU visible (the HIP path has no CPU fallback); "
                          "--launch-only checks the launcher alone")
-    device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+    # SR_BENCH_REHEARSE=1 (rehearsal only, never a measurement): every rank on cuda:0 over gloo, so
+    # the N-rank path (sharding plan, collectives, extras, the JSON line) runs end to end on a
+    # one-GPU box; the driver's multi-GPU runs leave it unset (one GPU per rank, RCCL)
+    rehearse = os.environ.get("SR_BENCH_REHEARSE", "0") == "1"
+    device = torch.device("cuda", 0 if rehearse else local) if on_gpu else torch.device("cpu")
     if on_gpu:
         torch.cuda.set_device(device)
     use_pg = "WORLD_SIZE" in os.environ  # torchrun / the launcher, any world size
     if use_pg:
-        dist.init_process_group("nccl" if on_gpu else "gloo")
+        dist.init_process_group("nccl" if on_gpu and not rehearse else "gloo")
     seen = ranks_report(device)
     if args.launch_only:
         if rank == 0:
@@ -591,6 +595,8 @@ def main():
             "cpu_baseline": cpu,
             "extra_configs": extras,
         }
+        if rehearse:
+            line["rehearsal"] = "SR_BENCH_REHEARSE: every rank on cuda:0 over gloo (a code-path check, not a measurement)"
         if calib and calib.get("tflops"):
             # views/s as if on a box whose calibration GEMM runs CALIB_REF_TFLOPS (round-over-round
             # comparisons independent of the box the driver drew; the raw value stays `value`)
