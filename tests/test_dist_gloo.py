@@ -209,7 +209,7 @@ def test_sharded_global_partials_plan(G, r, force):
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("G,N", [(8, 32), (8, 64), (4, 32), (3, 32), (6, 32)])
+@pytest.mark.parametrize("G,N", [(8, 32), (8, 64), (4, 32), (4, 64), (3, 32), (6, 32), (2, 32), (2, 64), (8, 128)])
 def test_sharded_global_plan_fits_one_merge(G, N):
     """Every rank's key-split plan of the frame-sharded global attention at the BASELINE sizes
     (P = 1,374 tokens, 16 heads; C3 / N=64 over G ranks) ends in ONE sr_attn_merge_n of at most
