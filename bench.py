@@ -122,7 +122,7 @@ def kernel_of_class(entry):
 
 
 TRAFFIC_FILES = [os.path.join(REPO, "profiles", f) for f in
-                 ("r06_s2_pmc_traffic.json", "r06_final_pmc_traffic.json", "r06_pmc_traffic.json", "r05_final2_pmc_traffic.json",
+                 ("r06_s3_pmc_traffic.json", "r06_s2_pmc_traffic.json", "r06_final_pmc_traffic.json", "r06_pmc_traffic.json", "r05_final2_pmc_traffic.json",
                   "r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03b_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r02_pmc_traffic_c5_fp8qkv.json")]
 
 
